@@ -1,0 +1,191 @@
+/*
+ * ksg.h -- C ABI of the MI355X-native kube-scheduler node-evaluation path.
+ *
+ * This is the drop-in boundary for the per-pod hot path of kube-scheduler:
+ *   PreFilter -> Filter -> PreScore -> Score -> NormalizeScore -> weight/sum -> host selection
+ * as driven by Scheduler.schedulePod (pkg/scheduler/schedule_one.go:564-618),
+ * findNodesThatFitPod (schedule_one.go:622-712), findNodesThatPassFilters (:771-854),
+ * prioritizeNodes (:937-1048) and the nodeScoreHeap pop (:1050-1098), followed by
+ * Scheduler.assume (:1102-1137) -> Cache.AssumePod (backend/cache/cache.go:397).
+ *
+ * Objects cross the boundary as the Kubernetes JSON encoding of v1.Node / v1.Pod /
+ * v1.Namespace (what `json.Marshal` of the client-go object produces), so the Go side
+ * of a cgo shim needs no hand-written marshalling of the scheduler types.  Everything
+ * else is plain pointers + sizes; no torch / HIP types appear in any signature.
+ *
+ * Error convention (mirrors fwk.Status, staging/src/k8s.io/kube-scheduler/framework/
+ * interface.go:43-80,130-135): functions return 0 (KSG_OK) on success and a negative
+ * KSG_E* value on failure; ksg_last_error() returns the message.  A scheduling
+ * outcome (Unschedulable, UnschedulableAndUnresolvable, plugin Error) is not an ABI
+ * failure: it is reported in ksg_result.status with the fwk.Code numbering.
+ *
+ * Threading: one context per scheduling goroutine, not thread-safe -- exactly as
+ * ScheduleOne is serialised (schedule_one.go:65-66, scheduler.go:538).
+ */
+#ifndef KSG_H_
+#define KSG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSG_ABI_VERSION 1
+
+/* ---- return codes of the ABI functions ------------------------------------------ */
+#define KSG_OK 0
+#define KSG_EINVAL (-1)   /* malformed JSON / object / argument */
+#define KSG_ENOTFOUND (-2) /* unknown node / pod / handle */
+#define KSG_EEXIST (-3)   /* object already present */
+#define KSG_EDEVICE (-4)  /* HIP / RCCL failure */
+#define KSG_ENOTSUP (-5)  /* feature outside the supported parity contract */
+#define KSG_ENOMEM (-6)
+
+/* ---- fwk.Code (interface.go:46-99) ----------------------------------------------- */
+#define KSG_CODE_SUCCESS 0
+#define KSG_CODE_ERROR 1
+#define KSG_CODE_UNSCHEDULABLE 2
+#define KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE 3
+#define KSG_CODE_WAIT 4
+#define KSG_CODE_SKIP 5
+#define KSG_CODE_PENDING 6
+
+/* ---- in-tree plugins on the hot path (names.go); ids index every per-plugin array ---
+ * Filter order = pkg/scheduler/apis/config/testing/defaults/defaults.go:84-101
+ * (volume/DRA/NodeDeclaredFeatures plugins Skip for the pods of the parity contract).
+ * Score order  = defaults.go:119-143. */
+#define KSG_PLUGIN_NODE_UNSCHEDULABLE 0
+#define KSG_PLUGIN_NODE_NAME 1
+#define KSG_PLUGIN_TAINT_TOLERATION 2
+#define KSG_PLUGIN_NODE_AFFINITY 3
+#define KSG_PLUGIN_NODE_PORTS 4
+#define KSG_PLUGIN_NODE_RESOURCES_FIT 5
+#define KSG_PLUGIN_POD_TOPOLOGY_SPREAD 6
+#define KSG_PLUGIN_INTER_POD_AFFINITY 7
+#define KSG_PLUGIN_BALANCED_ALLOCATION 8
+#define KSG_PLUGIN_IMAGE_LOCALITY 9
+#define KSG_NUM_PLUGINS 10
+#define KSG_PLUGIN_NONE 255
+
+/* ---- failure reason bits (one bit per distinct upstream reason string) ------------- */
+#define KSG_R_UNSCHEDULABLE (1u << 0)        /* "node(s) were unschedulable" */
+#define KSG_R_NODE_NAME (1u << 1)            /* "node(s) didn't match the requested node name" */
+#define KSG_R_TAINT (1u << 2)                /* "node(s) had untolerated taint(s)" */
+#define KSG_R_NODE_AFFINITY_POD (1u << 3)    /* "node(s) didn't match Pod's node affinity/selector" */
+#define KSG_R_NODE_AFFINITY_ENFORCED (1u << 4)/* "node(s) didn't match scheduler-enforced node affinity" */
+#define KSG_R_NODE_PORTS (1u << 5)           /* "node(s) didn't have free ports for the requested pod ports" */
+#define KSG_R_TOO_MANY_PODS (1u << 6)        /* "Too many pods" */
+#define KSG_R_INSUFFICIENT_CPU (1u << 7)     /* "Insufficient cpu" */
+#define KSG_R_INSUFFICIENT_MEMORY (1u << 8)  /* "Insufficient memory" */
+#define KSG_R_INSUFFICIENT_EPHEMERAL (1u << 9)/* "Insufficient ephemeral-storage" */
+#define KSG_R_INSUFFICIENT_SCALAR (1u << 10) /* "Insufficient <extended resource>" (any) */
+#define KSG_R_PTS_MISSING_LABEL (1u << 11)   /* "...topology spread constraints (missing required label)" */
+#define KSG_R_PTS_SKEW (1u << 12)            /* "node(s) didn't match pod topology spread constraints" */
+#define KSG_R_IPA_AFFINITY (1u << 13)        /* "node(s) didn't match pod affinity rules" */
+#define KSG_R_IPA_ANTI_AFFINITY (1u << 14)   /* "node(s) didn't match pod anti-affinity rules" */
+#define KSG_R_IPA_EXISTING_ANTI (1u << 15)   /* "node(s) didn't satisfy existing pods anti-affinity rules" */
+#define KSG_R_PREFILTER (1u << 16)           /* node rejected by a PreFilter status / PreFilterResult */
+
+typedef struct ksg_ctx ksg_ctx;
+
+/* ScheduleResult (schedule_one.go:613-617) + the FitError/Error outcome. */
+typedef struct ksg_result {
+  int32_t status;          /* KSG_CODE_SUCCESS, or the code of the FitError/Error */
+  int32_t node_index;      /* snapshot index of SuggestedHost, -1 if none */
+  int32_t evaluated_nodes; /* ScheduleResult.EvaluatedNodes */
+  int32_t feasible_nodes;  /* ScheduleResult.FeasibleNodes */
+  int64_t total_score;     /* TotalScore of the chosen node (0 if F <= 1) */
+} ksg_result;
+
+/* Full per-node view of one cycle, used by parity tests and diagnosis rebuilding
+ * (Diagnosis.NodeToStatus, framework/types.go:1082-1180; NodePluginScores,
+ * interface.go:284-295).  All arrays are caller-owned, sized for ksg_num_nodes()
+ * (and KSG_NUM_PLUGINS x num_nodes for plugin_scores), indexed by snapshot index. */
+typedef struct ksg_eval_out {
+  int32_t prefilter_code;    /* non-success PreFilter status code (0 if PreFilter passed) */
+  int32_t prefilter_plugin;  /* plugin that produced it, KSG_PLUGIN_NONE otherwise */
+  uint8_t *node_code;        /* [N] fwk.Code of the node's Filter status (0 = feasible) */
+  uint8_t *node_plugin;      /* [N] first failing Filter plugin, KSG_PLUGIN_NONE if feasible */
+  uint32_t *node_reasons;    /* [N] KSG_R_* bits of that status */
+  uint32_t score_plugin_mask;/* out: bit p set if score plugin p ran (not skipped) */
+  int64_t *plugin_scores;    /* [KSG_NUM_PLUGINS][N] weighted normalised score (feasible nodes) */
+  int64_t *total_scores;     /* [N] TotalScore (feasible nodes; 0 elsewhere) */
+} ksg_eval_out;
+
+/* ---- context ------------------------------------------------------------------------
+ * config_json mirrors the KubeSchedulerConfiguration subset that shapes this path
+ * (staging/src/k8s.io/kube-scheduler/config/v1/types.go:44-160, defaults.go):
+ *   {"percentageOfNodesToScore": 100,
+ *    "scoreWeights": {"TaintToleration":3, ...},           (default_plugins.go:35-50)
+ *    "disabledPlugins": ["ImageLocality", ...],
+ *    "nodeResourcesFit": {"scoringStrategy": {"type": "LeastAllocated",
+ *                         "resources": [{"name":"cpu","weight":1}, ...],
+ *                         "requestedToCapacityRatio": {"shape": [...]}},
+ *                         "ignoredResources": [], "ignoredResourceGroups": []},
+ *    "balancedAllocation": {"resources": [...]},
+ *    "interPodAffinity": {"hardPodAffinityWeight": 1, "ignorePreferredTermsOfExistingPods": false},
+ *    "nodeAffinity": {"addedAffinity": <v1.NodeAffinity>},
+ *    "device": 0, "distributed": {"worldSize": 1, "rank": 0, "ncclId": "<hex>"}}
+ * Absent keys take the upstream defaults.  Returns NULL on failure (ksg_create_error()). */
+ksg_ctx *ksg_create(const char *config_json, size_t len);
+const char *ksg_create_error(void);
+void ksg_destroy(ksg_ctx *ctx);
+const char *ksg_last_error(const ksg_ctx *ctx);
+
+/* ---- cluster-state mirror: replaces the Cache event methods that feed the snapshot
+ * (backend/cache/cache.go:515-695, eventhandlers.go:51-412).  Snapshot node order is
+ * the nodeTree zone round-robin order (node_tree.go:119-143). */
+int ksg_upsert_namespace(ksg_ctx *ctx, const char *ns_json, size_t len);
+int ksg_add_node(ksg_ctx *ctx, const char *node_json, size_t len);
+int ksg_update_node(ksg_ctx *ctx, const char *node_json, size_t len);
+int ksg_remove_node(ksg_ctx *ctx, const char *name);
+int ksg_add_pod(ksg_ctx *ctx, const char *pod_json, size_t len); /* bound: spec.nodeName set */
+int ksg_remove_pod(ksg_ctx *ctx, const char *uid);
+int ksg_num_nodes(const ksg_ctx *ctx);
+/* name of the node at snapshot index `index`; returns its length or a KSG_E* code */
+int ksg_node_name(const ksg_ctx *ctx, int32_t index, char *buf, size_t cap);
+
+/* ---- pods to schedule: compiled once, like PodInfo creation (framework/types.go:1183) */
+int ksg_pod_compile(ksg_ctx *ctx, const char *pod_json, size_t len, int32_t *handle);
+int ksg_pod_release(ksg_ctx *ctx, int32_t handle);
+
+/* ---- scheduling cycles -------------------------------------------------------------- */
+#define KSG_FLAG_ASSUME 1u /* on success, AssumePod the pod onto the chosen node */
+
+/* One cycle; `eval` may be NULL.  Replaces schedulePod for one pod. */
+int ksg_schedule_one(ksg_ctx *ctx, int32_t handle, uint32_t flags, ksg_result *result,
+                     ksg_eval_out *eval);
+/* n cycles in queue order with sequential semantics: pod i sees the assumes of pods
+ * 0..i-1 (KSG_FLAG_ASSUME).  The whole batch runs device-resident. */
+int ksg_schedule_batch(ksg_ctx *ctx, const int32_t *handles, int32_t n, uint32_t flags,
+                       ksg_result *results);
+/* Cache.ForgetPod (cache.go:412) of an assumed pod -- unreserveAndForget (schedule_one.go:358) */
+int ksg_forget(ksg_ctx *ctx, int32_t handle);
+
+/* ---- plugin-granular entry points ---------------------------------------------------
+ * The FilterPlugin contract of one plugin over every snapshot node: its PreFilter
+ * (interface.go:513-532) then Filter (interface.go:542-567) per node.  *prefilter_code
+ * gets the PreFilter status (KSG_CODE_SKIP: the Filter did not run; codes are all 0).
+ * codes[N] / reasons[N] receive each node's Filter status. */
+int ksg_run_filter_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, int32_t *prefilter_code,
+                          uint8_t *codes, uint32_t *reasons);
+/* The ScorePlugin + ScoreExtensions contract of one plugin with every snapshot node as
+ * the node list: PreScore (interface.go:598-606), Score per node (:619-628) into raw[N],
+ * NormalizeScore (:609-614) into normalized[N] (unweighted).  *status_code gets the
+ * PreScore status (KSG_CODE_SKIP: not scored) or a Score error. */
+int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, int32_t *status_code,
+                         int64_t *raw, int64_t *normalized);
+
+/* ---- measurement hooks -------------------------------------------------------------- */
+/* Average device time (ms) per launch of the dominant kernel over the last
+ * ksg_schedule_batch, measured with HIP events on the launch stream, and the
+ * algorithmic bytes one launch of it moves (roofline accounting). */
+int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
+                                double *bytes_per_launch, int32_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSG_H_ */

@@ -1,0 +1,1659 @@
+// oracle.cpp -- PARITY ORACLE: CPU restatement of kube-scheduler's per-pod node
+// evaluation (test infrastructure; never shipped, never the thing measured as GPU).
+//
+// Follows, step by step and in the reference's own data structures' semantics:
+//   Scheduler.schedulePod            pkg/scheduler/schedule_one.go:564-618
+//   findNodesThatFitPod              schedule_one.go:622-712
+//   findNodesThatPassFilters         schedule_one.go:771-854   (parallelism=1 order)
+//   numFeasibleNodesToFind           schedule_one.go:858-884
+//   prioritizeNodes                  schedule_one.go:937-1048
+//   nodeScoreHeap + container/heap   schedule_one.go:1050-1098 (Go stdlib heap, literal)
+//   RunPreFilter/Filter/PreScore/ScorePlugins  framework/runtime/framework.go:934-1458
+//   plugins: nodeunschedulable, nodename, tainttoleration, nodeaffinity, nodeports,
+//            noderesources (fit, least/most/RTCR, balanced), podtopologyspread,
+//            interpodaffinity, imagelocality           (framework/plugins/*)
+//   cache/snapshot: NodeInfo.update (framework/types.go:445-468), nodeTree
+//            (backend/cache/node_tree.go), image states (cache.go:712-759)
+// Parity is pinned by the reference's own unit-test vectors (tests/golden/).
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ksg_oracle.h"
+#include "oracle_model.hpp"
+
+using namespace oracle;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Go math.Log (src/math/log.go, FreeBSD e_log.c algorithm), restated bit-for-bit
+// ---------------------------------------------------------------------------
+double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01,
+               L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01,
+               L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (std::isnan(x) || std::isinf(x)) return x;
+  if (x < 0) return NAN;
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = std::frexp(x, &ki);
+  if (f1 < 0.70710678118654752440084436210484903928483593768847) {  // Sqrt2/2
+    f1 *= 2;
+    ki--;
+  }
+  double f = f1 - 1;
+  double k = (double)ki;
+  double s = f / (2 + f);
+  double s2 = s * s;
+  double s4 = s2 * s2;
+  double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  double R = t1 + t2;
+  double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+// ---------------------------------------------------------------------------
+// container/heap (Go stdlib) with nodeScoreHeap.Less (schedule_one.go:1082-1085)
+// ---------------------------------------------------------------------------
+struct HeapEnt { int64_t total; int64_t randomizer; int32_t idx; };
+static bool heap_less(const std::vector<HeapEnt>& h, int i, int j) {
+  return h[i].total > h[j].total || (h[i].total == h[j].total && h[i].randomizer > h[j].randomizer);
+}
+static void heap_down(std::vector<HeapEnt>& h, int i0, int n) {
+  int i = i0;
+  while (true) {
+    int j1 = 2 * i + 1;
+    if (j1 >= n || j1 < 0) break;
+    int j = j1;
+    int j2 = j1 + 1;
+    if (j2 < n && heap_less(h, j2, j1)) j = j2;
+    if (!heap_less(h, j, i)) break;
+    std::swap(h[i], h[j]);
+    i = j;
+  }
+}
+static int heap_pop_index(std::vector<HeapEnt> h) {  // heap.Init then heap.Pop
+  int n = (int)h.size();
+  for (int i = n / 2 - 1; i >= 0; i--) heap_down(h, i, n);
+  // Pop: swap(0, n-1), down(0, n-1), return h[n-1] == the root after Init
+  return h[0].idx;
+}
+
+// ---------------------------------------------------------------------------
+// configuration
+// ---------------------------------------------------------------------------
+static const char* kPluginNames[KSG_NUM_PLUGINS] = {
+    "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts",
+    "NodeResourcesFit", "PodTopologySpread", "InterPodAffinity", "NodeResourcesBalancedAllocation",
+    "ImageLocality"};
+static int plugin_id(const std::string& n) {
+  for (int i = 0; i < KSG_NUM_PLUGINS; ++i)
+    if (n == kPluginNames[i]) return i;
+  if (n == "BalancedAllocation") return KSG_PLUGIN_BALANCED_ALLOCATION;
+  return -1;
+}
+
+struct Config {
+  int pct = 100;
+  bool taintCompareOps = false;  // featureGates.TaintTolerationComparisonOperators
+  bool enabled[KSG_NUM_PLUGINS];
+  int64_t weight[KSG_NUM_PLUGINS];
+  int fitStrategy = 0;  // 0 LeastAllocated 1 MostAllocated 2 RequestedToCapacityRatio
+  std::vector<std::pair<std::string, int64_t>> fitResources{{"cpu", 1}, {"memory", 1}};
+  std::vector<std::pair<int64_t, int64_t>> rtcrShape;  // (utilization, score*10)
+  std::set<std::string> ignoredResources, ignoredResourceGroups;
+  std::vector<std::pair<std::string, int64_t>> balancedResources{{"cpu", 1}, {"memory", 1}};
+  int32_t hardPodAffinityWeight = 1;
+  bool ignorePreferredTermsOfExistingPods = false;
+  bool hasAddedRequired = false;
+  std::vector<ParsedNodeSelectorTerm> addedRequired;
+  bool hasAddedPreferred = false;
+  PreferredTerms addedPreferred;
+  Config() {
+    // default_plugins.go:35-50
+    const int64_t w[KSG_NUM_PLUGINS] = {0, 0, 3, 2, 0, 1, 2, 2, 1, 1};
+    for (int i = 0; i < KSG_NUM_PLUGINS; ++i) { enabled[i] = true; weight[i] = w[i]; }
+  }
+};
+
+static std::vector<std::pair<std::string, int64_t>> decode_res_specs(const mj::Value* v) {
+  std::vector<std::pair<std::string, int64_t>> out;
+  if (v && v->is_arr())
+    for (auto& r : v->arr) {
+      int64_t w = r.i64("weight", 0);
+      if (w == 0) w = 1;  // defaults.go:218-221
+      out.push_back({r.str("name"), w});
+    }
+  return out;
+}
+
+static bool decode_config(const mj::Value& v, Config* c, std::string* err) {
+  if (!v.is_obj()) return true;
+  if (v.has("percentageOfNodesToScore")) c->pct = (int)v.i64("percentageOfNodesToScore");
+  if (auto fg = v.has("featureGates")) c->taintCompareOps = fg->boolean("TaintTolerationComparisonOperators");
+  if (auto w = v.has("scoreWeights"))
+    for (auto& kv : w->obj) {
+      int id = plugin_id(kv.first);
+      if (id < 0) { *err = "unknown plugin " + kv.first; return false; }
+      c->weight[id] = std::strtoll(kv.second.s.c_str(), nullptr, 10);
+    }
+  if (auto d = v.has("disabledPlugins"))
+    for (auto& x : d->arr) {
+      int id = plugin_id(x.s);
+      if (id < 0) { *err = "unknown plugin " + x.s; return false; }
+      c->enabled[id] = false;
+    }
+  if (auto f = v.has("nodeResourcesFit")) {
+    if (auto ss = f->has("scoringStrategy")) {
+      std::string t = ss->str("type", "LeastAllocated");
+      if (t == "LeastAllocated") c->fitStrategy = 0;
+      else if (t == "MostAllocated") c->fitStrategy = 1;
+      else if (t == "RequestedToCapacityRatio") c->fitStrategy = 2;
+      else { *err = "bad scoring strategy"; return false; }
+      if (ss->has("resources")) c->fitResources = decode_res_specs(ss->get("resources"));
+      if (auto r = ss->has("requestedToCapacityRatio"))
+        if (auto sh = r->has("shape"))
+          for (auto& p : sh->arr)  // score scaled by MaxNodeScore/MaxCustomPriorityScore (=10)
+            c->rtcrShape.push_back({p.i64("utilization"), p.i64("score") * 10});
+    }
+    if (auto ir = f->has("ignoredResources"))
+      for (auto& x : ir->arr) c->ignoredResources.insert(x.s);
+    if (auto ig = f->has("ignoredResourceGroups"))
+      for (auto& x : ig->arr) c->ignoredResourceGroups.insert(x.s);
+  }
+  if (auto b = v.has("balancedAllocation"))
+    if (b->has("resources")) c->balancedResources = decode_res_specs(b->get("resources"));
+  if (auto ipa = v.has("interPodAffinity")) {
+    if (ipa->has("hardPodAffinityWeight")) c->hardPodAffinityWeight = (int32_t)ipa->i64("hardPodAffinityWeight");
+    c->ignorePreferredTermsOfExistingPods = ipa->boolean("ignorePreferredTermsOfExistingPods");
+  }
+  if (auto na = v.has("nodeAffinity"))
+    if (auto aa = na->has("addedAffinity")) {
+      if (auto rq = aa->has("requiredDuringSchedulingIgnoredDuringExecution")) {
+        std::vector<NodeSelectorTerm> terms;
+        if (auto ts = rq->has("nodeSelectorTerms"))
+          for (auto& t : ts->arr) {
+            NodeSelectorTerm nt;
+            for (auto& e : t.has("matchExpressions") ? t.get("matchExpressions")->arr : std::vector<mj::Value>{}) {
+              std::vector<std::string> vals;
+              if (auto vs = e.has("values")) for (auto& x : vs->arr) vals.push_back(x.s);
+              nt.matchExpressions.push_back({e.str("key"), e.str("operator"), vals});
+            }
+            for (auto& e : t.has("matchFields") ? t.get("matchFields")->arr : std::vector<mj::Value>{}) {
+              std::vector<std::string> vals;
+              if (auto vs = e.has("values")) for (auto& x : vs->arr) vals.push_back(x.s);
+              nt.matchFields.push_back({e.str("key"), e.str("operator"), vals});
+            }
+            terms.push_back(nt);
+          }
+        if (!new_node_selector(terms, &c->addedRequired)) { *err = "bad addedAffinity"; return false; }
+        c->hasAddedRequired = true;
+      }
+      if (auto pf = aa->has("preferredDuringSchedulingIgnoredDuringExecution")) {
+        std::vector<PreferredSchedulingTerm> terms;
+        for (auto& t : pf->arr) {
+          PreferredSchedulingTerm p;
+          p.weight = (int32_t)t.i64("weight");
+          if (auto pr = t.has("preference")) {
+            for (auto& e : pr->has("matchExpressions") ? pr->get("matchExpressions")->arr : std::vector<mj::Value>{}) {
+              std::vector<std::string> vals;
+              if (auto vs = e.has("values")) for (auto& x : vs->arr) vals.push_back(x.s);
+              p.preference.matchExpressions.push_back({e.str("key"), e.str("operator"), vals});
+            }
+          }
+          terms.push_back(p);
+        }
+        if (!terms.empty()) {
+          if (!new_preferred_terms(terms, &c->addedPreferred)) { *err = "bad addedAffinity"; return false; }
+          c->hasAddedPreferred = true;
+        }
+      }
+    }
+  return true;
+}
+
+// apis/config/validation/validation_pluginargs.go:81-97,176-239,295-340
+static bool validate_config(const Config& c, std::string* err) {
+  for (auto& r : c.fitResources)
+    if (r.second <= 0 || r.second > 100) { *err = "resource weight of " + r.first + " not in valid range (0, 100]"; return false; }
+  std::set<std::string> seen;
+  for (auto& r : c.balancedResources) {
+    if (!seen.insert(r.first).second) { *err = "duplicate balanced resource " + r.first; return false; }
+    if (r.second != 1) { *err = "balanced resource weight must be 1"; return false; }
+  }
+  if (c.hardPodAffinityWeight < 0 || c.hardPodAffinityWeight > 100) { *err = "hardPodAffinityWeight not in [0,100]"; return false; }
+  if (c.fitStrategy == 2) {
+    if (c.rtcrShape.empty()) { *err = "requestedToCapacityRatio shape required"; return false; }
+    for (size_t i = 0; i < c.rtcrShape.size(); ++i) {
+      if (i && c.rtcrShape[i - 1].first >= c.rtcrShape[i].first) { *err = "shape not sorted"; return false; }
+      if (c.rtcrShape[i].first < 0 || c.rtcrShape[i].first > 100) { *err = "utilization out of range"; return false; }
+      if (c.rtcrShape[i].second < 0 || c.rtcrShape[i].second > 100) { *err = "score out of range"; return false; }
+    }
+  }
+  for (int p = 0; p < KSG_NUM_PLUGINS; ++p)
+    if (c.weight[p] < 0) { *err = "negative plugin weight"; return false; }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// cache / snapshot state
+// ---------------------------------------------------------------------------
+struct ImageState { int64_t size = 0; std::set<std::string> nodes; };
+using HostPorts = std::map<std::string, std::set<std::pair<std::string, int32_t>>>;  // ip -> {(proto, port)}
+
+struct NodeInfoO {  // framework.NodeInfo (framework/types.go:172-220)
+  Node node;
+  std::vector<PodInfo*> pods;
+  std::vector<PodInfo*> podsWithAffinity, podsWithRequiredAntiAffinity;
+  Resource requested, nonzero, allocatable;
+  HostPorts usedPorts;
+};
+
+struct HostPortWant { std::string ip, proto; int32_t port; };
+// util.GetHostPorts (scheduler/util/utils.go:241-272)
+static std::vector<HostPortWant> get_host_ports(const Pod& p) {
+  std::vector<HostPortWant> out;
+  auto take = [&](const Container& c) {
+    for (auto& cp : c.ports)
+      if (cp.hostPort > 0) out.push_back({cp.hostIP, cp.protocol, cp.hostPort});
+  };
+  for (auto& c : p.initContainers)
+    if (c.restartAlways) take(c);
+  for (auto& c : p.containers) take(c);
+  return out;
+}
+static void sanitize(std::string& ip, std::string& proto) {  // HostPortInfo.sanitize (types.go:634-641)
+  if (ip.empty()) ip = "0.0.0.0";
+  if (proto.empty()) proto = "TCP";
+}
+static bool check_conflict(const HostPorts& h, std::string ip, std::string proto, int32_t port) {  // :603-631
+  if (port <= 0) return false;
+  sanitize(ip, proto);
+  auto pp = std::make_pair(proto, port);
+  if (ip == "0.0.0.0") {
+    for (auto& kv : h)
+      if (kv.second.count(pp)) return true;
+    return false;
+  }
+  for (const std::string& key : {std::string("0.0.0.0"), ip}) {
+    auto it = h.find(key);
+    if (it != h.end() && it->second.count(pp)) return true;
+  }
+  return false;
+}
+
+static Resource node_allocatable(const Node& n) {  // NewResource(node.Status.Allocatable), types.go:1263-1291
+  Resource r;
+  for (auto& kv : n.allocatable) {
+    if (kv.first == "cpu") r.milliCPU += kv.second;
+    else if (kv.first == "memory") r.memory += milli_to_value(kv.second);
+    else if (kv.first == "pods") r.allowedPods += milli_to_value(kv.second);
+    else if (kv.first == "ephemeral-storage") r.ephemeral += milli_to_value(kv.second);
+    else if (is_scalar_resource_name(kv.first)) r.scalar[kv.first] += milli_to_value(kv.second);
+  }
+  return r;
+}
+
+static void node_update(NodeInfoO& ni, PodInfo* pi, int64_t sign) {  // NodeInfo.update, types.go:445-468
+  const PodResource& pr = pi->calc;
+  ni.requested.milliCPU += sign * pr.res.milliCPU;
+  ni.requested.memory += sign * pr.res.memory;
+  ni.requested.ephemeral += sign * pr.res.ephemeral;
+  for (auto& kv : pr.res.scalar) ni.requested.scalar[kv.first] += sign * kv.second;
+  ni.nonzero.milliCPU += sign * pr.non0CPU;
+  ni.nonzero.memory += sign * pr.non0Mem;
+  for (auto hp : get_host_ports(pi->pod)) {  // updateUsedPorts :503-511
+    if (hp.port <= 0) continue;
+    sanitize(hp.ip, hp.proto);
+    if (sign > 0) ni.usedPorts[hp.ip].insert({hp.proto, hp.port});
+    else {
+      auto it = ni.usedPorts.find(hp.ip);
+      if (it != ni.usedPorts.end()) {
+        it->second.erase({hp.proto, hp.port});
+        if (it->second.empty()) ni.usedPorts.erase(it);
+      }
+    }
+  }
+}
+static void node_add_pod(NodeInfoO& ni, PodInfo* pi) {  // AddPodInfo :367-376
+  ni.pods.push_back(pi);
+  if (pi->withAffinity()) ni.podsWithAffinity.push_back(pi);
+  if (pi->withRequiredAnti()) ni.podsWithRequiredAntiAffinity.push_back(pi);
+  node_update(ni, pi, 1);
+}
+static void remove_from_slice(std::vector<PodInfo*>& s, const std::string& uid) {  // :397-420
+  for (size_t i = 0; i < s.size(); ++i)
+    if (s[i]->pod.uid == uid) {
+      s[i] = s.back();
+      s.pop_back();
+      return;
+    }
+}
+static bool node_remove_pod(NodeInfoO& ni, const std::string& uid) {  // RemovePod :423-441
+  PodInfo* found = nullptr;
+  for (auto* p : ni.pods)
+    if (p->pod.uid == uid) found = p;
+  if (!found) return false;
+  if (found->withAffinity()) remove_from_slice(ni.podsWithAffinity, uid);
+  if (found->withRequiredAnti()) remove_from_slice(ni.podsWithRequiredAntiAffinity, uid);
+  remove_from_slice(ni.pods, uid);
+  node_update(ni, found, -1);
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// status helpers
+// ---------------------------------------------------------------------------
+struct Status {
+  int code = KSG_CODE_SUCCESS;
+  uint32_t reasons = 0;
+  int plugin = KSG_PLUGIN_NONE;
+  bool ok() const { return code == KSG_CODE_SUCCESS; }
+};
+static Status mk(int code, uint32_t r) { Status s; s.code = code; s.reasons = r; return s; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// the oracle context
+// ---------------------------------------------------------------------------
+struct ksgo_ctx {
+  Config cfg;
+  std::string err;
+  std::map<std::string, Namespace> namespaces;
+  std::map<std::string, std::unique_ptr<NodeInfoO>> nodes;
+  // nodeTree (backend/cache/node_tree.go)
+  std::vector<std::string> zones;
+  std::map<std::string, std::vector<std::string>> tree;
+  std::map<std::string, ImageState> imageStates;  // cache.imageStates
+  std::map<std::string, std::unique_ptr<PodInfo>> pods;  // bound/assumed pods by uid
+  std::vector<NodeInfoO*> list;  // snapshot nodeInfoList order
+  bool listDirty = true;
+  int64_t nextStartNodeIndex = 0;
+  std::map<int32_t, std::unique_ptr<Pod>> queue;  // compiled pods
+  int32_t nextHandle = 1;
+  std::map<int32_t, std::string> assumedUid;  // handle -> assumed pod uid
+
+  void rebuild_list() {  // nodeTree.list (node_tree.go:119-143) -> updateNodeInfoSnapshotList
+    if (!listDirty) return;
+    list.clear();
+    size_t maxLen = 0;
+    for (auto& z : zones) maxLen = std::max(maxLen, tree[z].size());
+    for (size_t idx = 0; idx < maxLen; ++idx)
+      for (auto& z : zones) {
+        auto& na = tree[z];
+        if (idx < na.size()) list.push_back(nodes[na[idx]].get());
+      }
+    listDirty = false;
+  }
+  const Labels* ns_labels(const std::string& ns) const {  // GetNamespaceLabelsSnapshot (ipa plugin.go:150-159)
+    auto it = namespaces.find(ns);
+    return it == namespaces.end() ? nullptr : &it->second.labels;
+  }
+  ImageState* image_state(const std::string& name) {
+    auto it = imageStates.find(name);
+    return it == imageStates.end() ? nullptr : &it->second;
+  }
+};
+
+namespace {
+
+static thread_local std::string g_create_error;
+
+// ===========================================================================
+// per-cycle evaluation
+// ===========================================================================
+struct Cycle {
+  ksgo_ctx* c;
+  const Pod* pod;
+  PodInfo pinfo;
+  bool pinfoOk = true;
+  bool skipFilter[KSG_NUM_PLUGINS] = {};
+  bool skipScore[KSG_NUM_PLUGINS] = {};
+  // Fit prefilter state
+  Resource podReq;
+  // NodePorts
+  std::vector<HostPortWant> wantPorts;
+  // NodeAffinity
+  RequiredNodeAffinity reqNA;
+  PreferredTerms prefNA;
+  bool hasPrefNA = false;
+  // TaintToleration
+  std::vector<Toleration> tolPrefer;
+  // Fit / Balanced PreScore
+  std::vector<int64_t> fitPodReqs, balPodReqs;
+  // PTS
+  struct TSC { int32_t maxSkew; std::string key; Selector sel; int32_t minDomains; bool affHonor, taintHonor; };
+  std::vector<TSC> ptsF;
+  std::vector<std::map<std::string, int64_t>> tpMatch;  // TpValueToMatchNum
+  std::vector<int64_t> critMin;
+  std::vector<TSC> ptsS;
+  std::set<std::string> ignored;
+  std::vector<std::map<std::string, int64_t>> tpCounts;  // TopologyValueToPodCounts (entries exist)
+  std::vector<double> tpWeight;
+  // IPA
+  std::map<std::pair<std::string, std::string>, int64_t> existingAnti, affCounts, antiCounts;
+  std::map<std::string, std::map<std::string, int64_t>> topoScore;
+  std::vector<AffinityTerm> ipaReqAff, ipaReqAnti;
+  std::vector<WeightedAffinityTerm> ipaPrefAff, ipaPrefAnti;
+  const Labels* nsLabels = nullptr;
+};
+
+static std::vector<int> prefilter_order() {  // defaults.go PreFilter list
+  return {KSG_PLUGIN_NODE_AFFINITY, KSG_PLUGIN_NODE_PORTS, KSG_PLUGIN_NODE_RESOURCES_FIT,
+          KSG_PLUGIN_POD_TOPOLOGY_SPREAD, KSG_PLUGIN_INTER_POD_AFFINITY};
+}
+static const int kFilterOrder[] = {KSG_PLUGIN_NODE_UNSCHEDULABLE, KSG_PLUGIN_NODE_NAME, KSG_PLUGIN_TAINT_TOLERATION,
+                                   KSG_PLUGIN_NODE_AFFINITY,      KSG_PLUGIN_NODE_PORTS, KSG_PLUGIN_NODE_RESOURCES_FIT,
+                                   KSG_PLUGIN_POD_TOPOLOGY_SPREAD, KSG_PLUGIN_INTER_POD_AFFINITY};
+static const int kPreScoreOrder[] = {KSG_PLUGIN_TAINT_TOLERATION, KSG_PLUGIN_NODE_AFFINITY, KSG_PLUGIN_NODE_RESOURCES_FIT,
+                                     KSG_PLUGIN_POD_TOPOLOGY_SPREAD, KSG_PLUGIN_INTER_POD_AFFINITY,
+                                     KSG_PLUGIN_BALANCED_ALLOCATION};
+static const int kScoreOrder[] = {KSG_PLUGIN_TAINT_TOLERATION, KSG_PLUGIN_NODE_AFFINITY, KSG_PLUGIN_NODE_RESOURCES_FIT,
+                                  KSG_PLUGIN_POD_TOPOLOGY_SPREAD, KSG_PLUGIN_INTER_POD_AFFINITY,
+                                  KSG_PLUGIN_BALANCED_ALLOCATION, KSG_PLUGIN_IMAGE_LOCALITY};
+
+// ---- PodTopologySpread helpers (podtopologyspread/common.go) -------------------------
+static bool node_labels_match_spread(const Labels& nl, const std::vector<Cycle::TSC>& cs) {  // :73-80
+  for (auto& c : cs)
+    if (!nl.count(c.key)) return false;
+  return true;
+}
+static bool match_inclusion(const Cycle& cy, const Cycle::TSC& c, const Node& n) {  // :43-57
+  if (c.affHonor && !cy.reqNA.match(n)) return false;
+  if (c.taintHonor && find_untolerated_noschedule(n.taints, cy.pod->tolerations)) return false;
+  return true;
+}
+static int64_t count_pods_match(const std::vector<PodInfo*>& pods, const Selector& sel, const std::string& ns) {  // :145-160
+  if (sel.empty()) return 0;
+  int64_t n = 0;
+  for (auto* p : pods) {
+    if (p->pod.terminating || p->pod.ns != ns) continue;
+    if (selector_matches(sel, p->pod.labels)) ++n;
+  }
+  return n;
+}
+// filterTopologySpreadConstraints (common.go:87-128)
+static bool filter_tsc(const Pod& pod, const std::string& action, std::vector<Cycle::TSC>* out) {
+  out->clear();
+  for (auto& c : pod.tsc) {
+    if (c.whenUnsatisfiable != action) continue;
+    Selector sel;
+    if (!label_selector_as_selector(c.labelSelector, &sel)) return false;
+    if (!c.matchLabelKeys.empty()) {  // MatchLabelKeysInPodTopologySpread (on by default)
+      std::vector<std::pair<std::string, std::string>> ml;
+      for (auto& k : c.matchLabelKeys) {
+        auto it = pod.labels.find(k);
+        if (it != pod.labels.end()) ml.push_back({k, it->second});
+      }
+      if (!ml.empty() && !sel.nothing) {  // mergeLabelSetWithSelector :130-143
+        Selector merged;
+        std::map<std::string, std::string> set(ml.begin(), ml.end());
+        for (auto& kv : set) merged.reqs.push_back({kv.first, Op::Equals, {kv.second}});
+        for (auto& r : sel.reqs) merged.reqs.push_back(r);
+        sel = merged;
+      }
+    }
+    Cycle::TSC t;
+    t.maxSkew = c.maxSkew;
+    t.key = c.topologyKey;
+    t.sel = sel;
+    t.minDomains = c.hasMinDomains ? c.minDomains : 1;
+    t.affHonor = c.nodeAffinityPolicy.empty() ? true : c.nodeAffinityPolicy == "Honor";
+    t.taintHonor = c.nodeTaintsPolicy.empty() ? false : c.nodeTaintsPolicy == "Honor";
+    out->push_back(t);
+  }
+  return true;
+}
+
+// ---- IPA helpers --------------------------------------------------------------------
+using PairCounts = std::map<std::pair<std::string, std::string>, int64_t>;
+static bool pod_matches_all_terms(const std::vector<AffinityTerm>& terms, const Pod& p) {  // filtering.go:188-200
+  if (terms.empty()) return false;
+  for (auto& t : terms)
+    if (!t.matches(p, nullptr)) return false;
+  return true;
+}
+// mergeAffinityTermNamespacesIfNotEmpty (interpodaffinity/plugin.go:134-147): the term's
+// namespace set gains the namespaces the selector lists; the selector itself is kept
+// (the assignment to NamespaceSelector in the reference hits a copy).
+static void merge_ns(ksgo_ctx* c, AffinityTerm& at) {
+  if (at.nsSelector.empty()) return;
+  for (auto& kv : c->namespaces)
+    if (selector_matches(at.nsSelector, kv.second.labels)) at.namespaces.insert(kv.first);
+}
+
+// ===========================================================================
+// PreFilter (framework.go:934-995)
+// ===========================================================================
+static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std::string>* nodeNames,
+                                   bool* restricts) {
+  ksgo_ctx* c = cy.c;
+  const Pod& pod = *cy.pod;
+  *skip = false;
+  *restricts = false;
+  switch (p) {
+    case KSG_PLUGIN_NODE_AFFINITY: {  // node_affinity.go:148-198
+      bool noNA = !pod.hasRequiredNA;
+      if (noNA && !c->cfg.hasAddedRequired && !pod.hasNodeSelector) { *skip = true; return Status{}; }
+      cy.reqNA = get_required_node_affinity(pod);
+      if (noNA || pod.requiredNA.empty()) return Status{};
+      std::set<std::string> names;
+      bool namesNil = true;
+      for (auto& t : pod.requiredNA) {
+        bool termNil = true;
+        std::set<std::string> termNames;
+        for (auto& r : t.matchFields)
+          if (r.key == "metadata.name" && r.op == "In") {
+            std::set<std::string> s(r.values.begin(), r.values.end());
+            if (termNil) { termNames = s; termNil = false; }
+            else {
+              std::set<std::string> x;
+              for (auto& n : termNames)
+                if (s.count(n)) x.insert(n);
+              termNames = x;
+            }
+          }
+        if (termNil) return Status{};  // all nodes eligible
+        namesNil = false;
+        names.insert(termNames.begin(), termNames.end());
+      }
+      if (!namesNil && names.empty()) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_PREFILTER);
+      if (!names.empty()) { *restricts = true; nodeNames->assign(names.begin(), names.end()); }
+      return Status{};
+    }
+    case KSG_PLUGIN_NODE_PORTS:  // node_ports.go:73-82
+      cy.wantPorts = get_host_ports(pod);
+      if (cy.wantPorts.empty()) *skip = true;
+      return Status{};
+    case KSG_PLUGIN_NODE_RESOURCES_FIT: {  // fit.go:317-335 computePodResourceRequest
+      ResList reqs = pod_requests(pod, nullptr);
+      Resource r;  // SetMaxResource (types.go:1325-1344)
+      for (auto& kv : reqs) {
+        if (kv.first == "memory") r.memory = std::max(r.memory, milli_to_value(kv.second));
+        else if (kv.first == "cpu") r.milliCPU = std::max(r.milliCPU, kv.second);
+        else if (kv.first == "ephemeral-storage") r.ephemeral = std::max(r.ephemeral, milli_to_value(kv.second));
+        else if (is_scalar_resource_name(kv.first)) r.scalar[kv.first] = std::max(r.scalar[kv.first], milli_to_value(kv.second));
+      }
+      cy.podReq = r;
+      return Status{};
+    }
+    case KSG_PLUGIN_POD_TOPOLOGY_SPREAD: {  // filtering.go:139-149, 237-311
+      if (!filter_tsc(pod, "DoNotSchedule", &cy.ptsF)) return mk(KSG_CODE_ERROR, 0);
+      if (cy.ptsF.empty()) { *skip = true; return Status{}; }
+      size_t nc = cy.ptsF.size();
+      cy.tpMatch.assign(nc, {});
+      for (auto* ni : c->list) {
+        const Node& n = ni->node;
+        if (!node_labels_match_spread(n.labels, cy.ptsF)) continue;
+        for (size_t i = 0; i < nc; ++i) {
+          auto& con = cy.ptsF[i];
+          if (!match_inclusion(cy, con, n)) continue;
+          const std::string& v = n.labels.at(con.key);
+          cy.tpMatch[i][v] += count_pods_match(ni->pods, con.sel, pod.ns);
+        }
+      }
+      cy.critMin.assign(nc, INT32_MAX);
+      for (size_t i = 0; i < nc; ++i)
+        for (auto& kv : cy.tpMatch[i]) cy.critMin[i] = std::min(cy.critMin[i], kv.second);
+      return Status{};
+    }
+    case KSG_PLUGIN_INTER_POD_AFFINITY: {  // interpodaffinity/filtering.go:286-321
+      PodInfo pi;
+      if (!new_pod_info(pod, &pi)) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_PREFILTER);
+      cy.ipaReqAff = pi.reqAff;
+      cy.ipaReqAnti = pi.reqAnti;
+      for (auto& t : cy.ipaReqAff) merge_ns(c, t);
+      for (auto& t : cy.ipaReqAnti) merge_ns(c, t);
+      cy.nsLabels = c->ns_labels(pod.ns);
+      cy.existingAnti.clear();
+      for (auto* ni : c->list) {  // getExistingAntiAffinityCounts :216-240
+        for (auto* ep : ni->podsWithRequiredAntiAffinity)
+          for (auto& t : ep->reqAnti)
+            if (t.matches(pod, cy.nsLabels)) {
+              auto it = ni->node.labels.find(t.topologyKey);
+              if (it != ni->node.labels.end()) cy.existingAnti[{t.topologyKey, it->second}] += 1;
+            }
+      }
+      cy.affCounts.clear();
+      cy.antiCounts.clear();
+      if (!cy.ipaReqAff.empty() || !cy.ipaReqAnti.empty()) {  // :246-283
+        for (auto* ni : c->list)
+          for (auto* ep : ni->pods) {
+            if (pod_matches_all_terms(cy.ipaReqAff, ep->pod))
+              for (auto& t : cy.ipaReqAff) {
+                auto it = ni->node.labels.find(t.topologyKey);
+                if (it != ni->node.labels.end()) cy.affCounts[{t.topologyKey, it->second}] += 1;
+              }
+            for (auto& t : cy.ipaReqAnti)
+              if (t.matches(ep->pod, nullptr)) {
+                auto it = ni->node.labels.find(t.topologyKey);
+                if (it != ni->node.labels.end()) cy.antiCounts[{t.topologyKey, it->second}] += 1;
+              }
+          }
+      }
+      if (cy.existingAnti.empty() && cy.ipaReqAff.empty() && cy.ipaReqAnti.empty()) *skip = true;
+      return Status{};
+    }
+  }
+  return Status{};
+}
+
+// ===========================================================================
+// Filter plugins
+// ===========================================================================
+static Status run_filter(Cycle& cy, int p, NodeInfoO* ni) {
+  const Pod& pod = *cy.pod;
+  const Node& node = ni->node;
+  switch (p) {
+    case KSG_PLUGIN_NODE_UNSCHEDULABLE: {  // node_unschedulable.go:125-143
+      if (!node.unschedulable) return Status{};
+      Taint t{"node.kubernetes.io/unschedulable", "", "NoSchedule"};
+      if (!tolerations_tolerate(pod.tolerations, t)) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_UNSCHEDULABLE);
+      return Status{};
+    }
+    case KSG_PLUGIN_NODE_NAME:  // node_name.go:67-83
+      if (!pod.nodeName.empty() && pod.nodeName != node.name)
+        return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_NODE_NAME);
+      return Status{};
+    case KSG_PLUGIN_TAINT_TOLERATION:  // taint_toleration.go:102-116
+      if (find_untolerated_noschedule(node.taints, pod.tolerations))
+        return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_TAINT);
+      return Status{};
+    case KSG_PLUGIN_NODE_AFFINITY: {  // node_affinity.go:207-228
+      if (cy.c->cfg.hasAddedRequired) {
+        bool m = false;
+        for (auto& t : cy.c->cfg.addedRequired)
+          if (t.match(node)) { m = true; break; }
+        if (!m) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_NODE_AFFINITY_ENFORCED);
+      }
+      if (!cy.reqNA.match(node)) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_NODE_AFFINITY_POD);
+      return Status{};
+    }
+    case KSG_PLUGIN_NODE_PORTS:  // node_ports.go:150-176
+      for (auto& w : cy.wantPorts)
+        if (check_conflict(ni->usedPorts, w.ip, w.proto, w.port)) return mk(KSG_CODE_UNSCHEDULABLE, KSG_R_NODE_PORTS);
+      return Status{};
+    case KSG_PLUGIN_NODE_RESOURCES_FIT: {  // fit.go:593-734
+      const Resource& r = cy.podReq;
+      uint32_t reasons = 0;
+      bool unresolvable = false;
+      if ((int64_t)ni->pods.size() + 1 > ni->allocatable.allowedPods) reasons |= KSG_R_TOO_MANY_PODS;
+      bool anyScalar = false;
+      for (auto& kv : r.scalar) anyScalar = true, (void)kv;
+      if (!(r.milliCPU == 0 && r.memory == 0 && r.ephemeral == 0 && !anyScalar)) {
+        if (r.milliCPU > 0 && r.milliCPU > ni->allocatable.milliCPU - ni->requested.milliCPU) {
+          reasons |= KSG_R_INSUFFICIENT_CPU;
+          if (r.milliCPU > ni->allocatable.milliCPU) unresolvable = true;
+        }
+        if (r.memory > 0 && r.memory > ni->allocatable.memory - ni->requested.memory) {
+          reasons |= KSG_R_INSUFFICIENT_MEMORY;
+          if (r.memory > ni->allocatable.memory) unresolvable = true;
+        }
+        if (r.ephemeral > 0 && r.ephemeral > ni->allocatable.ephemeral - ni->requested.ephemeral) {
+          reasons |= KSG_R_INSUFFICIENT_EPHEMERAL;
+          if (r.ephemeral > ni->allocatable.ephemeral) unresolvable = true;
+        }
+        for (auto& kv : r.scalar) {
+          if (kv.second == 0) continue;
+          bool extended = kv.first.find('/') != std::string::npos && kv.first.find("kubernetes.io/") == std::string::npos;
+          if (extended) {
+            std::string prefix = kv.first.substr(0, kv.first.find('/'));
+            if (cy.c->cfg.ignoredResources.count(kv.first) || cy.c->cfg.ignoredResourceGroups.count(prefix)) continue;
+          }
+          int64_t alloc = ni->allocatable.scalar.count(kv.first) ? ni->allocatable.scalar.at(kv.first) : 0;
+          int64_t used = ni->requested.scalar.count(kv.first) ? ni->requested.scalar.at(kv.first) : 0;
+          if (kv.second > alloc - used) {
+            reasons |= KSG_R_INSUFFICIENT_SCALAR;
+            if (kv.second > alloc) unresolvable = true;
+          }
+        }
+      }
+      if (reasons) return mk(unresolvable ? KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : KSG_CODE_UNSCHEDULABLE, reasons);
+      return Status{};
+    }
+    case KSG_PLUGIN_POD_TOPOLOGY_SPREAD: {  // filtering.go:314-359
+      if (cy.ptsF.empty()) return Status{};
+      for (size_t i = 0; i < cy.ptsF.size(); ++i) {
+        auto& con = cy.ptsF[i];
+        auto it = node.labels.find(con.key);
+        if (it == node.labels.end()) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_PTS_MISSING_LABEL);
+        int64_t minMatch = cy.critMin[i];
+        if ((int64_t)cy.tpMatch[i].size() < con.minDomains) minMatch = 0;
+        int64_t self = selector_matches(con.sel, pod.labels) ? 1 : 0;
+        auto mt = cy.tpMatch[i].find(it->second);
+        int64_t matchNum = mt == cy.tpMatch[i].end() ? 0 : mt->second;
+        if (matchNum + self - minMatch > con.maxSkew) return mk(KSG_CODE_UNSCHEDULABLE, KSG_R_PTS_SKEW);
+      }
+      return Status{};
+    }
+    case KSG_PLUGIN_INTER_POD_AFFINITY: {  // interpodaffinity/filtering.go:364-444
+      // satisfyPodAffinity :394-420
+      bool podsExist = true;
+      for (auto& t : cy.ipaReqAff) {
+        auto it = node.labels.find(t.topologyKey);
+        if (it == node.labels.end()) return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_IPA_AFFINITY);
+        auto ct = cy.affCounts.find({t.topologyKey, it->second});
+        if (ct == cy.affCounts.end() || ct->second <= 0) podsExist = false;
+      }
+      if (!podsExist) {
+        if (!(cy.affCounts.empty() && pod_matches_all_terms(cy.ipaReqAff, pod)))
+          return mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_IPA_AFFINITY);
+      }
+      // satisfyPodAntiAffinity :379-391
+      if (!cy.antiCounts.empty())
+        for (auto& t : cy.ipaReqAnti) {
+          auto it = node.labels.find(t.topologyKey);
+          if (it == node.labels.end()) continue;
+          auto ct = cy.antiCounts.find({t.topologyKey, it->second});
+          if (ct != cy.antiCounts.end() && ct->second > 0) return mk(KSG_CODE_UNSCHEDULABLE, KSG_R_IPA_ANTI_AFFINITY);
+        }
+      // satisfyExistingPodsAntiAffinity :364-376
+      if (!cy.existingAnti.empty())
+        for (auto& kv : node.labels) {
+          auto ct = cy.existingAnti.find({kv.first, kv.second});
+          if (ct != cy.existingAnti.end() && ct->second > 0) return mk(KSG_CODE_UNSCHEDULABLE, KSG_R_IPA_EXISTING_ANTI);
+        }
+      return Status{};
+    }
+  }
+  return Status{};
+}
+
+// ===========================================================================
+// Score plugins
+// ===========================================================================
+// resource_allocation.go:236-259 calculatePodResourceRequest
+static int64_t pod_resource_request(const Pod& pod, const std::string& name, bool useRequested) {
+  ResList nonMissing;
+  if (!useRequested) { nonMissing["cpu"] = 100; nonMissing["memory"] = 200LL * 1024 * 1024 * 1000; }
+  ResList reqs = pod_requests(pod, useRequested ? nullptr : &nonMissing);
+  auto it = reqs.find(name);
+  int64_t m = it == reqs.end() ? 0 : it->second;
+  return name == "cpu" ? m : milli_to_value(m);
+}
+
+// resource_allocation.go:167-232
+static void node_alloc_request(const NodeInfoO* ni, const std::vector<std::pair<std::string, int64_t>>& res,
+                               const std::vector<int64_t>& podReqs, bool useRequested,
+                               std::vector<int64_t>* requested, std::vector<int64_t>* allocated,
+                               std::vector<int64_t>* allocatable) {
+  size_t n = res.size();
+  requested->assign(n, 0);
+  allocated->assign(n, 0);
+  allocatable->assign(n, 0);
+  const Resource& rq = useRequested ? ni->requested : ni->nonzero;
+  for (size_t i = 0; i < n; ++i) {
+    const std::string& name = res[i].first;
+    if (podReqs[i] == 0 && is_scalar_resource_name(name)) continue;
+    int64_t a = 0, al = 0;
+    if (name == "cpu") { a = ni->allocatable.milliCPU; al = rq.milliCPU; }
+    else if (name == "memory") { a = ni->allocatable.memory; al = rq.memory; }
+    else if (name == "ephemeral-storage") { a = ni->allocatable.ephemeral; al = ni->requested.ephemeral; }
+    else {
+      auto it = ni->allocatable.scalar.find(name);
+      if (it != ni->allocatable.scalar.end()) {
+        a = it->second;
+        auto jt = ni->requested.scalar.find(name);
+        al = jt == ni->requested.scalar.end() ? 0 : jt->second;
+      }
+    }
+    if (a == 0) continue;
+    (*allocatable)[i] = a;
+    (*allocated)[i] = al;
+    (*requested)[i] = al + podReqs[i];
+  }
+}
+
+static int64_t fit_score(const Config& cfg, const std::vector<int64_t>& requested, const std::vector<int64_t>& allocatable) {
+  int64_t nodeScore = 0, weightSum = 0;
+  const auto& res = cfg.fitResources;
+  if (cfg.fitStrategy == 0) {  // least_allocated.go:30-61
+    for (size_t i = 0; i < requested.size(); ++i) {
+      if (allocatable[i] == 0) continue;
+      int64_t w = res[i].second;
+      int64_t s = requested[i] > allocatable[i] ? 0 : ((allocatable[i] - requested[i]) * 100) / allocatable[i];
+      nodeScore += s * w;
+      weightSum += w;
+    }
+    return weightSum == 0 ? 0 : nodeScore / weightSum;
+  }
+  if (cfg.fitStrategy == 1) {  // most_allocated.go:30-65
+    for (size_t i = 0; i < requested.size(); ++i) {
+      if (allocatable[i] == 0) continue;
+      int64_t w = res[i].second;
+      int64_t rq = requested[i] > allocatable[i] ? allocatable[i] : requested[i];
+      nodeScore += (rq * 100) / allocatable[i] * w;
+      weightSum += w;
+    }
+    return weightSum == 0 ? 0 : nodeScore / weightSum;
+  }
+  // requested_to_capacity_ratio.go:30-58 + helper/shape_score.go:39-51
+  auto shape = [&](int64_t p) -> int64_t {
+    const auto& s = cfg.rtcrShape;
+    for (size_t i = 0; i < s.size(); ++i)
+      if (p <= s[i].first) {
+        if (i == 0) return s[0].second;
+        return s[i - 1].second + (s[i].second - s[i - 1].second) * (p - s[i - 1].first) / (s[i].first - s[i - 1].first);
+      }
+    return s.back().second;
+  };
+  for (size_t i = 0; i < requested.size(); ++i) {
+    if (allocatable[i] == 0) continue;
+    int64_t w = res[i].second;
+    int64_t rs = (requested[i] > allocatable[i]) ? shape(100) : shape(requested[i] * 100 / allocatable[i]);
+    if (rs > 0) { nodeScore += rs * w; weightSum += w; }
+  }
+  if (weightSum == 0) return 0;
+  return (int64_t)std::round((double)nodeScore / (double)weightSum);
+}
+
+static int64_t balanced_resource_score(const std::vector<int64_t>& req, const std::vector<int64_t>& alloc) {  // :220-254
+  std::vector<double> fr;
+  double total = 0;
+  for (size_t i = 0; i < req.size(); ++i) {
+    if (alloc[i] == 0) continue;
+    double f = (double)req[i] / (double)alloc[i];
+    if (f > 1) f = 1;
+    total += f;
+    fr.push_back(f);
+  }
+  double std_ = 0.0;
+  if (fr.size() == 2) {
+    std_ = std::fabs((fr[0] - fr[1]) / 2);
+  } else if (fr.size() > 2) {
+    double mean = total / (double)fr.size();
+    double sum = 0;
+    for (double f : fr) {
+      double d = f - mean;
+      double sq = d * d;
+      sum = sum + sq;
+    }
+    std_ = std::sqrt(sum / (double)fr.size());
+  }
+  double one_minus = 1 - std_;
+  double scaled = one_minus * 100.0;
+  return (int64_t)scaled;
+}
+
+
+// ---- RunPreScorePlugins body for one plugin (framework.go:1300-1333) -------------
+static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& nodes) {
+  ksgo_ctx* c = cy.c;
+  const Pod& pod = *cy.pod;
+  switch (p) {
+    case KSG_PLUGIN_TAINT_TOLERATION:  // taint_toleration.go:140-147
+      cy.tolPrefer.clear();
+      for (auto& t : pod.tolerations)
+        if (t.effect.empty() || t.effect == "PreferNoSchedule") cy.tolPrefer.push_back(t);
+      break;
+    case KSG_PLUGIN_NODE_AFFINITY: {  // node_affinity.go:242-256
+      cy.hasPrefNA = false;
+      if (pod.hasPreferredNA) {
+        if (!new_preferred_terms(pod.preferredNA, &cy.prefNA)) return mk(KSG_CODE_ERROR, 0);
+        cy.hasPrefNA = true;
+      }
+      if (!cy.hasPrefNA && !c->cfg.hasAddedPreferred) return mk(KSG_CODE_SKIP, 0);
+      break;
+    }
+    case KSG_PLUGIN_NODE_RESOURCES_FIT:  // fit.go:136-153
+      cy.fitPodReqs.clear();
+      for (auto& r : c->cfg.fitResources) cy.fitPodReqs.push_back(pod_resource_request(pod, r.first, false));
+      break;
+    case KSG_PLUGIN_BALANCED_ALLOCATION: {  // balanced_allocation.go:78-100
+      cy.balPodReqs.clear();
+      bool best = true;
+      for (auto& r : c->cfg.balancedResources) {
+        cy.balPodReqs.push_back(pod_resource_request(pod, r.first, true));
+        if (cy.balPodReqs.back() != 0) best = false;
+      }
+      if (best) return mk(KSG_CODE_SKIP, 0);
+      break;
+    }
+    case KSG_PLUGIN_POD_TOPOLOGY_SPREAD: {  // scoring.go:118-194
+      if (c->list.empty()) { return mk(KSG_CODE_SKIP, 0); }
+      bool requireAll = !pod.tsc.empty();  // systemDefaulted = true
+      if (!filter_tsc(pod, "ScheduleAnyway", &cy.ptsS)) return mk(KSG_CODE_ERROR, 0);
+      if (cy.ptsS.empty()) { return mk(KSG_CODE_SKIP, 0); }
+      size_t nc = cy.ptsS.size();
+      cy.ignored.clear();
+      cy.tpCounts.assign(nc, {});
+      std::vector<int64_t> topoSize(nc, 0);
+      for (auto* ni : nodes) {  // initPreScoreState :61-115
+        if (requireAll && !node_labels_match_spread(ni->node.labels, cy.ptsS)) {
+          cy.ignored.insert(ni->node.name);
+          continue;
+        }
+        for (size_t i = 0; i < nc; ++i) {
+          if (cy.ptsS[i].key == "kubernetes.io/hostname") continue;
+          auto it = ni->node.labels.find(cy.ptsS[i].key);
+          std::string v = it == ni->node.labels.end() ? "" : it->second;
+          if (!cy.tpCounts[i].count(v)) { cy.tpCounts[i][v] = 0; topoSize[i]++; }
+        }
+      }
+      cy.tpWeight.assign(nc, 0);
+      for (size_t i = 0; i < nc; ++i) {
+        int64_t sz = topoSize[i];
+        if (cy.ptsS[i].key == "kubernetes.io/hostname") sz = (int64_t)nodes.size() - (int64_t)cy.ignored.size();
+        cy.tpWeight[i] = go_log((double)(sz + 2));
+      }
+      cy.reqNA = get_required_node_affinity(pod);
+      for (auto* ni : c->list) {  // processAllNode :155-189
+        if (requireAll && !node_labels_match_spread(ni->node.labels, cy.ptsS)) continue;
+        for (size_t i = 0; i < nc; ++i) {
+          auto& con = cy.ptsS[i];
+          if (!match_inclusion(cy, con, ni->node)) continue;
+          auto it = ni->node.labels.find(con.key);
+          std::string v = it == ni->node.labels.end() ? "" : it->second;
+          auto ct = cy.tpCounts[i].find(v);
+          if (ct == cy.tpCounts[i].end()) continue;
+          ct->second += count_pods_match(ni->pods, con.sel, pod.ns);
+        }
+      }
+      break;
+    }
+    case KSG_PLUGIN_INTER_POD_AFFINITY: {  // interpodaffinity/scoring.go:128-221
+      bool hasPrefA = pod.hasPodAffinity && !pod.affPref.empty();
+      bool hasPrefAnti = pod.hasPodAntiAffinity && !pod.antiPref.empty();
+      bool hasConstraints = hasPrefA || hasPrefAnti;
+      if (c->cfg.ignorePreferredTermsOfExistingPods && !hasConstraints) { return mk(KSG_CODE_SKIP, 0); }
+      PodInfo pi;
+      if (!new_pod_info(pod, &pi)) return mk(KSG_CODE_ERROR, 0);
+      cy.ipaPrefAff = pi.prefAff;
+      cy.ipaPrefAnti = pi.prefAnti;
+      for (auto& t : cy.ipaPrefAff) merge_ns(c, t.term);
+      for (auto& t : cy.ipaPrefAnti) merge_ns(c, t.term);
+      const Labels* nsl = c->ns_labels(pod.ns);
+      cy.topoScore.clear();
+      bool any = false;
+      auto processTerm = [&](std::map<std::string, std::map<std::string, int64_t>>& m, const AffinityTerm& t,
+                             int32_t weight, const Pod& target, const Labels* nl, const Node& node, int32_t mult) {
+        if (t.matches(target, nl)) {
+          auto it = node.labels.find(t.topologyKey);
+          if (it != node.labels.end()) m[t.topologyKey][it->second] += (int64_t)(weight * mult);
+        }
+      };
+      for (auto* ni : c->list) {
+        if (!hasConstraints && ni->podsWithAffinity.empty()) continue;
+        const auto& podsToProcess = hasConstraints ? ni->pods : ni->podsWithAffinity;
+        std::map<std::string, std::map<std::string, int64_t>> ts;
+        for (auto* ep : podsToProcess) {  // processExistingPod :81-125
+          const Node& node = ni->node;
+          if (node.labels.empty()) continue;
+          for (auto& t : cy.ipaPrefAff) processTerm(ts, t.term, t.weight, ep->pod, nullptr, node, 1);
+          for (auto& t : cy.ipaPrefAnti) processTerm(ts, t.term, t.weight, ep->pod, nullptr, node, -1);
+          if (c->cfg.hardPodAffinityWeight > 0)
+            for (auto& t : ep->reqAff) processTerm(ts, t, c->cfg.hardPodAffinityWeight, pod, nsl, node, 1);
+          for (auto& t : ep->prefAff) processTerm(ts, t.term, t.weight, pod, nsl, node, 1);
+          for (auto& t : ep->prefAnti) processTerm(ts, t.term, t.weight, pod, nsl, node, -1);
+        }
+        if (!ts.empty()) {
+          any = true;
+          for (auto& kv : ts)
+            for (auto& vv : kv.second) cy.topoScore[kv.first][vv.first] += vv.second;
+        }
+      }
+      if (!any) return mk(KSG_CODE_SKIP, 0);
+      break;
+    }
+  }
+  return Status{};
+}
+
+// ---- ScorePlugin.Score for one node ---------------------------------------------------
+static int64_t score_node(Cycle& cy, int p, NodeInfoO* ni, int* code) {
+  ksgo_ctx* c = cy.c;
+  const Pod& pod = *cy.pod;
+  const Node& node = ni->node;
+  int64_t s = 0;
+  *code = KSG_CODE_SUCCESS;
+    switch (p) {
+      case KSG_PLUGIN_TAINT_TOLERATION:  // taint_toleration.go:163-196
+        for (auto& t : node.taints)
+          if (t.effect == "PreferNoSchedule" && !tolerations_tolerate(cy.tolPrefer, t)) s++;
+        break;
+      case KSG_PLUGIN_NODE_AFFINITY:  // node_affinity.go:261-286
+        if (c->cfg.hasAddedPreferred) s += preferred_score(c->cfg.addedPreferred, node);
+        if (cy.hasPrefNA) s += preferred_score(cy.prefNA, node);
+        break;
+      case KSG_PLUGIN_NODE_RESOURCES_FIT: {  // fit.go:737-755, resource_allocation.go:138-165
+        if (c->cfg.fitResources.empty()) { *code = KSG_CODE_ERROR; return 0; }  // :149-151
+        std::vector<int64_t> rq, al, ac;
+        node_alloc_request(ni, c->cfg.fitResources, cy.fitPodReqs, false, &rq, &al, &ac);
+        s = fit_score(c->cfg, rq, ac);
+        break;
+      }
+      case KSG_PLUGIN_BALANCED_ALLOCATION: {  // balanced_allocation.go:146-218
+        if (c->cfg.balancedResources.empty()) { *code = KSG_CODE_ERROR; return 0; }
+        std::vector<int64_t> rq, al, ac;
+        node_alloc_request(ni, c->cfg.balancedResources, cy.balPodReqs, true, &rq, &al, &ac);
+        int64_t with = balanced_resource_score(rq, ac);
+        int64_t without = balanced_resource_score(al, ac);
+        s = 100 / 2 + (100 / 2 + with - without) / 2;
+        break;
+      }
+      case KSG_PLUGIN_IMAGE_LOCALITY: {  // image_locality.go:70-152
+        int64_t total = (int64_t)c->list.size();
+        int64_t sum = 0;
+        auto scaled = [&](const std::string& img) {
+          std::string nm = normalized_image_name(img);
+          bool onNode = false;
+          for (auto& im : node.images)
+            for (auto& n : im.names)
+              if (n == nm) onNode = true;
+          if (!onNode) return;
+          ImageState* st = c->image_state(nm);
+          double spread = (double)(int64_t)st->nodes.size() / (double)total;
+          sum += (int64_t)((double)st->size * spread);
+        };
+        for (auto& ctr : pod.initContainers) scaled(ctr.image);
+        for (auto& ctr : pod.containers) scaled(ctr.image);
+        int64_t imageCount = (int64_t)pod.initContainers.size() + (int64_t)pod.containers.size();
+        for (auto& v : pod.imageVolumes) { scaled(v); imageCount++; }
+        const int64_t mb = 1024 * 1024, minT = 23 * mb, maxT = 1000 * mb * imageCount;
+        if (sum < minT) sum = minT;
+        else if (sum > maxT) sum = maxT;
+        s = 100 * (sum - minT) / (maxT - minT);
+        break;
+      }
+      case KSG_PLUGIN_POD_TOPOLOGY_SPREAD: {  // scoring.go:199-226
+        if (cy.ignored.count(node.name)) { s = 0; break; }
+        double score = 0;
+        for (size_t k = 0; k < cy.ptsS.size(); ++k) {
+          auto& con = cy.ptsS[k];
+          auto it = node.labels.find(con.key);
+          if (it == node.labels.end()) continue;
+          int64_t cnt;
+          if (con.key == "kubernetes.io/hostname") cnt = count_pods_match(ni->pods, con.sel, pod.ns);
+          else cnt = cy.tpCounts[k].at(it->second);
+          double prod = (double)cnt * cy.tpWeight[k];
+          double term = prod + (double)(con.maxSkew - 1);
+          score += term;
+        }
+        s = (int64_t)std::round(score);
+        break;
+      }
+      case KSG_PLUGIN_INTER_POD_AFFINITY:  // scoring.go:240-255
+        for (auto& kv : cy.topoScore) {
+          auto it = node.labels.find(kv.first);
+          if (it == node.labels.end()) continue;
+          auto vt = kv.second.find(it->second);
+          if (vt != kv.second.end()) s += vt->second;
+        }
+        break;
+    }
+  return s;
+}
+
+// ---- ScoreExtensions.NormalizeScore -------------------------------------------------
+static void normalize_scores(Cycle& cy, int p, std::vector<int64_t>& sc, const std::vector<NodeInfoO*>& nodes) {
+  const int F = (int)nodes.size();
+
+    if (p == KSG_PLUGIN_TAINT_TOLERATION || p == KSG_PLUGIN_NODE_AFFINITY) {  // helper/normalize_score.go:27-55
+      bool reverse = p == KSG_PLUGIN_TAINT_TOLERATION;
+      int64_t maxCount = 0;
+      for (auto v : sc) maxCount = std::max(maxCount, v);
+      if (maxCount == 0) {
+        if (reverse)
+          for (auto& v : sc) v = 100;
+      } else {
+        for (auto& v : sc) {
+          int64_t x = 100 * v / maxCount;
+          v = reverse ? 100 - x : x;
+        }
+      }
+    } else if (p == KSG_PLUGIN_POD_TOPOLOGY_SPREAD) {  // scoring.go:229-268
+      int64_t mn = INT64_MAX, mx = 0;
+      std::vector<bool> ign(F);
+      for (int i = 0; i < F; ++i) {
+        ign[i] = cy.ignored.count(nodes[i]->node.name) > 0;
+        if (ign[i]) { sc[i] = -1; continue; }
+        mn = std::min(mn, sc[i]);
+        mx = std::max(mx, sc[i]);
+      }
+      for (int i = 0; i < F; ++i) {
+        if (sc[i] == -1) { sc[i] = 0; continue; }
+        if (mx == 0) { sc[i] = 100; continue; }
+        sc[i] = 100 * (mx + mn - sc[i]) / mx;
+      }
+    } else if (p == KSG_PLUGIN_INTER_POD_AFFINITY) {  // scoring.go:258-290
+      if (!cy.topoScore.empty()) {
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+        for (auto v : sc) { mx = std::max(mx, v); mn = std::min(mn, v); }
+        int64_t diff = mx - mn;
+        for (auto& v : sc) {
+          double f = 0;
+          if (diff > 0) f = 100.0 * ((double)(v - mn) / (double)diff);
+          v = (int64_t)f;
+        }
+      }
+    }
+  
+}
+
+}  // namespace
+
+// ===========================================================================
+// schedulePod (schedule_one.go:564-618)
+// ===========================================================================
+static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out* ev) {
+  c->rebuild_list();
+  g_taint_compare_ops = c->cfg.taintCompareOps;
+  const int N = (int)c->list.size();
+  res->status = KSG_CODE_SUCCESS;
+  res->node_index = -1;
+  res->evaluated_nodes = 0;
+  res->feasible_nodes = 0;
+  res->total_score = 0;
+  if (ev) {
+    ev->prefilter_code = 0;
+    ev->prefilter_plugin = KSG_PLUGIN_NONE;
+    ev->score_plugin_mask = 0;
+    for (int i = 0; i < N; ++i) {
+      if (ev->node_code) ev->node_code[i] = 0;
+      if (ev->node_plugin) ev->node_plugin[i] = KSG_PLUGIN_NONE;
+      if (ev->node_reasons) ev->node_reasons[i] = 0;
+      if (ev->total_scores) ev->total_scores[i] = 0;
+    }
+    if (ev->plugin_scores)
+      for (int i = 0; i < N * KSG_NUM_PLUGINS; ++i) ev->plugin_scores[i] = 0;
+  }
+  std::unordered_map<const NodeInfoO*, int> index;
+  for (int i = 0; i < N; ++i) index[c->list[i]] = i;
+  if (N == 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }  // ErrNoNodesAvailable
+
+  Cycle cy;
+  cy.c = c;
+  cy.pod = &pod;
+  cy.reqNA = get_required_node_affinity(pod);  // PTS computes its own copy (filtering.go:257)
+  // ---- RunPreFilterPlugins (framework.go:934-995)
+  Status returnStatus;
+  bool resultAll = true;
+  std::set<std::string> resultNames;
+  for (int p : prefilter_order()) {
+    if (!c->cfg.enabled[p]) { cy.skipFilter[p] = true; continue; }
+    bool skip = false, restricts = false;
+    std::vector<std::string> names;
+    Status s = run_prefilter_plugin(cy, p, &skip, &names, &restricts);
+    if (skip) { cy.skipFilter[p] = true; continue; }
+    if (!s.ok()) {
+      s.plugin = p;
+      if (s.code == KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE) { returnStatus = s; break; }
+      if (s.code == KSG_CODE_UNSCHEDULABLE) { returnStatus = s; continue; }
+      res->status = KSG_CODE_ERROR;
+      if (ev) { ev->prefilter_code = KSG_CODE_ERROR; ev->prefilter_plugin = p; }
+      return KSG_OK;
+    }
+    if (restricts) {  // PreFilterResult.Merge
+      std::set<std::string> ns(names.begin(), names.end());
+      if (resultAll) { resultNames = ns; resultAll = false; }
+      else {
+        std::set<std::string> x;
+        for (auto& n : resultNames)
+          if (ns.count(n)) x.insert(n);
+        resultNames = x;
+      }
+      if (resultNames.empty()) { returnStatus = mk(KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, KSG_R_PREFILTER); returnStatus.plugin = p; break; }
+    }
+  }
+  for (int p = 0; p < KSG_NUM_PLUGINS; ++p)
+    if (!c->cfg.enabled[p]) cy.skipFilter[p] = true;
+  if (!returnStatus.ok()) {  // schedule_one.go:635-648: every node gets the PreFilter status
+    res->status = KSG_CODE_UNSCHEDULABLE;  // FitError
+    res->evaluated_nodes = 0;
+    if (ev) {
+      ev->prefilter_code = returnStatus.code;
+      ev->prefilter_plugin = returnStatus.plugin;
+      for (int i = 0; i < N; ++i) {
+        if (ev->node_code) ev->node_code[i] = (uint8_t)returnStatus.code;
+        if (ev->node_plugin) ev->node_plugin[i] = (uint8_t)returnStatus.plugin;
+        if (ev->node_reasons) ev->node_reasons[i] = returnStatus.reasons | KSG_R_PREFILTER;
+      }
+    }
+    return KSG_OK;
+  }
+
+  // ---- nodes to evaluate (schedule_one.go:671-682; map order -> snapshot order)
+  std::vector<NodeInfoO*> nodes;
+  if (resultAll) nodes = c->list;
+  else {
+    for (auto* ni : c->list)
+      if (resultNames.count(ni->node.name)) nodes.push_back(ni);
+    if (ev)
+      for (int i = 0; i < N; ++i)
+        if (!resultNames.count(c->list[i]->node.name)) {
+          if (ev->node_code) ev->node_code[i] = KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+          if (ev->node_reasons) ev->node_reasons[i] = KSG_R_PREFILTER;
+        }
+  }
+
+  // ---- findNodesThatPassFilters (schedule_one.go:771-854), sequential order
+  bool hasScore = false;
+  for (int p : kScoreOrder)
+    if (c->cfg.enabled[p]) hasScore = true;
+  int numAll = (int)nodes.size();
+  int64_t numToFind;
+  {  // numFeasibleNodesToFind :858-884
+    if (numAll < 100) numToFind = numAll;
+    else {
+      int64_t pct = c->cfg.pct;
+      if (pct == 0) { pct = 50 - numAll / 125; if (pct < 5) pct = 5; }
+      numToFind = (int64_t)numAll * pct / 100;
+      if (numToFind < 100) numToFind = 100;
+    }
+    if (!hasScore) numToFind = 1;
+  }
+  std::vector<NodeInfoO*> feasible;
+  int failed = 0;
+  for (int i = 0; i < numAll; ++i) {
+    NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
+    Status st;
+    for (int p : kFilterOrder) {
+      if (cy.skipFilter[p]) continue;
+      st = run_filter(cy, p, ni);
+      if (!st.ok()) { st.plugin = p; break; }
+    }
+    if (st.ok()) {
+      if ((int64_t)feasible.size() + 1 > numToFind) break;  // cancel: enough feasible nodes
+      feasible.push_back(ni);
+    } else {
+      ++failed;
+      if (ev) {
+        int idx = index[ni];
+        if (ev->node_code) ev->node_code[idx] = (uint8_t)st.code;
+        if (ev->node_plugin) ev->node_plugin[idx] = (uint8_t)st.plugin;
+        if (ev->node_reasons) ev->node_reasons[idx] = st.reasons;
+      }
+    }
+  }
+  int processed = (int)feasible.size() + failed;
+  int diagLen = failed;  // NodeToStatus.Len(): explicit per-node statuses only
+  c->nextStartNodeIndex = (c->nextStartNodeIndex + processed) % N;  // :686-687
+  if (feasible.empty()) {  // FitError (schedule_one.go:579-585)
+    res->status = KSG_CODE_UNSCHEDULABLE;
+    res->feasible_nodes = 0;
+    res->evaluated_nodes = diagLen;
+    return KSG_OK;
+  }
+  res->feasible_nodes = (int)feasible.size();
+  if (feasible.size() == 1) {  // :588-598
+    res->node_index = index[feasible[0]];
+    res->evaluated_nodes = 1 + diagLen;
+    return KSG_OK;
+  }
+  res->evaluated_nodes = (int)feasible.size() + diagLen;
+
+  // ---- prioritizeNodes (:937-1048)
+  const int F = (int)feasible.size();
+  std::vector<int64_t> totals(F, 0);
+  if (!hasScore) {
+    for (int i = 0; i < F; ++i) totals[i] = 1;
+  } else {
+    // RunPreScorePlugins (framework.go:1300-1333)
+    for (int p : kPreScoreOrder) {
+      if (!c->cfg.enabled[p]) { cy.skipScore[p] = true; continue; }
+      Status st = prescore_plugin(cy, p, feasible);
+      if (st.code == KSG_CODE_SKIP) { cy.skipScore[p] = true; continue; }
+      if (!st.ok()) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+    }
+    // RunScorePlugins (framework.go:1351-1458)
+    std::vector<int> active;
+    for (int p : kScoreOrder)
+      if (c->cfg.enabled[p] && !cy.skipScore[p]) active.push_back(p);
+    std::vector<std::vector<int64_t>> scores(active.size(), std::vector<int64_t>(F, 0));
+    for (size_t a = 0; a < active.size(); ++a) {
+      int p = active[a];
+      for (int i = 0; i < F; ++i) {
+        int code;
+        scores[a][i] = score_node(cy, p, feasible[i], &code);
+        if (code != KSG_CODE_SUCCESS) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+      }
+      normalize_scores(cy, p, scores[a], feasible);
+    }
+    // weights + totals (framework.go:1428-1452)
+    for (size_t a = 0; a < active.size(); ++a) {
+      int p = active[a];
+      if (ev) ev->score_plugin_mask |= 1u << p;
+      for (int i = 0; i < F; ++i) {
+        int64_t s = scores[a][i];
+        if (s > 100 || s < 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+        int64_t w = s * c->cfg.weight[p];
+        totals[i] += w;
+        if (ev && ev->plugin_scores) ev->plugin_scores[(size_t)p * N + index[feasible[i]]] = w;
+      }
+    }
+  }
+  if (ev && ev->total_scores)
+    for (int i = 0; i < F; ++i) ev->total_scores[index[feasible[i]]] = totals[i];
+  // ---- host selection: heap.Init + heap.Pop (schedule_one.go:605-606,1054-1063)
+  std::vector<HeapEnt> h(F);
+  for (int i = 0; i < F; ++i) h[i] = {totals[i], 0, i};
+  int win = heap_pop_index(h);
+  res->node_index = index[feasible[win]];
+  res->total_score = totals[win];
+  return KSG_OK;
+}
+
+// ===========================================================================
+// C API
+// ===========================================================================
+extern "C" {
+
+ksgo_ctx* ksgo_create(const char* json, size_t len) {
+  auto* c = new ksgo_ctx();
+  try {
+    if (json && len) {
+      mj::Value v = mj::parse(json, len);
+      std::string err;
+      if (!decode_config(v, &c->cfg, &err) || !validate_config(c->cfg, &err)) {
+        g_create_error = err;
+        delete c;
+        return nullptr;
+      }
+    }
+  } catch (std::exception& e) {
+    g_create_error = e.what();
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+const char* ksgo_create_error(void) { return g_create_error.c_str(); }
+void ksgo_destroy(ksgo_ctx* c) { delete c; }
+const char* ksgo_last_error(const ksgo_ctx* c) { return c->err.c_str(); }
+
+int ksgo_upsert_namespace(ksgo_ctx* c, const char* json, size_t len) {
+  try {
+    Namespace ns;
+    if (!decode_namespace(mj::parse(json, len), &ns, &c->err)) return KSG_EINVAL;
+    c->namespaces[ns.name] = ns;
+    return KSG_OK;
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+
+static void add_node_images(ksgo_ctx* c, const Node& n) {  // cache.go:712-735
+  for (auto& im : n.images)
+    for (auto& name : im.names) {
+      auto it = c->imageStates.find(name);
+      if (it == c->imageStates.end()) {
+        ImageState st;
+        st.size = im.sizeBytes;
+        st.nodes.insert(n.name);
+        c->imageStates[name] = st;
+      } else {
+        it->second.nodes.insert(n.name);
+      }
+    }
+}
+static void remove_node_images(ksgo_ctx* c, const Node& n) {  // cache.go:740-759
+  for (auto& im : n.images)
+    for (auto& name : im.names) {
+      auto it = c->imageStates.find(name);
+      if (it != c->imageStates.end()) {
+        it->second.nodes.erase(n.name);
+        if (it->second.nodes.empty()) c->imageStates.erase(it);
+      }
+    }
+}
+static void tree_add(ksgo_ctx* c, const Node& n) {  // node_tree.go:52-70
+  std::string z = get_zone_key(n);
+  auto it = c->tree.find(z);
+  if (it == c->tree.end()) { c->zones.push_back(z); c->tree[z] = {n.name}; }
+  else {
+    for (auto& nm : it->second)
+      if (nm == n.name) return;
+    it->second.push_back(n.name);
+  }
+}
+static void tree_remove(ksgo_ctx* c, const Node& n) {  // node_tree.go:73-98
+  std::string z = get_zone_key(n);
+  auto it = c->tree.find(z);
+  if (it == c->tree.end()) return;
+  auto& na = it->second;
+  for (size_t i = 0; i < na.size(); ++i)
+    if (na[i] == n.name) {
+      na.erase(na.begin() + i);
+      if (na.empty()) {
+        c->tree.erase(it);
+        c->zones.erase(std::find(c->zones.begin(), c->zones.end(), z));
+      }
+      return;
+    }
+}
+
+int ksgo_add_node(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:630-646
+  try {
+    Node n;
+    if (!decode_node(mj::parse(json, len), &n, &c->err)) return KSG_EINVAL;
+    auto it = c->nodes.find(n.name);
+    NodeInfoO* ni;
+    if (it == c->nodes.end()) {
+      auto up = std::make_unique<NodeInfoO>();
+      ni = up.get();
+      c->nodes[n.name] = std::move(up);
+    } else {
+      ni = it->second.get();
+      remove_node_images(c, ni->node);
+    }
+    tree_add(c, n);
+    add_node_images(c, n);
+    ni->node = n;
+    ni->allocatable = node_allocatable(n);
+    c->listDirty = true;
+    return KSG_OK;
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+
+int ksgo_update_node(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:648-670
+  try {
+    Node n;
+    if (!decode_node(mj::parse(json, len), &n, &c->err)) return KSG_EINVAL;
+    auto it = c->nodes.find(n.name);
+    if (it == c->nodes.end()) return ksgo_add_node(c, json, len);
+    NodeInfoO* ni = it->second.get();
+    remove_node_images(c, ni->node);
+    if (get_zone_key(ni->node) != get_zone_key(n)) { tree_remove(c, ni->node); tree_add(c, n); }
+    add_node_images(c, n);
+    ni->node = n;
+    ni->allocatable = node_allocatable(n);
+    c->listDirty = true;
+    return KSG_OK;
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+
+int ksgo_remove_node(ksgo_ctx* c, const char* name) {  // cache.go:672-695
+  auto it = c->nodes.find(name);
+  if (it == c->nodes.end()) return KSG_ENOTFOUND;
+  remove_node_images(c, it->second->node);
+  tree_remove(c, it->second->node);
+  for (auto* p : it->second->pods) c->pods.erase(p->pod.uid);
+  c->nodes.erase(it);
+  c->listDirty = true;
+  return KSG_OK;
+}
+
+int ksgo_add_pod(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:515-545 addPod
+  try {
+    Pod p;
+    if (!decode_pod(mj::parse(json, len), &p, &c->err)) return KSG_EINVAL;
+    if (p.nodeName.empty()) { c->err = "pod is not bound"; return KSG_EINVAL; }
+    if (c->pods.count(p.uid)) { c->err = "pod exists"; return KSG_EEXIST; }
+    auto it = c->nodes.find(p.nodeName);
+    if (it == c->nodes.end()) { c->err = "unknown node " + p.nodeName; return KSG_ENOTFOUND; }
+    auto pi = std::make_unique<PodInfo>();
+    new_pod_info(p, pi.get());
+    node_add_pod(*it->second, pi.get());
+    c->pods[p.uid] = std::move(pi);
+    return KSG_OK;
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+
+int ksgo_remove_pod(ksgo_ctx* c, const char* uid) {
+  auto it = c->pods.find(uid);
+  if (it == c->pods.end()) return KSG_ENOTFOUND;
+  auto nt = c->nodes.find(it->second->pod.nodeName);
+  if (nt != c->nodes.end()) node_remove_pod(*nt->second, uid);
+  c->pods.erase(it);
+  return KSG_OK;
+}
+
+int ksgo_num_nodes(const ksgo_ctx* c) {
+  const_cast<ksgo_ctx*>(c)->rebuild_list();
+  return (int)c->list.size();
+}
+
+int ksgo_node_name(const ksgo_ctx* c, int32_t index, char* buf, size_t cap) {
+  const_cast<ksgo_ctx*>(c)->rebuild_list();
+  if (index < 0 || index >= (int32_t)c->list.size()) return KSG_ENOTFOUND;
+  const std::string& n = c->list[index]->node.name;
+  if (buf && cap) {
+    size_t k = std::min(cap - 1, n.size());
+    std::memcpy(buf, n.data(), k);
+    buf[k] = 0;
+  }
+  return (int)n.size();
+}
+
+int ksgo_pod_compile(ksgo_ctx* c, const char* json, size_t len, int32_t* handle) {
+  try {
+    auto p = std::make_unique<Pod>();
+    if (!decode_pod(mj::parse(json, len), p.get(), &c->err)) return KSG_EINVAL;
+    int32_t h = c->nextHandle++;
+    c->queue[h] = std::move(p);
+    *handle = h;
+    return KSG_OK;
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+
+int ksgo_pod_release(ksgo_ctx* c, int32_t handle) {
+  return c->queue.erase(handle) ? KSG_OK : KSG_ENOTFOUND;
+}
+
+int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* result, ksg_eval_out* ev) {
+  auto it = c->queue.find(handle);
+  if (it == c->queue.end()) return KSG_ENOTFOUND;
+  int rc = run_cycle(c, *it->second, result, ev);
+  if (rc != KSG_OK) return rc;
+  if ((flags & KSG_FLAG_ASSUME) && result->status == KSG_CODE_SUCCESS && result->node_index >= 0) {
+    // Scheduler.assume (schedule_one.go:1102-1137) -> Cache.AssumePod (cache.go:397)
+    Pod p = *it->second;
+    p.nodeName = c->list[result->node_index]->node.name;
+    if (c->pods.count(p.uid)) p.uid = p.uid + "#" + std::to_string(handle);
+    auto pi = std::make_unique<PodInfo>();
+    new_pod_info(p, pi.get());
+    node_add_pod(*c->nodes[p.nodeName], pi.get());
+    c->assumedUid[handle] = p.uid;
+    c->pods[p.uid] = std::move(pi);
+  }
+  return KSG_OK;
+}
+
+int ksgo_schedule_batch(ksgo_ctx* c, const int32_t* handles, int32_t n, uint32_t flags, ksg_result* results) {
+  for (int32_t i = 0; i < n; ++i) {
+    int rc = ksgo_schedule_one(c, handles[i], flags, &results[i], nullptr);
+    if (rc != KSG_OK) return rc;
+  }
+  return KSG_OK;
+}
+
+int ksgo_forget(ksgo_ctx* c, int32_t handle) {  // Cache.ForgetPod (cache.go:412-434)
+  auto it = c->assumedUid.find(handle);
+  if (it == c->assumedUid.end()) return KSG_ENOTFOUND;
+  int rc = ksgo_remove_pod(c, it->second.c_str());
+  c->assumedUid.erase(it);
+  return rc;
+}
+
+
+// ---- plugin-granular entry points (FilterPlugin / ScorePlugin contracts) --------------
+static Cycle* new_cycle(ksgo_ctx* c, const Pod& pod) {
+  c->rebuild_list();
+  g_taint_compare_ops = c->cfg.taintCompareOps;
+  Cycle* cy = new Cycle();
+  cy->c = c;
+  cy->pod = &pod;
+  cy->reqNA = get_required_node_affinity(pod);
+  return cy;
+}
+
+int ksgo_run_filter_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, int32_t* prefilter_code, uint8_t* codes,
+                           uint32_t* reasons) {
+  auto it = c->queue.find(handle);
+  if (it == c->queue.end()) return KSG_ENOTFOUND;
+  if (plugin < 0 || plugin > KSG_PLUGIN_INTER_POD_AFFINITY) return KSG_EINVAL;
+  std::unique_ptr<Cycle> cy(new_cycle(c, *it->second));
+  const int N = (int)c->list.size();
+  *prefilter_code = KSG_CODE_SUCCESS;
+  for (int i = 0; i < N; ++i) { codes[i] = 0; reasons[i] = 0; }
+  bool hasPre = false;
+  for (int p : prefilter_order()) hasPre |= p == plugin;
+  if (hasPre) {
+    bool skip = false, restricts = false;
+    std::vector<std::string> names;
+    Status s = run_prefilter_plugin(*cy, plugin, &skip, &names, &restricts);
+    if (skip) { *prefilter_code = KSG_CODE_SKIP; return KSG_OK; }
+    if (!s.ok()) {
+      *prefilter_code = s.code;
+      for (int i = 0; i < N; ++i) { codes[i] = (uint8_t)s.code; reasons[i] = s.reasons | KSG_R_PREFILTER; }
+      return KSG_OK;
+    }
+  }
+  for (int i = 0; i < N; ++i) {
+    Status st = run_filter(*cy, plugin, c->list[i]);
+    codes[i] = (uint8_t)st.code;
+    reasons[i] = st.reasons;
+  }
+  return KSG_OK;
+}
+
+int ksgo_run_score_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, int32_t* status_code, int64_t* raw,
+                          int64_t* normalized) {
+  auto it = c->queue.find(handle);
+  if (it == c->queue.end()) return KSG_ENOTFOUND;
+  bool isScore = false;
+  for (int p : kScoreOrder) isScore |= p == plugin;
+  if (!isScore) return KSG_EINVAL;
+  std::unique_ptr<Cycle> cy(new_cycle(c, *it->second));
+  const int N = (int)c->list.size();
+  for (int i = 0; i < N; ++i) { raw[i] = 0; normalized[i] = 0; }
+  *status_code = KSG_CODE_SUCCESS;
+  bool hasPre = false;
+  for (int p : kPreScoreOrder) hasPre |= p == plugin;
+  if (hasPre) {
+    Status st = prescore_plugin(*cy, plugin, c->list);
+    if (!st.ok()) { *status_code = st.code; return KSG_OK; }
+  }
+  std::vector<int64_t> sc(N);
+  for (int i = 0; i < N; ++i) {
+    int code;
+    sc[i] = score_node(*cy, plugin, c->list[i], &code);
+    raw[i] = sc[i];
+    if (code != KSG_CODE_SUCCESS) *status_code = code;
+  }
+  if (*status_code != KSG_CODE_SUCCESS) return KSG_OK;
+  normalize_scores(*cy, plugin, sc, c->list);
+  for (int i = 0; i < N; ++i) normalized[i] = sc[i];
+  return KSG_OK;
+}
+
+double ksgo_go_log(double x) { return go_log(x); }
+
+int32_t ksgo_heap_root(const int64_t* scores, int32_t n) {
+  if (n <= 0) return -1;
+  std::vector<HeapEnt> h(n);
+  for (int32_t i = 0; i < n; ++i) h[i] = {scores[i], 0, i};
+  return heap_pop_index(h);
+}
+
+}  // extern "C"

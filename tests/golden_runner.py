@@ -1,0 +1,96 @@
+"""Runs the golden fixtures (tests/golden/*.json) against any ksg.h backend."""
+import glob
+import json
+import os
+
+from ksg.abi import KsgError
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_cases():
+    out = []
+    for path in sorted(glob.glob(os.path.join(HERE, "golden", "*.json"))):
+        group = os.path.splitext(os.path.basename(path))[0]
+        with open(path) as f:
+            for i, c in enumerate(json.load(f)["cases"]):
+                out.append((f"{group}[{i}] {c['name']}", c))
+    return out
+
+
+def build(make_backend, case):
+    b = make_backend(case.get("config") or {})
+    for ns in case.get("namespaces", []):
+        b.upsert_namespace(ns)
+    for n in case["nodes"]:
+        b.add_node(n)
+    for p in case.get("existing", []):
+        b.add_pod(p)
+    return b
+
+
+def run_case(make_backend, case):
+    """Returns a list of mismatch strings (empty == parity)."""
+    if case["kind"] == "config_error":
+        try:
+            make_backend(case["config"])
+        except KsgError:
+            return []
+        return ["config accepted but the reference rejects it"]
+    b = build(make_backend, case)
+    names = b.node_names()
+    h = b.compile(case["pod"])
+    want_names = [n["metadata"]["name"] for n in case["nodes"]]
+    errs = []
+    e = case["expect"]
+    if case["kind"] == "score":
+        st, raw, nrm = b.run_score_plugin(h, case["plugin"])
+        if st != e["status"]:
+            errs.append(f"status {st} != {e['status']}")
+        if e["status"] in (0,):
+            got = nrm if "normalized" in e else raw
+            want = e.get("normalized", e.get("raw"))
+            by = dict(zip(names, got))
+            gl = [by[n] for n in want_names]
+            if gl != want:
+                errs.append(f"scores {gl} != {want}")
+    elif case["kind"] == "filter":
+        pc, codes, reasons = b.run_filter_plugin(h, case["plugin"])
+        if pc != e["prefilter"]:
+            errs.append(f"prefilter {pc} != {e['prefilter']}")
+        if e["prefilter"] == 0:
+            byc = dict(zip(names, codes))
+            gl = [byc[n] for n in want_names]
+            if gl != e["codes"]:
+                errs.append(f"codes {gl} != {e['codes']}")
+            if "reasons" in e:
+                byr = dict(zip(names, reasons))
+                gr = [byr[n] for n in want_names]
+                if gr != e["reasons"]:
+                    errs.append(f"reasons {gr} != {e['reasons']}")
+    elif case["kind"] == "cycle":
+        errs += run_cycle_case(b, case, names)
+    b.close()
+    return errs
+
+
+def run_cycle_case(b, case, names):
+    errs = []
+    e = case["expect"]
+    r, ev = b.schedule_one(b.compile(case["pod"]), assume=False, evaluate=True)
+    if "node" in e:
+        got = names[r.node_index] if r.node_index >= 0 else None
+        if got != e["node"]:
+            errs.append(f"node {got} != {e['node']}")
+    if "status" in e and r.status != e["status"]:
+        errs.append(f"status {r.status} != {e['status']}")
+    if "totals" in e:
+        by = dict(zip(names, ev["total_scores"]))
+        for n, v in e["totals"].items():
+            if by[n] != v:
+                errs.append(f"total[{n}] {by[n]} != {v}")
+    if "feasible" in e and r.feasible_nodes != e["feasible"]:
+        errs.append(f"feasible {r.feasible_nodes} != {e['feasible']}")
+    if "evaluated" in e and r.evaluated_nodes != e["evaluated"]:
+        errs.append(f"evaluated {r.evaluated_nodes} != {e['evaluated']}")
+    return errs
