@@ -1,0 +1,183 @@
+"""Throughput of the MI355X node-evaluation path on scheduler_perf SchedulingBasic (BASELINE C2).
+
+Workload (BASELINE.json configs[1]): 5000 node-default nodes, 1000 bound init pods, then the
+measured pod-default pods scheduled one cycle at a time (each assume lands before the next
+pod), percentageOfNodesToScore=100, default plugins.  A "step" is one ksg_schedule_batch over
+`--batch` pods; the default 10 steps x 1000 pods are the config's 10000 measured pods.
+Warmup pods are scheduled and then forgotten (Cache.ForgetPod) so the timed region starts
+from the config's initial state.  Pod objects are decoded into the queue (ksg_pod_compile)
+before timing, as the informer would have delivered them; the timed region covers PreFilter/
+PreScore compilation, the H2D descriptor copy, both kernels per pod, the D2H results and the
+host-side assume bookkeeping.
+
+Multi-GPU (--gpus N under torch.distributed.run): every rank runs its own scheduler replica
+over its own copy of the cluster and its own pod stream (weak scaling, no data-path
+collective); DESIGN.md §6 describes the node-sharded RCCL design that replaces this for C5.
+
+The CPU baseline is the parity oracle (oracle/, a C++ restatement of the reference) timed
+on a bounded sample of the same pod stream from the same initial state, one host thread.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-kubernetes_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, "HBM")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--init-pods", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=1000)
+    ap.add_argument("--timing-stride", type=int, default=8, help="time every k-th filter kernel with HIP events")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the oracle CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_filter_score.json"),
+                    help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
+    return ap.parse_args()
+
+
+def cpu_baseline(nodes, init, pods, budget_s):
+    """Oracle (C++ restatement of the reference), 1 thread, same pods from the same state."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_binding import oracle
+    o = oracle({})
+    for n in nodes:
+        o.add_node(n)
+    for p in init:
+        o.add_pod(p)
+    hs = [o.compile(p) for p in pods]
+    done = 0
+    t0 = time.perf_counter()
+    chunk = 50
+    while done < len(hs) and time.perf_counter() - t0 < budget_s:
+        o.schedule_batch(hs[done:done + chunk], assume=True)
+        done += min(chunk, len(hs) - done)
+    dt = time.perf_counter() - t0
+    o.close()
+    return done / dt, done, dt
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    from ksg.native import Scheduler
+    from ksg.synth import scheduling_basic
+
+    n_meas = a.steps * a.batch
+    n_warm = a.warmup * a.batch
+    nodes, init, pods = scheduling_basic(a.nodes, a.init_pods, n_warm + n_meas)
+    for k, p in enumerate(pods):  # distinct uids per rank (independent replicas)
+        p["metadata"]["uid"] = f"r{rank}-{k}"
+    s = Scheduler({"device": local, "kernelTimingStride": a.timing_stride})
+    for n in nodes:
+        s.add_node(n)
+    for p in init:
+        s.add_pod(p)
+    handles = [s.compile(p) for p in pods]
+    warm, meas = handles[:n_warm], handles[n_warm:]
+
+    for w in range(a.warmup):  # untimed; then ForgetPod so the timed run starts from the config state
+        s.schedule_batch(warm[w * a.batch:(w + 1) * a.batch], assume=True)
+    for h in warm:
+        try:
+            s.forget(h)
+        except Exception:
+            pass
+
+    placed = 0
+    kstats = []
+    barrier()
+    t0 = time.perf_counter()
+    for st in range(a.steps):
+        rs = s.schedule_batch(meas[st * a.batch:(st + 1) * a.batch], assume=True)
+        kstats.append(s.kernel_stats())
+        placed += sum(1 for r in rs if r.status == 0)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        pl = torch.tensor([placed], dtype=torch.int64, device="cuda")
+        dist.all_reduce(pl)
+        placed = int(pl.item())
+
+    total_pods = n_meas * world
+    pods_s = total_pods / dt
+    evals_s = pods_s * a.nodes
+    kms = sum(k[0] for k in kstats) / len(kstats)
+    kbytes = sum(k[1] for k in kstats) / len(kstats)
+    achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    traffic = None
+    if os.path.exists(a.traffic):
+        try:
+            tj = json.load(open(a.traffic))
+            if tj.get("nodes") == a.nodes:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds)
+            cpu = {"value": round(v, 2), "unit": "pods/s", "cores": 1, "kind": "port",
+                   "node_evals_per_s": round(v * a.nodes, 1),
+                   "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
+                             f"{cdt:.1f} s, oracle/ C++ restatement, 1 thread"}
+        out = {
+            "metric": "pods scheduled/sec + node-evals/sec at 5k/100k nodes, 1/2/4/8 MI355X",
+            "value": round(pods_s, 2),
+            "unit": "pods/s",
+            "node_evals_per_s": round(evals_s, 1),
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (scheduler_perf node-default / pod-default templates, seeded)",
+            "config": {"workload": f"SchedulingBasic {a.nodes} nodes / {a.init_pods} init pods / "
+                                   f"{n_meas} measured pods per GPU (BASELINE configs[1])",
+                       "nodes": a.nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": 100,
+                       "plugins": "default", "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "placed": placed,
+            "roofline": {"bound": "hbm", "kernel": "k_filter_score", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic, "avg_kernel_us": round(kms * 1e3, 3),
+                         "algo_bytes_per_launch": round(kbytes, 1)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    s.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

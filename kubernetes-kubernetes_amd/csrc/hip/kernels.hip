@@ -1,0 +1,633 @@
+// kernels.hip -- per-pod node evaluation on gfx950 (CDNA4, wave64).
+//
+// One pod is evaluated by two launches over the snapshot's nodes (one thread per node,
+// 256-thread blocks = 4 waves):
+//
+//   k_filter_score  : RunFilterPlugins for every node (framework/runtime/framework.go:1105-1138)
+//                     in the default filter order, the raw Score of every active plugin for
+//                     the feasible nodes (framework.go:1378-1402), the feasibility bitmask by
+//                     wave ballots, per-block feasible counts, and per-plugin max/min of the
+//                     raw scores that a NormalizeScore needs (block reduction + one atomic).
+//   k_select        : NormalizeScore + weight + sum (framework.go:1409-1452) for every feasible
+//                     node, the node's position in the feasible list (global prefix of the
+//                     per-block counts + ballot popcounts), the packed (TotalScore, heap
+//                     pre-order key) max that reproduces heap.Init+Pop (schedule_one.go:
+//                     1054-1085), and -- in the last block to arrive -- the winner lookup and
+//                     the device-side AssumePod (NodeInfo.update, framework/types.go:445-468).
+//
+// Integer arithmetic is int64 with truncating division as in Go; the two FP64 paths
+// (BalancedAllocation, RequestedToCapacityRatio rounding) are compiled with
+// -ffp-contract=off so no a*b+c is fused (Go/amd64 never fuses).
+#include <hip/hip_runtime.h>
+
+#include "../common/desc.h"
+
+namespace ksg {
+
+#define KSG_R_UNSCHEDULABLE (1u << 0)
+#define KSG_R_NODE_NAME (1u << 1)
+#define KSG_R_TAINT (1u << 2)
+#define KSG_R_NODE_AFFINITY_POD (1u << 3)
+#define KSG_R_NODE_AFFINITY_ENFORCED (1u << 4)
+#define KSG_R_NODE_PORTS (1u << 5)
+#define KSG_R_TOO_MANY_PODS (1u << 6)
+#define KSG_R_INSUFFICIENT_CPU (1u << 7)
+#define KSG_R_INSUFFICIENT_MEMORY (1u << 8)
+#define KSG_R_INSUFFICIENT_EPHEMERAL (1u << 9)
+#define KSG_R_INSUFFICIENT_SCALAR (1u << 10)
+#define KSG_R_PREFILTER (1u << 16)
+
+enum : int { P_UNSCHED = 0, P_NODENAME = 1, P_TAINT = 2, P_NA = 3, P_PORTS = 4, P_FIT = 5, P_PTS = 6,
+             P_IPA = 7, P_BAL = 8, P_IMG = 9 };
+enum : uint32_t { C_OK = 0, C_ERROR = 1, C_UNSCHED = 2, C_UU = 3 };
+
+template <typename T>
+__device__ __forceinline__ const T* at(const uint8_t* base, int32_t off) {
+  return reinterpret_cast<const T*>(base + off);
+}
+__device__ __forceinline__ bool bit(const uint8_t* base, int32_t off, uint32_t id, int32_t nwords) {
+  uint32_t w = id >> 5;
+  if ((int32_t)w >= nwords) return false;
+  return (at<uint32_t>(base, off)[w] >> (id & 31u)) & 1u;
+}
+
+// ---- selector programs ---------------------------------------------------------------------
+// labels.Requirement.Matches (apimachinery/pkg/labels/selector.go:247-294) against the
+// node's label columns; metadata.name field requirements (nodeaffinity.go:190-201).
+__device__ bool req_match(const MirrorView& m, const uint8_t* base, const PodDesc& d, const SelReq& r, int i) {
+  const size_t col = (size_t)r.slot * (size_t)m.cap + (size_t)i;
+  switch (r.op) {
+    case SEL_IN:
+    case SEL_NOTIN: {
+      int32_t v = m.labels[col];
+      if (v < 0) return r.op == SEL_NOTIN;
+      const int32_t* vals = at<int32_t>(base, d.vals_off) + r.vals_off;
+      bool has = false;
+      for (int k = 0; k < r.nvals; ++k) has |= vals[k] == v;
+      return r.op == SEL_IN ? has : !has;
+    }
+    case SEL_EXISTS: return m.labels[col] >= 0;
+    case SEL_DNE: return m.labels[col] < 0;
+    case SEL_GT:
+    case SEL_LT: {
+      if (m.labels[col] < 0 || !m.label_num_ok[col]) return false;
+      int64_t x = m.label_num[col];
+      return r.op == SEL_GT ? x > r.num : x < r.num;
+    }
+    case SEL_NODE_EQ: return (int64_t)i == r.num;
+    case SEL_NODE_NE: return (int64_t)i != r.num;
+    case SEL_TRUE: return true;
+    default: return false;
+  }
+}
+__device__ bool term_match(const MirrorView& m, const uint8_t* base, const PodDesc& d, const SelTerm& t, int i) {
+  if (t.parse_err) return false;
+  const SelReq* reqs = at<SelReq>(base, d.req_off) + t.req_off;
+  for (int k = 0; k < t.nreq; ++k)
+    if (!req_match(m, base, d, reqs[k], i)) return false;
+  return true;
+}
+__device__ bool prog_any(const MirrorView& m, const uint8_t* base, const PodDesc& d, SelProg p, int i) {
+  const SelTerm* terms = at<SelTerm>(base, p.term_off);
+  for (int k = 0; k < p.nterm; ++k)
+    if (term_match(m, base, d, terms[k], i)) return true;
+  return false;
+}
+__device__ int64_t prog_weight(const MirrorView& m, const uint8_t* base, const PodDesc& d, SelProg p, int i) {
+  const SelTerm* terms = at<SelTerm>(base, p.term_off);
+  int64_t s = 0;
+  for (int k = 0; k < p.nterm; ++k)
+    if (term_match(m, base, d, terms[k], i)) s += terms[k].weight;
+  return s;
+}
+
+// ---- resources --------------------------------------------------------------------------------
+__device__ __forceinline__ void node_res(const MirrorView& m, const ScoreRes& r, int i, bool useRequested,
+                                         int64_t* alloc, int64_t* allocated) {
+  // resource_allocation.go:198-232 calculateResourceAllocatableRequest
+  switch (r.kind) {
+    case RES_CPU: *alloc = m.alloc_cpu[i]; *allocated = useRequested ? m.req_cpu[i] : m.nz_cpu[i]; break;
+    case RES_MEM: *alloc = m.alloc_mem[i]; *allocated = useRequested ? m.req_mem[i] : m.nz_mem[i]; break;
+    case RES_EPH: *alloc = m.alloc_eph[i]; *allocated = m.req_eph[i]; break;
+    case RES_SCALAR: {
+      size_t c = (size_t)r.slot * (size_t)m.cap + (size_t)i;
+      *alloc = m.scalar_alloc[c];
+      *allocated = m.scalar_req[c];
+      break;
+    }
+    default: *alloc = 0; *allocated = 0;
+  }
+}
+
+__device__ int64_t rtcr_shape(const uint8_t* base, const PodDesc& d, int64_t p) {  // helper/shape_score.go:39-51
+  const int64_t* s = at<int64_t>(base, d.rtcr_off);
+  for (int k = 0; k < d.n_rtcr; ++k)
+    if (p <= s[2 * k]) {
+      if (k == 0) return s[1];
+      return s[2 * k - 1] + (s[2 * k + 1] - s[2 * k - 1]) * (p - s[2 * k - 2]) / (s[2 * k] - s[2 * k - 2]);
+    }
+  return s[2 * d.n_rtcr - 1];
+}
+
+// NodeResourcesFit.Score (fit.go:737-755 -> resource_allocation.go:138-193 + scorer)
+__device__ int64_t fit_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+  const ScoreRes* res = at<ScoreRes>(base, d.fit_res_off);
+  int64_t nodeScore = 0, weightSum = 0;
+  for (int k = 0; k < d.n_fit_res; ++k) {
+    const ScoreRes r = res[k];
+    if (r.kind == RES_SKIP) continue;
+    int64_t alloc, allocated;
+    node_res(m, r, i, false, &alloc, &allocated);
+    if (alloc == 0) continue;
+    int64_t requested = allocated + r.pod_req;
+    int64_t s;
+    if (d.fit_strategy == 0) {  // least_allocated.go:52-61
+      s = requested > alloc ? 0 : ((alloc - requested) * 100) / alloc;
+    } else if (d.fit_strategy == 1) {  // most_allocated.go:55-65
+      int64_t rq = requested > alloc ? alloc : requested;
+      s = (rq * 100) / alloc;
+    } else {  // requested_to_capacity_ratio.go:30-36
+      s = requested > alloc ? rtcr_shape(base, d, 100) : rtcr_shape(base, d, requested * 100 / alloc);
+      if (s <= 0) continue;
+    }
+    nodeScore += s * r.weight;
+    weightSum += r.weight;
+  }
+  if (weightSum == 0) return 0;
+  if (d.fit_strategy == 2) return (int64_t)round((double)nodeScore / (double)weightSum);
+  return nodeScore / weightSum;
+}
+
+// balanced_allocation.go:220-254
+__device__ int64_t balanced_score(const int64_t* req, const int64_t* alloc, int n) {
+  double fr[8];
+  int nf = 0;
+  double total = 0;
+  for (int k = 0; k < n; ++k) {
+    if (alloc[k] == 0) continue;
+    double f = (double)req[k] / (double)alloc[k];
+    if (f > 1) f = 1;
+    total = total + f;
+    fr[nf++] = f;
+  }
+  double sd = 0.0;
+  if (nf == 2) {
+    sd = fabs((fr[0] - fr[1]) / 2);
+  } else if (nf > 2) {
+    double mean = total / (double)nf;
+    double sum = 0;
+    for (int k = 0; k < nf; ++k) {
+      double dd = fr[k] - mean;
+      double sq = dd * dd;
+      sum = sum + sq;
+    }
+    sd = sqrt(sum / (double)nf);
+  }
+  double om = 1 - sd;
+  double sc = om * 100.0;
+  return (int64_t)sc;
+}
+
+__device__ int64_t balanced_alloc_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+  const ScoreRes* res = at<ScoreRes>(base, d.bal_res_off);
+  int64_t requested[8], allocated[8], allocatable[8];
+  int n = d.n_bal_res;
+  for (int k = 0; k < n; ++k) {
+    requested[k] = allocated[k] = allocatable[k] = 0;
+    const ScoreRes r = res[k];
+    if (r.kind == RES_SKIP) continue;
+    int64_t alloc, al;
+    node_res(m, r, i, true, &alloc, &al);
+    if (alloc == 0) continue;
+    allocatable[k] = alloc;
+    allocated[k] = al;
+    requested[k] = al + r.pod_req;
+  }
+  int64_t with = balanced_score(requested, allocatable, n);
+  int64_t without = balanced_score(allocated, allocatable, n);
+  return 100 / 2 + (100 / 2 + with - without) / 2;  // balanced_allocation.go:204-218
+}
+
+// image_locality.go:70-152 (per-image scaled scores precomputed per pod on the host)
+__device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+  const ImageTerm* terms = at<ImageTerm>(base, d.img_off);
+  const uint32_t lo = m.img_off[i], hi = m.img_off[i + 1];
+  int64_t sum = 0;
+  for (int k = 0; k < d.n_img; ++k) {
+    const uint32_t want = (uint32_t)terms[k].image;
+    bool on = false;
+    for (uint32_t q = lo; q < hi; ++q) on |= m.img_ids[q] == want;
+    if (on) sum += terms[k].scaled * terms[k].mult;
+  }
+  const int64_t mb = 1024 * 1024, minT = 23 * mb, maxT = 1000 * mb * d.img_count;
+  if (sum < minT) sum = minT;
+  else if (sum > maxT) sum = maxT;
+  return 100 * (sum - minT) / (maxT - minT);
+}
+
+// ---- filters ------------------------------------------------------------------------------------
+// Returns the packed Filter status of node i (0 = Success), first failing plugin in the
+// RunFilterPlugins order wins.  *raw_taint gets the PreferNoSchedule count while the taint
+// list is in registers.
+__device__ uint32_t run_filters(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i,
+                                int64_t* raw_taint) {
+  const uint32_t fm = d.filter_mask;
+  // NodeUnschedulable (node_unschedulable.go:125-143)
+  if ((fm >> P_UNSCHED) & 1u)
+    if ((m.flags[i] & 1u) && !(d.flags & DF_TOLERATES_UNSCHED)) return pack_status(C_UU, P_UNSCHED, KSG_R_UNSCHEDULABLE);
+  // NodeName (node_name.go:67-83)
+  if ((fm >> P_NODENAME) & 1u)
+    if (d.node_name != -1 && d.node_name != i) return pack_status(C_UU, P_NODENAME, KSG_R_NODE_NAME);
+  // TaintToleration (taint_toleration.go:102-116, 163-196)
+  {
+    const uint32_t lo = m.taint_off[i], hi = m.taint_off[i + 1];
+    bool untol = false;
+    int64_t cnt = 0;
+    for (uint32_t q = lo; q < hi; ++q) {
+      uint32_t id = m.taint_ids[q];
+      untol |= bit(base, d.untol_ns_off, id, d.n_taint_words);
+      cnt += bit(base, d.intol_pns_off, id, d.n_taint_words) ? 1 : 0;
+    }
+    *raw_taint = cnt;
+    if (((fm >> P_TAINT) & 1u) && untol) return pack_status(C_UU, P_TAINT, KSG_R_TAINT);
+  }
+  // NodeAffinity (node_affinity.go:207-228)
+  if ((fm >> P_NA) & 1u) {
+    if ((d.flags & DF_HAS_ADDED_NA) && !prog_any(m, base, d, d.na_added, i))
+      return pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_ENFORCED);
+    if ((d.flags & DF_HAS_SELECTOR) && !prog_any(m, base, d, d.na_selector, i))
+      return pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_POD);
+    if ((d.flags & DF_HAS_REQUIRED_NA) && !prog_any(m, base, d, d.na_required, i))
+      return pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_POD);
+  }
+  // NodePorts (node_ports.go:150-176 -> HostPortInfo.CheckConflict, precompiled per port id)
+  if ((fm >> P_PORTS) & 1u) {
+    const uint32_t* slots = m.ports + (size_t)i * kPortSlots;
+    for (int s = 0; s < kPortSlots; ++s) {
+      uint32_t pid = slots[s];
+      if (pid != 0xffffffffu && bit(base, d.port_conflict_off, pid, d.n_port_words))
+        return pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
+    }
+  }
+  // NodeResourcesFit (fit.go:593-734 fitsRequest)
+  if ((fm >> P_FIT) & 1u) {
+    uint32_t reasons = 0;
+    bool unresolvable = false;
+    if ((int64_t)m.num_pods[i] + 1 > (int64_t)m.alloc_pods[i]) reasons |= KSG_R_TOO_MANY_PODS;
+    if (d.fit_any) {
+      const int64_t acpu = m.alloc_cpu[i], amem = m.alloc_mem[i], aeph = m.alloc_eph[i];
+      if (d.req_cpu > 0 && d.req_cpu > acpu - m.req_cpu[i]) {
+        reasons |= KSG_R_INSUFFICIENT_CPU;
+        unresolvable |= d.req_cpu > acpu;
+      }
+      if (d.req_mem > 0 && d.req_mem > amem - m.req_mem[i]) {
+        reasons |= KSG_R_INSUFFICIENT_MEMORY;
+        unresolvable |= d.req_mem > amem;
+      }
+      if (d.req_eph > 0 && d.req_eph > aeph - m.req_eph[i]) {
+        reasons |= KSG_R_INSUFFICIENT_EPHEMERAL;
+        unresolvable |= d.req_eph > aeph;
+      }
+      const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
+      for (int k = 0; k < d.n_scalar; ++k) {
+        size_t c = (size_t)sr[k].slot * (size_t)m.cap + (size_t)i;
+        int64_t a = m.scalar_alloc[c];
+        if (sr[k].qty > a - m.scalar_req[c]) {
+          reasons |= KSG_R_INSUFFICIENT_SCALAR;
+          unresolvable |= sr[k].qty > a;
+        }
+      }
+    }
+    if (reasons) return pack_status(unresolvable ? C_UU : C_UNSCHED, P_FIT, reasons);
+  }
+  return 0;
+}
+
+// ---- wave/block reductions ------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = __shfl_xor(v, o, 64);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// =====================================================================================================
+// k_filter_score
+// =====================================================================================================
+__global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView b, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool valid = i < m.n;
+  const bool eval = (d.flags & DF_EVAL_OUT) != 0;
+
+  uint32_t st = 0;
+  int64_t raw_taint = 0;
+  if (valid) {
+    if (d.flags & DF_PREFILTER_REJECT) {
+      st = pack_status((uint32_t)d.prefilter_code, (uint32_t)d.prefilter_plugin & 15u, KSG_R_PREFILTER);
+    } else if (d.flags & DF_SUBSET) {
+      // PreFilterResult.NodeNames: nodes outside are UnschedulableAndUnresolvable (schedule_one.go:671-682)
+      const int32_t* sub = at<int32_t>(base, d.subset_off);
+      bool in = false;
+      for (int k = 0; k < d.subset_cnt; ++k) in |= sub[k] == i;
+      st = in ? 0u : pack_status(C_UU, 15u, KSG_R_PREFILTER);
+    }
+    if (st == 0) {
+      uint32_t f = run_filters(m, base, d, i, &raw_taint);
+      st = (d.flags & DF_ALL_FEASIBLE) ? 0u : f;
+    }
+  }
+  const bool feas = valid && st == 0;
+  const unsigned long long ballot = __ballot(feas);
+  if (lane == 0) b.fmask[(size_t)blockIdx.x * (kBlock / 64) + wave] = ballot;
+  if (valid) b.status[i] = st;
+
+  // raw scores of the feasible nodes (framework.go:1378-1402)
+  int64_t fixed = 0;
+  int64_t rawv[kNumPlugins];
+#pragma unroll
+  for (int p = 0; p < kNumPlugins; ++p) rawv[p] = 0;
+  const uint32_t sm = d.score_mask;
+  if (feas) {
+    if ((sm >> P_TAINT) & 1u) rawv[P_TAINT] = raw_taint;
+    if ((sm >> P_NA) & 1u) {
+      int64_t s = 0;
+      if (d.flags & DF_HAS_ADDED_PREF) s += prog_weight(m, base, d, d.na_added_pref, i);
+      if (d.flags & DF_HAS_PREF_NA) s += prog_weight(m, base, d, d.na_preferred, i);
+      rawv[P_NA] = s;
+    }
+    if ((sm >> P_FIT) & 1u) { rawv[P_FIT] = fit_score(m, base, d, i); fixed += rawv[P_FIT] * d.weight[P_FIT]; }
+    if ((sm >> P_BAL) & 1u) { rawv[P_BAL] = balanced_alloc_score(m, base, d, i); fixed += rawv[P_BAL] * d.weight[P_BAL]; }
+    if ((sm >> P_IMG) & 1u) { rawv[P_IMG] = image_score(m, base, d, i); fixed += rawv[P_IMG] * d.weight[P_IMG]; }
+    b.fixed[i] = fixed;
+    const size_t cap = (size_t)m.cap;
+    if ((sm >> P_TAINT) & 1u) b.raw[P_TAINT * cap + i] = rawv[P_TAINT];
+    if ((sm >> P_NA) & 1u) b.raw[P_NA * cap + i] = rawv[P_NA];
+    if (eval) {
+      b.raw[P_FIT * cap + i] = rawv[P_FIT];
+      b.raw[P_BAL * cap + i] = rawv[P_BAL];
+      b.raw[P_IMG * cap + i] = rawv[P_IMG];
+    }
+  }
+
+  // per-block feasible count + per-plugin max of the normalising plugins' raw scores
+  __shared__ uint32_t s_cnt[kBlock / 64];
+  __shared__ unsigned long long s_max[2][kBlock / 64];
+  unsigned long long mt = feas ? enc_i64(rawv[P_TAINT]) : 0ull;
+  unsigned long long mn = feas ? enc_i64(rawv[P_NA]) : 0ull;
+  mt = wave_max_u64(mt);
+  mn = wave_max_u64(mn);
+  if (lane == 0) {
+    s_cnt[wave] = (uint32_t)__popcll(ballot);
+    s_max[0][wave] = mt;
+    s_max[1][wave] = mn;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    unsigned long long a = 0, bb = 0;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      c += s_cnt[w];
+      a = s_max[0][w] > a ? s_max[0][w] : a;
+      bb = s_max[1][w] > bb ? s_max[1][w] : bb;
+    }
+    b.blk_cnt[blockIdx.x] = c;
+    if (c) {
+      PodStats* ps = b.stats + pod;
+      if ((sm >> P_TAINT) & 1u) atomicMax(&ps->max_raw[P_TAINT], a);
+      if ((sm >> P_NA) & 1u) atomicMax(&ps->max_raw[P_NA], bb);
+    }
+  }
+}
+
+// =====================================================================================================
+// k_select
+// =====================================================================================================
+__device__ __forceinline__ uint32_t wave_prefix_count(unsigned long long ballot, int lane) {
+  return (uint32_t)__popcll(lane ? (ballot & ((1ull << lane) - 1ull)) : 0ull);
+}
+
+__global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, int pod, int nblocks) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cap = (size_t)m.cap;
+  const bool eval = (d.flags & DF_EVAL_OUT) != 0;
+
+  // ---- global feasible count F, this block's exclusive prefix, and P(s) = feasible nodes
+  // before the rotation start (nextStartNodeIndex, schedule_one.go:808) -- one strided pass
+  const int s = d.rot_start;
+  const int sb = s / kBlock;
+  __shared__ uint32_t s_red[kBlock / 64][3];
+  uint32_t pre = 0, tot = 0, pres = 0;
+  for (int k = threadIdx.x; k < nblocks; k += kBlock) {
+    uint32_t c = b.blk_cnt[k];
+    tot += c;
+    if (k < (int)blockIdx.x) pre += c;
+    if (k < sb) pres += c;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pre += __shfl_xor(pre, o, 64);
+    tot += __shfl_xor(tot, o, 64);
+    pres += __shfl_xor(pres, o, 64);
+  }
+  if (lane == 0) { s_red[wave][0] = pre; s_red[wave][1] = tot; s_red[wave][2] = pres; }
+  __syncthreads();
+  pre = 0;
+  tot = 0;
+  pres = 0;
+  for (int w = 0; w < kBlock / 64; ++w) { pre += s_red[w][0]; tot += s_red[w][1]; pres += s_red[w][2]; }
+  const uint32_t F = tot;
+  uint32_t ps_before = 0;
+  if (s > 0 && F > 0) {
+    const uint64_t* fw = b.fmask + (size_t)sb * (kBlock / 64);
+    int rem = s - sb * kBlock;
+    uint32_t acc = pres;
+    for (int w = 0; w < kBlock / 64 && rem > 0; ++w) {
+      int take = rem >= 64 ? 64 : rem;
+      uint64_t msk = take == 64 ? ~0ull : ((1ull << take) - 1ull);
+      acc += (uint32_t)__popcll(fw[w] & msk);
+      rem -= take;
+    }
+    ps_before = acc;
+  }
+
+  // ---- normalise + weight + total for this node (framework.go:1409-1452)
+  const unsigned long long ballot = b.fmask[(size_t)blockIdx.x * (kBlock / 64) + wave];
+  __shared__ uint32_t s_wcnt[kBlock / 64];
+  if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(ballot);
+  __syncthreads();
+  uint32_t wave_pre = 0;
+  for (int w = 0; w < wave; ++w) wave_pre += s_wcnt[w];
+  const bool feas = i < m.n && ((ballot >> lane) & 1ull);
+
+  unsigned long long key = 0;
+  if (feas) {
+    const uint32_t g = pre + wave_pre + wave_prefix_count(ballot, lane);  // rank in snapshot order
+    const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;  // rank in evaluation order
+    int64_t total;
+    if (d.flags & DF_NO_SCORE) {
+      total = 1;
+    } else {
+      total = b.fixed[i];
+      const uint32_t sm = d.score_mask;
+      if ((sm >> P_TAINT) & 1u) {  // DefaultNormalizeScore(100, reverse=true) (helper/normalize_score.go:27-55)
+        const int64_t mx = dec_i64(ps->max_raw[P_TAINT]);
+        const int64_t r = b.raw[P_TAINT * cap + i];
+        const int64_t v = mx == 0 ? 100 : 100 - 100 * r / mx;
+        total += v * d.weight[P_TAINT];
+        if (eval) b.out_scores[P_TAINT * cap + i] = v * d.weight[P_TAINT];
+      }
+      if ((sm >> P_NA) & 1u) {  // DefaultNormalizeScore(100, reverse=false)
+        const int64_t mx = dec_i64(ps->max_raw[P_NA]);
+        const int64_t r = b.raw[P_NA * cap + i];
+        const int64_t v = mx == 0 ? 0 : 100 * r / mx;
+        total += v * d.weight[P_NA];
+        if (eval) b.out_scores[P_NA * cap + i] = v * d.weight[P_NA];
+      }
+      if (eval) {
+        if ((sm >> P_FIT) & 1u) b.out_scores[P_FIT * cap + i] = b.raw[P_FIT * cap + i] * d.weight[P_FIT];
+        if ((sm >> P_BAL) & 1u) b.out_scores[P_BAL * cap + i] = b.raw[P_BAL * cap + i] * d.weight[P_BAL];
+        if ((sm >> P_IMG) & 1u) b.out_scores[P_IMG * cap + i] = b.raw[P_IMG * cap + i] * d.weight[P_IMG];
+      }
+    }
+    if (eval) b.out_total[i] = total;
+    key = pack_best(total, pos);
+  }
+  key = wave_max_u64(key);
+  __shared__ unsigned long long s_key[kBlock / 64];
+  if (lane == 0) s_key[wave] = key;
+  __syncthreads();
+
+  // ---- one atomic per block, then the arrival ticket (Guideline 16: release before the ticket)
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    unsigned long long k = 0;
+    for (int w = 0; w < kBlock / 64; ++w) k = s_key[w] > k ? s_key[w] : k;
+    if (k) atomicMax(&ps->best, k);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    uint32_t t = atomicAdd(&ps->done, 1u);
+    s_last = (t == (uint32_t)nblocks - 1u) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  // ================= last block: winner lookup + AssumePod =================
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __shared__ uint32_t s_chunk[kBlock + 1];
+  __shared__ int s_node;
+  if (threadIdx.x == 0) s_node = -1;
+  const unsigned long long best = __hip_atomic_load(&ps->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (F > 0) {
+    // heap position of the winner -> global feasible rank g (undo the rotation)
+    const uint32_t pos = preorder_pos((1u << kPreBits) - 1u - (uint32_t)(best & ((1ull << kPreBits) - 1ull)));
+    uint32_t g = pos + ps_before;
+    if (g >= F) g -= F;
+    // each thread owns a contiguous chunk of blocks; exclusive scan of chunk sums in LDS
+    const int per = (nblocks + kBlock - 1) / kBlock;
+    const int c0 = threadIdx.x * per;
+    const int c1 = (c0 + per) < nblocks ? (c0 + per) : nblocks;
+    uint32_t csum = 0;
+    for (int k = c0; k < c1; ++k) csum += b.blk_cnt[k];
+    s_chunk[threadIdx.x + 1] = csum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_chunk[0] = 0;
+      for (int k = 1; k <= kBlock; ++k) s_chunk[k] += s_chunk[k - 1];
+    }
+    __syncthreads();
+    uint32_t acc = s_chunk[threadIdx.x];
+    if (g >= acc && g < s_chunk[threadIdx.x + 1]) {  // exactly one thread owns rank g
+      for (int k = c0; k < c1; ++k) {
+        const uint32_t c = b.blk_cnt[k];
+        if (g < acc + c) {
+          uint32_t need = g - acc;
+          const uint64_t* fw = b.fmask + (size_t)k * (kBlock / 64);
+          for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t wc = (uint32_t)__popcll(fw[w]);
+            if (need < wc) {
+              uint64_t x = fw[w];
+              for (uint32_t q = 0; q < need; ++q) x &= x - 1ull;  // drop the lowest set bits
+              s_node = k * kBlock + w * 64 + (int)__builtin_ctzll(x);
+              break;
+            }
+            need -= wc;
+          }
+          break;
+        }
+        acc += c;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    DevResult r;
+    r.node = F > 0 ? s_node : -1;
+    r.feasible = (int32_t)F;
+    r.evaluated = 0;
+    r.total = F > 0 ? (int64_t)(best >> kPreBits) : 0;
+    r.key = best;
+    r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
+    if (d.flags & DF_PREFILTER_REJECT) r.status = (int32_t)C_UNSCHED;
+    if ((d.flags & DF_SCORE_ERROR) && F > 1) {  // prioritizeNodes error (schedule_one.go:600-603)
+      r.status = (int32_t)C_ERROR;
+      r.node = -1;
+    }
+    ps->feasible = F;
+    // AssumePod (schedule_one.go:1102-1137 -> NodeInfo.update, framework/types.go:445-468)
+    if ((d.flags & DF_ASSUME) && r.node >= 0) {
+      const int j = r.node;
+      m.req_cpu[j] += d.a_cpu;
+      m.req_mem[j] += d.a_mem;
+      m.req_eph[j] += d.a_eph;
+      m.nz_cpu[j] += d.a_nz_cpu;
+      m.nz_mem[j] += d.a_nz_mem;
+      m.num_pods[j] += 1;
+      const ScalarReq* sr = at<ScalarReq>(base, d.a_scalar_off);
+      for (int k = 0; k < d.n_a_scalar; ++k) m.scalar_req[(size_t)sr[k].slot * cap + j] += sr[k].qty;
+      const uint32_t* pp = at<uint32_t>(base, d.pod_ports_off);
+      uint32_t* slots = m.ports + (size_t)j * kPortSlots;
+      for (int k = 0; k < d.n_pod_ports; ++k) {  // HostPortInfo.Add: set semantics
+        bool present = false;
+        int empty = -1;
+        for (int q = 0; q < kPortSlots; ++q) {
+          present |= slots[q] == pp[k];
+          if (slots[q] == 0xffffffffu && empty < 0) empty = q;
+        }
+        if (!present && empty >= 0) slots[empty] = pp[k];
+      }
+    }
+    b.results[pod] = r;
+  }
+}
+
+}  // namespace ksg
+
+// ---- host-side launchers (C++ linkage, called by the host library) ------------------------------
+namespace ksg {
+hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
+  const int nb = (m.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_filter_score, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
+  return hipGetLastError();
+}
+hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
+  const int nb = (m.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_select, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
+  return hipGetLastError();
+}
+}  // namespace ksg

@@ -1,0 +1,244 @@
+// capi.cpp -- the extern "C" boundary declared in include/ksg.h.
+//
+// Every entry point catches C++ exceptions and maps them to KSG_E* codes; nothing here falls
+// back to a CPU evaluation -- a missing/broken device is KSG_EDEVICE.
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+
+#include "host.hpp"
+
+using namespace ksg;
+
+struct ksg_ctx {
+  std::unique_ptr<Cluster> cluster;
+  std::unique_ptr<Engine> engine;
+  std::string err;
+};
+
+static thread_local std::string g_create_error;
+
+#define GUARD(body)                                   \
+  try {                                               \
+    body                                              \
+  } catch (const std::bad_alloc&) {                   \
+    ctx->err = "out of memory";                       \
+    return KSG_ENOMEM;                                \
+  } catch (const std::exception& e) {                 \
+    ctx->err = e.what();                              \
+    return KSG_EINVAL;                                \
+  }
+
+static int with_err(ksg_ctx* ctx, int rc) {
+  if (rc != KSG_OK) {
+    if (!ctx->cluster->err.empty()) ctx->err = ctx->cluster->err;
+    ctx->cluster->err.clear();
+  }
+  return rc;
+}
+
+extern "C" {
+
+ksg_ctx* ksg_create(const char* config_json, size_t len) {
+  try {
+    Config cfg;
+    std::string err;
+    if (config_json && len && !decode_config(config_json, len, &cfg, &err)) {
+      g_create_error = err;
+      return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+      g_create_error = "no HIP device visible (the engine has no CPU fallback)";
+      return nullptr;
+    }
+    if (cfg.device < 0 || cfg.device >= ndev) {
+      g_create_error = "device index out of range";
+      return nullptr;
+    }
+    auto* ctx = new ksg_ctx();
+    ctx->cluster.reset(new Cluster(cfg));
+    if (!ctx->cluster->err.empty()) {
+      g_create_error = ctx->cluster->err;
+      delete ctx;
+      return nullptr;
+    }
+    ctx->engine.reset(new Engine(ctx->cluster.get()));
+    return ctx;
+  } catch (const std::exception& e) {
+    g_create_error = e.what();
+    return nullptr;
+  }
+}
+
+const char* ksg_create_error(void) { return g_create_error.c_str(); }
+
+void ksg_destroy(ksg_ctx* ctx) {
+  if (!ctx) return;
+  ctx->engine.reset();
+  ctx->cluster.reset();
+  delete ctx;
+}
+
+const char* ksg_last_error(const ksg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int ksg_upsert_namespace(ksg_ctx* ctx, const char* ns_json, size_t len) {
+  if (!ctx || !ns_json) return KSG_EINVAL;
+  GUARD({
+    NamespaceSpec ns;
+    if (!decode_namespace(ns_json, len, &ns, &ctx->err)) return KSG_EINVAL;
+    return with_err(ctx, ctx->cluster->upsert_namespace(ns));
+  })
+}
+
+int ksg_add_node(ksg_ctx* ctx, const char* node_json, size_t len) {
+  if (!ctx || !node_json) return KSG_EINVAL;
+  GUARD({
+    NodeSpec n;
+    if (!decode_node(node_json, len, &n, &ctx->err)) return KSG_EINVAL;
+    return with_err(ctx, ctx->cluster->add_node(std::move(n)));
+  })
+}
+
+int ksg_update_node(ksg_ctx* ctx, const char* node_json, size_t len) {
+  if (!ctx || !node_json) return KSG_EINVAL;
+  GUARD({
+    NodeSpec n;
+    if (!decode_node(node_json, len, &n, &ctx->err)) return KSG_EINVAL;
+    return with_err(ctx, ctx->cluster->update_node(std::move(n)));
+  })
+}
+
+int ksg_remove_node(ksg_ctx* ctx, const char* name) {
+  if (!ctx || !name) return KSG_EINVAL;
+  GUARD({ return with_err(ctx, ctx->cluster->remove_node(name)); })
+}
+
+int ksg_add_pod(ksg_ctx* ctx, const char* pod_json, size_t len) {
+  if (!ctx || !pod_json) return KSG_EINVAL;
+  GUARD({
+    PodSpec p;
+    if (!decode_pod(pod_json, len, &p, &ctx->err)) return KSG_EINVAL;
+    if (p.node_name.empty()) {
+      ctx->err = "ksg_add_pod: pod is not bound (spec.nodeName empty)";
+      return KSG_EINVAL;
+    }
+    return with_err(ctx, ctx->cluster->add_pod(p));
+  })
+}
+
+int ksg_remove_pod(ksg_ctx* ctx, const char* uid) {
+  if (!ctx || !uid) return KSG_EINVAL;
+  GUARD({ return with_err(ctx, ctx->cluster->remove_pod(uid)); })
+}
+
+int ksg_num_nodes(const ksg_ctx* ctx) {
+  if (!ctx) return KSG_EINVAL;
+  return (int)const_cast<ksg_ctx*>(ctx)->cluster->order().size();
+}
+
+int ksg_node_name(const ksg_ctx* ctx, int32_t index, char* buf, size_t cap) {
+  if (!ctx) return KSG_EINVAL;
+  const auto& o = const_cast<ksg_ctx*>(ctx)->cluster->order();
+  if (index < 0 || (size_t)index >= o.size()) return KSG_ENOTFOUND;
+  const std::string& s = o[(size_t)index];
+  if (buf && cap) {
+    size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int)s.size();
+}
+
+int ksg_pod_compile(ksg_ctx* ctx, const char* pod_json, size_t len, int32_t* handle) {
+  if (!ctx || !pod_json || !handle) return KSG_EINVAL;
+  GUARD({
+    PodSpec p;
+    if (!decode_pod(pod_json, len, &p, &ctx->err)) return KSG_EINVAL;
+    const int32_t h = ctx->engine->next_handle++;
+    ctx->engine->queue[h] = std::move(p);
+    *handle = h;
+    return KSG_OK;
+  })
+}
+
+int ksg_pod_release(ksg_ctx* ctx, int32_t handle) {
+  if (!ctx) return KSG_EINVAL;
+  return ctx->engine->queue.erase(handle) ? KSG_OK : KSG_ENOTFOUND;
+}
+
+int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* result, ksg_eval_out* eval) {
+  if (!ctx || !result) return KSG_EINVAL;
+  GUARD({
+    auto it = ctx->engine->queue.find(handle);
+    if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    std::vector<const PodSpec*> pods{&it->second};
+    std::vector<int32_t> hs{handle};
+    return with_err(ctx, ctx->engine->run_batch(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, result, eval));
+  })
+}
+
+int ksg_schedule_batch(ksg_ctx* ctx, const int32_t* handles, int32_t n, uint32_t flags, ksg_result* results) {
+  if (!ctx || n < 0 || (n && (!handles || !results))) return KSG_EINVAL;
+  GUARD({
+    std::vector<const PodSpec*> pods;
+    std::vector<int32_t> hs(handles, handles + n);
+    pods.reserve((size_t)n);
+    for (int32_t i = 0; i < n; ++i) {
+      auto it = ctx->engine->queue.find(handles[i]);
+      if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+      pods.push_back(&it->second);
+    }
+    return with_err(ctx, ctx->engine->run_batch(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, results, nullptr));
+  })
+}
+
+int ksg_forget(ksg_ctx* ctx, int32_t handle) {  // Cache.ForgetPod (backend/cache/cache.go:412-434)
+  if (!ctx) return KSG_EINVAL;
+  GUARD({
+    auto it = ctx->engine->assumed.find(handle);
+    if (it == ctx->engine->assumed.end()) return KSG_ENOTFOUND;
+    std::string uid = it->second;
+    ctx->engine->assumed.erase(it);
+    return with_err(ctx, ctx->cluster->remove_pod(uid));
+  })
+}
+
+int ksg_run_filter_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t* prefilter_code, uint8_t* codes,
+                          uint32_t* reasons) {
+  if (!ctx || !prefilter_code || plugin < 0 || plugin > KSG_PLUGIN_INTER_POD_AFFINITY) return KSG_EINVAL;
+  GUARD({
+    auto it = ctx->engine->queue.find(handle);
+    if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::FILTER_ONE, plugin, prefilter_code, codes,
+                                                 reasons, nullptr, nullptr));
+  })
+}
+
+int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t* status_code, int64_t* raw,
+                         int64_t* normalized) {
+  if (!ctx || !status_code) return KSG_EINVAL;
+  if (plugin != KSG_PLUGIN_TAINT_TOLERATION && plugin != KSG_PLUGIN_NODE_AFFINITY &&
+      plugin != KSG_PLUGIN_NODE_RESOURCES_FIT && plugin != KSG_PLUGIN_POD_TOPOLOGY_SPREAD &&
+      plugin != KSG_PLUGIN_INTER_POD_AFFINITY && plugin != KSG_PLUGIN_BALANCED_ALLOCATION &&
+      plugin != KSG_PLUGIN_IMAGE_LOCALITY)
+    return KSG_EINVAL;
+  GUARD({
+    auto it = ctx->engine->queue.find(handle);
+    if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::SCORE_ONE, plugin, status_code, nullptr,
+                                                 nullptr, raw, normalized));
+  })
+}
+
+int ksg_last_batch_kernel_stats(const ksg_ctx* ctx, double* avg_kernel_ms, double* bytes_per_launch,
+                                int32_t* launches) {
+  if (!ctx) return KSG_EINVAL;
+  if (avg_kernel_ms) *avg_kernel_ms = ctx->engine->last_kernel_ms;
+  if (bytes_per_launch) *bytes_per_launch = ctx->engine->last_bytes;
+  if (launches) *launches = ctx->engine->last_launches;
+  return KSG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,480 @@
+// cluster.cpp -- host cache shadow and the HBM mirror of the snapshot.
+//
+// Mirrors backend/cache/cache.go (AddNode/UpdateNode/RemoveNode :630-695, AddPod/RemovePod
+// :515-597, image states :712-759), NodeInfo.update (framework/types.go:445-468) and the
+// nodeTree zone round-robin order (node_tree.go:52-143).  Node add/remove re-lays the mirror
+// out (the snapshot list is rebuilt then too, cache.go:318-358); pod events touch one node.
+#include <algorithm>
+#include <cstring>
+
+#include "host.hpp"
+
+namespace ksg {
+
+static const char* zone_key(const NodeSpec& n, std::string* out) {  // node/topology/helpers.go:31-58
+  auto get = [&](const char* a, const char* b) -> std::string {
+    for (auto& kv : n.labels)
+      if (kv.first == a) return kv.second;
+    for (auto& kv : n.labels)
+      if (kv.first == b) return kv.second;
+    return "";
+  };
+  std::string zone = get("failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone");
+  std::string region = get("failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region");
+  if (region.empty() && zone.empty()) out->clear();
+  else *out = region + std::string(":\0:", 3) + zone;
+  return out->c_str();
+}
+
+Cluster::Cluster(const Config& c) : cfg(c) {
+  std::memset(&view, 0, sizeof(view));
+  if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+    err = "cannot open HIP device " + std::to_string(cfg.device);
+}
+
+Cluster::~Cluster() {
+  free_all();
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+void* Cluster::dalloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+  bufs_.push_back({p, bytes});
+  return p;
+}
+void Cluster::free_all() {
+  for (auto& b : bufs_) (void)hipFree(b.p);
+  bufs_.clear();
+}
+
+int32_t Cluster::key_id(const std::string& k) {
+  int32_t id = label_keys.get(k);
+  if ((size_t)id >= keys.size()) keys.resize(id + 1);
+  return id;
+}
+int32_t Cluster::scalar_slot(const std::string& n) {
+  int32_t id = scalar_ix.find(n);
+  if (id >= 0) return id;
+  if ((int)scalar_ix.strs.size() >= kMaxScalar) return -1;
+  layout_dirty = true;  // a new column must exist on the device
+  return scalar_ix.get(n);
+}
+uint32_t Cluster::port_id(std::string ip, std::string proto, int32_t port) {  // HostPortInfo.sanitize
+  if (ip.empty()) ip = "0.0.0.0";
+  if (proto.empty()) proto = "TCP";
+  std::string k = ip + "/" + proto + "/" + std::to_string(port);
+  int32_t id = port_ix.find(k);
+  if (id >= 0) return (uint32_t)id;
+  id = port_ix.get(k);
+  ports.push_back({ip, proto, port});
+  return (uint32_t)id;
+}
+
+// ---- nodeTree ---------------------------------------------------------------------------------
+void Cluster::tree_add(const NodeSpec& n) {
+  std::string z;
+  zone_key(n, &z);
+  auto it = tree_.find(z);
+  if (it == tree_.end()) {
+    zones_.push_back(z);
+    tree_[z] = {n.name};
+  } else if (std::find(it->second.begin(), it->second.end(), n.name) == it->second.end()) {
+    it->second.push_back(n.name);
+  }
+  order_dirty_ = true;
+}
+void Cluster::tree_remove(const NodeSpec& n) {
+  std::string z;
+  zone_key(n, &z);
+  auto it = tree_.find(z);
+  if (it == tree_.end()) return;
+  auto& v = it->second;
+  auto jt = std::find(v.begin(), v.end(), n.name);
+  if (jt == v.end()) return;
+  v.erase(jt);
+  if (v.empty()) {
+    tree_.erase(it);
+    zones_.erase(std::find(zones_.begin(), zones_.end(), z));
+  }
+  order_dirty_ = true;
+}
+const std::vector<std::string>& Cluster::order() {
+  if (order_dirty_) {
+    order_.clear();
+    size_t longest = 0;
+    for (auto& z : zones_) longest = std::max(longest, tree_[z].size());
+    for (size_t k = 0; k < longest; ++k)
+      for (auto& z : zones_) {
+        auto& v = tree_[z];
+        if (k < v.size()) order_.push_back(v[k]);
+      }
+    index_.clear();
+    for (size_t i = 0; i < order_.size(); ++i) index_[order_[i]] = (int32_t)i;
+    order_dirty_ = false;
+    layout_dirty = true;
+  }
+  return order_;
+}
+int32_t Cluster::index_of(const std::string& n) const {
+  auto it = index_.find(n);
+  return it == index_.end() ? -1 : it->second;
+}
+NodeRec* Cluster::node(const std::string& name) {
+  auto it = nodes_.find(name);
+  return it == nodes_.end() ? nullptr : it->second.get();
+}
+
+// ---- cache events -------------------------------------------------------------------------------
+int Cluster::upsert_namespace(const NamespaceSpec& ns) {
+  namespaces[ns.name] = ns;
+  return KSG_OK;
+}
+
+void Cluster::add_images(const NodeSpec& n) {
+  for (auto& im : n.images)
+    for (auto& name : im.names) {
+      auto it = image_states.find(name);
+      if (it == image_states.end()) {
+        ImageState st;
+        st.size = im.size;  // first registration wins (cache.go:717-722)
+        st.nodes.insert(n.name);
+        image_states.emplace(name, std::move(st));
+      } else {
+        it->second.nodes.insert(n.name);
+      }
+      image_ix.get(name);
+    }
+}
+void Cluster::remove_images(const NodeSpec& n) {
+  for (auto& im : n.images)
+    for (auto& name : im.names) {
+      auto it = image_states.find(name);
+      if (it == image_states.end()) continue;
+      it->second.nodes.erase(n.name);
+      if (it->second.nodes.empty()) image_states.erase(it);
+    }
+}
+
+void Cluster::intern_node(NodeRec& r) {
+  r.labels.clear();
+  for (auto& kv : r.spec.labels) {
+    int32_t k = key_id(kv.first);
+    r.labels.push_back({k, keys[k].values.get(kv.second)});
+  }
+  r.taint_ids.clear();
+  for (auto& t : r.spec.taints) {
+    std::string key = t[0] + '\x1f' + t[1] + '\x1f' + t[2];
+    int32_t id = taint_ix.find(key);
+    if (id < 0) {
+      id = taint_ix.get(key);
+      taints.push_back({t[0], t[1], t[2]});
+    }
+    r.taint_ids.push_back((uint32_t)id);
+  }
+  r.image_ids.clear();
+  for (auto& im : r.spec.images)
+    for (auto& name : im.names) r.image_ids.push_back((uint32_t)image_ix.get(name));
+  std::sort(r.image_ids.begin(), r.image_ids.end());
+  r.image_ids.erase(std::unique(r.image_ids.begin(), r.image_ids.end()), r.image_ids.end());
+  // NewResource(node.Status.Allocatable) (framework/types.go:1263-1291)
+  r.alloc_cpu = r.alloc_mem = r.alloc_eph = r.alloc_pods = 0;
+  r.scalar_alloc.clear();
+  for (auto& a : r.spec.alloc) {
+    if (a.name == "cpu") r.alloc_cpu += a.milli;
+    else if (a.name == "memory") r.alloc_mem += milli_ceil(a.milli);
+    else if (a.name == "pods") r.alloc_pods += milli_ceil(a.milli);
+    else if (a.name == "ephemeral-storage") r.alloc_eph += milli_ceil(a.milli);
+    else if (scalar_resource(a.name)) {
+      int32_t s = scalar_slot(a.name);
+      if (s >= 0) r.scalar_alloc[s] += milli_ceil(a.milli);
+    }
+  }
+}
+
+int Cluster::add_node(NodeSpec&& n) {
+  auto it = nodes_.find(n.name);
+  if (it != nodes_.end()) return update_node(std::move(n));
+  auto rec = std::make_unique<NodeRec>();
+  rec->spec = std::move(n);
+  tree_add(rec->spec);
+  add_images(rec->spec);
+  intern_node(*rec);
+  nodes_[rec->spec.name] = std::move(rec);
+  layout_dirty = true;
+  return KSG_OK;
+}
+
+int Cluster::update_node(NodeSpec&& n) {
+  auto it = nodes_.find(n.name);
+  if (it == nodes_.end()) return add_node(std::move(n));
+  NodeRec& r = *it->second;
+  remove_images(r.spec);
+  std::string z0, z1;
+  zone_key(r.spec, &z0);
+  zone_key(n, &z1);
+  if (z0 != z1) {
+    tree_remove(r.spec);
+    tree_add(n);
+  }
+  add_images(n);
+  r.spec = std::move(n);
+  intern_node(r);
+  layout_dirty = true;
+  return KSG_OK;
+}
+
+int Cluster::remove_node(const std::string& name) {
+  auto it = nodes_.find(name);
+  if (it == nodes_.end()) { err = "unknown node " + name; return KSG_ENOTFOUND; }
+  remove_images(it->second->spec);
+  tree_remove(it->second->spec);
+  for (auto& uid : it->second->pods) pods.erase(uid);
+  nodes_.erase(it);
+  layout_dirty = true;
+  return KSG_OK;
+}
+
+void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo.update
+  r.req_cpu += sign * bp.res.cpu;
+  r.req_mem += sign * bp.res.mem;
+  r.req_eph += sign * bp.res.eph;
+  r.nz_cpu += sign * bp.res.nz_cpu;
+  r.nz_mem += sign * bp.res.nz_mem;
+  r.num_pods += sign;
+  for (auto& s : bp.res.scalar) {
+    int32_t slot = scalar_slot(s.first);
+    if (slot >= 0) r.scalar_req[slot] += sign * s.second;
+  }
+  for (uint32_t p : bp.port_ids) {  // HostPortInfo.Add/Remove: set semantics (types.go:555-587)
+    if (sign > 0) r.ports.insert(p);
+    else r.ports.erase(p);
+  }
+}
+
+int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done) {
+  const std::string uid = uid_override.empty() ? p.uid : uid_override;
+  if (p.node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
+  if (pods.count(uid)) { err = "pod " + uid + " exists"; return KSG_EEXIST; }
+  NodeRec* r = node(p.node_name);
+  if (!r) { err = "unknown node " + p.node_name; return KSG_ENOTFOUND; }
+  BoundPod bp;
+  bp.uid = uid;
+  bp.node = p.node_name;
+  bp.res = calc_resources(p);
+  bp.with_affinity = p.has_pod_affinity || p.has_pod_anti;
+  pods_with_affinity += bp.with_affinity ? 1 : 0;
+  auto take = [&](const Container& c) {
+    for (auto& hp : c.ports)
+      if (hp.port > 0) bp.port_ids.push_back(port_id(hp.ip, hp.proto, hp.port));
+  };
+  for (auto& c : p.init_containers)
+    if (c.sidecar) take(c);
+  for (auto& c : p.containers) take(c);
+  apply_pod(*r, bp, +1);
+  r->pods.push_back(uid);
+  pods.emplace(uid, std::move(bp));
+  order();
+  if (!layout_dirty && !device_done) return upload_node_dynamic(index_of(r->spec.name));
+  return KSG_OK;
+}
+
+int Cluster::remove_pod(const std::string& uid) {
+  auto it = pods.find(uid);
+  if (it == pods.end()) { err = "unknown pod " + uid; return KSG_ENOTFOUND; }
+  NodeRec* r = node(it->second.node);
+  pods_with_affinity -= it->second.with_affinity ? 1 : 0;
+  if (r) {
+    apply_pod(*r, it->second, -1);
+    auto& v = r->pods;
+    auto jt = std::find(v.begin(), v.end(), uid);
+    if (jt != v.end()) {  // removeFromSlice: swap with last (framework/types.go:397-420)
+      *jt = v.back();
+      v.pop_back();
+    }
+  }
+  pods.erase(it);
+  order();
+  if (r && !layout_dirty) return upload_node_dynamic(index_of(r->spec.name));
+  return KSG_OK;
+}
+
+// ---- HBM mirror -----------------------------------------------------------------------------------
+#define HIPCHK(x)                                            \
+  do {                                                       \
+    hipError_t e_ = (x);                                     \
+    if (e_ != hipSuccess) {                                  \
+      err = std::string(#x) + ": " + hipGetErrorString(e_); \
+      return KSG_EDEVICE;                                    \
+    }                                                        \
+  } while (0)
+
+int Cluster::ensure_mirror() {
+  order();
+  if (!layout_dirty) return KSG_OK;
+  HIPCHK(hipStreamSynchronize(stream));
+  free_all();
+  const int32_t n = (int32_t)order_.size();
+  const int32_t cap = ((n + kBlock - 1) / kBlock) * kBlock + kBlock;
+  // keep the label slot assignment; grow slot capacity geometrically
+  int32_t used = 0;
+  for (auto& k : keys) used += k.slot >= 0;
+  slots_used_ = used;
+  slots_cap_ = std::max(8, slots_used_ * 2);
+  std::memset(&view, 0, sizeof(view));
+  view.n = n;
+  view.cap = cap;
+  auto a64 = [&]() { return (int64_t*)dalloc((size_t)cap * 8); };
+  view.alloc_cpu = a64();
+  view.alloc_mem = a64();
+  view.alloc_eph = a64();
+  view.alloc_pods = (int32_t*)dalloc((size_t)cap * 4);
+  view.flags = (uint32_t*)dalloc((size_t)cap * 4);
+  view.scalar_alloc = (int64_t*)dalloc((size_t)cap * 8 * kMaxScalar);
+  view.req_cpu = a64();
+  view.req_mem = a64();
+  view.req_eph = a64();
+  view.nz_cpu = a64();
+  view.nz_mem = a64();
+  view.num_pods = (int32_t*)dalloc((size_t)cap * 4);
+  view.scalar_req = (int64_t*)dalloc((size_t)cap * 8 * kMaxScalar);
+  view.taint_off = (uint32_t*)dalloc((size_t)(cap + 1) * 4);
+  view.img_off = (uint32_t*)dalloc((size_t)(cap + 1) * 4);
+  view.labels = (int32_t*)dalloc((size_t)cap * 4 * slots_cap_);
+  view.label_num = (int64_t*)dalloc((size_t)cap * 8 * slots_cap_);
+  view.label_num_ok = (uint8_t*)dalloc((size_t)cap * slots_cap_);
+  view.ports = (uint32_t*)dalloc((size_t)cap * 4 * kPortSlots);
+
+  std::vector<int64_t> acpu(cap, 0), amem(cap, 0), aeph(cap, 0), rcpu(cap, 0), rmem(cap, 0), reph(cap, 0),
+      zcpu(cap, 0), zmem(cap, 0);
+  std::vector<int32_t> apods(cap, 0), npods(cap, 0);
+  std::vector<uint32_t> flags(cap, 0), toff(cap + 1, 0), ioff(cap + 1, 0), tids, iids;
+  std::vector<int64_t> salloc((size_t)cap * kMaxScalar, 0), sreq((size_t)cap * kMaxScalar, 0);
+  std::vector<uint32_t> ports((size_t)cap * kPortSlots, 0xffffffffu);
+  for (int32_t i = 0; i < n; ++i) {
+    const NodeRec& r = *nodes_[order_[i]];
+    acpu[i] = r.alloc_cpu;
+    amem[i] = r.alloc_mem;
+    aeph[i] = r.alloc_eph;
+    apods[i] = (int32_t)r.alloc_pods;
+    flags[i] = r.spec.unschedulable ? 1u : 0u;
+    rcpu[i] = r.req_cpu;
+    rmem[i] = r.req_mem;
+    reph[i] = r.req_eph;
+    zcpu[i] = r.nz_cpu;
+    zmem[i] = r.nz_mem;
+    npods[i] = r.num_pods;
+    for (auto& kv : r.scalar_alloc) salloc[(size_t)kv.first * cap + i] = kv.second;
+    for (auto& kv : r.scalar_req) sreq[(size_t)kv.first * cap + i] = kv.second;
+    toff[i] = (uint32_t)tids.size();
+    tids.insert(tids.end(), r.taint_ids.begin(), r.taint_ids.end());
+    ioff[i] = (uint32_t)iids.size();
+    iids.insert(iids.end(), r.image_ids.begin(), r.image_ids.end());
+    if (r.ports.size() > (size_t)kPortSlots) { err = "node " + r.spec.name + " uses more host ports than supported"; return KSG_ENOTSUP; }
+    int q = 0;
+    for (uint32_t p : r.ports) ports[(size_t)i * kPortSlots + q++] = p;
+  }
+  for (int32_t i = n; i <= cap; ++i) {
+    toff[i] = (uint32_t)tids.size();
+    ioff[i] = (uint32_t)iids.size();
+  }
+  taint_ids_per_node = n ? (double)tids.size() / n : 0.0;
+  img_ids_per_node = n ? (double)iids.size() / n : 0.0;
+  view.taint_ids = (uint32_t*)dalloc(std::max<size_t>(tids.size(), 1) * 4);
+  view.img_ids = (uint32_t*)dalloc(std::max<size_t>(iids.size(), 1) * 4);
+  auto up = [&](const void* dst, const void* src, size_t bytes) {
+    return hipMemcpyAsync(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice, stream);
+  };
+  HIPCHK(up(view.alloc_cpu, acpu.data(), (size_t)cap * 8));
+  HIPCHK(up(view.alloc_mem, amem.data(), (size_t)cap * 8));
+  HIPCHK(up(view.alloc_eph, aeph.data(), (size_t)cap * 8));
+  HIPCHK(up(view.alloc_pods, apods.data(), (size_t)cap * 4));
+  HIPCHK(up(view.flags, flags.data(), (size_t)cap * 4));
+  HIPCHK(up(view.scalar_alloc, salloc.data(), salloc.size() * 8));
+  HIPCHK(up(view.req_cpu, rcpu.data(), (size_t)cap * 8));
+  HIPCHK(up(view.req_mem, rmem.data(), (size_t)cap * 8));
+  HIPCHK(up(view.req_eph, reph.data(), (size_t)cap * 8));
+  HIPCHK(up(view.nz_cpu, zcpu.data(), (size_t)cap * 8));
+  HIPCHK(up(view.nz_mem, zmem.data(), (size_t)cap * 8));
+  HIPCHK(up(view.num_pods, npods.data(), (size_t)cap * 4));
+  HIPCHK(up(view.scalar_req, sreq.data(), sreq.size() * 8));
+  HIPCHK(up(view.taint_off, toff.data(), toff.size() * 4));
+  HIPCHK(up(view.img_off, ioff.data(), ioff.size() * 4));
+  if (!tids.empty()) HIPCHK(up(view.taint_ids, tids.data(), tids.size() * 4));
+  if (!iids.empty()) HIPCHK(up(view.img_ids, iids.data(), iids.size() * 4));
+  HIPCHK(up(view.ports, ports.data(), ports.size() * 4));
+  HIPCHK(hipStreamSynchronize(stream));
+  layout_dirty = false;
+  for (int32_t k = 0; k < (int32_t)keys.size(); ++k)
+    if (keys[k].slot >= 0) {
+      int rc = upload_label_column(k);
+      if (rc) return rc;
+    }
+  return KSG_OK;
+}
+
+int Cluster::upload_label_column(int32_t key) {
+  const int32_t slot = keys[key].slot;
+  const int32_t cap = view.cap;
+  std::vector<int32_t> col(cap, -1);
+  std::vector<int64_t> num(cap, 0);
+  std::vector<uint8_t> ok(cap, 0);
+  // numeric value per local value id (labels.Requirement Gt/Lt parse, selector.go:265-289)
+  auto& vals = keys[key].values.strs;
+  std::vector<int64_t> vnum(vals.size(), 0);
+  std::vector<uint8_t> vok(vals.size(), 0);
+  for (size_t v = 0; v < vals.size(); ++v) vok[v] = parse_go_int(vals[v], &vnum[v]) ? 1 : 0;
+  for (int32_t i = 0; i < view.n; ++i) {
+    const NodeRec& r = *nodes_[order_[i]];
+    for (auto& kv : r.labels)
+      if (kv.first == key) {
+        col[i] = kv.second;
+        num[i] = vnum[kv.second];
+        ok[i] = vok[kv.second];
+      }
+  }
+  const size_t off = (size_t)slot * cap;
+  HIPCHK(hipMemcpyAsync(const_cast<int32_t*>(view.labels) + off, col.data(), (size_t)cap * 4, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(const_cast<int64_t*>(view.label_num) + off, num.data(), (size_t)cap * 8, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(const_cast<uint8_t*>(view.label_num_ok) + off, ok.data(), (size_t)cap, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  return KSG_OK;
+}
+
+int Cluster::ensure_label_slot(int32_t key) {
+  if (keys[key].slot >= 0) return KSG_OK;
+  keys[key].slot = slots_used_++;
+  if (layout_dirty || slots_used_ > slots_cap_) {
+    layout_dirty = true;  // regrow on the next ensure_mirror
+    return ensure_mirror();
+  }
+  return upload_label_column(key);
+}
+
+int Cluster::upload_node_dynamic(int32_t i) {
+  if (i < 0 || layout_dirty) return KSG_OK;
+  const NodeRec& r = *nodes_[order_[i]];
+  const int32_t cap = view.cap;
+  HIPCHK(hipMemcpyAsync(view.req_cpu + i, &r.req_cpu, 8, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(view.req_mem + i, &r.req_mem, 8, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(view.req_eph + i, &r.req_eph, 8, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(view.nz_cpu + i, &r.nz_cpu, 8, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(view.nz_mem + i, &r.nz_mem, 8, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(view.num_pods + i, &r.num_pods, 4, hipMemcpyHostToDevice, stream));
+  for (int s = 0; s < kMaxScalar; ++s) {
+    auto it = r.scalar_req.find(s);
+    int64_t v = it == r.scalar_req.end() ? 0 : it->second;
+    HIPCHK(hipMemcpyAsync(view.scalar_req + (size_t)s * cap + i, &v, 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  if (r.ports.size() > (size_t)kPortSlots) { err = "too many host ports on node"; return KSG_ENOTSUP; }
+  uint32_t slots[kPortSlots];
+  for (int q = 0; q < kPortSlots; ++q) slots[q] = 0xffffffffu;
+  int q = 0;
+  for (uint32_t p : r.ports) slots[q++] = p;
+  HIPCHK(hipMemcpyAsync(view.ports + (size_t)i * kPortSlots, slots, sizeof(slots), hipMemcpyHostToDevice, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  return KSG_OK;
+}
+
+}  // namespace ksg

@@ -1,0 +1,821 @@
+// engine.cpp -- per-pod compilation into PodDesc programs and batched kernel execution.
+//
+// compile() does, once per pod and on the host, exactly the O(pod) work the reference's
+// PreFilter/PreScore plugins do (cycle-state construction), but against interned cluster
+// tables so the per-node work left for the GPU is table lookups:
+//   NodeResourcesFit  PreFilter/PreScore  fit.go:136-153,317-335; resource_allocation.go:236-267
+//   BalancedAllocation PreScore            balanced_allocation.go:78-100
+//   TaintToleration   tolerations -> bitmaps over distinct taints (taint_toleration.go:102-175)
+//   NodeAffinity      PreFilter/PreScore  node_affinity.go:148-256 -> selector programs
+//   NodePorts         PreFilter            node_ports.go:73-82 -> conflict bitmap over port ids
+//   ImageLocality     per-image scaled scores (image_locality.go:141-148)
+// run_batch() then launches k_filter_score + k_select per pod on one stream with no host
+// round trip inside the batch (device-side AssumePod), and reads the results back once.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "host.hpp"
+
+namespace ksg {
+
+hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+
+#define HIPCHK(x)                                               \
+  do {                                                          \
+    hipError_t e_ = (x);                                        \
+    if (e_ != hipSuccess) {                                     \
+      c->err = std::string(#x) + ": " + hipGetErrorString(e_); \
+      return KSG_EDEVICE;                                       \
+    }                                                           \
+  } while (0)
+
+enum : int { P_UNSCHED = 0, P_NODENAME = 1, P_TAINT = 2, P_NA = 3, P_PORTS = 4, P_FIT = 5, P_PTS = 6,
+             P_IPA = 7, P_BAL = 8, P_IMG = 9 };
+
+// ---- blob builder ------------------------------------------------------------------------------
+// The header is kept outside the byte vector (put() may reallocate it) and copied in by finish().
+struct Blob {
+  PodDesc hdr;
+  std::vector<uint8_t> b;
+  Blob() {
+    std::memset(&hdr, 0, sizeof(hdr));
+    b.resize((sizeof(PodDesc) + 15) & ~size_t(15), 0);
+  }
+  PodDesc& d() { return hdr; }
+  template <typename T>
+  int32_t put(const T* p, size_t n) {
+    size_t off = (b.size() + 7) & ~size_t(7);
+    b.resize(off + sizeof(T) * n, 0);
+    if (n) std::memcpy(b.data() + off, p, sizeof(T) * n);
+    return (int32_t)off;
+  }
+  template <typename T>
+  int32_t put(const std::vector<T>& v) { return put(v.data(), v.size()); }
+  void finish() {
+    b.resize((b.size() + 15) & ~size_t(15), 0);
+    hdr.blob_bytes = (uint32_t)b.size();
+    std::memcpy(b.data(), &hdr, sizeof(hdr));
+  }
+};
+
+// selector-program builder (labels.Requirement semantics, apimachinery/pkg/labels/selector.go)
+struct SelBuilder {
+  Cluster* c;
+  std::vector<SelReq> reqs;
+  std::vector<SelTerm> terms;
+  std::vector<int32_t> vals;
+  int rc = KSG_OK;
+
+  int32_t slot_of(const std::string& key) {
+    int32_t k = c->key_id(key);
+    int r = c->ensure_label_slot(k);
+    if (r) rc = r;
+    return c->keys[k].slot;
+  }
+  void add_in(SelReq& r, const std::string& key, const std::vector<std::string>& values) {
+    int32_t k = c->key_id(key);
+    r.vals_off = (int32_t)vals.size();
+    for (auto& v : values) {
+      int32_t id = c->keys[k].values.find(v);
+      if (id >= 0) vals.push_back(id);
+    }
+    r.nvals = (int32_t)vals.size() - r.vals_off;
+  }
+  // one labels.Requirement; returns false on a NewRequirement validation error
+  bool label_req(const Expr& e, std::vector<SelReq>* out) {
+    SelReq r{};
+    r.slot = slot_of(e.key);
+    bool ok = valid_label_key(e.key);
+    if (e.op == "In" || e.op == "NotIn") {
+      r.op = e.op == "In" ? SEL_IN : SEL_NOTIN;
+      ok = ok && !e.values.empty();
+      add_in(r, e.key, e.values);
+    } else if (e.op == "Exists" || e.op == "DoesNotExist") {
+      r.op = e.op == "Exists" ? SEL_EXISTS : SEL_DNE;
+      ok = ok && e.values.empty();
+    } else if (e.op == "Gt" || e.op == "Lt") {
+      r.op = e.op == "Gt" ? SEL_GT : SEL_LT;
+      ok = ok && e.values.size() == 1 && parse_go_int(e.values[0], &r.num);
+    } else {
+      return false;
+    }
+    for (auto& v : e.values) ok = ok && valid_label_value(v);
+    out->push_back(r);
+    return ok;
+  }
+  // nodeaffinity.newNodeSelectorTerm + nodeSelectorTerm.match (nodeaffinity.go:170-201)
+  SelTerm node_term(const NSTerm& t, int32_t weight) {
+    SelTerm st{};
+    st.weight = weight;
+    std::vector<SelReq> rs;
+    bool ok = true;
+    for (auto& e : t.exprs) ok = label_req(e, &rs) && ok;
+    for (auto& f : t.fields) {
+      if ((f.op != "In" && f.op != "NotIn") || f.values.size() != 1) { ok = false; continue; }
+      SelReq r{};
+      const bool in = f.op == "In";
+      if (f.key == "metadata.name") {
+        r.op = in ? SEL_NODE_EQ : SEL_NODE_NE;
+        r.num = c->index_of(f.values[0]);  // -1: no such node, never equal
+      } else {  // fields.Set{"metadata.name"}.Get(other) == ""
+        const bool eq = f.values[0].empty();
+        r.op = (in ? eq : !eq) ? SEL_TRUE : SEL_FALSE;
+      }
+      rs.push_back(r);
+    }
+    st.req_off = (int32_t)reqs.size();
+    st.nreq = (int32_t)rs.size();
+    st.parse_err = ok ? 0 : 1;
+    reqs.insert(reqs.end(), rs.begin(), rs.end());
+    return st;
+  }
+};
+
+static bool empty_term(const NSTerm& t) { return t.exprs.empty() && t.fields.empty(); }
+
+// ---- compile ---------------------------------------------------------------------------------------
+int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out) {
+  const Config& cfg = c->cfg;
+  const int32_t N = (int32_t)c->order().size();
+  Blob B;
+  PodDesc& D = B.d();
+  D.node_name = -1;
+  D.rot_start = 0;
+  D.prefilter_plugin = 15;
+  for (int i = 0; i < kNumPlugins; ++i) D.weight[i] = cfg.weight[i];
+  *out = CompiledPod{};
+  out->num_all = N;
+
+  // features not yet on the device path: refuse loudly rather than fall back to the CPU
+  const bool pts_on = mode == CYCLE ? cfg.enabled[P_PTS] : plugin == P_PTS;
+  const bool ipa_on = mode == CYCLE ? cfg.enabled[P_IPA] : plugin == P_IPA;
+  const bool has_ipa = p.has_pod_affinity || p.has_pod_anti || c->pods_with_affinity > 0;
+  if ((pts_on && (!p.spreads.empty() || mode != CYCLE)) || (ipa_on && (has_ipa || mode != CYCLE))) {
+    c->err = "PodTopologySpread / InterPodAffinity are not on the device path yet";
+    return KSG_ENOTSUP;
+  }
+
+  // ---- which plugins run (PreFilter/PreScore Skip, framework.go:960-962,1324-1327)
+  // fmask/smask start as "would run" and lose the plugins whose PreFilter/PreScore Skips;
+  // the profile's enabled set is applied per mode at the end.
+  uint32_t fmask = (1u << (P_FIT + 1)) - 1u, smask = 0;
+  for (int q : {P_TAINT, P_NA, P_FIT, P_BAL, P_IMG}) smask |= 1u << q;
+
+  SelBuilder sb{c};
+  // NodeAffinity PreFilter (node_affinity.go:148-198)
+  const bool noNA = !p.has_required_na;
+  if (noNA && !cfg.has_added_required && !p.has_node_selector) fmask &= ~(1u << P_NA);
+  std::vector<int32_t> subset;
+  bool restricted = false, conflict = false;
+  if (!noNA && !p.required_na.empty()) {
+    std::set<std::string> names;
+    bool namesNil = true, allNodes = false;
+    for (auto& t : p.required_na) {
+      bool termNil = true;
+      std::set<std::string> tn;
+      for (auto& r : t.fields)
+        if (r.key == "metadata.name" && r.op == "In") {
+          std::set<std::string> s(r.values.begin(), r.values.end());
+          if (termNil) { tn = s; termNil = false; }
+          else {
+            std::set<std::string> x;
+            for (auto& n : tn)
+              if (s.count(n)) x.insert(n);
+            tn = x;
+          }
+        }
+      if (termNil) { allNodes = true; break; }
+      namesNil = false;
+      names.insert(tn.begin(), tn.end());
+    }
+    if (!allNodes) {
+      if (!namesNil && names.empty()) conflict = true;
+      else if (!names.empty()) {
+        restricted = true;
+        for (auto& n : names) {
+          int32_t ix = c->index_of(n);
+          if (ix >= 0) subset.push_back(ix);
+        }
+        std::sort(subset.begin(), subset.end());
+      }
+    }
+  }
+  if (cfg.has_added_required) {
+    std::vector<SelTerm> ts;
+    for (auto& t : cfg.added_required)
+      if (!empty_term(t)) ts.push_back(sb.node_term(t, 0));
+    D.flags |= DF_HAS_ADDED_NA;
+    D.na_added.nterm = (int32_t)ts.size();
+    D.na_added.term_off = (int32_t)sb.terms.size();
+    sb.terms.insert(sb.terms.end(), ts.begin(), ts.end());
+  }
+  if (!p.node_selector.empty()) {  // labels.SelectorFromSet (no validation)
+    SelTerm st{};
+    st.req_off = (int32_t)sb.reqs.size();
+    for (auto& kv : p.node_selector) {
+      SelReq r{};
+      r.slot = sb.slot_of(kv.first);
+      r.op = SEL_IN;
+      sb.add_in(r, kv.first, {kv.second});
+      sb.reqs.push_back(r);
+    }
+    st.nreq = (int32_t)p.node_selector.size();
+    D.flags |= DF_HAS_SELECTOR;
+    D.na_selector.term_off = (int32_t)sb.terms.size();
+    D.na_selector.nterm = 1;
+    sb.terms.push_back(st);
+  }
+  if (p.has_required_na) {
+    std::vector<SelTerm> ts;
+    for (auto& t : p.required_na)
+      if (!empty_term(t)) ts.push_back(sb.node_term(t, 0));
+    D.flags |= DF_HAS_REQUIRED_NA;
+    D.na_required.term_off = (int32_t)sb.terms.size();
+    D.na_required.nterm = (int32_t)ts.size();
+    sb.terms.insert(sb.terms.end(), ts.begin(), ts.end());
+  }
+  // NodeAffinity PreScore (node_affinity.go:242-256): preferred terms, Skip when none
+  bool pref_err = false;
+  auto pref_prog = [&](const std::vector<std::pair<int32_t, NSTerm>>& in, SelProg* prog, bool pod_terms) {
+    std::vector<SelTerm> ts;
+    for (auto& t : in) {
+      if (t.first == 0 || empty_term(t.second)) continue;
+      SelTerm st = sb.node_term(t.second, t.first);
+      if (st.parse_err) pref_err |= pod_terms;  // config terms are validated at create
+      else ts.push_back(st);
+    }
+    prog->term_off = (int32_t)sb.terms.size();
+    prog->nterm = (int32_t)ts.size();
+    sb.terms.insert(sb.terms.end(), ts.begin(), ts.end());
+  };
+  if (cfg.has_added_pref) {
+    D.flags |= DF_HAS_ADDED_PREF;
+    pref_prog(cfg.added_pref, &D.na_added_pref, false);
+  }
+  if (p.has_preferred_na) {
+    D.flags |= DF_HAS_PREF_NA;
+    pref_prog(p.preferred_na, &D.na_preferred, true);
+  }
+  if (!p.has_preferred_na && !cfg.has_added_pref) smask &= ~(1u << P_NA);
+  if (sb.rc) return sb.rc;
+
+  // NodeName (node_name.go:67-83)
+  if (!p.node_name.empty()) {
+    int32_t ix = c->index_of(p.node_name);
+    D.node_name = ix >= 0 ? ix : -2;
+  }
+
+  // TaintToleration: per distinct taint, "not tolerated" bits (taint_toleration.go:102-196)
+  {
+    const size_t T = c->taints.size();
+    const int32_t words = (int32_t)((T + 31) / 32);
+    std::vector<uint32_t> untol(words, 0), intol(words, 0);
+    std::vector<const Tol*> pref;
+    for (auto& t : p.tolerations)
+      if (t.effect.empty() || t.effect == "PreferNoSchedule") pref.push_back(&t);
+    for (size_t id = 0; id < T; ++id) {
+      const TaintRec& tr = c->taints[id];
+      if (tr.effect == "NoSchedule" || tr.effect == "NoExecute") {
+        bool ok = false;
+        for (auto& t : p.tolerations) ok = ok || tolerates(t, tr.key, tr.value, tr.effect, cfg.taint_cmp_ops);
+        if (!ok) untol[id / 32] |= 1u << (id % 32);
+      } else if (tr.effect == "PreferNoSchedule") {
+        bool ok = false;
+        for (auto* t : pref) ok = ok || tolerates(*t, tr.key, tr.value, tr.effect, cfg.taint_cmp_ops);
+        if (!ok) intol[id / 32] |= 1u << (id % 32);
+      }
+    }
+    D.n_taint_words = words;
+    D.untol_ns_off = B.put(untol);
+    D.intol_pns_off = B.put(intol);
+    for (auto& t : p.tolerations)  // NodeUnschedulable (node_unschedulable.go:133-138)
+      if (tolerates(t, "node.kubernetes.io/unschedulable", "", "NoSchedule", cfg.taint_cmp_ops)) D.flags |= DF_TOLERATES_UNSCHED;
+  }
+
+  // NodePorts PreFilter (node_ports.go:73-82) -> conflict bitmap over distinct port ids
+  std::vector<HostPort> want;
+  for (auto& k : p.init_containers)
+    if (k.sidecar)
+      for (auto& hp : k.ports)
+        if (hp.port > 0) want.push_back(hp);
+  for (auto& k : p.containers)
+    for (auto& hp : k.ports)
+      if (hp.port > 0) want.push_back(hp);
+  if (want.empty()) fmask &= ~(1u << P_PORTS);
+  std::vector<uint32_t> own;
+  for (auto& hp : want) own.push_back(c->port_id(hp.ip, hp.proto, hp.port));
+  {
+    const size_t P = c->ports.size();
+    const int32_t words = (int32_t)((P + 31) / 32);
+    std::vector<uint32_t> conf(words, 0);
+    for (size_t id = 0; id < P; ++id) {
+      const PortRec& pr = c->ports[id];
+      bool hit = false;
+      for (auto& w : want) {  // HostPortInfo.CheckConflict (kube-scheduler/framework/types.go:603-631)
+        std::string ip = w.ip.empty() ? "0.0.0.0" : w.ip, proto = w.proto.empty() ? "TCP" : w.proto;
+        if (proto != pr.proto || w.port != pr.port) continue;
+        if (ip == "0.0.0.0" || pr.ip == "0.0.0.0" || pr.ip == ip) hit = true;
+      }
+      if (hit) conf[id / 32] |= 1u << (id % 32);
+    }
+    D.n_port_words = words;
+    D.port_conflict_off = B.put(conf);
+    std::sort(own.begin(), own.end());
+    own.erase(std::unique(own.begin(), own.end()), own.end());
+    D.n_pod_ports = (int32_t)own.size();
+    D.pod_ports_off = B.put(own);
+  }
+
+  // NodeResourcesFit PreFilter + assume payload (fit.go:317-335; framework/types.go:1035-1076)
+  const PodResources res = calc_resources(p);
+  out->res = res;
+  out->port_ids = own;
+  D.req_cpu = res.cpu;
+  D.req_mem = res.mem;
+  D.req_eph = res.eph;
+  std::vector<ScalarReq> fsr, asr;
+  for (auto& s : res.scalar) {
+    int32_t slot = c->scalar_slot(s.first);
+    if (slot < 0) { c->err = "too many extended resources"; return KSG_ENOTSUP; }
+    asr.push_back({slot, 0, s.second});
+    if (s.second == 0) continue;
+    const bool extended = s.first.find('/') != std::string::npos && s.first.find("kubernetes.io/") == std::string::npos;
+    if (extended) {
+      std::string prefix = s.first.substr(0, s.first.find('/'));
+      if (cfg.ignored_res.count(s.first) || cfg.ignored_groups.count(prefix)) continue;
+    }
+    fsr.push_back({slot, 0, s.second});
+  }
+  D.fit_any = (res.cpu > 0 || res.mem > 0 || res.eph > 0 || !res.scalar.empty()) ? 1 : 0;
+  D.n_scalar = (int32_t)fsr.size();
+  D.scalar_off = B.put(fsr);
+  D.a_cpu = res.cpu;
+  D.a_mem = res.mem;
+  D.a_eph = res.eph;
+  D.a_nz_cpu = res.nz_cpu;
+  D.a_nz_mem = res.nz_mem;
+  D.n_a_scalar = (int32_t)asr.size();
+  D.a_scalar_off = B.put(asr);
+
+  // NodeResourcesFit / BalancedAllocation PreScore (resource_allocation.go:167-267)
+  auto score_res = [&](const std::vector<std::pair<std::string, int64_t>>& specs, bool useRequested,
+                       bool* best_effort) {
+    std::vector<ScoreRes> v;
+    ResVec nm;
+    if (!useRequested) nm = {{"cpu", 100}, {"memory", 200LL * 1024 * 1024 * 1000}};
+    const ResVec reqs = pod_requests(p, useRequested ? nullptr : &nm);
+    *best_effort = true;
+    for (auto& sp : specs) {
+      ScoreRes r{};
+      r.weight = sp.second;
+      int64_t m = 0;
+      for (auto& x : reqs)
+        if (x.name == sp.first) m = x.milli;
+      r.pod_req = sp.first == "cpu" ? m : milli_ceil(m);
+      if (r.pod_req != 0) *best_effort = false;
+      if (sp.first == "cpu") r.kind = RES_CPU;
+      else if (sp.first == "memory") r.kind = RES_MEM;
+      else if (sp.first == "ephemeral-storage") r.kind = RES_EPH;
+      else if (scalar_resource(sp.first)) {
+        if (r.pod_req == 0) r.kind = RES_SKIP;
+        else {
+          int32_t slot = c->scalar_slot(sp.first);
+          r.kind = slot >= 0 ? RES_SCALAR : RES_SKIP;
+          r.slot = slot;
+        }
+      } else {
+        r.kind = RES_SKIP;  // no such allocatable: (0, 0) -> skipped
+      }
+      v.push_back(r);
+    }
+    return v;
+  };
+  bool be_fit, be_bal;
+  std::vector<ScoreRes> fr = score_res(cfg.fit_res, false, &be_fit);
+  std::vector<ScoreRes> br = score_res(cfg.bal_res, true, &be_bal);
+  if (br.size() > 8 || fr.size() > 64) { c->err = "too many scoring resources"; return KSG_ENOTSUP; }
+  D.fit_strategy = cfg.fit_strategy;
+  D.n_fit_res = (int32_t)fr.size();
+  D.fit_res_off = B.put(fr);
+  D.n_bal_res = (int32_t)br.size();
+  D.bal_res_off = B.put(br);
+  std::vector<int64_t> shape;
+  for (auto& pt : cfg.rtcr) { shape.push_back(pt.first); shape.push_back(pt.second); }
+  D.n_rtcr = (int32_t)cfg.rtcr.size();
+  D.rtcr_off = B.put(shape);
+  if (be_bal) smask &= ~(1u << P_BAL);  // balanced_allocation.go:80-85
+
+  // ImageLocality (image_locality.go:70-152)
+  {
+    std::vector<std::string> names;
+    for (auto& k : p.init_containers) names.push_back(k.image);
+    for (auto& k : p.containers) names.push_back(k.image);
+    for (auto& v : p.image_volumes) names.push_back(v);
+    std::vector<ImageTerm> terms;
+    for (auto& nm : names) {
+      std::string n = nm;  // normalizedImageName (:154-159)
+      auto colon = n.rfind(':'), slash = n.rfind('/');
+      long lc = colon == std::string::npos ? -1 : (long)colon, ls = slash == std::string::npos ? -1 : (long)slash;
+      if (lc <= ls) n += ":latest";
+      auto st = c->image_states.find(n);
+      if (st == c->image_states.end()) continue;
+      int32_t id = c->image_ix.find(n);
+      auto it = std::find_if(terms.begin(), terms.end(), [&](const ImageTerm& t) { return t.image == id; });
+      if (it != terms.end()) { it->mult++; continue; }
+      const double spread = (double)(int64_t)st->second.nodes.size() / (double)N;
+      terms.push_back({id, 1, (int64_t)((double)st->second.size * spread)});
+    }
+    D.n_img = (int32_t)terms.size();
+    D.img_off = B.put(terms);
+    D.img_count = (int64_t)names.size();
+  }
+
+  // selector program pools
+  D.req_off = B.put(sb.reqs);
+  D.vals_off = B.put(sb.vals);
+  const int32_t term_base = B.put(sb.terms);
+  for (SelProg* pr : {&D.na_required, &D.na_selector, &D.na_added, &D.na_preferred, &D.na_added_pref})
+    pr->term_off = term_base + pr->term_off * (int32_t)sizeof(SelTerm);
+  // selector terms hold req offsets in units of SelReq; vals_off in units of int32 (kernel indexes arrays)
+
+  // ---- mode-specific masks
+  // PreScore/Score errors: NodeAffinity preferred-term parse error (node_affinity.go:243-246),
+  // NodeResourcesFit with no scoring resources (resource_allocation.go:149-151)
+  const bool score_err = (pref_err && cfg.enabled[P_NA]) || (cfg.enabled[P_FIT] && cfg.fit_res.empty());
+  if (mode == CYCLE) {
+    for (int q = 0; q < kNumPlugins; ++q)
+      if (!cfg.enabled[q]) { fmask &= ~(1u << q); smask &= ~(1u << q); }
+    bool any_score = false;
+    for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) any_score |= cfg.enabled[q];
+    if (!any_score) {
+      c->err = "a profile without score plugins (numNodesToFind = 1) is not supported";
+      return KSG_ENOTSUP;
+    }
+    if (N >= 100 && cfg.pct != 100) {
+      c->err = "percentageOfNodesToScore != 100 (sampling) is not supported on the device path";
+      return KSG_ENOTSUP;
+    }
+    if (score_err) D.flags |= DF_SCORE_ERROR;
+    if (conflict) {  // PreFilter UnschedulableAndUnresolvable: every node gets it
+      D.flags |= DF_PREFILTER_REJECT;
+      D.prefilter_code = 3;
+      D.prefilter_plugin = P_NA;
+      out->prefilter_reject = true;
+      out->prefilter_code = 3;
+      out->prefilter_plugin = P_NA;
+    } else if (restricted) {
+      D.flags |= DF_SUBSET;
+      D.subset_cnt = (int32_t)subset.size();
+      D.subset_off = B.put(subset);
+      out->num_all = (int32_t)subset.size();
+      if (!subset.empty()) D.rot_start = subset[(size_t)(c->next_start % (int64_t)subset.size())];
+    } else {
+      D.rot_start = N ? (int32_t)(c->next_start % N) : 0;
+    }
+  } else if (mode == FILTER_ONE) {
+    fmask &= 1u << plugin;
+    if (plugin == P_NA && conflict) {
+      out->prefilter_reject = true;
+      out->prefilter_code = 3;
+      out->prefilter_plugin = P_NA;
+    }
+    smask = 0;
+    eval = true;
+  } else {  // SCORE_ONE
+    if ((plugin == P_NA && pref_err) || (plugin == P_FIT && cfg.fit_res.empty())) out->error = true;
+    fmask = 0;
+    smask &= 1u << plugin;
+    for (int i = 0; i < kNumPlugins; ++i) D.weight[i] = 1;
+    D.flags |= DF_ALL_FEASIBLE;
+    eval = true;
+  }
+  D.filter_mask = fmask;
+  D.score_mask = smask;
+  out->score_mask = smask;
+  if (assume) D.flags |= DF_ASSUME;
+  if (eval) D.flags |= DF_EVAL_OUT;
+  B.finish();
+  out->blob = std::move(B.b);
+  return KSG_OK;
+}
+
+// ---- batch execution ---------------------------------------------------------------------------------
+Engine::Engine(Cluster* cl) : c(cl) {
+  (void)hipEventCreate(&ev0);
+  (void)hipEventCreate(&ev1);
+}
+// Algorithmic HBM bytes of one k_filter_score launch: every SoA field the pod's active plugins
+// must read for a node, plus what the launch writes, each counted once per node.
+double Engine::algo_bytes(const PodDesc& d) const {
+  const double N = (double)c->view.n;
+  const uint32_t fm = d.filter_mask, sm = d.score_mask;
+  double b = 4.0 + 1.0 / 8.0;                              // status word + feasibility bit
+  if (fm & (1u << P_UNSCHED)) b += 4;                      // flags
+  b += 4 + 4 * c->taint_ids_per_node;                      // taint CSR offset + ids (TaintToleration)
+  if (fm & (1u << P_NA)) {
+    b += 4.0 * (d.na_required.nterm + d.na_selector.nterm + d.na_added.nterm);  // one label column per term (lower bound)
+  }
+  if (fm & (1u << P_PORTS)) b += 4.0 * kPortSlots;
+  if (fm & (1u << P_FIT)) {
+    b += 4 + 4;                                            // alloc pods, pod count
+    if (d.fit_any) {
+      b += d.req_cpu > 0 ? 16 : 0;                         // alloc + requested milliCPU
+      b += d.req_mem > 0 ? 16 : 0;
+      b += d.req_eph > 0 ? 16 : 0;
+      b += 16.0 * d.n_scalar;
+    }
+  }
+  if (sm & ((1u << P_FIT) | (1u << P_BAL))) b += 16;       // NonZeroRequested cpu/mem (alloc/requested reused)
+  if (sm & (1u << P_NA)) b += 4.0 * (d.na_preferred.nterm + d.na_added_pref.nterm);
+  if ((sm & (1u << P_IMG)) && d.n_img) b += 4 + 4 * c->img_ids_per_node;
+  if (sm & ((1u << P_FIT) | (1u << P_BAL) | (1u << P_IMG))) b += 8;  // weighted fixed-score sum
+  if (sm & (1u << P_TAINT)) b += 8;                        // raw TaintToleration score
+  if (sm & (1u << P_NA)) b += 8;                           // raw NodeAffinity score
+  return b * N;
+}
+
+Engine::~Engine() {
+  for (hipEvent_t e : tev) (void)hipEventDestroy(e);
+  for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
+                    &d_total})
+    if (b->p) (void)hipFree(b->p);
+  if (h_pinned) (void)hipHostFree(h_pinned);
+  if (ev0) (void)hipEventDestroy(ev0);
+  if (ev1) (void)hipEventDestroy(ev1);
+}
+
+int Engine::ensure(DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return KSG_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  size_t want = std::max<size_t>(bytes + bytes / 2, 256);
+  HIPCHK(hipMalloc(&b.p, want));
+  b.bytes = want;
+  return KSG_OK;
+}
+
+int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval) {
+  const size_t cap = (size_t)c->view.cap;
+  const size_t nb = cap / kBlock + 1;
+  int rc;
+  if ((rc = ensure(d_descs, desc_bytes))) return rc;
+  if ((rc = ensure(d_off, (size_t)pods * 4))) return rc;
+  if ((rc = ensure(d_stats, (size_t)pods * sizeof(PodStats)))) return rc;
+  if ((rc = ensure(d_results, (size_t)pods * sizeof(DevResult)))) return rc;
+  if ((rc = ensure(d_status, cap * 4))) return rc;
+  if ((rc = ensure(d_fmask, nb * (kBlock / 64) * 8))) return rc;
+  if ((rc = ensure(d_blk, nb * 4))) return rc;
+  if ((rc = ensure(d_fixed, cap * 8))) return rc;
+  if ((rc = ensure(d_raw, cap * 8 * kNumPlugins))) return rc;
+  if (eval) {
+    if ((rc = ensure(d_out, cap * 8 * kNumPlugins))) return rc;
+    if ((rc = ensure(d_total, cap * 8))) return rc;
+  }
+  const size_t need = desc_bytes + (size_t)pods * (4 + sizeof(PodStats) + sizeof(DevResult)) + 256;
+  if (h_pinned_bytes < need) {
+    if (h_pinned) (void)hipHostFree(h_pinned);
+    h_pinned = nullptr;
+    h_pinned_bytes = 0;
+    size_t want = need * 2;
+    HIPCHK(hipHostMalloc(&h_pinned, want, hipHostMallocDefault));
+    h_pinned_bytes = want;
+  }
+  return KSG_OK;
+}
+
+BatchView Engine::bview(int pods) {
+  (void)pods;
+  BatchView b{};
+  b.descs = (const uint8_t*)d_descs.p;
+  b.desc_off = (const uint32_t*)d_off.p;
+  b.stats = (PodStats*)d_stats.p;
+  b.results = (DevResult*)d_results.p;
+  b.status = (uint32_t*)d_status.p;
+  b.fmask = (uint64_t*)d_fmask.p;
+  b.blk_cnt = (uint32_t*)d_blk.p;
+  b.fixed = (int64_t*)d_fixed.p;
+  b.raw = (int64_t*)d_raw.p;
+  b.out_scores = (int64_t*)d_out.p;
+  b.out_total = (int64_t*)d_total.p;
+  return b;
+}
+
+int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
+                      ksg_result* results, ksg_eval_out* eval) {
+  const int n = (int)pods.size();
+  if (n == 0) return KSG_OK;
+  if (eval && n != 1) return KSG_EINVAL;
+  c->order();
+  if (c->order().empty()) {  // ErrNoNodesAvailable (schedule_one.go:569-571)
+    for (int i = 0; i < n; ++i) results[i] = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
+    return KSG_OK;
+  }
+  // ---- compile every pod (may materialise label columns / relayout the mirror)
+  std::vector<CompiledPod> cp(n);
+  int64_t start = c->next_start;
+  for (int i = 0; i < n; ++i) {
+    int rc = compile(*pods[i], CYCLE, -1, assume, eval != nullptr, &cp[i]);
+    if (rc) { c->next_start = start; return rc; }
+    if (!cp[i].prefilter_reject) {
+      // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
+      const int64_t N = (int64_t)c->order().size();
+      c->next_start = (c->next_start + cp[i].num_all) % N;
+    }
+  }
+  int rc = c->ensure_mirror();
+  if (rc) return rc;
+  // ---- stage descriptors + stats in pinned memory, one H2D
+  size_t desc_bytes = 0;
+  for (auto& x : cp) desc_bytes += x.blob.size();
+  if ((rc = ensure_scratch(desc_bytes, n, eval != nullptr))) return rc;
+  uint8_t* hp = (uint8_t*)h_pinned;
+  std::vector<uint32_t> offs(n);
+  size_t o = 0;
+  for (int i = 0; i < n; ++i) {
+    offs[i] = (uint32_t)o;
+    std::memcpy(hp + o, cp[i].blob.data(), cp[i].blob.size());
+    o += cp[i].blob.size();
+  }
+  std::memcpy(hp + o, offs.data(), (size_t)n * 4);
+  PodStats* hs = (PodStats*)(hp + ((o + (size_t)n * 4 + 15) & ~size_t(15)));
+  for (int i = 0; i < n; ++i) {
+    std::memset(&hs[i], 0, sizeof(PodStats));
+    for (int q = 0; q < kNumPlugins; ++q) {
+      hs[i].max_raw[q] = enc_i64(INT64_MIN);
+      hs[i].min_raw[q] = enc_i64(INT64_MAX);
+    }
+  }
+  hipStream_t s = c->stream;
+  const MirrorView& m = c->view;
+  HIPCHK(hipMemcpyAsync(d_descs.p, hp, o, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_off.p, hp + o, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_stats.p, hs, (size_t)n * sizeof(PodStats), hipMemcpyHostToDevice, s));
+  if (eval) {
+    HIPCHK(hipMemsetAsync(d_out.p, 0, (size_t)m.cap * 8 * kNumPlugins, s));
+    HIPCHK(hipMemsetAsync(d_total.p, 0, (size_t)m.cap * 8, s));
+  }
+  const BatchView bv = bview(n);
+  const int stride = c->cfg.timing_stride;
+  const size_t npairs = stride > 0 ? (size_t)((n + stride - 1) / stride) : 0;
+  while (tev.size() < 2 * npairs) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    tev.push_back(e);
+  }
+  HIPCHK(hipEventRecord(ev0, s));
+  int launches = 0, timed = 0;
+  double bytes = 0;
+  for (int i = 0; i < n; ++i) {
+    if (cp[i].error) continue;
+    const bool t = stride > 0 && i % stride == 0;
+    if (t) HIPCHK(hipEventRecord(tev[2 * (size_t)timed], s));
+    HIPCHK(launch_filter_score(m, bv, i, s));
+    if (t) HIPCHK(hipEventRecord(tev[2 * (size_t)timed++ + 1], s));
+    HIPCHK(launch_select(m, bv, i, s));
+    bytes += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[i].blob.data()));
+    launches++;
+  }
+  HIPCHK(hipEventRecord(ev1, s));
+  DevResult* hr = (DevResult*)(hs + n);
+  HIPCHK(hipMemcpyAsync(hr, d_results.p, (size_t)n * sizeof(DevResult), hipMemcpyDeviceToHost, s));
+  std::vector<uint32_t> st;
+  std::vector<int64_t> outs, tot;
+  if (eval) {
+    st.resize(m.n);
+    outs.resize((size_t)m.cap * kNumPlugins);
+    tot.resize(m.n);
+    HIPCHK(hipMemcpyAsync(st.data(), d_status.p, (size_t)m.n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(outs.data(), d_out.p, outs.size() * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, ev0, ev1);
+  last_kernel_ms = launches ? ms / (2.0 * launches) : 0;
+  if (timed) {
+    double sum = 0;
+    for (int k = 0; k < timed; ++k) {
+      float x = 0;
+      HIPCHK(hipEventElapsedTime(&x, tev[2 * (size_t)k], tev[2 * (size_t)k + 1]));
+      sum += x;
+    }
+    last_kernel_ms = sum / timed;
+  }
+  last_bytes = launches ? bytes / launches : 0;
+  last_launches = launches;
+
+  // ---- results + host shadow of the device-side assumes
+  for (int i = 0; i < n; ++i) {
+    ksg_result& r = results[i];
+    if (cp[i].error) { r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0}; continue; }
+    const DevResult& d = hr[i];
+    r.status = d.status;
+    r.node_index = d.node;
+    r.feasible_nodes = d.feasible;
+    r.evaluated_nodes = d.feasible > 0 ? cp[i].num_all : (cp[i].prefilter_reject ? 0 : cp[i].num_all);
+    r.total_score = d.feasible > 1 ? d.total : 0;
+    if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
+    if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
+      PodSpec ap = *pods[i];
+      ap.node_name = c->order()[r.node_index];
+      static uint64_t seq = 0;
+      std::string uid = ap.uid + "#a" + std::to_string(++seq);
+      int rc2 = c->add_pod(ap, uid, /*device_done=*/true);
+      if (rc2) return rc2;
+      assumed[handles.empty() ? -1 : handles[i]] = uid;
+    }
+  }
+  if (eval) {
+    const int32_t N = m.n;
+    eval->prefilter_code = cp[0].prefilter_reject ? cp[0].prefilter_code : 0;
+    eval->prefilter_plugin = cp[0].prefilter_reject ? cp[0].prefilter_plugin : 255;
+    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject) ? cp[0].score_mask : 0;
+    for (int32_t i = 0; i < N; ++i) {
+      const uint32_t w = st[i];
+      if (eval->node_code) eval->node_code[i] = (uint8_t)status_code(w);
+      if (eval->node_plugin) eval->node_plugin[i] = status_plugin(w) == 15u ? 255 : (uint8_t)status_plugin(w);
+      if (eval->node_reasons) eval->node_reasons[i] = status_reasons(w);
+      const bool scored = hr[0].feasible > 1 && status_code(w) == 0;
+      if (eval->total_scores) eval->total_scores[i] = scored ? tot[i] : 0;
+      if (eval->plugin_scores)
+        for (int q = 0; q < kNumPlugins; ++q)
+          eval->plugin_scores[(size_t)q * N + i] = scored ? outs[(size_t)q * m.cap + i] : 0;
+    }
+  }
+  return KSG_OK;
+}
+
+int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, int32_t* code, uint8_t* codes, uint32_t* reasons,
+                       int64_t* raw, int64_t* norm) {
+  const int32_t N = (int32_t)c->order().size();
+  *code = KSG_CODE_SUCCESS;
+  for (int32_t i = 0; i < N; ++i) {
+    if (codes) codes[i] = 0;
+    if (reasons) reasons[i] = 0;
+    if (raw) raw[i] = 0;
+    if (norm) norm[i] = 0;
+  }
+  CompiledPod cp;
+  int rc = compile(p, mode, plugin, false, true, &cp);
+  if (rc) return rc;
+  const PodDesc& D = *reinterpret_cast<const PodDesc*>(cp.blob.data());
+  if (mode == FILTER_ONE) {
+    // the plugin's own PreFilter first (framework.go:934-995): Skip, or a rejection every node gets
+    if (!(D.filter_mask & (1u << plugin))) { *code = KSG_CODE_SKIP; return KSG_OK; }
+    if (cp.prefilter_reject) {
+      *code = cp.prefilter_code;
+      for (int32_t i = 0; i < N; ++i) {
+        if (codes) codes[i] = (uint8_t)cp.prefilter_code;
+        if (reasons) reasons[i] = KSG_R_PREFILTER;
+      }
+      return KSG_OK;
+    }
+  } else {
+    if (cp.error) { *code = KSG_CODE_ERROR; return KSG_OK; }
+    if (!(D.score_mask & (1u << plugin))) { *code = KSG_CODE_SKIP; return KSG_OK; }
+  }
+  if ((rc = c->ensure_mirror())) return rc;
+  if ((rc = ensure_scratch(cp.blob.size(), 1, true))) return rc;
+  uint8_t* hp = (uint8_t*)h_pinned;
+  std::memcpy(hp, cp.blob.data(), cp.blob.size());
+  uint32_t off0 = 0;
+  PodStats* hs = (PodStats*)(hp + ((cp.blob.size() + 15) & ~size_t(15)));
+  std::memset(hs, 0, sizeof(PodStats));
+  for (int q = 0; q < kNumPlugins; ++q) {
+    hs->max_raw[q] = enc_i64(INT64_MIN);
+    hs->min_raw[q] = enc_i64(INT64_MAX);
+  }
+  hipStream_t s = c->stream;
+  const MirrorView& m = c->view;
+  HIPCHK(hipMemcpyAsync(d_descs.p, hp, cp.blob.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_off.p, &off0, 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_stats.p, hs, sizeof(PodStats), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(d_out.p, 0, (size_t)m.cap * 8 * kNumPlugins, s));
+  const BatchView bv = bview(1);
+  HIPCHK(launch_filter_score(m, bv, 0, s));
+  if (mode == SCORE_ONE) HIPCHK(launch_select(m, bv, 0, s));
+  std::vector<uint32_t> st(N);
+  std::vector<int64_t> rv(N), nv(N);
+  if (mode == FILTER_ONE) {
+    HIPCHK(hipMemcpyAsync(st.data(), d_status.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+  } else {
+    HIPCHK(hipMemcpyAsync(rv.data(), (int64_t*)d_raw.p + (size_t)plugin * m.cap, (size_t)N * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(nv.data(), (int64_t*)d_out.p + (size_t)plugin * m.cap, (size_t)N * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  for (int32_t i = 0; i < N; ++i) {
+    if (mode == FILTER_ONE) {
+      if (codes) codes[i] = (uint8_t)status_code(st[i]);
+      if (reasons) reasons[i] = status_reasons(st[i]);
+    } else {
+      if (raw) raw[i] = rv[i];
+      if (norm) norm[i] = nv[i];
+    }
+  }
+  return KSG_OK;
+}
+
+}  // namespace ksg

@@ -1,0 +1,328 @@
+// host.hpp -- host side of the MI355X node-evaluation engine.
+//
+// Layers (bottom-up):
+//   objects  : v1.Node / v1.Pod / v1.Namespace decoded from JSON into scheduler-facing specs
+//   Cluster  : the scheduler cache mirror on the host -- interning tables (label keys/values,
+//              taints, images, host ports, extended resources), NodeInfo shadows, bound pods,
+//              nodeTree order (backend/cache/node_tree.go) -- plus the HBM mirror it feeds
+//   Engine   : per-pod compilation (PreFilter/PreScore work that is O(pod), not O(nodes)) into
+//              PodDesc programs, batch launch of the per-node kernels, result readback
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../common/desc.h"
+#include "json.hpp"
+#include "ksg.h"
+
+namespace ksg {
+
+// ===================================================================================
+// objects
+// ===================================================================================
+using StrMap = std::vector<std::pair<std::string, std::string>>;  // sorted by key
+
+struct ResAmount {  // v1.ResourceList entry, quantity in milli-units (Quantity.MilliValue())
+  std::string name;
+  int64_t milli;
+};
+using ResVec = std::vector<ResAmount>;
+
+bool parse_quantity(const std::string& s, int64_t* milli);
+int64_t milli_ceil(int64_t m);  // Quantity.Value() from milli-units (rounds up)
+bool parse_go_int(const std::string& s, int64_t* v);  // strconv.ParseInt(s, 10, 64)
+bool valid_label_key(const std::string& k);            // validation.IsQualifiedName
+bool valid_label_value(const std::string& v);          // validation.IsValidLabelValue
+bool scalar_resource(const std::string& n);            // scheduler/util/utils.go:200-203
+
+struct Expr { std::string key, op; std::vector<std::string> values; };
+struct NSTerm { std::vector<Expr> exprs, fields; };
+struct LabelSel {  // metav1.LabelSelector; present=false is a nil selector
+  bool present = false;
+  StrMap match;
+  std::vector<Expr> exprs;
+};
+struct PATerm {
+  LabelSel sel;
+  std::vector<std::string> namespaces;
+  LabelSel ns_sel;
+  std::string topo;
+  int32_t weight = 0;
+};
+struct Tol { std::string key, op, value, effect; };
+struct HostPort { std::string ip, proto; int32_t port; };
+struct Container {
+  std::string image;
+  ResVec req;
+  std::vector<HostPort> ports;
+  bool sidecar = false;
+};
+struct Spread {
+  int32_t max_skew = 0;
+  std::string key, when;
+  LabelSel sel;
+  int32_t min_domains = 1;
+  bool aff_honor = true, taint_honor = false;
+  std::vector<std::string> match_label_keys;
+};
+
+struct PodSpec {
+  std::string name, ns, uid;
+  StrMap labels;
+  bool terminating = false;
+  std::string node_name;
+  bool has_node_selector = false;
+  StrMap node_selector;
+  bool has_required_na = false;
+  std::vector<NSTerm> required_na;
+  bool has_preferred_na = false;
+  std::vector<std::pair<int32_t, NSTerm>> preferred_na;
+  bool has_pod_affinity = false, has_pod_anti = false;
+  std::vector<PATerm> aff_req, anti_req, aff_pref, anti_pref;
+  std::vector<Tol> tolerations;
+  std::vector<Container> containers, init_containers;
+  bool has_overhead = false;
+  ResVec overhead, pod_requests;
+  std::vector<Spread> spreads;
+  std::vector<std::string> image_volumes;
+};
+struct NodeImage { std::vector<std::string> names; int64_t size; };
+struct NodeSpec {
+  std::string name;
+  StrMap labels;
+  bool unschedulable = false;
+  std::vector<std::array<std::string, 3>> taints;  // key, value, effect
+  ResVec alloc;
+  std::vector<NodeImage> images;
+};
+struct NamespaceSpec { std::string name; StrMap labels; };
+
+bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err);
+bool decode_node(const char* p, size_t n, NodeSpec* out, std::string* err);
+bool decode_namespace(const char* p, size_t n, NamespaceSpec* out, std::string* err);
+
+// pod requests (component-helpers/resource/helpers.go:151-291) for the scheduler's uses
+struct PodResources {
+  int64_t cpu = 0, mem = 0, eph = 0;  // Requested contribution (Resource.Add semantics)
+  std::vector<std::pair<std::string, int64_t>> scalar;
+  int64_t nz_cpu = 0, nz_mem = 0;
+  // Fit filter max-request vector (SetMaxResource) -- identical values in practice
+};
+ResVec pod_requests(const PodSpec& p, const ResVec* non_missing);
+PodResources calc_resources(const PodSpec& p);
+bool tolerates(const Tol& t, const std::string& key, const std::string& value, const std::string& effect,
+               bool cmp_ops);
+
+// ===================================================================================
+// config (KubeSchedulerConfiguration subset)
+// ===================================================================================
+struct Config {
+  int pct = 100;
+  bool enabled[kNumPlugins];
+  int64_t weight[kNumPlugins];
+  int fit_strategy = 0;
+  std::vector<std::pair<std::string, int64_t>> fit_res{{"cpu", 1}, {"memory", 1}};
+  std::vector<std::pair<int64_t, int64_t>> rtcr;
+  std::set<std::string> ignored_res, ignored_groups;
+  std::vector<std::pair<std::string, int64_t>> bal_res{{"cpu", 1}, {"memory", 1}};
+  int32_t hard_weight = 1;
+  bool ignore_pref_existing = false;
+  bool taint_cmp_ops = false;
+  bool has_added_required = false;
+  std::vector<NSTerm> added_required;
+  bool has_added_pref = false;
+  std::vector<std::pair<int32_t, NSTerm>> added_pref;
+  int device = 0;
+  int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
+  Config();
+};
+bool decode_config(const char* p, size_t n, Config* c, std::string* err);
+bool valid_ns_term(const NSTerm& t);
+
+// ===================================================================================
+// Cluster: host shadow + interning
+// ===================================================================================
+struct Interner {
+  std::unordered_map<std::string, int32_t> ids;
+  std::vector<std::string> strs;
+  int32_t get(const std::string& s) {
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    int32_t id = (int32_t)strs.size();
+    ids.emplace(s, id);
+    strs.push_back(s);
+    return id;
+  }
+  int32_t find(const std::string& s) const {
+    auto it = ids.find(s);
+    return it == ids.end() ? -1 : it->second;
+  }
+};
+
+struct LabelKey {
+  Interner values;      // local value ids
+  int32_t slot = -1;    // materialised HBM column, -1 if none
+};
+
+struct BoundPod {  // a pod in the cache (added bound or assumed)
+  std::string uid, node;
+  PodResources res;
+  std::vector<uint32_t> port_ids;
+  bool with_affinity = false;  // podWithAffinity (framework/types.go:386-389)
+};
+
+struct NodeRec {
+  NodeSpec spec;
+  std::vector<std::pair<int32_t, int32_t>> labels;  // (key id, local value id)
+  std::vector<uint32_t> taint_ids;
+  std::vector<uint32_t> image_ids;  // sorted unique image name ids on the node
+  int64_t alloc_cpu = 0, alloc_mem = 0, alloc_eph = 0, alloc_pods = 0;
+  std::map<int32_t, int64_t> scalar_alloc;
+  // NodeInfo.Requested / NonZeroRequested / Pods / UsedPorts
+  int64_t req_cpu = 0, req_mem = 0, req_eph = 0, nz_cpu = 0, nz_mem = 0;
+  int32_t num_pods = 0;
+  std::map<int32_t, int64_t> scalar_req;
+  std::set<uint32_t> ports;
+  std::vector<std::string> pods;  // uids in NodeInfo.Pods order
+};
+
+struct TaintRec { std::string key, value, effect; };
+struct PortRec { std::string ip, proto; int32_t port; };
+struct ImageState { int64_t size = 0; std::set<std::string> nodes; };
+
+// device mirror buffers
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+class Cluster {
+ public:
+  explicit Cluster(const Config& cfg);
+  ~Cluster();
+  Config cfg;
+  std::string err;
+
+  // informer-fed cache events
+  int upsert_namespace(const NamespaceSpec& ns);
+  int add_node(NodeSpec&& n);
+  int update_node(NodeSpec&& n);
+  int remove_node(const std::string& name);
+  // device_done: the HBM mirror already holds the pod (device-side AssumePod)
+  int add_pod(const PodSpec& p, const std::string& uid_override = "", bool device_done = false);
+  int remove_pod(const std::string& uid);
+  int32_t pods_with_affinity = 0;
+
+  // snapshot order (nodeTree.list)
+  const std::vector<std::string>& order();
+  int32_t index_of(const std::string& node) const;
+  NodeRec* node(const std::string& name);
+
+  // interning used by the compiler
+  Interner label_keys;
+  std::vector<LabelKey> keys;
+  Interner taint_ix;
+  std::vector<TaintRec> taints;
+  Interner image_ix;
+  std::map<std::string, ImageState> image_states;
+  Interner port_ix;
+  std::vector<PortRec> ports;
+  Interner scalar_ix;  // extended / scalar resource columns
+  std::map<std::string, NamespaceSpec> namespaces;
+  std::map<std::string, BoundPod> pods;
+
+  int32_t key_id(const std::string& k);
+  int32_t scalar_slot(const std::string& n);  // -1 if too many distinct scalars
+  uint32_t port_id(std::string ip, std::string proto, int32_t port);
+
+  // ---- HBM mirror
+  MirrorView view;
+  hipStream_t stream = nullptr;
+  bool layout_dirty = true;
+  int ensure_mirror();                       // (re)build device arrays if dirty
+  int ensure_label_slot(int32_t key);        // materialise a label column
+  int upload_node_dynamic(int32_t idx);      // push one node's Requested/ports to HBM
+  int64_t next_start = 0;                    // Scheduler.nextStartNodeIndex
+  double taint_ids_per_node = 0, img_ids_per_node = 0;  // CSR densities (algorithmic-bytes model)
+
+ private:
+  std::vector<std::string> zones_;
+  std::map<std::string, std::vector<std::string>> tree_;
+  std::unordered_map<std::string, std::unique_ptr<NodeRec>> nodes_;
+  std::vector<std::string> order_;
+  std::unordered_map<std::string, int32_t> index_;
+  bool order_dirty_ = true;
+  int32_t slots_used_ = 0, slots_cap_ = 0;
+  std::vector<DevBuf> bufs_;
+
+  void tree_add(const NodeSpec& n);
+  void tree_remove(const NodeSpec& n);
+  void intern_node(NodeRec& r);
+  void add_images(const NodeSpec& n);
+  void remove_images(const NodeSpec& n);
+  void apply_pod(NodeRec& r, const BoundPod& bp, int sign);
+  void* dalloc(size_t bytes);
+  void free_all();
+  int upload_label_column(int32_t key);
+};
+
+// ===================================================================================
+// Engine: pod compilation + kernel batches
+// ===================================================================================
+struct CompiledPod {
+  std::vector<uint8_t> blob;  // PodDesc + payload, 16-byte multiple
+  PodResources res;
+  std::vector<uint32_t> port_ids;
+  int32_t num_all = 0;        // nodes in the evaluation list
+  int32_t subset_first = -1;  // for nextStart bookkeeping
+  bool prefilter_reject = false;
+  int32_t prefilter_code = 0, prefilter_plugin = 255;
+  bool error = false;         // PreScore/Score error -> status Error, no launch
+  uint32_t score_mask = 0;
+};
+
+class Engine {
+ public:
+  explicit Engine(Cluster* c);
+  ~Engine();
+  Cluster* c;
+  std::map<int32_t, PodSpec> queue;
+  std::map<int32_t, std::string> assumed;  // handle -> uid
+  int32_t next_handle = 1;
+
+  enum Mode { CYCLE, FILTER_ONE, SCORE_ONE };
+  // compile `p` for the current cluster; rot_start from Cluster::next_start
+  int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out);
+  // run a batch of cycles (device-resident, sequential semantics)
+  int run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
+                ksg_result* results, ksg_eval_out* eval);
+  int run_plugin(const PodSpec& p, Mode mode, int plugin, int32_t* code, uint8_t* codes, uint32_t* reasons,
+                 int64_t* raw, int64_t* norm);
+
+  // measurement: average k_filter_score duration (sampled with events when cfg.timing_stride > 0,
+  // else the batch's kernel time / launches) and its algorithmic bytes per launch
+  double algo_bytes(const PodDesc& d) const;
+  double last_kernel_ms = 0, last_bytes = 0;
+  int32_t last_launches = 0;
+
+ private:
+  // per-batch device scratch
+  DevBuf d_descs, d_off, d_stats, d_results, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
+  void* h_pinned = nullptr;
+  size_t h_pinned_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> tev;  // sampled k_filter_score timing events (pairs)
+  int ensure(DevBuf& b, size_t bytes);
+  int ensure_scratch(size_t desc_bytes, int pods, bool eval);
+  BatchView bview(int pods);
+};
+
+}  // namespace ksg

@@ -1,0 +1,585 @@
+// objects.cpp -- v1 object decoding and the O(pod) helper semantics the compiler needs.
+#include <algorithm>
+#include <climits>
+
+#include "host.hpp"
+
+namespace ksg {
+
+// ---- resource.Quantity -> milli-units (apimachinery/pkg/api/resource/quantity.go) ------------
+// The value is held exactly as digits * 2^b2 * 10^e10 and scaled to milli with a
+// round-up (MilliValue / ScaledValue semantics).
+bool parse_quantity(const std::string& s, int64_t* milli) {
+  const char* p = s.c_str();
+  const char* e = p + s.size();
+  int sign = 1;
+  if (p < e && (*p == '+' || *p == '-')) sign = (*p++ == '-') ? -1 : 1;
+  unsigned __int128 digits = 0;
+  int frac_digits = 0, nd = 0;
+  bool seen_dot = false;
+  for (; p < e; ++p) {
+    if (*p >= '0' && *p <= '9') {
+      if (digits > ((unsigned __int128)1 << 96)) return false;
+      digits = digits * 10u + (unsigned)(*p - '0');
+      nd++;
+      if (seen_dot) frac_digits++;
+    } else if (*p == '.' && !seen_dot) {
+      seen_dot = true;
+    } else {
+      break;
+    }
+  }
+  if (nd == 0) return false;
+  const std::string suffix(p, e);
+  int b2 = 0, e10 = 0;
+  if (suffix.empty()) {
+  } else if (suffix.size() == 2 && suffix[1] == 'i') {
+    static const char* bin = "KMGTPE";
+    const char* q = std::strchr(bin, suffix[0]);
+    if (!q) return false;
+    b2 = 10 * (int)(q - bin + 1);
+  } else if (suffix.size() == 1) {
+    switch (suffix[0]) {
+      case 'n': e10 = -9; break;
+      case 'u': e10 = -6; break;
+      case 'm': e10 = -3; break;
+      case 'k': e10 = 3; break;
+      case 'M': e10 = 6; break;
+      case 'G': e10 = 9; break;
+      case 'T': e10 = 12; break;
+      case 'P': e10 = 15; break;
+      case 'E': e10 = 18; break;
+      default: return false;
+    }
+  } else if (suffix[0] == 'e' || suffix[0] == 'E') {
+    int64_t x;
+    if (!parse_go_int(suffix.substr(1), &x) || x < -40 || x > 40) return false;
+    e10 = (int)x;
+  } else {
+    return false;
+  }
+  const unsigned __int128 cap = (unsigned __int128)1 << 120;
+  unsigned __int128 v = digits << b2;
+  int scale = e10 - frac_digits + 3;
+  for (; scale > 0; --scale) {
+    v *= 10u;
+    if (v > cap) { *milli = sign > 0 ? LLONG_MAX : LLONG_MIN; return true; }
+  }
+  if (scale < 0) {
+    unsigned __int128 d = 1;
+    for (; scale < 0 && d < cap; ++scale) d *= 10u;
+    v = sign > 0 ? (v + d - 1) / d : v / d;
+  }
+  if (v > (unsigned __int128)LLONG_MAX) v = LLONG_MAX;
+  *milli = sign > 0 ? (int64_t)v : -(int64_t)v;
+  return true;
+}
+
+int64_t milli_ceil(int64_t m) { return m >= 0 ? m / 1000 + (m % 1000 ? 1 : 0) : -((-m) / 1000); }
+
+bool parse_go_int(const std::string& s, int64_t* v) {
+  if (s.empty()) return false;
+  size_t i = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+  if (i == s.size()) return false;
+  const bool neg = s[0] == '-';
+  unsigned __int128 acc = 0;
+  for (; i < s.size(); ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    acc = acc * 10 + (unsigned)(s[i] - '0');
+    if (acc > (unsigned __int128)LLONG_MAX + 1) return false;
+  }
+  if (!neg && acc > (unsigned __int128)LLONG_MAX) return false;
+  *v = neg ? (int64_t)(-(__int128)acc) : (int64_t)acc;
+  return true;
+}
+
+// ---- validation (apimachinery/pkg/util/validation/validation.go) -----------------------------
+static bool alnum(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
+static bool qualified_name_part(const std::string& s) {
+  if (s.empty() || s.size() > 63 || !alnum(s.front()) || !alnum(s.back())) return false;
+  return std::all_of(s.begin(), s.end(), [](char c) { return alnum(c) || c == '-' || c == '_' || c == '.'; });
+}
+static bool dns_subdomain(const std::string& s) {
+  if (s.empty() || s.size() > 253) return false;
+  size_t i = 0;
+  while (i <= s.size()) {
+    size_t j = s.find('.', i);
+    if (j == std::string::npos) j = s.size();
+    if (j == i) return false;
+    auto low = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
+    if (!low(s[i]) || !low(s[j - 1])) return false;
+    for (size_t k = i; k < j; ++k)
+      if (!low(s[k]) && s[k] != '-') return false;
+    i = j + 1;
+  }
+  return true;
+}
+bool valid_label_key(const std::string& k) {
+  size_t sl = k.find('/');
+  if (sl == std::string::npos) return qualified_name_part(k);
+  if (k.find('/', sl + 1) != std::string::npos) return false;
+  return dns_subdomain(k.substr(0, sl)) && qualified_name_part(k.substr(sl + 1));
+}
+bool valid_label_value(const std::string& v) { return v.empty() || qualified_name_part(v); }
+
+bool scalar_resource(const std::string& n) {  // v1helper Is{Extended,HugePage,PrefixedNative,AttachableVolume}
+  const bool prefixed_native = n.find("kubernetes.io/") != std::string::npos;
+  const bool native = n.find('/') == std::string::npos || prefixed_native;
+  const bool extended = !native && n.rfind("requests.", 0) != 0 && valid_label_key("requests." + n);
+  return extended || n.rfind("hugepages-", 0) == 0 || prefixed_native || n.rfind("attachable-volumes-", 0) == 0;
+}
+
+// ---- JSON decoding ------------------------------------------------------------------------
+static StrMap kv_map(const JDoc& d, const JVal* o) {
+  StrMap m;
+  d.each(o, [&](const JVal& v) {
+    if (v.type == JVal::STR) m.emplace_back(v.key, v.s);
+  });
+  std::sort(m.begin(), m.end());
+  return m;
+}
+static std::vector<std::string> str_list(const JDoc& d, const JVal* a) {
+  std::vector<std::string> out;
+  d.each(a, [&](const JVal& v) {
+    if (v.type == JVal::STR) out.push_back(v.s);
+  });
+  return out;
+}
+static bool res_list(const JDoc& d, const JVal* o, ResVec* out, std::string* err) {
+  bool ok = true;
+  d.each(o, [&](const JVal& v) {
+    int64_t m;
+    if (!ok) return;
+    if (!parse_quantity(v.s, &m)) {
+      *err = "invalid quantity " + v.key + "=" + v.s;
+      ok = false;
+      return;
+    }
+    out->push_back({v.key, m});
+  });
+  return ok;
+}
+static std::vector<Expr> exprs(const JDoc& d, const JVal* a) {
+  std::vector<Expr> out;
+  d.each(a, [&](const JVal& e) { out.push_back({d.str(e, "key"), d.str(e, "operator"), str_list(d, d.get(e, "values"))}); });
+  return out;
+}
+static NSTerm ns_term(const JDoc& d, const JVal& t) {
+  return NSTerm{exprs(d, d.get(t, "matchExpressions")), exprs(d, d.get(t, "matchFields"))};
+}
+static LabelSel label_sel(const JDoc& d, const JVal* v) {
+  LabelSel s;
+  if (!v) return s;
+  s.present = true;
+  s.match = kv_map(d, d.get(*v, "matchLabels"));
+  s.exprs = exprs(d, d.get(*v, "matchExpressions"));
+  return s;
+}
+static PATerm pa_term(const JDoc& d, const JVal& t, int32_t weight) {
+  PATerm p;
+  p.sel = label_sel(d, d.get(t, "labelSelector"));
+  p.namespaces = str_list(d, d.get(t, "namespaces"));
+  p.ns_sel = label_sel(d, d.get(t, "namespaceSelector"));
+  p.topo = d.str(t, "topologyKey");
+  p.weight = weight;
+  return p;
+}
+static bool container(const JDoc& d, const JVal& c, Container* out, std::string* err) {
+  out->image = d.str(c, "image");
+  if (const JVal* r = d.get(c, "resources"))
+    if (!res_list(d, d.get(*r, "requests"), &out->req, err)) return false;
+  d.each(d.get(c, "ports"), [&](const JVal& p) {
+    out->ports.push_back({d.str(p, "hostIP"), d.str(p, "protocol"), (int32_t)d.num(p, "hostPort")});
+  });
+  out->sidecar = d.str(c, "restartPolicy") == "Always";
+  return true;
+}
+
+bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
+  try {
+    JDoc d(p, n);
+    const JVal& r = d.root();
+    const JVal* md = d.get(r, "metadata");
+    if (!md) { *err = "pod without metadata"; return false; }
+    out->name = d.str(*md, "name");
+    out->ns = d.str(*md, "namespace", "default");
+    if (out->ns.empty()) out->ns = "default";
+    out->uid = d.str(*md, "uid");
+    if (out->uid.empty()) out->uid = out->ns + "/" + out->name;
+    out->labels = kv_map(d, d.get(*md, "labels"));
+    out->terminating = d.present(*md, "deletionTimestamp");
+    const JVal* sp = d.get(r, "spec");
+    if (!sp) return true;
+    out->node_name = d.str(*sp, "nodeName");
+    if (const JVal* ns = d.get(*sp, "nodeSelector")) {
+      out->has_node_selector = true;
+      out->node_selector = kv_map(d, ns);
+    }
+    if (const JVal* af = d.get(*sp, "affinity")) {
+      if (const JVal* na = d.get(*af, "nodeAffinity")) {
+        if (const JVal* rq = d.get(*na, "requiredDuringSchedulingIgnoredDuringExecution")) {
+          out->has_required_na = true;
+          d.each(d.get(*rq, "nodeSelectorTerms"), [&](const JVal& t) { out->required_na.push_back(ns_term(d, t)); });
+        }
+        if (const JVal* pf = d.get(*na, "preferredDuringSchedulingIgnoredDuringExecution")) {
+          out->has_preferred_na = true;
+          d.each(pf, [&](const JVal& t) {
+            const JVal* pr = d.get(t, "preference");
+            out->preferred_na.push_back({(int32_t)d.num(t, "weight"), pr ? ns_term(d, *pr) : NSTerm{}});
+          });
+        }
+      }
+      auto pa = [&](const char* key, bool* has, std::vector<PATerm>* req, std::vector<PATerm>* pref) {
+        const JVal* a = d.get(*af, key);
+        if (!a) return;
+        *has = true;
+        d.each(d.get(*a, "requiredDuringSchedulingIgnoredDuringExecution"),
+               [&](const JVal& t) { req->push_back(pa_term(d, t, 0)); });
+        d.each(d.get(*a, "preferredDuringSchedulingIgnoredDuringExecution"), [&](const JVal& t) {
+          const JVal* pt = d.get(t, "podAffinityTerm");
+          PATerm x = pt ? pa_term(d, *pt, (int32_t)d.num(t, "weight")) : PATerm{};
+          x.weight = (int32_t)d.num(t, "weight");
+          pref->push_back(x);
+        });
+      };
+      pa("podAffinity", &out->has_pod_affinity, &out->aff_req, &out->aff_pref);
+      pa("podAntiAffinity", &out->has_pod_anti, &out->anti_req, &out->anti_pref);
+    }
+    d.each(d.get(*sp, "tolerations"), [&](const JVal& t) {
+      out->tolerations.push_back({d.str(t, "key"), d.str(t, "operator"), d.str(t, "value"), d.str(t, "effect")});
+    });
+    bool ok = true;
+    d.each(d.get(*sp, "containers"), [&](const JVal& c) {
+      Container k;
+      ok = ok && container(d, c, &k, err);
+      out->containers.push_back(std::move(k));
+    });
+    d.each(d.get(*sp, "initContainers"), [&](const JVal& c) {
+      Container k;
+      ok = ok && container(d, c, &k, err);
+      out->init_containers.push_back(std::move(k));
+    });
+    if (!ok) return false;
+    if (const JVal* oh = d.get(*sp, "overhead")) {
+      out->has_overhead = true;
+      if (!res_list(d, oh, &out->overhead, err)) return false;
+    }
+    if (const JVal* rs = d.get(*sp, "resources"))
+      if (!res_list(d, d.get(*rs, "requests"), &out->pod_requests, err)) return false;
+    d.each(d.get(*sp, "topologySpreadConstraints"), [&](const JVal& c) {
+      Spread s;
+      s.max_skew = (int32_t)d.num(c, "maxSkew");
+      s.key = d.str(c, "topologyKey");
+      s.when = d.str(c, "whenUnsatisfiable");
+      s.sel = label_sel(d, d.get(c, "labelSelector"));
+      if (d.present(c, "minDomains")) s.min_domains = (int32_t)d.num(c, "minDomains");
+      const std::string ap = d.str(c, "nodeAffinityPolicy"), tp = d.str(c, "nodeTaintsPolicy");
+      s.aff_honor = ap.empty() || ap == "Honor";  // common.go:113-114 defaults
+      s.taint_honor = tp == "Honor";
+      s.match_label_keys = str_list(d, d.get(c, "matchLabelKeys"));
+      out->spreads.push_back(std::move(s));
+    });
+    d.each(d.get(*sp, "volumes"), [&](const JVal& v) {
+      if (const JVal* im = d.get(v, "image")) out->image_volumes.push_back(d.str(*im, "reference"));
+    });
+    return true;
+  } catch (std::exception& e) {
+    *err = e.what();
+    return false;
+  }
+}
+
+bool decode_node(const char* p, size_t n, NodeSpec* out, std::string* err) {
+  try {
+    JDoc d(p, n);
+    const JVal& r = d.root();
+    const JVal* md = d.get(r, "metadata");
+    if (!md || d.str(*md, "name").empty()) { *err = "node without name"; return false; }
+    out->name = d.str(*md, "name");
+    out->labels = kv_map(d, d.get(*md, "labels"));
+    if (const JVal* sp = d.get(r, "spec")) {
+      out->unschedulable = d.boolean(*sp, "unschedulable");
+      d.each(d.get(*sp, "taints"), [&](const JVal& t) {
+        out->taints.push_back({d.str(t, "key"), d.str(t, "value"), d.str(t, "effect")});
+      });
+    }
+    if (const JVal* st = d.get(r, "status")) {
+      if (!res_list(d, d.get(*st, "allocatable"), &out->alloc, err)) return false;
+      d.each(d.get(*st, "images"), [&](const JVal& im) {
+        out->images.push_back({str_list(d, d.get(im, "names")), d.num(im, "sizeBytes")});
+      });
+    }
+    return true;
+  } catch (std::exception& e) {
+    *err = e.what();
+    return false;
+  }
+}
+
+bool decode_namespace(const char* p, size_t n, NamespaceSpec* out, std::string* err) {
+  try {
+    JDoc d(p, n);
+    const JVal* md = d.get(d.root(), "metadata");
+    if (!md || d.str(*md, "name").empty()) { *err = "namespace without name"; return false; }
+    out->name = d.str(*md, "name");
+    out->labels = kv_map(d, d.get(*md, "labels"));
+    return true;
+  } catch (std::exception& e) {
+    *err = e.what();
+    return false;
+  }
+}
+
+// ---- resource requests (component-helpers/resource/helpers.go:151-348) ------------------------
+static void add_res(ResVec& a, const ResVec& b) {
+  for (const auto& x : b) {
+    auto it = std::find_if(a.begin(), a.end(), [&](const ResAmount& r) { return r.name == x.name; });
+    if (it == a.end()) a.push_back(x);
+    else it->milli += x.milli;
+  }
+}
+static void max_res(ResVec& a, const ResVec& b) {
+  for (const auto& x : b) {
+    auto it = std::find_if(a.begin(), a.end(), [&](const ResAmount& r) { return r.name == x.name; });
+    if (it == a.end()) a.push_back(x);
+    else if (x.milli > it->milli) it->milli = x.milli;
+  }
+}
+static bool has_res(const ResVec& a, const std::string& n) {
+  return std::any_of(a.begin(), a.end(), [&](const ResAmount& r) { return r.name == n; });
+}
+static ResVec with_non_missing(const ResVec& req, const ResVec* nm) {
+  ResVec out = req;
+  if (!nm) return out;
+  for (const auto& x : *nm)
+    if (!has_res(req, x.name)) add_res(out, {x});
+  return out;
+}
+static bool pod_level_supported(const std::string& n) {
+  return n == "cpu" || n == "memory" || n.rfind("hugepages-", 0) == 0;
+}
+
+ResVec pod_requests(const PodSpec& p, const ResVec* non_missing) {
+  ResVec reqs;
+  for (const auto& c : p.containers) add_res(reqs, with_non_missing(c.req, non_missing));
+  ResVec restartable, init;
+  for (const auto& c : p.init_containers) {
+    ResVec cr = with_non_missing(c.req, non_missing);
+    if (c.sidecar) {
+      add_res(reqs, cr);
+      add_res(restartable, cr);
+      cr = restartable;
+    } else {
+      ResVec tmp;
+      add_res(tmp, cr);
+      add_res(tmp, restartable);
+      cr = tmp;
+    }
+    max_res(init, cr);
+  }
+  max_res(reqs, init);
+  bool pod_level = false;
+  for (const auto& r : p.pod_requests) pod_level |= pod_level_supported(r.name);
+  if (pod_level)
+    for (const auto& r : p.pod_requests)
+      if (pod_level_supported(r.name)) {
+        auto it = std::find_if(reqs.begin(), reqs.end(), [&](const ResAmount& x) { return x.name == r.name; });
+        if (it == reqs.end()) reqs.push_back(r);
+        else it->milli = r.milli;
+      }
+  if (p.has_overhead) add_res(reqs, p.overhead);
+  return reqs;
+}
+
+PodResources calc_resources(const PodSpec& p) {  // framework/types.go:1035-1076
+  const ResVec requests = pod_requests(p, nullptr);
+  bool pod_level = false;
+  for (const auto& r : p.pod_requests) pod_level |= pod_level_supported(r.name);
+  ResVec nm;  // getNonMissingContainerRequests (types.go:1387-1415)
+  const int64_t cpu_def = 100, mem_def = 200LL * 1024 * 1024 * 1000;
+  if (!pod_level || !has_res(requests, "cpu")) nm.push_back({"cpu", cpu_def});
+  if (!pod_level || !has_res(requests, "memory")) nm.push_back({"memory", mem_def});
+  const ResVec non0 = nm.empty() ? requests : pod_requests(p, &nm);
+  PodResources out;
+  for (const auto& r : requests) {
+    if (r.name == "cpu") out.cpu += r.milli;
+    else if (r.name == "memory") out.mem += milli_ceil(r.milli);
+    else if (r.name == "ephemeral-storage") out.eph += milli_ceil(r.milli);
+    else if (r.name != "pods" && scalar_resource(r.name)) out.scalar.push_back({r.name, milli_ceil(r.milli)});
+  }
+  for (const auto& r : non0) {
+    if (r.name == "cpu") out.nz_cpu = r.milli;
+    else if (r.name == "memory") out.nz_mem = milli_ceil(r.milli);
+  }
+  return out;
+}
+
+// api/core/v1/toleration.go:52-112
+static bool decimal_integer(const std::string& v) {
+  if (v.empty()) return false;
+  size_t i = v[0] == '-' ? 1 : 0;
+  if (i == v.size()) return false;
+  if (v[i] == '0') return v.size() == 1;
+  for (; i < v.size(); ++i)
+    if (v[i] < '0' || v[i] > '9') return false;
+  return true;
+}
+bool tolerates(const Tol& t, const std::string& key, const std::string& value, const std::string& effect,
+               bool cmp_ops) {
+  if (!t.effect.empty() && t.effect != effect) return false;
+  if (!t.key.empty() && t.key != key) return false;
+  if (t.op.empty() || t.op == "Equal") return t.value == value;
+  if (t.op == "Exists") return true;
+  if ((t.op == "Lt" || t.op == "Gt") && cmp_ops) {
+    int64_t a, b;
+    if (!decimal_integer(t.value) || !parse_go_int(t.value, &a)) return false;
+    if (!decimal_integer(value) || !parse_go_int(value, &b)) return false;
+    return t.op == "Lt" ? b < a : b > a;
+  }
+  return false;
+}
+
+// ---- config --------------------------------------------------------------------------------
+static const char* kPluginNames[kNumPlugins] = {
+    "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts", "NodeResourcesFit",
+    "PodTopologySpread", "InterPodAffinity", "NodeResourcesBalancedAllocation", "ImageLocality"};
+
+Config::Config() {
+  static const int64_t w[kNumPlugins] = {0, 0, 3, 2, 0, 1, 2, 2, 1, 1};  // default_plugins.go:35-50
+  for (int i = 0; i < kNumPlugins; ++i) {
+    enabled[i] = true;
+    weight[i] = w[i];
+  }
+}
+
+static int plugin_by_name(const std::string& n) {
+  for (int i = 0; i < kNumPlugins; ++i)
+    if (n == kPluginNames[i]) return i;
+  return -1;
+}
+
+// nodeaffinity.newNodeSelectorTerm validity: labels.NewRequirement for matchExpressions
+// (apimachinery/pkg/labels/selector.go:210-245), one value + In/NotIn for matchFields
+bool valid_ns_term(const NSTerm& t) {
+  for (auto& e : t.exprs) {
+    if (!valid_label_key(e.key)) return false;
+    if (e.op == "In" || e.op == "NotIn") {
+      if (e.values.empty()) return false;
+    } else if (e.op == "Exists" || e.op == "DoesNotExist") {
+      if (!e.values.empty()) return false;
+    } else if (e.op == "Gt" || e.op == "Lt") {
+      int64_t v;
+      if (e.values.size() != 1 || !parse_go_int(e.values[0], &v)) return false;
+    } else {
+      return false;
+    }
+    for (auto& v : e.values)
+      if (!valid_label_value(v)) return false;
+  }
+  for (auto& f : t.fields)
+    if (f.values.size() != 1 || (f.op != "In" && f.op != "NotIn")) return false;
+  return true;
+}
+
+bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
+  if (!p || n == 0) return true;
+  try {
+    JDoc d(p, n);
+    const JVal& r = d.root();
+    if (d.present(r, "percentageOfNodesToScore")) c->pct = (int)d.num(r, "percentageOfNodesToScore");
+    if (const JVal* fg = d.get(r, "featureGates")) c->taint_cmp_ops = d.boolean(*fg, "TaintTolerationComparisonOperators");
+    c->device = (int)d.num(r, "device", 0);
+    c->timing_stride = (int)d.num(r, "kernelTimingStride", 0);
+    bool ok = true;
+    d.each(d.get(r, "scoreWeights"), [&](const JVal& v) {
+      int id = plugin_by_name(v.key);
+      if (id < 0) { ok = false; *err = "unknown plugin " + v.key; return; }
+      c->weight[id] = std::strtoll(v.s.c_str(), nullptr, 10);
+    });
+    d.each(d.get(r, "disabledPlugins"), [&](const JVal& v) {
+      int id = plugin_by_name(v.s);
+      if (id < 0) { ok = false; *err = "unknown plugin " + v.s; return; }
+      c->enabled[id] = false;
+    });
+    if (!ok) return false;
+    auto res_specs = [&](const JVal* a) {
+      std::vector<std::pair<std::string, int64_t>> out;
+      d.each(a, [&](const JVal& x) {
+        int64_t w = d.num(x, "weight", 0);
+        out.push_back({d.str(x, "name"), w == 0 ? 1 : w});  // v1 defaulting (defaults.go:218-221)
+      });
+      return out;
+    };
+    if (const JVal* f = d.get(r, "nodeResourcesFit")) {
+      if (const JVal* ss = d.get(*f, "scoringStrategy")) {
+        const std::string t = d.str(*ss, "type", "LeastAllocated");
+        if (t == "LeastAllocated") c->fit_strategy = 0;
+        else if (t == "MostAllocated") c->fit_strategy = 1;
+        else if (t == "RequestedToCapacityRatio") c->fit_strategy = 2;
+        else { *err = "unsupported scoring strategy " + t; return false; }
+        if (d.present(*ss, "resources")) c->fit_res = res_specs(d.get(*ss, "resources"));
+        if (const JVal* rc = d.get(*ss, "requestedToCapacityRatio"))
+          d.each(d.get(*rc, "shape"), [&](const JVal& pt) {
+            c->rtcr.push_back({d.num(pt, "utilization"), d.num(pt, "score") * 10});  // MaxNodeScore/MaxCustomPriorityScore
+          });
+      }
+      for (auto& s : str_list(d, d.get(*f, "ignoredResources"))) c->ignored_res.insert(s);
+      for (auto& s : str_list(d, d.get(*f, "ignoredResourceGroups"))) c->ignored_groups.insert(s);
+    }
+    if (const JVal* b = d.get(r, "balancedAllocation"))
+      if (d.present(*b, "resources")) c->bal_res = res_specs(d.get(*b, "resources"));
+    if (const JVal* ipa = d.get(r, "interPodAffinity")) {
+      if (d.present(*ipa, "hardPodAffinityWeight")) c->hard_weight = (int32_t)d.num(*ipa, "hardPodAffinityWeight");
+      c->ignore_pref_existing = d.boolean(*ipa, "ignorePreferredTermsOfExistingPods");
+    }
+    if (const JVal* na = d.get(r, "nodeAffinity"))
+      if (const JVal* aa = d.get(*na, "addedAffinity")) {
+        if (const JVal* rq = d.get(*aa, "requiredDuringSchedulingIgnoredDuringExecution")) {
+          c->has_added_required = true;
+          d.each(d.get(*rq, "nodeSelectorTerms"), [&](const JVal& t) { c->added_required.push_back(ns_term(d, t)); });
+        }
+        d.each(d.get(*aa, "preferredDuringSchedulingIgnoredDuringExecution"), [&](const JVal& t) {
+          const JVal* pr = d.get(t, "preference");
+          c->added_pref.push_back({(int32_t)d.num(t, "weight"), pr ? ns_term(d, *pr) : NSTerm{}});
+          c->has_added_pref = true;
+        });
+      }
+    // validation (apis/config/validation/validation_pluginargs.go)
+    for (auto& x : c->fit_res)
+      if (x.second <= 0 || x.second > 100) { *err = "resource weight of " + x.first + " not in valid range (0, 100]"; return false; }
+    std::set<std::string> seen;
+    for (auto& x : c->bal_res) {
+      if (!seen.insert(x.first).second) { *err = "duplicate resource " + x.first; return false; }
+      if (x.second != 1) { *err = "balanced allocation resource weight must be 1"; return false; }
+    }
+    if (c->hard_weight < 0 || c->hard_weight > 100) { *err = "hardPodAffinityWeight not in [0, 100]"; return false; }
+    if (c->fit_strategy == 2) {
+      if (c->rtcr.empty()) { *err = "requestedToCapacityRatio shape required"; return false; }
+      for (size_t i = 0; i < c->rtcr.size(); ++i) {
+        if ((i && c->rtcr[i - 1].first >= c->rtcr[i].first) || c->rtcr[i].first < 0 || c->rtcr[i].first > 100 ||
+            c->rtcr[i].second < 0 || c->rtcr[i].second > 100) {
+          *err = "invalid requestedToCapacityRatio shape";
+          return false;
+        }
+      }
+    }
+    for (int i = 0; i < kNumPlugins; ++i)
+      if (c->weight[i] < 0) { *err = "negative weight"; return false; }
+    // NodeAffinity New(): addedAffinity must parse (node_affinity.go New -> nodeaffinity.NewNodeSelector /
+    // NewPreferredSchedulingTerms); empty terms and weight-0 preferred terms are ignored there
+    for (auto& t : c->added_required)
+      if (!(t.exprs.empty() && t.fields.empty()) && !valid_ns_term(t)) { *err = "invalid addedAffinity"; return false; }
+    for (auto& t : c->added_pref)
+      if (t.first != 0 && !(t.second.exprs.empty() && t.second.fields.empty()) && !valid_ns_term(t.second)) {
+        *err = "invalid addedAffinity";
+        return false;
+      }
+    if (c->pct != 100 && c->pct != 0) { /* accepted; sampling handled by the engine */ }
+    return true;
+  } catch (std::exception& e) {
+    *err = e.what();
+    return false;
+  }
+}
+
+}  // namespace ksg

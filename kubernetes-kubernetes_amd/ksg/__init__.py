@@ -5,3 +5,4 @@ include/ksg.h); this package only binds it and mirrors the reference's
 scheduler/framework interface for tests and benchmarks.
 """
 from . import abi, objects  # noqa: F401
+from .abi import KsgError  # noqa: F401

@@ -1,0 +1,44 @@
+"""Loader for the product library lib/libksg.so (HIP kernels for gfx950 + the C ABI).
+
+There is deliberately no fallback: if the library is missing, fails to load, or no HIP
+device is visible, `Scheduler(...)` raises.  The parity oracle lives in oracle/ and is
+never reachable from here.
+"""
+import ctypes as C
+import os
+
+from .abi import Backend, KsgError
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(PKG, "lib", "libksg.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "ksg.h")
+
+_lib = None
+
+
+def load():
+    """dlopen libksg.so (raises KsgError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise KsgError(f"{LIB} not built: run `make -C {PKG}` or __graft_entry__.build()")
+        lib = C.CDLL(LIB)
+        lib.ksg_last_batch_kernel_stats.restype = C.c_int
+        lib.ksg_last_batch_kernel_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                                    C.POINTER(C.c_int32)]
+        _lib = lib
+    return _lib
+
+
+class Scheduler(Backend):
+    """One kube-scheduler profile + cache mirror resident in HBM (ksg_create)."""
+
+    def __init__(self, config=None):
+        super().__init__(load(), "ksg_", config)
+
+    def kernel_stats(self):
+        """(avg per-kernel ms, algorithmic bytes per launch, kernel pairs) of the last batch."""
+        ms, by, n = C.c_double(), C.c_double(), C.c_int32()
+        self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n)),
+                  "kernel_stats")
+        return ms.value, by.value, n.value

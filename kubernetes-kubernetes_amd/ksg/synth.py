@@ -1,0 +1,69 @@
+"""Seeded synthetic clusters shaped like the reference's scheduler_perf workloads.
+
+SchedulingBasic (test/integration/scheduler_perf/misc/performance-config.yaml:57-63):
+  nodes from templates/node-default.yaml -- allocatable cpu 4, memory 32Gi, pods 110,
+  label kubernetes.io/hostname (node_util.go:99-111);
+  pods from templates/pod-default.yaml -- one container, requests cpu 100m / memory 500Mi,
+  image registry.k8s.io/pause:3.10.2, containerPort 80 without a hostPort.
+`hetero=True` is SURVEY.md §8(d)'s heterogeneous variant (mixed capacities, pre-load, images)
+that makes scores untied so placement parity is exercised on distinct maxima too.
+"""
+import random
+
+from .objects import NodeW, PodW
+
+PAUSE = "registry.k8s.io/pause:3.10.2"
+GI = 1024 ** 3
+
+
+def node_default(name):
+    return (NodeW(name).capacity({"cpu": "4", "memory": "32Gi", "pods": "110"})
+            .label("kubernetes.io/hostname", name).obj())
+
+
+def pod_default(name, ns="default", node=None):
+    p = PodW(name, ns).container(image=PAUSE, requests={"cpu": "100m", "memory": "500Mi"},
+                                 ports=[{"containerPort": 80}])
+    if node:
+        p.node(node)
+    return p.obj()
+
+
+def scheduling_basic(n_nodes, n_init, n_pods, hetero=False, seed=0x5EED):
+    """-> (nodes, init_pods (bound), measured pods), all as v1 JSON dicts."""
+    rng = random.Random(seed)
+    nodes = []
+    images = [(f"registry.example/img-{k}:v1", rng.randint(10, 2000) * 1000 * 1000) for k in range(16)]
+    for i in range(n_nodes):
+        name = f"node-{i:06d}"
+        if not hetero:
+            nodes.append(node_default(name))
+            continue
+        cpu = rng.choice([4, 8, 16, 32, 64])
+        mem = rng.choice([16, 32, 64, 128, 256])
+        w = (NodeW(name).capacity({"cpu": str(cpu), "memory": f"{mem}Gi", "pods": "110"})
+             .label("kubernetes.io/hostname", name).label("topology.kubernetes.io/zone", f"zone-{i % 10}"))
+        imgs = rng.sample(images, rng.randint(0, 3))
+        if imgs:
+            w.images({n: s for n, s in imgs})
+        nodes.append(w.obj())
+    init = []
+    names = [n["metadata"]["name"] for n in nodes]
+    for k in range(n_init):
+        if hetero:
+            node = rng.choice(names)
+            p = PodW(f"init-{k}", "default").container(
+                image=PAUSE, requests={"cpu": f"{rng.randint(1, 8) * 250}m", "memory": f"{rng.randint(1, 16) * 256}Mi"})
+            init.append(p.node(node).obj())
+        else:
+            init.append(pod_default(f"init-{k}", node=names[k % len(names)]))
+    pods = []
+    for k in range(n_pods):
+        if hetero:
+            p = PodW(f"pod-{k}", "default").container(
+                image=rng.choice([PAUSE] + [n for n, _ in images]),
+                requests={"cpu": f"{rng.randint(1, 10) * 100}m", "memory": f"{rng.randint(1, 20) * 100}Mi"})
+            pods.append(p.obj())
+        else:
+            pods.append(pod_default(f"pod-{k}"))
+    return nodes, init, pods

@@ -381,6 +381,7 @@ struct ksgo_ctx {
   std::vector<NodeInfoO*> list;  // snapshot nodeInfoList order
   bool listDirty = true;
   int64_t nextStartNodeIndex = 0;
+  uint64_t assumeSeq = 0;
   std::map<int32_t, std::unique_ptr<Pod>> queue;  // compiled pods
   int32_t nextHandle = 1;
   std::map<int32_t, std::string> assumedUid;  // handle -> assumed pod uid
@@ -1549,7 +1550,7 @@ int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* r
     // Scheduler.assume (schedule_one.go:1102-1137) -> Cache.AssumePod (cache.go:397)
     Pod p = *it->second;
     p.nodeName = c->list[result->node_index]->node.name;
-    if (c->pods.count(p.uid)) p.uid = p.uid + "#" + std::to_string(handle);
+    p.uid = p.uid + "#a" + std::to_string(++c->assumeSeq);  // unique per assume
     auto pi = std::make_unique<PodInfo>();
     new_pod_info(p, pi.get());
     node_add_pod(*c->nodes[p.nodeName], pi.get());

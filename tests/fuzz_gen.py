@@ -1,0 +1,155 @@
+"""Seeded random clusters + pod streams for product-vs-oracle parity (node-local plugins).
+
+Covers the features the device path implements: resources (incl. init/sidecar containers,
+overhead, pod-level requests, extended resources), unschedulable nodes, taints/tolerations of
+every effect, nodeSelector, required/preferred node affinity (all operators, matchFields ->
+PreFilterResult subsets), host ports (incl. 0.0.0.0 wildcards), images, nodeName, and the
+profile knobs (scoring strategies, resource lists, added affinity, weights, disabled plugins).
+"""
+import random
+
+from ksg.objects import NodeW, PodW, expr
+
+ZONES = ["zone-a", "zone-b", "zone-c"]
+TAINT_KEYS = ["dedicated", "gpu", "spot"]
+IMAGES = [("registry.example/app:v1", 300 * 1000 * 1000), ("registry.example/db", 900 * 1000 * 1000),
+          ("docker.io/library/nginx:1.25", 60 * 1000 * 1000), ("registry.example/big:2", 1500 * 1000 * 1000)]
+
+
+def rand_node(rng, i, extended=True):
+    name = f"n{i:05d}"
+    cpu = rng.choice(["2", "4", "8", "16", "3500m"])
+    mem = rng.choice(["4Gi", "8Gi", "16Gi", "32Gi", "12000Mi"])
+    cap = {"cpu": cpu, "memory": mem, "pods": str(rng.choice([3, 10, 110]))}
+    if rng.random() < 0.3:
+        cap["ephemeral-storage"] = rng.choice(["10Gi", "100Gi"])
+    if extended and rng.random() < 0.3:
+        cap["example.com/gpu"] = str(rng.randint(0, 4))
+    w = NodeW(name).capacity(cap).label("kubernetes.io/hostname", name)
+    if rng.random() < 0.9:
+        w.label("topology.kubernetes.io/zone", rng.choice(ZONES))
+    if rng.random() < 0.5:
+        w.label("disk", rng.choice(["ssd", "hdd"]))
+    if rng.random() < 0.6:
+        w.label("gen", str(rng.randint(1, 6)))
+    if rng.random() < 0.07:
+        w.unschedulable()
+    taints = []
+    for _ in range(rng.choice([0, 0, 0, 1, 2])):
+        taints.append({"key": rng.choice(TAINT_KEYS), "value": rng.choice(["", "x", "y"]),
+                       "effect": rng.choice(["NoSchedule", "PreferNoSchedule", "PreferNoSchedule", "NoExecute"])})
+    if taints:
+        w.taints(taints)
+    imgs = rng.sample(IMAGES, rng.randint(0, 2))
+    if imgs:
+        w.images({n: s for n, s in imgs})
+    return w.obj()
+
+
+def rand_requests(rng):
+    r = {}
+    if rng.random() < 0.8:
+        r["cpu"] = rng.choice(["100m", "250m", "500m", "1", "1500m", "3"])
+    if rng.random() < 0.8:
+        r["memory"] = rng.choice(["128Mi", "500Mi", "1Gi", "3Gi", "7Gi"])
+    if rng.random() < 0.1:
+        r["ephemeral-storage"] = "1Gi"
+    if rng.random() < 0.1:
+        r["example.com/gpu"] = str(rng.randint(1, 2))
+    return r
+
+
+def rand_tolerations(rng):
+    out = []
+    for _ in range(rng.choice([0, 0, 1, 2])):
+        op = rng.choice(["Equal", "Exists"])
+        t = {"key": rng.choice(TAINT_KEYS + [""]) if op == "Exists" else rng.choice(TAINT_KEYS), "operator": op}
+        if op == "Equal":
+            t["value"] = rng.choice(["", "x", "y"])
+        eff = rng.choice(["", "NoSchedule", "PreferNoSchedule", "NoExecute"])
+        if eff:
+            t["effect"] = eff
+        out.append(t)
+    return out
+
+
+def rand_expr(rng, names):
+    k = rng.random()
+    if k < 0.3:
+        return expr("topology.kubernetes.io/zone", rng.choice(["In", "NotIn"]), rng.sample(ZONES, rng.randint(1, 2)))
+    if k < 0.5:
+        return expr("disk", rng.choice(["Exists", "DoesNotExist"]))
+    if k < 0.7:
+        return expr("gen", rng.choice(["Gt", "Lt"]), [str(rng.randint(1, 5))])
+    if k < 0.8:
+        return expr("kubernetes.io/hostname", "In", rng.sample(names, min(3, len(names))))
+    return expr("disk", "In", [rng.choice(["ssd", "hdd", "nvme"])])
+
+
+def rand_pod(rng, k, names, ns="default"):
+    p = PodW(f"p{k}", ns)
+    for _ in range(rng.choice([1, 1, 2])):
+        ports = None
+        if rng.random() < 0.12:
+            ports = [{"containerPort": 8080, "hostPort": rng.choice([80, 443, 8080]),
+                      "protocol": rng.choice(["TCP", "UDP"]), **({"hostIP": "10.0.0.1"} if rng.random() < 0.3 else {})}]
+        img = rng.choice([n for n, _ in IMAGES] + ["registry.example/other:1", ""])
+        p.container(image=img, requests=rand_requests(rng), ports=ports)
+    if rng.random() < 0.1:
+        p.init_req(rand_requests(rng), sidecar=rng.random() < 0.5)
+    if rng.random() < 0.05:
+        p.overhead({"cpu": "50m", "memory": "64Mi"})
+    tol = rand_tolerations(rng)
+    if tol:
+        p.tolerations(tol)
+    if rng.random() < 0.15:
+        p.node_selector({"topology.kubernetes.io/zone": rng.choice(ZONES)})
+    r = rng.random()
+    if r < 0.2:
+        terms = [{"matchExpressions": [rand_expr(rng, names) for _ in range(rng.randint(1, 2))]}
+                 for _ in range(rng.randint(1, 2))]
+        p.node_affinity_required(terms)
+    elif r < 0.25 and names:
+        p.node_affinity_required([{"matchFields": [
+            {"key": "metadata.name", "operator": "In", "values": rng.sample(names, min(len(names), rng.randint(1, 4)))}]}])
+    if rng.random() < 0.25:
+        p.node_affinity_preferred([(rng.randint(1, 100), {"matchExpressions": [rand_expr(rng, names)]})
+                                   for _ in range(rng.randint(1, 3))])
+    if rng.random() < 0.02 and names:
+        p.o["spec"]["nodeName"] = rng.choice(names + ["missing-node"])
+    return p.obj()
+
+
+CONFIGS = [
+    {},
+    {"nodeResourcesFit": {"scoringStrategy": {"type": "MostAllocated"}}},
+    {"nodeResourcesFit": {"scoringStrategy": {
+        "type": "RequestedToCapacityRatio",
+        "resources": [{"name": "cpu", "weight": 2}, {"name": "memory", "weight": 1}, {"name": "example.com/gpu", "weight": 3}],
+        "requestedToCapacityRatio": {"shape": [{"utilization": 0, "score": 10}, {"utilization": 60, "score": 3},
+                                               {"utilization": 100, "score": 0}]}}}},
+    {"nodeResourcesFit": {"scoringStrategy": {"type": "LeastAllocated", "resources": [
+        {"name": "cpu", "weight": 1}, {"name": "memory", "weight": 2}, {"name": "example.com/gpu", "weight": 5}]}},
+     "balancedAllocation": {"resources": [{"name": "cpu", "weight": 1}, {"name": "memory", "weight": 1},
+                                          {"name": "example.com/gpu", "weight": 1}]}},
+    {"nodeAffinity": {"addedAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+            {"matchExpressions": [{"key": "gen", "operator": "Lt", "values": ["6"]}]}]},
+        "preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": 7, "preference": {"matchExpressions": [{"key": "disk", "operator": "In", "values": ["ssd"]}]}}]}}},
+    {"disabledPlugins": ["ImageLocality", "NodeResourcesBalancedAllocation"], "scoreWeights": {"TaintToleration": "1"}},
+]
+
+
+def rand_cluster(seed, n_nodes, n_existing, cfg_index=None):
+    rng = random.Random(seed)
+    cfg = CONFIGS[cfg_index if cfg_index is not None else rng.randrange(len(CONFIGS))]
+    nodes = [rand_node(rng, i) for i in range(n_nodes)]
+    names = [n["metadata"]["name"] for n in nodes]
+    existing = []
+    for k in range(n_existing):
+        p = rand_pod(rng, 100000 + k, names)
+        p["spec"].pop("affinity", None)
+        p["spec"]["nodeName"] = rng.choice(names)
+        existing.append(p)
+    return rng, cfg, nodes, existing, names

@@ -1,0 +1,149 @@
+"""Parity of the HIP path (libksg.so through the C ABI) against the CPU oracle.
+
+Bar: bit-exact -- identical feasible sets, per-node Filter codes/plugins/reasons, per-plugin
+weighted int64 score vectors, TotalScores, chosen node (incl. the heap tie-break), and
+EvaluatedNodes/FeasibleNodes, over pod sequences where each assume lands before the next pod.
+"""
+import random
+
+import pytest
+
+from fuzz_gen import rand_cluster, rand_pod
+from golden_runner import load_cases, run_case
+from oracle_binding import oracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = load_cases()
+
+
+@pytest.fixture(scope="module")
+def native():
+    from ksg.native import Scheduler
+    return Scheduler
+
+
+@pytest.mark.parametrize("name,case", CASES, ids=[c[0] for c in CASES])
+def test_golden_vectors_on_device(native, name, case):
+    errs = run_case(native, case)
+    assert not errs, f"{case['src']}: {errs}"
+
+
+def _pair(native, cfg, nodes, existing):
+    bs = []
+    for make in (native, oracle):
+        b = make(cfg)
+        for n in nodes:
+            b.add_node(n)
+        for p in existing:
+            b.add_pod(p)
+        bs.append(b)
+    assert bs[0].node_names() == bs[1].node_names()
+    return bs
+
+
+def _cmp_cycle(g, o, pod, tag, evaluate=True):
+    hg, ho = g.compile(pod), o.compile(pod)
+    rg, eg = g.schedule_one(hg, assume=True, evaluate=evaluate)
+    ro, eo = o.schedule_one(ho, assume=True, evaluate=evaluate)
+    assert rg.as_tuple() == ro.as_tuple(), f"{tag}: result {rg.as_tuple()} != oracle {ro.as_tuple()}"
+    if evaluate:
+        for k in eo:
+            assert eg[k] == eo[k], f"{tag}: eval[{k}] differs"
+    return hg, ho, rg
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_sequences_match_oracle(native, seed):
+    rng, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=rng_nodes(seed), n_existing=40)
+    g, o = _pair(native, cfg, nodes, existing)
+    for k in range(40):
+        _cmp_cycle(g, o, rand_pod(rng, k, names), f"seed {seed} pod {k}")
+
+
+def rng_nodes(seed):
+    return [7, 60, 130, 257, 300, 600][seed % 6]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_batch_matches_sequential_oracle(native, seed):
+    rng, cfg, nodes, existing, names = rand_cluster(1000 + seed, n_nodes=513, n_existing=100)
+    g, o = _pair(native, cfg, nodes, existing)
+    pods = [rand_pod(rng, k, names) for k in range(150)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"seed {seed} pod {k}"
+
+
+def test_ties_follow_heap_preorder(native):
+    """All nodes identical: every TotalScore ties, so placement is the heap pre-order rule."""
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(1000, 0, 400)
+    g, o = _pair(native, {}, nodes, init)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"pod {k}"
+
+
+def test_scheduling_basic_5k_hetero(native):
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(5000, 1000, 300, hetero=True)
+    g, o = _pair(native, {}, nodes, init)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"pod {k}"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_plugin_entry_points(native, seed):
+    rng, cfg, nodes, existing, names = rand_cluster(2000 + seed, n_nodes=97, n_existing=30)
+    g, o = _pair(native, cfg, nodes, existing)
+    for k in range(25):
+        pod = rand_pod(rng, k, names)
+        hg, ho = g.compile(pod), o.compile(pod)
+        for plugin in ["NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts",
+                       "NodeResourcesFit"]:
+            assert g.run_filter_plugin(hg, plugin) == o.run_filter_plugin(ho, plugin), f"{plugin} pod {k}"
+        for plugin in ["TaintToleration", "NodeAffinity", "NodeResourcesFit", "NodeResourcesBalancedAllocation",
+                       "ImageLocality"]:
+            assert g.run_score_plugin(hg, plugin) == o.run_score_plugin(ho, plugin), f"{plugin} pod {k}"
+
+
+def test_forget_and_cache_events(native):
+    rng, cfg, nodes, existing, names = rand_cluster(77, n_nodes=200, n_existing=50, cfg_index=0)
+    g, o = _pair(native, cfg, nodes, existing)
+    handles = []
+    for k in range(30):
+        hg, ho, _ = _cmp_cycle(g, o, rand_pod(rng, k, names), f"pod {k}")
+        handles.append((hg, ho))
+    for hg, ho in handles[::3]:  # Cache.ForgetPod of a third of the assumed pods
+        g.forget(hg)
+        o.forget(ho)
+    for victim in names[5:40:7]:  # node removals re-order the snapshot
+        g.remove_node(victim)
+        o.remove_node(victim)
+    for p in existing[:10]:
+        g.remove_pod(p["metadata"]["uid"])
+        o.remove_pod(p["metadata"]["uid"])
+    upd = dict(nodes[50])
+    upd["metadata"] = dict(upd["metadata"], labels={"kubernetes.io/hostname": names[50], "disk": "ssd"})
+    g.update_node(upd)
+    o.update_node(upd)
+    for i in range(3):
+        extra = dict(nodes[0])
+        extra["metadata"] = {"name": f"late-{i}", "labels": {"topology.kubernetes.io/zone": "zone-c"}}
+        g.add_node(extra)
+        o.add_node(extra)
+    assert g.node_names() == o.node_names()
+    for k in range(30, 60):
+        _cmp_cycle(g, o, rand_pod(rng, k, names), f"after events pod {k}")
+
+
+def test_empty_cluster_and_unschedulable(native):
+    g, o = _pair(native, {}, [], [])
+    pod = rand_pod(random.Random(1), 0, [])
+    hg, ho = g.compile(pod), o.compile(pod)
+    assert g.schedule_one(hg)[0].as_tuple() == o.schedule_one(ho)[0].as_tuple()
