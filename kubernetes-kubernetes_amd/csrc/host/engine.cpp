@@ -736,7 +736,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (int32_t i = 0; i < N; ++i) {
       const uint32_t w = st[i];
       if (eval->node_code) eval->node_code[i] = (uint8_t)status_code(w);
-      if (eval->node_plugin) eval->node_plugin[i] = status_plugin(w) == 15u ? 255 : (uint8_t)status_plugin(w);
+      if (eval->node_plugin)  // feasible nodes and PreFilterResult exclusions carry no plugin
+        eval->node_plugin[i] = (status_code(w) == 0 || status_plugin(w) == 15u) ? 255 : (uint8_t)status_plugin(w);
       if (eval->node_reasons) eval->node_reasons[i] = status_reasons(w);
       const bool scored = hr[0].feasible > 1 && status_code(w) == 0;
       if (eval->total_scores) eval->total_scores[i] = scored ? tot[i] : 0;
