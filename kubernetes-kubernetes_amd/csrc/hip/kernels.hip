@@ -18,6 +18,7 @@
 // Integer arithmetic is int64 with truncating division as in Go; the two FP64 paths
 // (BalancedAllocation, RequestedToCapacityRatio rounding) are compiled with
 // -ffp-contract=off so no a*b+c is fused (Go/amd64 never fuses).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "../common/desc.h"
@@ -620,9 +621,15 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
 
 // ---- host-side launchers (C++ linkage, called by the host library) ------------------------------
 namespace ksg {
-hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
+// t0/t1 non-null: the events are attached to the dispatch packet itself (hipExtLaunchKernel), so
+// their elapsed time is the kernel's own begin/end -- the same interval rocprofv3 reports.
+hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
+                               hipEvent_t t1) {
   const int nb = (m.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_filter_score, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
+  if (t0)
+    hipExtLaunchKernelGGL(k_filter_score, dim3(nb), dim3(kBlock), 0, s, t0, t1, 0, m, b, pod);
+  else
+    hipLaunchKernelGGL(k_filter_score, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
   return hipGetLastError();
 }
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {

@@ -19,7 +19,8 @@
 
 namespace ksg {
 
-hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0 = nullptr,
+                               hipEvent_t t1 = nullptr);
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
 
 #define HIPCHK(x)                                               \
@@ -671,9 +672,12 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   for (int i = 0; i < n; ++i) {
     if (cp[i].error) continue;
     const bool t = stride > 0 && i % stride == 0;
-    if (t) HIPCHK(hipEventRecord(tev[2 * (size_t)timed], s));
-    HIPCHK(launch_filter_score(m, bv, i, s));
-    if (t) HIPCHK(hipEventRecord(tev[2 * (size_t)timed++ + 1], s));
+    if (t) {
+      HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1]));
+      timed++;
+    } else {
+      HIPCHK(launch_filter_score(m, bv, i, s));
+    }
     HIPCHK(launch_select(m, bv, i, s));
     bytes += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[i].blob.data()));
     launches++;

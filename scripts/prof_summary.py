@@ -1,0 +1,72 @@
+"""Summarise rocprofv3 rocpd databases (gpurun_out/prof/*) into committed text/JSON under profiles/.
+
+  python scripts/prof_summary.py <tag> [nodes]
+writes profiles/<tag>_kernel_stats.txt (per-kernel calls / total / average duration, the
+`--kernel-trace --stats` summary), profiles/<tag>_pmc.txt (FETCH_SIZE / WRITE_SIZE per kernel),
+and profiles/traffic_k_filter_score.json (HBM bytes per k_filter_score launch for bench.py).
+"""
+import json
+import os
+import sqlite3
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "gpurun_out", "prof")
+
+
+def short(name):
+    return name.split("(")[0]
+
+
+def main():
+    tag = sys.argv[1]
+    nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    c = sqlite3.connect(os.path.join(PROF, "trace", "run_results.db"))
+    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    lines = [f"# rocprofv3 --kernel-trace --stats -- python3 bench.py (tag {tag})",
+             f"{'kernel':60s} {'calls':>8s} {'total_us':>12s} {'avg_us':>9s} {'pct':>6s}"]
+    for n, calls, tot, avg, pct in rows:  # top_kernels is in us; kernels.duration is ns
+        lines.append(f"{short(n):60s} {calls:8d} {tot:12.1f} {avg:9.3f} {pct:6.2f}")
+    # per-dispatch durations of the roofline kernel
+    d = [r[0] for r in c.execute("select duration from kernels where name like '%k_filter_score%'")]
+    if d:
+        d.sort()
+        lines.append(f"k_filter_score dispatch duration us: median {d[len(d) // 2] / 1e3:.3f} "
+                     f"p10 {d[len(d) // 10] / 1e3:.3f} p90 {d[9 * len(d) // 10] / 1e3:.3f}")
+    open(os.path.join(out, f"{tag}_kernel_stats.txt"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+    per = {}
+    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+        p = os.path.join(PROF, sub, "run_results.db")
+        if not os.path.exists(p):
+            continue
+        cc = sqlite3.connect(p)
+        for name, val in cc.execute("select kernel_name, value from counters_collection where counter_name=?",
+                                    (counter,)):
+            per.setdefault(short(name), {}).setdefault(counter, []).append(val)
+    pl = [f"# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB per dispatch (tag {tag})",
+          "# gfx950: FETCH_SIZE under-reports wide streaming reads by 2x (MI355X_MICROARCH.md HBM section);",
+          "# the access widths here are 4-8 B/lane (uncalibrated) -- both raw and x2 are listed."]
+    traffic = None
+    for k, v in sorted(per.items()):
+        f = v.get("FETCH_SIZE", [])
+        w = v.get("WRITE_SIZE", [])
+        fa = sum(f) / len(f) if f else 0.0
+        wa = sum(w) / len(w) if w else 0.0
+        pl.append(f"{k:60s} dispatches {len(f):6d} FETCH_KiB {fa:10.2f} (x2 {2 * fa:10.2f}) WRITE_KiB {wa:10.2f}")
+        if k.endswith("k_filter_score"):
+            traffic = {"nodes": nodes, "fetch_kib_raw": fa, "write_kib": wa,
+                       "bytes_per_launch": round((fa + wa) * 1024.0, 1),
+                       "bytes_per_launch_fetch_x2": round((2 * fa + wa) * 1024.0, 1),
+                       "note": "FETCH_SIZE+WRITE_SIZE per k_filter_score dispatch, separate PMC passes"}
+    open(os.path.join(out, f"{tag}_pmc.txt"), "w").write("\n".join(pl) + "\n")
+    print("\n".join(pl))
+    if traffic:
+        json.dump(traffic, open(os.path.join(out, "traffic_k_filter_score.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
