@@ -171,17 +171,15 @@ int ksg_forget(ksg_ctx *ctx, int32_t handle);
  * codes[N] / reasons[N] receive each node's Filter status. */
 int ksg_run_filter_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, int32_t *prefilter_code,
                           uint8_t *codes, uint32_t *reasons);
-/* The ScorePlugin + ScoreExtensions contract of one plugin with every snapshot node as
- * the node list: PreScore (interface.go:598-606), Score per node (:619-628) into raw[N],
- * NormalizeScore (:609-614) into normalized[N] (unweighted).  *status_code gets the
- * PreScore status (KSG_CODE_SKIP: not scored) or a Score error. */
-int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, int32_t *status_code,
-                         int64_t *raw, int64_t *normalized);
+/* The ScorePlugin + ScoreExtensions contract of one plugin: PreScore (interface.go:598-606)
+ * over the node list, Score per listed node (:619-628) into raw[N], NormalizeScore
+ * (:609-614) over the list into normalized[N] (unweighted).  The list is the snapshot nodes
+ * with nodes[i] != 0 (nodes == NULL: every node) -- the feasible list prioritizeNodes would
+ * pass; unlisted entries stay 0.  *status_code gets the PreScore status (KSG_CODE_SKIP: not
+ * scored) or a Score error. */
+int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uint8_t *nodes,
+                         int32_t *status_code, int64_t *raw, int64_t *normalized);
 
-/* ---- measurement hooks -------------------------------------------------------------- */
-/* Average device time (ms) per launch of the dominant kernel over the last
- * ksg_schedule_batch, measured with HIP events on the launch stream, and the
- * algorithmic bytes one launch of it moves (roofline accounting). */
 int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
                                 double *bytes_per_launch, int32_t *launches);
 

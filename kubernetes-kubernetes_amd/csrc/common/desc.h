@@ -88,6 +88,7 @@ enum DescFlags : uint32_t {
   DF_HAS_PREF_NA = 1u << 10,       // pod preferred node affinity present
   DF_HAS_ADDED_PREF = 1u << 11,    // NodeAffinityArgs.addedAffinity.preferred present
   DF_SCORE_ERROR = 1u << 12,       // PreScore/Score returns Error: the cycle fails iff scoring runs (F > 1)
+  DF_NODE_LIST = 1u << 13,         // plugin-eval mode: only the nodes in the bitmap at node_list_off are listed
 };
 
 struct PodDesc {
@@ -112,7 +113,7 @@ struct PodDesc {
   int32_t n_rtcr, rtcr_off;        // int64 pairs (utilization, score) for the broken-linear shape
   int32_t n_bal_res, bal_res_off;  // ScoreRes (pod_req = Requested, useRequested=true)
   // TaintToleration: bitmaps over distinct taint ids
-  int32_t n_taint_words, untol_ns_off, intol_pns_off, pad1;
+  int32_t n_taint_words, untol_ns_off, intol_pns_off, node_list_off;
   // NodeAffinity
   SelProg na_required;   // pod required terms (OR)
   SelProg na_selector;   // nodeSelector as a single AND term

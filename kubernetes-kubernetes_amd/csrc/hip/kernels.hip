@@ -347,7 +347,11 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
     }
     if (st == 0) {
       uint32_t f = run_filters(m, base, d, i, &raw_taint);
-      st = (d.flags & DF_ALL_FEASIBLE) ? 0u : f;
+      if (d.flags & DF_ALL_FEASIBLE)  // plugin-eval mode: the caller's node list is the feasible list
+        f = ((d.flags & DF_NODE_LIST) && !bit(base, d.node_list_off, (uint32_t)i, (m.n + 31) / 32))
+                ? pack_status(C_UU, 15u, 0u)
+                : 0u;
+      st = f;
     }
   }
   const bool feas = valid && st == 0;

@@ -211,13 +211,13 @@ int ksg_run_filter_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t*
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
-    return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::FILTER_ONE, plugin, prefilter_code, codes,
-                                                 reasons, nullptr, nullptr));
+    return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::FILTER_ONE, plugin, nullptr, prefilter_code,
+                                                 codes, reasons, nullptr, nullptr));
   })
 }
 
-int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t* status_code, int64_t* raw,
-                         int64_t* normalized) {
+int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, const uint8_t* nodes, int32_t* status_code,
+                         int64_t* raw, int64_t* normalized) {
   if (!ctx || !status_code) return KSG_EINVAL;
   if (plugin != KSG_PLUGIN_TAINT_TOLERATION && plugin != KSG_PLUGIN_NODE_AFFINITY &&
       plugin != KSG_PLUGIN_NODE_RESOURCES_FIT && plugin != KSG_PLUGIN_POD_TOPOLOGY_SPREAD &&
@@ -227,7 +227,7 @@ int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t* 
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
-    return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::SCORE_ONE, plugin, status_code, nullptr,
+    return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::SCORE_ONE, plugin, nodes, status_code, nullptr,
                                                  nullptr, raw, normalized));
   })
 }

@@ -137,7 +137,8 @@ struct SelBuilder {
 static bool empty_term(const NSTerm& t) { return t.exprs.empty() && t.fields.empty(); }
 
 // ---- compile ---------------------------------------------------------------------------------------
-int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out) {
+int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
+                    const uint8_t* node_list) {
   const Config& cfg = c->cfg;
   const int32_t N = (int32_t)c->order().size();
   Blob B;
@@ -490,6 +491,13 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     smask &= 1u << plugin;
     for (int i = 0; i < kNumPlugins; ++i) D.weight[i] = 1;
     D.flags |= DF_ALL_FEASIBLE;
+    if (node_list) {
+      std::vector<uint32_t> bm((size_t)(N + 31) / 32, 0);
+      for (int32_t i = 0; i < N; ++i)
+        if (node_list[i]) bm[(size_t)i / 32] |= 1u << (i % 32);
+      D.flags |= DF_NODE_LIST;
+      D.node_list_off = B.put(bm);
+    }
     eval = true;
   }
   D.filter_mask = fmask;
@@ -753,8 +761,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   return KSG_OK;
 }
 
-int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, int32_t* code, uint8_t* codes, uint32_t* reasons,
-                       int64_t* raw, int64_t* norm) {
+int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* nodes, int32_t* code, uint8_t* codes,
+                       uint32_t* reasons, int64_t* raw, int64_t* norm) {
   const int32_t N = (int32_t)c->order().size();
   *code = KSG_CODE_SUCCESS;
   for (int32_t i = 0; i < N; ++i) {
@@ -764,7 +772,7 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, int32_t* code, u
     if (norm) norm[i] = 0;
   }
   CompiledPod cp;
-  int rc = compile(p, mode, plugin, false, true, &cp);
+  int rc = compile(p, mode, plugin, false, true, &cp, nodes);
   if (rc) return rc;
   const PodDesc& D = *reinterpret_cast<const PodDesc*>(cp.blob.data());
   if (mode == FILTER_ONE) {
@@ -815,7 +823,7 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, int32_t* code, u
     if (mode == FILTER_ONE) {
       if (codes) codes[i] = (uint8_t)status_code(st[i]);
       if (reasons) reasons[i] = status_reasons(st[i]);
-    } else {
+    } else if (!nodes || nodes[i]) {
       if (raw) raw[i] = rv[i];
       if (norm) norm[i] = nv[i];
     }

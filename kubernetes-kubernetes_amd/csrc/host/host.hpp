@@ -300,12 +300,13 @@ class Engine {
 
   enum Mode { CYCLE, FILTER_ONE, SCORE_ONE };
   // compile `p` for the current cluster; rot_start from Cluster::next_start
-  int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out);
+  int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
+              const uint8_t* node_list = nullptr);
   // run a batch of cycles (device-resident, sequential semantics)
   int run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                 ksg_result* results, ksg_eval_out* eval);
-  int run_plugin(const PodSpec& p, Mode mode, int plugin, int32_t* code, uint8_t* codes, uint32_t* reasons,
-                 int64_t* raw, int64_t* norm);
+  int run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* nodes, int32_t* code, uint8_t* codes,
+                 uint32_t* reasons, int64_t* raw, int64_t* norm);
 
   // measurement: average k_filter_score duration (sampled with events when cfg.timing_stride > 0,
   // else the batch's kernel time / launches) and its algorithmic bytes per launch

@@ -100,7 +100,8 @@ def _sig(lib, prefix):
     d("schedule_batch", C.c_int, vp, C.POINTER(i32), i32, u32, C.POINTER(Result))
     d("forget", C.c_int, vp, i32)
     d("run_filter_plugin", C.c_int, vp, i32, i32, C.POINTER(i32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint32))
-    d("run_score_plugin", C.c_int, vp, i32, i32, C.POINTER(i32), C.POINTER(C.c_int64), C.POINTER(C.c_int64))
+    d("run_score_plugin", C.c_int, vp, i32, i32, C.POINTER(C.c_uint8), C.POINTER(i32), C.POINTER(C.c_int64),
+      C.POINTER(C.c_int64))
     return f
 
 
@@ -243,12 +244,18 @@ class Backend:
         self._chk(self.f["run_filter_plugin"](self.ctx, handle, pid, C.byref(pc), codes, reas), "run_filter_plugin")
         return pc.value, list(codes[:n]), list(reas[:n])
 
-    def run_score_plugin(self, handle, plugin):
-        """PreScore + Score + NormalizeScore of one plugin -> (status, raw, normalized)."""
+    def run_score_plugin(self, handle, plugin, nodes=None):
+        """PreScore + Score + NormalizeScore of one plugin over a node list (default: every
+        node; else an iterable of snapshot indices) -> (status, raw, normalized)."""
         pid = PLUGIN_ID[plugin] if isinstance(plugin, str) else plugin
         n = self.num_nodes()
         st = C.c_int32()
         raw = (C.c_int64 * max(n, 1))()
         nrm = (C.c_int64 * max(n, 1))()
-        self._chk(self.f["run_score_plugin"](self.ctx, handle, pid, C.byref(st), raw, nrm), "run_score_plugin")
+        mask = None
+        if nodes is not None:
+            mask = (C.c_uint8 * max(n, 1))()
+            for i in nodes:
+                mask[i] = 1
+        self._chk(self.f["run_score_plugin"](self.ctx, handle, pid, mask, C.byref(st), raw, nrm), "run_score_plugin")
         return st.value, list(raw[:n]), list(nrm[:n])

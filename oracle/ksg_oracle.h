@@ -38,8 +38,8 @@ int ksgo_schedule_batch(ksgo_ctx *ctx, const int32_t *handles, int32_t n, uint32
 int ksgo_forget(ksgo_ctx *ctx, int32_t handle);
 int ksgo_run_filter_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, int32_t *prefilter_code,
                            uint8_t *codes, uint32_t *reasons);
-int ksgo_run_score_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, int32_t *status_code,
-                          int64_t *raw, int64_t *normalized);
+int ksgo_run_score_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, const uint8_t *nodes,
+                          int32_t *status_code, int64_t *raw, int64_t *normalized);
 
 /* Go math.Log restatement (exposed so tests can compare it with libm). */
 double ksgo_go_log(double x);

@@ -1618,8 +1618,8 @@ int ksgo_run_filter_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, int32_t*
   return KSG_OK;
 }
 
-int ksgo_run_score_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, int32_t* status_code, int64_t* raw,
-                          int64_t* normalized) {
+int ksgo_run_score_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, const uint8_t* nodes, int32_t* status_code,
+                          int64_t* raw, int64_t* normalized) {
   auto it = c->queue.find(handle);
   if (it == c->queue.end()) return KSG_ENOTFOUND;
   bool isScore = false;
@@ -1629,22 +1629,27 @@ int ksgo_run_score_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, int32_t* 
   const int N = (int)c->list.size();
   for (int i = 0; i < N; ++i) { raw[i] = 0; normalized[i] = 0; }
   *status_code = KSG_CODE_SUCCESS;
+  // the node list prioritizeNodes would pass (feasible nodes in snapshot order)
+  std::vector<NodeInfoO*> list;
+  std::vector<int> idx;
+  for (int i = 0; i < N; ++i)
+    if (!nodes || nodes[i]) { list.push_back(c->list[i]); idx.push_back(i); }
   bool hasPre = false;
   for (int p : kPreScoreOrder) hasPre |= p == plugin;
   if (hasPre) {
-    Status st = prescore_plugin(*cy, plugin, c->list);
+    Status st = prescore_plugin(*cy, plugin, list);
     if (!st.ok()) { *status_code = st.code; return KSG_OK; }
   }
-  std::vector<int64_t> sc(N);
-  for (int i = 0; i < N; ++i) {
+  std::vector<int64_t> sc(list.size());
+  for (size_t i = 0; i < list.size(); ++i) {
     int code;
-    sc[i] = score_node(*cy, plugin, c->list[i], &code);
-    raw[i] = sc[i];
+    sc[i] = score_node(*cy, plugin, list[i], &code);
+    raw[idx[i]] = sc[i];
     if (code != KSG_CODE_SUCCESS) *status_code = code;
   }
   if (*status_code != KSG_CODE_SUCCESS) return KSG_OK;
-  normalize_scores(*cy, plugin, sc, c->list);
-  for (int i = 0; i < N; ++i) normalized[i] = sc[i];
+  normalize_scores(*cy, plugin, sc, list);
+  for (size_t i = 0; i < list.size(); ++i) normalized[idx[i]] = sc[i];
   return KSG_OK;
 }
 

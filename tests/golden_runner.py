@@ -44,14 +44,16 @@ def run_case(make_backend, case):
     errs = []
     e = case["expect"]
     if case["kind"] == "score":
-        st, raw, nrm = b.run_score_plugin(h, case["plugin"])
+        scored = case.get("scored")
+        idx = [names.index(n) for n in scored] if scored is not None else None
+        st, raw, nrm = b.run_score_plugin(h, case["plugin"], idx)
         if st != e["status"]:
             errs.append(f"status {st} != {e['status']}")
         if e["status"] in (0,):
             got = nrm if "normalized" in e else raw
             want = e.get("normalized", e.get("raw"))
             by = dict(zip(names, got))
-            gl = [by[n] for n in want_names]
+            gl = [by[n] for n in (scored if scored is not None else want_names)]
             if gl != want:
                 errs.append(f"scores {gl} != {want}")
     elif case["kind"] == "filter":
