@@ -23,6 +23,8 @@ constexpr int kNumPlugins = 10;  // KSG_NUM_PLUGINS
 constexpr int kBlock = 256;      // threads per block of the per-node kernels (4 waves)
 constexpr int kMaxScalar = 16;   // interned extended/scalar resource columns
 constexpr int kPortSlots = 8;    // used-port slots per node (grown by the host if exceeded)
+constexpr int kMaxCons = 8;      // PodTopologySpread constraints per kind per pod
+constexpr int kMaxPodTerms = 8;  // InterPodAffinity terms per kind per pod
 
 // ---- selector programs (labels.Selector / nodeaffinity terms compiled to slots) ----------
 enum SelOp : int32_t {
@@ -74,6 +76,55 @@ struct ImageTerm {  // one image id the pod references that exists in the cluste
   int64_t scaled;   // scaledImageScore: int64(float64(size) * numNodes/totalNodes) (image_locality.go:141-148)
 };
 
+// ---- metav1.LabelSelector programs (labels.Selector over pod / namespace labels) -----------
+// int32 stream: [nothing, nreq, {key, op, nvals, value ids...} x nreq]; label sets are sorted
+// uint64 (key id << 32 | value id) arrays.  apimachinery/pkg/labels/selector.go:247-294,419-426
+enum LSelOp : int32_t { LS_IN = 0, LS_NOTIN = 1, LS_EXISTS = 2, LS_DNE = 3 };
+
+// PodTopologySpread constraint as compiled by the host (podtopologyspread/common.go:87-128)
+struct PtsCons {
+  int32_t slot;         // label column of the topology key
+  int32_t max_skew;
+  int32_t min_domains;
+  int32_t self_match;   // the incoming pod matches its own selector (filtering.go:338-341)
+  int32_t aff_honor;    // NodeAffinityPolicy == Honor
+  int32_t taint_honor;  // NodeTaintsPolicy == Honor
+  int32_t hostname;     // score: kubernetes.io/hostname counts per node (scoring.go:207-214)
+  int32_t sel;          // selector program offset (int32 units, pod selector pool)
+  int32_t hist_base;    // arena entries: per-domain (or per-node) matching pod counts
+  int32_t pres_base;    // arena entries: domain presence flags
+  int32_t nvals;        // domains (label values of the key)
+  int32_t pad;
+};
+// an InterPodAffinity term of the incoming pod (interpodaffinity/filtering.go:246-283, scoring.go:81-125)
+struct IpaTerm {
+  int32_t slot;         // label column of the topology key
+  int32_t weight;
+  int32_t hist_base;    // arena base of this topology key's counts
+  int32_t sel;          // selector program offset
+  int32_t ns_off, ns_cnt;  // namespace ids (pod selector pool, int32 units)
+  int32_t all_ns;       // namespaceSelector matches the empty label set
+  int32_t pad;
+};
+struct KeyHist { int32_t slot; int32_t base; };
+// an existing pod's affinity term (device term table, kube-scheduler/framework/types.go:380-396)
+enum TermKind : int32_t { T_DEAD = -1, T_REQ_AFF = 0, T_REQ_ANTI = 1, T_PREF_AFF = 2, T_PREF_ANTI = 3 };
+struct DTerm {
+  int32_t owner;        // pod-table slot
+  int32_t kind;         // TermKind
+  int32_t weight;
+  int32_t key;          // topology key id
+  int32_t sel;          // term pool offsets (int32 units)
+  int32_t nssel;
+  int32_t ns_off, ns_cnt;
+};
+enum IpaFlags : uint32_t {
+  IPA_SELF_ALL = 1u << 0,   // the incoming pod matches all its own required affinity terms
+  IPA_PREF = 1u << 1,       // incoming preferred terms are processed against every pod (hasConstraints)
+  IPA_EXIST_FILTER = 1u << 2,  // existing required anti-affinity terms are checked (Filter active)
+  IPA_EXIST_SCORE = 1u << 3,   // existing pods' terms contribute to the score (PreScore active)
+};
+
 enum DescFlags : uint32_t {
   DF_TOLERATES_UNSCHED = 1u << 0,  // pod tolerates node.kubernetes.io/unschedulable:NoSchedule
   DF_HAS_SELECTOR = 1u << 1,       // RequiredNodeAffinity.labelSelector (pod.spec.nodeSelector)
@@ -89,6 +140,7 @@ enum DescFlags : uint32_t {
   DF_HAS_ADDED_PREF = 1u << 11,    // NodeAffinityArgs.addedAffinity.preferred present
   DF_SCORE_ERROR = 1u << 12,       // PreScore/Score returns Error: the cycle fails iff scoring runs (F > 1)
   DF_NODE_LIST = 1u << 13,         // plugin-eval mode: only the nodes in the bitmap at node_list_off are listed
+  DF_AGGREGATE = 1u << 14,         // PTS/IPA counts: k_aggregate runs before the node pass
 };
 
 struct PodDesc {
@@ -130,6 +182,20 @@ struct PodDesc {
   // AssumePod payload: PodInfo.CalculateResource (framework/types.go:1035-1076)
   int64_t a_cpu, a_mem, a_eph, a_nz_cpu, a_nz_mem;
   int32_t n_a_scalar, a_scalar_off;  // ScalarReq
+  // ---- PodTopologySpread / InterPodAffinity (pod-table aggregation)
+  int32_t ns_id, slot;               // incoming pod's namespace id; reserved pod-table slot (assume)
+  int32_t n_lbl, lbl_off;            // incoming pod labels (uint64 pairs, sorted)
+  int32_t n_nslbl, nslbl_off;        // labels of the incoming pod's namespace
+  int32_t sel_pool_off;              // int32 pool: selector programs + namespace id lists
+  int32_t n_ptsf, ptsf_off, n_ptss, ptss_off;  // PtsCons (DoNotSchedule / ScheduleAnyway)
+  uint32_t ipa_flags;
+  int32_t hard_weight;
+  int32_t n_raff, raff_off, n_ranti, ranti_off, n_paff, paff_off, n_panti, panti_off;  // IpaTerm
+  int32_t n_keytab, keytab_off;      // int32 [key id][2]: existing-anti / topology-score arena base, -1 none
+  int32_t n_exkeys, exkeys_off;      // KeyHist: existing anti-affinity counts (Filter)
+  int32_t n_topokeys, topokeys_off;  // KeyHist: topology scores (Score)
+  int32_t arena_words;               // arena entries this pod uses (zeroed again by k_select)
+  int32_t pad2;
 };
 
 // Per-pod device result (ScheduleResult + diagnostics), written by the select kernel.
@@ -140,6 +206,8 @@ struct DevResult {
   int32_t evaluated;
   int64_t total;
   uint64_t key;       // winning packed key (debug)
+  uint32_t ipa_any;   // PodStats::ipa_any (PreFilter / PreScore Skip decisions taken on the device)
+  uint32_t pad[3];
 };
 
 // Per-pod scratch (zeroed by the host before each batch).
@@ -149,7 +217,13 @@ struct PodStats {
   unsigned long long min_raw[kNumPlugins];  // enc_i64, init enc_i64(INT64_MAX) for min
   uint32_t done;            // arrival ticket of the select kernel's blocks
   uint32_t feasible;
-  uint32_t pad[2];
+  uint32_t done_agg;        // arrival ticket of k_aggregate's blocks
+  uint32_t ipa_any;         // bit0 affinity counts, bit1 anti counts, bit2 existing anti, bit3 topology score
+  long long pts_min[kMaxCons];        // critical-path minimum per DoNotSchedule constraint
+  uint32_t pts_ndom[kMaxCons];        // domains per DoNotSchedule constraint
+  uint32_t pts_distinct[kMaxCons];    // feasible, non-ignored domains per ScheduleAnyway constraint
+  uint32_t pts_nonignored;            // feasible nodes carrying every ScheduleAnyway key
+  uint32_t pad[3];
 };
 
 // Node mirror view passed to kernels by value.
@@ -177,6 +251,20 @@ struct MirrorView {
   const int64_t* label_num;       // [slots][cap] parsed integer value
   const uint8_t* label_num_ok;    // [slots][cap]
   uint32_t* ports;                // [cap][kPortSlots] port id, 0xffffffff empty
+  // pod table (NodeInfo.Pods of every node, flattened; slots indexed by the host)
+  int32_t pods_hw;                // slots in use (high-water mark)
+  int32_t n_terms;                // term table entries in use
+  int32_t* pod_node;              // [slot] snapshot index, -1 free / not assumed
+  const int32_t* pod_ns;          // [slot] namespace id
+  const uint32_t* pod_flags;      // [slot] bit0 terminating
+  const uint32_t* pod_lbl_off;    // [slot] offset into lbl_pool
+  const uint32_t* pod_lbl_cnt;    // [slot]
+  const unsigned long long* lbl_pool;  // (key << 32 | value) sorted per pod
+  const DTerm* terms;             // existing pods' affinity terms
+  const int32_t* term_pool;       // their selector programs / namespace id lists
+  const double* log_tab;          // go math.Log(k) for k in [0, log_n)
+  int32_t log_n;
+  int32_t pad_;
 };
 
 // Everything a per-pod kernel launch needs besides the mirror.
@@ -192,6 +280,7 @@ struct BatchView {
   int64_t* raw;           // [kNumPlugins][cap] raw scores of normalising plugins (+ eval mode: all)
   int64_t* out_scores;    // eval mode: [kNumPlugins][cap] weighted normalised scores
   int64_t* out_total;     // eval mode: [cap]
+  unsigned long long* arena;  // PTS/IPA histograms (zero between pods)
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)
@@ -220,6 +309,47 @@ KSG_HD inline uint32_t preorder_pos(uint32_t key) {  // inverse of preorder_key
 KSG_HD inline unsigned long long pack_best(int64_t total, uint32_t p) {
   return ((unsigned long long)total << kPreBits) | (unsigned long long)((1u << kPreBits) - 1u - preorder_key(p));
 }
+// ---- label sets and selector programs (shared by the host compiler and the kernels) -------
+KSG_HD inline int32_t lset_find(const unsigned long long* set, int32_t n, uint32_t key) {
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(set[mid] >> 32) < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < n && (uint32_t)(set[lo] >> 32) == key) ? (int32_t)(uint32_t)set[lo] : -1;
+}
+// labels.Selector.Matches over a sorted label set (selector.go:247-294, 419-426)
+KSG_HD inline bool lsel_match(const int32_t* prog, const unsigned long long* set, int32_t n) {
+  if (prog[0]) return false;  // nothingSelector
+  const int32_t nreq = prog[1];
+  const int32_t* r = prog + 2;
+  for (int32_t q = 0; q < nreq; ++q) {
+    const int32_t key = r[0], op = r[1], nv = r[2];
+    const int32_t v = lset_find(set, n, (uint32_t)key);
+    bool ok;
+    if (op == LS_IN || op == LS_NOTIN) {
+      bool has = false;
+      if (v >= 0)
+        for (int32_t k = 0; k < nv; ++k) has |= r[3 + k] == v;
+      ok = op == LS_IN ? (v >= 0 && has) : (v < 0 || !has);
+    } else if (op == LS_EXISTS) {
+      ok = v >= 0;
+    } else {
+      ok = v < 0;
+    }
+    if (!ok) return false;
+    r += 3 + nv;
+  }
+  return true;
+}
+KSG_HD inline bool lsel_empty(const int32_t* prog) { return prog[0] == 0 && prog[1] == 0; }
+KSG_HD inline bool id_in(const int32_t* ids, int32_t n, int32_t x) {
+  for (int32_t k = 0; k < n; ++k)
+    if (ids[k] == x) return true;
+  return false;
+}
+
 // order-preserving int64 <-> uint64 (so signed min/max use unsigned atomics)
 KSG_HD inline unsigned long long enc_i64(int64_t v) { return (unsigned long long)v ^ 0x8000000000000000ull; }
 KSG_HD inline int64_t dec_i64(unsigned long long u) { return (int64_t)(u ^ 0x8000000000000000ull); }

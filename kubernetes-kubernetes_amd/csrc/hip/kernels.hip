@@ -21,86 +21,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
-#include "../common/desc.h"
+#include "device.hpp"
 
 namespace ksg {
-
-#define KSG_R_UNSCHEDULABLE (1u << 0)
-#define KSG_R_NODE_NAME (1u << 1)
-#define KSG_R_TAINT (1u << 2)
-#define KSG_R_NODE_AFFINITY_POD (1u << 3)
-#define KSG_R_NODE_AFFINITY_ENFORCED (1u << 4)
-#define KSG_R_NODE_PORTS (1u << 5)
-#define KSG_R_TOO_MANY_PODS (1u << 6)
-#define KSG_R_INSUFFICIENT_CPU (1u << 7)
-#define KSG_R_INSUFFICIENT_MEMORY (1u << 8)
-#define KSG_R_INSUFFICIENT_EPHEMERAL (1u << 9)
-#define KSG_R_INSUFFICIENT_SCALAR (1u << 10)
-#define KSG_R_PREFILTER (1u << 16)
-
-enum : int { P_UNSCHED = 0, P_NODENAME = 1, P_TAINT = 2, P_NA = 3, P_PORTS = 4, P_FIT = 5, P_PTS = 6,
-             P_IPA = 7, P_BAL = 8, P_IMG = 9 };
-enum : uint32_t { C_OK = 0, C_ERROR = 1, C_UNSCHED = 2, C_UU = 3 };
-
-template <typename T>
-__device__ __forceinline__ const T* at(const uint8_t* base, int32_t off) {
-  return reinterpret_cast<const T*>(base + off);
-}
-__device__ __forceinline__ bool bit(const uint8_t* base, int32_t off, uint32_t id, int32_t nwords) {
-  uint32_t w = id >> 5;
-  if ((int32_t)w >= nwords) return false;
-  return (at<uint32_t>(base, off)[w] >> (id & 31u)) & 1u;
-}
-
-// ---- selector programs ---------------------------------------------------------------------
-// labels.Requirement.Matches (apimachinery/pkg/labels/selector.go:247-294) against the
-// node's label columns; metadata.name field requirements (nodeaffinity.go:190-201).
-__device__ bool req_match(const MirrorView& m, const uint8_t* base, const PodDesc& d, const SelReq& r, int i) {
-  const size_t col = (size_t)r.slot * (size_t)m.cap + (size_t)i;
-  switch (r.op) {
-    case SEL_IN:
-    case SEL_NOTIN: {
-      int32_t v = m.labels[col];
-      if (v < 0) return r.op == SEL_NOTIN;
-      const int32_t* vals = at<int32_t>(base, d.vals_off) + r.vals_off;
-      bool has = false;
-      for (int k = 0; k < r.nvals; ++k) has |= vals[k] == v;
-      return r.op == SEL_IN ? has : !has;
-    }
-    case SEL_EXISTS: return m.labels[col] >= 0;
-    case SEL_DNE: return m.labels[col] < 0;
-    case SEL_GT:
-    case SEL_LT: {
-      if (m.labels[col] < 0 || !m.label_num_ok[col]) return false;
-      int64_t x = m.label_num[col];
-      return r.op == SEL_GT ? x > r.num : x < r.num;
-    }
-    case SEL_NODE_EQ: return (int64_t)i == r.num;
-    case SEL_NODE_NE: return (int64_t)i != r.num;
-    case SEL_TRUE: return true;
-    default: return false;
-  }
-}
-__device__ bool term_match(const MirrorView& m, const uint8_t* base, const PodDesc& d, const SelTerm& t, int i) {
-  if (t.parse_err) return false;
-  const SelReq* reqs = at<SelReq>(base, d.req_off) + t.req_off;
-  for (int k = 0; k < t.nreq; ++k)
-    if (!req_match(m, base, d, reqs[k], i)) return false;
-  return true;
-}
-__device__ bool prog_any(const MirrorView& m, const uint8_t* base, const PodDesc& d, SelProg p, int i) {
-  const SelTerm* terms = at<SelTerm>(base, p.term_off);
-  for (int k = 0; k < p.nterm; ++k)
-    if (term_match(m, base, d, terms[k], i)) return true;
-  return false;
-}
-__device__ int64_t prog_weight(const MirrorView& m, const uint8_t* base, const PodDesc& d, SelProg p, int i) {
-  const SelTerm* terms = at<SelTerm>(base, p.term_off);
-  int64_t s = 0;
-  for (int k = 0; k < p.nterm; ++k)
-    if (term_match(m, base, d, terms[k], i)) s += terms[k].weight;
-  return s;
-}
 
 // ---- resources --------------------------------------------------------------------------------
 __device__ __forceinline__ void node_res(const MirrorView& m, const ScoreRes& r, int i, bool useRequested,
@@ -231,7 +154,7 @@ __device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const P
 // RunFilterPlugins order wins.  *raw_taint gets the PreferNoSchedule count while the taint
 // list is in registers.
 __device__ uint32_t run_filters(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i,
-                                int64_t* raw_taint) {
+                                int64_t* raw_taint, const PodStats* ps, const unsigned long long* arena) {
   const uint32_t fm = d.filter_mask;
   // NodeUnschedulable (node_unschedulable.go:125-143)
   if ((fm >> P_UNSCHED) & 1u)
@@ -301,6 +224,46 @@ __device__ uint32_t run_filters(const MirrorView& m, const uint8_t* base, const 
     }
     if (reasons) return pack_status(unresolvable ? C_UU : C_UNSCHED, P_FIT, reasons);
   }
+  // PodTopologySpread (podtopologyspread/filtering.go:314-359) against k_aggregate's counts
+  if ((fm >> P_PTS) & 1u) {
+    const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
+    for (int32_t c = 0; c < d.n_ptsf; ++c) {
+      const int32_t v = node_label(m, cs[c].slot, i);
+      if (v < 0) return pack_status(C_UU, P_PTS, KSG_R_PTS_MISSING_LABEL);
+      const int64_t minMatch = (int64_t)ps->pts_ndom[c] < (int64_t)cs[c].min_domains ? 0 : ps->pts_min[c];
+      const int64_t matchNum = (int64_t)arena[cs[c].hist_base + v];
+      if (matchNum + cs[c].self_match - minMatch > (int64_t)cs[c].max_skew)
+        return pack_status(C_UNSCHED, P_PTS, KSG_R_PTS_SKEW);
+    }
+  }
+  // InterPodAffinity (interpodaffinity/filtering.go:364-444)
+  if ((fm >> P_IPA) & 1u) {
+    const IpaTerm* ra = at<IpaTerm>(base, d.raff_off);
+    bool podsExist = true;  // satisfyPodAffinity :394-420
+    for (int32_t k = 0; k < d.n_raff; ++k) {
+      const int32_t v = node_label(m, ra[k].slot, i);
+      if (v < 0) return pack_status(C_UU, P_IPA, KSG_R_IPA_AFFINITY);
+      if ((int64_t)arena[ra[k].hist_base + v] <= 0) podsExist = false;
+    }
+    if (!podsExist && !((ps->ipa_any & 1u) == 0 && (d.ipa_flags & IPA_SELF_ALL)))
+      return pack_status(C_UU, P_IPA, KSG_R_IPA_AFFINITY);
+    if (ps->ipa_any & 2u) {  // satisfyPodAntiAffinity :379-391
+      const IpaTerm* rn = at<IpaTerm>(base, d.ranti_off);
+      for (int32_t k = 0; k < d.n_ranti; ++k) {
+        const int32_t v = node_label(m, rn[k].slot, i);
+        if (v >= 0 && (int64_t)arena[rn[k].hist_base + v] > 0)
+          return pack_status(C_UNSCHED, P_IPA, KSG_R_IPA_ANTI_AFFINITY);
+      }
+    }
+    if (ps->ipa_any & 4u) {  // satisfyExistingPodsAntiAffinity :364-376
+      const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
+      for (int32_t k = 0; k < d.n_exkeys; ++k) {
+        const int32_t v = node_label(m, ek[k].slot, i);
+        if (v >= 0 && (int64_t)arena[ek[k].base + v] > 0)
+          return pack_status(C_UNSCHED, P_IPA, KSG_R_IPA_EXISTING_ANTI);
+      }
+    }
+  }
   return 0;
 }
 
@@ -346,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
       st = in ? 0u : pack_status(C_UU, 15u, KSG_R_PREFILTER);
     }
     if (st == 0) {
-      uint32_t f = run_filters(m, base, d, i, &raw_taint);
+      uint32_t f = run_filters(m, base, d, i, &raw_taint, b.stats + pod, b.arena);
       if (d.flags & DF_ALL_FEASIBLE)  // plugin-eval mode: the caller's node list is the feasible list
         f = ((d.flags & DF_NODE_LIST) && !bit(base, d.node_list_off, (uint32_t)i, (m.n + 31) / 32))
                 ? pack_status(C_UU, 15u, 0u)
@@ -385,34 +348,79 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
       b.raw[P_BAL * cap + i] = rawv[P_BAL];
       b.raw[P_IMG * cap + i] = rawv[P_IMG];
     }
+    if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.Score (interpodaffinity/scoring.go:240-255)
+      const KeyHist* tk = at<KeyHist>(base, d.topokeys_off);
+      int64_t s = 0;
+      for (int32_t k = 0; k < d.n_topokeys; ++k) {
+        const int32_t v = node_label(m, tk[k].slot, i);
+        if (v >= 0) s += (int64_t)b.arena[tk[k].base + v];
+      }
+      rawv[P_IPA] = s;
+      b.raw[P_IPA * cap + i] = s;
+    }
+  }
+  // PodTopologySpread PreScore over the feasible list: ignored nodes and per-constraint domain
+  // counts feed the normalising weights (podtopologyspread/scoring.go:61-115)
+  bool pts_counted = false;
+  if (feas && ((sm >> P_PTS) & 1u)) {
+    const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+    bool ignored = false;
+    for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
+    if (!ignored) {
+      pts_counted = true;
+      PodStats* ps = b.stats + pod;
+      for (int32_t c = 0; c < d.n_ptss; ++c) {
+        if (cs[c].hostname) continue;
+        unsigned long long* pp = b.arena + cs[c].pres_base + node_label(m, cs[c].slot, i);
+        if (*pp == 0ull && atomicExch(pp, 1ull) == 0ull) atomicAdd(&ps->pts_distinct[c], 1u);
+      }
+    }
   }
 
-  // per-block feasible count + per-plugin max of the normalising plugins' raw scores
-  __shared__ uint32_t s_cnt[kBlock / 64];
-  __shared__ unsigned long long s_max[2][kBlock / 64];
+  // per-block feasible count + per-plugin max (and IPA min) of the normalising plugins' raw scores
+  __shared__ uint32_t s_cnt[kBlock / 64], s_pts[kBlock / 64];
+  __shared__ unsigned long long s_max[3][kBlock / 64], s_min[kBlock / 64];
   unsigned long long mt = feas ? enc_i64(rawv[P_TAINT]) : 0ull;
   unsigned long long mn = feas ? enc_i64(rawv[P_NA]) : 0ull;
+  unsigned long long mi = feas ? enc_i64(rawv[P_IPA]) : 0ull;
+  unsigned long long ni = feas ? enc_i64(rawv[P_IPA]) : ~0ull;
   mt = wave_max_u64(mt);
   mn = wave_max_u64(mn);
+  if ((sm >> P_IPA) & 1u) {
+    mi = wave_max_u64(mi);
+    ni = wave_min_u64(ni);
+  }
+  const unsigned long long pball = __ballot(pts_counted);
   if (lane == 0) {
     s_cnt[wave] = (uint32_t)__popcll(ballot);
+    s_pts[wave] = (uint32_t)__popcll(pball);
     s_max[0][wave] = mt;
     s_max[1][wave] = mn;
+    s_max[2][wave] = mi;
+    s_min[wave] = ni;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    unsigned long long a = 0, bb = 0;
+    uint32_t c = 0, pc = 0;
+    unsigned long long a = 0, bb = 0, ia = 0, in = ~0ull;
     for (int w = 0; w < kBlock / 64; ++w) {
       c += s_cnt[w];
+      pc += s_pts[w];
       a = s_max[0][w] > a ? s_max[0][w] : a;
       bb = s_max[1][w] > bb ? s_max[1][w] : bb;
+      ia = s_max[2][w] > ia ? s_max[2][w] : ia;
+      in = s_min[w] < in ? s_min[w] : in;
     }
     b.blk_cnt[blockIdx.x] = c;
     if (c) {
       PodStats* ps = b.stats + pod;
       if ((sm >> P_TAINT) & 1u) atomicMax(&ps->max_raw[P_TAINT], a);
       if ((sm >> P_NA) & 1u) atomicMax(&ps->max_raw[P_NA], bb);
+      if ((sm >> P_IPA) & 1u) {
+        atomicMax(&ps->max_raw[P_IPA], ia);
+        atomicMin(&ps->min_raw[P_IPA], in);
+      }
+      if (pc) atomicAdd(&ps->pts_nonignored, pc);
     }
   }
 }
@@ -505,6 +513,26 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
         total += v * d.weight[P_NA];
         if (eval) b.out_scores[P_NA * cap + i] = v * d.weight[P_NA];
       }
+      if ((sm >> P_PTS) & 1u) {  // PodTopologySpread.NormalizeScore (podtopologyspread/scoring.go:229-268)
+        const int64_t mx = dec_i64(ps->max_raw[P_PTS]), mn = dec_i64(ps->min_raw[P_PTS]);
+        const int64_t r = b.raw[P_PTS * cap + i];
+        const int64_t v = r == -1 ? 0 : (mx == 0 ? 100 : 100 * (mx + mn - r) / mx);
+        total += v * d.weight[P_PTS];
+        if (eval) b.out_scores[P_PTS * cap + i] = v * d.weight[P_PTS];
+      }
+      if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.NormalizeScore (interpodaffinity/scoring.go:258-290)
+        const int64_t r = b.raw[P_IPA * cap + i];
+        int64_t v = r;
+        if (ps->ipa_any & 8u) {
+          const int64_t mx = dec_i64(ps->max_raw[P_IPA]), mn = dec_i64(ps->min_raw[P_IPA]);
+          const int64_t diff = mx - mn;
+          double f = 0.0;
+          if (diff > 0) f = 100.0 * ((double)(r - mn) / (double)diff);
+          v = (int64_t)f;
+        }
+        total += v * d.weight[P_IPA];
+        if (eval) b.out_scores[P_IPA * cap + i] = v * d.weight[P_IPA];
+      }
       if (eval) {
         if ((sm >> P_FIT) & 1u) b.out_scores[P_FIT * cap + i] = b.raw[P_FIT * cap + i] * d.weight[P_FIT];
         if ((sm >> P_BAL) & 1u) b.out_scores[P_BAL * cap + i] = b.raw[P_BAL * cap + i] * d.weight[P_BAL];
@@ -514,6 +542,8 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
     if (eval) b.out_total[i] = total;
     key = pack_best(total, pos);
   }
+  // the PTS/IPA histograms of this pod are dead now: zero them for the next pod on the stream
+  for (int w = blockIdx.x * kBlock + threadIdx.x; w < d.arena_words; w += nblocks * kBlock) b.arena[w] = 0ull;
   key = wave_max_u64(key);
   __shared__ unsigned long long s_key[kBlock / 64];
   if (lane == 0) s_key[wave] = key;
@@ -588,6 +618,7 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
     r.total = F > 0 ? (int64_t)(best >> kPreBits) : 0;
     r.key = best;
     r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
+    r.ipa_any = ps->ipa_any;
     if (d.flags & DF_PREFILTER_REJECT) r.status = (int32_t)C_UNSCHED;
     if ((d.flags & DF_SCORE_ERROR) && F > 1) {  // prioritizeNodes error (schedule_one.go:600-603)
       r.status = (int32_t)C_ERROR;
@@ -607,6 +638,7 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
       for (int k = 0; k < d.n_a_scalar; ++k) m.scalar_req[(size_t)sr[k].slot * cap + j] += sr[k].qty;
       const uint32_t* pp = at<uint32_t>(base, d.pod_ports_off);
       uint32_t* slots = m.ports + (size_t)j * kPortSlots;
+      if (d.slot >= 0) m.pod_node[d.slot] = j;  // the pod joins NodeInfo.Pods (pod table)
       for (int k = 0; k < d.n_pod_ports; ++k) {  // HostPortInfo.Add: set semantics
         bool present = false;
         int empty = -1;

@@ -34,6 +34,8 @@ Cluster::Cluster(const Config& c) : cfg(c) {
 
 Cluster::~Cluster() {
   free_all();
+  for (auto& b : pt_dev_)
+    if (b.p) (void)hipFree(b.p);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -229,7 +231,13 @@ int Cluster::remove_node(const std::string& name) {
   if (it == nodes_.end()) { err = "unknown node " + name; return KSG_ENOTFOUND; }
   remove_images(it->second->spec);
   tree_remove(it->second->spec);
-  for (auto& uid : it->second->pods) pods.erase(uid);
+  for (auto& uid : it->second->pods) {
+    auto pt = pods.find(uid);
+    if (pt == pods.end()) continue;
+    pods_with_affinity -= pt->second.with_affinity ? 1 : 0;
+    pod_table_drop(pt->second.slot);
+    pods.erase(pt);
+  }
   nodes_.erase(it);
   layout_dirty = true;
   return KSG_OK;
@@ -252,7 +260,7 @@ void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo
   }
 }
 
-int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done) {
+int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done, int32_t slot) {
   const std::string uid = uid_override.empty() ? p.uid : uid_override;
   if (p.node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
   if (pods.count(uid)) { err = "pod " + uid + " exists"; return KSG_EEXIST; }
@@ -273,8 +281,15 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   for (auto& c : p.containers) take(c);
   apply_pod(*r, bp, +1);
   r->pods.push_back(uid);
-  pods.emplace(uid, std::move(bp));
   order();
+  const int32_t idx = layout_dirty ? -1 : index_of(r->spec.name);  // re-derived on relayout
+  if (slot >= 0) {
+    pt_node[slot] = idx;  // the device table already holds it (k_select's assume)
+    bp.slot = slot;
+  } else {
+    bp.slot = pod_table_put(p, idx);
+  }
+  pods.emplace(uid, std::move(bp));
   if (!layout_dirty && !device_done) return upload_node_dynamic(index_of(r->spec.name));
   return KSG_OK;
 }
@@ -284,6 +299,7 @@ int Cluster::remove_pod(const std::string& uid) {
   if (it == pods.end()) { err = "unknown pod " + uid; return KSG_ENOTFOUND; }
   NodeRec* r = node(it->second.node);
   pods_with_affinity -= it->second.with_affinity ? 1 : 0;
+  pod_table_drop(it->second.slot);
   if (r) {
     apply_pod(*r, it->second, -1);
     auto& v = r->pods;
@@ -311,7 +327,7 @@ int Cluster::remove_pod(const std::string& uid) {
 
 int Cluster::ensure_mirror() {
   order();
-  if (!layout_dirty) return KSG_OK;
+  if (!layout_dirty) return upload_pod_table();
   HIPCHK(hipStreamSynchronize(stream));
   free_all();
   const int32_t n = (int32_t)order_.size();
@@ -410,7 +426,11 @@ int Cluster::ensure_mirror() {
       int rc = upload_label_column(k);
       if (rc) return rc;
     }
-  return KSG_OK;
+  // snapshot indices moved: re-derive every pod's node index in the pod table
+  for (auto& kv : pods)
+    if (kv.second.slot >= 0) pt_node[kv.second.slot] = index_of(kv.second.node);
+  pods_dirty = true;
+  return upload_pod_table();
 }
 
 int Cluster::upload_label_column(int32_t key) {

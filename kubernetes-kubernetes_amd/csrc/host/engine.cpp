@@ -22,6 +22,8 @@ namespace ksg {
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0 = nullptr,
                                hipEvent_t t1 = nullptr);
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, const PodDesc& d, hipStream_t s);
+hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
 
 #define HIPCHK(x)                                               \
   do {                                                          \
@@ -150,20 +152,11 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   *out = CompiledPod{};
   out->num_all = N;
 
-  // features not yet on the device path: refuse loudly rather than fall back to the CPU
-  const bool pts_on = mode == CYCLE ? cfg.enabled[P_PTS] : plugin == P_PTS;
-  const bool ipa_on = mode == CYCLE ? cfg.enabled[P_IPA] : plugin == P_IPA;
-  const bool has_ipa = p.has_pod_affinity || p.has_pod_anti || c->pods_with_affinity > 0;
-  if ((pts_on && (!p.spreads.empty() || mode != CYCLE)) || (ipa_on && (has_ipa || mode != CYCLE))) {
-    c->err = "PodTopologySpread / InterPodAffinity are not on the device path yet";
-    return KSG_ENOTSUP;
-  }
-
   // ---- which plugins run (PreFilter/PreScore Skip, framework.go:960-962,1324-1327)
   // fmask/smask start as "would run" and lose the plugins whose PreFilter/PreScore Skips;
   // the profile's enabled set is applied per mode at the end.
-  uint32_t fmask = (1u << (P_FIT + 1)) - 1u, smask = 0;
-  for (int q : {P_TAINT, P_NA, P_FIT, P_BAL, P_IMG}) smask |= 1u << q;
+  uint32_t fmask = (1u << (P_IPA + 1)) - 1u, smask = 0;
+  for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) smask |= 1u << q;
 
   SelBuilder sb{c};
   // NodeAffinity PreFilter (node_affinity.go:148-198)
@@ -434,6 +427,12 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     D.img_count = (int64_t)names.size();
   }
 
+  // PodTopologySpread / InterPodAffinity: per-domain aggregation programs
+  {
+    const int rc = compile_topology(p, mode, plugin, N, &B, &D, &fmask, &smask, out);
+    if (rc) return rc;
+  }
+
   // selector program pools
   D.req_off = B.put(sb.reqs);
   D.vals_off = B.put(sb.vals);
@@ -460,13 +459,19 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
       return KSG_ENOTSUP;
     }
     if (score_err) D.flags |= DF_SCORE_ERROR;
-    if (conflict) {  // PreFilter UnschedulableAndUnresolvable: every node gets it
+    if (conflict || (!out->prefilter_error && out->ipa_parse_error)) {
+      // PreFilter UnschedulableAndUnresolvable (NodeAffinity conflict, InterPodAffinity parse):
+      // every node gets it (schedule_one.go:635-648)
+      const int32_t pl = conflict ? P_NA : P_IPA;
       D.flags |= DF_PREFILTER_REJECT;
       D.prefilter_code = 3;
-      D.prefilter_plugin = P_NA;
+      D.prefilter_plugin = pl;
       out->prefilter_reject = true;
       out->prefilter_code = 3;
-      out->prefilter_plugin = P_NA;
+      out->prefilter_plugin = pl;
+      out->prefilter_error = false;
+    } else if (out->prefilter_error) {
+      // PodTopologySpread PreFilter Error: the cycle errors before filtering (run_batch)
     } else if (restricted) {
       D.flags |= DF_SUBSET;
       D.subset_cnt = (int32_t)subset.size();
@@ -478,6 +483,11 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     }
   } else if (mode == FILTER_ONE) {
     fmask &= 1u << plugin;
+    if ((plugin == P_PTS && out->prefilter_error) || (plugin == P_IPA && out->ipa_parse_error)) {
+      out->prefilter_reject = true;
+      out->prefilter_code = plugin == P_PTS ? 1 : 3;
+      out->prefilter_plugin = plugin;
+    }
     if (plugin == P_NA && conflict) {
       out->prefilter_reject = true;
       out->prefilter_code = 3;
@@ -486,7 +496,8 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     smask = 0;
     eval = true;
   } else {  // SCORE_ONE
-    if ((plugin == P_NA && pref_err) || (plugin == P_FIT && cfg.fit_res.empty())) out->error = true;
+    if ((plugin == P_NA && pref_err) || (plugin == P_FIT && cfg.fit_res.empty()) || out->topo_score_error)
+      out->error = true;
     fmask = 0;
     smask &= 1u << plugin;
     for (int i = 0; i < kNumPlugins; ++i) D.weight[i] = 1;
@@ -503,10 +514,256 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   D.filter_mask = fmask;
   D.score_mask = smask;
   out->score_mask = smask;
-  if (assume) D.flags |= DF_ASSUME;
+  if (assume) {
+    D.flags |= DF_ASSUME;
+    D.slot = c->pod_table_put(p, -1);  // live once k_select's assume writes its node index
+    out->slot = D.slot;
+  }
   if (eval) D.flags |= DF_EVAL_OUT;
   B.finish();
   out->blob = std::move(B.b);
+  return KSG_OK;
+}
+
+// ---- PodTopologySpread / InterPodAffinity compilation ----------------------------------------------------
+// The O(pod) half of calPreFilterState / initPreScoreState (podtopologyspread/filtering.go:237-311,
+// scoring.go:61-115) and of the InterPodAffinity PreFilter/PreScore (interpodaffinity/filtering.go:286-321,
+// scoring.go:128-221): constraints and terms become selector programs over interned labels, and every
+// per-domain map of the reference becomes an arena histogram indexed by the topology key's value id.
+int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* Bp, PodDesc* Dp,
+                             uint32_t* fmask, uint32_t* smask, CompiledPod* out) {
+  Blob& B = *Bp;
+  PodDesc& D = *Dp;
+  const Config& cfg = c->cfg;
+  // the plugins this evaluation actually runs (profile in CYCLE mode, the one plugin otherwise)
+  uint32_t* const fmask_caller = fmask;
+  uint32_t* const smask_caller = smask;
+  uint32_t fm = *fmask, sm = *smask;
+  if (mode == CYCLE) {
+    for (int q = 0; q < kNumPlugins; ++q)
+      if (!cfg.enabled[q]) { fm &= ~(1u << q); sm &= ~(1u << q); }
+  } else if (mode == FILTER_ONE) {
+    fm &= 1u << plugin;
+    sm = 0;
+  } else {
+    fm = 0;
+    sm &= 1u << plugin;
+  }
+  const uint32_t fm_in = fm, sm_in = sm;
+  fmask = &fm;
+  smask = &sm;
+  std::vector<int32_t> pool;  // selector programs + namespace id lists
+  int32_t arena = 0;
+  auto alloc = [&](int32_t n) {
+    const int32_t b = arena;
+    arena += n;
+    return b;
+  };
+  auto nvals = [&](int32_t key) { return (int32_t)c->keys[key].values.strs.size(); };
+  auto slot_of = [&](int32_t key) -> int32_t {
+    c->ensure_label_slot(key);
+    return c->keys[key].slot;
+  };
+  const std::vector<unsigned long long> podset = c->label_set(p.labels);
+  D.ns_id = c->ns_id(p.ns);
+  D.slot = -1;
+
+  // ---------------- PodTopologySpread (filterTopologySpreadConstraints, common.go:87-128)
+  auto build_cons = [&](const char* action, std::vector<PtsCons>* cons, bool score) -> bool {
+    for (auto& sp : p.spreads) {
+      if (sp.when != action) continue;
+      StrMap ml;
+      for (auto& k : sp.match_label_keys)  // MatchLabelKeysInPodTopologySpread (on by default)
+        for (auto& kv : p.labels)
+          if (kv.first == k) ml.push_back(kv);
+      std::sort(ml.begin(), ml.end());
+      PtsCons pc{};
+      if (!c->compile_lsel(sp.sel, sp.sel.present ? &ml : nullptr, &pool, &pc.sel)) return false;
+      const int32_t key = c->key_id(sp.key);
+      pc.slot = slot_of(key);
+      pc.max_skew = sp.max_skew;
+      pc.min_domains = sp.min_domains;
+      pc.self_match = lsel_match(pool.data() + pc.sel, podset.data(), (int32_t)podset.size()) ? 1 : 0;
+      pc.aff_honor = sp.aff_honor ? 1 : 0;
+      pc.taint_honor = sp.taint_honor ? 1 : 0;
+      pc.hostname = (score && sp.key == "kubernetes.io/hostname") ? 1 : 0;
+      pc.nvals = pc.hostname ? N : nvals(key);
+      pc.hist_base = alloc(pc.nvals);
+      pc.pres_base = pc.hostname ? -1 : alloc(pc.nvals);
+      cons->push_back(pc);
+    }
+    return true;
+  };
+  std::vector<PtsCons> ptsf, ptss;
+  if (*fmask & (1u << P_PTS)) {
+    if (!build_cons("DoNotSchedule", &ptsf, false)) {  // PreFilter Error (filtering.go:146-148)
+      out->prefilter_error = true;
+      ptsf.clear();
+    }
+    if (ptsf.empty()) *fmask &= ~(1u << P_PTS);  // PreFilter Skip: no hard constraints
+  }
+  if (*smask & (1u << P_PTS)) {
+    if (!build_cons("ScheduleAnyway", &ptss, true)) {
+      out->topo_score_error = true;  // PreScore Error (scoring.go:132-134)
+      D.flags |= DF_SCORE_ERROR;
+      ptss.clear();
+    }
+    if (ptss.empty() || N == 0) *smask &= ~(1u << P_PTS);
+  }
+  if (ptsf.size() > (size_t)kMaxCons || ptss.size() > (size_t)kMaxCons) {
+    c->err = "more topology spread constraints than the device path supports";
+    return KSG_ENOTSUP;
+  }
+
+  // ---------------- InterPodAffinity (framework.NewPodInfo for the incoming pod)
+  const bool ipa_f = (*fmask >> P_IPA) & 1u, ipa_s = (*smask >> P_IPA) & 1u;
+  std::vector<IpaTerm> raff, ranti, paff, panti;
+  std::map<int32_t, int32_t> aff_base, anti_base, topo_base, exanti_base;
+  bool parse_ok = true;
+  auto own_terms = [&](const std::vector<PATerm>& in, std::vector<IpaTerm>* o, std::map<int32_t, int32_t>* bases,
+                       bool pref) {
+    for (auto& t : in) {
+      IpaTerm it{};
+      it.weight = t.weight;
+      int32_t nssel;
+      if (!c->compile_lsel(t.sel, nullptr, &pool, &it.sel) || !c->compile_lsel(t.ns_sel, nullptr, &pool, &nssel)) {
+        parse_ok = false;
+        return;
+      }
+      static const unsigned long long kNone = 0;
+      it.all_ns = lsel_match(pool.data() + nssel, &kNone, 0) ? 1 : 0;
+      // namespaces (types.go:422-448) merged with the namespaces the selector matches
+      // (mergeAffinityTermNamespacesIfNotEmpty, interpodaffinity/plugin.go:134-147)
+      std::vector<int32_t> ns;
+      if (t.namespaces.empty() && !t.ns_sel.present) ns.push_back(c->ns_id(p.ns));
+      else
+        for (auto& n : t.namespaces) ns.push_back(c->ns_id(n));
+      if (!lsel_empty(pool.data() + nssel))
+        for (auto& kv : c->namespaces) {
+          const auto nl = c->label_set(kv.second.labels);
+          if (lsel_match(pool.data() + nssel, nl.data(), (int32_t)nl.size())) ns.push_back(c->ns_id(kv.first));
+        }
+      it.ns_off = (int32_t)pool.size();
+      it.ns_cnt = (int32_t)ns.size();
+      pool.insert(pool.end(), ns.begin(), ns.end());
+      const int32_t key = c->key_id(t.topo);
+      it.slot = slot_of(key);
+      auto b = bases->find(key);
+      if (b == bases->end()) b = bases->emplace(key, alloc(nvals(key))).first;
+      it.hist_base = b->second;
+      (void)pref;
+      o->push_back(it);
+    }
+  };
+  const bool hasConstraints =
+      (p.has_pod_affinity && !p.aff_pref.empty()) || (p.has_pod_anti && !p.anti_pref.empty());  // scoring.go:148-150
+  if (ipa_f || ipa_s) {
+    std::vector<IpaTerm> tmp;
+    std::map<int32_t, int32_t> scratch;
+    // parse check of every category first (NewPodInfo fails as a whole)
+    if (p.has_pod_affinity) own_terms(p.aff_req, &raff, &aff_base, false);
+    if (p.has_pod_anti) own_terms(p.anti_req, &ranti, &anti_base, false);
+    if (p.has_pod_affinity) own_terms(p.aff_pref, &paff, &topo_base, true);
+    if (p.has_pod_anti) own_terms(p.anti_pref, &panti, &topo_base, true);
+    if (!parse_ok) {
+      raff.clear(); ranti.clear(); paff.clear(); panti.clear();
+      if (ipa_f) out->ipa_parse_error = true;  // PreFilter UnschedulableAndUnresolvable (filtering.go:294-296)
+      if (ipa_s) {                             // PreScore Error (scoring.go:176-179)
+        D.flags |= DF_SCORE_ERROR;
+        out->topo_score_error = true;
+      }
+    }
+    if (raff.size() > (size_t)kMaxPodTerms || ranti.size() > (size_t)kMaxPodTerms ||
+        paff.size() > (size_t)kMaxPodTerms || panti.size() > (size_t)kMaxPodTerms) {
+      c->err = "more pod (anti-)affinity terms than the device path supports";
+      return KSG_ENOTSUP;
+    }
+    out->ipa_own_req = !raff.empty() || !ranti.empty();
+    bool self_all = !raff.empty();
+    for (auto& t : raff)
+      self_all = self_all && (t.all_ns || id_in(pool.data() + t.ns_off, t.ns_cnt, D.ns_id)) &&
+                 lsel_match(pool.data() + t.sel, podset.data(), (int32_t)podset.size());
+    if (self_all) D.ipa_flags |= IPA_SELF_ALL;
+    if (!ipa_f) { raff.clear(); ranti.clear(); }
+    if (ipa_f && parse_ok && !c->exanti_keys.empty()) {
+      D.ipa_flags |= IPA_EXIST_FILTER;
+      for (auto& kv : c->exanti_keys) exanti_base[kv.first] = alloc(nvals(kv.first));
+    }
+    // PreScore: IgnorePreferredTermsOfExistingPods && !hasConstraints -> Skip (scoring.go:152-156)
+    if (ipa_s && cfg.ignore_pref_existing && !hasConstraints) *smask &= ~(1u << P_IPA);
+    if ((*smask >> P_IPA) & 1u) {
+      if (hasConstraints && parse_ok) D.ipa_flags |= IPA_PREF;
+      else { paff.clear(); panti.clear(); }
+      std::set<int32_t> ekeys;
+      if (cfg.hard_weight > 0)
+        for (auto& kv : c->score_keys_req) ekeys.insert(kv.first);
+      for (auto& kv : c->score_keys_pref) ekeys.insert(kv.first);
+      if (!ekeys.empty() && parse_ok) D.ipa_flags |= IPA_EXIST_SCORE;
+      for (int32_t k : ekeys)
+        if (!topo_base.count(k)) topo_base[k] = alloc(nvals(k));
+    } else {
+      paff.clear();
+      panti.clear();
+    }
+  }
+  D.hard_weight = cfg.hard_weight;
+
+  // key table for the existing-term pass: {label slot, existing-anti base, topology-score base}
+  std::vector<int32_t> keytab;
+  if (!exanti_base.empty() || ((D.ipa_flags & IPA_EXIST_SCORE) != 0)) {
+    const int32_t nk = (int32_t)c->label_keys.strs.size();
+    keytab.assign((size_t)nk * 3, -1);
+    for (auto& kv : exanti_base) {
+      keytab[(size_t)kv.first * 3] = slot_of(kv.first);
+      keytab[(size_t)kv.first * 3 + 1] = kv.second;
+    }
+    for (auto& kv : topo_base) {
+      keytab[(size_t)kv.first * 3] = slot_of(kv.first);
+      keytab[(size_t)kv.first * 3 + 2] = kv.second;
+    }
+    D.n_keytab = nk;
+  }
+  std::vector<KeyHist> exkeys, topokeys;
+  for (auto& kv : exanti_base) exkeys.push_back({c->keys[kv.first].slot, kv.second});
+  for (auto& kv : topo_base) topokeys.push_back({c->keys[kv.first].slot, kv.second});
+
+  const bool agg = !ptsf.empty() || !ptss.empty() || !raff.empty() || !ranti.empty() || !exkeys.empty() ||
+                   ((*smask >> P_IPA) & 1u);
+  if (agg) D.flags |= DF_AGGREGATE;
+  D.n_lbl = (int32_t)podset.size();
+  D.lbl_off = B.put(podset);
+  {
+    std::vector<unsigned long long> nsl;
+    auto it = c->namespaces.find(p.ns);  // GetNamespaceLabelsSnapshot (interpodaffinity/plugin.go:150-159)
+    if (it != c->namespaces.end()) nsl = c->label_set(it->second.labels);
+    D.n_nslbl = (int32_t)nsl.size();
+    D.nslbl_off = B.put(nsl);
+  }
+  D.sel_pool_off = B.put(pool);
+  D.n_ptsf = (int32_t)ptsf.size();
+  D.ptsf_off = B.put(ptsf);
+  D.n_ptss = (int32_t)ptss.size();
+  D.ptss_off = B.put(ptss);
+  D.n_raff = (int32_t)raff.size();
+  D.raff_off = B.put(raff);
+  D.n_ranti = (int32_t)ranti.size();
+  D.ranti_off = B.put(ranti);
+  D.n_paff = (int32_t)paff.size();
+  D.paff_off = B.put(paff);
+  D.n_panti = (int32_t)panti.size();
+  D.panti_off = B.put(panti);
+  D.keytab_off = B.put(keytab);
+  D.n_exkeys = (int32_t)exkeys.size();
+  D.exkeys_off = B.put(exkeys);
+  D.n_topokeys = (int32_t)topokeys.size();
+  D.topokeys_off = B.put(topokeys);
+  D.arena_words = arena;
+  out->arena_words = arena;
+  // Skips decided here propagate to the caller's masks (PTS without constraints, IPA ignore rule)
+  for (int q : {P_PTS, P_IPA}) {
+    if (((fm_in >> q) & 1u) && !((fm >> q) & 1u)) *fmask_caller &= ~(1u << q);
+    if (((sm_in >> q) & 1u) && !((sm >> q) & 1u)) *smask_caller &= ~(1u << q);
+  }
   return KSG_OK;
 }
 
@@ -548,7 +805,7 @@ double Engine::algo_bytes(const PodDesc& d) const {
 Engine::~Engine() {
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total})
+                    &d_total, &d_arena})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -566,7 +823,7 @@ int Engine::ensure(DevBuf& b, size_t bytes) {
   return KSG_OK;
 }
 
-int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval) {
+int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena_words) {
   const size_t cap = (size_t)c->view.cap;
   const size_t nb = cap / kBlock + 1;
   int rc;
@@ -582,6 +839,11 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval) {
   if (eval) {
     if ((rc = ensure(d_out, cap * 8 * kNumPlugins))) return rc;
     if ((rc = ensure(d_total, cap * 8))) return rc;
+  }
+  if (d_arena.bytes < (size_t)arena_words * 8 + 8) {
+    const size_t old = d_arena.bytes;
+    if ((rc = ensure(d_arena, (size_t)arena_words * 8 + 8))) return rc;
+    if (d_arena.bytes != old) HIPCHK(hipMemsetAsync(d_arena.p, 0, d_arena.bytes, c->stream));
   }
   const size_t need = desc_bytes + (size_t)pods * (4 + sizeof(PodStats) + sizeof(DevResult)) + 256;
   if (h_pinned_bytes < need) {
@@ -609,6 +871,7 @@ BatchView Engine::bview(int pods) {
   b.raw = (int64_t*)d_raw.p;
   b.out_scores = (int64_t*)d_out.p;
   b.out_total = (int64_t*)d_total.p;
+  b.arena = (unsigned long long*)d_arena.p;
   return b;
 }
 
@@ -627,8 +890,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   int64_t start = c->next_start;
   for (int i = 0; i < n; ++i) {
     int rc = compile(*pods[i], CYCLE, -1, assume, eval != nullptr, &cp[i]);
-    if (rc) { c->next_start = start; return rc; }
-    if (!cp[i].prefilter_reject) {
+    if (rc) {
+      c->next_start = start;
+      for (int j = 0; j < i; ++j) c->pod_table_drop(cp[j].slot);
+      return rc;
+    }
+    if (cp[i].prefilter_error) cp[i].error = true;  // PreFilter Error: status Error, no launch
+    if (!cp[i].prefilter_reject && !cp[i].prefilter_error) {
       // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
       const int64_t N = (int64_t)c->order().size();
       c->next_start = (c->next_start + cp[i].num_all) % N;
@@ -638,8 +906,12 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (rc) return rc;
   // ---- stage descriptors + stats in pinned memory, one H2D
   size_t desc_bytes = 0;
-  for (auto& x : cp) desc_bytes += x.blob.size();
-  if ((rc = ensure_scratch(desc_bytes, n, eval != nullptr))) return rc;
+  int32_t arena_words = 0;
+  for (auto& x : cp) {
+    desc_bytes += x.blob.size();
+    arena_words = std::max(arena_words, x.arena_words);
+  }
+  if ((rc = ensure_scratch(desc_bytes, n, eval != nullptr, arena_words))) return rc;
   uint8_t* hp = (uint8_t*)h_pinned;
   std::vector<uint32_t> offs(n);
   size_t o = 0;
@@ -679,6 +951,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   double bytes = 0;
   for (int i = 0; i < n; ++i) {
     if (cp[i].error) continue;
+    const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
+    if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));
     const bool t = stride > 0 && i % stride == 0;
     if (t) {
       HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1]));
@@ -686,6 +960,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     } else {
       HIPCHK(launch_filter_score(m, bv, i, s));
     }
+    if (hd.score_mask & (1u << P_PTS)) HIPCHK(launch_pts_score(m, bv, i, s));
     HIPCHK(launch_select(m, bv, i, s));
     bytes += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[i].blob.data()));
     launches++;
@@ -722,7 +997,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // ---- results + host shadow of the device-side assumes
   for (int i = 0; i < n; ++i) {
     ksg_result& r = results[i];
-    if (cp[i].error) { r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0}; continue; }
+    if (cp[i].error) {
+      r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
+      c->pod_table_drop(cp[i].slot);
+      continue;
+    }
     const DevResult& d = hr[i];
     r.status = d.status;
     r.node_index = d.node;
@@ -735,16 +1014,20 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       ap.node_name = c->order()[r.node_index];
       static uint64_t seq = 0;
       std::string uid = ap.uid + "#a" + std::to_string(++seq);
-      int rc2 = c->add_pod(ap, uid, /*device_done=*/true);
+      int rc2 = c->add_pod(ap, uid, /*device_done=*/true, cp[i].slot);
       if (rc2) return rc2;
       assumed[handles.empty() ? -1 : handles[i]] = uid;
+    } else {
+      c->pod_table_drop(cp[i].slot);  // not placed: the reserved pod-table slot never went live
     }
   }
   if (eval) {
     const int32_t N = m.n;
     eval->prefilter_code = cp[0].prefilter_reject ? cp[0].prefilter_code : 0;
     eval->prefilter_plugin = cp[0].prefilter_reject ? cp[0].prefilter_plugin : 255;
-    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject) ? cp[0].score_mask : 0;
+    uint32_t smask = cp[0].score_mask;
+    if (!(hr[0].ipa_any & 8u)) smask &= ~(1u << P_IPA);  // InterPodAffinity PreScore Skip (scoring.go:207-209)
+    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject) ? smask : 0;
     for (int32_t i = 0; i < N; ++i) {
       const uint32_t w = st[i];
       if (eval->node_code) eval->node_code[i] = (uint8_t)status_code(w);
@@ -776,8 +1059,7 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
   if (rc) return rc;
   const PodDesc& D = *reinterpret_cast<const PodDesc*>(cp.blob.data());
   if (mode == FILTER_ONE) {
-    // the plugin's own PreFilter first (framework.go:934-995): Skip, or a rejection every node gets
-    if (!(D.filter_mask & (1u << plugin))) { *code = KSG_CODE_SKIP; return KSG_OK; }
+    // the plugin's own PreFilter first (framework.go:934-995): a rejection every node gets, or Skip
     if (cp.prefilter_reject) {
       *code = cp.prefilter_code;
       for (int32_t i = 0; i < N; ++i) {
@@ -786,12 +1068,13 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
       }
       return KSG_OK;
     }
+    if (!(D.filter_mask & (1u << plugin))) { *code = KSG_CODE_SKIP; return KSG_OK; }
   } else {
     if (cp.error) { *code = KSG_CODE_ERROR; return KSG_OK; }
     if (!(D.score_mask & (1u << plugin))) { *code = KSG_CODE_SKIP; return KSG_OK; }
   }
   if ((rc = c->ensure_mirror())) return rc;
-  if ((rc = ensure_scratch(cp.blob.size(), 1, true))) return rc;
+  if ((rc = ensure_scratch(cp.blob.size(), 1, true, cp.arena_words))) return rc;
   uint8_t* hp = (uint8_t*)h_pinned;
   std::memcpy(hp, cp.blob.data(), cp.blob.size());
   uint32_t off0 = 0;
@@ -808,8 +1091,16 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
   HIPCHK(hipMemcpyAsync(d_stats.p, hs, sizeof(PodStats), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(d_out.p, 0, (size_t)m.cap * 8 * kNumPlugins, s));
   const BatchView bv = bview(1);
+  if (D.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, 0, D, s));
   HIPCHK(launch_filter_score(m, bv, 0, s));
-  if (mode == SCORE_ONE) HIPCHK(launch_select(m, bv, 0, s));
+  if (mode == SCORE_ONE) {
+    if (D.score_mask & (1u << P_PTS)) HIPCHK(launch_pts_score(m, bv, 0, s));
+    HIPCHK(launch_select(m, bv, 0, s));
+  } else if (D.arena_words) {
+    HIPCHK(hipMemsetAsync(d_arena.p, 0, (size_t)D.arena_words * 8, s));  // k_select did not run
+  }
+  PodStats hstat;
+  HIPCHK(hipMemcpyAsync(&hstat, d_stats.p, sizeof(PodStats), hipMemcpyDeviceToHost, s));
   std::vector<uint32_t> st(N);
   std::vector<int64_t> rv(N), nv(N);
   if (mode == FILTER_ONE) {
@@ -819,12 +1110,22 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
     HIPCHK(hipMemcpyAsync(nv.data(), (int64_t*)d_out.p + (size_t)plugin * m.cap, (size_t)N * 8, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  if (plugin == P_IPA) {
+    // InterPodAffinity's Skip decisions depend on device counts: PreFilter skips when no existing
+    // anti-affinity term matched and the pod has no required terms (filtering.go:315-317);
+    // PreScore skips when no term contributed (scoring.go:207-209)
+    const bool skip = mode == FILTER_ONE ? (!cp.ipa_own_req && !(hstat.ipa_any & 4u)) : !(hstat.ipa_any & 8u);
+    if (skip) {
+      *code = KSG_CODE_SKIP;
+      return KSG_OK;
+    }
+  }
   for (int32_t i = 0; i < N; ++i) {
     if (mode == FILTER_ONE) {
       if (codes) codes[i] = (uint8_t)status_code(st[i]);
       if (reasons) reasons[i] = status_reasons(st[i]);
     } else if (!nodes || nodes[i]) {
-      if (raw) raw[i] = rv[i];
+      if (raw) raw[i] = (plugin == P_PTS && rv[i] == -1) ? 0 : rv[i];  // ignored node (scoring.go:203-205)
       if (norm) norm[i] = nv[i];
     }
   }

@@ -177,6 +177,7 @@ struct BoundPod {  // a pod in the cache (added bound or assumed)
   PodResources res;
   std::vector<uint32_t> port_ids;
   bool with_affinity = false;  // podWithAffinity (framework/types.go:386-389)
+  int32_t slot = -1;           // pod-table slot (PTS/IPA aggregation)
 };
 
 struct NodeRec {
@@ -217,7 +218,8 @@ class Cluster {
   int update_node(NodeSpec&& n);
   int remove_node(const std::string& name);
   // device_done: the HBM mirror already holds the pod (device-side AssumePod)
-  int add_pod(const PodSpec& p, const std::string& uid_override = "", bool device_done = false);
+  // slot: the pod-table slot reserved for an assumed pod at compile time (-1: allocate one)
+  int add_pod(const PodSpec& p, const std::string& uid_override = "", bool device_done = false, int32_t slot = -1);
   int remove_pod(const std::string& uid);
   int32_t pods_with_affinity = 0;
 
@@ -240,6 +242,28 @@ class Cluster {
   std::map<std::string, BoundPod> pods;
 
   int32_t key_id(const std::string& k);
+  Interner ns_ix;  // namespace names
+  int32_t ns_id(const std::string& ns) { return ns_ix.get(ns); }
+  // sorted (key id << 32 | value id) set of a label map; values are interned
+  std::vector<unsigned long long> label_set(const StrMap& labels);
+  // metav1.LabelSelectorAsSelector into an int32 program appended to *pool; false on a parse error
+  bool compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off);
+
+  // ---- pod table: every bound/assumed pod as (node, namespace, flags, labels) + its affinity terms
+  std::vector<int32_t> pt_node, pt_ns;
+  std::vector<uint32_t> pt_flags, pt_lbl_off, pt_lbl_cnt;
+  std::vector<unsigned long long> pt_pool;
+  std::vector<int32_t> pt_free;
+  std::vector<std::vector<int32_t>> pt_terms;  // slot -> term indices
+  std::vector<DTerm> tt;
+  std::vector<int32_t> tt_pool, tt_free;
+  std::map<int32_t, int32_t> exanti_keys, score_keys_req, score_keys_pref;  // key id -> live term count
+  bool pods_dirty = true;
+  // reserve a slot for `p` (node index -1 until placed); its terms go live with the slot
+  int32_t pod_table_put(const PodSpec& p, int32_t node_index);
+  void pod_table_drop(int32_t slot);
+  int upload_pod_table();
+  std::vector<double> log_tab;  // go math.Log(k), k < log_n
   int32_t scalar_slot(const std::string& n);  // -1 if too many distinct scalars
   uint32_t port_id(std::string ip, std::string proto, int32_t port);
 
@@ -262,6 +286,8 @@ class Cluster {
   bool order_dirty_ = true;
   int32_t slots_used_ = 0, slots_cap_ = 0;
   std::vector<DevBuf> bufs_;
+  DevBuf pt_dev_[9];  // pod table / term table device arrays (own lifetime, grown geometrically)
+  int grow(DevBuf& b, size_t bytes);
 
   void tree_add(const NodeSpec& n);
   void tree_remove(const NodeSpec& n);
@@ -287,7 +313,14 @@ struct CompiledPod {
   int32_t prefilter_code = 0, prefilter_plugin = 255;
   bool error = false;         // PreScore/Score error -> status Error, no launch
   uint32_t score_mask = 0;
+  int32_t slot = -1;          // pod-table slot reserved for the assume
+  bool prefilter_error = false;  // a PreFilter returned Error (PodTopologySpread selector)
+  bool ipa_own_req = false;   // the pod has required (anti-)affinity terms (IPA PreFilter Skip rule)
+  bool ipa_parse_error = false;  // IPA PreFilter: NewPodInfo failed -> UnschedulableAndUnresolvable
+  bool topo_score_error = false; // PTS/IPA PreScore Error
+  int32_t arena_words = 0;
 };
+struct Blob;
 
 class Engine {
  public:
@@ -302,6 +335,8 @@ class Engine {
   // compile `p` for the current cluster; rot_start from Cluster::next_start
   int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
               const uint8_t* node_list = nullptr);
+  int compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* B, PodDesc* D, uint32_t* fmask,
+                       uint32_t* smask, CompiledPod* out);
   // run a batch of cycles (device-resident, sequential semantics)
   int run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                 ksg_result* results, ksg_eval_out* eval);
@@ -317,12 +352,13 @@ class Engine {
  private:
   // per-batch device scratch
   DevBuf d_descs, d_off, d_stats, d_results, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
+  DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)
   void* h_pinned = nullptr;
   size_t h_pinned_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;  // sampled k_filter_score timing events (pairs)
   int ensure(DevBuf& b, size_t bytes);
-  int ensure_scratch(size_t desc_bytes, int pods, bool eval);
+  int ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena_words);
   BatchView bview(int pods);
 };
 

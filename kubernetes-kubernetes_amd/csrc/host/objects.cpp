@@ -204,7 +204,6 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
     out->name = d.str(*md, "name");
     out->ns = d.str(*md, "namespace", "default");
     if (out->ns.empty()) out->ns = "default";  // apiserver defaulting of metadata.namespace
-    if (out->ns.empty()) out->ns = "default";
     out->uid = d.str(*md, "uid");
     if (out->uid.empty()) out->uid = out->ns + "/" + out->name;
     out->labels = kv_map(d, d.get(*md, "labels"));

@@ -1,0 +1,282 @@
+// podtable.cpp -- the pod table behind PodTopologySpread and InterPodAffinity on the device.
+//
+// The reference walks NodeInfo.Pods of every snapshot node in PreFilter/PreScore
+// (podtopologyspread/filtering.go:237-311, scoring.go:118-194; interpodaffinity/filtering.go:216-283,
+// scoring.go:128-221).  Here every bound or assumed pod is one slot of a flat structure-of-arrays
+// table in HBM -- node index, namespace id, terminating flag, sorted label set -- and every
+// affinity term an existing pod carries (framework.PodInfo's RequiredAffinityTerms etc.,
+// kube-scheduler/framework/types.go:380-396, 1183-1226) is one entry of a term table.  The
+// per-pod aggregation kernel (k_aggregate) streams both tables into per-domain histograms.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "host.hpp"
+
+namespace ksg {
+
+std::vector<unsigned long long> Cluster::label_set(const StrMap& labels) {
+  std::vector<unsigned long long> out;
+  out.reserve(labels.size());
+  for (auto& kv : labels) {
+    const int32_t k = key_id(kv.first);
+    const int32_t v = keys[k].values.get(kv.second);
+    out.push_back(((unsigned long long)(uint32_t)k << 32) | (uint32_t)v);
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+// metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:36-71) with
+// labels.NewRequirement validation (selector.go:185-226).  merge_labels: the matchLabelKeys
+// label set PodTopologySpread prepends (common.go:96-106,130-143).
+bool Cluster::compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off) {
+  *off = (int32_t)pool->size();
+  if (!s.present) {  // nil selector: labels.Nothing()
+    pool->push_back(1);
+    pool->push_back(0);
+    return true;
+  }
+  struct Req { std::string key; int32_t op; std::vector<std::string> vals; };
+  std::vector<Req> reqs;
+  bool ok = true;
+  for (auto& kv : s.match) {
+    ok = ok && valid_label_key(kv.first) && valid_label_value(kv.second);
+    reqs.push_back({kv.first, LS_IN, {kv.second}});
+  }
+  for (auto& e : s.exprs) {
+    int32_t op;
+    if (e.op == "In") op = LS_IN;
+    else if (e.op == "NotIn") op = LS_NOTIN;
+    else if (e.op == "Exists") op = LS_EXISTS;
+    else if (e.op == "DoesNotExist") op = LS_DNE;
+    else return false;
+    ok = ok && valid_label_key(e.key);
+    if (op == LS_IN || op == LS_NOTIN) ok = ok && !e.values.empty();
+    else ok = ok && e.values.empty();
+    for (auto& v : e.values) ok = ok && valid_label_value(v);
+    reqs.push_back({e.key, op, e.values});
+  }
+  if (!ok) return false;
+  if (merge_labels && !merge_labels->empty())
+    for (auto& kv : *merge_labels) reqs.push_back({kv.first, LS_IN, {kv.second}});
+  pool->push_back(0);
+  pool->push_back((int32_t)reqs.size());
+  for (auto& r : reqs) {
+    const int32_t k = key_id(r.key);
+    pool->push_back(k);
+    pool->push_back(r.op);
+    pool->push_back((int32_t)r.vals.size());
+    for (auto& v : r.vals) pool->push_back(keys[k].values.get(v));
+  }
+  return true;
+}
+
+// framework.NewPodInfo + GetPod*AffinityTerms for an existing pod: a category whose terms do
+// not parse is dropped as a whole (the oracle does the same, oracle_model.cpp new_pod_info).
+int32_t Cluster::pod_table_put(const PodSpec& p, int32_t node_index) {
+  int32_t s;
+  if (!pt_free.empty()) {
+    s = pt_free.back();
+    pt_free.pop_back();
+  } else {
+    s = (int32_t)pt_node.size();
+    pt_node.push_back(-1);
+    pt_ns.push_back(0);
+    pt_flags.push_back(0);
+    pt_lbl_off.push_back(0);
+    pt_lbl_cnt.push_back(0);
+    pt_terms.emplace_back();
+  }
+  pt_node[s] = node_index;
+  pt_ns[s] = ns_id(p.ns);
+  pt_flags[s] = p.terminating ? 1u : 0u;
+  const auto ls = label_set(p.labels);
+  pt_lbl_off[s] = (uint32_t)pt_pool.size();
+  pt_lbl_cnt[s] = (uint32_t)ls.size();
+  pt_pool.insert(pt_pool.end(), ls.begin(), ls.end());
+
+  auto category = [&](const std::vector<PATerm>& in, int32_t kind) {
+    const size_t pool0 = tt_pool.size();
+    std::vector<DTerm> out;
+    for (auto& t : in) {
+      DTerm d{};
+      d.owner = s;
+      d.kind = kind;
+      d.weight = t.weight;
+      d.key = key_id(t.topo);
+      if (!compile_lsel(t.sel, nullptr, &tt_pool, &d.sel) || !compile_lsel(t.ns_sel, nullptr, &tt_pool, &d.nssel)) {
+        tt_pool.resize(pool0);
+        return;
+      }
+      d.ns_off = (int32_t)tt_pool.size();
+      if (t.namespaces.empty() && !t.ns_sel.present) {  // newAffinityTerm defaulting (types.go:422-448)
+        tt_pool.push_back(ns_id(p.ns));
+      } else {
+        for (auto& n : t.namespaces) tt_pool.push_back(ns_id(n));
+      }
+      d.ns_cnt = (int32_t)tt_pool.size() - d.ns_off;
+      out.push_back(d);
+    }
+    for (auto& d : out) {
+      ensure_label_slot(d.key);
+      int32_t j;
+      if (!tt_free.empty()) {
+        j = tt_free.back();
+        tt_free.pop_back();
+        tt[j] = d;
+      } else {
+        j = (int32_t)tt.size();
+        tt.push_back(d);
+      }
+      pt_terms[s].push_back(j);
+      auto& m = kind == T_REQ_ANTI ? exanti_keys : kind == T_REQ_AFF ? score_keys_req : score_keys_pref;
+      m[d.key]++;
+    }
+  };
+  if (p.has_pod_affinity) {
+    category(p.aff_req, T_REQ_AFF);
+    category(p.aff_pref, T_PREF_AFF);
+  }
+  if (p.has_pod_anti) {
+    category(p.anti_req, T_REQ_ANTI);
+    category(p.anti_pref, T_PREF_ANTI);
+  }
+  pods_dirty = true;
+  return s;
+}
+
+void Cluster::pod_table_drop(int32_t s) {
+  if (s < 0 || s >= (int32_t)pt_node.size()) return;
+  for (int32_t j : pt_terms[s]) {
+    DTerm& d = tt[j];
+    auto& m = d.kind == T_REQ_ANTI ? exanti_keys : d.kind == T_REQ_AFF ? score_keys_req : score_keys_pref;
+    auto it = m.find(d.key);
+    if (it != m.end() && --it->second <= 0) m.erase(it);
+    d.kind = T_DEAD;
+    d.owner = -1;
+    tt_free.push_back(j);
+  }
+  pt_terms[s].clear();
+  pt_node[s] = -1;
+  pt_lbl_cnt[s] = 0;
+  pt_free.push_back(s);
+  pods_dirty = true;
+}
+
+int Cluster::grow(DevBuf& b, size_t bytes) {
+  if (b.p && b.bytes >= bytes) return KSG_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  const size_t want = std::max<size_t>(4096, bytes + bytes / 2);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    err = "hipMalloc failed for the pod table";
+    return KSG_EDEVICE;
+  }
+  b.bytes = want;
+  return KSG_OK;
+}
+
+// Go's math.Log (math/log.go: the FreeBSD e_log.c reduction and polynomial), evaluated without
+// fused multiply-adds (objects are built with -ffp-contract=off) -- the weights
+// PodTopologySpread multiplies domain counts by (scoring.go:287-299).
+static double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (std::isnan(x) || (std::isinf(x) && x > 0)) return x;
+  if (x < 0) return std::nan("");
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = std::frexp(x, &ki);
+  if (f1 < M_SQRT2 / 2) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1;
+  const double k = (double)ki;
+  const double s = f / (2 + f);
+  const double s2 = s * s;
+  const double s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2;
+  const double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+int Cluster::upload_pod_table() {
+  // log table covers topoSize + 2 for every topoSize <= N (scoring.go:293-299)
+  const int32_t need_log = (int32_t)order_.size() + 4;
+  bool log_dirty = false;
+  if ((int32_t)log_tab.size() < need_log) {
+    const size_t old = log_tab.size();
+    log_tab.resize((size_t)need_log * 2);
+    for (size_t k = old; k < log_tab.size(); ++k) log_tab[k] = go_log((double)k);
+    log_dirty = true;
+  }
+  if (!pods_dirty && !log_dirty) return KSG_OK;
+  // compact the label pool when most of it is garbage
+  size_t live = 0;
+  for (size_t s = 0; s < pt_node.size(); ++s) live += pt_lbl_cnt[s];
+  if (pt_pool.size() > 4 * live + 65536) {
+    std::vector<unsigned long long> np;
+    np.reserve(live * 2);
+    for (size_t s = 0; s < pt_node.size(); ++s) {
+      const uint32_t o = pt_lbl_off[s], c = pt_lbl_cnt[s];
+      pt_lbl_off[s] = (uint32_t)np.size();
+      np.insert(np.end(), pt_pool.begin() + o, pt_pool.begin() + o + c);
+    }
+    pt_pool.swap(np);
+  }
+  int rc;
+  const size_t P = pt_node.size(), T = tt.size();
+  if ((rc = grow(pt_dev_[0], P * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[1], P * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[2], P * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[3], P * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[4], P * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[5], pt_pool.size() * 8 + 8))) return rc;
+  if ((rc = grow(pt_dev_[6], T * sizeof(DTerm) + sizeof(DTerm)))) return rc;
+  if ((rc = grow(pt_dev_[7], tt_pool.size() * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[8], log_tab.size() * 8))) return rc;
+  auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+    if (!bytes) return KSG_OK;
+    if (hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
+      err = "pod table upload failed";
+      return KSG_EDEVICE;
+    }
+    return KSG_OK;
+  };
+  if ((rc = up(pt_dev_[0], pt_node.data(), P * 4))) return rc;
+  if ((rc = up(pt_dev_[1], pt_ns.data(), P * 4))) return rc;
+  if ((rc = up(pt_dev_[2], pt_flags.data(), P * 4))) return rc;
+  if ((rc = up(pt_dev_[3], pt_lbl_off.data(), P * 4))) return rc;
+  if ((rc = up(pt_dev_[4], pt_lbl_cnt.data(), P * 4))) return rc;
+  if ((rc = up(pt_dev_[5], pt_pool.data(), pt_pool.size() * 8))) return rc;
+  if ((rc = up(pt_dev_[6], tt.data(), T * sizeof(DTerm)))) return rc;
+  if ((rc = up(pt_dev_[7], tt_pool.data(), tt_pool.size() * 4))) return rc;
+  if ((rc = up(pt_dev_[8], log_tab.data(), log_tab.size() * 8))) return rc;
+  if (hipStreamSynchronize(stream) != hipSuccess) {  // host vectors may change right after
+    err = "pod table upload failed";
+    return KSG_EDEVICE;
+  }
+  view.pods_hw = (int32_t)P;
+  view.n_terms = (int32_t)T;
+  view.pod_node = (int32_t*)pt_dev_[0].p;
+  view.pod_ns = (const int32_t*)pt_dev_[1].p;
+  view.pod_flags = (const uint32_t*)pt_dev_[2].p;
+  view.pod_lbl_off = (const uint32_t*)pt_dev_[3].p;
+  view.pod_lbl_cnt = (const uint32_t*)pt_dev_[4].p;
+  view.lbl_pool = (const unsigned long long*)pt_dev_[5].p;
+  view.terms = (const DTerm*)pt_dev_[6].p;
+  view.term_pool = (const int32_t*)pt_dev_[7].p;
+  view.log_tab = (const double*)pt_dev_[8].p;
+  view.log_n = (int32_t)log_tab.size();
+  pods_dirty = false;
+  return KSG_OK;
+}
+
+}  // namespace ksg

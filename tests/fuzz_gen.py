@@ -8,7 +8,7 @@ profile knobs (scoring strategies, resource lists, added affinity, weights, disa
 """
 import random
 
-from ksg.objects import NodeW, PodW, expr
+from ksg.objects import NodeW, PodW, expr, make_namespace
 
 ZONES = ["zone-a", "zone-b", "zone-c"]
 TAINT_KEYS = ["dedicated", "gpu", "spot"]
@@ -86,8 +86,79 @@ def rand_expr(rng, names):
     return expr("disk", "In", [rng.choice(["ssd", "hdd", "nvme"])])
 
 
-def rand_pod(rng, k, names, ns="default"):
+APPS = ["web", "db", "cache", "batch"]
+NAMESPACES = [("default", {"team": "a"}), ("prod", {"team": "a", "env": "prod"}), ("dev", {"team": "b"})]
+TOPO_KEYS = ["topology.kubernetes.io/zone", "kubernetes.io/hostname", "disk"]
+
+
+def rand_label_selector(rng):
+    r = rng.random()
+    if r < 0.1:
+        return None  # nil selector
+    if r < 0.15:
+        return {}  # everything
+    if r < 0.6:
+        return {"matchLabels": {"app": rng.choice(APPS)}}
+    if r < 0.8:
+        return {"matchExpressions": [{"key": "app", "operator": rng.choice(["In", "NotIn"]),
+                                      "values": rng.sample(APPS, rng.randint(1, 2))}]}
+    return {"matchExpressions": [{"key": rng.choice(["tier", "app"]), "operator": rng.choice(["Exists", "DoesNotExist"])}]}
+
+
+def rand_pa_term(rng):
+    t = {"topologyKey": rng.choice(TOPO_KEYS)}
+    sel = rand_label_selector(rng)
+    if sel is not None:
+        t["labelSelector"] = sel
+    r = rng.random()
+    if r < 0.2:
+        t["namespaces"] = rng.sample([n for n, _ in NAMESPACES], rng.randint(1, 2))
+    elif r < 0.35:
+        t["namespaceSelector"] = rng.choice([{}, {"matchLabels": {"team": "a"}}, {"matchLabels": {"env": "prod"}}])
+    return t
+
+
+def add_topology(rng, p, allow_required=True):
+    """Pod (anti-)affinity terms and topology spread constraints."""
+    spec = p.o["spec"]
+    if rng.random() < 0.3:
+        aff = spec.setdefault("affinity", {})
+        for kind in ("podAffinity", "podAntiAffinity"):
+            if rng.random() < 0.5:
+                continue
+            a = aff.setdefault(kind, {})
+            if allow_required and rng.random() < 0.5:
+                a["requiredDuringSchedulingIgnoredDuringExecution"] = [rand_pa_term(rng) for _ in range(rng.randint(1, 2))]
+            if rng.random() < 0.6:
+                a["preferredDuringSchedulingIgnoredDuringExecution"] = [
+                    {"weight": rng.randint(1, 100), "podAffinityTerm": rand_pa_term(rng)} for _ in range(rng.randint(1, 2))]
+    if rng.random() < 0.3:
+        for _ in range(rng.randint(1, 2)):
+            c = {"maxSkew": rng.randint(1, 3), "topologyKey": rng.choice(TOPO_KEYS),
+                 "whenUnsatisfiable": rng.choice(["DoNotSchedule", "ScheduleAnyway"])}
+            sel = rand_label_selector(rng)
+            if sel is not None:
+                c["labelSelector"] = sel
+            if rng.random() < 0.2:
+                c["minDomains"] = rng.randint(1, 4)
+                c["whenUnsatisfiable"] = "DoNotSchedule"
+            if rng.random() < 0.2:
+                c["nodeTaintsPolicy"] = rng.choice(["Honor", "Ignore"])
+            if rng.random() < 0.2:
+                c["nodeAffinityPolicy"] = rng.choice(["Honor", "Ignore"])
+            if rng.random() < 0.15:
+                c["matchLabelKeys"] = ["tier"]
+            spec.setdefault("topologySpreadConstraints", []).append(c)
+
+
+def rand_pod(rng, k, names, ns=None, topology=True):
+    ns = ns or rng.choice([n for n, _ in NAMESPACES])
     p = PodW(f"p{k}", ns)
+    p.label("app", rng.choice(APPS))
+    if rng.random() < 0.5:
+        p.label("tier", rng.choice(["fe", "be"]))
+    if rng.random() < 0.05:
+        p.terminating()
     for _ in range(rng.choice([1, 1, 2])):
         ports = None
         if rng.random() < 0.12:
@@ -117,6 +188,8 @@ def rand_pod(rng, k, names, ns="default"):
                                    for _ in range(rng.randint(1, 3))])
     if rng.random() < 0.02 and names:
         p.o["spec"]["nodeName"] = rng.choice(names + ["missing-node"])
+    if topology:
+        add_topology(rng, p)
     return p.obj()
 
 
@@ -138,18 +211,24 @@ CONFIGS = [
         "preferredDuringSchedulingIgnoredDuringExecution": [
             {"weight": 7, "preference": {"matchExpressions": [{"key": "disk", "operator": "In", "values": ["ssd"]}]}}]}}},
     {"disabledPlugins": ["ImageLocality", "NodeResourcesBalancedAllocation"], "scoreWeights": {"TaintToleration": "1"}},
+    {"interPodAffinity": {"hardPodAffinityWeight": 5}},
+    {"interPodAffinity": {"ignorePreferredTermsOfExistingPods": True, "hardPodAffinityWeight": 0}},
 ]
 
 
-def rand_cluster(seed, n_nodes, n_existing, cfg_index=None):
+def rand_cluster(seed, n_nodes, n_existing, cfg_index=None, topology=True):
     rng = random.Random(seed)
     cfg = CONFIGS[cfg_index if cfg_index is not None else rng.randrange(len(CONFIGS))]
     nodes = [rand_node(rng, i) for i in range(n_nodes)]
     names = [n["metadata"]["name"] for n in nodes]
     existing = []
     for k in range(n_existing):
-        p = rand_pod(rng, 100000 + k, names)
-        p["spec"].pop("affinity", None)
+        p = rand_pod(rng, 100000 + k, names, topology=topology)
+        p["spec"].get("affinity", {}).pop("nodeAffinity", None)
         p["spec"]["nodeName"] = rng.choice(names)
         existing.append(p)
     return rng, cfg, nodes, existing, names
+
+
+def namespaces():
+    return [make_namespace(n, l) for n, l in NAMESPACES]

@@ -8,7 +8,7 @@ import random
 
 import pytest
 
-from fuzz_gen import rand_cluster, rand_pod
+from fuzz_gen import namespaces, rand_cluster, rand_pod
 from golden_runner import load_cases, run_case
 from oracle_binding import oracle
 
@@ -33,6 +33,8 @@ def _pair(native, cfg, nodes, existing):
     bs = []
     for make in (native, oracle):
         b = make(cfg)
+        for ns in namespaces():
+            b.upsert_namespace(ns)
         for n in nodes:
             b.add_node(n)
         for p in existing:
@@ -53,9 +55,9 @@ def _cmp_cycle(g, o, pod, tag, evaluate=True):
     return hg, ho, rg
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(32))
 def test_random_sequences_match_oracle(native, seed):
-    rng, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=rng_nodes(seed), n_existing=40)
+    rng, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=rng_nodes(seed), n_existing=60)
     g, o = _pair(native, cfg, nodes, existing)
     for k in range(40):
         _cmp_cycle(g, o, rand_pod(rng, k, names), f"seed {seed} pod {k}")
@@ -105,11 +107,13 @@ def test_plugin_entry_points(native, seed):
         pod = rand_pod(rng, k, names)
         hg, ho = g.compile(pod), o.compile(pod)
         for plugin in ["NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts",
-                       "NodeResourcesFit"]:
+                       "NodeResourcesFit", "PodTopologySpread", "InterPodAffinity"]:
             assert g.run_filter_plugin(hg, plugin) == o.run_filter_plugin(ho, plugin), f"{plugin} pod {k}"
-        for plugin in ["TaintToleration", "NodeAffinity", "NodeResourcesFit", "NodeResourcesBalancedAllocation",
-                       "ImageLocality"]:
+        listed = sorted(rng.sample(range(len(names)), len(names) // 2))
+        for plugin in ["TaintToleration", "NodeAffinity", "NodeResourcesFit", "PodTopologySpread", "InterPodAffinity",
+                       "NodeResourcesBalancedAllocation", "ImageLocality"]:
             assert g.run_score_plugin(hg, plugin) == o.run_score_plugin(ho, plugin), f"{plugin} pod {k}"
+            assert g.run_score_plugin(hg, plugin, listed) == o.run_score_plugin(ho, plugin, listed), f"{plugin} {k}"
 
 
 def test_forget_and_cache_events(native):
