@@ -282,13 +282,10 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   apply_pod(*r, bp, +1);
   r->pods.push_back(uid);
   order();
-  const int32_t idx = layout_dirty ? -1 : index_of(r->spec.name);  // re-derived on relayout
-  if (slot >= 0) {
-    pt_node[slot] = idx;  // the device table already holds it (k_select's assume)
-    bp.slot = slot;
-  } else {
-    bp.slot = pod_table_put(p, idx);
-  }
+  // pod_table_put may materialise label columns (and relayout the mirror), so the node index is
+  // taken afterwards; while the layout is dirty it is re-derived by the next ensure_mirror
+  bp.slot = slot >= 0 ? slot : pod_table_put(p, -1);
+  pt_node[bp.slot] = layout_dirty ? -1 : index_of(r->spec.name);
   pods.emplace(uid, std::move(bp));
   if (!layout_dirty && !device_done) return upload_node_dynamic(index_of(r->spec.name));
   return KSG_OK;
@@ -481,11 +478,11 @@ int Cluster::upload_node_dynamic(int32_t i) {
   HIPCHK(hipMemcpyAsync(view.nz_cpu + i, &r.nz_cpu, 8, hipMemcpyHostToDevice, stream));
   HIPCHK(hipMemcpyAsync(view.nz_mem + i, &r.nz_mem, 8, hipMemcpyHostToDevice, stream));
   HIPCHK(hipMemcpyAsync(view.num_pods + i, &r.num_pods, 4, hipMemcpyHostToDevice, stream));
+  int64_t sv[kMaxScalar];
   for (int s = 0; s < kMaxScalar; ++s) {
     auto it = r.scalar_req.find(s);
-    int64_t v = it == r.scalar_req.end() ? 0 : it->second;
-    HIPCHK(hipMemcpyAsync(view.scalar_req + (size_t)s * cap + i, &v, 8, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipStreamSynchronize(stream));
+    sv[s] = it == r.scalar_req.end() ? 0 : it->second;
+    HIPCHK(hipMemcpyAsync(view.scalar_req + (size_t)s * cap + i, &sv[s], 8, hipMemcpyHostToDevice, stream));
   }
   if (r.ports.size() > (size_t)kPortSlots) { err = "too many host ports on node"; return KSG_ENOTSUP; }
   uint32_t slots[kPortSlots];

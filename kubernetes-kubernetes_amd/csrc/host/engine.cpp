@@ -1073,6 +1073,10 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
     if (cp.error) { *code = KSG_CODE_ERROR; return KSG_OK; }
     if (!(D.score_mask & (1u << plugin))) { *code = KSG_CODE_SKIP; return KSG_OK; }
   }
+  if (N == 0) {  // nothing to launch; only InterPodAffinity's Skip depends on counts (none here)
+    if (plugin == P_IPA) *code = (mode == FILTER_ONE && cp.ipa_own_req) ? KSG_CODE_SUCCESS : KSG_CODE_SKIP;
+    return KSG_OK;
+  }
   if ((rc = c->ensure_mirror())) return rc;
   if ((rc = ensure_scratch(cp.blob.size(), 1, true, cp.arena_words))) return rc;
   uint8_t* hp = (uint8_t*)h_pinned;
