@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c2-hetero", "c3", "c4", "c4-anti"],
+                    help="c2 SchedulingBasic (the metric's config); c3 SchedulingPodAffinity; c4 TopologySpreading")
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--init-pods", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=1000)
@@ -43,6 +45,10 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_filter_score.json"),
                     help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
+
+
+WORKLOAD_NAMES = {"c2": "SchedulingBasic", "c2-hetero": "SchedulingBasic (heterogeneous nodes)",
+                  "c3": "SchedulingPodAffinity", "c4": "TopologySpreading", "c4-anti": "PreferredPodAntiAffinity"}
 
 
 def cpu_baseline(nodes, init, pods, budget_s):
@@ -84,11 +90,17 @@ def main():
         torch.cuda.synchronize()
 
     from ksg.native import Scheduler
-    from ksg.synth import scheduling_basic
+    from ksg import synth
 
     n_meas = a.steps * a.batch
     n_warm = a.warmup * a.batch
-    nodes, init, pods = scheduling_basic(a.nodes, a.init_pods, n_warm + n_meas)
+    if a.workload in ("c2", "c2-hetero"):
+        nodes, init, pods = synth.scheduling_basic(a.nodes, a.init_pods, n_warm + n_meas, hetero=a.workload == "c2-hetero")
+    elif a.workload == "c3":
+        nodes, init, pods = synth.scheduling_pod_affinity(a.nodes, a.init_pods, n_warm + n_meas)
+    else:
+        nodes, init, pods = synth.topology_spreading(a.nodes, a.init_pods, n_warm + n_meas,
+                                                     preferred_anti=a.workload == "c4-anti")
     for k, p in enumerate(pods):  # distinct uids per rank (independent replicas)
         p["metadata"]["uid"] = f"r{rank}-{k}"
     s = Scheduler({"device": local, "kernelTimingStride": a.timing_stride})
@@ -162,8 +174,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (scheduler_perf node-default / pod-default templates, seeded)",
-            "config": {"workload": f"SchedulingBasic {a.nodes} nodes / {a.init_pods} init pods / "
-                                   f"{n_meas} measured pods per GPU (BASELINE configs[1])",
+            "config": {"workload": f"{WORKLOAD_NAMES[a.workload]} {a.nodes} nodes / {a.init_pods} init pods / "
+                                   f"{n_meas} measured pods per GPU" + (" (BASELINE configs[1])" if a.workload == "c2" else ""),
                        "nodes": a.nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": 100,
                        "plugins": "default", "parallelism": f"replicas{world}" if world > 1 else "single"},
             "placed": placed,

@@ -67,3 +67,67 @@ def scheduling_basic(n_nodes, n_init, n_pods, hetero=False, seed=0x5EED):
         else:
             pods.append(pod_default(f"pod-{k}"))
     return nodes, init, pods
+
+
+def _pause_pod(name, ns, labels):
+    p = PodW(name, ns).labels(labels).container(image=PAUSE, requests={"cpu": "100m", "memory": "500Mi"},
+                                                ports=[{"containerPort": 80}])
+    return p
+
+
+def pod_with_pod_affinity(name, ns):
+    """templates/pod-with-pod-affinity.yaml: required affinity to color=blue in the zone."""
+    p = _pause_pod(name, ns, {"color": "blue"})
+    p.o["spec"]["affinity"] = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [{
+        "labelSelector": {"matchLabels": {"color": "blue"}}, "topologyKey": "topology.kubernetes.io/zone",
+        "namespaces": ["sched-1", "sched-0"]}]}}
+    return p.obj()
+
+
+def pod_with_topology_spreading(name, ns):
+    """templates/pod-with-topology-spreading.yaml: zone spread, maxSkew 5, DoNotSchedule."""
+    p = _pause_pod(name, ns, {"color": "blue"})
+    p.o["spec"]["topologySpreadConstraints"] = [{
+        "maxSkew": 5, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule",
+        "labelSelector": {"matchLabels": {"color": "blue"}}}]
+    return p.obj()
+
+
+def pod_with_preferred_pod_anti_affinity(name, ns):
+    """templates/pod-with-preferred-pod-anti-affinity.yaml: soft hostname anti-affinity, weight 1."""
+    p = _pause_pod(name, ns, {"color": "yellow"})
+    p.o["spec"]["affinity"] = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [{
+        "weight": 1, "podAffinityTerm": {"labelSelector": {"matchLabels": {"color": "yellow"}},
+                                         "topologyKey": "kubernetes.io/hostname",
+                                         "namespaces": ["sched-1", "sched-0"]}}]}}
+    return p.obj()
+
+
+def scheduling_pod_affinity(n_nodes, n_init, n_pods, seed=0x5EED):
+    """BASELINE C3 / SchedulingPodAffinity (affinity/performance-config.yaml:96-139): every node in
+    zone1; init pods (sched-0) and measured pods (sched-1) from pod-with-pod-affinity."""
+    nodes = [NodeW(f"node-{i:06d}").capacity({"cpu": "4", "memory": "32Gi", "pods": "110"})
+             .label("kubernetes.io/hostname", f"node-{i:06d}").label("topology.kubernetes.io/zone", "zone1").obj()
+             for i in range(n_nodes)]
+    names = [n["metadata"]["name"] for n in nodes]
+    init = []
+    for k in range(n_init):
+        p = pod_with_pod_affinity(f"init-{k}", "sched-0")
+        p["spec"]["nodeName"] = names[k % n_nodes]
+        init.append(p)
+    pods = [pod_with_pod_affinity(f"pod-{k}", "sched-1") for k in range(n_pods)]
+    return nodes, init, pods
+
+
+def topology_spreading(n_nodes, n_init, n_pods, preferred_anti=False, seed=0x5EED):
+    """BASELINE C4 / TopologySpreading (topology_spreading/performance-config.yaml:20-59): zones
+    moon-1/2/3 round-robin, init pod-default pods, measured pod-with-topology-spreading (or, with
+    preferred_anti, pod-with-preferred-pod-anti-affinity)."""
+    nodes = [NodeW(f"node-{i:06d}").capacity({"cpu": "4", "memory": "32Gi", "pods": "110"})
+             .label("kubernetes.io/hostname", f"node-{i:06d}")
+             .label("topology.kubernetes.io/zone", f"moon-{i % 3 + 1}").obj() for i in range(n_nodes)]
+    names = [n["metadata"]["name"] for n in nodes]
+    init = [pod_default(f"init-{k}", ns="sched-0", node=names[k % n_nodes]) for k in range(n_init)]
+    make = pod_with_preferred_pod_anti_affinity if preferred_anti else pod_with_topology_spreading
+    pods = [make(f"pod-{k}", "sched-1") for k in range(n_pods)]
+    return nodes, init, pods

@@ -153,3 +153,26 @@ def test_empty_cluster_and_unschedulable(native):
     pod = rand_pod(random.Random(1), 0, [])
     hg, ho = g.compile(pod), o.compile(pod)
     assert g.schedule_one(hg)[0].as_tuple() == o.schedule_one(ho)[0].as_tuple()
+
+
+def _stream(native, nodes, init, pods, cfg=None):
+    g, o = _pair(native, cfg or {}, nodes, init)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"pod {k}"
+
+
+def test_c3_pod_affinity_1k(native):
+    from ksg.synth import scheduling_pod_affinity
+    _stream(native, *scheduling_pod_affinity(1000, 1000, 150))
+
+
+def test_c4_topology_spreading_3k(native):
+    from ksg.synth import topology_spreading
+    _stream(native, *topology_spreading(3000, 3000, 150))
+
+
+def test_c4_preferred_anti_affinity_2k(native):
+    from ksg.synth import topology_spreading
+    _stream(native, *topology_spreading(2000, 2000, 120, preferred_anti=True))
