@@ -10,9 +10,14 @@ before timing, as the informer would have delivered them; the timed region cover
 PreScore compilation, the H2D descriptor copy, both kernels per pod, the D2H results and the
 host-side assume bookkeeping.
 
-Multi-GPU (--gpus N under torch.distributed.run): every rank runs its own scheduler replica
-over its own copy of the cluster and its own pod stream (weak scaling, no data-path
-collective); DESIGN.md §6 describes the node-sharded RCCL design that replaces this for C5.
+Multi-GPU (--gpus N under torch.distributed.run), DESIGN.md §6.  Default `--mode sharded`: ONE
+scheduler whose snapshot is sharded by node across the N GPUs -- every rank holds the mirror,
+evaluates its contiguous node range, and per pod two (three with PodTopologySpread scoring) RCCL
+all-reduces over xGMI carry the feasible counts, NormalizeScore maxima and the packed
+(TotalScore, heap pre-order key, node) argmax; every rank applies the same AssumePod.  With
+`--node-scaling weak` (default for c2-c4) the cluster grows with N (nodes x N, per-GPU work
+fixed); `strong` keeps the cluster fixed (default for c5, the 100k-node config).  `--mode
+replicas` instead runs N independent schedulers (own cluster, own pod stream, no collective).
 
 The CPU baseline is the parity oracle (oracle/, a C++ restatement of the reference) timed
 on a bounded sample of the same pod stream from the same initial state, one host thread.
@@ -34,10 +39,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c2-hetero", "c3", "c4", "c4-anti"],
-                    help="c2 SchedulingBasic (the metric's config); c3 SchedulingPodAffinity; c4 TopologySpreading")
-    ap.add_argument("--nodes", type=int, default=5000)
-    ap.add_argument("--init-pods", type=int, default=1000)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c2-hetero", "c3", "c4", "c4-anti", "c5"],
+                    help="c2 SchedulingBasic (the metric's config); c3 SchedulingPodAffinity; c4 TopologySpreading; "
+                         "c5 100k-node mixed cluster")
+    ap.add_argument("--nodes", type=int, default=None, help="cluster nodes at N=1 (c2-c4: 5000, c5: 100000)")
+    ap.add_argument("--init-pods", type=int, default=None, help="bound pods at N=1 (c2-c4: 1000, c5: 10000)")
+    ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"], help="multi-GPU mode (N>1)")
+    ap.add_argument("--node-scaling", default=None, choices=["weak", "strong"],
+                    help="sharded mode: grow the cluster with N (weak) or keep it fixed (strong)")
     ap.add_argument("--batch", type=int, default=1000)
     ap.add_argument("--timing-stride", type=int, default=8, help="time every k-th filter kernel with HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the oracle CPU baseline sample")
@@ -48,7 +57,9 @@ def parse():
 
 
 WORKLOAD_NAMES = {"c2": "SchedulingBasic", "c2-hetero": "SchedulingBasic (heterogeneous nodes)",
-                  "c3": "SchedulingPodAffinity", "c4": "TopologySpreading", "c4-anti": "PreferredPodAntiAffinity"}
+                  "c3": "SchedulingPodAffinity", "c4": "TopologySpreading", "c4-anti": "PreferredPodAntiAffinity",
+                  "c5": "Mixed 100k-node cluster (50% default, 10% each node-affinity / pod-affinity / "
+                        "anti-affinity / preferred anti-affinity / zone spread)"}
 
 
 def cpu_baseline(nodes, init, pods, budget_s):
@@ -89,21 +100,35 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    from ksg.native import Scheduler
+    from ksg.native import Scheduler, comm_unique_id
     from ksg import synth
 
+    c5 = a.workload == "c5"
+    sharded = world > 1 and a.mode == "sharded"
+    scaling = a.node_scaling or ("strong" if c5 else "weak")
+    grow = world if (sharded and scaling == "weak") else 1
+    n_nodes = (a.nodes or (100000 if c5 else 5000)) * grow
+    n_init = (a.init_pods if a.init_pods is not None else (10000 if c5 else 1000)) * grow
     n_meas = a.steps * a.batch
     n_warm = a.warmup * a.batch
     if a.workload in ("c2", "c2-hetero"):
-        nodes, init, pods = synth.scheduling_basic(a.nodes, a.init_pods, n_warm + n_meas, hetero=a.workload == "c2-hetero")
+        nodes, init, pods = synth.scheduling_basic(n_nodes, n_init, n_warm + n_meas, hetero=a.workload == "c2-hetero")
     elif a.workload == "c3":
-        nodes, init, pods = synth.scheduling_pod_affinity(a.nodes, a.init_pods, n_warm + n_meas)
+        nodes, init, pods = synth.scheduling_pod_affinity(n_nodes, n_init, n_warm + n_meas)
+    elif c5:
+        nodes, init, pods = synth.mixed_cluster(n_nodes, n_init, n_warm + n_meas)
     else:
-        nodes, init, pods = synth.topology_spreading(a.nodes, a.init_pods, n_warm + n_meas,
+        nodes, init, pods = synth.topology_spreading(n_nodes, n_init, n_warm + n_meas,
                                                      preferred_anti=a.workload == "c4-anti")
-    for k, p in enumerate(pods):  # distinct uids per rank (independent replicas)
-        p["metadata"]["uid"] = f"r{rank}-{k}"
-    s = Scheduler({"device": local, "kernelTimingStride": a.timing_stride})
+    cfg = {"device": local, "kernelTimingStride": a.timing_stride}
+    if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        cfg["distributed"] = {"worldSize": world, "rank": rank, "ncclId": obj[0]}
+    else:
+        for k, p in enumerate(pods):  # distinct uids per rank (independent replicas)
+            p["metadata"]["uid"] = f"r{rank}-{k}"
+    s = Scheduler(cfg)
     for n in nodes:
         s.add_node(n)
     for p in init:
@@ -137,9 +162,11 @@ def main():
         dist.all_reduce(pl)
         placed = int(pl.item())
 
-    total_pods = n_meas * world
+    total_pods = n_meas * (1 if sharded else world)  # sharded: one scheduler, every rank sees every pod
+    if sharded:
+        placed //= world
     pods_s = total_pods / dt
-    evals_s = pods_s * a.nodes
+    evals_s = pods_s * n_nodes
     kms = sum(k[0] for k in kstats) / len(kstats)
     kbytes = sum(k[1] for k in kstats) / len(kstats)
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
@@ -147,7 +174,7 @@ def main():
     if os.path.exists(a.traffic):
         try:
             tj = json.load(open(a.traffic))
-            if tj.get("nodes") == a.nodes:
+            if tj.get("nodes") == n_nodes and world == 1:
                 traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
@@ -157,7 +184,7 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds)
             cpu = {"value": round(v, 2), "unit": "pods/s", "cores": 1, "kind": "port",
-                   "node_evals_per_s": round(v * a.nodes, 1),
+                   "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
                              f"{cdt:.1f} s, oracle/ C++ restatement, 1 thread"}
         out = {
@@ -170,14 +197,18 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if (sharded and scaling == "strong") else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (scheduler_perf node-default / pod-default templates, seeded)",
-            "config": {"workload": f"{WORKLOAD_NAMES[a.workload]} {a.nodes} nodes / {a.init_pods} init pods / "
-                                   f"{n_meas} measured pods per GPU" + (" (BASELINE configs[1])" if a.workload == "c2" else ""),
-                       "nodes": a.nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": 100,
-                       "plugins": "default", "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "config": {"workload": f"{WORKLOAD_NAMES[a.workload]} {n_nodes} nodes / {n_init} init pods / "
+                                   f"{n_meas} measured pods" + ("" if sharded else " per GPU")
+                                   + (" (BASELINE configs[1])" if a.workload == "c2" and world == 1 else "")
+                                   + (" (BASELINE configs[4])" if c5 else ""),
+                       "nodes": n_nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": 100,
+                       "plugins": "default",
+                       "parallelism": (f"nodes-sharded{world} (RCCL all-reduce per pod)" if sharded
+                                       else f"replicas{world}" if world > 1 else "single")},
             "placed": placed,
             "roofline": {"bound": "hbm", "kernel": "k_filter_score", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

@@ -180,6 +180,22 @@ int ksg_run_filter_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, int32_t 
 int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uint8_t *nodes,
                          int32_t *status_code, int64_t *raw, int64_t *normalized);
 
+/* ---- node-sharded evaluation ---------------------------------------------
+ * A context created with {"distributed": {"worldSize": W, "rank": r, "ncclId": "<hex>"}}
+ * holds the whole cluster mirror (every rank is fed the same informer events) and evaluates
+ * the nodes of its contiguous range of the snapshot order; per pod, RCCL all-reduces carry the
+ * feasible counts, the NormalizeScore maxima/minima (framework.go:1409-1423) and every rank's
+ * best (TotalScore, heap pre-order key, node) -- the argmax of selectHost (schedule_one.go:
+ * 1054-1085) -- so every rank returns the identical ScheduleResult and applies the identical
+ * AssumePod.  ksg_create is collective across the W ranks (ncclCommInitRank).  With
+ * "localGroup": "<name>" instead of ncclId, W contexts in ONE process on one device form the
+ * group (each driven by its own thread); used to test the sharded path on one GPU.
+ * ksg_comm_unique_id writes ncclGetUniqueId as 256 hex characters + NUL (rank 0 calls it and
+ * hands it to the other ranks) and returns the length. */
+int ksg_comm_unique_id(char *buf, size_t cap);
+/* first snapshot index and count of the nodes this rank evaluates */
+int ksg_shard_range(const ksg_ctx *ctx, int32_t *first_node, int32_t *num_nodes);
+
 int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
                                 double *bytes_per_launch, int32_t *launches);
 

@@ -25,6 +25,7 @@ constexpr int kMaxScalar = 16;   // interned extended/scalar resource columns
 constexpr int kPortSlots = 8;    // used-port slots per node (grown by the host if exceeded)
 constexpr int kMaxCons = 8;      // PodTopologySpread constraints per kind per pod
 constexpr int kMaxPodTerms = 8;  // InterPodAffinity terms per kind per pod
+constexpr int kMaxShards = 8;    // node shards (GPUs) of one node-sharded scheduler
 
 // ---- selector programs (labels.Selector / nodeaffinity terms compiled to slots) ----------
 enum SelOp : int32_t {
@@ -281,6 +282,32 @@ struct BatchView {
   int64_t* out_scores;    // eval mode: [kNumPlugins][cap] weighted normalised scores
   int64_t* out_total;     // eval mode: [cap]
   unsigned long long* arena;  // PTS/IPA histograms (zero between pods)
+};
+
+// ---- node-sharded evaluation ----------------------------------------------------
+// Every rank holds the whole mirror (replicated by the informer feed) and evaluates the nodes of
+// its contiguous block range.  Per pod, fixed-layout uint64 vectors are all-reduced with MAX:
+// per-rank slots (zero elsewhere) carry counts, encoded int64 maxima carry the normalisation
+// maxima, and bitwise-NOT of encoded minima carry the minima (0 is the identity of every slot).
+enum XaWord : int {
+  XA_CNT = 0,                   // [kMaxShards] feasible nodes of rank r
+  XA_BELOW = kMaxShards,        // [kMaxShards] feasible nodes of rank r before nextStartNodeIndex
+  XA_NONIGN = 2 * kMaxShards,   // [kMaxShards] PodTopologySpread non-ignored feasible nodes of rank r
+  XA_MAX_TAINT = 3 * kMaxShards,
+  XA_MAX_NA,
+  XA_MAX_IPA,
+  XA_NMIN_IPA,
+  XA_WORDS = 4 * kMaxShards,
+};
+enum XpWord : int { XP_MAX_PTS = 0, XP_NMIN_PTS = 1, XP_WORDS = 4 };
+enum XbWord : int { XB_KEY = 0, XB_NODE = kMaxShards, XB_WORDS = 2 * kMaxShards };
+struct RankPtrs { unsigned long long* p[kMaxShards]; };  // every rank's exchange vector (local transport)
+struct ShardView {
+  int32_t world, rank;
+  int32_t blk0, nblk;         // this rank's kBlock-node blocks [blk0, blk0 + nblk)
+  unsigned long long* xa;     // [pods][XA_WORDS]
+  unsigned long long* xp;     // [pods][XP_WORDS]
+  unsigned long long* xb;     // [pods][XB_WORDS]
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -174,15 +174,18 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
       if (s_arena[w]) atomicAdd(&b.arena[w], s_arena[w]);
   if (tid == 0 && s_any) atomicOr(&ps->ipa_any, s_any);
   __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics performed before the ticket
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t t = atomicAdd(&ps->done_agg, 1u);
+    // every count/flag this block published is an agent-scope atomic: wait for them to be
+    // performed, then take the ticket (no L2 write-back fence; the last block reads the arena
+    // with agent-scope atomic loads)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(&ps->done_agg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (t == (uint32_t)(nb_node + nb_pod + nb_term) - 1u) ? 1u : 0u;
   }
   __syncthreads();
   if (!s_last || d.n_ptsf == 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // critical-path minimum over the present domains of each DoNotSchedule constraint
   // (criticalPaths, filtering.go:64-110; minMatchNum :111-124)
   const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
@@ -215,16 +218,17 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
 
 // PodTopologySpread.Score for every feasible node (podtopologyspread/scoring.go:199-226): raw = round(
 // sum_c cnt_c * log(topoSize_c + 2) + (maxSkew_c - 1)), -1 for ignored nodes; min/max for NormalizeScore.
-__global__ __launch_bounds__(kBlock) void k_pts_score(MirrorView m, BatchView b, int pod) {
+__global__ __launch_bounds__(kBlock) void k_pts_score(MirrorView m, BatchView b, int pod, int blk0) {
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
-  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const int blk = blk0 + (int)blockIdx.x;
+  const int i = blk * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t cap = (size_t)m.cap;
   bool scored = false;
   int64_t raw = 0;
-  if (i < m.n && ((b.fmask[(size_t)blockIdx.x * (kBlock / 64) + wave] >> lane) & 1ull)) {
+  if (i < m.n && ((b.fmask[(size_t)blk * (kBlock / 64) + wave] >> lane) & 1ull)) {
     const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
     bool ignored = false;
     for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
@@ -292,9 +296,10 @@ hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, co
   return hipGetLastError();
 }
 
-hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
-  const int nb = (m.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_pts_score, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
+hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0, int nblk) {
+  if (nblk < 0) nblk = (m.n + kBlock - 1) / kBlock;
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pts_score, dim3(nblk), dim3(kBlock), 0, s, m, b, pod, blk0);
   return hipGetLastError();
 }
 

@@ -29,6 +29,24 @@ enum : int { P_UNSCHED = 0, P_NODENAME = 1, P_TAINT = 2, P_NA = 3, P_PORTS = 4, 
              P_IPA = 7, P_BAL = 8, P_IMG = 9 };
 enum : uint32_t { C_OK = 0, C_ERROR = 1, C_UNSCHED = 2, C_UU = 3 };
 
+// Go int64 `a / b` (truncating) without the ~60-instruction 64-bit division expansion on the
+// common path: operands that fit 32 bits use the 32-bit unit; non-negative operands below 2^52
+// divide in FP64 (exact inputs, correctly rounded quotient) and the truncated quotient is fixed
+// up by one with the exact remainder.  Anything else takes the generic int64 division.
+__device__ __forceinline__ int64_t go_div(int64_t a, int64_t b) {
+  if (a >= 0 && b > 0) {
+    if (((uint64_t)a | (uint64_t)b) >> 32 == 0) return (int64_t)((uint32_t)a / (uint32_t)b);
+    if (a < (1ll << 52) && b < (1ll << 52)) {
+      int64_t q = (int64_t)((double)a / (double)b);
+      const int64_t r = a - q * b;
+      if (r < 0) --q;
+      else if (r >= b) ++q;
+      return q;
+    }
+  }
+  return a / b;
+}
+
 template <typename T>
 __device__ __forceinline__ const T* at(const uint8_t* base, int32_t off) {
   return reinterpret_cast<const T*>(base + off);

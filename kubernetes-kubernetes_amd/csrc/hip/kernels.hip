@@ -26,13 +26,38 @@
 namespace ksg {
 
 // ---- resources --------------------------------------------------------------------------------
-__device__ __forceinline__ void node_res(const MirrorView& m, const ScoreRes& r, int i, bool useRequested,
-                                         int64_t* alloc, int64_t* allocated) {
+// The node columns every default-plugin pod reads, loaded once at kernel entry (independent of the
+// pod descriptor, so the loads are in flight while the descriptor's scalar loads resolve).
+struct NodeCore {
+  int64_t acpu, amem, aeph, rcpu, rmem, reph, nzcpu, nzmem;
+  int32_t apods, npods;
+  uint32_t flags, tlo, thi;
+};
+__device__ __forceinline__ NodeCore load_core(const MirrorView& m, int i) {
+  NodeCore c;
+  c.acpu = m.alloc_cpu[i];
+  c.amem = m.alloc_mem[i];
+  c.aeph = m.alloc_eph[i];
+  c.rcpu = m.req_cpu[i];
+  c.rmem = m.req_mem[i];
+  c.reph = m.req_eph[i];
+  c.nzcpu = m.nz_cpu[i];
+  c.nzmem = m.nz_mem[i];
+  c.apods = m.alloc_pods[i];
+  c.npods = m.num_pods[i];
+  c.flags = m.flags[i];
+  c.tlo = m.taint_off[i];
+  c.thi = m.taint_off[i + 1];
+  return c;
+}
+
+__device__ __forceinline__ void node_res(const MirrorView& m, const NodeCore& nc, const ScoreRes& r, int i,
+                                         bool useRequested, int64_t* alloc, int64_t* allocated) {
   // resource_allocation.go:198-232 calculateResourceAllocatableRequest
   switch (r.kind) {
-    case RES_CPU: *alloc = m.alloc_cpu[i]; *allocated = useRequested ? m.req_cpu[i] : m.nz_cpu[i]; break;
-    case RES_MEM: *alloc = m.alloc_mem[i]; *allocated = useRequested ? m.req_mem[i] : m.nz_mem[i]; break;
-    case RES_EPH: *alloc = m.alloc_eph[i]; *allocated = m.req_eph[i]; break;
+    case RES_CPU: *alloc = nc.acpu; *allocated = useRequested ? nc.rcpu : nc.nzcpu; break;
+    case RES_MEM: *alloc = nc.amem; *allocated = useRequested ? nc.rmem : nc.nzmem; break;
+    case RES_EPH: *alloc = nc.aeph; *allocated = nc.reph; break;
     case RES_SCALAR: {
       size_t c = (size_t)r.slot * (size_t)m.cap + (size_t)i;
       *alloc = m.scalar_alloc[c];
@@ -48,30 +73,30 @@ __device__ int64_t rtcr_shape(const uint8_t* base, const PodDesc& d, int64_t p) 
   for (int k = 0; k < d.n_rtcr; ++k)
     if (p <= s[2 * k]) {
       if (k == 0) return s[1];
-      return s[2 * k - 1] + (s[2 * k + 1] - s[2 * k - 1]) * (p - s[2 * k - 2]) / (s[2 * k] - s[2 * k - 2]);
+      return s[2 * k - 1] + go_div((s[2 * k + 1] - s[2 * k - 1]) * (p - s[2 * k - 2]), s[2 * k] - s[2 * k - 2]);
     }
   return s[2 * d.n_rtcr - 1];
 }
 
 // NodeResourcesFit.Score (fit.go:737-755 -> resource_allocation.go:138-193 + scorer)
-__device__ int64_t fit_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+__device__ int64_t fit_score(const MirrorView& m, const NodeCore& nc, const uint8_t* base, const PodDesc& d, int i) {
   const ScoreRes* res = at<ScoreRes>(base, d.fit_res_off);
   int64_t nodeScore = 0, weightSum = 0;
   for (int k = 0; k < d.n_fit_res; ++k) {
     const ScoreRes r = res[k];
     if (r.kind == RES_SKIP) continue;
     int64_t alloc, allocated;
-    node_res(m, r, i, false, &alloc, &allocated);
+    node_res(m, nc, r, i, false, &alloc, &allocated);
     if (alloc == 0) continue;
     int64_t requested = allocated + r.pod_req;
     int64_t s;
     if (d.fit_strategy == 0) {  // least_allocated.go:52-61
-      s = requested > alloc ? 0 : ((alloc - requested) * 100) / alloc;
+      s = requested > alloc ? 0 : go_div((alloc - requested) * 100, alloc);
     } else if (d.fit_strategy == 1) {  // most_allocated.go:55-65
       int64_t rq = requested > alloc ? alloc : requested;
-      s = (rq * 100) / alloc;
+      s = go_div(rq * 100, alloc);
     } else {  // requested_to_capacity_ratio.go:30-36
-      s = requested > alloc ? rtcr_shape(base, d, 100) : rtcr_shape(base, d, requested * 100 / alloc);
+      s = requested > alloc ? rtcr_shape(base, d, 100) : rtcr_shape(base, d, go_div(requested * 100, alloc));
       if (s <= 0) continue;
     }
     nodeScore += s * r.weight;
@@ -79,7 +104,7 @@ __device__ int64_t fit_score(const MirrorView& m, const uint8_t* base, const Pod
   }
   if (weightSum == 0) return 0;
   if (d.fit_strategy == 2) return (int64_t)round((double)nodeScore / (double)weightSum);
-  return nodeScore / weightSum;
+  return go_div(nodeScore, weightSum);
 }
 
 // balanced_allocation.go:220-254
@@ -112,7 +137,8 @@ __device__ int64_t balanced_score(const int64_t* req, const int64_t* alloc, int 
   return (int64_t)sc;
 }
 
-__device__ int64_t balanced_alloc_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+__device__ int64_t balanced_alloc_score(const MirrorView& m, const NodeCore& nc, const uint8_t* base,
+                                        const PodDesc& d, int i) {
   const ScoreRes* res = at<ScoreRes>(base, d.bal_res_off);
   int64_t requested[8], allocated[8], allocatable[8];
   int n = d.n_bal_res;
@@ -121,7 +147,7 @@ __device__ int64_t balanced_alloc_score(const MirrorView& m, const uint8_t* base
     const ScoreRes r = res[k];
     if (r.kind == RES_SKIP) continue;
     int64_t alloc, al;
-    node_res(m, r, i, true, &alloc, &al);
+    node_res(m, nc, r, i, true, &alloc, &al);
     if (alloc == 0) continue;
     allocatable[k] = alloc;
     allocated[k] = al;
@@ -146,25 +172,25 @@ __device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const P
   const int64_t mb = 1024 * 1024, minT = 23 * mb, maxT = 1000 * mb * d.img_count;
   if (sum < minT) sum = minT;
   else if (sum > maxT) sum = maxT;
-  return 100 * (sum - minT) / (maxT - minT);
+  return go_div(100 * (sum - minT), maxT - minT);
 }
 
 // ---- filters ------------------------------------------------------------------------------------
 // Returns the packed Filter status of node i (0 = Success), first failing plugin in the
 // RunFilterPlugins order wins.  *raw_taint gets the PreferNoSchedule count while the taint
 // list is in registers.
-__device__ uint32_t run_filters(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i,
+__device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const uint8_t* base, const PodDesc& d, int i,
                                 int64_t* raw_taint, const PodStats* ps, const unsigned long long* arena) {
   const uint32_t fm = d.filter_mask;
   // NodeUnschedulable (node_unschedulable.go:125-143)
   if ((fm >> P_UNSCHED) & 1u)
-    if ((m.flags[i] & 1u) && !(d.flags & DF_TOLERATES_UNSCHED)) return pack_status(C_UU, P_UNSCHED, KSG_R_UNSCHEDULABLE);
+    if ((nc.flags & 1u) && !(d.flags & DF_TOLERATES_UNSCHED)) return pack_status(C_UU, P_UNSCHED, KSG_R_UNSCHEDULABLE);
   // NodeName (node_name.go:67-83)
   if ((fm >> P_NODENAME) & 1u)
     if (d.node_name != -1 && d.node_name != i) return pack_status(C_UU, P_NODENAME, KSG_R_NODE_NAME);
   // TaintToleration (taint_toleration.go:102-116, 163-196)
   {
-    const uint32_t lo = m.taint_off[i], hi = m.taint_off[i + 1];
+    const uint32_t lo = nc.tlo, hi = nc.thi;
     bool untol = false;
     int64_t cnt = 0;
     for (uint32_t q = lo; q < hi; ++q) {
@@ -197,18 +223,18 @@ __device__ uint32_t run_filters(const MirrorView& m, const uint8_t* base, const 
   if ((fm >> P_FIT) & 1u) {
     uint32_t reasons = 0;
     bool unresolvable = false;
-    if ((int64_t)m.num_pods[i] + 1 > (int64_t)m.alloc_pods[i]) reasons |= KSG_R_TOO_MANY_PODS;
+    if ((int64_t)nc.npods + 1 > (int64_t)nc.apods) reasons |= KSG_R_TOO_MANY_PODS;
     if (d.fit_any) {
-      const int64_t acpu = m.alloc_cpu[i], amem = m.alloc_mem[i], aeph = m.alloc_eph[i];
-      if (d.req_cpu > 0 && d.req_cpu > acpu - m.req_cpu[i]) {
+      const int64_t acpu = nc.acpu, amem = nc.amem, aeph = nc.aeph;
+      if (d.req_cpu > 0 && d.req_cpu > acpu - nc.rcpu) {
         reasons |= KSG_R_INSUFFICIENT_CPU;
         unresolvable |= d.req_cpu > acpu;
       }
-      if (d.req_mem > 0 && d.req_mem > amem - m.req_mem[i]) {
+      if (d.req_mem > 0 && d.req_mem > amem - nc.rmem) {
         reasons |= KSG_R_INSUFFICIENT_MEMORY;
         unresolvable |= d.req_mem > amem;
       }
-      if (d.req_eph > 0 && d.req_eph > aeph - m.req_eph[i]) {
+      if (d.req_eph > 0 && d.req_eph > aeph - nc.reph) {
         reasons |= KSG_R_INSUFFICIENT_EPHEMERAL;
         unresolvable |= d.req_eph > aeph;
       }
@@ -286,18 +312,25 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 }
 
 // =====================================================================================================
-// k_filter_score
+// per-node evaluation (shared by k_filter_score and the persistent k_sched_loop)
 // =====================================================================================================
-__global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView b, int pod) {
-  const uint8_t* base = b.descs + b.desc_off[pod];
-  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
-  const int i = blockIdx.x * kBlock + threadIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool valid = i < m.n;
-  const bool eval = (d.flags & DF_EVAL_OUT) != 0;
+struct NodeEval {
+  uint32_t st;      // packed Filter status (0 = feasible)
+  bool pts;         // feasible and not ignored by PodTopologySpread scoring
+  int64_t rt, rna, ripa;  // raw TaintToleration / NodeAffinity / InterPodAffinity scores
+};
 
+// RunFilterPlugins + the raw Score of every active plugin for node i (framework.go:1105-1138,
+// 1378-1402); writes the node's status word, the weighted sum of the non-normalising scores and
+// the raw scores the normalising plugins need.
+__device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d, int pod,
+                              int i, bool valid) {
+  const bool eval = (d.flags & DF_EVAL_OUT) != 0;
+  NodeEval r{0u, false, 0, 0, 0};
   uint32_t st = 0;
   int64_t raw_taint = 0;
+  NodeCore nc{};
+  if (valid) nc = load_core(m, i);
   if (valid) {
     if (d.flags & DF_PREFILTER_REJECT) {
       st = pack_status((uint32_t)d.prefilter_code, (uint32_t)d.prefilter_plugin & 15u, KSG_R_PREFILTER);
@@ -309,65 +342,59 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
       st = in ? 0u : pack_status(C_UU, 15u, KSG_R_PREFILTER);
     }
     if (st == 0) {
-      uint32_t f = run_filters(m, base, d, i, &raw_taint, b.stats + pod, b.arena);
+      uint32_t f = run_filters(m, nc, base, d, i, &raw_taint, b.stats + pod, b.arena);
       if (d.flags & DF_ALL_FEASIBLE)  // plugin-eval mode: the caller's node list is the feasible list
         f = ((d.flags & DF_NODE_LIST) && !bit(base, d.node_list_off, (uint32_t)i, (m.n + 31) / 32))
                 ? pack_status(C_UU, 15u, 0u)
                 : 0u;
       st = f;
     }
+    b.status[i] = st;
   }
-  const bool feas = valid && st == 0;
-  const unsigned long long ballot = __ballot(feas);
-  if (lane == 0) b.fmask[(size_t)blockIdx.x * (kBlock / 64) + wave] = ballot;
-  if (valid) b.status[i] = st;
+  r.st = valid ? st : 1u;
+  if (!valid || st != 0) return r;
 
-  // raw scores of the feasible nodes (framework.go:1378-1402)
+  // raw scores of the feasible node (framework.go:1378-1402)
   int64_t fixed = 0;
-  int64_t rawv[kNumPlugins];
-#pragma unroll
-  for (int p = 0; p < kNumPlugins; ++p) rawv[p] = 0;
   const uint32_t sm = d.score_mask;
-  if (feas) {
-    if ((sm >> P_TAINT) & 1u) rawv[P_TAINT] = raw_taint;
-    if ((sm >> P_NA) & 1u) {
-      int64_t s = 0;
-      if (d.flags & DF_HAS_ADDED_PREF) s += prog_weight(m, base, d, d.na_added_pref, i);
-      if (d.flags & DF_HAS_PREF_NA) s += prog_weight(m, base, d, d.na_preferred, i);
-      rawv[P_NA] = s;
+  const size_t cap = (size_t)m.cap;
+  if ((sm >> P_TAINT) & 1u) r.rt = raw_taint;
+  if ((sm >> P_NA) & 1u) {
+    int64_t sc = 0;
+    if (d.flags & DF_HAS_ADDED_PREF) sc += prog_weight(m, base, d, d.na_added_pref, i);
+    if (d.flags & DF_HAS_PREF_NA) sc += prog_weight(m, base, d, d.na_preferred, i);
+    r.rna = sc;
+  }
+  int64_t rf = 0, rb = 0, ri = 0;
+  if ((sm >> P_FIT) & 1u) { rf = fit_score(m, nc, base, d, i); fixed += rf * d.weight[P_FIT]; }
+  if ((sm >> P_BAL) & 1u) { rb = balanced_alloc_score(m, nc, base, d, i); fixed += rb * d.weight[P_BAL]; }
+  if ((sm >> P_IMG) & 1u) { ri = image_score(m, base, d, i); fixed += ri * d.weight[P_IMG]; }
+  b.fixed[i] = fixed;
+  if ((sm >> P_TAINT) & 1u) b.raw[P_TAINT * cap + i] = r.rt;
+  if ((sm >> P_NA) & 1u) b.raw[P_NA * cap + i] = r.rna;
+  if (eval) {
+    b.raw[P_FIT * cap + i] = rf;
+    b.raw[P_BAL * cap + i] = rb;
+    b.raw[P_IMG * cap + i] = ri;
+  }
+  if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.Score (interpodaffinity/scoring.go:240-255)
+    const KeyHist* tk = at<KeyHist>(base, d.topokeys_off);
+    int64_t sc = 0;
+    for (int32_t k = 0; k < d.n_topokeys; ++k) {
+      const int32_t v = node_label(m, tk[k].slot, i);
+      if (v >= 0) sc += (int64_t)b.arena[tk[k].base + v];
     }
-    if ((sm >> P_FIT) & 1u) { rawv[P_FIT] = fit_score(m, base, d, i); fixed += rawv[P_FIT] * d.weight[P_FIT]; }
-    if ((sm >> P_BAL) & 1u) { rawv[P_BAL] = balanced_alloc_score(m, base, d, i); fixed += rawv[P_BAL] * d.weight[P_BAL]; }
-    if ((sm >> P_IMG) & 1u) { rawv[P_IMG] = image_score(m, base, d, i); fixed += rawv[P_IMG] * d.weight[P_IMG]; }
-    b.fixed[i] = fixed;
-    const size_t cap = (size_t)m.cap;
-    if ((sm >> P_TAINT) & 1u) b.raw[P_TAINT * cap + i] = rawv[P_TAINT];
-    if ((sm >> P_NA) & 1u) b.raw[P_NA * cap + i] = rawv[P_NA];
-    if (eval) {
-      b.raw[P_FIT * cap + i] = rawv[P_FIT];
-      b.raw[P_BAL * cap + i] = rawv[P_BAL];
-      b.raw[P_IMG * cap + i] = rawv[P_IMG];
-    }
-    if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.Score (interpodaffinity/scoring.go:240-255)
-      const KeyHist* tk = at<KeyHist>(base, d.topokeys_off);
-      int64_t s = 0;
-      for (int32_t k = 0; k < d.n_topokeys; ++k) {
-        const int32_t v = node_label(m, tk[k].slot, i);
-        if (v >= 0) s += (int64_t)b.arena[tk[k].base + v];
-      }
-      rawv[P_IPA] = s;
-      b.raw[P_IPA * cap + i] = s;
-    }
+    r.ripa = sc;
+    b.raw[P_IPA * cap + i] = sc;
   }
   // PodTopologySpread PreScore over the feasible list: ignored nodes and per-constraint domain
   // counts feed the normalising weights (podtopologyspread/scoring.go:61-115)
-  bool pts_counted = false;
-  if (feas && ((sm >> P_PTS) & 1u)) {
+  if ((sm >> P_PTS) & 1u) {
     const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
     bool ignored = false;
     for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
     if (!ignored) {
-      pts_counted = true;
+      r.pts = true;
       PodStats* ps = b.stats + pod;
       for (int32_t c = 0; c < d.n_ptss; ++c) {
         if (cs[c].hostname) continue;
@@ -376,21 +403,38 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
       }
     }
   }
+  return r;
+}
+
+// =====================================================================================================
+// k_filter_score
+// =====================================================================================================
+__global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView b, int pod, int blk0) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  const int blk = blk0 + (int)blockIdx.x;  // node-sharded launches cover blocks [blk0, blk0 + gridDim.x)
+  const int i = blk * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const NodeEval ne = eval_node(m, b, base, d, pod, i, i < m.n);
+  const bool feas = ne.st == 0;
+  const unsigned long long ballot = __ballot(feas);
+  if (lane == 0) b.fmask[(size_t)blk * (kBlock / 64) + wave] = ballot;
+  const uint32_t sm = d.score_mask;
 
   // per-block feasible count + per-plugin max (and IPA min) of the normalising plugins' raw scores
   __shared__ uint32_t s_cnt[kBlock / 64], s_pts[kBlock / 64];
   __shared__ unsigned long long s_max[3][kBlock / 64], s_min[kBlock / 64];
-  unsigned long long mt = feas ? enc_i64(rawv[P_TAINT]) : 0ull;
-  unsigned long long mn = feas ? enc_i64(rawv[P_NA]) : 0ull;
-  unsigned long long mi = feas ? enc_i64(rawv[P_IPA]) : 0ull;
-  unsigned long long ni = feas ? enc_i64(rawv[P_IPA]) : ~0ull;
+  unsigned long long mt = feas ? enc_i64(ne.rt) : 0ull;
+  unsigned long long mn = feas ? enc_i64(ne.rna) : 0ull;
+  unsigned long long mi = feas ? enc_i64(ne.ripa) : 0ull;
+  unsigned long long ni = feas ? enc_i64(ne.ripa) : ~0ull;
   mt = wave_max_u64(mt);
   mn = wave_max_u64(mn);
   if ((sm >> P_IPA) & 1u) {
     mi = wave_max_u64(mi);
     ni = wave_min_u64(ni);
   }
-  const unsigned long long pball = __ballot(pts_counted);
+  const unsigned long long pball = __ballot(ne.pts);
   if (lane == 0) {
     s_cnt[wave] = (uint32_t)__popcll(ballot);
     s_pts[wave] = (uint32_t)__popcll(pball);
@@ -411,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
       ia = s_max[2][w] > ia ? s_max[2][w] : ia;
       in = s_min[w] < in ? s_min[w] : in;
     }
-    b.blk_cnt[blockIdx.x] = c;
+    b.blk_cnt[blk] = c;
     if (c) {
       PodStats* ps = b.stats + pod;
       if ((sm >> P_TAINT) & 1u) atomicMax(&ps->max_raw[P_TAINT], a);
@@ -426,20 +470,256 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
 }
 
 // =====================================================================================================
-// k_select
+// k_select (+ the node-sharded k_select_shard / k_commit)
 // =====================================================================================================
 __device__ __forceinline__ uint32_t wave_prefix_count(unsigned long long ballot, int lane) {
   return (uint32_t)__popcll(lane ? (ballot & ((1ull << lane) - 1ull)) : 0ull);
+}
+
+// The maxima / minima the NormalizeScore passes need, gathered over the whole feasible list.
+struct NormStats {
+  int64_t mx_taint, mx_na, mx_pts, mn_pts, mx_ipa, mn_ipa;
+  uint32_t ipa_any;
+};
+
+// NormalizeScore + weight + sum for feasible node i (framework.go:1409-1452)
+__device__ int64_t node_total(const BatchView& b, const PodDesc& d, const NormStats& ns, size_t cap, int i,
+                              bool eval) {
+  if (d.flags & DF_NO_SCORE) return 1;  // no score plugins: TotalScore 1 (schedule_one.go:948-957)
+  int64_t total = b.fixed[i];
+  const uint32_t sm = d.score_mask;
+  if ((sm >> P_TAINT) & 1u) {  // DefaultNormalizeScore(100, reverse=true) (helper/normalize_score.go:27-55)
+    const int64_t mx = ns.mx_taint;
+    const int64_t r = b.raw[P_TAINT * cap + i];
+    const int64_t v = mx == 0 ? 100 : 100 - go_div(100 * r, mx);
+    total += v * d.weight[P_TAINT];
+    if (eval) b.out_scores[P_TAINT * cap + i] = v * d.weight[P_TAINT];
+  }
+  if ((sm >> P_NA) & 1u) {  // DefaultNormalizeScore(100, reverse=false)
+    const int64_t mx = ns.mx_na;
+    const int64_t r = b.raw[P_NA * cap + i];
+    const int64_t v = mx == 0 ? 0 : go_div(100 * r, mx);
+    total += v * d.weight[P_NA];
+    if (eval) b.out_scores[P_NA * cap + i] = v * d.weight[P_NA];
+  }
+  if ((sm >> P_PTS) & 1u) {  // PodTopologySpread.NormalizeScore (podtopologyspread/scoring.go:229-268)
+    const int64_t mx = ns.mx_pts, mn = ns.mn_pts;
+    const int64_t r = b.raw[P_PTS * cap + i];
+    const int64_t v = r == -1 ? 0 : (mx == 0 ? 100 : go_div(100 * (mx + mn - r), mx));
+    total += v * d.weight[P_PTS];
+    if (eval) b.out_scores[P_PTS * cap + i] = v * d.weight[P_PTS];
+  }
+  if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.NormalizeScore (interpodaffinity/scoring.go:258-290)
+    const int64_t r = b.raw[P_IPA * cap + i];
+    int64_t v = r;
+    if (ns.ipa_any & 8u) {
+      const int64_t mx = ns.mx_ipa, mn = ns.mn_ipa;
+      const int64_t diff = mx - mn;
+      double f = 0.0;
+      if (diff > 0) f = 100.0 * ((double)(r - mn) / (double)diff);
+      v = (int64_t)f;
+    }
+    total += v * d.weight[P_IPA];
+    if (eval) b.out_scores[P_IPA * cap + i] = v * d.weight[P_IPA];
+  }
+  if (eval) {
+    if ((sm >> P_FIT) & 1u) b.out_scores[P_FIT * cap + i] = b.raw[P_FIT * cap + i] * d.weight[P_FIT];
+    if ((sm >> P_BAL) & 1u) b.out_scores[P_BAL * cap + i] = b.raw[P_BAL * cap + i] * d.weight[P_BAL];
+    if ((sm >> P_IMG) & 1u) b.out_scores[P_IMG * cap + i] = b.raw[P_IMG * cap + i] * d.weight[P_IMG];
+  }
+  return total;
+}
+
+// Block-cooperative: the snapshot index of the g-th feasible node (0-based) counted over the
+// blocks [k0, k1) of blk_cnt / fmask; -1 if g is not in that range.  All threads must call it.
+__device__ int find_rank_node(const BatchView& b, int k0, int k1, uint32_t g) {
+  __shared__ uint32_t s_wsum[kBlock / 64];
+  __shared__ int s_node;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_node = -1;
+  // each thread owns a contiguous chunk of blocks; block-wide exclusive scan of the chunk sums
+  // (wave shuffles + one LDS word per wave)
+  const int nb = k1 - k0;
+  const int per = (nb + kBlock - 1) / kBlock;
+  const int c0 = k0 + threadIdx.x * per;
+  const int c1 = (c0 + per) < k1 ? (c0 + per) : k1;
+  uint32_t csum = 0;
+  for (int k = c0; k < c1; ++k) csum += b.blk_cnt[k];
+  uint32_t incl = csum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint32_t acc = incl - csum;
+  for (int w = 0; w < wave; ++w) acc += s_wsum[w];
+  if (g >= acc && g < acc + csum) {  // exactly one thread owns rank g
+    for (int k = c0; k < c1; ++k) {
+      const uint32_t c = b.blk_cnt[k];
+      if (g < acc + c) {
+        uint32_t need = g - acc;
+        const uint64_t* fw = b.fmask + (size_t)k * (kBlock / 64);
+        for (int w = 0; w < kBlock / 64; ++w) {
+          const uint32_t wc = (uint32_t)__popcll(fw[w]);
+          if (need < wc) {
+            uint64_t x = fw[w];
+            for (uint32_t q = 0; q < need; ++q) x &= x - 1ull;  // drop the lowest set bits
+            s_node = k * kBlock + w * 64 + (int)__builtin_ctzll(x);
+            break;
+          }
+          need -= wc;
+        }
+        break;
+      }
+      acc += c;
+    }
+  }
+  __syncthreads();
+  return s_node;
+}
+
+// Feasible nodes of blocks [k0, k1) with snapshot index < s (block-cooperative, thread 0's value
+// is the total; other threads' values are partial).
+__device__ uint32_t count_below(const BatchView& b, int k0, int k1, int s) {
+  __shared__ uint32_t s_red[kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sb = s / kBlock;
+  uint32_t c = 0;
+  for (int k = k0 + threadIdx.x; k < k1; k += kBlock) {
+    if (k < sb) {
+      c += b.blk_cnt[k];
+    } else if (k == sb) {
+      const uint64_t* fw = b.fmask + (size_t)sb * (kBlock / 64);
+      int rem = s - sb * kBlock;
+      for (int w = 0; w < kBlock / 64 && rem > 0; ++w) {
+        const int take = rem >= 64 ? 64 : rem;
+        const uint64_t msk = take == 64 ? ~0ull : ((1ull << take) - 1ull);
+        c += (uint32_t)__popcll(fw[w] & msk);
+        rem -= take;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) s_red[wave] = c;
+  __syncthreads();
+  c = 0;
+  for (int w = 0; w < kBlock / 64; ++w) c += s_red[w];
+  __syncthreads();
+  return c;
+}
+
+// Normalise every feasible node of this block, reduce the packed (TotalScore, heap pre-order
+// key) max into *best, zero this pod's share of the arena, take the arrival ticket.  Returns
+// true in the last block to arrive (which may then read *best).
+__device__ bool select_block(const MirrorView& m, const BatchView& b, const PodDesc& d, PodStats* ps,
+                             const NormStats& ns, int blk, int nblocks, uint32_t pre, uint32_t F, uint32_t ps_before,
+                             int arena_base, int arena_stride) {
+  const int i = blk * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cap = (size_t)m.cap;
+  const bool eval = (d.flags & DF_EVAL_OUT) != 0;
+  const unsigned long long ballot = b.fmask[(size_t)blk * (kBlock / 64) + wave];
+  __shared__ uint32_t s_wcnt[kBlock / 64];
+  if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(ballot);
+  __syncthreads();
+  uint32_t wave_pre = 0;
+  for (int w = 0; w < wave; ++w) wave_pre += s_wcnt[w];
+  const bool feas = i < m.n && ((ballot >> lane) & 1ull);
+
+  unsigned long long key = 0;
+  if (feas) {
+    const uint32_t g = pre + wave_pre + wave_prefix_count(ballot, lane);  // rank in snapshot order
+    const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;  // rank in evaluation order
+    const int64_t total = node_total(b, d, ns, cap, i, eval);
+    if (eval) b.out_total[i] = total;
+    key = pack_best(total, pos);
+  }
+  // the PTS/IPA histograms of this pod are dead now: zero them for the next pod on the stream
+  for (int w = arena_base + threadIdx.x; w < d.arena_words; w += arena_stride) b.arena[w] = 0ull;
+  key = wave_max_u64(key);
+  __shared__ unsigned long long s_key[kBlock / 64];
+  if (lane == 0) s_key[wave] = key;
+  __syncthreads();
+
+  // ---- one atomic per block, then the arrival ticket.  The only cross-block payload read in
+  // this launch is ps->best, itself an agent-scope atomic: the atomicMax has returned before the
+  // ticket add is issued, and the last block reads it with an agent-scope load -- no L2
+  // write-back/invalidate fences needed (MI355X_MICROARCH.md, valid hand-off forms: 8-B agent
+  // atomics both sides).  blk_cnt / fmask were written by the previous launch.
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    unsigned long long k = 0;
+    for (int w = 0; w < kBlock / 64; ++w) k = s_key[w] > k ? s_key[w] : k;
+    if (k) (void)__hip_atomic_fetch_max(&ps->best, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t t = __hip_atomic_fetch_add(&ps->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == (uint32_t)nblocks - 1u) ? 1u : 0u;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// DevResult + AssumePod of the chosen node (schedule_one.go:1102-1137 -> NodeInfo.update,
+// framework/types.go:445-468) on this replica of the mirror.  One thread.
+__device__ void commit_result(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d,
+                              PodStats* ps, int pod, uint32_t F, int node, unsigned long long best) {
+  const size_t cap = (size_t)m.cap;
+  DevResult r;
+  r.node = F > 0 ? node : -1;
+  r.feasible = (int32_t)F;
+  r.evaluated = 0;
+  r.total = F > 0 ? (int64_t)(best >> kPreBits) : 0;
+  r.key = best;
+  r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
+  r.ipa_any = ps->ipa_any;
+  if (d.flags & DF_PREFILTER_REJECT) r.status = (int32_t)C_UNSCHED;
+  if ((d.flags & DF_SCORE_ERROR) && F > 1) {  // prioritizeNodes error (schedule_one.go:600-603)
+    r.status = (int32_t)C_ERROR;
+    r.node = -1;
+  }
+  ps->feasible = F;
+  if ((d.flags & DF_ASSUME) && r.node >= 0) {
+    const int j = r.node;
+    m.req_cpu[j] += d.a_cpu;
+    m.req_mem[j] += d.a_mem;
+    m.req_eph[j] += d.a_eph;
+    m.nz_cpu[j] += d.a_nz_cpu;
+    m.nz_mem[j] += d.a_nz_mem;
+    m.num_pods[j] += 1;
+    const ScalarReq* sr = at<ScalarReq>(base, d.a_scalar_off);
+    for (int k = 0; k < d.n_a_scalar; ++k) m.scalar_req[(size_t)sr[k].slot * cap + j] += sr[k].qty;
+    const uint32_t* pp = at<uint32_t>(base, d.pod_ports_off);
+    uint32_t* slots = m.ports + (size_t)j * kPortSlots;
+    if (d.slot >= 0) m.pod_node[d.slot] = j;  // the pod joins NodeInfo.Pods (pod table)
+    for (int k = 0; k < d.n_pod_ports; ++k) {  // HostPortInfo.Add: set semantics
+      bool present = false;
+      int empty = -1;
+      for (int q = 0; q < kPortSlots; ++q) {
+        present |= slots[q] == pp[k];
+        if (slots[q] == 0xffffffffu && empty < 0) empty = q;
+      }
+      if (!present && empty >= 0) slots[empty] = pp[k];
+    }
+  }
+  b.results[pod] = r;
+}
+
+__device__ __forceinline__ uint32_t winner_rank(unsigned long long best, uint32_t ps_before, uint32_t F) {
+  // heap position of the winner -> global feasible rank g (undo the rotation)
+  const uint32_t pos = preorder_pos((1u << kPreBits) - 1u - (uint32_t)(best & ((1ull << kPreBits) - 1ull)));
+  uint32_t g = pos + ps_before;
+  if (g >= F) g -= F;
+  return g;
 }
 
 __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, int pod, int nblocks) {
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
-  const int i = blockIdx.x * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t cap = (size_t)m.cap;
-  const bool eval = (d.flags & DF_EVAL_OUT) != 0;
 
   // ---- global feasible count F, this block's exclusive prefix, and P(s) = feasible nodes
   // before the rotation start (nextStartNodeIndex, schedule_one.go:808) -- one strided pass
@@ -479,177 +759,182 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
     }
     ps_before = acc;
   }
-
-  // ---- normalise + weight + total for this node (framework.go:1409-1452)
-  const unsigned long long ballot = b.fmask[(size_t)blockIdx.x * (kBlock / 64) + wave];
-  __shared__ uint32_t s_wcnt[kBlock / 64];
-  if (lane == 0) s_wcnt[wave] = (uint32_t)__popcll(ballot);
-  __syncthreads();
-  uint32_t wave_pre = 0;
-  for (int w = 0; w < wave; ++w) wave_pre += s_wcnt[w];
-  const bool feas = i < m.n && ((ballot >> lane) & 1ull);
-
-  unsigned long long key = 0;
-  if (feas) {
-    const uint32_t g = pre + wave_pre + wave_prefix_count(ballot, lane);  // rank in snapshot order
-    const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;  // rank in evaluation order
-    int64_t total;
-    if (d.flags & DF_NO_SCORE) {
-      total = 1;
-    } else {
-      total = b.fixed[i];
-      const uint32_t sm = d.score_mask;
-      if ((sm >> P_TAINT) & 1u) {  // DefaultNormalizeScore(100, reverse=true) (helper/normalize_score.go:27-55)
-        const int64_t mx = dec_i64(ps->max_raw[P_TAINT]);
-        const int64_t r = b.raw[P_TAINT * cap + i];
-        const int64_t v = mx == 0 ? 100 : 100 - 100 * r / mx;
-        total += v * d.weight[P_TAINT];
-        if (eval) b.out_scores[P_TAINT * cap + i] = v * d.weight[P_TAINT];
-      }
-      if ((sm >> P_NA) & 1u) {  // DefaultNormalizeScore(100, reverse=false)
-        const int64_t mx = dec_i64(ps->max_raw[P_NA]);
-        const int64_t r = b.raw[P_NA * cap + i];
-        const int64_t v = mx == 0 ? 0 : 100 * r / mx;
-        total += v * d.weight[P_NA];
-        if (eval) b.out_scores[P_NA * cap + i] = v * d.weight[P_NA];
-      }
-      if ((sm >> P_PTS) & 1u) {  // PodTopologySpread.NormalizeScore (podtopologyspread/scoring.go:229-268)
-        const int64_t mx = dec_i64(ps->max_raw[P_PTS]), mn = dec_i64(ps->min_raw[P_PTS]);
-        const int64_t r = b.raw[P_PTS * cap + i];
-        const int64_t v = r == -1 ? 0 : (mx == 0 ? 100 : 100 * (mx + mn - r) / mx);
-        total += v * d.weight[P_PTS];
-        if (eval) b.out_scores[P_PTS * cap + i] = v * d.weight[P_PTS];
-      }
-      if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.NormalizeScore (interpodaffinity/scoring.go:258-290)
-        const int64_t r = b.raw[P_IPA * cap + i];
-        int64_t v = r;
-        if (ps->ipa_any & 8u) {
-          const int64_t mx = dec_i64(ps->max_raw[P_IPA]), mn = dec_i64(ps->min_raw[P_IPA]);
-          const int64_t diff = mx - mn;
-          double f = 0.0;
-          if (diff > 0) f = 100.0 * ((double)(r - mn) / (double)diff);
-          v = (int64_t)f;
-        }
-        total += v * d.weight[P_IPA];
-        if (eval) b.out_scores[P_IPA * cap + i] = v * d.weight[P_IPA];
-      }
-      if (eval) {
-        if ((sm >> P_FIT) & 1u) b.out_scores[P_FIT * cap + i] = b.raw[P_FIT * cap + i] * d.weight[P_FIT];
-        if ((sm >> P_BAL) & 1u) b.out_scores[P_BAL * cap + i] = b.raw[P_BAL * cap + i] * d.weight[P_BAL];
-        if ((sm >> P_IMG) & 1u) b.out_scores[P_IMG * cap + i] = b.raw[P_IMG * cap + i] * d.weight[P_IMG];
-      }
-    }
-    if (eval) b.out_total[i] = total;
-    key = pack_best(total, pos);
-  }
-  // the PTS/IPA histograms of this pod are dead now: zero them for the next pod on the stream
-  for (int w = blockIdx.x * kBlock + threadIdx.x; w < d.arena_words; w += nblocks * kBlock) b.arena[w] = 0ull;
-  key = wave_max_u64(key);
-  __shared__ unsigned long long s_key[kBlock / 64];
-  if (lane == 0) s_key[wave] = key;
-  __syncthreads();
-
-  // ---- one atomic per block, then the arrival ticket (Guideline 16: release before the ticket)
-  __shared__ uint32_t s_last;
-  if (threadIdx.x == 0) {
-    unsigned long long k = 0;
-    for (int w = 0; w < kBlock / 64; ++w) k = s_key[w] > k ? s_key[w] : k;
-    if (k) atomicMax(&ps->best, k);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    uint32_t t = atomicAdd(&ps->done, 1u);
-    s_last = (t == (uint32_t)nblocks - 1u) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!s_last) return;
+  NormStats ns;
+  ns.mx_taint = dec_i64(ps->max_raw[P_TAINT]);
+  ns.mx_na = dec_i64(ps->max_raw[P_NA]);
+  ns.mx_pts = dec_i64(ps->max_raw[P_PTS]);
+  ns.mn_pts = dec_i64(ps->min_raw[P_PTS]);
+  ns.mx_ipa = dec_i64(ps->max_raw[P_IPA]);
+  ns.mn_ipa = dec_i64(ps->min_raw[P_IPA]);
+  ns.ipa_any = ps->ipa_any;
+  if (!select_block(m, b, d, ps, ns, blockIdx.x, nblocks, pre, F, ps_before, blockIdx.x * kBlock, nblocks * kBlock))
+    return;
 
   // ================= last block: winner lookup + AssumePod =================
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  __shared__ uint32_t s_chunk[kBlock + 1];
-  __shared__ int s_node;
-  if (threadIdx.x == 0) s_node = -1;
   const unsigned long long best = __hip_atomic_load(&ps->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (F > 0) {
-    // heap position of the winner -> global feasible rank g (undo the rotation)
-    const uint32_t pos = preorder_pos((1u << kPreBits) - 1u - (uint32_t)(best & ((1ull << kPreBits) - 1ull)));
-    uint32_t g = pos + ps_before;
-    if (g >= F) g -= F;
-    // each thread owns a contiguous chunk of blocks; exclusive scan of chunk sums in LDS
-    const int per = (nblocks + kBlock - 1) / kBlock;
-    const int c0 = threadIdx.x * per;
-    const int c1 = (c0 + per) < nblocks ? (c0 + per) : nblocks;
-    uint32_t csum = 0;
-    for (int k = c0; k < c1; ++k) csum += b.blk_cnt[k];
-    s_chunk[threadIdx.x + 1] = csum;
+  int node = -1;
+  if (F > 0) node = find_rank_node(b, 0, nblocks, winner_rank(best, ps_before, F));
+  if (threadIdx.x == 0) commit_result(m, b, base, d, ps, pod, F, node, best);
+}
+
+// ---- node-sharded path ----------------------------------------------------------------
+// k_xpack_a (1 block): this rank's share of the first exchange -- feasible count, feasible nodes
+// before nextStartNodeIndex, PodTopologySpread non-ignored count, normalisation maxima/minima.
+__global__ __launch_bounds__(kBlock) void k_xpack_a(BatchView b, ShardView sv, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  const PodStats* ps = b.stats + pod;
+  const int k0 = sv.blk0, k1 = sv.blk0 + sv.nblk;
+  __shared__ uint32_t s_red[kBlock / 64];
+  uint32_t c = 0;
+  for (int k = k0 + threadIdx.x; k < k1; k += kBlock) c += b.blk_cnt[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  c = 0;
+  for (int w = 0; w < kBlock / 64; ++w) c += s_red[w];
+  const uint32_t below = d.rot_start > 0 ? count_below(b, k0, k1, d.rot_start) : 0u;
+  unsigned long long* x = sv.xa + (size_t)pod * XA_WORDS;
+  if (threadIdx.x < XA_WORDS) {
+    const int w = threadIdx.x;
+    unsigned long long v = 0;
+    if (w == XA_CNT + sv.rank) v = c;
+    else if (w == XA_BELOW + sv.rank) v = below;
+    else if (w == XA_NONIGN + sv.rank) v = ps->pts_nonignored;
+    else if (w == XA_MAX_TAINT) v = ps->max_raw[P_TAINT];
+    else if (w == XA_MAX_NA) v = ps->max_raw[P_NA];
+    else if (w == XA_MAX_IPA) v = ps->max_raw[P_IPA];
+    else if (w == XA_NMIN_IPA) v = ~ps->min_raw[P_IPA];
+    x[w] = v;
+  }
+}
+
+// k_unpack_pts (1 block): after the first exchange (and the all-reduce of the ScheduleAnyway
+// domain-presence words), the global topology sizes PodTopologySpread.Score normalises with.
+__global__ __launch_bounds__(kBlock) void k_unpack_pts(BatchView b, ShardView sv, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  const unsigned long long* x = sv.xa + (size_t)pod * XA_WORDS;
+  const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+  __shared__ uint32_t s_red[kBlock / 64];
+  for (int32_t c = 0; c < d.n_ptss; ++c) {
+    if (cs[c].hostname) continue;
+    uint32_t n = 0;
+    for (int v = threadIdx.x; v < cs[c].nvals; v += kBlock) n += b.arena[cs[c].pres_base + v] ? 1u : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = n;
     __syncthreads();
     if (threadIdx.x == 0) {
-      s_chunk[0] = 0;
-      for (int k = 1; k <= kBlock; ++k) s_chunk[k] += s_chunk[k - 1];
-    }
-    __syncthreads();
-    uint32_t acc = s_chunk[threadIdx.x];
-    if (g >= acc && g < s_chunk[threadIdx.x + 1]) {  // exactly one thread owns rank g
-      for (int k = c0; k < c1; ++k) {
-        const uint32_t c = b.blk_cnt[k];
-        if (g < acc + c) {
-          uint32_t need = g - acc;
-          const uint64_t* fw = b.fmask + (size_t)k * (kBlock / 64);
-          for (int w = 0; w < kBlock / 64; ++w) {
-            const uint32_t wc = (uint32_t)__popcll(fw[w]);
-            if (need < wc) {
-              uint64_t x = fw[w];
-              for (uint32_t q = 0; q < need; ++q) x &= x - 1ull;  // drop the lowest set bits
-              s_node = k * kBlock + w * 64 + (int)__builtin_ctzll(x);
-              break;
-            }
-            need -= wc;
-          }
-          break;
-        }
-        acc += c;
-      }
+      uint32_t t = 0;
+      for (int w = 0; w < kBlock / 64; ++w) t += s_red[w];
+      ps->pts_distinct[c] = t;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    DevResult r;
-    r.node = F > 0 ? s_node : -1;
-    r.feasible = (int32_t)F;
-    r.evaluated = 0;
-    r.total = F > 0 ? (int64_t)(best >> kPreBits) : 0;
-    r.key = best;
-    r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
-    r.ipa_any = ps->ipa_any;
-    if (d.flags & DF_PREFILTER_REJECT) r.status = (int32_t)C_UNSCHED;
-    if ((d.flags & DF_SCORE_ERROR) && F > 1) {  // prioritizeNodes error (schedule_one.go:600-603)
-      r.status = (int32_t)C_ERROR;
-      r.node = -1;
+    uint32_t t = 0;
+    for (int r = 0; r < sv.world; ++r) t += (uint32_t)x[XA_NONIGN + r];
+    ps->pts_nonignored = t;
+  }
+}
+
+// k_xpack_p (1 thread): PodTopologySpread raw-score max/min of this rank for the second exchange
+__global__ void k_xpack_p(BatchView b, ShardView sv, int pod) {
+  const PodStats* ps = b.stats + pod;
+  unsigned long long* x = sv.xp + (size_t)pod * XP_WORDS;
+  x[XP_MAX_PTS] = ps->max_raw[P_PTS];
+  x[XP_NMIN_PTS] = ~ps->min_raw[P_PTS];
+  x[2] = 0;
+  x[3] = 0;
+}
+
+// k_select_shard: k_select over this rank's blocks with the all-reduced statistics; the last
+// block writes this rank's best (key, node) into the final exchange vector.
+__global__ __launch_bounds__(kBlock) void k_select_shard(MirrorView m, BatchView b, ShardView sv, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  const unsigned long long* xa = sv.xa + (size_t)pod * XA_WORDS;
+  const unsigned long long* xp = sv.xp + (size_t)pod * XP_WORDS;
+  const int blk = sv.blk0 + blockIdx.x;
+  if (sv.nblk == 0) {  // an empty shard publishes an empty share and still zeroes its arena
+    for (int w = threadIdx.x; w < d.arena_words; w += kBlock) b.arena[w] = 0ull;
+    if (threadIdx.x < XB_WORDS) sv.xb[(size_t)pod * XB_WORDS + threadIdx.x] = 0ull;
+    return;
+  }
+  uint32_t F = 0, shard_pre = 0, ps_before = 0;
+  for (int r = 0; r < sv.world; ++r) {
+    const uint32_t c = (uint32_t)xa[XA_CNT + r];
+    F += c;
+    if (r < sv.rank) shard_pre += c;
+    ps_before += (uint32_t)xa[XA_BELOW + r];
+  }
+  __shared__ uint32_t s_red[kBlock / 64];
+  uint32_t pre = 0;
+  for (int k = sv.blk0 + threadIdx.x; k < blk; k += kBlock) pre += b.blk_cnt[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = pre;
+  __syncthreads();
+  pre = shard_pre;
+  for (int w = 0; w < kBlock / 64; ++w) pre += s_red[w];
+  NormStats ns;
+  ns.mx_taint = dec_i64(xa[XA_MAX_TAINT]);
+  ns.mx_na = dec_i64(xa[XA_MAX_NA]);
+  ns.mx_ipa = dec_i64(xa[XA_MAX_IPA]);
+  ns.mn_ipa = dec_i64(~xa[XA_NMIN_IPA]);
+  ns.mx_pts = dec_i64(xp[XP_MAX_PTS]);
+  ns.mn_pts = dec_i64(~xp[XP_NMIN_PTS]);
+  ns.ipa_any = ps->ipa_any;
+  if (!select_block(m, b, d, ps, ns, blk, sv.nblk, pre, F, ps_before, blockIdx.x * kBlock, sv.nblk * kBlock))
+    return;
+  const unsigned long long best = __hip_atomic_load(&ps->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int node = -1;
+  if (best) node = find_rank_node(b, sv.blk0, sv.blk0 + sv.nblk, winner_rank(best, ps_before, F) - shard_pre);
+  unsigned long long* xb = sv.xb + (size_t)pod * XB_WORDS;
+  if (threadIdx.x < XB_WORDS) {
+    const int w = threadIdx.x;
+    unsigned long long v = 0;
+    if (w == XB_KEY + sv.rank) v = best;
+    else if (w == XB_NODE + sv.rank) v = node >= 0 ? (unsigned long long)(node + 1) : 0ull;
+    xb[w] = v;
+  }
+}
+
+// k_commit (1 thread): the winner over all ranks (distinct ranks hold distinct feasible
+// positions, so the packed keys never tie), result + AssumePod on this replica.
+__global__ void k_commit(MirrorView m, BatchView b, ShardView sv, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  const unsigned long long* xa = sv.xa + (size_t)pod * XA_WORDS;
+  const unsigned long long* xb = sv.xb + (size_t)pod * XB_WORDS;
+  uint32_t F = 0;
+  for (int r = 0; r < sv.world; ++r) F += (uint32_t)xa[XA_CNT + r];
+  unsigned long long best = 0;
+  int node = -1;
+  for (int r = 0; r < sv.world; ++r)
+    if (xb[XB_KEY + r] > best) {
+      best = xb[XB_KEY + r];
+      node = (int)xb[XB_NODE + r] - 1;
     }
-    ps->feasible = F;
-    // AssumePod (schedule_one.go:1102-1137 -> NodeInfo.update, framework/types.go:445-468)
-    if ((d.flags & DF_ASSUME) && r.node >= 0) {
-      const int j = r.node;
-      m.req_cpu[j] += d.a_cpu;
-      m.req_mem[j] += d.a_mem;
-      m.req_eph[j] += d.a_eph;
-      m.nz_cpu[j] += d.a_nz_cpu;
-      m.nz_mem[j] += d.a_nz_mem;
-      m.num_pods[j] += 1;
-      const ScalarReq* sr = at<ScalarReq>(base, d.a_scalar_off);
-      for (int k = 0; k < d.n_a_scalar; ++k) m.scalar_req[(size_t)sr[k].slot * cap + j] += sr[k].qty;
-      const uint32_t* pp = at<uint32_t>(base, d.pod_ports_off);
-      uint32_t* slots = m.ports + (size_t)j * kPortSlots;
-      if (d.slot >= 0) m.pod_node[d.slot] = j;  // the pod joins NodeInfo.Pods (pod table)
-      for (int k = 0; k < d.n_pod_ports; ++k) {  // HostPortInfo.Add: set semantics
-        bool present = false;
-        int empty = -1;
-        for (int q = 0; q < kPortSlots; ++q) {
-          present |= slots[q] == pp[k];
-          if (slots[q] == 0xffffffffu && empty < 0) empty = q;
-        }
-        if (!present && empty >= 0) slots[empty] = pp[k];
-      }
+  commit_result(m, b, base, d, ps, pod, F, node, best);
+}
+
+// k_max_reduce: the in-process (same-device) all-reduce of the local communicator:
+// dst[w] = max over the ranks' vectors.  Safe in place: max is idempotent, so a rank reading a
+// vector another rank has already overwritten with the result still reads the same maximum.
+__global__ __launch_bounds__(kBlock) void k_max_reduce(unsigned long long* dst, RankPtrs src, int nsrc, int count) {
+  for (int w = blockIdx.x * kBlock + threadIdx.x; w < count; w += gridDim.x * kBlock) {
+    unsigned long long v = 0;
+    for (int r = 0; r < nsrc; ++r) {
+      const unsigned long long x = __hip_atomic_load(src.p[r] + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v = x > v ? x : v;
     }
-    b.results[pod] = r;
+    dst[w] = v;
   }
 }
 
@@ -659,18 +944,47 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
 namespace ksg {
 // t0/t1 non-null: the events are attached to the dispatch packet itself (hipExtLaunchKernel), so
 // their elapsed time is the kernel's own begin/end -- the same interval rocprofv3 reports.
+// blk0/nblk: the node blocks to evaluate (nblk < 0: all of them).
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
-                               hipEvent_t t1) {
-  const int nb = (m.n + kBlock - 1) / kBlock;
+                               hipEvent_t t1, int blk0, int nblk) {
+  if (nblk < 0) nblk = (m.n + kBlock - 1) / kBlock;
+  if (nblk == 0) return hipSuccess;
   if (t0)
-    hipExtLaunchKernelGGL(k_filter_score, dim3(nb), dim3(kBlock), 0, s, t0, t1, 0, m, b, pod);
+    hipExtLaunchKernelGGL(k_filter_score, dim3(nblk), dim3(kBlock), 0, s, t0, t1, 0, m, b, pod, blk0);
   else
-    hipLaunchKernelGGL(k_filter_score, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
+    hipLaunchKernelGGL(k_filter_score, dim3(nblk), dim3(kBlock), 0, s, m, b, pod, blk0);
   return hipGetLastError();
 }
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
   const int nb = (m.n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_select, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
+  return hipGetLastError();
+}
+hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_xpack_a, dim3(1), dim3(kBlock), 0, s, b, sv, pod);
+  return hipGetLastError();
+}
+hipError_t launch_unpack_pts(const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack_pts, dim3(1), dim3(kBlock), 0, s, b, sv, pod);
+  return hipGetLastError();
+}
+hipError_t launch_xpack_p(const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_xpack_p, dim3(1), dim3(1), 0, s, b, sv, pod);
+  return hipGetLastError();
+}
+// nblk == 0 (an empty shard) still launches one block: the rank must publish its (empty) share
+hipError_t launch_select_shard(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
+  ShardView v = sv;
+  hipLaunchKernelGGL(k_select_shard, dim3(v.nblk > 0 ? v.nblk : 1), dim3(kBlock), 0, s, m, b, v, pod);
+  return hipGetLastError();
+}
+hipError_t launch_commit(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_commit, dim3(1), dim3(1), 0, s, m, b, sv, pod);
+  return hipGetLastError();
+}
+hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int nsrc, int count, hipStream_t s) {
+  const int nb = (count + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_max_reduce, dim3(nb < 64 ? (nb > 0 ? nb : 1) : 64), dim3(kBlock), 0, s, dst, src, nsrc, count);
   return hipGetLastError();
 }
 }  // namespace ksg

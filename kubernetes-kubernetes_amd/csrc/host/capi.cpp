@@ -1,3 +1,4 @@
+#include <algorithm>
 // capi.cpp -- the extern "C" boundary declared in include/ksg.h.
 //
 // Every entry point catches C++ exceptions and maps them to KSG_E* codes; nothing here falls
@@ -7,6 +8,7 @@
 #include <new>
 #include <string>
 
+#include "comm.hpp"
 #include "host.hpp"
 
 using namespace ksg;
@@ -65,6 +67,15 @@ ksg_ctx* ksg_create(const char* config_json, size_t len) {
       return nullptr;
     }
     ctx->engine.reset(new Engine(ctx->cluster.get()));
+    if (cfg.world > 1) {  // node-sharded: join the exchange group (collective across the ranks)
+      std::string err;
+      ctx->engine->comm = make_comm(cfg, &err);
+      if (!ctx->engine->comm) {
+        g_create_error = err;
+        delete ctx;
+        return nullptr;
+      }
+    }
     return ctx;
   } catch (const std::exception& e) {
     g_create_error = e.what();
@@ -230,6 +241,34 @@ int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, const uin
     return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::SCORE_ONE, plugin, nodes, status_code, nullptr,
                                                  nullptr, raw, normalized));
   })
+}
+
+int ksg_comm_unique_id(char* buf, size_t cap) {
+  try {
+    std::string hex, err;
+    int rc = comm_unique_id(&hex, &err);
+    if (rc) {
+      g_create_error = err;
+      return rc;
+    }
+    if (!buf || cap < hex.size() + 1) return KSG_EINVAL;
+    std::memcpy(buf, hex.c_str(), hex.size() + 1);
+    return (int)hex.size();
+  } catch (const std::exception& e) {
+    g_create_error = e.what();
+    return KSG_EINVAL;
+  }
+}
+
+int ksg_shard_range(const ksg_ctx* ctx, int32_t* first_node, int32_t* num_nodes) {
+  if (!ctx || !first_node || !num_nodes) return KSG_EINVAL;
+  int32_t b0 = 0, nb = 0;
+  const int32_t n = (int32_t)ctx->cluster->order().size();
+  ctx->engine->shard_range(n, &b0, &nb);
+  const int32_t lo = std::min<int32_t>(b0 * kBlock, n), hi = std::min<int32_t>((b0 + nb) * kBlock, n);
+  *first_node = lo;
+  *num_nodes = hi - lo;
+  return KSG_OK;
 }
 
 int ksg_last_batch_kernel_stats(const ksg_ctx* ctx, double* avg_kernel_ms, double* bytes_per_launch,

@@ -1,0 +1,44 @@
+// comm.hpp -- the per-pod exchange of the node-sharded scheduler.
+//
+// Each rank evaluates a contiguous block range of the snapshot order; per pod the ranks
+// all-reduce (MAX) small fixed-layout uint64 vectors (desc.h XaWord/XpWord/XbWord): feasible
+// counts, NormalizeScore maxima/minima, PodTopologySpread domain presence, and the packed
+// (TotalScore, heap pre-order key) + node of every rank's best node.  The exchange is
+// stream-ordered: it is enqueued between the kernels of a pod, so a whole batch of pods runs
+// without a host round trip.
+//
+// Two transports behind one interface:
+//   RcclComm  -- one process per GPU, RCCL ncclAllReduce(ncclUint64, ncclMax) over xGMI.
+//   LocalComm -- ranks in one process sharing one device (threads, one context each); the
+//                all-reduce is an event-ordered max-reduce kernel reading every rank's vector.
+//                This is how the sharded path is exercised on a single-GPU box.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+
+namespace ksg {
+
+struct Config;
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  int world = 1, rank = 0;
+  // in-stream all-reduce(MAX) of `count` uint64 words at device pointer `buf`, in place
+  virtual int all_reduce_max(unsigned long long* buf, size_t count, hipStream_t s) = 0;
+  // brackets several all-reduces that may be fused (ncclGroupStart/End)
+  virtual int group_begin() { return 0; }
+  virtual int group_end() { return 0; }
+  // end of a batch: every rank's stream has drained (already synchronised by the caller)
+  virtual int batch_end() { return 0; }
+  std::string err;
+};
+
+// nullptr + *err on failure; cfg.world == 1 never creates one
+std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err);
+// ncclGetUniqueId as 256 hex characters (rank 0 creates it and hands it to every rank)
+int comm_unique_id(std::string* hex, std::string* err);
+
+}  // namespace ksg

@@ -15,15 +15,22 @@
 #include <cmath>
 #include <cstring>
 
+#include "comm.hpp"
 #include "host.hpp"
 
 namespace ksg {
 
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0 = nullptr,
-                               hipEvent_t t1 = nullptr);
+                               hipEvent_t t1 = nullptr, int blk0 = 0, int nblk = -1);
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
 hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, const PodDesc& d, hipStream_t s);
-hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0 = 0,
+                            int nblk = -1);
+hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+hipError_t launch_unpack_pts(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+hipError_t launch_xpack_p(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+hipError_t launch_select_shard(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+hipError_t launch_commit(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
 
 #define HIPCHK(x)                                               \
   do {                                                          \
@@ -701,6 +708,10 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       if (!ekeys.empty() && parse_ok) D.ipa_flags |= IPA_EXIST_SCORE;
       for (int32_t k : ekeys)
         if (!topo_base.count(k)) topo_base[k] = alloc(nvals(k));
+      // Neither the pod's preferred terms nor any existing pod's scoring terms can add to
+      // topologyScore, so it stays empty and PreScore returns Skip (scoring.go:207-209) -- known
+      // here without counting anything on the device.
+      if (!(D.ipa_flags & (IPA_PREF | IPA_EXIST_SCORE)) && !(D.flags & DF_SCORE_ERROR)) *smask &= ~(1u << P_IPA);
     } else {
       paff.clear();
       panti.clear();
@@ -805,7 +816,7 @@ double Engine::algo_bytes(const PodDesc& d) const {
 Engine::~Engine() {
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena})
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -839,6 +850,12 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena
   if (eval) {
     if ((rc = ensure(d_out, cap * 8 * kNumPlugins))) return rc;
     if ((rc = ensure(d_total, cap * 8))) return rc;
+  }
+  if (comm) {
+    if ((rc = ensure(d_xa, (size_t)pods * XA_WORDS * 8))) return rc;
+    if ((rc = ensure(d_xp, (size_t)pods * XP_WORDS * 8))) return rc;
+    if ((rc = ensure(d_xb, (size_t)pods * XB_WORDS * 8))) return rc;
+    HIPCHK(hipMemsetAsync(d_xp.p, 0, (size_t)pods * XP_WORDS * 8, c->stream));
   }
   if (d_arena.bytes < (size_t)arena_words * 8 + 8) {
     const size_t old = d_arena.bytes;
@@ -880,6 +897,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const int n = (int)pods.size();
   if (n == 0) return KSG_OK;
   if (eval && n != 1) return KSG_EINVAL;
+  if (eval && comm) {
+    c->err = "per-node evaluation output is not gathered across node shards (use an unsharded context)";
+    return KSG_ENOTSUP;
+  }
   c->order();
   if (c->order().empty()) {  // ErrNoNodesAvailable (schedule_one.go:569-571)
     for (int i = 0; i < n; ++i) results[i] = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
@@ -949,7 +970,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   HIPCHK(hipEventRecord(ev0, s));
   int launches = 0, timed = 0;
   double bytes = 0;
-  for (int i = 0; i < n; ++i) {
+  if (comm) {
+    if ((rc = run_sharded(cp, bv, n, &launches, &bytes, &timed))) return rc;
+  }
+  for (int i = 0; i < n && !comm; ++i) {
     if (cp[i].error) continue;
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
     if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));
@@ -979,6 +1003,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  if (comm && comm->batch_end()) {
+    c->err = comm->err;
+    return KSG_EDEVICE;
+  }
   float ms = 0;
   (void)hipEventElapsedTime(&ms, ev0, ev1);
   last_kernel_ms = launches ? ms / (2.0 * launches) : 0;
@@ -1040,6 +1068,76 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         for (int q = 0; q < kNumPlugins; ++q)
           eval->plugin_scores[(size_t)q * N + i] = scored ? outs[(size_t)q * m.cap + i] : 0;
     }
+  }
+  return KSG_OK;
+}
+
+// This rank's contiguous block range of the snapshot order.
+void Engine::shard_range(int32_t n, int32_t* blk0, int32_t* nblk) const {
+  const int64_t NB = ((int64_t)n + kBlock - 1) / kBlock;
+  const int W = c->cfg.world, r = c->cfg.rank;
+  const int64_t b0 = NB * r / W, b1 = NB * (r + 1) / W;
+  *blk0 = (int32_t)b0;
+  *nblk = (int32_t)(b1 - b0);
+}
+
+// Node-sharded cycles: per pod, the replicated pod-table aggregation, this rank's node blocks,
+// then the stream-ordered exchanges (comm.hpp) between the kernels -- 2 all-reduces per pod
+// (3 when PodTopologySpread scores) and still no host round trip inside the batch.
+int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int n, int* launches,
+                        double* bytes, int* timed_out) {
+  hipStream_t s = c->stream;
+  const MirrorView& m = c->view;
+  ShardView sv{};
+  sv.world = c->cfg.world;
+  sv.rank = c->cfg.rank;
+  shard_range(m.n, &sv.blk0, &sv.nblk);
+  shard_blk0 = sv.blk0;
+  shard_nblk = sv.nblk;
+  sv.xa = (unsigned long long*)d_xa.p;
+  sv.xp = (unsigned long long*)d_xp.p;
+  sv.xb = (unsigned long long*)d_xb.p;
+  const double frac = m.n > 0 ? std::min(1.0, (double)sv.nblk * kBlock / (double)m.n) : 0.0;
+  const int stride = c->cfg.timing_stride;
+  int& timed = *timed_out;
+  auto xchg = [&](unsigned long long* p, size_t count) -> int {
+    if (comm->all_reduce_max(p, count, s)) {
+      c->err = comm->err;
+      return KSG_EDEVICE;
+    }
+    return KSG_OK;
+  };
+  for (int i = 0; i < n; ++i) {
+    if (cp[i].error) continue;
+    const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
+    if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));  // replicated pod table
+    if (stride > 0 && i % stride == 0 && sv.nblk > 0) {
+      HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1], sv.blk0, sv.nblk));
+      timed++;
+    } else {
+      HIPCHK(launch_filter_score(m, bv, i, s, nullptr, nullptr, sv.blk0, sv.nblk));
+    }
+    HIPCHK(launch_xpack_a(bv, sv, i, s));
+    const bool pts = (hd.score_mask & (1u << P_PTS)) != 0;
+    if (comm->group_begin()) return KSG_EDEVICE;
+    int rc = xchg(sv.xa + (size_t)i * XA_WORDS, XA_WORDS);
+    if (!rc && pts) {  // ScheduleAnyway domain presence (arena words) is OR-ed across shards
+      const PtsCons* cs = reinterpret_cast<const PtsCons*>(cp[i].blob.data() + hd.ptss_off);
+      for (int32_t k = 0; k < hd.n_ptss && !rc; ++k)
+        if (!cs[k].hostname && cs[k].nvals > 0) rc = xchg(bv.arena + cs[k].pres_base, (size_t)cs[k].nvals);
+    }
+    if (comm->group_end() || rc) return rc ? rc : KSG_EDEVICE;
+    if (pts) {
+      HIPCHK(launch_unpack_pts(bv, sv, i, s));
+      HIPCHK(launch_pts_score(m, bv, i, s, sv.blk0, sv.nblk));
+      HIPCHK(launch_xpack_p(bv, sv, i, s));
+      if ((rc = xchg(sv.xp + (size_t)i * XP_WORDS, XP_WORDS))) return rc;
+    }
+    HIPCHK(launch_select_shard(m, bv, sv, i, s));
+    if ((rc = xchg(sv.xb + (size_t)i * XB_WORDS, XB_WORDS))) return rc;
+    HIPCHK(launch_commit(m, bv, sv, i, s));
+    *bytes += algo_bytes(hd) * frac;
+    (*launches)++;
   }
   return KSG_OK;
 }

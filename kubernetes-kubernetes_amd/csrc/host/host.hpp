@@ -142,6 +142,10 @@ struct Config {
   std::vector<std::pair<int32_t, NSTerm>> added_pref;
   int device = 0;
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
+  // node-sharded evaluation: this context evaluates the snapshot-order block range of `rank`
+  // out of `world`; the per-pod exchanges run over RCCL (nccl_id) or in-process (local_group)
+  int world = 1, rank = 0;
+  std::string nccl_id, local_group;
   Config();
 };
 bool decode_config(const char* p, size_t n, Config* c, std::string* err);
@@ -321,6 +325,7 @@ struct CompiledPod {
   int32_t arena_words = 0;
 };
 struct Blob;
+class Comm;
 
 class Engine {
  public:
@@ -348,11 +353,18 @@ class Engine {
   double algo_bytes(const PodDesc& d) const;
   double last_kernel_ms = 0, last_bytes = 0;
   int32_t last_launches = 0;
+  // node-sharded evaluation (cfg.world > 1): this rank's block range + the exchange transport
+  std::unique_ptr<Comm> comm;
+  int32_t shard_blk0 = 0, shard_nblk = -1;
+  void shard_range(int32_t n, int32_t* blk0, int32_t* nblk) const;
 
  private:
   // per-batch device scratch
   DevBuf d_descs, d_off, d_stats, d_results, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
   DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)
+  DevBuf d_xa, d_xp, d_xb;  // node-sharded exchange vectors, one set per pod of the batch
+  int run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int n, int* launches, double* bytes,
+                  int* timed);
   void* h_pinned = nullptr;
   size_t h_pinned_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -490,6 +490,20 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     if (const JVal* fg = d.get(r, "featureGates")) c->taint_cmp_ops = d.boolean(*fg, "TaintTolerationComparisonOperators");
     c->device = (int)d.num(r, "device", 0);
     c->timing_stride = (int)d.num(r, "kernelTimingStride", 0);
+    if (const JVal* ds = d.get(r, "distributed")) {  // node-sharded evaluation
+      c->world = (int)d.num(*ds, "worldSize", 1);
+      c->rank = (int)d.num(*ds, "rank", 0);
+      c->nccl_id = d.str(*ds, "ncclId");
+      c->local_group = d.str(*ds, "localGroup");
+      if (c->world < 1 || c->world > kMaxShards || c->rank < 0 || c->rank >= c->world) {
+        *err = "distributed: worldSize must be in [1, 8] and 0 <= rank < worldSize";
+        return false;
+      }
+      if (c->world > 1 && c->nccl_id.empty() == c->local_group.empty()) {
+        *err = "distributed: exactly one of ncclId (RCCL) or localGroup (in-process ranks) is required";
+        return false;
+      }
+    }
     bool ok = true;
     d.each(d.get(r, "scoreWeights"), [&](const JVal& v) {
       int id = plugin_by_name(v.key);

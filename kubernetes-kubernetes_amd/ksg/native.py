@@ -26,6 +26,11 @@ def load():
         lib.ksg_last_batch_kernel_stats.restype = C.c_int
         lib.ksg_last_batch_kernel_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                                     C.POINTER(C.c_int32)]
+        lib.ksg_comm_unique_id.restype = C.c_int
+        lib.ksg_comm_unique_id.argtypes = [C.c_char_p, C.c_size_t]
+        lib.ksg_create_error.restype = C.c_char_p
+        lib.ksg_shard_range.restype = C.c_int
+        lib.ksg_shard_range.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         _lib = lib
     return _lib
 
@@ -42,3 +47,19 @@ class Scheduler(Backend):
         self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n)),
                   "kernel_stats")
         return ms.value, by.value, n.value
+
+    def shard_range(self):
+        """(first snapshot index, node count) this rank evaluates (node-sharded contexts)."""
+        a, n = C.c_int32(), C.c_int32()
+        self._chk(self.lib.ksg_shard_range(self.ctx, C.byref(a), C.byref(n)), "shard_range")
+        return a.value, n.value
+
+
+def comm_unique_id():
+    """ncclGetUniqueId as hex (rank 0 creates it; every rank passes it as distributed.ncclId)."""
+    lib = load()
+    buf = C.create_string_buffer(512)
+    rc = lib.ksg_comm_unique_id(buf, 512)
+    if rc < 0:
+        raise KsgError(f"ksg_comm_unique_id: rc={rc}: {lib.ksg_create_error().decode(errors='replace')}")
+    return buf.value.decode()

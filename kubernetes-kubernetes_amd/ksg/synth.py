@@ -131,3 +131,67 @@ def topology_spreading(n_nodes, n_init, n_pods, preferred_anti=False, seed=0x5EE
     make = pod_with_preferred_pod_anti_affinity if preferred_anti else pod_with_topology_spreading
     pods = [make(f"pod-{k}", "sched-1") for k in range(n_pods)]
     return nodes, init, pods
+
+
+def pod_with_node_affinity(name, ns, zones):
+    """templates/pod-with-node-affinity.yaml: required zone In [...]"""
+    p = _pause_pod(name, ns, {"color": "green"})
+    p.o["spec"]["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+        "nodeSelectorTerms": [{"matchExpressions": [
+            {"key": "topology.kubernetes.io/zone", "operator": "In", "values": zones}]}]}}}
+    return p.obj()
+
+
+def pod_with_required_anti_affinity(name, ns):
+    """templates/pod-with-pod-anti-affinity.yaml: required hostname anti-affinity to itself."""
+    p = _pause_pod(name, ns, {"color": "red"})
+    p.o["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [{
+        "labelSelector": {"matchLabels": {"color": "red"}}, "topologyKey": "kubernetes.io/hostname",
+        "namespaces": ["sched-1", "sched-0"]}]}}
+    return p.obj()
+
+
+def mixed_cluster(n_nodes, n_init, n_pods, zones=10, seed=0x5EED):
+    """BASELINE C5: n_nodes heterogeneous nodes in `zones` zones round-robin, 1 %
+    tainted NoSchedule, pre-loaded with n_init bound pod-default / affinity-seed pods; the measured
+    stream draws 50 % pod-default, 10 % each node-affinity, required pod-affinity, required
+    hostname anti-affinity, preferred hostname anti-affinity, zone spread (fixed proportions,
+    seeded order)."""
+    rng = random.Random(seed)
+    nodes = []
+    for i in range(n_nodes):
+        name = f"node-{i:06d}"
+        w = (NodeW(name).capacity({"cpu": str(rng.choice([8, 16, 32, 64])),
+                                   "memory": f"{rng.choice([32, 64, 128, 256])}Gi", "pods": "110"})
+             .label("kubernetes.io/hostname", name).label("topology.kubernetes.io/zone", f"zone-{i % zones}"))
+        if i % 100 == 37:
+            w.taints([{"key": "dedicated", "value": "infra", "effect": "NoSchedule"}])
+        nodes.append(w.obj())
+    names = [n["metadata"]["name"] for n in nodes]
+    init = []
+    for k in range(n_init):
+        node = names[rng.randrange(n_nodes)]
+        if k % 10 == 0:  # seeds for the required pod-affinity pods (color=blue in some zones)
+            p = _pause_pod(f"init-{k}", "sched-0", {"color": "blue"}).obj()
+            p["spec"]["nodeName"] = node
+            init.append(p)
+        else:
+            init.append(pod_default(f"init-{k}", ns="sched-0", node=node))
+    kinds = ["default"] * 5 + ["node-affinity", "pod-affinity", "anti-affinity", "preferred-anti", "spread"]
+    pods = []
+    for k in range(n_pods):
+        kind = kinds[rng.randrange(len(kinds))]
+        nm = f"pod-{k}"
+        if kind == "default":
+            pods.append(pod_default(nm, ns="sched-1"))
+        elif kind == "node-affinity":
+            pods.append(pod_with_node_affinity(nm, "sched-1", [f"zone-{z}" for z in rng.sample(range(zones), 2)]))
+        elif kind == "pod-affinity":
+            pods.append(pod_with_pod_affinity(nm, "sched-1"))
+        elif kind == "anti-affinity":
+            pods.append(pod_with_required_anti_affinity(nm, "sched-1"))
+        elif kind == "preferred-anti":
+            pods.append(pod_with_preferred_pod_anti_affinity(nm, "sched-1"))
+        else:
+            pods.append(pod_with_topology_spreading(nm, "sched-1"))
+    return nodes, init, pods

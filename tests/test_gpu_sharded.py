@@ -1,0 +1,136 @@
+"""Node-sharded evaluation on the device, against the CPU oracle.
+
+W scheduler contexts on ONE GPU form an in-process exchange group ("localGroup"): each holds
+the whole cluster mirror, evaluates its contiguous range of the snapshot order, and exchanges
+counts / NormalizeScore maxima / best keys through the same stream-ordered all-reduce slots the
+RCCL transport uses (comm.hpp) -- only the transport differs.  Every rank must return the
+oracle's ScheduleResult for every pod of the stream (sequential assume semantics), including
+empty shards (clusters smaller than W * 256 nodes) and PodTopologySpread/InterPodAffinity pods.
+"""
+import threading
+import uuid
+
+import pytest
+
+from fuzz_gen import namespaces, rand_cluster, rand_pod
+from oracle_binding import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _group(world, cfg, nodes, existing):
+    from ksg.native import Scheduler
+    name = f"t-{uuid.uuid4().hex[:8]}"
+    ranks = []
+    for r in range(world):
+        s = Scheduler(dict(cfg, device=0, distributed={"worldSize": world, "rank": r, "localGroup": name}))
+        for ns in namespaces():
+            s.upsert_namespace(ns)
+        for n in nodes:
+            s.add_node(n)
+        for p in existing:
+            s.add_pod(p)
+        ranks.append(s)
+    o = oracle(cfg)
+    for ns in namespaces():
+        o.upsert_namespace(ns)
+    for n in nodes:
+        o.add_node(n)
+    for p in existing:
+        o.add_pod(p)
+    for s in ranks:
+        assert s.node_names() == o.node_names()
+    return ranks, o
+
+
+def _run_ranks(ranks, pods, chunk):
+    """schedule_batch on every rank concurrently (one thread per rank, as the exchange needs)."""
+    hs = [[s.compile(p) for p in pods] for s in ranks]
+    out = [[] for _ in ranks]
+    errs = []
+
+    def work(r):
+        try:
+            for k in range(0, len(pods), chunk):
+                out[r].extend(x.as_tuple() for x in ranks[r].schedule_batch(hs[r][k:k + chunk], assume=True))
+        except Exception as e:  # surfaced below
+            errs.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(len(ranks))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    return out
+
+
+def _check(ranks, o, pods, chunk=64):
+    got = _run_ranks(ranks, pods, chunk)
+    for k, p in enumerate(pods):
+        want = o.schedule_one(o.compile(p), assume=True)[0].as_tuple()
+        for r in range(len(ranks)):
+            assert got[r][k] == want, f"rank {r} pod {k}: {got[r][k]} != oracle {want}"
+
+
+def test_shard_ranges_partition_the_snapshot():
+    from ksg.synth import scheduling_basic
+    nodes, _, _ = scheduling_basic(1300, 0, 0)
+    ranks, _ = _group(3, {}, nodes, [])
+    spans = [s.shard_range() for s in ranks]
+    assert spans[0][0] == 0
+    for (a, n), (b, _) in zip(spans, spans[1:]):
+        assert a + n == b and a % 256 == 0
+    assert spans[-1][0] + spans[-1][1] == 1300
+
+
+@pytest.mark.parametrize("world,seed", [(2, 0), (2, 1), (3, 2), (4, 3), (8, 4), (2, 5)])
+def test_random_streams_match_oracle(world, seed):
+    rng, cfg, nodes, existing, names = rand_cluster(3000 + seed, n_nodes=[700, 1100, 900, 1300, 2100, 600][seed],
+                                                    n_existing=120)
+    ranks, o = _group(world, cfg, nodes, existing)
+    _check(ranks, o, [rand_pod(rng, k, names) for k in range(80)], chunk=32)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_small_cluster_with_empty_shards(world):
+    rng, cfg, nodes, existing, names = rand_cluster(41, n_nodes=130, n_existing=30)
+    ranks, o = _group(world, cfg, nodes, existing)
+    _check(ranks, o, [rand_pod(rng, k, names) for k in range(40)])
+
+
+def test_ties_follow_heap_preorder_across_shards():
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(2000, 0, 300)
+    ranks, o = _group(4, {}, nodes, init)
+    _check(ranks, o, pods, chunk=100)
+
+
+def test_c4_topology_spreading_sharded():
+    from ksg.synth import topology_spreading
+    nodes, init, pods = topology_spreading(2000, 2000, 100)
+    ranks, o = _group(2, {}, nodes, init)
+    _check(ranks, o, pods, chunk=50)
+
+
+def test_c4_preferred_anti_affinity_sharded():
+    from ksg.synth import topology_spreading
+    nodes, init, pods = topology_spreading(1500, 1500, 80, preferred_anti=True)
+    ranks, o = _group(3, {}, nodes, init)
+    _check(ranks, o, pods, chunk=40)
+
+
+def test_c3_pod_affinity_sharded():
+    from ksg.synth import scheduling_pod_affinity
+    nodes, init, pods = scheduling_pod_affinity(1000, 1000, 100)
+    ranks, o = _group(2, {}, nodes, init)
+    _check(ranks, o, pods, chunk=50)
+
+
+def test_eval_output_is_refused_when_sharded():
+    from ksg.abi import KsgError
+    rng, cfg, nodes, existing, names = rand_cluster(5, n_nodes=50, n_existing=5)
+    ranks, _ = _group(2, cfg, nodes, existing)
+    h = ranks[0].compile(rand_pod(rng, 0, names))
+    with pytest.raises(KsgError, match="not gathered"):
+        ranks[0].schedule_one(h, evaluate=True)
