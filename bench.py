@@ -45,13 +45,15 @@ def parse():
     ap.add_argument("--nodes", type=int, default=None, help="cluster nodes at N=1 (c2-c4: 5000, c5: 100000)")
     ap.add_argument("--init-pods", type=int, default=None, help="bound pods at N=1 (c2-c4: 1000, c5: 10000)")
     ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"], help="multi-GPU mode (N>1)")
+    ap.add_argument("--shard-single", action="store_true",
+                    help="run the node-sharded pipeline (RCCL transport) even at N=1 -- a check of that path")
     ap.add_argument("--node-scaling", default=None, choices=["weak", "strong"],
                     help="sharded mode: grow the cluster with N (weak) or keep it fixed (strong)")
     ap.add_argument("--batch", type=int, default=1000)
     ap.add_argument("--timing-stride", type=int, default=8, help="time every k-th filter kernel with HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_filter_score.json"),
+    ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
 
@@ -104,7 +106,7 @@ def main():
     from ksg import synth
 
     c5 = a.workload == "c5"
-    sharded = world > 1 and a.mode == "sharded"
+    sharded = (world > 1 and a.mode == "sharded") or a.shard_single
     scaling = a.node_scaling or ("strong" if c5 else "weak")
     grow = world if (sharded and scaling == "weak") else 1
     n_nodes = (a.nodes or (100000 if c5 else 5000)) * grow
@@ -123,7 +125,8 @@ def main():
     cfg = {"device": local, "kernelTimingStride": a.timing_stride}
     if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
         obj = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(obj, src=0)
         cfg["distributed"] = {"worldSize": world, "rank": rank, "ncclId": obj[0]}
     else:
         for k, p in enumerate(pods):  # distinct uids per rank (independent replicas)
@@ -169,12 +172,14 @@ def main():
     evals_s = pods_s * n_nodes
     kms = sum(k[0] for k in kstats) / len(kstats)
     kbytes = sum(k[1] for k in kstats) / len(kstats)
+    kname = max(set(k[3] for k in kstats), key=lambda nm: sum(1 for k in kstats if k[3] == nm))
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
-    if os.path.exists(a.traffic):
+    tpath = a.traffic or os.path.join(ROOT, "profiles", f"traffic_{kname}.json")
+    if os.path.exists(tpath):
         try:
-            tj = json.load(open(a.traffic))
-            if tj.get("nodes") == n_nodes and world == 1:
+            tj = json.load(open(tpath))
+            if tj.get("nodes") == n_nodes and world == 1 and tj.get("workload", "c2") == a.workload:
                 traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
@@ -210,7 +215,7 @@ def main():
                        "parallelism": (f"nodes-sharded{world} (RCCL all-reduce per pod)" if sharded
                                        else f"replicas{world}" if world > 1 else "single")},
             "placed": placed,
-            "roofline": {"bound": "hbm", "kernel": "k_filter_score", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "avg_kernel_us": round(kms * 1e3, 3),
                          "algo_bytes_per_launch": round(kbytes, 1)},

@@ -26,6 +26,8 @@ constexpr int kPortSlots = 8;    // used-port slots per node (grown by the host 
 constexpr int kMaxCons = 8;      // PodTopologySpread constraints per kind per pod
 constexpr int kMaxPodTerms = 8;  // InterPodAffinity terms per kind per pod
 constexpr int kMaxShards = 8;    // node shards (GPUs) of one node-sharded scheduler
+constexpr int kBlobLds = 16384;  // pod programs up to this size are staged in LDS by the kernels
+constexpr int kLoopMaxBlk = 4;   // k_sched_loop: node blocks per workgroup (scores kept in registers)
 
 // ---- selector programs (labels.Selector / nodeaffinity terms compiled to slots) ----------
 enum SelOp : int32_t {
@@ -142,6 +144,7 @@ enum DescFlags : uint32_t {
   DF_SCORE_ERROR = 1u << 12,       // PreScore/Score returns Error: the cycle fails iff scoring runs (F > 1)
   DF_NODE_LIST = 1u << 13,         // plugin-eval mode: only the nodes in the bitmap at node_list_off are listed
   DF_AGGREGATE = 1u << 14,         // PTS/IPA counts: k_aggregate runs before the node pass
+  DF_FAST = 1u << 15,              // default-plugin shape: straight-line cpu/mem Fit + BalancedAllocation (eval_node_fast)
 };
 
 struct PodDesc {
@@ -308,6 +311,19 @@ struct ShardView {
   unsigned long long* xa;     // [pods][XA_WORDS]
   unsigned long long* xp;     // [pods][XP_WORDS]
   unsigned long long* xb;     // [pods][XB_WORDS]
+};
+
+// ---- persistent scheduling loop (k_sched_loop) -------------------------------------
+// One launch evaluates a run of consecutive pods: `nwg` resident workgroups each own a contiguous
+// range of node blocks for the whole run and meet at two device-scope arrival counters per pod.
+struct LoopView {
+  int32_t first_pod, npods;  // pods [first_pod, first_pod + npods) of the batch
+  int32_t nwg;               // workgroups (all resident; one per CU at most)
+  int32_t nblocks;           // kBlock-node blocks of the snapshot
+  unsigned long long* gran;  // [npods][nwg][3] exchange granules (zeroed by the host per batch)
+  uint32_t* fail;            // set when a spin gives up (a workgroup never arrived)
+  unsigned long long* stamps;  // diagnostic build only: [npods][8] s_memrealtime per phase (nullptr)
+  const uint32_t* desc_bytes;  // [batch pods] program sizes (indexed like BatchView::desc_off)
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -175,6 +175,29 @@ __device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const P
   return go_div(100 * (sum - minT), maxT - minT);
 }
 
+// ---- diagnostic build (make DIAG=1 -> lib/libksg_diag.so): per-step stamps inside eval_node ----------
+#ifdef KSG_DIAG
+__device__ unsigned long long* g_diag;  // [64] slots, workgroup 0 lane 0, last pod wins
+__shared__ unsigned long long s_diag[24];  // stamps land in LDS (a global store's ack would skew the next one)
+#define DIAG_STAMP(k)                                                                       \
+  do {                                                                                      \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                             \
+    if (blockIdx.x == 0 && threadIdx.x == 0) s_diag[k] = __builtin_amdgcn_s_memrealtime();  \
+  } while (0)
+#define DIAG_FLUSH()                                                                        \
+  do {                                                                                      \
+    if (g_diag && blockIdx.x == 0 && threadIdx.x == 0)                                      \
+      for (int k_ = 0; k_ < 24; ++k_) g_diag[k_] = s_diag[k_];                              \
+  } while (0)
+#else
+#define DIAG_FLUSH() \
+  do {               \
+  } while (0)
+#define DIAG_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 // ---- filters ------------------------------------------------------------------------------------
 // Returns the packed Filter status of node i (0 = Success), first failing plugin in the
 // RunFilterPlugins order wins.  *raw_taint gets the PreferNoSchedule count while the taint
@@ -318,19 +341,24 @@ struct NodeEval {
   uint32_t st;      // packed Filter status (0 = feasible)
   bool pts;         // feasible and not ignored by PodTopologySpread scoring
   int64_t rt, rna, ripa;  // raw TaintToleration / NodeAffinity / InterPodAffinity scores
+  int64_t fixed;    // weighted sum of the non-normalising scores (Fit, BalancedAllocation, ImageLocality)
 };
 
 // RunFilterPlugins + the raw Score of every active plugin for node i (framework.go:1105-1138,
-// 1378-1402); writes the node's status word, the weighted sum of the non-normalising scores and
-// the raw scores the normalising plugins need.
+// 1378-1402).  kStore: write the node's status word (evaluation output), the weighted sum of the
+// non-normalising scores and the raw scores the normalising plugins need to the batch scratch
+// (the launch path's k_select reads them back; the persistent loop keeps them in registers).
+template <bool kStore>
 __device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d, int pod,
                               int i, bool valid) {
   const bool eval = (d.flags & DF_EVAL_OUT) != 0;
-  NodeEval r{0u, false, 0, 0, 0};
+  NodeEval r{0u, false, 0, 0, 0, 0};
   uint32_t st = 0;
   int64_t raw_taint = 0;
   NodeCore nc{};
+  DIAG_STAMP(0);
   if (valid) nc = load_core(m, i);
+  DIAG_STAMP(1);
   if (valid) {
     if (d.flags & DF_PREFILTER_REJECT) {
       st = pack_status((uint32_t)d.prefilter_code, (uint32_t)d.prefilter_plugin & 15u, KSG_R_PREFILTER);
@@ -349,8 +377,9 @@ __device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uin
                 : 0u;
       st = f;
     }
-    b.status[i] = st;
+    if (kStore && eval) b.status[i] = st;
   }
+  DIAG_STAMP(2);
   r.st = valid ? st : 1u;
   if (!valid || st != 0) return r;
 
@@ -366,13 +395,20 @@ __device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uin
     r.rna = sc;
   }
   int64_t rf = 0, rb = 0, ri = 0;
+  DIAG_STAMP(3);
   if ((sm >> P_FIT) & 1u) { rf = fit_score(m, nc, base, d, i); fixed += rf * d.weight[P_FIT]; }
+  DIAG_STAMP(4);
   if ((sm >> P_BAL) & 1u) { rb = balanced_alloc_score(m, nc, base, d, i); fixed += rb * d.weight[P_BAL]; }
+  DIAG_STAMP(5);
   if ((sm >> P_IMG) & 1u) { ri = image_score(m, base, d, i); fixed += ri * d.weight[P_IMG]; }
-  b.fixed[i] = fixed;
-  if ((sm >> P_TAINT) & 1u) b.raw[P_TAINT * cap + i] = r.rt;
-  if ((sm >> P_NA) & 1u) b.raw[P_NA * cap + i] = r.rna;
-  if (eval) {
+  DIAG_STAMP(6);
+  r.fixed = fixed;
+  if (kStore) {
+    b.fixed[i] = fixed;
+    if ((sm >> P_TAINT) & 1u) b.raw[P_TAINT * cap + i] = r.rt;
+    if ((sm >> P_NA) & 1u) b.raw[P_NA * cap + i] = r.rna;
+  }
+  if (kStore && eval) {
     b.raw[P_FIT * cap + i] = rf;
     b.raw[P_BAL * cap + i] = rb;
     b.raw[P_IMG * cap + i] = ri;
@@ -385,7 +421,7 @@ __device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uin
       if (v >= 0) sc += (int64_t)b.arena[tk[k].base + v];
     }
     r.ripa = sc;
-    b.raw[P_IPA * cap + i] = sc;
+    if (kStore) b.raw[P_IPA * cap + i] = sc;
   }
   // PodTopologySpread PreScore over the feasible list: ignored nodes and per-constraint domain
   // counts feed the normalising weights (podtopologyspread/scoring.go:61-115)
@@ -403,19 +439,195 @@ __device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uin
       }
     }
   }
+  DIAG_STAMP(7);
+  return r;
+}
+
+// ---- the pod program in LDS ------------------------------------------------------------------------
+// Every node thread reads the same PodDesc fields and blob arrays, often behind data-dependent
+// branches; read from global memory they are re-fetched at L2 latency after every store the
+// compiler cannot prove disjoint.  Programs up to kBlobLds bytes are staged in LDS once per
+// workgroup (16 B per thread per step); larger ones run from global memory (kLds = false).
+__device__ __forceinline__ void stage_blob(const uint8_t* g, uint32_t bytes, uint8_t* lds) {
+  const uint4* src = reinterpret_cast<const uint4*>(g);
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  for (uint32_t o = threadIdx.x; o < bytes / 16u; o += kBlock) dst[o] = src[o];
+}
+
+// =====================================================================================================
+// eval_node_fast -- the default-plugin shape, straight-line (DF_FAST, set by the host compiler)
+// =====================================================================================================
+// Pods whose NodeResourcesFit scores exactly cpu+memory (LeastAllocated / MostAllocated), whose
+// BalancedAllocation uses cpu+memory, that request no extended resources, have no PreFilterResult
+// subset and no image present in the cluster.  The pod's parameters are read from the LDS program
+// once per pod into registers (PodFast); the node's filters and the two score chains are
+// branch-light straight-line code the compiler can interleave.  Same arithmetic as the generic
+// path (fit.go:647-734, least_allocated.go:30-61, most_allocated.go:55-65,
+// balanced_allocation.go:204-254).
+struct PodFast {
+  uint32_t flags, fm, sm;
+  int32_t node_name, n_taint_words, untol_off, intol_off, fit_any, most;
+  int64_t req_cpu, req_mem, req_eph;
+  int64_t fw_cpu, fw_mem, fpr_cpu, fpr_mem;  // Fit score: weights, pod requests (non-zero defaults)
+  int64_t bpr_cpu, bpr_mem;                  // BalancedAllocation pod requests
+  int64_t wt_fit, wt_bal;
+};
+__device__ __forceinline__ PodFast load_fast(const uint8_t* base, const PodDesc& d) {
+  PodFast f;
+  f.flags = d.flags;
+  f.fm = d.filter_mask;
+  f.sm = d.score_mask;
+  f.node_name = d.node_name;
+  f.n_taint_words = d.n_taint_words;
+  f.untol_off = d.untol_ns_off;
+  f.intol_off = d.intol_pns_off;
+  f.fit_any = d.fit_any;
+  f.most = d.fit_strategy == 1;
+  f.req_cpu = d.req_cpu;
+  f.req_mem = d.req_mem;
+  f.req_eph = d.req_eph;
+  const ScoreRes* fr = at<ScoreRes>(base, d.fit_res_off);
+  const ScoreRes* br = at<ScoreRes>(base, d.bal_res_off);
+  f.fw_cpu = fr[0].weight;
+  f.fw_mem = fr[1].weight;
+  f.fpr_cpu = fr[0].pod_req;
+  f.fpr_mem = fr[1].pod_req;
+  f.bpr_cpu = br[0].pod_req;
+  f.bpr_mem = br[1].pod_req;
+  f.wt_fit = d.weight[P_FIT];
+  f.wt_bal = d.weight[P_BAL];
+  return f;
+}
+// floor(a / b) for 0 <= a < 2^52, 0 < b < 2^52 (host-checked bounds): correctly rounded FP64
+// quotient, truncated, fixed up by one with the exact remainder
+__device__ __forceinline__ int64_t fdiv52(int64_t a, int64_t b) {
+  int64_t q = (int64_t)((double)a / (double)b);
+  const int64_t r = a - q * b;
+  q -= r < 0 ? 1 : 0;
+  q += r >= b ? 1 : 0;
+  return q;
+}
+// balanced_allocation.go:220-254 for the (cpu, memory) pair
+__device__ __forceinline__ int64_t bal2(int64_t rc, int64_t ac, int64_t rm, int64_t am) {
+  double f0 = ac != 0 ? (double)rc / (double)ac : 0.0;
+  double f1 = am != 0 ? (double)rm / (double)am : 0.0;
+  f0 = f0 > 1 ? 1 : f0;
+  f1 = f1 > 1 ? 1 : f1;
+  double sd = 0.0;
+  if (ac != 0 && am != 0) sd = fabs((f0 - f1) / 2);
+  const double om = 1 - sd;
+  const double sc = om * 100.0;
+  return (int64_t)sc;
+}
+__device__ NodeEval eval_node_fast(const MirrorView& m, const PodFast& pf, const uint8_t* base, const PodDesc& d,
+                                   int i, bool valid) {
+  NodeEval r{1u, false, 0, 0, 0, 0};
+  if (!valid) return r;
+  DIAG_STAMP(8);
+  const NodeCore nc = load_core(m, i);
+  DIAG_STAMP(9);
+  bool untol = false;
+  int64_t tcnt = 0;
+  for (uint32_t q = nc.tlo; q < nc.thi; ++q) {
+    const uint32_t id = m.taint_ids[q];
+    untol |= bit(base, pf.untol_off, id, pf.n_taint_words);
+    tcnt += bit(base, pf.intol_off, id, pf.n_taint_words) ? 1 : 0;
+  }
+  DIAG_STAMP(10);
+  // Fit filter inputs (fit.go:650-699): independent of the filter order, computed up front
+  const bool too_many = (int64_t)nc.npods + 1 > (int64_t)nc.apods;
+  const bool ic = pf.fit_any && pf.req_cpu > 0 && pf.req_cpu > nc.acpu - nc.rcpu;
+  const bool im = pf.fit_any && pf.req_mem > 0 && pf.req_mem > nc.amem - nc.rmem;
+  const bool ie = pf.fit_any && pf.req_eph > 0 && pf.req_eph > nc.aeph - nc.reph;
+  uint32_t st = 0;
+  const uint32_t fm = pf.fm;
+  if (((fm >> P_UNSCHED) & 1u) && (nc.flags & 1u) && !(pf.flags & DF_TOLERATES_UNSCHED)) {
+    st = pack_status(C_UU, P_UNSCHED, KSG_R_UNSCHEDULABLE);
+  } else if (((fm >> P_NODENAME) & 1u) && pf.node_name != -1 && pf.node_name != i) {
+    st = pack_status(C_UU, P_NODENAME, KSG_R_NODE_NAME);
+  } else if (((fm >> P_TAINT) & 1u) && untol) {
+    st = pack_status(C_UU, P_TAINT, KSG_R_TAINT);
+  } else {
+    if ((fm >> P_NA) & 1u) {  // NodeAffinity (node_affinity.go:207-228), generic programs
+      if ((pf.flags & DF_HAS_ADDED_NA) && !prog_any(m, base, d, d.na_added, i))
+        st = pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_ENFORCED);
+      else if ((pf.flags & DF_HAS_SELECTOR) && !prog_any(m, base, d, d.na_selector, i))
+        st = pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_POD);
+      else if ((pf.flags & DF_HAS_REQUIRED_NA) && !prog_any(m, base, d, d.na_required, i))
+        st = pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_POD);
+    }
+    if (st == 0 && ((fm >> P_PORTS) & 1u)) {  // NodePorts
+      const uint32_t* slots = m.ports + (size_t)i * kPortSlots;
+      for (int k = 0; k < kPortSlots; ++k) {
+        const uint32_t pid = slots[k];
+        if (pid != 0xffffffffu && bit(base, d.port_conflict_off, pid, d.n_port_words)) {
+          st = pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
+          break;
+        }
+      }
+    }
+    if (st == 0 && ((fm >> P_FIT) & 1u) && (too_many || ic || im || ie)) {
+      const uint32_t reasons = (too_many ? KSG_R_TOO_MANY_PODS : 0u) | (ic ? KSG_R_INSUFFICIENT_CPU : 0u) |
+                               (im ? KSG_R_INSUFFICIENT_MEMORY : 0u) | (ie ? KSG_R_INSUFFICIENT_EPHEMERAL : 0u);
+      const bool unres = (ic && pf.req_cpu > nc.acpu) || (im && pf.req_mem > nc.amem) || (ie && pf.req_eph > nc.aeph);
+      st = pack_status(unres ? C_UU : C_UNSCHED, P_FIT, reasons);
+    }
+  }
+  r.st = st;
+  DIAG_STAMP(11);
+  if (st != 0) return r;
+  const uint32_t sm = pf.sm;
+  r.rt = ((sm >> P_TAINT) & 1u) ? tcnt : 0;
+  if ((sm >> P_NA) & 1u) {
+    int64_t sc = 0;
+    if (pf.flags & DF_HAS_ADDED_PREF) sc += prog_weight(m, base, d, d.na_added_pref, i);
+    if (pf.flags & DF_HAS_PREF_NA) sc += prog_weight(m, base, d, d.na_preferred, i);
+    r.rna = sc;
+  }
+  int64_t fixed = 0;
+  DIAG_STAMP(12);
+  if ((sm >> P_FIT) & 1u) {  // resource_allocation.go:138-165 with cpu (NonZeroRequested) and memory
+    const int64_t qc = nc.nzcpu + pf.fpr_cpu, qm = nc.nzmem + pf.fpr_mem;
+    int64_t sc, smm;
+    if (pf.most) {  // most_allocated.go:55-65
+      sc = nc.acpu != 0 ? fdiv52((qc > nc.acpu ? nc.acpu : qc) * 100, nc.acpu) : 0;
+      smm = nc.amem != 0 ? fdiv52((qm > nc.amem ? nc.amem : qm) * 100, nc.amem) : 0;
+    } else {  // least_allocated.go:52-61
+      sc = nc.acpu != 0 && qc <= nc.acpu ? fdiv52((nc.acpu - qc) * 100, nc.acpu) : 0;
+      smm = nc.amem != 0 && qm <= nc.amem ? fdiv52((nc.amem - qm) * 100, nc.amem) : 0;
+    }
+    const int64_t ws = (nc.acpu != 0 ? pf.fw_cpu : 0) + (nc.amem != 0 ? pf.fw_mem : 0);
+    const int64_t num = (nc.acpu != 0 ? sc * pf.fw_cpu : 0) + (nc.amem != 0 ? smm * pf.fw_mem : 0);
+    fixed += (ws == 0 ? 0 : go_div(num, ws)) * pf.wt_fit;
+  }
+  DIAG_STAMP(13);
+  if ((sm >> P_BAL) & 1u) {  // balanced_allocation.go:204-218 (Requested, useRequested=true)
+    const int64_t with = bal2(nc.rcpu + pf.bpr_cpu, nc.acpu, nc.rmem + pf.bpr_mem, nc.amem);
+    const int64_t without = bal2(nc.rcpu, nc.acpu, nc.rmem, nc.amem);
+    fixed += (100 / 2 + (100 / 2 + with - without) / 2) * pf.wt_bal;
+  }
+  r.fixed = fixed;  // ImageLocality: no image of the pod exists in the cluster -> 0 (host-checked)
+  DIAG_STAMP(14);
   return r;
 }
 
 // =====================================================================================================
 // k_filter_score
 // =====================================================================================================
+template <bool kLds>
 __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView b, int pod, int blk0) {
+  __shared__ __align__(16) uint8_t s_blob[kLds ? kBlobLds : 16];
   const uint8_t* base = b.descs + b.desc_off[pod];
+  if constexpr (kLds) {
+    stage_blob(base, reinterpret_cast<const PodDesc*>(base)->blob_bytes, s_blob);
+    __syncthreads();
+    base = s_blob;
+  }
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   const int blk = blk0 + (int)blockIdx.x;  // node-sharded launches cover blocks [blk0, blk0 + gridDim.x)
   const int i = blk * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const NodeEval ne = eval_node(m, b, base, d, pod, i, i < m.n);
+  const NodeEval ne = eval_node<true>(m, b, base, d, pod, i, i < m.n);
   const bool feas = ne.st == 0;
   const unsigned long long ballot = __ballot(feas);
   if (lane == 0) b.fmask[(size_t)blk * (kBlock / 64) + wave] = ballot;
@@ -715,8 +927,15 @@ __device__ __forceinline__ uint32_t winner_rank(unsigned long long best, uint32_
   return g;
 }
 
+template <bool kLds>
 __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, int pod, int nblocks) {
+  __shared__ __align__(16) uint8_t s_blob[kLds ? kBlobLds : 16];
   const uint8_t* base = b.descs + b.desc_off[pod];
+  if constexpr (kLds) {
+    stage_blob(base, reinterpret_cast<const PodDesc*>(base)->blob_bytes, s_blob);
+    __syncthreads();
+    base = s_blob;
+  }
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -938,6 +1157,319 @@ __global__ __launch_bounds__(kBlock) void k_max_reduce(unsigned long long* dst, 
   }
 }
 
+// =====================================================================================================
+// k_sched_loop -- the persistent scheduling loop
+// =====================================================================================================
+// One launch schedules a run of consecutive pods (node-local plugins only: no pod-table
+// aggregation).  Workgroup w owns the node blocks [k0, k1) (at most kLoopMaxBlk) for the whole
+// run, so the AssumePod of a pod is applied by the owner of the chosen node and only ever read back
+// by that same workgroup: the mirror needs no cross-workgroup hand-off.  Per pod:
+//   stage    the pod program into LDS (issued for pod q+1 before pod q's second exchange)
+//   phase 1  RunFilterPlugins + raw scores of my nodes; the fixed score and the raw normalising
+//            scores stay in registers, the feasibility ballots in LDS
+//   xchg A   every workgroup publishes two 8-byte granules {valid, feasible count | count before
+//            nextStartNodeIndex} and {valid, max raw TaintToleration + 1 | max raw NodeAffinity + 1};
+//            one wave per workgroup sweeps all of them (the data is the flag: R2 of the hand-off
+//            recipe -- no fences, no counters)
+//   phase 2  positions in the rotated feasible list, NormalizeScore + weights, packed
+//            (TotalScore, heap pre-order key) max of my nodes
+//   xchg B   one granule {valid, key} per workgroup, swept the same way; the thread holding the
+//            global maximum applies AssumePod and writes the result.
+// Granules live in a per-batch array zeroed by the host; every granule is written exactly once.
+constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr unsigned long long kValid = 1ull << 63;
+
+// diagnostic phase stamps (config "loopStamps"): workgroup 0's lane 0, 100 MHz constant clock
+__device__ __forceinline__ void stamp(const LoopView& lv, int q, int k) {
+  if (lv.stamps && threadIdx.x == 0) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// One wave: poll granules g[v * stride + off] for v < G until all are valid (relaxed agent-scope
+// loads, s_sleep between passes).  Fills x[] (up to kMaxSweep per lane); false on give-up.
+constexpr int kMaxSweep = 4;  // G <= 256 workgroups
+__device__ __forceinline__ bool sweep(const unsigned long long* g, int G, int stride, int off,
+                                      unsigned long long (&x)[kMaxSweep], uint32_t* fail) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kMaxSweep; ++r) {
+      const int v = lane + 64 * r;
+      x[r] = v < G ? __hip_atomic_load(g + (size_t)v * stride + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : kValid;
+      ok &= (x[r] & kValid) != 0;
+    }
+    if (__all(ok)) return true;
+    if (spins >= kSpinLimit) {
+      __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if ((spins & 63u) == 63u && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// the two granules of exchange A in one pass per poll
+__device__ __forceinline__ bool sweep2(const unsigned long long* g, int G, unsigned long long (&x0)[kMaxSweep],
+                                       unsigned long long (&x1)[kMaxSweep], uint32_t* fail) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kMaxSweep; ++r) {
+      const int v = lane + 64 * r;
+      x0[r] = v < G ? __hip_atomic_load(g + (size_t)v * 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kValid;
+      x1[r] = v < G ? __hip_atomic_load(g + (size_t)v * 3 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kValid;
+      ok &= (x0[r] & x1[r] & kValid) != 0;
+    }
+    if (__all(ok)) return true;
+    if (spins >= kSpinLimit) {
+      __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if ((spins & 63u) == 63u && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// NormalizeScore + weights for the loop's plugin set (TaintToleration, NodeAffinity normalised;
+// Fit / BalancedAllocation / ImageLocality already in `fixed`) -- framework.go:1409-1452
+__device__ __forceinline__ int64_t loop_total(const PodDesc& d, int64_t fixed, int64_t rt, int64_t rn, int64_t mx_t,
+                                              int64_t mx_n) {
+  if (d.flags & DF_NO_SCORE) return 1;
+  int64_t total = fixed;
+  const uint32_t sm = d.score_mask;
+  if ((sm >> P_TAINT) & 1u) total += (mx_t == 0 ? 100 : 100 - go_div(100 * rt, mx_t)) * d.weight[P_TAINT];
+  if ((sm >> P_NA) & 1u) total += (mx_n == 0 ? 0 : go_div(100 * rn, mx_n)) * d.weight[P_NA];
+  return total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
+  __shared__ __align__(16) uint8_t s_blob[kBlobLds];
+  __shared__ unsigned long long s_ball[kLoopMaxBlk][kBlock / 64];
+  __shared__ int64_t s_fx[kLoopMaxBlk][kBlock], s_rt[kLoopMaxBlk][kBlock], s_rn[kLoopMaxBlk][kBlock];
+  __shared__ uint32_t s_u[2][kBlock / 64];
+  __shared__ unsigned long long s_x[2][kBlock / 64];
+  __shared__ uint32_t s_ok, s_F, s_pre, s_before;
+  __shared__ unsigned long long s_mt, s_mn, s_best;
+  const int w = blockIdx.x, G = lv.nwg;
+  const int k0 = (int)((int64_t)lv.nblocks * w / G), k1 = (int)((int64_t)lv.nblocks * (w + 1) / G);
+  const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long* gran = lv.gran;  // [npods][G][3]
+
+  // prefetch registers for the next pod program (16 B per thread per step; the rest synchronously)
+  constexpr int kPre = 2;
+  uint4 pre[kPre];
+  uint32_t pre_bytes = 0;
+  auto fetch = [&](int pod) {  // offsets/sizes of the batch's programs: two independent loads
+    const uint8_t* g = b.descs + b.desc_off[pod];
+    pre_bytes = lv.desc_bytes[pod];
+#pragma unroll
+    for (int r = 0; r < kPre; ++r) {
+      const uint32_t o = threadIdx.x + (uint32_t)r * kBlock;
+      if (o < pre_bytes / 16u) pre[r] = reinterpret_cast<const uint4*>(g)[o];
+    }
+  };
+  auto land = [&](int pod) {  // write the prefetched part, load the remainder
+    uint4* dst = reinterpret_cast<uint4*>(s_blob);
+#pragma unroll
+    for (int r = 0; r < kPre; ++r) {
+      const uint32_t o = threadIdx.x + (uint32_t)r * kBlock;
+      if (o < pre_bytes / 16u) dst[o] = pre[r];
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(b.descs + b.desc_off[pod]);
+    for (uint32_t o = threadIdx.x + kPre * kBlock; o < pre_bytes / 16u; o += kBlock) dst[o] = src[o];
+  };
+  if (lv.npods > 0) fetch(lv.first_pod);
+
+  for (int q = 0; q < lv.npods; ++q) {
+    const int pod = lv.first_pod + q;
+    land(pod);
+    __syncthreads();
+    const uint8_t* base = s_blob;
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    PodStats* ps = b.stats + pod;
+    const int s = d.rot_start;
+    unsigned long long* gq = gran + (size_t)q * G * 3;
+
+    // ---- phase 1: RunFilterPlugins + raw scores of my nodes (scores stay in LDS, own slots)
+    if (w == 0) stamp(lv, q, 0);
+    unsigned long long mt = 0, mn = 0;
+    uint32_t cnt = 0, below = 0;
+    DIAG_STAMP(16);
+    const bool fast = (d.flags & DF_FAST) != 0;
+    const PodFast pf = load_fast(base, d);
+    DIAG_STAMP(17);
+#pragma unroll 1
+    for (int kk = 0; kk < nk; ++kk) {
+      const int i = (k0 + kk) * kBlock + threadIdx.x;
+      const NodeEval ne = fast ? eval_node_fast(m, pf, base, d, i, i < m.n) : eval_node<false>(m, b, base, d, pod, i, i < m.n);
+      const bool feas = ne.st == 0;
+      const unsigned long long ballot = __ballot(feas);
+      if (lane == 0) s_ball[kk][wave] = ballot;
+      s_fx[kk][threadIdx.x] = ne.fixed;
+      s_rt[kk][threadIdx.x] = ne.rt;
+      s_rn[kk][threadIdx.x] = ne.rna;
+      if (feas) {
+        const unsigned long long et = enc_i64(ne.rt), en = enc_i64(ne.rna);
+        mt = et > mt ? et : mt;
+        mn = en > mn ? en : mn;
+        cnt += 1;
+        below += i < s ? 1u : 0u;
+      }
+    }
+    DIAG_STAMP(18);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cnt += __shfl_xor(cnt, o, 64);
+      below += __shfl_xor(below, o, 64);
+    }
+    mt = wave_max_u64(mt);
+    mn = wave_max_u64(mn);
+    if (lane == 0) {
+      s_u[0][wave] = cnt;
+      s_u[1][wave] = below;
+      s_x[0][wave] = mt;
+      s_x[1][wave] = mn;
+    }
+    __syncthreads();
+    if (w == 0) stamp(lv, q, 1);
+
+    // ---- exchange A
+    if (wave == 0) {
+      if (lane == 0) {
+        uint32_t c = 0, bl = 0;
+        unsigned long long a = 0, bb = 0;
+        for (int v = 0; v < kBlock / 64; ++v) {
+          c += s_u[0][v];
+          bl += s_u[1][v];
+          a = s_x[0][v] > a ? s_x[0][v] : a;
+          bb = s_x[1][v] > bb ? s_x[1][v] : bb;
+        }
+        // raw scores are >= 0 and bounded (host-checked): +1 so that 0 means "no feasible node"
+        const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;
+        const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;
+        __hip_atomic_store(gq + (size_t)w * 3, kValid | ((unsigned long long)bl << 24) | c, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gq + (size_t)w * 3 + 1, kValid | (np1 << 31) | tp1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (w == 0) stamp(lv, q, 2);
+      unsigned long long x0[kMaxSweep], x1[kMaxSweep];
+      const bool ok = sweep2(gq, G, x0, x1, lv.fail);
+      uint32_t F = 0, wp = 0, bf = 0;
+      unsigned long long tmax = 0, nmax = 0;
+#pragma unroll
+      for (int r = 0; r < kMaxSweep; ++r) {
+        const int v = lane + 64 * r;
+        if (v < G) {
+          const uint32_t c = (uint32_t)(x0[r] & 0xffffffull);
+          F += c;
+          if (v < w) wp += c;
+          bf += (uint32_t)((x0[r] >> 24) & 0xffffffull);
+          const unsigned long long t = x1[r] & 0x7fffffffull, n = (x1[r] >> 31) & 0xffffffffull;
+          tmax = t > tmax ? t : tmax;
+          nmax = n > nmax ? n : nmax;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        F += __shfl_xor(F, o, 64);
+        wp += __shfl_xor(wp, o, 64);
+        bf += __shfl_xor(bf, o, 64);
+        const unsigned long long t2 = __shfl_xor(tmax, o, 64), n2 = __shfl_xor(nmax, o, 64);
+        tmax = t2 > tmax ? t2 : tmax;
+        nmax = n2 > nmax ? n2 : nmax;
+      }
+      if (lane == 0) {
+        s_ok = ok ? 1u : 0u;
+        s_F = F;
+        s_pre = wp;
+        s_before = bf;
+        s_mt = tmax;
+        s_mn = nmax;
+      }
+      if (w == 0) stamp(lv, q, 3);
+    }
+    __syncthreads();
+    if (!s_ok) return;
+
+    // ---- phase 2: positions, NormalizeScore + weights, my best packed key
+    const uint32_t F = s_F, ps_before = s_before;
+    const int64_t mx_t = s_mt ? (int64_t)s_mt - 1 : 0, mx_n = s_mn ? (int64_t)s_mn - 1 : 0;
+    unsigned long long key = 0;
+    int knode = -1;
+    uint32_t acc = s_pre;  // feasible nodes before node block kk of my range
+#pragma unroll 1
+    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+      if (kk < nk) {
+        uint32_t wbefore = 0, tot = 0;
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+          const uint32_t pc = (uint32_t)__popcll(s_ball[kk][v]);
+          wbefore += v < wave ? pc : 0u;
+          tot += pc;
+        }
+        const unsigned long long ballot = s_ball[kk][wave];
+        if ((ballot >> lane) & 1ull) {
+          const uint32_t g = acc + wbefore + wave_prefix_count(ballot, lane);
+          const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
+          const unsigned long long kv = pack_best(
+              loop_total(d, s_fx[kk][threadIdx.x], s_rt[kk][threadIdx.x], s_rn[kk][threadIdx.x], mx_t, mx_n), pos);
+          if (kv > key) {
+            key = kv;
+            knode = (k0 + kk) * kBlock + (int)threadIdx.x;
+          }
+        }
+        acc += tot;
+      }
+    }
+    const unsigned long long wkey = wave_max_u64(key);
+    if (lane == 0) s_x[0][wave] = wkey;
+    __syncthreads();
+    if (w == 0) stamp(lv, q, 4);
+    // the next pod's program: issue its loads now, they land after exchange B
+    if (q + 1 < lv.npods) fetch(pod + 1);
+
+    // ---- exchange B
+    if (wave == 0) {
+      if (lane == 0) {
+        unsigned long long kk = 0;
+        for (int v = 0; v < kBlock / 64; ++v) kk = s_x[0][v] > kk ? s_x[0][v] : kk;
+        __hip_atomic_store(gq + (size_t)w * 3 + 2, kValid | kk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (w == 0) stamp(lv, q, 5);
+      unsigned long long xb[kMaxSweep];
+      const bool ok = sweep(gq, G, 3, 2, xb, lv.fail);
+      unsigned long long bm = 0;
+#pragma unroll
+      for (int r = 0; r < kMaxSweep; ++r) {
+        const unsigned long long v = (lane + 64 * r) < G ? (xb[r] & ~kValid) : 0ull;
+        bm = v > bm ? v : bm;
+      }
+      bm = wave_max_u64(bm);
+      if (lane == 0) {
+        s_ok = ok ? 1u : 0u;
+        s_best = bm;
+      }
+      if (w == 0) stamp(lv, q, 6);
+    }
+    __syncthreads();
+    if (!s_ok) return;
+
+    // ---- the thread holding the winning key (keys are unique: positions are) assumes + reports
+    const unsigned long long best = s_best;
+    if (F == 0) {
+      if (w == 0 && threadIdx.x == 0) commit_result(m, b, base, d, ps, pod, F, -1, best);
+    } else if (key == best && knode >= 0) {
+      commit_result(m, b, base, d, ps, pod, F, knode, best);
+    }
+    DIAG_FLUSH();
+    __syncthreads();  // the assume lands before my next pod's phase 1; s_blob is free again
+  }
+}
+
 }  // namespace ksg
 
 // ---- host-side launchers (C++ linkage, called by the host library) ------------------------------
@@ -946,18 +1478,28 @@ namespace ksg {
 // their elapsed time is the kernel's own begin/end -- the same interval rocprofv3 reports.
 // blk0/nblk: the node blocks to evaluate (nblk < 0: all of them).
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
-                               hipEvent_t t1, int blk0, int nblk) {
+                               hipEvent_t t1, int blk0, int nblk, bool lds) {
   if (nblk < 0) nblk = (m.n + kBlock - 1) / kBlock;
   if (nblk == 0) return hipSuccess;
-  if (t0)
-    hipExtLaunchKernelGGL(k_filter_score, dim3(nblk), dim3(kBlock), 0, s, t0, t1, 0, m, b, pod, blk0);
-  else
-    hipLaunchKernelGGL(k_filter_score, dim3(nblk), dim3(kBlock), 0, s, m, b, pod, blk0);
+  if (lds) {
+    if (t0)
+      hipExtLaunchKernelGGL(k_filter_score<true>, dim3(nblk), dim3(kBlock), 0, s, t0, t1, 0, m, b, pod, blk0);
+    else
+      hipLaunchKernelGGL(k_filter_score<true>, dim3(nblk), dim3(kBlock), 0, s, m, b, pod, blk0);
+  } else {
+    if (t0)
+      hipExtLaunchKernelGGL(k_filter_score<false>, dim3(nblk), dim3(kBlock), 0, s, t0, t1, 0, m, b, pod, blk0);
+    else
+      hipLaunchKernelGGL(k_filter_score<false>, dim3(nblk), dim3(kBlock), 0, s, m, b, pod, blk0);
+  }
   return hipGetLastError();
 }
-hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
+hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, bool lds) {
   const int nb = (m.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_select, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
+  if (lds)
+    hipLaunchKernelGGL(k_select<true>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
+  else
+    hipLaunchKernelGGL(k_select<false>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
   return hipGetLastError();
 }
 hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
@@ -987,4 +1529,15 @@ hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int n
   hipLaunchKernelGGL(k_max_reduce, dim3(nb < 64 ? (nb > 0 ? nb : 1) : 64), dim3(kBlock), 0, s, dst, src, nsrc, count);
   return hipGetLastError();
 }
+hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
+                             hipEvent_t t0, hipEvent_t t1) {
+  if (t0)
+    hipExtLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kBlock), 0, s, t0, t1, 0, m, b, lv);
+  else
+    hipLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kBlock), 0, s, m, b, lv);
+  return hipGetLastError();
+}
+#ifdef KSG_DIAG
+hipError_t set_diag(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &p, sizeof(p)); }
+#endif
 }  // namespace ksg

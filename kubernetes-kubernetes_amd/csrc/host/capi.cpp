@@ -67,7 +67,7 @@ ksg_ctx* ksg_create(const char* config_json, size_t len) {
       return nullptr;
     }
     ctx->engine.reset(new Engine(ctx->cluster.get()));
-    if (cfg.world > 1) {  // node-sharded: join the exchange group (collective across the ranks)
+    if (cfg.sharded()) {  // node-sharded: join the exchange group (collective across the ranks)
       std::string err;
       ctx->engine->comm = make_comm(cfg, &err);
       if (!ctx->engine->comm) {
@@ -272,8 +272,9 @@ int ksg_shard_range(const ksg_ctx* ctx, int32_t* first_node, int32_t* num_nodes)
 }
 
 int ksg_last_batch_kernel_stats(const ksg_ctx* ctx, double* avg_kernel_ms, double* bytes_per_launch,
-                                int32_t* launches) {
+                                int32_t* launches, int32_t* kernel) {
   if (!ctx) return KSG_EINVAL;
+  if (kernel) *kernel = ctx->engine->last_kernel;
   if (avg_kernel_ms) *avg_kernel_ms = ctx->engine->last_kernel_ms;
   if (bytes_per_launch) *bytes_per_launch = ctx->engine->last_bytes;
   if (launches) *launches = ctx->engine->last_launches;

@@ -192,6 +192,8 @@ void Cluster::intern_node(NodeRec& r) {
       if (s >= 0) r.scalar_alloc[s] += milli_ceil(a.milli);
     }
   }
+  // magnitude bound of cpu/memory allocatable ever seen (eval_node_fast's FP64 division domain)
+  for (int64_t v : {r.alloc_cpu, r.alloc_mem}) alloc_bound = std::max(alloc_bound, v < 0 ? INT64_MAX : v);
 }
 
 int Cluster::add_node(NodeSpec&& n) {
@@ -362,6 +364,7 @@ int Cluster::ensure_mirror() {
       zcpu(cap, 0), zmem(cap, 0);
   std::vector<int32_t> apods(cap, 0), npods(cap, 0);
   std::vector<uint32_t> flags(cap, 0), toff(cap + 1, 0), ioff(cap + 1, 0), tids, iids;
+  int64_t taint_max = 0;
   std::vector<int64_t> salloc((size_t)cap * kMaxScalar, 0), sreq((size_t)cap * kMaxScalar, 0);
   std::vector<uint32_t> ports((size_t)cap * kPortSlots, 0xffffffffu);
   for (int32_t i = 0; i < n; ++i) {
@@ -381,6 +384,7 @@ int Cluster::ensure_mirror() {
     for (auto& kv : r.scalar_req) sreq[(size_t)kv.first * cap + i] = kv.second;
     toff[i] = (uint32_t)tids.size();
     tids.insert(tids.end(), r.taint_ids.begin(), r.taint_ids.end());
+    taint_max = std::max<int64_t>(taint_max, (int64_t)r.taint_ids.size());
     ioff[i] = (uint32_t)iids.size();
     iids.insert(iids.end(), r.image_ids.begin(), r.image_ids.end());
     if (r.ports.size() > (size_t)kPortSlots) { err = "node " + r.spec.name + " uses more host ports than supported"; return KSG_ENOTSUP; }
@@ -392,6 +396,7 @@ int Cluster::ensure_mirror() {
     ioff[i] = (uint32_t)iids.size();
   }
   taint_ids_per_node = n ? (double)tids.size() / n : 0.0;
+  taint_max_per_node = taint_max;
   img_ids_per_node = n ? (double)iids.size() / n : 0.0;
   view.taint_ids = (uint32_t*)dalloc(std::max<size_t>(tids.size(), 1) * 4);
   view.img_ids = (uint32_t*)dalloc(std::max<size_t>(iids.size(), 1) * 4);

@@ -164,7 +164,7 @@ class LocalComm : public Comm {
 };
 
 std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err) {
-  if (cfg.world <= 1) return nullptr;
+  if (!cfg.sharded()) return nullptr;
   if (!cfg.nccl_id.empty()) {
     ncclUniqueId id;
     if (!hex_to_id(cfg.nccl_id, &id)) {

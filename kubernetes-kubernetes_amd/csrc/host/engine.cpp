@@ -13,6 +13,7 @@
 // round trip inside the batch (device-side AssumePod), and reads the results back once.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 #include "comm.hpp"
@@ -20,9 +21,9 @@
 
 namespace ksg {
 
-hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0 = nullptr,
-                               hipEvent_t t1 = nullptr, int blk0 = 0, int nblk = -1);
-hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
+                               hipEvent_t t1, int blk0, int nblk, bool lds);
+hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, bool lds);
 hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, const PodDesc& d, hipStream_t s);
 hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0 = 0,
                             int nblk = -1);
@@ -31,6 +32,11 @@ hipError_t launch_unpack_pts(const BatchView& b, const ShardView& sv, int pod, h
 hipError_t launch_xpack_p(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
 hipError_t launch_select_shard(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
 hipError_t launch_commit(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+#ifdef KSG_DIAG
+hipError_t set_diag(unsigned long long* p);
+#endif
+hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
+                             hipEvent_t t0, hipEvent_t t1);
 
 #define HIPCHK(x)                                               \
   do {                                                          \
@@ -527,6 +533,20 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     out->slot = D.slot;
   }
   if (eval) D.flags |= DF_EVAL_OUT;
+  // DF_FAST: the straight-line default-plugin evaluation (kernels.hip eval_node_fast)
+  {
+    const uint32_t topo = (1u << P_PTS) | (1u << P_IPA);
+    const bool shape = fr.size() == 2 && fr[0].kind == RES_CPU && fr[1].kind == RES_MEM && br.size() == 2 &&
+                       br[0].kind == RES_CPU && br[1].kind == RES_MEM && (cfg.fit_strategy == 0 || cfg.fit_strategy == 1);
+    // PodTopologySpread / InterPodAffinity filters with nothing to check (no constraints, no terms,
+    // no existing anti-affinity) leave their mask bits set but never reject: not a reason to leave
+    const bool topo_filter = D.n_ptsf > 0 || D.n_raff > 0 || D.n_ranti > 0 || (D.ipa_flags & IPA_EXIST_FILTER);
+    if (mode == CYCLE && shape && D.n_scalar == 0 && !topo_filter && !(smask & topo) &&
+        (D.n_img == 0 || !(smask & (1u << P_IMG))) &&
+        !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR)) &&
+        c->alloc_bound < ((int64_t)1 << 52) / 100)
+      D.flags |= DF_FAST;
+  }
   B.finish();
   out->blob = std::move(B.b);
   return KSG_OK;
@@ -782,6 +802,32 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
 Engine::Engine(Cluster* cl) : c(cl) {
   (void)hipEventCreate(&ev0);
   (void)hipEventCreate(&ev1);
+  if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, c->cfg.device) != hipSuccess)
+    cu_count = 0;
+}
+
+// A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
+// PodTopologySpread / InterPodAffinity scores, no per-node evaluation output).
+bool Engine::loop_ok(const CompiledPod& p) const {
+  if (p.error) return false;
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
+  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE)) return false;
+  if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
+  if (p.blob.size() > (size_t)kBlobLds) return false;
+  // the exchange granules carry raw TaintToleration counts in 31 bits, raw NodeAffinity sums in
+  // 32 bits and the packed key in 63 bits: bound the pod's possible values
+  int64_t wsum = 0;
+  for (int q = 0; q < kNumPlugins; ++q) {
+    if (d.weight[q] < 0) return false;
+    wsum += (d.score_mask >> q) & 1u ? d.weight[q] : 0;
+  }
+  if (wsum > ((int64_t)1 << 26)) return false;  // TotalScore <= 100 * wsum < 2^33, key < 2^62
+  int64_t pref = 0;
+  for (SelProg pg : {d.na_preferred, d.na_added_pref}) {
+    const SelTerm* t = reinterpret_cast<const SelTerm*>(p.blob.data() + pg.term_off);
+    for (int k = 0; k < pg.nterm; ++k) pref += t[k].weight < 0 ? -(int64_t)t[k].weight : t[k].weight;
+  }
+  return pref < ((int64_t)1 << 31);
 }
 // Algorithmic HBM bytes of one k_filter_score launch: every SoA field the pod's active plugins
 // must read for a node, plus what the launch writes, each counted once per node.
@@ -815,8 +861,9 @@ double Engine::algo_bytes(const PodDesc& d) const {
 
 Engine::~Engine() {
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : lev) (void)hipEventDestroy(e);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb})
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_wgcnt, &d_fail})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -839,7 +886,7 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena
   const size_t nb = cap / kBlock + 1;
   int rc;
   if ((rc = ensure(d_descs, desc_bytes))) return rc;
-  if ((rc = ensure(d_off, (size_t)pods * 4))) return rc;
+  if ((rc = ensure(d_off, (size_t)pods * 8))) return rc;
   if ((rc = ensure(d_stats, (size_t)pods * sizeof(PodStats)))) return rc;
   if ((rc = ensure(d_results, (size_t)pods * sizeof(DevResult)))) return rc;
   if ((rc = ensure(d_status, cap * 4))) return rc;
@@ -862,7 +909,7 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena
     if ((rc = ensure(d_arena, (size_t)arena_words * 8 + 8))) return rc;
     if (d_arena.bytes != old) HIPCHK(hipMemsetAsync(d_arena.p, 0, d_arena.bytes, c->stream));
   }
-  const size_t need = desc_bytes + (size_t)pods * (4 + sizeof(PodStats) + sizeof(DevResult)) + 256;
+  const size_t need = desc_bytes + (size_t)pods * (8 + sizeof(PodStats) + sizeof(DevResult)) + 256;
   if (h_pinned_bytes < need) {
     if (h_pinned) (void)hipHostFree(h_pinned);
     h_pinned = nullptr;
@@ -942,7 +989,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     o += cp[i].blob.size();
   }
   std::memcpy(hp + o, offs.data(), (size_t)n * 4);
-  PodStats* hs = (PodStats*)(hp + ((o + (size_t)n * 4 + 15) & ~size_t(15)));
+  for (int i = 0; i < n; ++i) {  // program sizes follow the offsets (k_sched_loop's prefetch)
+    const uint32_t sz = (uint32_t)cp[i].blob.size();
+    std::memcpy(hp + o + (size_t)(n + i) * 4, &sz, 4);
+  }
+  PodStats* hs = (PodStats*)(hp + ((o + (size_t)n * 8 + 15) & ~size_t(15)));
   for (int i = 0; i < n; ++i) {
     std::memset(&hs[i], 0, sizeof(PodStats));
     for (int q = 0; q < kNumPlugins; ++q) {
@@ -953,7 +1004,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   hipStream_t s = c->stream;
   const MirrorView& m = c->view;
   HIPCHK(hipMemcpyAsync(d_descs.p, hp, o, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d_off.p, hp + o, (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_off.p, hp + o, (size_t)n * 8, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(d_stats.p, hs, (size_t)n * sizeof(PodStats), hipMemcpyHostToDevice, s));
   if (eval) {
     HIPCHK(hipMemsetAsync(d_out.p, 0, (size_t)m.cap * 8 * kNumPlugins, s));
@@ -973,21 +1024,66 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (comm) {
     if ((rc = run_sharded(cp, bv, n, &launches, &bytes, &timed))) return rc;
   }
-  for (int i = 0; i < n && !comm; ++i) {
-    if (cp[i].error) continue;
+  // persistent-loop geometry: G resident workgroups, each <= 64 node blocks (k_sched_loop)
+  const int NB = (m.n + kBlock - 1) / kBlock;
+  const int max_wg = std::min(256, cu_count > 0 ? cu_count : 256);  // one resident workgroup per CU at most
+  int G = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
+  G = std::min(std::max(G, (NB + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(NB, max_wg));
+  const bool use_loop = !comm && !eval && c->cfg.persistent_loop && NB > 0 && (int64_t)G * kLoopMaxBlk >= NB &&
+                        (int64_t)c->taint_max_per_node < ((int64_t)1 << 30);
+  struct LoopRun { int first, count; double bytes; };
+  std::vector<LoopRun> runs;
+  if (use_loop) {
+    if ((rc = ensure(d_wgcnt, (size_t)n * G * 3 * 8))) return rc;
+    if ((rc = ensure(d_fail, 16))) return rc;
+    HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
+    HIPCHK(hipMemsetAsync(d_wgcnt.p, 0, (size_t)n * G * 3 * 8, s));  // every granule invalid
+    if (c->cfg.loop_stamps) {
+      if ((rc = ensure(d_stamps, (size_t)n * 8 * 8 + 64 * 8))) return rc;
+      HIPCHK(hipMemsetAsync(d_stamps.p, 0, (size_t)n * 8 * 8 + 64 * 8, s));
+#ifdef KSG_DIAG
+      HIPCHK(set_diag((unsigned long long*)d_stamps.p + (size_t)n * 8));
+#endif
+    }
+  }
+  for (int i = 0; i < n && !comm;) {
+    if (cp[i].error) {
+      ++i;
+      continue;
+    }
+    if (use_loop && loop_ok(cp[i])) {  // a run of node-local pods: one k_sched_loop launch
+      int j = i;
+      double rb = 0;
+      while (j < n && loop_ok(cp[j])) rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data()));
+      while (lev.size() < 2 * (runs.size() + 1)) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        lev.push_back(e);
+      }
+      LoopView lv{i, j - i, G, NB, (unsigned long long*)d_wgcnt.p + (size_t)i * G * 3, (uint32_t*)d_fail.p,
+                  c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr,
+                  (const uint32_t*)d_off.p + n};
+      HIPCHK(launch_sched_loop(m, bv, lv, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
+      runs.push_back({i, j - i, rb});
+      launches += j - i;
+      i = j;
+      continue;
+    }
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
+    const bool lds = cp[i].blob.size() <= (size_t)kBlobLds;
     if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));
     const bool t = stride > 0 && i % stride == 0;
     if (t) {
-      HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1]));
+      HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1], 0, -1, lds));
       timed++;
     } else {
-      HIPCHK(launch_filter_score(m, bv, i, s));
+      HIPCHK(launch_filter_score(m, bv, i, s, nullptr, nullptr, 0, -1, lds));
     }
     if (hd.score_mask & (1u << P_PTS)) HIPCHK(launch_pts_score(m, bv, i, s));
-    HIPCHK(launch_select(m, bv, i, s));
-    bytes += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[i].blob.data()));
+    HIPCHK(launch_select(m, bv, i, s, lds));
+    bytes += algo_bytes(hd);
     launches++;
+    ++i;
   }
   HIPCHK(hipEventRecord(ev1, s));
   DevResult* hr = (DevResult*)(hs + n);
@@ -1007,6 +1103,14 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     c->err = comm->err;
     return KSG_EDEVICE;
   }
+  if (!runs.empty()) {
+    uint32_t fail = 0;
+    HIPCHK(hipMemcpy(&fail, d_fail.p, 4, hipMemcpyDeviceToHost));
+    if (fail) {
+      c->err = "k_sched_loop: a workgroup never reached a per-pod arrival counter (spin limit)";
+      return KSG_EDEVICE;
+    }
+  }
   float ms = 0;
   (void)hipEventElapsedTime(&ms, ev0, ev1);
   last_kernel_ms = launches ? ms / (2.0 * launches) : 0;
@@ -1021,6 +1125,59 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   last_bytes = launches ? bytes / launches : 0;
   last_launches = launches;
+  last_kernel = 0;
+  if (!runs.empty()) {  // the loop dominates: per-pod time inside k_sched_loop and bytes per pod
+    double lms = 0, lb = 0;
+    int lp = 0;
+    for (size_t r = 0; r < runs.size(); ++r) {
+      float x = 0;
+      HIPCHK(hipEventElapsedTime(&x, lev[2 * r], lev[2 * r + 1]));
+      lms += x;
+      lb += runs[r].bytes;
+      lp += runs[r].count;
+    }
+    if (lp * 2 >= launches) {
+      last_kernel = 1;
+      last_kernel_ms = lms / lp;
+      last_bytes = lb / lp;
+    }
+    if (c->cfg.loop_stamps) {  // mean per-phase time (us) of the looped pods, workgroup 0's view
+      std::vector<unsigned long long> st((size_t)n * 8);
+      HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+      double acc[8] = {0};
+      int cnt = 0;
+      for (auto& r : runs)
+        for (int q = r.first; q < r.first + r.count; ++q) {
+          const unsigned long long* t = &st[(size_t)q * 8];
+          const unsigned long long nxt = q + 1 < r.first + r.count ? st[(size_t)(q + 1) * 8] : 0;
+          if (!t[0] || !t[6] || !nxt) continue;
+          for (int k = 1; k <= 6; ++k) acc[k] += (double)(t[k] - t[k - 1]) / 100.0;
+          acc[7] += (double)(nxt - t[6]) / 100.0;
+          cnt++;
+        }
+#ifdef KSG_DIAG
+      {
+        unsigned long long dg[20];
+        HIPCHK(hipMemcpy(dg, (unsigned long long*)d_stamps.p + (size_t)n * 8, sizeof dg, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[fast path of the last pod, us] load_fast %.3f | load_core %.3f taints %.3f filters %.3f "
+                     "nascore %.3f fit %.3f balanced %.3f | loop body total %.3f\n", (dg[17] - dg[16]) / 100.0,
+                     (dg[9] - dg[8]) / 100.0, (dg[10] - dg[9]) / 100.0, (dg[11] - dg[10]) / 100.0,
+                     (dg[12] - dg[11]) / 100.0, (dg[13] - dg[12]) / 100.0, (dg[14] - dg[13]) / 100.0,
+                     (dg[18] - dg[17]) / 100.0);
+        std::fprintf(stderr, "[eval_node steps of the last pod, us] load_core %.3f filters %.3f pre-score %.3f fit %.3f "
+                     "balanced %.3f image %.3f rest %.3f\n", (dg[1] - dg[0]) / 100.0, (dg[2] - dg[1]) / 100.0,
+                     (dg[3] - dg[2]) / 100.0, (dg[4] - dg[3]) / 100.0, (dg[5] - dg[4]) / 100.0,
+                     (dg[6] - dg[5]) / 100.0, (dg[7] - dg[6]) / 100.0);
+      }
+#endif
+      if (cnt)
+        std::fprintf(stderr,
+                     "[k_sched_loop stamps, %d pods, us] phase1 %.3f publishA %.3f waitA %.3f phase2 %.3f "
+                     "publishB %.3f waitB %.3f phase3+next %.3f\n",
+                     cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt,
+                     acc[7] / cnt);
+    }
+  }
 
   // ---- results + host shadow of the device-side assumes
   for (int i = 0; i < n; ++i) {
@@ -1112,10 +1269,11 @@ int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv,
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
     if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));  // replicated pod table
     if (stride > 0 && i % stride == 0 && sv.nblk > 0) {
-      HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1], sv.blk0, sv.nblk));
+      HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1], sv.blk0, sv.nblk,
+                                 cp[i].blob.size() <= (size_t)kBlobLds));
       timed++;
     } else {
-      HIPCHK(launch_filter_score(m, bv, i, s, nullptr, nullptr, sv.blk0, sv.nblk));
+      HIPCHK(launch_filter_score(m, bv, i, s, nullptr, nullptr, sv.blk0, sv.nblk, cp[i].blob.size() <= (size_t)kBlobLds));
     }
     HIPCHK(launch_xpack_a(bv, sv, i, s));
     const bool pts = (hd.score_mask & (1u << P_PTS)) != 0;
@@ -1194,10 +1352,11 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
   HIPCHK(hipMemsetAsync(d_out.p, 0, (size_t)m.cap * 8 * kNumPlugins, s));
   const BatchView bv = bview(1);
   if (D.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, 0, D, s));
-  HIPCHK(launch_filter_score(m, bv, 0, s));
+  const bool lds = cp.blob.size() <= (size_t)kBlobLds;
+  HIPCHK(launch_filter_score(m, bv, 0, s, nullptr, nullptr, 0, -1, lds));
   if (mode == SCORE_ONE) {
     if (D.score_mask & (1u << P_PTS)) HIPCHK(launch_pts_score(m, bv, 0, s));
-    HIPCHK(launch_select(m, bv, 0, s));
+    HIPCHK(launch_select(m, bv, 0, s, lds));
   } else if (D.arena_words) {
     HIPCHK(hipMemsetAsync(d_arena.p, 0, (size_t)D.arena_words * 8, s));  // k_select did not run
   }

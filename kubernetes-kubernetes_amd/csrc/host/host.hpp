@@ -142,10 +142,15 @@ struct Config {
   std::vector<std::pair<int32_t, NSTerm>> added_pref;
   int device = 0;
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
+  bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
+  int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
+  bool loop_stamps = false;     // diagnostic: per-phase s_memrealtime stamps of k_sched_loop (stderr)
   // node-sharded evaluation: this context evaluates the snapshot-order block range of `rank`
   // out of `world`; the per-pod exchanges run over RCCL (nccl_id) or in-process (local_group)
   int world = 1, rank = 0;
   std::string nccl_id, local_group;
+  // a transport was configured: run the node-sharded pipeline even at worldSize 1 (tests it alone)
+  bool sharded() const { return world > 1 || !nccl_id.empty() || !local_group.empty(); }
   Config();
 };
 bool decode_config(const char* p, size_t n, Config* c, std::string* err);
@@ -280,6 +285,8 @@ class Cluster {
   int upload_node_dynamic(int32_t idx);      // push one node's Requested/ports to HBM
   int64_t next_start = 0;                    // Scheduler.nextStartNodeIndex
   double taint_ids_per_node = 0, img_ids_per_node = 0;  // CSR densities (algorithmic-bytes model)
+  int64_t taint_max_per_node = 0;                        // bounds k_sched_loop's raw-score granules
+  int64_t alloc_bound = 0;                               // max cpu/memory allocatable seen (INT64_MAX: a negative one)
 
  private:
   std::vector<std::string> zones_;
@@ -353,6 +360,9 @@ class Engine {
   double algo_bytes(const PodDesc& d) const;
   double last_kernel_ms = 0, last_bytes = 0;
   int32_t last_launches = 0;
+  int32_t last_kernel = 0;  // 0: k_filter_score figures; 1: k_sched_loop (per-pod time in the loop)
+  int cu_count = 0;
+  bool loop_ok(const CompiledPod& p) const;
   // node-sharded evaluation (cfg.world > 1): this rank's block range + the exchange transport
   std::unique_ptr<Comm> comm;
   int32_t shard_blk0 = 0, shard_nblk = -1;
@@ -363,6 +373,8 @@ class Engine {
   DevBuf d_descs, d_off, d_stats, d_results, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
   DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)
   DevBuf d_xa, d_xp, d_xb;  // node-sharded exchange vectors, one set per pod of the batch
+  DevBuf d_wgcnt, d_fail, d_stamps;  // k_sched_loop: per-pod per-workgroup counts, give-up flag, stamps
+  std::vector<hipEvent_t> lev;  // k_sched_loop timing events (pairs)
   int run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int n, int* launches, double* bytes,
                   int* timed);
   void* h_pinned = nullptr;

@@ -490,6 +490,9 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     if (const JVal* fg = d.get(r, "featureGates")) c->taint_cmp_ops = d.boolean(*fg, "TaintTolerationComparisonOperators");
     c->device = (int)d.num(r, "device", 0);
     c->timing_stride = (int)d.num(r, "kernelTimingStride", 0);
+    if (const JVal* pl = d.get(r, "persistentLoop")) c->persistent_loop = pl->type == JVal::BOOL && pl->b;
+    c->loop_wg = (int)d.num(r, "loopWorkgroups", 0);
+    c->loop_stamps = d.boolean(r, "loopStamps");
     if (const JVal* ds = d.get(r, "distributed")) {  // node-sharded evaluation
       c->world = (int)d.num(*ds, "worldSize", 1);
       c->rank = (int)d.num(*ds, "rank", 0);
@@ -499,7 +502,8 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
         *err = "distributed: worldSize must be in [1, 8] and 0 <= rank < worldSize";
         return false;
       }
-      if (c->world > 1 && c->nccl_id.empty() == c->local_group.empty()) {
+      if ((c->world > 1 || !c->nccl_id.empty() || !c->local_group.empty()) &&
+          c->nccl_id.empty() == c->local_group.empty()) {
         *err = "distributed: exactly one of ncclId (RCCL) or localGroup (in-process ranks) is required";
         return false;
       }

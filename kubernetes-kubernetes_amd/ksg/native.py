@@ -10,7 +10,7 @@ import os
 from .abi import Backend, KsgError
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(PKG, "lib", "libksg.so")
+LIB = os.environ.get("KSG_LIB") or os.path.join(PKG, "lib", "libksg.so")  # KSG_LIB: the diagnostic build
 HEADER = os.path.join(os.path.dirname(PKG), "include", "ksg.h")
 
 _lib = None
@@ -25,7 +25,7 @@ def load():
         lib = C.CDLL(LIB)
         lib.ksg_last_batch_kernel_stats.restype = C.c_int
         lib.ksg_last_batch_kernel_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
-                                                    C.POINTER(C.c_int32)]
+                                                    C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         lib.ksg_comm_unique_id.restype = C.c_int
         lib.ksg_comm_unique_id.argtypes = [C.c_char_p, C.c_size_t]
         lib.ksg_create_error.restype = C.c_char_p
@@ -42,11 +42,12 @@ class Scheduler(Backend):
         super().__init__(load(), "ksg_", config)
 
     def kernel_stats(self):
-        """(avg per-kernel ms, algorithmic bytes per launch, kernel pairs) of the last batch."""
-        ms, by, n = C.c_double(), C.c_double(), C.c_int32()
-        self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n)),
+        """(avg ms, algorithmic bytes, pods, kernel name) of the last batch: per k_filter_score
+        launch, or per pod inside the persistent k_sched_loop when most pods ran there."""
+        ms, by, n, k = C.c_double(), C.c_double(), C.c_int32(), C.c_int32()
+        self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n), C.byref(k)),
                   "kernel_stats")
-        return ms.value, by.value, n.value
+        return ms.value, by.value, n.value, ("k_sched_loop" if k.value == 1 else "k_filter_score")
 
     def shard_range(self):
         """(first snapshot index, node count) this rank evaluates (node-sharded contexts)."""

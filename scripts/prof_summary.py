@@ -1,9 +1,10 @@
 """Summarise rocprofv3 rocpd databases (gpurun_out/prof/*) into committed text/JSON under profiles/.
 
-  python scripts/prof_summary.py <tag> [nodes]
+  python scripts/prof_summary.py <tag> [nodes] [workload] [pods_per_loop_dispatch]
 writes profiles/<tag>_kernel_stats.txt (per-kernel calls / total / average duration, the
 `--kernel-trace --stats` summary), profiles/<tag>_pmc.txt (FETCH_SIZE / WRITE_SIZE per kernel),
-and profiles/traffic_k_filter_score.json (HBM bytes per k_filter_score launch for bench.py).
+and profiles/traffic_<kernel>.json (HBM bytes per k_filter_score launch, or per pod of a
+k_sched_loop dispatch, for bench.py's roofline.traffic).
 """
 import json
 import os
@@ -21,6 +22,8 @@ def short(name):
 def main():
     tag = sys.argv[1]
     nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
+    workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
+    loop_pods = int(sys.argv[4]) if len(sys.argv) > 4 else 1000
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     c = sqlite3.connect(os.path.join(PROF, "trace", "run_results.db"))
@@ -30,11 +33,15 @@ def main():
     for n, calls, tot, avg, pct in rows:  # top_kernels is in us; kernels.duration is ns
         lines.append(f"{short(n):60s} {calls:8d} {tot:12.1f} {avg:9.3f} {pct:6.2f}")
     # per-dispatch durations of the roofline kernel
-    d = [r[0] for r in c.execute("select duration from kernels where name like '%k_filter_score%'")]
-    if d:
-        d.sort()
-        lines.append(f"k_filter_score dispatch duration us: median {d[len(d) // 2] / 1e3:.3f} "
-                     f"p10 {d[len(d) // 10] / 1e3:.3f} p90 {d[9 * len(d) // 10] / 1e3:.3f}")
+    for kn in ("k_filter_score", "k_sched_loop"):
+        d = [r[0] for r in c.execute(f"select duration from kernels where name like '%{kn}%'")]
+        if d:
+            d.sort()
+            lines.append(f"{kn} dispatch duration us: median {d[len(d) // 2] / 1e3:.3f} "
+                         f"p10 {d[len(d) // 10] / 1e3:.3f} p90 {d[9 * len(d) // 10] / 1e3:.3f}")
+            if kn == "k_sched_loop":
+                lines.append(f"k_sched_loop per pod us ({loop_pods} pods per dispatch): median "
+                             f"{d[len(d) // 2] / 1e3 / loop_pods:.3f}")
     open(os.path.join(out, f"{tag}_kernel_stats.txt"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
@@ -50,22 +57,26 @@ def main():
     pl = [f"# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB per dispatch (tag {tag})",
           "# gfx950: FETCH_SIZE under-reports wide streaming reads by 2x (MI355X_MICROARCH.md HBM section);",
           "# the access widths here are 4-8 B/lane (uncalibrated) -- both raw and x2 are listed."]
-    traffic = None
+    traffic = {}
     for k, v in sorted(per.items()):
         f = v.get("FETCH_SIZE", [])
         w = v.get("WRITE_SIZE", [])
         fa = sum(f) / len(f) if f else 0.0
         wa = sum(w) / len(w) if w else 0.0
         pl.append(f"{k:60s} dispatches {len(f):6d} FETCH_KiB {fa:10.2f} (x2 {2 * fa:10.2f}) WRITE_KiB {wa:10.2f}")
-        if k.endswith("k_filter_score"):
-            traffic = {"nodes": nodes, "fetch_kib_raw": fa, "write_kib": wa,
-                       "bytes_per_launch": round((fa + wa) * 1024.0, 1),
-                       "bytes_per_launch_fetch_x2": round((2 * fa + wa) * 1024.0, 1),
-                       "note": "FETCH_SIZE+WRITE_SIZE per k_filter_score dispatch, separate PMC passes"}
+        for kn, per_unit in (("k_filter_score", 1), ("k_sched_loop", loop_pods)):
+            if k.endswith(kn):
+                traffic[kn] = {"kernel": kn, "nodes": nodes, "workload": workload, "fetch_kib_raw": fa / per_unit,
+                               "write_kib": wa / per_unit,
+                               "bytes_per_launch": round((fa + wa) * 1024.0 / per_unit, 1),
+                               "bytes_per_launch_fetch_x2": round((2 * fa + wa) * 1024.0 / per_unit, 1),
+                               "note": f"FETCH_SIZE+WRITE_SIZE per {kn} dispatch"
+                                       + (f" / {per_unit} pods" if per_unit > 1 else "")
+                                       + ", separate PMC passes (tag " + tag + ")"}
     open(os.path.join(out, f"{tag}_pmc.txt"), "w").write("\n".join(pl) + "\n")
     print("\n".join(pl))
-    if traffic:
-        json.dump(traffic, open(os.path.join(out, "traffic_k_filter_score.json"), "w"), indent=1)
+    for kn, t in traffic.items():
+        json.dump(t, open(os.path.join(out, f"traffic_{kn}.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -176,3 +176,32 @@ def test_c4_topology_spreading_3k(native):
 def test_c4_preferred_anti_affinity_2k(native):
     from ksg.synth import topology_spreading
     _stream(native, *topology_spreading(2000, 2000, 120, preferred_anti=True))
+
+
+@pytest.mark.parametrize("wg", [1, 3, 7, 64, 256])
+def test_persistent_loop_geometries(native, wg):
+    """k_sched_loop with 1..256 workgroups (1 -> one workgroup owns every node block) against the
+    oracle: heterogeneous nodes (untied scores), then all-tied nodes (heap pre-order)."""
+    from ksg.synth import scheduling_basic
+    for hetero, n_nodes in ((True, 3000), (False, 1500)):
+        nodes, init, pods = scheduling_basic(n_nodes, 300, 250, hetero=hetero)
+        g, o = _pair(native, {"loopWorkgroups": wg}, nodes, init)
+        rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+        for k, p in enumerate(pods):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[k].as_tuple() == ro.as_tuple(), f"wg {wg} hetero {hetero} pod {k}"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_persistent_loop_mixed_runs(native, seed):
+    """Random pods: runs of node-local pods go through k_sched_loop, PTS/IPA pods through the
+    per-pod launches, interleaved on one stream -- identical to the loop-less path and the oracle."""
+    rng, cfg, nodes, existing, names = rand_cluster(5000 + seed, n_nodes=800, n_existing=80)
+    g, o = _pair(native, cfg, nodes, existing)
+    g2, _ = _pair(native, dict(cfg, persistentLoop=False), nodes, existing)
+    pods = [rand_pod(rng, k, names) for k in range(120)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"

@@ -134,3 +134,23 @@ def test_eval_output_is_refused_when_sharded():
     h = ranks[0].compile(rand_pod(rng, 0, names))
     with pytest.raises(KsgError, match="not gathered"):
         ranks[0].schedule_one(h, evaluate=True)
+
+
+def test_rccl_transport_single_rank_matches_oracle():
+    """The RCCL transport itself (ncclGetUniqueId -> ncclCommInitRank -> in-stream ncclAllReduce
+    MAX between the kernels) at worldSize 1 -- the one-GPU box cannot host two RCCL ranks."""
+    from ksg.native import Scheduler, comm_unique_id
+    rng, cfg, nodes, existing, names = rand_cluster(4242, n_nodes=900, n_existing=80)
+    s = Scheduler(dict(cfg, device=0, distributed={"worldSize": 1, "rank": 0, "ncclId": comm_unique_id()}))
+    o = oracle(cfg)
+    for b in (s, o):
+        for ns in namespaces():
+            b.upsert_namespace(ns)
+        for n in nodes:
+            b.add_node(n)
+        for p in existing:
+            b.add_pod(p)
+    pods = [rand_pod(rng, k, names) for k in range(80)]
+    got = [r.as_tuple() for r in s.schedule_batch([s.compile(p) for p in pods], assume=True)]
+    for k, p in enumerate(pods):
+        assert got[k] == o.schedule_one(o.compile(p), assume=True)[0].as_tuple(), f"pod {k}"
