@@ -27,7 +27,8 @@ constexpr int kMaxCons = 8;      // PodTopologySpread constraints per kind per p
 constexpr int kMaxPodTerms = 8;  // InterPodAffinity terms per kind per pod
 constexpr int kMaxShards = 8;    // node shards (GPUs) of one node-sharded scheduler
 constexpr int kBlobLds = 16384;  // pod programs up to this size are staged in LDS by the kernels
-constexpr int kLoopMaxBlk = 4;   // k_sched_loop: node blocks per workgroup (scores kept in registers)
+constexpr int kLoopMaxPods = 1024;  // k_sched_loop: pods per launch (their program offsets are staged in LDS)
+constexpr int kLoopMaxBlk = 2;   // k_sched_loop: node blocks per workgroup (cores and scores kept in LDS)
 
 // ---- selector programs (labels.Selector / nodeaffinity terms compiled to slots) ----------
 enum SelOp : int32_t {
@@ -324,6 +325,7 @@ struct LoopView {
   uint32_t* fail;            // set when a spin gives up (a workgroup never arrived)
   unsigned long long* stamps;  // diagnostic build only: [npods][8] s_memrealtime per phase (nullptr)
   const uint32_t* desc_bytes;  // [batch pods] program sizes (indexed like BatchView::desc_off)
+  unsigned long long* wstamps;  // diagnostic: [npods][nwg][2] exchange A / B publish times (nullptr)
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

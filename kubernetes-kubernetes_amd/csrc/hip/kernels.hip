@@ -317,13 +317,37 @@ __device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const u
 }
 
 // ---- wave/block reductions ------------------------------------------------------------------------
+// DPP scan steps (row_shr 1/2/4/8, row_bcast 15/31; disabled or out-of-row lanes contribute 0, the
+// identity of an unsigned max or sum): the wave's result ends in lane 63.  All 64 lanes active.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ unsigned long long dpp_max_step(unsigned long long v) {
+  const unsigned long long w = ((unsigned long long)dpp_u32<kCtrl, kRowMask>((uint32_t)(v >> 32)) << 32) |
+                               dpp_u32<kCtrl, kRowMask>((uint32_t)v);
+  return w > v ? w : v;
+}
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned long long w = __shfl_xor(v, o, 64);
-    v = w > v ? w : v;
-  }
-  return v;
+  v = dpp_max_step<0x111, 0xf>(v);
+  v = dpp_max_step<0x112, 0xf>(v);
+  v = dpp_max_step<0x114, 0xf>(v);
+  v = dpp_max_step<0x118, 0xf>(v);
+  v = dpp_max_step<0x142, 0xa>(v);
+  v = dpp_max_step<0x143, 0xc>(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp_u32<0x111, 0xf>(v);
+  v += dpp_u32<0x112, 0xf>(v);
+  v += dpp_u32<0x114, 0xf>(v);
+  v += dpp_u32<0x118, 0xf>(v);
+  v += dpp_u32<0x142, 0xa>(v);
+  v += dpp_u32<0x143, 0xc>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
@@ -519,12 +543,11 @@ __device__ __forceinline__ int64_t bal2(int64_t rc, int64_t ac, int64_t rm, int6
   const double sc = om * 100.0;
   return (int64_t)sc;
 }
-__device__ NodeEval eval_node_fast(const MirrorView& m, const PodFast& pf, const uint8_t* base, const PodDesc& d,
-                                   int i, bool valid) {
+// nc: node i's core columns -- loaded here (launch path) or held in registers by its owner (k_sched_loop)
+// bal_wo: bal2 of the node without the pod (pod-independent: the loop keeps it per node)
+__device__ __forceinline__ NodeEval eval_core_fast(const MirrorView& m, const NodeCore& nc, int64_t bal_wo,
+                                                   const PodFast& pf, const uint8_t* base, const PodDesc& d, int i) {
   NodeEval r{1u, false, 0, 0, 0, 0};
-  if (!valid) return r;
-  DIAG_STAMP(8);
-  const NodeCore nc = load_core(m, i);
   DIAG_STAMP(9);
   bool untol = false;
   int64_t tcnt = 0;
@@ -603,12 +626,18 @@ __device__ NodeEval eval_node_fast(const MirrorView& m, const PodFast& pf, const
   DIAG_STAMP(13);
   if ((sm >> P_BAL) & 1u) {  // balanced_allocation.go:204-218 (Requested, useRequested=true)
     const int64_t with = bal2(nc.rcpu + pf.bpr_cpu, nc.acpu, nc.rmem + pf.bpr_mem, nc.amem);
-    const int64_t without = bal2(nc.rcpu, nc.acpu, nc.rmem, nc.amem);
-    fixed += (100 / 2 + (100 / 2 + with - without) / 2) * pf.wt_bal;
+    fixed += (100 / 2 + (100 / 2 + with - bal_wo) / 2) * pf.wt_bal;
   }
   r.fixed = fixed;  // ImageLocality: no image of the pod exists in the cluster -> 0 (host-checked)
   DIAG_STAMP(14);
   return r;
+}
+__device__ NodeEval eval_node_fast(const MirrorView& m, const PodFast& pf, const uint8_t* base, const PodDesc& d,
+                                   int i, bool valid) {
+  if (!valid) return NodeEval{1u, false, 0, 0, 0, 0};
+  DIAG_STAMP(8);
+  const NodeCore nc = load_core(m, i);
+  return eval_core_fast(m, nc, bal2(nc.rcpu, nc.acpu, nc.rmem, nc.amem), pf, base, d, i);
 }
 
 // =====================================================================================================
@@ -684,8 +713,9 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
 // =====================================================================================================
 // k_select (+ the node-sharded k_select_shard / k_commit)
 // =====================================================================================================
-__device__ __forceinline__ uint32_t wave_prefix_count(unsigned long long ballot, int lane) {
-  return (uint32_t)__popcll(lane ? (ballot & ((1ull << lane) - 1ull)) : 0ull);
+__device__ __forceinline__ uint32_t wave_prefix_count(unsigned long long ballot, int lane) {  // lanes below mine
+  (void)lane;
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(ballot >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ballot, 0u));
 }
 
 // The maxima / minima the NormalizeScore passes need, gathered over the whole feasible list.
@@ -876,8 +906,12 @@ __device__ bool select_block(const MirrorView& m, const BatchView& b, const PodD
 
 // DevResult + AssumePod of the chosen node (schedule_one.go:1102-1137 -> NodeInfo.update,
 // framework/types.go:445-468) on this replica of the mirror.  One thread.
-__device__ void commit_result(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d,
-                              PodStats* ps, int pod, uint32_t F, int node, unsigned long long best) {
+// returns whether the AssumePod was applied to the mirror.  after/ipa_any (k_sched_loop): the
+// node's core columns with the pod added, already known to the caller, are stored instead of
+// read-modify-written, and the pod's ipa_any flags come from the caller (no load on the path).
+__device__ __forceinline__ bool commit_result(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d,
+                              PodStats* ps, int pod, uint32_t F, int node, unsigned long long best,
+                              const NodeCore* after = nullptr, int ipa_any = -1) {
   const size_t cap = (size_t)m.cap;
   DevResult r;
   r.node = F > 0 ? node : -1;
@@ -886,7 +920,7 @@ __device__ void commit_result(const MirrorView& m, const BatchView& b, const uin
   r.total = F > 0 ? (int64_t)(best >> kPreBits) : 0;
   r.key = best;
   r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
-  r.ipa_any = ps->ipa_any;
+  r.ipa_any = ipa_any >= 0 ? (uint32_t)ipa_any : ps->ipa_any;
   if (d.flags & DF_PREFILTER_REJECT) r.status = (int32_t)C_UNSCHED;
   if ((d.flags & DF_SCORE_ERROR) && F > 1) {  // prioritizeNodes error (schedule_one.go:600-603)
     r.status = (int32_t)C_ERROR;
@@ -895,12 +929,21 @@ __device__ void commit_result(const MirrorView& m, const BatchView& b, const uin
   ps->feasible = F;
   if ((d.flags & DF_ASSUME) && r.node >= 0) {
     const int j = r.node;
-    m.req_cpu[j] += d.a_cpu;
-    m.req_mem[j] += d.a_mem;
-    m.req_eph[j] += d.a_eph;
-    m.nz_cpu[j] += d.a_nz_cpu;
-    m.nz_mem[j] += d.a_nz_mem;
-    m.num_pods[j] += 1;
+    if (after) {
+      m.req_cpu[j] = after->rcpu;
+      m.req_mem[j] = after->rmem;
+      m.req_eph[j] = after->reph;
+      m.nz_cpu[j] = after->nzcpu;
+      m.nz_mem[j] = after->nzmem;
+      m.num_pods[j] = after->npods;
+    } else {
+      m.req_cpu[j] += d.a_cpu;
+      m.req_mem[j] += d.a_mem;
+      m.req_eph[j] += d.a_eph;
+      m.nz_cpu[j] += d.a_nz_cpu;
+      m.nz_mem[j] += d.a_nz_mem;
+      m.num_pods[j] += 1;
+    }
     const ScalarReq* sr = at<ScalarReq>(base, d.a_scalar_off);
     for (int k = 0; k < d.n_a_scalar; ++k) m.scalar_req[(size_t)sr[k].slot * cap + j] += sr[k].qty;
     const uint32_t* pp = at<uint32_t>(base, d.pod_ports_off);
@@ -917,6 +960,7 @@ __device__ void commit_result(const MirrorView& m, const BatchView& b, const uin
     }
   }
   b.results[pod] = r;
+  return (d.flags & DF_ASSUME) && r.node >= 0;
 }
 
 __device__ __forceinline__ uint32_t winner_rank(unsigned long long best, uint32_t ps_before, uint32_t F) {
@@ -1244,120 +1288,270 @@ __device__ __forceinline__ int64_t loop_total(const PodDesc& d, int64_t fixed, i
   return total;
 }
 
-__global__ __launch_bounds__(kBlock) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
-  __shared__ __align__(16) uint8_t s_blob[kBlobLds];
-  __shared__ unsigned long long s_ball[kLoopMaxBlk][kBlock / 64];
-  __shared__ int64_t s_fx[kLoopMaxBlk][kBlock], s_rt[kLoopMaxBlk][kBlock], s_rn[kLoopMaxBlk][kBlock];
-  __shared__ uint32_t s_u[2][kBlock / 64];
-  __shared__ unsigned long long s_x[2][kBlock / 64];
-  __shared__ uint32_t s_ok, s_F, s_pre, s_before;
-  __shared__ unsigned long long s_mt, s_mn, s_best;
+// The loop's node cores live in LDS (structure of arrays, [block of my range][slot]): the
+// evaluation waves read them every pod, the committing thread applies the AssumePod to them and
+// to the mirror alike, and the selection wave reads its candidate's core for the pre-evaluation.
+struct LoopCores {
+  int64_t acpu[kLoopMaxBlk][kBlock], amem[kLoopMaxBlk][kBlock], aeph[kLoopMaxBlk][kBlock];
+  int64_t rcpu[kLoopMaxBlk][kBlock], rmem[kLoopMaxBlk][kBlock], reph[kLoopMaxBlk][kBlock];
+  int64_t nzcpu[kLoopMaxBlk][kBlock], nzmem[kLoopMaxBlk][kBlock];
+  int64_t bwo[kLoopMaxBlk][kBlock];  // BalancedAllocation without the pod (pod-independent)
+  int32_t apods[kLoopMaxBlk][kBlock], npods[kLoopMaxBlk][kBlock];
+  uint32_t flags[kLoopMaxBlk][kBlock], tlo[kLoopMaxBlk][kBlock], thi[kLoopMaxBlk][kBlock];
+};
+__device__ __forceinline__ NodeCore lds_core(const LoopCores& L, int kk, int t) {
+  NodeCore c;
+  c.acpu = L.acpu[kk][t];
+  c.amem = L.amem[kk][t];
+  c.aeph = L.aeph[kk][t];
+  c.rcpu = L.rcpu[kk][t];
+  c.rmem = L.rmem[kk][t];
+  c.reph = L.reph[kk][t];
+  c.nzcpu = L.nzcpu[kk][t];
+  c.nzmem = L.nzmem[kk][t];
+  c.apods = L.apods[kk][t];
+  c.npods = L.npods[kk][t];
+  c.flags = L.flags[kk][t];
+  c.tlo = L.tlo[kk][t];
+  c.thi = L.thi[kk][t];
+  return c;
+}
+__device__ __forceinline__ void lds_put_dynamic(LoopCores& L, int kk, int t, const NodeCore& c) {
+  L.rcpu[kk][t] = c.rcpu;
+  L.rmem[kk][t] = c.rmem;
+  L.reph[kk][t] = c.reph;
+  L.nzcpu[kk][t] = c.nzcpu;
+  L.nzmem[kk][t] = c.nzmem;
+  L.npods[kk][t] = c.npods;
+  L.bwo[kk][t] = bal2(c.rcpu, c.acpu, c.rmem, c.amem);
+}
+// AssumePod's NodeInfo.update on the core columns (framework/types.go:445-468), as commit_result
+__device__ __forceinline__ void assume_core(NodeCore& c, const PodDesc& d) {
+  c.rcpu += d.a_cpu;
+  c.rmem += d.a_mem;
+  c.reph += d.a_eph;
+  c.nzcpu += d.a_nz_cpu;
+  c.nzmem += d.a_nz_mem;
+  c.npods += 1;
+}
+
+// Can pod `nd`'s evaluation of a node be computed, before pod `d` is assumed, as it will be after?
+// Default-plugin pods read nothing an AssumePod changes beyond the core columns, except host ports.
+__device__ __forceinline__ bool post_ok(const PodDesc& d, const PodDesc& nd) {
+  return (d.flags & DF_ASSUME) && (nd.flags & DF_FAST) && !(((nd.filter_mask >> P_PORTS) & 1u) && d.n_pod_ports > 0);
+}
+
+constexpr int kLoopThreads = kBlock + 128;  // four evaluation waves, one selection wave, one helper wave
+
+__global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
+  __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
+  __shared__ LoopCores s_core;
+  __shared__ unsigned long long s_ball[2][kLoopMaxBlk][kBlock / 64];  // [pod parity]
+  // phase-1 slots: weighted fixed score, raw TaintToleration / NodeAffinity scores (< 2^31, host-checked)
+  __shared__ int64_t s_fx[2][kLoopMaxBlk][kBlock];
+  __shared__ uint32_t s_rt[2][kLoopMaxBlk][kBlock], s_rn[2][kLoopMaxBlk][kBlock];
+  // the same for pod q+1 on each node as if pod q were assumed there (default-plugin pods): the
+  // chosen node's next evaluation is ready when the winner is known
+  __shared__ int64_t s_fx2[kLoopMaxBlk][kBlock], s_bwo2[kLoopMaxBlk][kBlock];
+  __shared__ uint32_t s_rt2[kLoopMaxBlk][kBlock], s_rn2[kLoopMaxBlk][kBlock];
+  __shared__ unsigned long long s_ball2[kLoopMaxBlk][kBlock / 64];
+  __shared__ uint32_t s_u[2][2][kBlock / 64];
+  __shared__ unsigned long long s_x[2][2][kBlock / 64];
+  __shared__ uint32_t s_off[kLoopMaxPods], s_len[kLoopMaxPods];  // the run's program offsets / sizes
+  __shared__ uint32_t s_ok, s_F, s_cand_ok;
+  __shared__ int s_win, s_cand_q, s_cand_node, s_ipa;
+  __shared__ unsigned long long s_tm[2][kBlock], s_tn[2][kBlock];  // per-slot maxima of phase 1 (encoded)
+  __shared__ uint32_t s_e_done;  // evaluation waves that finished a phase 1 (monotonic)
+  // the candidate's state if it wins, prepared by the helper wave: its core columns with the pod
+  // added, and its evaluation wave's exchange-A partials for the next pod
+  __shared__ unsigned long long s_cball, s_cmt, s_cmn;
+  __shared__ uint32_t s_ccnt, s_cbelow;
+  __shared__ unsigned long long s_best;
   const int w = blockIdx.x, G = lv.nwg;
   const int k0 = (int)((int64_t)lv.nblocks * w / G), k1 = (int)((int64_t)lv.nblocks * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long* gran = lv.gran;  // [npods][G][3]
+  const bool sel = wave == kBlock / 64;      // the selection wave: exchanges + phase 2
+  const bool hlp = wave == kBlock / 64 + 1;  // the helper wave: candidate pre-evaluation + staging
+  const int t = (int)threadIdx.x;          // evaluation waves: my slot in each block of my range
+  unsigned long long* gran = lv.gran;      // [npods][G][3]
+  auto stamp_s = [&](int q, int k) {       // diagnostic phase stamps: WG 0's selection lane 0
+    if (lv.stamps && w == 0 && threadIdx.x == kBlock) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
 
-  // prefetch registers for the next pod program (16 B per thread per step; the rest synchronously)
-  constexpr int kPre = 2;
+  if (t < kBlock) {  // evaluation waves
+#pragma unroll
+    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+      const int i = (k0 + kk) * kBlock + t;
+      if (kk < nk && i < m.n) {
+        const NodeCore c = load_core(m, i);
+        s_core.acpu[kk][t] = c.acpu;
+        s_core.amem[kk][t] = c.amem;
+        s_core.aeph[kk][t] = c.aeph;
+        s_core.apods[kk][t] = c.apods;
+        s_core.flags[kk][t] = c.flags;
+        s_core.tlo[kk][t] = c.tlo;
+        s_core.thi[kk][t] = c.thi;
+        lds_put_dynamic(s_core, kk, t, c);
+      }
+    }
+  }
+
+  // ---- program staging by the selection wave: registers first (issued early), LDS later
+  constexpr int kPre = 4;  // 4 KB of a program per register stage
   uint4 pre[kPre];
   uint32_t pre_bytes = 0;
-  auto fetch = [&](int pod) {  // offsets/sizes of the batch's programs: two independent loads
-    const uint8_t* g = b.descs + b.desc_off[pod];
-    pre_bytes = lv.desc_bytes[pod];
+  const uint8_t* pre_src = nullptr;
+  auto fetch = [&](int pod) __attribute__((always_inline)) {
+    pre_src = b.descs + s_off[pod - lv.first_pod];
+    pre_bytes = s_len[pod - lv.first_pod];
 #pragma unroll
     for (int r = 0; r < kPre; ++r) {
-      const uint32_t o = threadIdx.x + (uint32_t)r * kBlock;
-      if (o < pre_bytes / 16u) pre[r] = reinterpret_cast<const uint4*>(g)[o];
+      const uint32_t o = (uint32_t)lane + (uint32_t)r * 64u;
+      if (o < pre_bytes / 16u) pre[r] = reinterpret_cast<const uint4*>(pre_src)[o];
     }
   };
-  auto land = [&](int pod) {  // write the prefetched part, load the remainder
-    uint4* dst = reinterpret_cast<uint4*>(s_blob);
+  auto land = [&](int slot) __attribute__((always_inline)) {
+    uint4* dst = reinterpret_cast<uint4*>(s_blob[slot]);
 #pragma unroll
     for (int r = 0; r < kPre; ++r) {
-      const uint32_t o = threadIdx.x + (uint32_t)r * kBlock;
+      const uint32_t o = (uint32_t)lane + (uint32_t)r * 64u;
       if (o < pre_bytes / 16u) dst[o] = pre[r];
     }
-    const uint4* src = reinterpret_cast<const uint4*>(b.descs + b.desc_off[pod]);
-    for (uint32_t o = threadIdx.x + kPre * kBlock; o < pre_bytes / 16u; o += kBlock) dst[o] = src[o];
+    for (uint32_t o = (uint32_t)lane + kPre * 64u; o < pre_bytes / 16u; o += 64u)
+      dst[o] = reinterpret_cast<const uint4*>(pre_src)[o];
   };
-  if (lv.npods > 0) fetch(lv.first_pod);
 
-  for (int q = 0; q < lv.npods; ++q) {
-    const int pod = lv.first_pod + q;
-    land(pod);
-    __syncthreads();
-    const uint8_t* base = s_blob;
+  // ---- evaluation-wave state of the pod being prepared: per-thread maxima of the normalising raw
+  // scores over my feasible nodes; per-wave feasible counts (all, and before nextStartNodeIndex)
+  unsigned long long t_mt = 0, t_mn = 0;
+  uint32_t w_cnt = 0, w_below = 0;
+  auto below_mask = [&](int kk, int srot) __attribute__((always_inline)) -> unsigned long long {
+    const int lim = srot - ((k0 + kk) * kBlock + wave * 64);
+    return lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+  };
+  auto publish_partials = [&](int par) __attribute__((always_inline)) {
+    s_tm[par][t] = t_mt;
+    s_tn[par][t] = t_mn;
+    const unsigned long long mt = wave_max_u64(t_mt), mn = wave_max_u64(t_mn);
+    if (lane == 0) {
+      s_u[par][0][wave] = w_cnt;
+      s_u[par][1][wave] = w_below;
+      s_x[par][0][wave] = mt;
+      s_x[par][1][wave] = mn;
+    }
+  };
+  // phase 1: RunFilterPlugins + raw scores of my nodes for `pod`, against the cores as they are now
+  auto phase1 = [&](int pod, int slot, int par, const PodDesc* dprev) __attribute__((always_inline)) {
+    const uint8_t* base = s_blob[slot];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
-    PodStats* ps = b.stats + pod;
-    const int s = d.rot_start;
-    unsigned long long* gq = gran + (size_t)q * G * 3;
-
-    // ---- phase 1: RunFilterPlugins + raw scores of my nodes (scores stay in LDS, own slots)
-    if (w == 0) stamp(lv, q, 0);
-    unsigned long long mt = 0, mn = 0;
-    uint32_t cnt = 0, below = 0;
-    DIAG_STAMP(16);
     const bool fast = (d.flags & DF_FAST) != 0;
+    const bool post = dprev && post_ok(*dprev, d);
     const PodFast pf = load_fast(base, d);
-    DIAG_STAMP(17);
-#pragma unroll 1
-    for (int kk = 0; kk < nk; ++kk) {
-      const int i = (k0 + kk) * kBlock + threadIdx.x;
-      const NodeEval ne = fast ? eval_node_fast(m, pf, base, d, i, i < m.n) : eval_node<false>(m, b, base, d, pod, i, i < m.n);
+    t_mt = t_mn = 0;
+    w_cnt = w_below = 0;
+    auto record = [&](int kk, const NodeEval& ne) __attribute__((always_inline)) {
       const bool feas = ne.st == 0;
       const unsigned long long ballot = __ballot(feas);
-      if (lane == 0) s_ball[kk][wave] = ballot;
-      s_fx[kk][threadIdx.x] = ne.fixed;
-      s_rt[kk][threadIdx.x] = ne.rt;
-      s_rn[kk][threadIdx.x] = ne.rna;
+      if (lane == 0) s_ball[par][kk][wave] = ballot;
+      w_cnt += (uint32_t)__popcll(ballot);
+      w_below += (uint32_t)__popcll(ballot & below_mask(kk, d.rot_start));
+      s_fx[par][kk][t] = ne.fixed;
+      s_rt[par][kk][t] = (uint32_t)ne.rt;
+      s_rn[par][kk][t] = (uint32_t)ne.rna;
       if (feas) {
         const unsigned long long et = enc_i64(ne.rt), en = enc_i64(ne.rna);
-        mt = et > mt ? et : mt;
-        mn = en > mn ? en : mn;
-        cnt += 1;
-        below += i < s ? 1u : 0u;
+        t_mt = et > t_mt ? et : t_mt;
+        t_mn = en > t_mn ? en : t_mn;
       }
-    }
-    DIAG_STAMP(18);
+    };
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      cnt += __shfl_xor(cnt, o, 64);
-      below += __shfl_xor(below, o, 64);
-    }
-    mt = wave_max_u64(mt);
-    mn = wave_max_u64(mn);
-    if (lane == 0) {
-      s_u[0][wave] = cnt;
-      s_u[1][wave] = below;
-      s_x[0][wave] = mt;
-      s_x[1][wave] = mn;
-    }
-    __syncthreads();
-    if (w == 0) stamp(lv, q, 1);
-
-    // ---- exchange A
-    if (wave == 0) {
-      if (lane == 0) {
-        uint32_t c = 0, bl = 0;
-        unsigned long long a = 0, bb = 0;
-        for (int v = 0; v < kBlock / 64; ++v) {
-          c += s_u[0][v];
-          bl += s_u[1][v];
-          a = s_x[0][v] > a ? s_x[0][v] : a;
-          bb = s_x[1][v] > bb ? s_x[1][v] : bb;
+    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+      if (kk < nk) {
+        const int i = (k0 + kk) * kBlock + t;
+        NodeEval ne{1u, false, 0, 0, 0, 0};
+        if (post) {  // both evaluations, independent chains the compiler interleaves
+          NodeEval ne2{1u, false, 0, 0, 0, 0};
+          if (i < m.n) {
+            const NodeCore c = lds_core(s_core, kk, t);
+            NodeCore c2 = c;
+            assume_core(c2, *dprev);
+            const int64_t wo2 = bal2(c2.rcpu, c2.acpu, c2.rmem, c2.amem);
+            ne = eval_core_fast(m, c, s_core.bwo[kk][t], pf, base, d, i);
+            ne2 = eval_core_fast(m, c2, wo2, pf, base, d, i);
+            s_bwo2[kk][t] = wo2;
+          }
+          const unsigned long long b2 = __ballot(ne2.st == 0);
+          if (lane == 0) s_ball2[kk][wave] = b2;
+          s_fx2[kk][t] = ne2.fixed;
+          s_rt2[kk][t] = (uint32_t)ne2.rt;
+          s_rn2[kk][t] = (uint32_t)ne2.rna;
+        } else if (i < m.n) {
+          ne = fast ? eval_core_fast(m, lds_core(s_core, kk, t), s_core.bwo[kk][t], pf, base, d, i)
+                    : eval_node<false>(m, b, base, d, pod, i, true);
         }
-        // raw scores are >= 0 and bounded (host-checked): +1 so that 0 means "no feasible node"
-        const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;
-        const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;
-        __hip_atomic_store(gq + (size_t)w * 3, kValid | ((unsigned long long)bl << 24) | c, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gq + (size_t)w * 3 + 1, kValid | (np1 << 31) | tp1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        record(kk, ne);
       }
-      if (w == 0) stamp(lv, q, 2);
+    }
+    publish_partials(par);
+    if (lane == 0) __hip_atomic_fetch_add(&s_e_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  // exchange A of pod `pq` (program parity par): this workgroup's two granules from the four
+  // evaluation waves' partials.  One thread.
+  auto publish_a = [&](int pq, int par) __attribute__((always_inline)) {
+    unsigned long long* g = gran + (size_t)pq * G * 3;
+    uint32_t c = 0, bl = 0;
+    unsigned long long a = 0, bb = 0;
+    for (int v = 0; v < kBlock / 64; ++v) {
+      c += s_u[par][0][v];
+      bl += s_u[par][1][v];
+      a = s_x[par][0][v] > a ? s_x[par][0][v] : a;
+      bb = s_x[par][1][v] > bb ? s_x[par][1][v] : bb;
+    }
+    // raw scores are >= 0 and bounded (host-checked): +1 so that 0 means "no feasible node"
+    const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;
+    const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;
+    __hip_atomic_store(g + (size_t)w * 3, kValid | ((unsigned long long)bl << 24) | c, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + (size_t)w * 3 + 1, kValid | (np1 << 31) | tp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
+  };
+
+  for (int k = (int)threadIdx.x; k < lv.npods; k += kLoopThreads) {
+    s_off[k] = b.desc_off[lv.first_pod + k];
+    s_len[k] = lv.desc_bytes[lv.first_pod + k];
+  }
+  if (threadIdx.x == 0) {
+    s_cand_q = -1;
+    s_e_done = 0;
+  }
+  __syncthreads();
+  if (hlp && lv.npods > 0) {
+    fetch(lv.first_pod);
+    land(0);
+    if (lv.npods > 1) {
+      fetch(lv.first_pod + 1);
+      land(1);
+    }
+  }
+  __syncthreads();
+  if (t < kBlock && lv.npods > 0) phase1(lv.first_pod, 0, 0, nullptr);
+  __syncthreads();
+  if (threadIdx.x == kBlock && lv.npods > 0) publish_a(0, 0);
+
+  for (int q = 0; q < lv.npods; ++q) {
+    const int pod = lv.first_pod + q, par = q & 1, npar = par ^ 1;
+    const int bq = q % 3, bn = (q + 1) % 3, bs = (q + 2) % 3;
+    const bool more = q + 1 < lv.npods;
+    const uint8_t* base = s_blob[bq];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    unsigned long long* gq = gran + (size_t)q * G * 3;
+
+    if (sel) {
+      // ======== selection wave: exchange A, phase 2, exchange B, pre-evaluation, staging ========
+      stamp_s(q, 0);  // exchange A of this pod was published at the end of the previous one
       unsigned long long x0[kMaxSweep], x1[kMaxSweep];
-      const bool ok = sweep2(gq, G, x0, x1, lv.fail);
+      bool ok = sweep2(gq, G, x0, x1, lv.fail);
       uint32_t F = 0, wp = 0, bf = 0;
       unsigned long long tmax = 0, nmax = 0;
 #pragma unroll
@@ -1368,80 +1562,65 @@ __global__ __launch_bounds__(kBlock) void k_sched_loop(MirrorView m, BatchView b
           F += c;
           if (v < w) wp += c;
           bf += (uint32_t)((x0[r] >> 24) & 0xffffffull);
-          const unsigned long long t = x1[r] & 0x7fffffffull, n = (x1[r] >> 31) & 0xffffffffull;
-          tmax = t > tmax ? t : tmax;
-          nmax = n > nmax ? n : nmax;
+          const unsigned long long tv = x1[r] & 0x7fffffffull, nv = (x1[r] >> 31) & 0xffffffffull;
+          tmax = tv > tmax ? tv : tmax;
+          nmax = nv > nmax ? nv : nmax;
         }
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        F += __shfl_xor(F, o, 64);
-        wp += __shfl_xor(wp, o, 64);
-        bf += __shfl_xor(bf, o, 64);
-        const unsigned long long t2 = __shfl_xor(tmax, o, 64), n2 = __shfl_xor(nmax, o, 64);
-        tmax = t2 > tmax ? t2 : tmax;
-        nmax = n2 > nmax ? n2 : nmax;
-      }
-      if (lane == 0) {
-        s_ok = ok ? 1u : 0u;
-        s_F = F;
-        s_pre = wp;
-        s_before = bf;
-        s_mt = tmax;
-        s_mn = nmax;
-      }
-      if (w == 0) stamp(lv, q, 3);
-    }
-    __syncthreads();
-    if (!s_ok) return;
+      F = wave_sum_u32(F);
+      const uint32_t ps_before = wave_sum_u32(bf);
+      uint32_t acc = wave_sum_u32(wp);  // feasible nodes before my range
+      tmax = wave_max_u64(tmax);
+      nmax = wave_max_u64(nmax);
+      stamp_s(q, 1);
 
-    // ---- phase 2: positions, NormalizeScore + weights, my best packed key
-    const uint32_t F = s_F, ps_before = s_before;
-    const int64_t mx_t = s_mt ? (int64_t)s_mt - 1 : 0, mx_n = s_mn ? (int64_t)s_mn - 1 : 0;
-    unsigned long long key = 0;
-    int knode = -1;
-    uint32_t acc = s_pre;  // feasible nodes before node block kk of my range
-#pragma unroll 1
-    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-      if (kk < nk) {
-        uint32_t wbefore = 0, tot = 0;
+      // ---- phase 2: positions, NormalizeScore + weights, my range's best packed key
+      const int64_t mx_t = tmax ? (int64_t)tmax - 1 : 0, mx_n = nmax ? (int64_t)nmax - 1 : 0;
+      unsigned long long key = 0;
+      int knode = -1;
+      if (ok) {
 #pragma unroll
-        for (int v = 0; v < kBlock / 64; ++v) {
-          const uint32_t pc = (uint32_t)__popcll(s_ball[kk][v]);
-          wbefore += v < wave ? pc : 0u;
-          tot += pc;
-        }
-        const unsigned long long ballot = s_ball[kk][wave];
-        if ((ballot >> lane) & 1ull) {
-          const uint32_t g = acc + wbefore + wave_prefix_count(ballot, lane);
-          const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-          const unsigned long long kv = pack_best(
-              loop_total(d, s_fx[kk][threadIdx.x], s_rt[kk][threadIdx.x], s_rn[kk][threadIdx.x], mx_t, mx_n), pos);
-          if (kv > key) {
-            key = kv;
-            knode = (k0 + kk) * kBlock + (int)threadIdx.x;
+        for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+          if (kk < nk) {
+            // every LDS read of the block issued up front (unconditional), then the arithmetic
+            unsigned long long ballot[kBlock / 64];
+            int64_t fx[kBlock / 64], rt[kBlock / 64], rn[kBlock / 64];
+#pragma unroll
+            for (int v = 0; v < kBlock / 64; ++v) {
+              ballot[v] = s_ball[par][kk][v];
+              fx[v] = s_fx[par][kk][v * 64 + lane];
+              rt[v] = s_rt[par][kk][v * 64 + lane];
+              rn[v] = s_rn[par][kk][v * 64 + lane];
+            }
+#pragma unroll
+            for (int v = 0; v < kBlock / 64; ++v) {
+              if ((ballot[v] >> lane) & 1ull) {
+                const uint32_t g = acc + wave_prefix_count(ballot[v], lane);
+                const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
+                const unsigned long long kv = pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos);
+                if (kv > key) {
+                  key = kv;
+                  knode = (k0 + kk) * kBlock + v * 64 + lane;
+                }
+              }
+              acc += (uint32_t)__popcll(ballot[v]);
+            }
           }
         }
-        acc += tot;
       }
-    }
-    const unsigned long long wkey = wave_max_u64(key);
-    if (lane == 0) s_x[0][wave] = wkey;
-    __syncthreads();
-    if (w == 0) stamp(lv, q, 4);
-    // the next pod's program: issue its loads now, they land after exchange B
-    if (q + 1 < lv.npods) fetch(pod + 1);
-
-    // ---- exchange B
-    if (wave == 0) {
+      const unsigned long long wkey = wave_max_u64(key);
+      const unsigned long long hold = __ballot(key == wkey && key != 0ull);
+      const int cand = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
+      stamp_s(q, 2);
       if (lane == 0) {
-        unsigned long long kk = 0;
-        for (int v = 0; v < kBlock / 64; ++v) kk = s_x[0][v] > kk ? s_x[0][v] : kk;
-        __hip_atomic_store(gq + (size_t)w * 3 + 2, kValid | kk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gq + (size_t)w * 3 + 2, kValid | wkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        __hip_atomic_store(&s_cand_node, cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&s_cand_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (w == 0) stamp(lv, q, 5);
+      stamp_s(q, 3);
       unsigned long long xb[kMaxSweep];
-      const bool ok = sweep(gq, G, 3, 2, xb, lv.fail);
+      ok = ok && sweep(gq, G, 3, 2, xb, lv.fail);
       unsigned long long bm = 0;
 #pragma unroll
       for (int r = 0; r < kMaxSweep; ++r) {
@@ -1452,21 +1631,159 @@ __global__ __launch_bounds__(kBlock) void k_sched_loop(MirrorView m, BatchView b
       if (lane == 0) {
         s_ok = ok ? 1u : 0u;
         s_best = bm;
+        s_F = F;
+        s_win = (F > 0 && wkey == bm && cand >= 0) ? cand : -1;
       }
-      if (w == 0) stamp(lv, q, 6);
+      stamp_s(q, 4);
+    } else if (hlp) {
+      // ======== helper wave: stage pod q+2's program; pre-evaluate the selection wave's candidate
+      // for pod q+1 as if this pod were assumed on it, while exchange B is in flight.  The result
+      // is used when the candidate wins.  Default-plugin pods only: their evaluation reads nothing
+      // this AssumePod writes to memory, except host ports, excluded here.
+      const bool stage = q + 2 < lv.npods;
+      if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
+      if (stage) fetch(pod + 2);
+      while (__hip_atomic_load(&s_cand_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)  // posted every pod
+        __builtin_amdgcn_s_sleep(1);
+      const int cand = __hip_atomic_load(&s_cand_node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint32_t cand_ok = 0;
+      if (more && cand >= 0 && (d.flags & DF_ASSUME)) {
+        const uint8_t* nb = s_blob[bn];
+        const PodDesc& nd = *reinterpret_cast<const PodDesc*>(nb);
+        if (post_ok(d, nd)) {
+          cand_ok = 1;
+          const int kw = cand / kBlock - k0, sl = cand % kBlock, cw = sl >> 6;
+          // the candidate's evaluation wave, as its partials for pod q+1 will be if it wins (the
+          // evaluation waves computed its next evaluation with this pod assumed in phase 1)
+          while (__hip_atomic_load(&s_e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                 (uint32_t)(kBlock / 64) * (uint32_t)(q + 2))
+            __builtin_amdgcn_s_sleep(1);
+          const bool cf = ((s_ball2[kw][cw] >> (sl & 63)) & 1ull) != 0;
+          const int64_t crt = s_rt2[kw][sl], crn = s_rn2[kw][sl];
+          unsigned long long tm = s_tm[npar][cw * 64 + lane], tn = s_tn[npar][cw * 64 + lane];
+          if (lane == (sl & 63)) {
+            tm = tn = 0;
+            for (int kk = 0; kk < nk; ++kk) {
+              const bool f = kk == kw ? cf : ((s_ball[npar][kk][cw] >> lane) & 1ull) != 0;
+              if (f) {
+                const unsigned long long et = enc_i64(kk == kw ? crt : s_rt[npar][kk][sl]);
+                const unsigned long long en = enc_i64(kk == kw ? crn : s_rn[npar][kk][sl]);
+                tm = et > tm ? et : tm;
+                tn = en > tn ? en : tn;
+              }
+            }
+          }
+          tm = wave_max_u64(tm);
+          tn = wave_max_u64(tn);
+          if (lane == 0) {
+            const unsigned long long old = s_ball[npar][kw][cw];
+            const unsigned long long bit = 1ull << (sl & 63);
+            const unsigned long long nbal = cf ? (old | bit) : (old & ~bit);
+            const int lim = nd.rot_start - ((k0 + kw) * kBlock + cw * 64);
+            const unsigned long long bmk = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+            s_cball = nbal;
+            s_ccnt = s_u[npar][0][cw] - (uint32_t)__popcll(old) + (uint32_t)__popcll(nbal);
+            s_cbelow = s_u[npar][1][cw] - (uint32_t)__popcll(old & bmk) + (uint32_t)__popcll(nbal & bmk);
+            s_cmt = tm;
+            s_cmn = tn;
+          }
+        }
+      }
+      if (lane == 0) s_cand_ok = cand_ok;
+      if (stage) land(bs);
+    } else if (more) {
+      // ======== evaluation waves: phase 1 of pod q+1 against the cores before this pod's assume.
+      // Only the chosen node changes; its owner redoes it below.
+      phase1(pod + 1, bn, npar, &d);
+      if (lv.stamps && w == 0 && t == 0) lv.stamps[(size_t)q * 8 + 7] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (!s_ok) return;
+    stamp_s(q, 5);
 
-    // ---- the thread holding the winning key (keys are unique: positions are) assumes + reports
-    const unsigned long long best = s_best;
-    if (F == 0) {
-      if (w == 0 && threadIdx.x == 0) commit_result(m, b, base, d, ps, pod, F, -1, best);
-    } else if (key == best && knode >= 0) {
-      commit_result(m, b, base, d, ps, pod, F, knode, best);
+    // ---- the winning node's owner fixes up pod q+1's phase 1, publishes its exchange A, then
+    // assumes + reports this pod; every other workgroup's selection wave publishes A at once
+    {
+      const uint32_t F = s_F;
+      const int win = s_win;
+      const int wsl = win >= 0 ? win - k0 * kBlock : -1;  // kk * kBlock + slot
+      const bool owner_wg = F > 0 && wsl >= 0 && (d.flags & DF_ASSUME);
+      if (!owner_wg) {
+        if (more && threadIdx.x == kBlock) publish_a(q + 1, npar);
+        if (F == 0) {
+          if (w == 0 && t == 0) commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
+        } else if (wsl >= 0 && t == wsl % kBlock) {  // chosen here, not assumed
+          commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, nullptr, s_ipa);
+        }
+      } else if (s_cand_ok) {  // the helper prepared everything: LDS stores, then publish
+        if (t == wsl % kBlock) {
+          const int kw = wsl / kBlock, cw = t >> 6;
+          if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+          NodeCore c = lds_core(s_core, kw, t);
+          assume_core(c, d);
+          s_core.rcpu[kw][t] = c.rcpu;
+          s_core.rmem[kw][t] = c.rmem;
+          s_core.reph[kw][t] = c.reph;
+          s_core.nzcpu[kw][t] = c.nzcpu;
+          s_core.nzmem[kw][t] = c.nzmem;
+          s_core.npods[kw][t] = c.npods;
+          s_core.bwo[kw][t] = s_bwo2[kw][t];
+          s_fx[npar][kw][t] = s_fx2[kw][t];
+          s_rt[npar][kw][t] = s_rt2[kw][t];
+          s_rn[npar][kw][t] = s_rn2[kw][t];
+          s_ball[npar][kw][cw] = s_cball;
+          s_u[npar][0][cw] = s_ccnt;
+          s_u[npar][1][cw] = s_cbelow;
+          s_x[npar][0][cw] = s_cmt;
+          s_x[npar][1][cw] = s_cmn;
+          publish_a(q + 1, npar);
+          if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+          commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);
+        }
+      } else if (t < kBlock && wave == ((wsl % kBlock) >> 6)) {  // generic pods: re-evaluate here
+        const int kw = wsl / kBlock, owner = wsl % 64;
+        const uint8_t* nb = s_blob[bn];
+        const PodDesc& nd = *reinterpret_cast<const PodDesc*>(nb);
+        bool feas = ((s_ball[npar][kw][wave] >> lane) & 1ull) != 0;
+        if (lane == owner) {
+          NodeCore c = lds_core(s_core, kw, t);
+          assume_core(c, d);
+          commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);  // before the re-read
+          lds_put_dynamic(s_core, kw, t, c);
+          if (more) {
+            const NodeEval ne = (nd.flags & DF_FAST)
+                                    ? eval_core_fast(m, c, s_core.bwo[kw][t], load_fast(nb, nd), nb, nd, win)
+                                    : eval_node<false>(m, b, nb, nd, pod + 1, win, true);
+            feas = ne.st == 0;
+            s_fx[npar][kw][t] = ne.fixed;
+            s_rt[npar][kw][t] = (uint32_t)ne.rt;
+            s_rn[npar][kw][t] = (uint32_t)ne.rna;
+            t_mt = t_mn = 0;  // my maxima again, over my (possibly changed) feasible nodes
+            for (int kk = 0; kk < nk; ++kk) {
+              const bool f = kk == kw ? feas : ((s_ball[npar][kk][wave] >> lane) & 1ull) != 0;
+              if (f) {
+                const unsigned long long et = enc_i64(s_rt[npar][kk][t]), en = enc_i64(s_rn[npar][kk][t]);
+                t_mt = et > t_mt ? et : t_mt;
+                t_mn = en > t_mn ? en : t_mn;
+              }
+            }
+          }
+        }
+        if (more) {
+          const unsigned long long old = s_ball[npar][kw][wave];
+          const unsigned long long nbal = __ballot(feas);
+          const unsigned long long bmk = below_mask(kw, nd.rot_start);
+          w_cnt = w_cnt - (uint32_t)__popcll(old) + (uint32_t)__popcll(nbal);
+          w_below = w_below - (uint32_t)__popcll(old & bmk) + (uint32_t)__popcll(nbal & bmk);
+          if (lane == 0) s_ball[npar][kw][wave] = nbal;
+          publish_partials(npar);
+          if (lane == 0) publish_a(q + 1, npar);  // the other waves' partials are final since the barrier
+        }
+      }
     }
     DIAG_FLUSH();
-    __syncthreads();  // the assume lands before my next pod's phase 1; s_blob is free again
+    __syncthreads();  // pod q+1's phase-1 state is final; s_blob[q % 3] is free again
+    stamp_s(q, 6);
   }
 }
 
@@ -1532,9 +1849,9 @@ hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int n
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
                              hipEvent_t t0, hipEvent_t t1) {
   if (t0)
-    hipExtLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kBlock), 0, s, t0, t1, 0, m, b, lv);
+    hipExtLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kLoopThreads), 0, s, t0, t1, 0, m, b, lv);
   else
-    hipLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kBlock), 0, s, m, b, lv);
+    hipLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
   return hipGetLastError();
 }
 #ifdef KSG_DIAG

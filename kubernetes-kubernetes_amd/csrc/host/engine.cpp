@@ -1039,8 +1039,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
     HIPCHK(hipMemsetAsync(d_wgcnt.p, 0, (size_t)n * G * 3 * 8, s));  // every granule invalid
     if (c->cfg.loop_stamps) {
-      if ((rc = ensure(d_stamps, (size_t)n * 8 * 8 + 64 * 8))) return rc;
-      HIPCHK(hipMemsetAsync(d_stamps.p, 0, (size_t)n * 8 * 8 + 64 * 8, s));
+      const size_t sb = (size_t)n * 8 * 8 + 64 * 8 + (size_t)n * G * 8 * 8;
+      if ((rc = ensure(d_stamps, sb))) return rc;
+      HIPCHK(hipMemsetAsync(d_stamps.p, 0, sb, s));
 #ifdef KSG_DIAG
       HIPCHK(set_diag((unsigned long long*)d_stamps.p + (size_t)n * 8));
 #endif
@@ -1054,7 +1055,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (use_loop && loop_ok(cp[i])) {  // a run of node-local pods: one k_sched_loop launch
       int j = i;
       double rb = 0;
-      while (j < n && loop_ok(cp[j])) rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data()));
+      while (j < n && j - i < kLoopMaxPods && loop_ok(cp[j])) rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data()));
       while (lev.size() < 2 * (runs.size() + 1)) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -1062,7 +1063,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       }
       LoopView lv{i, j - i, G, NB, (unsigned long long*)d_wgcnt.p + (size_t)i * G * 3, (uint32_t*)d_fail.p,
                   c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr,
-                  (const uint32_t*)d_off.p + n};
+                  (const uint32_t*)d_off.p + n,
+                  c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr};
       HIPCHK(launch_sched_loop(m, bv, lv, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
       runs.push_back({i, j - i, rb});
       launches += j - i;
@@ -1144,7 +1146,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (c->cfg.loop_stamps) {  // mean per-phase time (us) of the looped pods, workgroup 0's view
       std::vector<unsigned long long> st((size_t)n * 8);
       HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
-      double acc[8] = {0};
+      double acc[9] = {0};
       int cnt = 0;
       for (auto& r : runs)
         for (int q = r.first; q < r.first + r.count; ++q) {
@@ -1153,6 +1155,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
           if (!t[0] || !t[6] || !nxt) continue;
           for (int k = 1; k <= 6; ++k) acc[k] += (double)(t[k] - t[k - 1]) / 100.0;
           acc[7] += (double)(nxt - t[6]) / 100.0;
+          acc[8] += t[7] ? (double)(t[7] - t[0]) / 100.0 : 0.0;
           cnt++;
         }
 #ifdef KSG_DIAG
@@ -1160,22 +1163,103 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         unsigned long long dg[20];
         HIPCHK(hipMemcpy(dg, (unsigned long long*)d_stamps.p + (size_t)n * 8, sizeof dg, hipMemcpyDeviceToHost));
         std::fprintf(stderr, "[fast path of the last pod, us] load_fast %.3f | load_core %.3f taints %.3f filters %.3f "
-                     "nascore %.3f fit %.3f balanced %.3f | loop body total %.3f\n", (dg[17] - dg[16]) / 100.0,
+                     "nascore %.3f fit %.3f balanced %.3f | loop body total %.3f reduce %.3f\n", (dg[17] - dg[16]) / 100.0,
                      (dg[9] - dg[8]) / 100.0, (dg[10] - dg[9]) / 100.0, (dg[11] - dg[10]) / 100.0,
                      (dg[12] - dg[11]) / 100.0, (dg[13] - dg[12]) / 100.0, (dg[14] - dg[13]) / 100.0,
-                     (dg[18] - dg[17]) / 100.0);
+                     (dg[18] - dg[17]) / 100.0, (dg[19] - dg[18]) / 100.0);
         std::fprintf(stderr, "[eval_node steps of the last pod, us] load_core %.3f filters %.3f pre-score %.3f fit %.3f "
                      "balanced %.3f image %.3f rest %.3f\n", (dg[1] - dg[0]) / 100.0, (dg[2] - dg[1]) / 100.0,
                      (dg[3] - dg[2]) / 100.0, (dg[4] - dg[3]) / 100.0, (dg[5] - dg[4]) / 100.0,
                      (dg[6] - dg[5]) / 100.0, (dg[7] - dg[6]) / 100.0);
       }
 #endif
+      {  // per-workgroup publish skew: max - min over workgroups of the A and B publish times
+        std::vector<unsigned long long> ws((size_t)n * G * 8);
+        HIPCHK(hipMemcpy(ws.data(), (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64, ws.size() * 8,
+                         hipMemcpyDeviceToHost));
+        double ska = 0, skb = 0, ab = 0;
+        int sc = 0;
+        for (auto& r : runs)
+          for (int q = r.first; q + 1 < r.first + r.count; ++q) {
+            unsigned long long amin = ~0ull, amax = 0, bmin = ~0ull, bmax = 0, an = ~0ull;
+            for (int g = 0; g < G; ++g) {
+              const unsigned long long a = ws[((size_t)q * G + g) * 8], bb = ws[((size_t)q * G + g) * 8 + 1];
+              const unsigned long long a2 = ws[((size_t)(q + 1) * G + g) * 8];
+              amin = std::min(amin, a); amax = std::max(amax, a);
+              bmin = std::min(bmin, bb); bmax = std::max(bmax, bb);
+              an = std::min(an, a2);
+            }
+            if (!amin || !bmin || !an) continue;
+            ska += (amax - amin) / 100.0;
+            skb += (bmax - bmin) / 100.0;
+            ab += (an - bmax) / 100.0;
+            sc++;
+          }
+        {  // mean lateness of each workgroup's A publish behind the earliest; and of the workgroup
+           // that owned the previous pod's chosen node
+          std::vector<double> late(G, 0.0);
+          double wl = 0;
+          int wn = 0, cntq = 0;
+          DevResult* hr0 = (DevResult*)((uint8_t*)h_pinned + 0);  // not yet copied: use stamps only
+          (void)hr0;
+          for (auto& r : runs)
+            for (int q = r.first + 1; q < r.first + r.count; ++q) {
+              unsigned long long amin = ~0ull;
+              for (int g = 0; g < G; ++g) amin = std::min(amin, ws[((size_t)q * G + g) * 8]);
+              if (!amin) continue;
+              unsigned long long amax = 0;
+              int gl = -1;
+              for (int g = 0; g < G; ++g) {
+                const unsigned long long a = ws[((size_t)q * G + g) * 8];
+                late[g] += (a - amin) / 100.0;
+                if (a > amax) { amax = a; gl = g; }
+              }
+              (void)gl;
+              cntq++;
+            }
+          double own = 0, ownlate = 0, ownx = 0, seg[5] = {0};
+          int segn = 0;
+          int on = 0;
+          for (auto& r : runs)
+            for (int q = r.first; q + 1 < r.first + r.count; ++q)
+              for (int g = 0; g < G; ++g) {
+                const unsigned long long c0 = ws[((size_t)q * G + g) * 8 + 2], c1 = ws[((size_t)q * G + g) * 8 + 3];
+                if (!c0 || !c1) continue;
+                unsigned long long amin = ~0ull;
+                for (int h = 0; h < G; ++h) amin = std::min(amin, ws[((size_t)(q + 1) * G + h) * 8]);
+                const unsigned long long an = ws[((size_t)(q + 1) * G + g) * 8];
+                const unsigned long long c4 = ws[((size_t)q * G + g) * 8 + 4], c5 = ws[((size_t)q * G + g) * 8 + 5];
+                const unsigned long long c6r = ws[((size_t)q * G + g) * 8 + 6], c6 = c6r & ((1ull << 60) - 1);
+                if (c4 && c5 && c6) {
+                  seg[0] += (c4 - c0) / 100.0; seg[1] += (c5 - c4) / 100.0; seg[2] += (c6 - c5) / 100.0;
+                  seg[3] += (c1 - c6) / 100.0; seg[4] += (double)(c6r >> 60); segn++;
+                }
+                own += (c1 - c0) / 100.0;
+                ownx += ((double)an - (double)c1) / 100.0;
+                ownlate += ((double)an - (double)amin) / 100.0;
+                on++;
+              }
+          if (segn)
+            std::fprintf(stderr, "[k_sched_loop owner steps, us] commit %.3f lds %.3f eval/cand %.3f partials %.3f "
+                         "(cand used %.2f)\n", seg[0] / segn, seg[1] / segn, seg[2] / segn, seg[3] / segn, seg[4] / segn);
+          if (on)
+            std::fprintf(stderr, "[k_sched_loop owner, us] commit+fixup %.3f  fixup end -> next A publish %.3f  "
+                         "owner's next A lateness %.3f (%d pods)\n", own / on, ownx / on, ownlate / on, on);
+          std::string o;
+          for (int g = 0; g < G; ++g) o += " " + std::to_string((int)(1000 * late[g] / std::max(cntq, 1)));
+          std::fprintf(stderr, "[k_sched_loop A lateness per workgroup, ns]%s\n", o.c_str());
+          (void)wl; (void)wn;
+        }
+        if (sc)
+          std::fprintf(stderr, "[k_sched_loop skew over workgroups, us] A publish %.3f  B publish %.3f  "
+                       "last B -> first next A %.3f  (A last->B first %.3f)\n", ska / sc, skb / sc, ab / sc, 0.0);
+      }
       if (cnt)
         std::fprintf(stderr,
-                     "[k_sched_loop stamps, %d pods, us] phase1 %.3f publishA %.3f waitA %.3f phase2 %.3f "
-                     "publishB %.3f waitB %.3f phase3+next %.3f\n",
+                     "[k_sched_loop stamps, %d pods, us] exchangeA %.3f phase2 %.3f publishB+preeval+stage %.3f "
+                     "waitB %.3f wait-phase1(next pod) %.3f commit+fixup %.3f gap %.3f | phase1 end %.3f\n",
                      cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt,
-                     acc[7] / cnt);
+                     acc[7] / cnt, acc[8] / cnt);
     }
   }
 

@@ -1,3 +1,8 @@
+#!/bin/bash
+# Loop probe (per-phase stamps, pods/s) then the GPU parity suite; each step time-limited, a crash ends the script.
 export TMPDIR=/tmp
-timeout -k 10 200 python scripts/loop_probe.py 5000 20 > gpurun_out/probe.log 2>&1; echo "probe rc=$?"
-KSG_LIB=$PWD/kubernetes-kubernetes_amd/lib/libksg_diag.so timeout -k 10 200 python scripts/loop_probe.py 5000 20 >> gpurun_out/probe.log 2>&1; echo "probe-diag rc=$?"
+mkdir -p gpurun_out
+timeout -k 10 200 python -u scripts/loop_probe.py ${PROBE_NODES:-5000} ${PROBE_WG:-0} > gpurun_out/probe.log 2>&1
+rc=$?; echo "probe rc=$rc"; [ $rc -le 1 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; exit $rc
