@@ -531,6 +531,19 @@ __device__ __forceinline__ int64_t fdiv52(int64_t a, int64_t b) {
   q += r >= b ? 1 : 0;
   return q;
 }
+// 0 <= x < 2^52 as a double, exactly: the integer in the mantissa of 2^52, minus 2^52
+__device__ __forceinline__ double u52_to_f64(int64_t x) {
+  return __longlong_as_double(x | 0x4330000000000000ll) - 4503599627370496.0;
+}
+// floor(a / b) for 0 <= a <= 100 b, 0 < b, a < 2^52 (the Least/MostAllocated ratios and the
+// weighted mean of Fit's scores): a * rcp(b) is within one of a / b, fixed up with the exact remainder
+__device__ __forceinline__ int64_t qdiv100(int64_t a, int64_t b) {
+  int32_t q = (int32_t)(u52_to_f64(a) * __builtin_amdgcn_rcp(u52_to_f64(b)));
+  const int64_t r = a - (int64_t)q * b;
+  q -= r < 0 ? 1 : 0;
+  q += r >= b ? 1 : 0;
+  return q;
+}
 // balanced_allocation.go:220-254 for the (cpu, memory) pair
 __device__ __forceinline__ int64_t bal2(int64_t rc, int64_t ac, int64_t rm, int64_t am) {
   double f0 = ac != 0 ? (double)rc / (double)ac : 0.0;
@@ -545,8 +558,11 @@ __device__ __forceinline__ int64_t bal2(int64_t rc, int64_t ac, int64_t rm, int6
 }
 // nc: node i's core columns -- loaded here (launch path) or held in registers by its owner (k_sched_loop)
 // bal_wo: bal2 of the node without the pod (pod-independent: the loop keeps it per node)
+// bal_with: bal2 of the node with the pod, when the caller already has it (else kNoBal)
+constexpr int64_t kNoBal = INT64_MIN;
 __device__ __forceinline__ NodeEval eval_core_fast(const MirrorView& m, const NodeCore& nc, int64_t bal_wo,
-                                                   const PodFast& pf, const uint8_t* base, const PodDesc& d, int i) {
+                                                   const PodFast& pf, const uint8_t* base, const PodDesc& d, int i,
+                                                   int64_t bal_with = kNoBal) {
   NodeEval r{1u, false, 0, 0, 0, 0};
   DIAG_STAMP(9);
   bool untol = false;
@@ -613,19 +629,20 @@ __device__ __forceinline__ NodeEval eval_core_fast(const MirrorView& m, const No
     const int64_t qc = nc.nzcpu + pf.fpr_cpu, qm = nc.nzmem + pf.fpr_mem;
     int64_t sc, smm;
     if (pf.most) {  // most_allocated.go:55-65
-      sc = nc.acpu != 0 ? fdiv52((qc > nc.acpu ? nc.acpu : qc) * 100, nc.acpu) : 0;
-      smm = nc.amem != 0 ? fdiv52((qm > nc.amem ? nc.amem : qm) * 100, nc.amem) : 0;
+      sc = nc.acpu > 0 ? qdiv100((qc > nc.acpu ? nc.acpu : qc) * 100, nc.acpu) : 0;
+      smm = nc.amem > 0 ? qdiv100((qm > nc.amem ? nc.amem : qm) * 100, nc.amem) : 0;
     } else {  // least_allocated.go:52-61
-      sc = nc.acpu != 0 && qc <= nc.acpu ? fdiv52((nc.acpu - qc) * 100, nc.acpu) : 0;
-      smm = nc.amem != 0 && qm <= nc.amem ? fdiv52((nc.amem - qm) * 100, nc.amem) : 0;
+      sc = nc.acpu > 0 && qc <= nc.acpu ? qdiv100((nc.acpu - qc) * 100, nc.acpu) : 0;
+      smm = nc.amem > 0 && qm <= nc.amem ? qdiv100((nc.amem - qm) * 100, nc.amem) : 0;
     }
     const int64_t ws = (nc.acpu != 0 ? pf.fw_cpu : 0) + (nc.amem != 0 ? pf.fw_mem : 0);
     const int64_t num = (nc.acpu != 0 ? sc * pf.fw_cpu : 0) + (nc.amem != 0 ? smm * pf.fw_mem : 0);
-    fixed += (ws == 0 ? 0 : go_div(num, ws)) * pf.wt_fit;
+    fixed += (ws == 0 ? 0 : qdiv100(num, ws)) * pf.wt_fit;  // weights > 0: num <= 100 ws
   }
   DIAG_STAMP(13);
   if ((sm >> P_BAL) & 1u) {  // balanced_allocation.go:204-218 (Requested, useRequested=true)
-    const int64_t with = bal2(nc.rcpu + pf.bpr_cpu, nc.acpu, nc.rmem + pf.bpr_mem, nc.amem);
+    const int64_t with =
+        bal_with != kNoBal ? bal_with : bal2(nc.rcpu + pf.bpr_cpu, nc.acpu, nc.rmem + pf.bpr_mem, nc.amem);
     fixed += (100 / 2 + (100 / 2 + with - bal_wo) / 2) * pf.wt_bal;
   }
   r.fixed = fixed;  // ImageLocality: no image of the pod exists in the cluster -> 0 (host-checked)
@@ -1335,6 +1352,17 @@ __device__ __forceinline__ void assume_core(NodeCore& c, const PodDesc& d) {
   c.npods += 1;
 }
 
+// exchange A's two granules from a workgroup's feasible count, count before nextStartNodeIndex and
+// encoded maxima of the raw TaintToleration / NodeAffinity scores (raw scores are >= 0 and bounded,
+// host-checked: +1 so that 0 means "no feasible node")
+__device__ __forceinline__ void a_granules(uint32_t c, uint32_t bl, unsigned long long a, unsigned long long bb,
+                                           unsigned long long* g0, unsigned long long* g1) {
+  const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;
+  const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;
+  *g0 = kValid | ((unsigned long long)bl << 24) | c;
+  *g1 = kValid | (np1 << 31) | tp1;
+}
+
 // Can pod `nd`'s evaluation of a node be computed, before pod `d` is assumed, as it will be after?
 // Default-plugin pods read nothing an AssumePod changes beyond the core columns, except host ports.
 __device__ __forceinline__ bool post_ok(const PodDesc& d, const PodDesc& nd) {
@@ -1365,6 +1393,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   // the candidate's state if it wins, prepared by the helper wave: its core columns with the pod
   // added, and its evaluation wave's exchange-A partials for the next pod
   __shared__ unsigned long long s_cball, s_cmt, s_cmn;
+  __shared__ unsigned long long s_ga[4];  // pod q+1's exchange-A granules: [0..1] candidate not chosen, [2..3] chosen
+  __shared__ int s_ga_q;                  // the pod whose s_ga is ready
   __shared__ uint32_t s_ccnt, s_cbelow;
   __shared__ unsigned long long s_best;
   const int w = blockIdx.x, G = lv.nwg;
@@ -1448,6 +1478,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     const bool fast = (d.flags & DF_FAST) != 0;
     const bool post = dprev && post_ok(*dprev, d);
     const PodFast pf = load_fast(base, d);
+    const bool bal = ((pf.sm >> P_BAL) & 1u) != 0;
+    const bool same_bal = post && dprev->a_cpu == pf.bpr_cpu && dprev->a_mem == pf.bpr_mem;
     t_mt = t_mn = 0;
     w_cnt = w_below = 0;
     auto record = [&](int kk, const NodeEval& ne) __attribute__((always_inline)) {
@@ -1476,8 +1508,12 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
             const NodeCore c = lds_core(s_core, kk, t);
             NodeCore c2 = c;
             assume_core(c2, *dprev);
-            const int64_t wo2 = bal2(c2.rcpu, c2.acpu, c2.rmem, c2.amem);
-            ne = eval_core_fast(m, c, s_core.bwo[kk][t], pf, base, d, i);
+            // BalancedAllocation: the node with pod q+1 is the node with pod q when their requests
+            // match (one template), so one bal2 serves both
+            int64_t with1 = kNoBal, wo2;
+            if (bal) with1 = bal2(c.rcpu + pf.bpr_cpu, c.acpu, c.rmem + pf.bpr_mem, c.amem);
+            wo2 = bal && same_bal ? with1 : bal2(c2.rcpu, c2.acpu, c2.rmem, c2.amem);
+            ne = eval_core_fast(m, c, s_core.bwo[kk][t], pf, base, d, i, with1);
             ne2 = eval_core_fast(m, c2, wo2, pf, base, d, i);
             s_bwo2[kk][t] = wo2;
           }
@@ -1508,12 +1544,10 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       a = s_x[par][0][v] > a ? s_x[par][0][v] : a;
       bb = s_x[par][1][v] > bb ? s_x[par][1][v] : bb;
     }
-    // raw scores are >= 0 and bounded (host-checked): +1 so that 0 means "no feasible node"
-    const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;
-    const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;
-    __hip_atomic_store(g + (size_t)w * 3, kValid | ((unsigned long long)bl << 24) | c, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + (size_t)w * 3 + 1, kValid | (np1 << 31) | tp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long g0, g1;
+    a_granules(c, bl, a, bb, &g0, &g1);
+    __hip_atomic_store(g + (size_t)w * 3, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + (size_t)w * 3 + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
   };
 
@@ -1523,6 +1557,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   }
   if (threadIdx.x == 0) {
     s_cand_q = -1;
+    s_ga_q = -1;
     s_e_done = 0;
   }
   __syncthreads();
@@ -1628,18 +1663,34 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
         bm = v > bm ? v : bm;
       }
       bm = wave_max_u64(bm);
+      const int win = (F > 0 && wkey == bm && cand >= 0) ? cand : -1;
       if (lane == 0) {
         s_ok = ok ? 1u : 0u;
         s_best = bm;
         s_F = F;
-        s_win = (F > 0 && wkey == bm && cand >= 0) ? cand : -1;
+        s_win = win;
+      }
+      // exchange A of pod q+1, now: the pair the helper prepared for this outcome.  A chosen node
+      // whose next evaluation was not prepared (generic pods) is fixed up after the barrier, and its
+      // owner publishes then.
+      if (more && ok) {
+        while (__hip_atomic_load(&s_ga_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+          __builtin_amdgcn_s_sleep(1);
+        const bool chosen = win >= 0 && (d.flags & DF_ASSUME);
+        if (lane == 0 && (!chosen || s_cand_ok)) {
+          unsigned long long* g = gran + (size_t)(q + 1) * G * 3 + (size_t)w * 3;
+          __hip_atomic_store(g, s_ga[chosen ? 2 : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(g + 1, s_ga[chosen ? 3 : 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lv.wstamps) lv.wstamps[((size_t)(q + 1) * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
+        }
       }
       stamp_s(q, 4);
     } else if (hlp) {
-      // ======== helper wave: stage pod q+2's program; pre-evaluate the selection wave's candidate
-      // for pod q+1 as if this pod were assumed on it, while exchange B is in flight.  The result
-      // is used when the candidate wins.  Default-plugin pods only: their evaluation reads nothing
-      // this AssumePod writes to memory, except host ports, excluded here.
+      // ======== helper wave: stage pod q+2's program; once phase 1 of pod q+1 is done and the
+      // selection wave's candidate known, prepare this workgroup's exchange-A granules of pod q+1
+      // both ways -- the candidate not chosen (phase 1 as it is), and chosen (its next evaluation
+      // with this pod assumed, computed in phase 1 for default-plugin pods) -- so the selection
+      // wave publishes the right pair as soon as exchange B resolves.
       const bool stage = q + 2 < lv.npods;
       if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
       if (stage) fetch(pod + 2);
@@ -1647,20 +1698,22 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
         __builtin_amdgcn_s_sleep(1);
       const int cand = __hip_atomic_load(&s_cand_node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       uint32_t cand_ok = 0;
-      if (more && cand >= 0 && (d.flags & DF_ASSUME)) {
+      if (more) {
         const uint8_t* nb = s_blob[bn];
         const PodDesc& nd = *reinterpret_cast<const PodDesc*>(nb);
-        if (post_ok(d, nd)) {
-          cand_ok = 1;
-          const int kw = cand / kBlock - k0, sl = cand % kBlock, cw = sl >> 6;
-          // the candidate's evaluation wave, as its partials for pod q+1 will be if it wins (the
-          // evaluation waves computed its next evaluation with this pod assumed in phase 1)
-          while (__hip_atomic_load(&s_e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                 (uint32_t)(kBlock / 64) * (uint32_t)(q + 2))
-            __builtin_amdgcn_s_sleep(1);
+        cand_ok = cand >= 0 && post_ok(d, nd) ? 1u : 0u;
+        while (__hip_atomic_load(&s_e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+               (uint32_t)(kBlock / 64) * (uint32_t)(q + 2))
+          __builtin_amdgcn_s_sleep(1);
+        int cw = -1;
+        unsigned long long tm = 0, tn = 0;
+        if (cand_ok) {  // the candidate's evaluation wave, as its partials will be if it wins
+          const int kw = cand / kBlock - k0, sl = cand % kBlock;
+          cw = sl >> 6;
           const bool cf = ((s_ball2[kw][cw] >> (sl & 63)) & 1ull) != 0;
           const int64_t crt = s_rt2[kw][sl], crn = s_rn2[kw][sl];
-          unsigned long long tm = s_tm[npar][cw * 64 + lane], tn = s_tn[npar][cw * 64 + lane];
+          tm = s_tm[npar][cw * 64 + lane];
+          tn = s_tn[npar][cw * 64 + lane];
           if (lane == (sl & 63)) {
             tm = tn = 0;
             for (int kk = 0; kk < nk; ++kk) {
@@ -1688,8 +1741,31 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
             s_cmn = tn;
           }
         }
+        if (lane == 0) {
+          uint32_t c = 0, bl = 0, cc = 0, cbl = 0;
+          unsigned long long xa = 0, xb = 0, ca = 0, cb = 0;
+          for (int v = 0; v < kBlock / 64; ++v) {
+            const uint32_t u0 = s_u[npar][0][v], u1 = s_u[npar][1][v];
+            const unsigned long long x0v = s_x[npar][0][v], x1v = s_x[npar][1][v];
+            c += u0;
+            bl += u1;
+            xa = x0v > xa ? x0v : xa;
+            xb = x1v > xb ? x1v : xb;
+            const uint32_t w0 = v == cw ? s_ccnt : u0, w1 = v == cw ? s_cbelow : u1;
+            const unsigned long long y0 = v == cw ? tm : x0v, y1 = v == cw ? tn : x1v;
+            cc += w0;
+            cbl += w1;
+            ca = y0 > ca ? y0 : ca;
+            cb = y1 > cb ? y1 : cb;
+          }
+          a_granules(c, bl, xa, xb, &s_ga[0], &s_ga[1]);
+          a_granules(cc, cbl, ca, cb, &s_ga[2], &s_ga[3]);
+        }
       }
-      if (lane == 0) s_cand_ok = cand_ok;
+      if (lane == 0) {
+        s_cand_ok = cand_ok;
+        __hip_atomic_store(&s_ga_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       if (stage) land(bs);
     } else if (more) {
       // ======== evaluation waves: phase 1 of pod q+1 against the cores before this pod's assume.
@@ -1708,8 +1784,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       const int win = s_win;
       const int wsl = win >= 0 ? win - k0 * kBlock : -1;  // kk * kBlock + slot
       const bool owner_wg = F > 0 && wsl >= 0 && (d.flags & DF_ASSUME);
-      if (!owner_wg) {
-        if (more && threadIdx.x == kBlock) publish_a(q + 1, npar);
+      if (!owner_wg) {  // exchange A of pod q+1 already published by the selection wave
         if (F == 0) {
           if (w == 0 && t == 0) commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
         } else if (wsl >= 0 && t == wsl % kBlock) {  // chosen here, not assumed
@@ -1736,7 +1811,6 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
           s_u[npar][1][cw] = s_cbelow;
           s_x[npar][0][cw] = s_cmt;
           s_x[npar][1][cw] = s_cmn;
-          publish_a(q + 1, npar);
           if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);
         }

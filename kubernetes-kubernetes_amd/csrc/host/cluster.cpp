@@ -262,15 +262,18 @@ void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo
   }
 }
 
-int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done, int32_t slot) {
+// node_override: the node an assumed pod was placed on (the spec itself is left unbound)
+int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done, int32_t slot,
+                     const std::string* node_override) {
   const std::string uid = uid_override.empty() ? p.uid : uid_override;
-  if (p.node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
+  const std::string& node_name = node_override ? *node_override : p.node_name;
+  if (node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
   if (pods.count(uid)) { err = "pod " + uid + " exists"; return KSG_EEXIST; }
-  NodeRec* r = node(p.node_name);
-  if (!r) { err = "unknown node " + p.node_name; return KSG_ENOTFOUND; }
+  NodeRec* r = node(node_name);
+  if (!r) { err = "unknown node " + node_name; return KSG_ENOTFOUND; }
   BoundPod bp;
   bp.uid = uid;
-  bp.node = p.node_name;
+  bp.node = node_name;
   bp.res = calc_resources(p);
   bp.with_affinity = p.has_pod_affinity || p.has_pod_anti;
   pods_with_affinity += bp.with_affinity ? 1 : 0;

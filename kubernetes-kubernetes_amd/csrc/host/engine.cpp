@@ -12,6 +12,7 @@
 // run_batch() then launches k_filter_score + k_select per pod on one stream with no host
 // round trip inside the batch (device-side AssumePod), and reads the results back once.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -862,6 +863,7 @@ double Engine::algo_bytes(const PodDesc& d) const {
 Engine::~Engine() {
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : cev) (void)hipEventDestroy(e);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_wgcnt, &d_fail})
     if (b->p) (void)hipFree(b->p);
@@ -909,7 +911,7 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena
     if ((rc = ensure(d_arena, (size_t)arena_words * 8 + 8))) return rc;
     if (d_arena.bytes != old) HIPCHK(hipMemsetAsync(d_arena.p, 0, d_arena.bytes, c->stream));
   }
-  const size_t need = desc_bytes + (size_t)pods * (8 + sizeof(PodStats) + sizeof(DevResult)) + 256;
+  const size_t need = desc_bytes + (size_t)pods * (8 + sizeof(PodStats) + sizeof(DevResult) + 4) + 256;
   if (h_pinned_bytes < need) {
     if (h_pinned) (void)hipHostFree(h_pinned);
     h_pinned = nullptr;
@@ -953,6 +955,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (int i = 0; i < n; ++i) results[i] = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
     return KSG_OK;
   }
+  using clk = std::chrono::steady_clock;
+  const auto T0 = clk::now();
   // ---- compile every pod (may materialise label columns / relayout the mirror)
   std::vector<CompiledPod> cp(n);
   int64_t start = c->next_start;
@@ -970,6 +974,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       c->next_start = (c->next_start + cp[i].num_all) % N;
     }
   }
+  const auto T1 = clk::now();
   int rc = c->ensure_mirror();
   if (rc) return rc;
   // ---- stage descriptors + stats in pinned memory, one H2D
@@ -1047,7 +1052,33 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
 #endif
     }
   }
+  // Host/device pipeline: the batch is enqueued as up to four chunks, each followed by the D2H of
+  // its results (and of the loop's give-up flag) and an event, so the host's bookkeeping of chunk
+  // k (the cache's assumed pods) runs while the device schedules chunk k+1.  Every pod was compiled
+  // above, against the cache as it was when the batch started, so the order of host work does not
+  // change any result.
+  DevResult* hr = (DevResult*)(hs + n);
+  uint32_t* hfail = (uint32_t*)(hr + n);
+  const int CH = (!comm && !eval && n >= 256) ? (n + 3) / 4 : n;
+  struct Chunk { int a, b; };
+  std::vector<Chunk> chunks;
+  while (cev.size() < (size_t)(n + CH - 1) / CH) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    cev.push_back(e);
+  }
+  auto close_chunk = [&](int upto) -> int {
+    const int a = chunks.empty() ? 0 : chunks.back().b;
+    HIPCHK(hipMemcpyAsync(hr + a, (DevResult*)d_results.p + a, (size_t)(upto - a) * sizeof(DevResult),
+                          hipMemcpyDeviceToHost, s));
+    if (use_loop) HIPCHK(hipMemcpyAsync(hfail + chunks.size(), d_fail.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(cev[chunks.size()], s));
+    chunks.push_back({a, upto});
+    return KSG_OK;
+  };
   for (int i = 0; i < n && !comm;) {
+    if (i > 0 && i % CH == 0 && (chunks.empty() || chunks.back().b < i))
+      if ((rc = close_chunk(i))) return rc;
     if (cp[i].error) {
       ++i;
       continue;
@@ -1055,7 +1086,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (use_loop && loop_ok(cp[i])) {  // a run of node-local pods: one k_sched_loop launch
       int j = i;
       double rb = 0;
-      while (j < n && j - i < kLoopMaxPods && loop_ok(cp[j])) rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data()));
+      const int cut = (i / CH + 1) * CH;
+      while (j < n && j < cut && j - i < kLoopMaxPods && loop_ok(cp[j]))
+        rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data()));
       while (lev.size() < 2 * (runs.size() + 1)) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -1088,8 +1121,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     ++i;
   }
   HIPCHK(hipEventRecord(ev1, s));
-  DevResult* hr = (DevResult*)(hs + n);
-  HIPCHK(hipMemcpyAsync(hr, d_results.p, (size_t)n * sizeof(DevResult), hipMemcpyDeviceToHost, s));
+  const auto T2 = clk::now();
+  if ((rc = close_chunk(n))) return rc;
   std::vector<uint32_t> st;
   std::vector<int64_t> outs, tot;
   if (eval) {
@@ -1100,7 +1133,45 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     HIPCHK(hipMemcpyAsync(outs.data(), d_out.p, outs.size() * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
   }
+  // results + host shadow of the device-side assumes for pods [a, b)
+  auto settle = [&](int a, int b) -> int {
+    for (int i = a; i < b; ++i) {
+      ksg_result& r = results[i];
+      if (cp[i].error) {
+        r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
+        c->pod_table_drop(cp[i].slot);
+        continue;
+      }
+      const DevResult& d = hr[i];
+      r.status = d.status;
+      r.node_index = d.node;
+      r.feasible_nodes = d.feasible;
+      r.evaluated_nodes = d.feasible > 0 ? cp[i].num_all : (cp[i].prefilter_reject ? 0 : cp[i].num_all);
+      r.total_score = d.feasible > 1 ? d.total : 0;
+      if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
+      if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
+        static uint64_t seq = 0;
+        std::string uid = pods[i]->uid + "#a" + std::to_string(++seq);
+        int rc2 = c->add_pod(*pods[i], uid, /*device_done=*/true, cp[i].slot, &c->order()[r.node_index]);
+        if (rc2) return rc2;
+        assumed[handles.empty() ? -1 : handles[i]] = uid;
+      } else {
+        c->pod_table_drop(cp[i].slot);  // not placed: the reserved pod-table slot never went live
+      }
+    }
+    return KSG_OK;
+  };
+  if (chunks.size() > 1)  // pipelined: settle each chunk as soon as its results have landed
+    for (size_t k = 0; k < chunks.size(); ++k) {
+      HIPCHK(hipEventSynchronize(cev[k]));
+      if (use_loop && hfail[k]) {
+        c->err = "k_sched_loop: a workgroup never reached a per-pod arrival counter (spin limit)";
+        return KSG_EDEVICE;
+      }
+      if ((rc = settle(chunks[k].a, chunks[k].b))) return rc;
+    }
   HIPCHK(hipStreamSynchronize(s));
+  const auto T3 = clk::now();
   if (comm && comm->batch_end()) {
     c->err = comm->err;
     return KSG_EDEVICE;
@@ -1264,31 +1335,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
 
   // ---- results + host shadow of the device-side assumes
-  for (int i = 0; i < n; ++i) {
-    ksg_result& r = results[i];
-    if (cp[i].error) {
-      r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
-      c->pod_table_drop(cp[i].slot);
-      continue;
-    }
-    const DevResult& d = hr[i];
-    r.status = d.status;
-    r.node_index = d.node;
-    r.feasible_nodes = d.feasible;
-    r.evaluated_nodes = d.feasible > 0 ? cp[i].num_all : (cp[i].prefilter_reject ? 0 : cp[i].num_all);
-    r.total_score = d.feasible > 1 ? d.total : 0;
-    if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
-    if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
-      PodSpec ap = *pods[i];
-      ap.node_name = c->order()[r.node_index];
-      static uint64_t seq = 0;
-      std::string uid = ap.uid + "#a" + std::to_string(++seq);
-      int rc2 = c->add_pod(ap, uid, /*device_done=*/true, cp[i].slot);
-      if (rc2) return rc2;
-      assumed[handles.empty() ? -1 : handles[i]] = uid;
-    } else {
-      c->pod_table_drop(cp[i].slot);  // not placed: the reserved pod-table slot never went live
-    }
+  if (chunks.size() <= 1)
+    if ((rc = settle(0, n))) return rc;
+  if (c->cfg.loop_stamps) {
+    const auto T4 = clk::now();
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    std::fprintf(stderr, "[host, us per pod] compile %.3f  stage+launch %.3f  wait %.3f  results+assume %.3f\n",
+                 us(T0, T1) / n, us(T1, T2) / n, us(T2, T3) / n, us(T3, T4) / n);
   }
   if (eval) {
     const int32_t N = m.n;

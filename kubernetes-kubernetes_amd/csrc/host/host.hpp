@@ -228,7 +228,8 @@ class Cluster {
   int remove_node(const std::string& name);
   // device_done: the HBM mirror already holds the pod (device-side AssumePod)
   // slot: the pod-table slot reserved for an assumed pod at compile time (-1: allocate one)
-  int add_pod(const PodSpec& p, const std::string& uid_override = "", bool device_done = false, int32_t slot = -1);
+  int add_pod(const PodSpec& p, const std::string& uid_override = "", bool device_done = false, int32_t slot = -1,
+              const std::string* node_override = nullptr);
   int remove_pod(const std::string& uid);
   int32_t pods_with_affinity = 0;
 
@@ -375,6 +376,7 @@ class Engine {
   DevBuf d_xa, d_xp, d_xb;  // node-sharded exchange vectors, one set per pod of the batch
   DevBuf d_wgcnt, d_fail, d_stamps;  // k_sched_loop: per-pod per-workgroup counts, give-up flag, stamps
   std::vector<hipEvent_t> lev;  // k_sched_loop timing events (pairs)
+  std::vector<hipEvent_t> cev;  // run_batch pipeline: one event per chunk (results landed)
   int run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int n, int* launches, double* bytes,
                   int* timed);
   void* h_pinned = nullptr;

@@ -231,6 +231,18 @@ class Backend:
         self._chk(self.f["schedule_batch"](self.ctx, hs, n, FLAG_ASSUME if assume else 0, rs), "schedule_batch")
         return [rs[i] for i in range(n)]
 
+    @staticmethod
+    def batch_arrays(handles):
+        """(c_int32 handle array, Result array) for schedule_batch_into: built once, outside a timed loop."""
+        n = len(handles)
+        return (C.c_int32 * n)(*handles), (Result * n)()
+
+    def schedule_batch_into(self, hs, rs, assume=True):
+        """ksg_schedule_batch over a prebuilt handle array into a prebuilt Result array (the shape a
+        cgo caller uses: no per-pod Python objects)."""
+        self._chk(self.f["schedule_batch"](self.ctx, hs, len(hs), FLAG_ASSUME if assume else 0, rs), "schedule_batch")
+        return rs
+
     def forget(self, handle):
         self._chk(self.f["forget"](self.ctx, handle), "forget")
 

