@@ -31,7 +31,7 @@ namespace ksg {
 struct NodeCore {
   int64_t acpu, amem, aeph, rcpu, rmem, reph, nzcpu, nzmem;
   int32_t apods, npods;
-  uint32_t flags, tlo, thi;
+  uint32_t flags, tlo, thi, ilo, ihi;  // taint and image CSR ranges
 };
 __device__ __forceinline__ NodeCore load_core(const MirrorView& m, int i) {
   NodeCore c;
@@ -48,6 +48,8 @@ __device__ __forceinline__ NodeCore load_core(const MirrorView& m, int i) {
   c.flags = m.flags[i];
   c.tlo = m.taint_off[i];
   c.thi = m.taint_off[i + 1];
+  c.ilo = m.img_off[i];
+  c.ihi = m.img_off[i + 1];
   return c;
 }
 
@@ -159,9 +161,9 @@ __device__ int64_t balanced_alloc_score(const MirrorView& m, const NodeCore& nc,
 }
 
 // image_locality.go:70-152 (per-image scaled scores precomputed per pod on the host)
-__device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+__device__ __forceinline__ int64_t image_score_range(const MirrorView& m, const uint8_t* base, const PodDesc& d,
+                                                     uint32_t lo, uint32_t hi) {
   const ImageTerm* terms = at<ImageTerm>(base, d.img_off);
-  const uint32_t lo = m.img_off[i], hi = m.img_off[i + 1];
   int64_t sum = 0;
   for (int k = 0; k < d.n_img; ++k) {
     const uint32_t want = (uint32_t)terms[k].image;
@@ -173,6 +175,9 @@ __device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const P
   if (sum < minT) sum = minT;
   else if (sum > maxT) sum = maxT;
   return go_div(100 * (sum - minT), maxT - minT);
+}
+__device__ int64_t image_score(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i) {
+  return image_score_range(m, base, d, m.img_off[i], m.img_off[i + 1]);
 }
 
 // ---- diagnostic build (make DIAG=1 -> lib/libksg_diag.so): per-step stamps inside eval_node ----------
@@ -645,7 +650,8 @@ __device__ __forceinline__ NodeEval eval_core_fast(const MirrorView& m, const No
         bal_with != kNoBal ? bal_with : bal2(nc.rcpu + pf.bpr_cpu, nc.acpu, nc.rmem + pf.bpr_mem, nc.amem);
     fixed += (100 / 2 + (100 / 2 + with - bal_wo) / 2) * pf.wt_bal;
   }
-  r.fixed = fixed;  // ImageLocality: no image of the pod exists in the cluster -> 0 (host-checked)
+  if ((sm >> P_IMG) & 1u) fixed += image_score_range(m, base, d, nc.ilo, nc.ihi) * d.weight[P_IMG];
+  r.fixed = fixed;
   DIAG_STAMP(14);
   return r;
 }
@@ -1315,6 +1321,7 @@ struct LoopCores {
   int64_t bwo[kLoopMaxBlk][kBlock];  // BalancedAllocation without the pod (pod-independent)
   int32_t apods[kLoopMaxBlk][kBlock], npods[kLoopMaxBlk][kBlock];
   uint32_t flags[kLoopMaxBlk][kBlock], tlo[kLoopMaxBlk][kBlock], thi[kLoopMaxBlk][kBlock];
+  uint32_t ilo[kLoopMaxBlk][kBlock], ihi[kLoopMaxBlk][kBlock];
 };
 __device__ __forceinline__ NodeCore lds_core(const LoopCores& L, int kk, int t) {
   NodeCore c;
@@ -1331,6 +1338,8 @@ __device__ __forceinline__ NodeCore lds_core(const LoopCores& L, int kk, int t) 
   c.flags = L.flags[kk][t];
   c.tlo = L.tlo[kk][t];
   c.thi = L.thi[kk][t];
+  c.ilo = L.ilo[kk][t];
+  c.ihi = L.ihi[kk][t];
   return c;
 }
 __device__ __forceinline__ void lds_put_dynamic(LoopCores& L, int kk, int t, const NodeCore& c) {
@@ -1422,6 +1431,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
         s_core.flags[kk][t] = c.flags;
         s_core.tlo[kk][t] = c.tlo;
         s_core.thi[kk][t] = c.thi;
+        s_core.ilo[kk][t] = c.ilo;
+        s_core.ihi[kk][t] = c.ihi;
         lds_put_dynamic(s_core, kk, t, c);
       }
     }
@@ -1532,6 +1543,42 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     publish_partials(par);
     if (lane == 0) __hip_atomic_fetch_add(&s_e_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
+  // phase 2 over the slots of evaluation waves [vlo, vhi) of every block of my range (the selection
+  // wave takes all four: splitting it with the helper wave slowed phase 1 more than it saved): positions in
+  // the rotated feasible list, NormalizeScore + weights, the best packed (TotalScore, pre-order) key
+  auto phase2_half = [&](int vlo, int vhi, uint32_t acc, uint32_t F, uint32_t ps_before, int64_t mx_t, int64_t mx_n,
+                         const PodDesc& d, int par, unsigned long long* key, int* knode) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+      if (kk < nk) {
+        // every LDS read of the block issued up front (unconditional), then the arithmetic
+        unsigned long long ballot[kBlock / 64];
+        int64_t fx[kBlock / 64], rt[kBlock / 64], rn[kBlock / 64];
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+          ballot[v] = s_ball[par][kk][v];
+          if (v >= vlo && v < vhi) {
+            fx[v] = s_fx[par][kk][v * 64 + lane];
+            rt[v] = s_rt[par][kk][v * 64 + lane];
+            rn[v] = s_rn[par][kk][v * 64 + lane];
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+          if (v >= vlo && v < vhi && ((ballot[v] >> lane) & 1ull)) {
+            const uint32_t g = acc + wave_prefix_count(ballot[v], lane);
+            const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
+            const unsigned long long kv = pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos);
+            if (kv > *key) {
+              *key = kv;
+              *knode = (k0 + kk) * kBlock + v * 64 + lane;
+            }
+          }
+          acc += (uint32_t)__popcll(ballot[v]);
+        }
+      }
+    }
+  };
   // exchange A of pod `pq` (program parity par): this workgroup's two granules from the four
   // evaluation waves' partials.  One thread.
   auto publish_a = [&](int pq, int par) __attribute__((always_inline)) {
@@ -1613,36 +1660,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       const int64_t mx_t = tmax ? (int64_t)tmax - 1 : 0, mx_n = nmax ? (int64_t)nmax - 1 : 0;
       unsigned long long key = 0;
       int knode = -1;
-      if (ok) {
-#pragma unroll
-        for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-          if (kk < nk) {
-            // every LDS read of the block issued up front (unconditional), then the arithmetic
-            unsigned long long ballot[kBlock / 64];
-            int64_t fx[kBlock / 64], rt[kBlock / 64], rn[kBlock / 64];
-#pragma unroll
-            for (int v = 0; v < kBlock / 64; ++v) {
-              ballot[v] = s_ball[par][kk][v];
-              fx[v] = s_fx[par][kk][v * 64 + lane];
-              rt[v] = s_rt[par][kk][v * 64 + lane];
-              rn[v] = s_rn[par][kk][v * 64 + lane];
-            }
-#pragma unroll
-            for (int v = 0; v < kBlock / 64; ++v) {
-              if ((ballot[v] >> lane) & 1ull) {
-                const uint32_t g = acc + wave_prefix_count(ballot[v], lane);
-                const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-                const unsigned long long kv = pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos);
-                if (kv > key) {
-                  key = kv;
-                  knode = (k0 + kk) * kBlock + v * 64 + lane;
-                }
-              }
-              acc += (uint32_t)__popcll(ballot[v]);
-            }
-          }
-        }
-      }
+      if (ok) phase2_half(0, kBlock / 64, acc, F, ps_before, mx_t, mx_n, d, par, &key, &knode);
       const unsigned long long wkey = wave_max_u64(key);
       const unsigned long long hold = __ballot(key == wkey && key != 0ull);
       const int cand = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;

@@ -543,7 +543,6 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     // no existing anti-affinity) leave their mask bits set but never reject: not a reason to leave
     const bool topo_filter = D.n_ptsf > 0 || D.n_raff > 0 || D.n_ranti > 0 || (D.ipa_flags & IPA_EXIST_FILTER);
     if (mode == CYCLE && shape && D.n_scalar == 0 && !topo_filter && !(smask & topo) &&
-        (D.n_img == 0 || !(smask & (1u << P_IMG))) &&
         !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR)) &&
         c->alloc_bound < ((int64_t)1 << 52) / 100)
       D.flags |= DF_FAST;

@@ -78,6 +78,27 @@ def main():
     for kn, t in traffic.items():
         json.dump(t, open(os.path.join(out, f"traffic_{kn}.json"), "w"), indent=1)
 
+    # shader-counter pass (scripts/gpu_prof_sq.sh): instruction mix per wave and per pod, clock
+    p = os.path.join(PROF, "pmc_sq", "run_results.db")
+    if os.path.exists(p):
+        cc = sqlite3.connect(p)
+        sq = {}
+        for name, cn, val in cc.execute("select kernel_name, counter_name, value from counters_collection"):
+            if "k_sched_loop" in name:
+                sq.setdefault(cn, []).append(val)
+        if sq:
+            avg = {k: sum(v) / len(v) for k, v in sq.items()}
+            waves = avg.get("SQ_WAVES", 1.0) or 1.0
+            sl = [f"# rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES "
+                  f"GRBM_GUI_ACTIVE GRBM_COUNT, k_sched_loop, per dispatch ({loop_pods} pods) (tag {tag})"]
+            for k in sorted(avg):
+                sl.append(f"{k:20s} {avg[k]:16.1f}")
+            for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+                if k in avg:
+                    sl.append(f"{k} per wave per pod: {avg[k] / waves / loop_pods:.1f}")
+            open(os.path.join(out, f"{tag}_pmc_sq.txt"), "w").write("\n".join(sl) + "\n")
+            print("\n".join(sl))
+
 
 if __name__ == "__main__":
     main()
