@@ -19,8 +19,9 @@ all-reduces over xGMI carry the feasible counts, NormalizeScore maxima and the p
 fixed); `strong` keeps the cluster fixed (default for c5, the 100k-node config).  `--mode
 replicas` instead runs N independent schedulers (own cluster, own pod stream, no collective).
 
-The CPU baseline is the parity oracle (oracle/, a C++ restatement of the reference) timed
-on a bounded sample of the same pod stream from the same initial state, one host thread.
+The CPU baseline is the parity oracle (oracle/, a C++ restatement of the reference) timed on a
+bounded sample of the same pod stream from the same initial state: its Filter/Score loops over
+nodes on 16 host threads (the reference's default parallelism), and on one thread beside it.
 """
 import argparse
 import json
@@ -55,6 +56,8 @@ def parse():
     ap.add_argument("--timing-stride", type=int, default=8, help="time every k-th filter kernel with HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the multi-core CPU baseline (the reference's default parallelism is 16)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
@@ -66,11 +69,24 @@ WORKLOAD_NAMES = {"c2": "SchedulingBasic", "c2-hetero": "SchedulingBasic (hetero
                         "anti-affinity / preferred anti-affinity / zone spread)"}
 
 
-def cpu_baseline(nodes, init, pods, budget_s):
-    """Oracle (C++ restatement of the reference), 1 thread, same pods from the same state."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(nodes, init, pods, budget_s, threads=1):
+    """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
+    Filter / Score loops over nodes on a pool of that many threads (the reference's
+    Parallelizer.Until with parallelism 16), results identical to the sequential oracle
+    (tests/test_oracle_parallel.py)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_binding import oracle
-    o = oracle({})
+    o = oracle({"cpuThreads": threads} if threads > 1 else {})
     for n in nodes:
         o.add_node(n)
     for p in init:
@@ -192,11 +208,16 @@ def main():
     if rank == 0:
         cpu = None
         if not a.no_cpu_baseline and world == 1:
-            v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds)
-            cpu = {"value": round(v, 2), "unit": "pods/s", "cores": 1, "kind": "port",
+            # the reference's default parallelism (16 goroutines over nodes), then one thread
+            v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads)
+            v1, done1, cdt1 = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1)
+            cpu = {"value": round(v, 2), "unit": "pods/s", "cores": a.cpu_threads, "kind": "port",
                    "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
-                             f"{cdt:.1f} s, oracle/ C++ restatement, 1 thread"}
+                             f"{cdt:.1f} s, oracle/ C++ restatement, Filter/Score over nodes on "
+                             f"{a.cpu_threads} threads ({cpu_model()}, {os.cpu_count()} logical CPUs visible)",
+                   "single_thread": {"value": round(v1, 2), "cores": 1,
+                                     "sample": f"first {done1} pods, {cdt1:.1f} s, 1 thread"}}
         out = {
             "metric": "pods scheduled/sec + node-evals/sec at 5k/100k nodes, 1/2/4/8 MI355X",
             "value": round(pods_s, 2),

@@ -16,7 +16,12 @@
 //            (backend/cache/node_tree.go), image states (cache.go:712-759)
 // Parity is pinned by the reference's own unit-test vectors (tests/golden/).
 #include <algorithm>
+#include <atomic>
 #include <climits>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -106,6 +111,7 @@ static int plugin_id(const std::string& n) {
 
 struct Config {
   int pct = 100;
+  int threads = 1;  // CPU-baseline mode: Filter / Score over nodes on this many threads (Parallelizer.Until)
   bool taintCompareOps = false;  // featureGates.TaintTolerationComparisonOperators
   bool enabled[KSG_NUM_PLUGINS];
   int64_t weight[KSG_NUM_PLUGINS];
@@ -141,6 +147,7 @@ static std::vector<std::pair<std::string, int64_t>> decode_res_specs(const mj::V
 static bool decode_config(const mj::Value& v, Config* c, std::string* err) {
   if (!v.is_obj()) return true;
   if (v.has("percentageOfNodesToScore")) c->pct = (int)v.i64("percentageOfNodesToScore");
+  if (v.has("cpuThreads")) c->threads = std::max(1, (int)v.i64("cpuThreads"));
   if (auto fg = v.has("featureGates")) c->taintCompareOps = fg->boolean("TaintTolerationComparisonOperators");
   if (auto w = v.has("scoreWeights"))
     for (auto& kv : w->obj) {
@@ -253,6 +260,7 @@ struct ImageState { int64_t size = 0; std::set<std::string> nodes; };
 using HostPorts = std::map<std::string, std::set<std::pair<std::string, int32_t>>>;  // ip -> {(proto, port)}
 
 struct NodeInfoO {  // framework.NodeInfo (framework/types.go:172-220)
+  int pos = -1;  // index in the snapshot list (set by rebuild_list; the result's node index)
   Node node;
   std::vector<PodInfo*> pods;
   std::vector<PodInfo*> podsWithAffinity, podsWithRequiredAntiAffinity;
@@ -368,8 +376,68 @@ static Status mk(int code, uint32_t r) { Status s; s.code = code; s.reasons = r;
 // ---------------------------------------------------------------------------
 // the oracle context
 // ---------------------------------------------------------------------------
+// Fork-join pool for the CPU-baseline mode: the reference runs the per-node Filter and Score
+// loops through Parallelizer.Until with 16 goroutines (framework/parallelize/parallelism.go:28,
+// schedule_one.go:840, framework.go:1378).  Workers stay parked on a condition variable between
+// pods; run(n, fn) calls fn(k) for k in [0, n) on n threads (the caller is worker 0).
+class Pool {
+ public:
+  explicit Pool(int n) : n_(n) {
+    for (int k = 1; k < n; ++k) th_.emplace_back([this, k] { loop(k); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return n_; }
+  void run(const std::function<void(int)>& fn) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      fn_ = &fn;
+      left_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return left_ == 0; });
+  }
+
+ private:
+  void loop(int k) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        f = fn_;
+      }
+      (*f)(k);
+      std::lock_guard<std::mutex> g(m_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  uint64_t gen_ = 0;
+  int left_ = 0;
+  bool stop_ = false;
+};
+
 struct ksgo_ctx {
   Config cfg;
+  std::unique_ptr<Pool> pool;  // cfg.threads > 1
   std::string err;
   std::map<std::string, Namespace> namespaces;
   std::map<std::string, std::unique_ptr<NodeInfoO>> nodes;
@@ -396,6 +464,7 @@ struct ksgo_ctx {
         auto& na = tree[z];
         if (idx < na.size()) list.push_back(nodes[na[idx]].get());
       }
+    for (size_t i = 0; i < list.size(); ++i) list[i]->pos = (int)i;
     listDirty = false;
   }
   const Labels* ns_labels(const std::string& ns) const {  // GetNamespaceLabelsSnapshot (ipa plugin.go:150-159)
@@ -1170,8 +1239,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     if (ev->plugin_scores)
       for (int i = 0; i < N * KSG_NUM_PLUGINS; ++i) ev->plugin_scores[i] = 0;
   }
-  std::unordered_map<const NodeInfoO*, int> index;
-  for (int i = 0; i < N; ++i) index[c->list[i]] = i;
+  auto idx_of = [](const NodeInfoO* ni) { return ni->pos; };
   if (N == 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }  // ErrNoNodesAvailable
 
   Cycle cy;
@@ -1257,24 +1325,53 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
   }
   std::vector<NodeInfoO*> feasible;
   int failed = 0;
-  for (int i = 0; i < numAll; ++i) {
-    NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
+  auto filter_node = [&](NodeInfoO* ni) {
     Status st;
     for (int p : kFilterOrder) {
       if (cy.skipFilter[p]) continue;
       st = run_filter(cy, p, ni);
       if (!st.ok()) { st.plugin = p; break; }
     }
-    if (st.ok()) {
-      if ((int64_t)feasible.size() + 1 > numToFind) break;  // cancel: enough feasible nodes
-      feasible.push_back(ni);
-    } else {
-      ++failed;
-      if (ev) {
-        int idx = index[ni];
-        if (ev->node_code) ev->node_code[idx] = (uint8_t)st.code;
-        if (ev->node_plugin) ev->node_plugin[idx] = (uint8_t)st.plugin;
-        if (ev->node_reasons) ev->node_reasons[idx] = st.reasons;
+    return st;
+  };
+  auto record_failed = [&](NodeInfoO* ni, const Status& st) {
+    if (ev) {
+      int idx = idx_of(ni);
+      if (ev->node_code) ev->node_code[idx] = (uint8_t)st.code;
+      if (ev->node_plugin) ev->node_plugin[idx] = (uint8_t)st.plugin;
+      if (ev->node_reasons) ev->node_reasons[idx] = st.reasons;
+    }
+  };
+  if (c->pool && numToFind >= numAll) {
+    // CPU-baseline mode: contiguous ranges of the rotated order on the pool's threads, then the
+    // per-range feasible lists concatenated in order -- the sequential loop's result exactly
+    // (with every node to be found there is no early stop to race on)
+    const int T = c->pool->size();
+    std::vector<std::vector<NodeInfoO*>> part(T);
+    std::vector<int> pfail(T, 0);
+    c->pool->run([&](int k) {
+      const int a = (int)((int64_t)numAll * k / T), b = (int)((int64_t)numAll * (k + 1) / T);
+      for (int i = a; i < b; ++i) {
+        NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
+        Status st = filter_node(ni);
+        if (st.ok()) part[k].push_back(ni);
+        else { ++pfail[k]; record_failed(ni, st); }
+      }
+    });
+    for (int k = 0; k < T; ++k) {
+      feasible.insert(feasible.end(), part[k].begin(), part[k].end());
+      failed += pfail[k];
+    }
+  } else {
+    for (int i = 0; i < numAll; ++i) {
+      NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
+      Status st = filter_node(ni);
+      if (st.ok()) {
+        if ((int64_t)feasible.size() + 1 > numToFind) break;  // cancel: enough feasible nodes
+        feasible.push_back(ni);
+      } else {
+        ++failed;
+        record_failed(ni, st);
       }
     }
   }
@@ -1289,7 +1386,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
   }
   res->feasible_nodes = (int)feasible.size();
   if (feasible.size() == 1) {  // :588-598
-    res->node_index = index[feasible[0]];
+    res->node_index = idx_of(feasible[0]);
     res->evaluated_nodes = 1 + diagLen;
     return KSG_OK;
   }
@@ -1315,10 +1412,24 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     std::vector<std::vector<int64_t>> scores(active.size(), std::vector<int64_t>(F, 0));
     for (size_t a = 0; a < active.size(); ++a) {
       int p = active[a];
-      for (int i = 0; i < F; ++i) {
-        int code;
-        scores[a][i] = score_node(cy, p, feasible[i], &code);
-        if (code != KSG_CODE_SUCCESS) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+      if (c->pool) {  // CPU-baseline mode: framework.go:1378 scores nodes in parallel
+        const int T = c->pool->size();
+        std::atomic<bool> bad{false};
+        c->pool->run([&](int k) {
+          const int lo = (int)((int64_t)F * k / T), hi = (int)((int64_t)F * (k + 1) / T);
+          for (int i = lo; i < hi; ++i) {
+            int code;
+            scores[a][i] = score_node(cy, p, feasible[i], &code);
+            if (code != KSG_CODE_SUCCESS) bad = true;
+          }
+        });
+        if (bad) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+      } else {
+        for (int i = 0; i < F; ++i) {
+          int code;
+          scores[a][i] = score_node(cy, p, feasible[i], &code);
+          if (code != KSG_CODE_SUCCESS) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+        }
       }
       normalize_scores(cy, p, scores[a], feasible);
     }
@@ -1331,17 +1442,17 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
         if (s > 100 || s < 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }
         int64_t w = s * c->cfg.weight[p];
         totals[i] += w;
-        if (ev && ev->plugin_scores) ev->plugin_scores[(size_t)p * N + index[feasible[i]]] = w;
+        if (ev && ev->plugin_scores) ev->plugin_scores[(size_t)p * N + idx_of(feasible[i])] = w;
       }
     }
   }
   if (ev && ev->total_scores)
-    for (int i = 0; i < F; ++i) ev->total_scores[index[feasible[i]]] = totals[i];
+    for (int i = 0; i < F; ++i) ev->total_scores[idx_of(feasible[i])] = totals[i];
   // ---- host selection: heap.Init + heap.Pop (schedule_one.go:605-606,1054-1063)
   std::vector<HeapEnt> h(F);
   for (int i = 0; i < F; ++i) h[i] = {totals[i], 0, i};
   int win = heap_pop_index(h);
-  res->node_index = index[feasible[win]];
+  res->node_index = idx_of(feasible[win]);
   res->total_score = totals[win];
   return KSG_OK;
 }
@@ -1368,6 +1479,7 @@ ksgo_ctx* ksgo_create(const char* json, size_t len) {
     delete c;
     return nullptr;
   }
+  if (c->cfg.threads > 1) c->pool.reset(new Pool(c->cfg.threads));
   return c;
 }
 const char* ksgo_create_error(void) { return g_create_error.c_str(); }

@@ -1,0 +1,51 @@
+"""The oracle's CPU-baseline mode (Filter / Score over nodes on a thread pool, as the reference's
+Parallelizer.Until with 16 goroutines) gives exactly the sequential oracle's results: every
+pod's result tuple and per-node evaluation output, over random clusters with every plugin.
+bench.py times this mode as the multi-core CPU baseline, so it must be the same algorithm."""
+import pytest
+
+from fuzz_gen import namespaces, rand_cluster, rand_pod
+from oracle_binding import oracle
+
+
+def _build(cfg, nodes, existing):
+    b = oracle(cfg)
+    for ns in namespaces():
+        b.upsert_namespace(ns)
+    for n in nodes:
+        b.add_node(n)
+    for p in existing:
+        b.add_pod(p)
+    return b
+
+
+@pytest.mark.parametrize("seed,threads", [(0, 2), (1, 4), (2, 16), (3, 3), (4, 16), (5, 7)])
+def test_parallel_oracle_matches_sequential(seed, threads):
+    rng, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=150 + 37 * seed, n_existing=60)
+    seq = _build(cfg, nodes, existing)
+    par = _build(dict(cfg, cpuThreads=threads), nodes, existing)
+    try:
+        for k in range(40):
+            pod = rand_pod(rng, k, names)
+            rs, es = seq.schedule_one(seq.compile(pod), assume=True, evaluate=True)
+            rp, ep = par.schedule_one(par.compile(pod), assume=True, evaluate=True)
+            assert rs.as_tuple() == rp.as_tuple(), f"pod {k}"
+            for key in es:
+                assert es[key] == ep[key], f"pod {k}: eval[{key}]"
+    finally:
+        seq.close()
+        par.close()
+
+
+def test_parallel_oracle_batch_c2_shape():
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(600, 100, 150, hetero=True)
+    seq = _build({}, nodes, init)
+    par = _build({"cpuThreads": 16}, nodes, init)
+    try:
+        a = seq.schedule_batch([seq.compile(p) for p in pods], assume=True)
+        b = par.schedule_batch([par.compile(p) for p in pods], assume=True)
+        assert [r.as_tuple() for r in a] == [r.as_tuple() for r in b]
+    finally:
+        seq.close()
+        par.close()
