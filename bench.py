@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--timing-stride", type=int, default=8, help="time every k-th filter kernel with HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-device-exchange", action="store_true",
+                    help="sharded: the per-pod RCCL all-reduce path for every pod (default: the loop's device exchange)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the multi-core CPU baseline (the reference's default parallelism is 16)")
     ap.add_argument("--traffic", default=None,
@@ -130,7 +132,7 @@ def main():
     n_nodes = (a.nodes or (100000 if c5 else 5000)) * grow
     n_init = (a.init_pods if a.init_pods is not None else (10000 if c5 else 1000)) * grow
     n_meas = a.steps * a.batch
-    n_warm = a.warmup * a.batch
+    n_warm = max(a.warmup, 1 if sharded else 0) * a.batch
     if a.workload in ("c2", "c2-hetero"):
         nodes, init, pods = synth.scheduling_basic(n_nodes, n_init, n_warm + n_meas, hetero=a.workload == "c2-hetero")
     elif a.workload == "c3":
@@ -140,30 +142,53 @@ def main():
     else:
         nodes, init, pods = synth.topology_spreading(n_nodes, n_init, n_warm + n_meas,
                                                      preferred_anti=a.workload == "c4-anti")
-    cfg = {"device": local, "kernelTimingStride": a.timing_stride}
-    if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
-        obj = [comm_unique_id() if rank == 0 else None]
-        if dist is not None:
-            dist.broadcast_object_list(obj, src=0)
-        cfg["distributed"] = {"worldSize": world, "rank": rank, "ncclId": obj[0]}
-    else:
+    if not sharded:
         for k, p in enumerate(pods):  # distinct uids per rank (independent replicas)
             p["metadata"]["uid"] = f"r{rank}-{k}"
-    s = Scheduler(cfg)
-    for n in nodes:
-        s.add_node(n)
-    for p in init:
-        s.add_pod(p)
-    handles = [s.compile(p) for p in pods]
-    warm, meas = handles[:n_warm], handles[n_warm:]
 
-    for w in range(a.warmup):  # untimed; then ForgetPod so the timed run starts from the config state
-        s.schedule_batch(warm[w * a.batch:(w + 1) * a.batch], assume=True)
-    for h in warm:
+    def build(dev_exchange):
+        """Scheduler with the cluster loaded, warm-up batches run (then forgotten, so the timed run
+        starts from the config state); None if the warm-up failed on this rank."""
+        cfg = {"device": local, "kernelTimingStride": a.timing_stride}
+        if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
+            obj = [comm_unique_id() if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(obj, src=0)
+            cfg["distributed"] = {"worldSize": world, "rank": rank, "ncclId": obj[0]}
+            cfg["deviceExchange"] = dev_exchange
+        s = Scheduler(cfg)
+        for n in nodes:
+            s.add_node(n)
+        for p in init:
+            s.add_pod(p)
+        handles = [s.compile(p) for p in pods]
         try:
-            s.forget(h)
-        except Exception:
-            pass
+            for w in range(max(a.warmup, 1 if sharded else 0)):
+                s.schedule_batch(handles[w * a.batch:(w + 1) * a.batch], assume=True)
+            for h in handles[:max(a.warmup, 1 if sharded else 0) * a.batch]:
+                try:
+                    s.forget(h)
+                except Exception:
+                    pass
+        except Exception as e:  # sharded device exchange unavailable here: reported, then the all-reduce path
+            print(f"rank {rank}: warm-up with deviceExchange={dev_exchange} failed: {e}", file=sys.stderr, flush=True)
+            s.close()
+            return None, None
+        return s, handles
+
+    dev_exchange = sharded and not a.no_device_exchange
+    s, handles = build(dev_exchange)
+    if sharded and dist is not None:  # every rank keeps the exchange mode only if every rank's warm-up passed
+        ok = torch.tensor([1 if s is not None else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and s is not None:
+            s.close()
+            s = None
+    if s is None:
+        dev_exchange = False
+        s, handles = build(False)
+    n_warm = max(a.warmup, 1 if sharded else 0) * a.batch
+    warm, meas = handles[:n_warm], handles[n_warm:]
 
     # the per-step handle / result arrays are built before timing, as a cgo caller holds them
     arrays = [s.batch_arrays(meas[st * a.batch:(st + 1) * a.batch]) for st in range(a.steps)]
@@ -238,8 +263,10 @@ def main():
                                    + (" (BASELINE configs[4])" if c5 else ""),
                        "nodes": n_nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": 100,
                        "plugins": "default",
-                       "parallelism": (f"nodes-sharded{world} (RCCL all-reduce per pod)" if sharded
-                                       else f"replicas{world}" if world > 1 else "single")},
+                       "parallelism": (f"nodes-sharded{world}" if sharded
+                                       else f"replicas{world}" if world > 1 else "single"),
+                       "exchange": ("device (loop granules stored into every rank's memory over xGMI)"
+                                    if dev_exchange else "RCCL all-reduce per pod") if sharded else None},
             "placed": placed,
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

@@ -319,14 +319,19 @@ struct ShardView {
 // range of node blocks for the whole run and meet at two device-scope arrival counters per pod.
 struct LoopView {
   int32_t first_pod, npods;  // pods [first_pod, first_pod + npods) of the batch
-  int32_t nwg;               // workgroups (all resident; one per CU at most)
-  int32_t nblocks;           // kBlock-node blocks of the snapshot
-  unsigned long long* gran;  // [npods][nwg][3] exchange granules (zeroed by the host per batch)
+  int32_t nwg;               // workgroups of this rank (all resident; one per CU at most)
+  int32_t blk0, nblk;        // this rank's kBlock-node blocks [blk0, blk0 + nblk) (all of them unsharded)
+  int32_t world, rank;       // node shards: participants are world * nwg workgroups, rank-major
+  uint32_t tag;              // this batch's granule tag (1..65535; 0 never valid)
+  unsigned long long* gran[kMaxShards];  // every rank's granule array, [pods][world * nwg][kGran]; [rank] is local
   uint32_t* fail;            // set when a spin gives up (a workgroup never arrived)
-  unsigned long long* stamps;  // diagnostic build only: [npods][8] s_memrealtime per phase (nullptr)
+  unsigned long long* stamps;  // diagnostic: [npods][8] s_memrealtime per phase (nullptr)
   const uint32_t* desc_bytes;  // [batch pods] program sizes (indexed like BatchView::desc_off)
-  unsigned long long* wstamps;  // diagnostic: [npods][nwg][2] exchange A / B publish times (nullptr)
+  unsigned long long* wstamps;  // diagnostic: [npods][nwg][8] exchange / owner times (nullptr)
 };
+// exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
+// A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)
+constexpr int kGran = 4;
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)
 KSG_HD inline uint32_t pack_status(uint32_t code, uint32_t plugin, uint32_t reasons) {

@@ -650,7 +650,8 @@ __device__ __forceinline__ NodeEval eval_core_fast(const MirrorView& m, const No
         bal_with != kNoBal ? bal_with : bal2(nc.rcpu + pf.bpr_cpu, nc.acpu, nc.rmem + pf.bpr_mem, nc.amem);
     fixed += (100 / 2 + (100 / 2 + with - bal_wo) / 2) * pf.wt_bal;
   }
-  if ((sm >> P_IMG) & 1u) fixed += image_score_range(m, base, d, nc.ilo, nc.ihi) * d.weight[P_IMG];
+  // ImageLocality: no image of the pod present anywhere (n_img == 0) scores 0 on every node
+  if (((sm >> P_IMG) & 1u) && d.n_img > 0) fixed += image_score_range(m, base, d, nc.ilo, nc.ihi) * d.weight[P_IMG];
   r.fixed = fixed;
   DIAG_STAMP(14);
   return r;
@@ -1242,59 +1243,67 @@ __global__ __launch_bounds__(kBlock) void k_max_reduce(unsigned long long* dst, 
 //            (TotalScore, heap pre-order key) max of my nodes
 //   xchg B   one granule {valid, key} per workgroup, swept the same way; the thread holding the
 //            global maximum applies AssumePod and writes the result.
-// Granules live in a per-batch array zeroed by the host; every granule is written exactly once.
+// A granule is {tag(16) | payload(48)}: the tag is the batch's (host counter, never 0), so an array
+// needs no zeroing between batches and a stale granule never matches.  Every granule is written
+// exactly once per batch, into every rank's array (the local one, and the peers' over xGMI).
 constexpr uint32_t kSpinLimit = 1u << 24;
-constexpr unsigned long long kValid = 1ull << 63;
+constexpr unsigned long long kPayload = (1ull << 48) - 1ull;
 
 // diagnostic phase stamps (config "loopStamps"): workgroup 0's lane 0, 100 MHz constant clock
 __device__ __forceinline__ void stamp(const LoopView& lv, int q, int k) {
   if (lv.stamps && threadIdx.x == 0) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
-// One wave: poll granules g[v * stride + off] for v < G until all are valid (relaxed agent-scope
-// loads, s_sleep between passes).  Fills x[] (up to kMaxSweep per lane); false on give-up.
-constexpr int kMaxSweep = 4;  // G <= 256 workgroups
-__device__ __forceinline__ bool sweep(const unsigned long long* g, int G, int stride, int off,
-                                      unsigned long long (&x)[kMaxSweep], uint32_t* fail) {
-  const int lane = threadIdx.x & 63;
-  for (uint32_t spins = 0;; ++spins) {
-    bool ok = true;
-#pragma unroll
-    for (int r = 0; r < kMaxSweep; ++r) {
-      const int v = lane + 64 * r;
-      x[r] = v < G ? __hip_atomic_load(g + (size_t)v * stride + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : kValid;
-      ok &= (x[r] & kValid) != 0;
-    }
-    if (__all(ok)) return true;
-    if (spins >= kSpinLimit) {
-      __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    if ((spins & 63u) == 63u && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-    __builtin_amdgcn_s_sleep(1);
+// publish one granule of pod q to every rank.  Unsharded: an agent-scope store.  Sharded: system
+// scope into each rank's array (the peers' are IPC-mapped, uncached device memory).
+__device__ __forceinline__ void gran_put(const LoopView& lv, int q, int gid, int slot, unsigned long long payload) {
+  const int P = lv.world * lv.nwg;
+  const unsigned long long v = ((unsigned long long)lv.tag << 48) | (payload & kPayload);
+  const size_t at = ((size_t)q * P + gid) * kGran + slot;
+  if (lv.world == 1) {
+    __hip_atomic_store(lv.gran[0] + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
+  for (int r = 0; r < lv.world; ++r) __hip_atomic_store(lv.gran[r] + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// the two granules of exchange A in one pass per poll
-__device__ __forceinline__ bool sweep2(const unsigned long long* g, int G, unsigned long long (&x0)[kMaxSweep],
-                                       unsigned long long (&x1)[kMaxSweep], uint32_t* fail) {
+// One wave: poll granules [slot0, slot0 + NS) of all P participants of pod q in the local array
+// until every tag matches (relaxed loads, s_sleep between passes).  x[s][r] = payload of
+// participant lane + 64 r; false on give-up.
+constexpr int kMaxSweep = 4;  // P <= 256 participants
+template <int NS>
+__device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep]) {
   const int lane = threadIdx.x & 63;
+  const int P = lv.world * lv.nwg;
+  const unsigned long long* g = lv.gran[lv.world == 1 ? 0 : lv.rank] + (size_t)q * P * kGran + slot0;
+  const unsigned long long want = (unsigned long long)lv.tag;
   for (uint32_t spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < kMaxSweep; ++r) {
       const int v = lane + 64 * r;
-      x0[r] = v < G ? __hip_atomic_load(g + (size_t)v * 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kValid;
-      x1[r] = v < G ? __hip_atomic_load(g + (size_t)v * 3 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kValid;
-      ok &= (x0[r] & x1[r] & kValid) != 0;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        unsigned long long y = want << 48;
+        if (v < P)
+          y = lv.world == 1 ? __hip_atomic_load(g + (size_t)v * kGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : __hip_atomic_load(g + (size_t)v * kGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok &= (y >> 48) == want;
+        x[k][r] = y & kPayload;
+      }
     }
     if (__all(ok)) return true;
-    if (spins >= kSpinLimit) {
-      __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (spins >= kSpinLimit) {  // give up: record which pod / granule / participant never came
+      const unsigned long long miss = __ballot(!ok);
+      if (lane == 0) {
+        __hip_atomic_store(lv.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       return false;
     }
-    if ((spins & 63u) == 63u && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if ((spins & 63u) == 63u && __hip_atomic_load(lv.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -1366,10 +1375,10 @@ __device__ __forceinline__ void assume_core(NodeCore& c, const PodDesc& d) {
 // host-checked: +1 so that 0 means "no feasible node")
 __device__ __forceinline__ void a_granules(uint32_t c, uint32_t bl, unsigned long long a, unsigned long long bb,
                                            unsigned long long* g0, unsigned long long* g1) {
-  const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;
-  const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;
-  *g0 = kValid | ((unsigned long long)bl << 24) | c;
-  *g1 = kValid | (np1 << 31) | tp1;
+  const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;   // < 2^24 (host-checked)
+  const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;  // < 2^24
+  *g0 = ((unsigned long long)bl << 20) | c;                                          // counts < 2^20
+  *g1 = (np1 << 24) | tp1;
 }
 
 // Can pod `nd`'s evaluation of a node be computed, before pod `d` is assumed, as it will be after?
@@ -1396,7 +1405,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   __shared__ unsigned long long s_x[2][2][kBlock / 64];
   __shared__ uint32_t s_off[kLoopMaxPods], s_len[kLoopMaxPods];  // the run's program offsets / sizes
   __shared__ uint32_t s_ok, s_F, s_cand_ok;
-  __shared__ int s_win, s_cand_q, s_cand_node, s_ipa;
+  __shared__ int s_win, s_cand_q, s_cand_node, s_ipa, s_gnode;
   __shared__ unsigned long long s_tm[2][kBlock], s_tn[2][kBlock];  // per-slot maxima of phase 1 (encoded)
   __shared__ uint32_t s_e_done;  // evaluation waves that finished a phase 1 (monotonic)
   // the candidate's state if it wins, prepared by the helper wave: its core columns with the pod
@@ -1407,13 +1416,13 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   __shared__ uint32_t s_ccnt, s_cbelow;
   __shared__ unsigned long long s_best;
   const int w = blockIdx.x, G = lv.nwg;
-  const int k0 = (int)((int64_t)lv.nblocks * w / G), k1 = (int)((int64_t)lv.nblocks * (w + 1) / G);
+  const int gid = lv.rank * G + w, P = lv.world * G;  // my participant index, participants (rank-major)
+  const int k0 = lv.blk0 + (int)((int64_t)lv.nblk * w / G), k1 = lv.blk0 + (int)((int64_t)lv.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool sel = wave == kBlock / 64;      // the selection wave: exchanges + phase 2
   const bool hlp = wave == kBlock / 64 + 1;  // the helper wave: candidate pre-evaluation + staging
   const int t = (int)threadIdx.x;          // evaluation waves: my slot in each block of my range
-  unsigned long long* gran = lv.gran;      // [npods][G][3]
   auto stamp_s = [&](int q, int k) {       // diagnostic phase stamps: WG 0's selection lane 0
     if (lv.stamps && w == 0 && threadIdx.x == kBlock) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
@@ -1582,7 +1591,6 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   // exchange A of pod `pq` (program parity par): this workgroup's two granules from the four
   // evaluation waves' partials.  One thread.
   auto publish_a = [&](int pq, int par) __attribute__((always_inline)) {
-    unsigned long long* g = gran + (size_t)pq * G * 3;
     uint32_t c = 0, bl = 0;
     unsigned long long a = 0, bb = 0;
     for (int v = 0; v < kBlock / 64; ++v) {
@@ -1593,8 +1601,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     }
     unsigned long long g0, g1;
     a_granules(c, bl, a, bb, &g0, &g1);
-    __hip_atomic_store(g + (size_t)w * 3, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + (size_t)w * 3 + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gran_put(lv, pq, gid, 0, g0);
+    gran_put(lv, pq, gid, 1, g1);
     if (lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
   };
 
@@ -1627,24 +1635,23 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     const bool more = q + 1 < lv.npods;
     const uint8_t* base = s_blob[bq];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
-    unsigned long long* gq = gran + (size_t)q * G * 3;
 
     if (sel) {
       // ======== selection wave: exchange A, phase 2, exchange B, pre-evaluation, staging ========
       stamp_s(q, 0);  // exchange A of this pod was published at the end of the previous one
-      unsigned long long x0[kMaxSweep], x1[kMaxSweep];
-      bool ok = sweep2(gq, G, x0, x1, lv.fail);
+      unsigned long long xa[2][kMaxSweep];
+      bool ok = gran_sweep<2>(lv, q, 0, xa);
       uint32_t F = 0, wp = 0, bf = 0;
       unsigned long long tmax = 0, nmax = 0;
 #pragma unroll
       for (int r = 0; r < kMaxSweep; ++r) {
         const int v = lane + 64 * r;
-        if (v < G) {
-          const uint32_t c = (uint32_t)(x0[r] & 0xffffffull);
+        if (v < P) {
+          const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
           F += c;
-          if (v < w) wp += c;
-          bf += (uint32_t)((x0[r] >> 24) & 0xffffffull);
-          const unsigned long long tv = x1[r] & 0x7fffffffull, nv = (x1[r] >> 31) & 0xffffffffull;
+          if (v < gid) wp += c;
+          bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
+          const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
           tmax = tv > tmax ? tv : tmax;
           nmax = nv > nmax ? nv : nmax;
         }
@@ -1666,27 +1673,46 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       const int cand = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
       stamp_s(q, 2);
       if (lane == 0) {
-        __hip_atomic_store(gq + (size_t)w * 3 + 2, kValid | wkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gran_put(lv, q, gid, 2, wkey);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
+        if (lv.world > 1) gran_put(lv, q, gid, 3, (unsigned long long)(uint32_t)cand);
         if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_cand_node, cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&s_cand_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       stamp_s(q, 3);
-      unsigned long long xb[kMaxSweep];
-      ok = ok && sweep(gq, G, 3, 2, xb, lv.fail);
+      unsigned long long xb[2][kMaxSweep];
+      if (lv.world == 1) {  // unsharded: the owner is found locally, only the keys cross workgroups
+        unsigned long long k1[1][kMaxSweep];
+        ok = ok && gran_sweep<1>(lv, q, 2, k1);
+#pragma unroll
+        for (int r = 0; r < kMaxSweep; ++r) {
+          xb[0][r] = k1[0][r];
+          xb[1][r] = 0;
+        }
+      } else {
+        ok = ok && gran_sweep<2>(lv, q, 2, xb);
+      }
       unsigned long long bm = 0;
+      int bnode = -1;
 #pragma unroll
       for (int r = 0; r < kMaxSweep; ++r) {
-        const unsigned long long v = (lane + 64 * r) < G ? (xb[r] & ~kValid) : 0ull;
-        bm = v > bm ? v : bm;
+        const unsigned long long v = (lane + 64 * r) < P ? xb[0][r] : 0ull;
+        if (v > bm) {
+          bm = v;
+          bnode = (int)(uint32_t)xb[1][r];
+        }
       }
-      bm = wave_max_u64(bm);
+      const unsigned long long gbest = wave_max_u64(bm);
+      const unsigned long long bh = __ballot(bm == gbest && gbest != 0ull);  // keys are unique
+      const int gnode = bh ? __builtin_amdgcn_readlane(bnode, (int)__builtin_ctzll(bh)) : -1;
+      bm = gbest;
       const int win = (F > 0 && wkey == bm && cand >= 0) ? cand : -1;
       if (lane == 0) {
         s_ok = ok ? 1u : 0u;
         s_best = bm;
         s_F = F;
         s_win = win;
+        s_gnode = F > 0 ? gnode : -1;
       }
       // exchange A of pod q+1, now: the pair the helper prepared for this outcome.  A chosen node
       // whose next evaluation was not prepared (generic pods) is fixed up after the barrier, and its
@@ -1696,9 +1722,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
           __builtin_amdgcn_s_sleep(1);
         const bool chosen = win >= 0 && (d.flags & DF_ASSUME);
         if (lane == 0 && (!chosen || s_cand_ok)) {
-          unsigned long long* g = gran + (size_t)(q + 1) * G * 3 + (size_t)w * 3;
-          __hip_atomic_store(g, s_ga[chosen ? 2 : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(g + 1, s_ga[chosen ? 3 : 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          gran_put(lv, q + 1, gid, 0, s_ga[chosen ? 2 : 0]);
+          gran_put(lv, q + 1, gid, 1, s_ga[chosen ? 3 : 1]);
           if (lv.wstamps) lv.wstamps[((size_t)(q + 1) * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
         }
       }
@@ -1802,11 +1827,15 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       const int win = s_win;
       const int wsl = win >= 0 ? win - k0 * kBlock : -1;  // kk * kBlock + slot
       const bool owner_wg = F > 0 && wsl >= 0 && (d.flags & DF_ASSUME);
+      const int gnode = s_gnode;
+      const bool remote = lv.world > 1 && F > 0 && (gnode < lv.blk0 * kBlock || gnode >= (lv.blk0 + lv.nblk) * kBlock);
       if (!owner_wg) {  // exchange A of pod q+1 already published by the selection wave
         if (F == 0) {
           if (w == 0 && t == 0) commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
         } else if (wsl >= 0 && t == wsl % kBlock) {  // chosen here, not assumed
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, nullptr, s_ipa);
+        } else if (remote && w == 0 && t == 0) {  // chosen on another rank: the result and this replica's assume
+          commit_result(m, b, base, d, b.stats + pod, pod, F, gnode, s_best, nullptr, s_ipa);
         }
       } else if (s_cand_ok) {  // the helper prepared everything: LDS stores, then publish
         if (t == wsl % kBlock) {

@@ -6,6 +6,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstring>
+#include <string>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -23,9 +25,6 @@ hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int n
 class RcclComm : public Comm {
  public:
   ncclComm_t comm = nullptr;
-  ~RcclComm() override {
-    if (comm) (void)ncclCommDestroy(comm);
-  }
   int all_reduce_max(unsigned long long* buf, size_t count, hipStream_t s) override {
     const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, comm, s);
     if (r != ncclSuccess) {
@@ -36,7 +35,57 @@ class RcclComm : public Comm {
   }
   int group_begin() override { return ncclGroupStart() == ncclSuccess ? KSG_OK : KSG_EDEVICE; }
   int group_end() override { return ncclGroupEnd() == ncclSuccess ? KSG_OK : KSG_EDEVICE; }
+  std::vector<void*> opened;  // peers' IPC mappings (closed on destruction)
+  ~RcclComm() override;
+  // IPC handles all-gathered over RCCL, then opened (hipIpcOpenMemHandle maps the peer GPU's memory)
+  int share_buffers(void* mine, std::vector<void*>* all) override {
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, mine) != hipSuccess) {
+      err = "hipIpcGetMemHandle failed";
+      return KSG_EDEVICE;
+    }
+    const size_t hb = sizeof(hipIpcMemHandle_t);
+    char* d = nullptr;
+    hipStream_t s = nullptr;
+    std::vector<char> hostv((size_t)world * hb);
+    if (hipMalloc(&d, (size_t)world * hb) != hipSuccess || hipStreamCreate(&s) != hipSuccess) {
+      err = "share_buffers: allocation failed";
+      return KSG_EDEVICE;
+    }
+    int rc = KSG_OK;
+    if (hipMemcpy(d + (size_t)rank * hb, &h, hb, hipMemcpyHostToDevice) != hipSuccess ||
+        ncclAllGather(d + (size_t)rank * hb, d, hb, ncclChar, comm, s) != ncclSuccess ||
+        hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(hostv.data(), d, (size_t)world * hb, hipMemcpyDeviceToHost) != hipSuccess) {
+      err = "share_buffers: handle all-gather failed";
+      rc = KSG_EDEVICE;
+    }
+    (void)hipFree(d);
+    (void)hipStreamDestroy(s);
+    if (rc) return rc;
+    all->assign(world, nullptr);
+    for (int r = 0; r < world; ++r) {
+      if (r == rank) {
+        (*all)[r] = mine;
+        continue;
+      }
+      hipIpcMemHandle_t ph;
+      std::memcpy(&ph, hostv.data() + (size_t)r * hb, hb);
+      void* p = nullptr;
+      if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        err = "hipIpcOpenMemHandle failed for rank " + std::to_string(r);
+        return KSG_EDEVICE;
+      }
+      opened.push_back(p);
+      (*all)[r] = p;
+    }
+    return KSG_OK;
+  }
 };
+RcclComm::~RcclComm() {
+  for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+  if (comm) (void)ncclCommDestroy(comm);
+}
 
 static bool hex_to_id(const std::string& hex, ncclUniqueId* id) {
   if (hex.size() != 2 * sizeof(id->internal)) return false;
@@ -150,6 +199,17 @@ class LocalComm : public Comm {
       err = "local exchange: reduce launch failed";
       return KSG_EDEVICE;
     }
+    return KSG_OK;
+  }
+
+  int share_buffers(void* mine, std::vector<void*>* all) override {  // one process: the pointers themselves
+    int sl = 0;
+    if (!rendezvous((unsigned long long*)mine, nullptr, 0, &sl)) {
+      err = "local exchange: buffer rendezvous timed out";
+      return KSG_EDEVICE;
+    }
+    all->assign(world, nullptr);
+    for (int r = 0; r < world; ++r) (*all)[r] = g->snap_bufs[sl][r];
     return KSG_OK;
   }
 

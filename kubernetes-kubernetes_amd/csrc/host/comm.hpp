@@ -17,6 +17,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace ksg {
 
@@ -33,6 +34,9 @@ class Comm {
   virtual int group_end() { return 0; }
   // end of a batch: every rank's stream has drained (already synchronised by the caller)
   virtual int batch_end() { return 0; }
+  // collective: every rank passes its device buffer; all[r] becomes rank r's buffer as mapped in
+  // this process (in-process: the pointer itself; RCCL ranks: an IPC mapping of the peer's memory)
+  virtual int share_buffers(void* mine, std::vector<void*>* all) = 0;
   std::string err;
 };
 

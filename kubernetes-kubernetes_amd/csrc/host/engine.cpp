@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 
@@ -814,20 +815,20 @@ bool Engine::loop_ok(const CompiledPod& p) const {
   if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE)) return false;
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
   if (p.blob.size() > (size_t)kBlobLds) return false;
-  // the exchange granules carry raw TaintToleration counts in 31 bits, raw NodeAffinity sums in
-  // 32 bits and the packed key in 63 bits: bound the pod's possible values
+  // the exchange granules carry raw TaintToleration counts and raw NodeAffinity sums (+1) in 24
+  // bits each and the packed key in 48: bound the pod's possible values
   int64_t wsum = 0;
   for (int q = 0; q < kNumPlugins; ++q) {
     if (d.weight[q] < 0) return false;
     wsum += (d.score_mask >> q) & 1u ? d.weight[q] : 0;
   }
-  if (wsum > ((int64_t)1 << 26)) return false;  // TotalScore <= 100 * wsum < 2^33, key < 2^62
+  if (wsum * 100 >= ((int64_t)1 << 19)) return false;  // TotalScore <= 100 * wsum < 2^19, key < 2^48
   int64_t pref = 0;
   for (SelProg pg : {d.na_preferred, d.na_added_pref}) {
     const SelTerm* t = reinterpret_cast<const SelTerm*>(p.blob.data() + pg.term_off);
     for (int k = 0; k < pg.nterm; ++k) pref += t[k].weight < 0 ? -(int64_t)t[k].weight : t[k].weight;
   }
-  return pref < ((int64_t)1 << 31);
+  return pref < ((int64_t)1 << 24) - 1;
 }
 // Algorithmic HBM bytes of one k_filter_score launch: every SoA field the pod's active plugins
 // must read for a node, plus what the launch writes, each counted once per node.
@@ -864,7 +865,7 @@ Engine::~Engine() {
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
   for (hipEvent_t e : cev) (void)hipEventDestroy(e);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_wgcnt, &d_fail})
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -938,6 +939,52 @@ BatchView Engine::bview(int pods) {
   b.out_total = (int64_t*)d_total.p;
   b.arena = (unsigned long long*)d_arena.p;
   return b;
+}
+
+// The loop's exchange granule array: fixed size (kLoopMaxPods pods x 256 participants), zeroed once,
+// never reallocated (a sharded context's peers map it over IPC).  Sharded, it is uncached device
+// memory: the peers' stores arrive over xGMI and the sweeps must not read a stale cached line.
+int Engine::gran_setup() {
+  if (!gran_all.empty()) return KSG_OK;
+  const size_t bytes = (size_t)kLoopMaxPods * 256 * kGran * 8;
+  void* p = nullptr;
+  if (comm) HIPCHK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
+  else HIPCHK(hipMalloc(&p, bytes));
+  d_gran.p = p;
+  d_gran.bytes = bytes;
+  HIPCHK(hipMemset(p, 0, bytes));
+  HIPCHK(hipDeviceSynchronize());
+  if (comm) {
+    std::vector<void*> all;
+    if (comm->share_buffers(p, &all)) {
+      c->err = comm->err;
+      return KSG_EDEVICE;
+    }
+    for (void* q : all) gran_all.push_back((unsigned long long*)q);
+  } else {
+    gran_all.push_back((unsigned long long*)p);
+  }
+  return KSG_OK;
+}
+
+// Each loop launch gets the next tag (every rank issues the same launches, so the tags agree).
+// After 65535 launches the array is zeroed again; sharded, behind an exchange, so that no rank
+// publishes into a peer's array before that peer has cleared it.
+int Engine::next_gran_tag(uint32_t* tag) {
+  if (++gran_tag > 0xFFFFu) {
+    gran_tag = 1;
+    HIPCHK(hipMemsetAsync(d_gran.p, 0, d_gran.bytes, c->stream));
+    if (comm) {
+      int rc;
+      if ((rc = ensure(d_xb, XB_WORDS * 8))) return rc;
+      if (comm->all_reduce_max((unsigned long long*)d_xb.p, 1, c->stream)) {
+        c->err = comm->err;
+        return KSG_EDEVICE;
+      }
+    }
+  }
+  *tag = gran_tag;
+  return KSG_OK;
 }
 
 int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
@@ -1025,23 +1072,35 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   HIPCHK(hipEventRecord(ev0, s));
   int launches = 0, timed = 0;
   double bytes = 0;
-  if (comm) {
-    if ((rc = run_sharded(cp, bv, n, &launches, &bytes, &timed))) return rc;
-  }
-  // persistent-loop geometry: G resident workgroups, each <= 64 node blocks (k_sched_loop)
+  // persistent-loop geometry: G resident workgroups per rank, each <= kLoopMaxBlk node blocks of
+  // the rank's shard (k_sched_loop).  Sharded, every rank uses the same G (from the largest shard):
+  // the exchange has world * G participants.
   const int NB = (m.n + kBlock - 1) / kBlock;
-  const int max_wg = std::min(256, cu_count > 0 ? cu_count : 256);  // one resident workgroup per CU at most
+  const int W = comm ? c->cfg.world : 1;
+  int32_t sblk0 = 0, snblk = NB;
+  if (comm) shard_range(m.n, &sblk0, &snblk);
+  const int NBs = (NB + W - 1) / W;
+  // one resident workgroup per CU; in-process ranks share one device
+  const int cus = cu_count > 0 ? cu_count : 256;
+  const int max_wg = std::min(256 / W, comm && c->cfg.nccl_id.empty() ? cus / W : cus);
   int G = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
-  G = std::min(std::max(G, (NB + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(NB, max_wg));
-  const bool use_loop = !comm && !eval && c->cfg.persistent_loop && NB > 0 && (int64_t)G * kLoopMaxBlk >= NB &&
-                        (int64_t)c->taint_max_per_node < ((int64_t)1 << 30);
+  G = std::min(std::max(G, (NBs + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NBs, 1), max_wg));
+  // In-process ranks (localGroup, one device) need every rank's loop resident at once: each rank has
+  // its own stream, and streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, default 4)
+  // share queues and serialise.  Such groups keep the all-reduce path.
+  static const int hwq = [] {
+    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+    return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
+  }();
+  const bool dx = comm && c->cfg.dev_exchange && (!c->cfg.nccl_id.empty() || W < hwq);
+  const bool use_loop = (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
+                        (int64_t)G * kLoopMaxBlk >= NBs && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   struct LoopRun { int first, count; double bytes; };
   std::vector<LoopRun> runs;
   if (use_loop) {
-    if ((rc = ensure(d_wgcnt, (size_t)n * G * 3 * 8))) return rc;
+    if ((rc = gran_setup())) return rc;
     if ((rc = ensure(d_fail, 16))) return rc;
     HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
-    HIPCHK(hipMemsetAsync(d_wgcnt.p, 0, (size_t)n * G * 3 * 8, s));  // every granule invalid
     if (c->cfg.loop_stamps) {
       const size_t sb = (size_t)n * 8 * 8 + 64 * 8 + (size_t)n * G * 8 * 8;
       if ((rc = ensure(d_stamps, sb))) return rc;
@@ -1058,7 +1117,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // change any result.
   DevResult* hr = (DevResult*)(hs + n);
   uint32_t* hfail = (uint32_t*)(hr + n);
-  const int CH = (!comm && !eval && n >= 256) ? (n + 3) / 4 : n;
+  const int CH = ((!comm || dx) && !eval && n >= 256) ? (n + 3) / 4 : n;
   struct Chunk { int a, b; };
   std::vector<Chunk> chunks;
   while (cev.size() < (size_t)(n + CH - 1) / CH) {
@@ -1075,7 +1134,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     chunks.push_back({a, upto});
     return KSG_OK;
   };
-  for (int i = 0; i < n && !comm;) {
+  for (int i = 0; i < n && (!comm || dx);) {
     if (i > 0 && i % CH == 0 && (chunks.empty() || chunks.back().b < i))
       if ((rc = close_chunk(i))) return rc;
     if (cp[i].error) {
@@ -1087,20 +1146,36 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       double rb = 0;
       const int cut = (i / CH + 1) * CH;
       while (j < n && j < cut && j - i < kLoopMaxPods && loop_ok(cp[j]))
-        rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data()));
+        rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data())) *
+              (comm && m.n > 0 ? std::min(1.0, (double)snblk * kBlock / (double)m.n) : 1.0);
       while (lev.size() < 2 * (runs.size() + 1)) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
         lev.push_back(e);
       }
-      LoopView lv{i, j - i, G, NB, (unsigned long long*)d_wgcnt.p + (size_t)i * G * 3, (uint32_t*)d_fail.p,
-                  c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr,
-                  (const uint32_t*)d_off.p + n,
-                  c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr};
+      LoopView lv{};
+      lv.first_pod = i;
+      lv.npods = j - i;
+      lv.nwg = G;
+      lv.blk0 = sblk0;
+      lv.nblk = snblk;
+      lv.world = W;
+      lv.rank = comm ? c->cfg.rank : 0;
+      if ((rc = next_gran_tag(&lv.tag))) return rc;
+      for (int r = 0; r < W; ++r) lv.gran[r] = gran_all[r];
+      lv.fail = (uint32_t*)d_fail.p;
+      lv.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr;
+      lv.desc_bytes = (const uint32_t*)d_off.p + n;
+      lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr;
       HIPCHK(launch_sched_loop(m, bv, lv, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
       runs.push_back({i, j - i, rb});
       launches += j - i;
       i = j;
+      continue;
+    }
+    if (comm) {  // sharded, not loop-eligible: the per-pod RCCL exchange path
+      if ((rc = run_sharded(cp, bv, i, i + 1, &launches, &bytes, &timed))) return rc;
+      ++i;
       continue;
     }
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
@@ -1119,6 +1194,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     launches++;
     ++i;
   }
+  if (comm && !dx)  // sharded without the device exchange: every pod through the RCCL path
+    if ((rc = run_sharded(cp, bv, 0, n, &launches, &bytes, &timed))) return rc;
   HIPCHK(hipEventRecord(ev1, s));
   const auto T2 = clk::now();
   if ((rc = close_chunk(n))) return rc;
@@ -1164,7 +1241,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (size_t k = 0; k < chunks.size(); ++k) {
       HIPCHK(hipEventSynchronize(cev[k]));
       if (use_loop && hfail[k]) {
-        c->err = "k_sched_loop: a workgroup never reached a per-pod arrival counter (spin limit)";
+        uint32_t f[4] = {0, 0, 0, 0};
+        (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
+        c->err = "k_sched_loop: an exchange granule never arrived (spin limit): pod " + std::to_string(f[1]) +
+                 " of its run, granule " + std::to_string(f[2]) + ", lane of the first missing participant " +
+                 std::to_string(f[3]);
         return KSG_EDEVICE;
       }
       if ((rc = settle(chunks[k].a, chunks[k].b))) return rc;
@@ -1377,7 +1458,7 @@ void Engine::shard_range(int32_t n, int32_t* blk0, int32_t* nblk) const {
 // Node-sharded cycles: per pod, the replicated pod-table aggregation, this rank's node blocks,
 // then the stream-ordered exchanges (comm.hpp) between the kernels -- 2 all-reduces per pod
 // (3 when PodTopologySpread scores) and still no host round trip inside the batch.
-int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int n, int* launches,
+int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int first, int last, int* launches,
                         double* bytes, int* timed_out) {
   hipStream_t s = c->stream;
   const MirrorView& m = c->view;
@@ -1400,7 +1481,7 @@ int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv,
     }
     return KSG_OK;
   };
-  for (int i = 0; i < n; ++i) {
+  for (int i = first; i < last; ++i) {
     if (cp[i].error) continue;
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
     if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));  // replicated pod table

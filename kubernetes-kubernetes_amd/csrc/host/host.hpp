@@ -144,6 +144,7 @@ struct Config {
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
+  bool dev_exchange = true;     // sharded: the loop's per-pod exchange device-to-device (granules over xGMI)
   bool loop_stamps = false;     // diagnostic: per-phase s_memrealtime stamps of k_sched_loop (stderr)
   // node-sharded evaluation: this context evaluates the snapshot-order block range of `rank`
   // out of `world`; the per-pod exchanges run over RCCL (nccl_id) or in-process (local_group)
@@ -374,11 +375,15 @@ class Engine {
   DevBuf d_descs, d_off, d_stats, d_results, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
   DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)
   DevBuf d_xa, d_xp, d_xb;  // node-sharded exchange vectors, one set per pod of the batch
-  DevBuf d_wgcnt, d_fail, d_stamps;  // k_sched_loop: per-pod per-workgroup counts, give-up flag, stamps
+  DevBuf d_gran, d_fail, d_stamps;  // k_sched_loop: exchange granules (local), give-up flag, stamps
+  std::vector<unsigned long long*> gran_all;  // every rank's granule array as mapped here ([rank] = d_gran)
+  uint32_t gran_tag = 0;
+  int gran_setup();
+  int next_gran_tag(uint32_t* tag);
   std::vector<hipEvent_t> lev;  // k_sched_loop timing events (pairs)
   std::vector<hipEvent_t> cev;  // run_batch pipeline: one event per chunk (results landed)
-  int run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int n, int* launches, double* bytes,
-                  int* timed);
+  int run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv, int first, int last, int* launches,
+                  double* bytes, int* timed);
   void* h_pinned = nullptr;
   size_t h_pinned_bytes = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
