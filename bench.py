@@ -162,6 +162,8 @@ def main():
         for p in init:
             s.add_pod(p)
         handles = [s.compile(p) for p in pods]
+        if dist is not None:  # the ranks' hosts loaded the cluster at their own pace: start together
+            dist.barrier()
         try:
             for w in range(max(a.warmup, 1 if sharded else 0)):
                 s.schedule_batch(handles[w * a.batch:(w + 1) * a.batch], assume=True)

@@ -1246,7 +1246,6 @@ __global__ __launch_bounds__(kBlock) void k_max_reduce(unsigned long long* dst, 
 // A granule is {tag(16) | payload(48)}: the tag is the batch's (host counter, never 0), so an array
 // needs no zeroing between batches and a stale granule never matches.  Every granule is written
 // exactly once per batch, into every rank's array (the local one, and the peers' over xGMI).
-constexpr uint32_t kSpinLimit = 1u << 24;
 constexpr unsigned long long kPayload = (1ull << 48) - 1ull;
 
 // diagnostic phase stamps (config "loopStamps"): workgroup 0's lane 0, 100 MHz constant clock
@@ -1277,6 +1276,9 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
   const int P = lv.world * lv.nwg;
   const unsigned long long* g = lv.gran[lv.world == 1 ? 0 : lv.rank] + (size_t)q * P * kGran + slot0;
   const unsigned long long want = (unsigned long long)lv.tag;
+  // give up after ~10 s of wall time (100 MHz constant clock): sharded ranks may start a launch
+  // seconds apart (their hosts load the cluster independently)
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   for (uint32_t spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
@@ -1293,7 +1295,8 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
       }
     }
     if (__all(ok)) return true;
-    if (spins >= kSpinLimit) {  // give up: record which pod / granule / participant never came
+    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
+      // give up: record which pod / granule / participant never came
       const unsigned long long miss = __ballot(!ok);
       if (lane == 0) {
         __hip_atomic_store(lv.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1092,7 +1092,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     const char* e = std::getenv("GPU_MAX_HW_QUEUES");
     return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
   }();
-  const bool dx = comm && c->cfg.dev_exchange && (!c->cfg.nccl_id.empty() || W < hwq);
+  const bool rccl = !c->cfg.nccl_id.empty();
+  const bool dx = comm && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) && (rccl || W < hwq);
   const bool use_loop = (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
                         (int64_t)G * kLoopMaxBlk >= NBs && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   struct LoopRun { int first, count; double bytes; };

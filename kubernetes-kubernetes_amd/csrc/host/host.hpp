@@ -144,7 +144,10 @@ struct Config {
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
-  bool dev_exchange = true;     // sharded: the loop's per-pod exchange device-to-device (granules over xGMI)
+  // sharded: the loop's per-pod exchange device-to-device (granules over xGMI).  Default on for RCCL
+  // ranks (one process per GPU); in-process groups (localGroup, one device) only when asked: their
+  // loops must share the device's queues, and residency of all of them at once is not guaranteed
+  int dev_exchange = -1;        // -1 default, 0 off, 1 on
   bool loop_stamps = false;     // diagnostic: per-phase s_memrealtime stamps of k_sched_loop (stderr)
   // node-sharded evaluation: this context evaluates the snapshot-order block range of `rank`
   // out of `world`; the per-pod exchanges run over RCCL (nccl_id) or in-process (local_group)

@@ -2,9 +2,9 @@
 
 W scheduler contexts on ONE GPU form an in-process exchange group ("localGroup"): each holds
 the whole cluster mirror, evaluates its contiguous range of the snapshot order, and exchanges
-counts / NormalizeScore maxima / best keys -- for loop-eligible pods through the persistent
-loop's granules stored into every rank's array (deviceExchange, the default), for the others
-through the same stream-ordered all-reduce slots the RCCL transport uses (comm.hpp).  Every rank must return the
+counts / NormalizeScore maxima / best keys through the same stream-ordered all-reduce slots the
+RCCL transport uses (comm.hpp); with deviceExchange (the RCCL ranks' default, opt-in here), the
+loop-eligible pods exchange through the persistent loop's granules stored into every rank's array.  Every rank must return the
 oracle's ScheduleResult for every pod of the stream (sequential assume semantics), including
 empty shards (clusters smaller than W * 256 nodes) and PodTopologySpread/InterPodAffinity pods.
 """
@@ -94,10 +94,10 @@ def test_random_streams_match_oracle(world, seed):
 
 
 @pytest.mark.parametrize("world,seed", [(2, 0), (3, 2)])
-def test_random_streams_match_oracle_exchange_path(world, seed):
-    """deviceExchange off: loop-eligible pods also take the per-pod all-reduce path."""
+def test_random_streams_match_oracle_device_exchange(world, seed):
+    """deviceExchange on (the RCCL ranks' default): loop-eligible pods exchange through granules."""
     rng, cfg, nodes, existing, names = rand_cluster(3000 + seed, n_nodes=[700, 1100, 900][seed], n_existing=120)
-    ranks, o = _group(world, dict(cfg, deviceExchange=False), nodes, existing)
+    ranks, o = _group(world, dict(cfg, deviceExchange=True), nodes, existing)
     _check(ranks, o, [rand_pod(rng, k, names) for k in range(80)], chunk=32)
 
 
@@ -109,7 +109,7 @@ def test_device_exchange_loop_c2(world):
     so W = 4 checks that they fall back to the all-reduce path."""
     from ksg.synth import scheduling_basic
     nodes, init, pods = scheduling_basic(600 * world + 77, 300, 600, hetero=True)
-    ranks, o = _group(world, {}, nodes, init)
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
     _check(ranks, o, pods, chunk=300)
 
 
