@@ -296,6 +296,13 @@ hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, co
   return hipGetLastError();
 }
 
+hipError_t warm_aggregate() {
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_aggregate));
+  if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_pts_score));
+  return e;
+}
+
 hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0, int nblk) {
   if (nblk < 0) nblk = (m.n + kBlock - 1) / kBlock;
   if (nblk == 0) return hipSuccess;

@@ -109,26 +109,44 @@ __device__ int64_t fit_score(const MirrorView& m, const NodeCore& nc, const uint
   return go_div(nodeScore, weightSum);
 }
 
-// balanced_allocation.go:220-254
-__device__ int64_t balanced_score(const int64_t* req, const int64_t* alloc, int n) {
-  double fr[8];
+// balanced_allocation.go:220-254, without private arrays (a per-lane array would live in scratch,
+// and a kernel with scratch waits for the runtime's scratch grant before its first wave starts).
+// Fraction f_k of resource k, or false when the node's allocatable is 0 (the reference skips it);
+// recomputed in the variance pass, bit-identically.
+__device__ __forceinline__ bool bal_frac(const MirrorView& m, const NodeCore& nc, const ScoreRes& r, int i, bool with,
+                                         double* f) {
+  if (r.kind == RES_SKIP) return false;
+  int64_t alloc, al;
+  node_res(m, nc, r, i, true, &alloc, &al);
+  if (alloc == 0) return false;
+  double x = (double)(with ? al + r.pod_req : al) / (double)alloc;
+  if (x > 1) x = 1;
+  *f = x;
+  return true;
+}
+
+__device__ int64_t balanced_score(const MirrorView& m, const NodeCore& nc, const ScoreRes* res, int n, int i,
+                                  bool with) {
   int nf = 0;
-  double total = 0;
+  double total = 0, f0 = 0, f1 = 0;
   for (int k = 0; k < n; ++k) {
-    if (alloc[k] == 0) continue;
-    double f = (double)req[k] / (double)alloc[k];
-    if (f > 1) f = 1;
+    double f;
+    if (!bal_frac(m, nc, res[k], i, with, &f)) continue;
     total = total + f;
-    fr[nf++] = f;
+    if (nf == 0) f0 = f;
+    else if (nf == 1) f1 = f;
+    ++nf;
   }
   double sd = 0.0;
   if (nf == 2) {
-    sd = fabs((fr[0] - fr[1]) / 2);
+    sd = fabs((f0 - f1) / 2);
   } else if (nf > 2) {
     double mean = total / (double)nf;
     double sum = 0;
-    for (int k = 0; k < nf; ++k) {
-      double dd = fr[k] - mean;
+    for (int k = 0; k < n; ++k) {
+      double f;
+      if (!bal_frac(m, nc, res[k], i, with, &f)) continue;
+      double dd = f - mean;
       double sq = dd * dd;
       sum = sum + sq;
     }
@@ -142,21 +160,8 @@ __device__ int64_t balanced_score(const int64_t* req, const int64_t* alloc, int 
 __device__ int64_t balanced_alloc_score(const MirrorView& m, const NodeCore& nc, const uint8_t* base,
                                         const PodDesc& d, int i) {
   const ScoreRes* res = at<ScoreRes>(base, d.bal_res_off);
-  int64_t requested[8], allocated[8], allocatable[8];
-  int n = d.n_bal_res;
-  for (int k = 0; k < n; ++k) {
-    requested[k] = allocated[k] = allocatable[k] = 0;
-    const ScoreRes r = res[k];
-    if (r.kind == RES_SKIP) continue;
-    int64_t alloc, al;
-    node_res(m, nc, r, i, true, &alloc, &al);
-    if (alloc == 0) continue;
-    allocatable[k] = alloc;
-    allocated[k] = al;
-    requested[k] = al + r.pod_req;
-  }
-  int64_t with = balanced_score(requested, allocatable, n);
-  int64_t without = balanced_score(allocated, allocatable, n);
+  const int64_t with = balanced_score(m, nc, res, d.n_bal_res, i, true);
+  const int64_t without = balanced_score(m, nc, res, d.n_bal_res, i, false);
   return 100 / 2 + (100 / 2 + with - without) / 2;  // balanced_allocation.go:204-218
 }
 
@@ -378,7 +383,7 @@ struct NodeEval {
 // non-normalising scores and the raw scores the normalising plugins need to the batch scratch
 // (the launch path's k_select reads them back; the persistent loop keeps them in registers).
 template <bool kStore>
-__device__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d, int pod,
+__device__ __forceinline__ NodeEval eval_node(const MirrorView& m, const BatchView& b, const uint8_t* base, const PodDesc& d, int pod,
                               int i, bool valid) {
   const bool eval = (d.flags & DF_EVAL_OUT) != 0;
   NodeEval r{0u, false, 0, 0, 0, 0};
@@ -1450,29 +1455,13 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     }
   }
 
-  // ---- program staging by the selection wave: registers first (issued early), LDS later
-  constexpr int kPre = 4;  // 4 KB of a program per register stage
-  uint4 pre[kPre];
-  uint32_t pre_bytes = 0;
-  const uint8_t* pre_src = nullptr;
-  auto fetch = [&](int pod) __attribute__((always_inline)) {
-    pre_src = b.descs + s_off[pod - lv.first_pod];
-    pre_bytes = s_len[pod - lv.first_pod];
-#pragma unroll
-    for (int r = 0; r < kPre; ++r) {
-      const uint32_t o = (uint32_t)lane + (uint32_t)r * 64u;
-      if (o < pre_bytes / 16u) pre[r] = reinterpret_cast<const uint4*>(pre_src)[o];
-    }
-  };
-  auto land = [&](int slot) __attribute__((always_inline)) {
+  // ---- program staging by the helper wave: straight from global memory into a free LDS slot (no
+  // register stage: one held across the helper's waits ended up in scratch)
+  auto stage_prog = [&](int pod, int slot) __attribute__((always_inline)) {
+    const uint4* src = reinterpret_cast<const uint4*>(b.descs + s_off[pod - lv.first_pod]);
+    const uint32_t n16 = s_len[pod - lv.first_pod] / 16u;
     uint4* dst = reinterpret_cast<uint4*>(s_blob[slot]);
-#pragma unroll
-    for (int r = 0; r < kPre; ++r) {
-      const uint32_t o = (uint32_t)lane + (uint32_t)r * 64u;
-      if (o < pre_bytes / 16u) dst[o] = pre[r];
-    }
-    for (uint32_t o = (uint32_t)lane + kPre * 64u; o < pre_bytes / 16u; o += 64u)
-      dst[o] = reinterpret_cast<const uint4*>(pre_src)[o];
+    for (uint32_t o = (uint32_t)lane; o < n16; o += 64u) dst[o] = src[o];
   };
 
   // ---- evaluation-wave state of the pod being prepared: per-thread maxima of the normalising raw
@@ -1620,12 +1609,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   }
   __syncthreads();
   if (hlp && lv.npods > 0) {
-    fetch(lv.first_pod);
-    land(0);
-    if (lv.npods > 1) {
-      fetch(lv.first_pod + 1);
-      land(1);
-    }
+    stage_prog(lv.first_pod, 0);
+    if (lv.npods > 1) stage_prog(lv.first_pod + 1, 1);
   }
   __syncthreads();
   if (t < kBlock && lv.npods > 0) phase1(lv.first_pod, 0, 0, nullptr);
@@ -1739,7 +1724,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       // wave publishes the right pair as soon as exchange B resolves.
       const bool stage = q + 2 < lv.npods;
       if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
-      if (stage) fetch(pod + 2);
+      if (stage) stage_prog(pod + 2, bs);  // s_blob[(q + 2) % 3] held pod q-1, free since the last barrier
       while (__hip_atomic_load(&s_cand_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)  // posted every pod
         __builtin_amdgcn_s_sleep(1);
       const int cand = __hip_atomic_load(&s_cand_node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1812,7 +1797,6 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
         s_cand_ok = cand_ok;
         __hip_atomic_store(&s_ga_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (stage) land(bs);
     } else if (more) {
       // ======== evaluation waves: phase 1 of pod q+1 against the cores before this pod's assume.
       // Only the chosen node changes; its owner redoes it below.
@@ -1977,6 +1961,22 @@ hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const Loop
   else
     hipLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
   return hipGetLastError();
+}
+// Loads the module's code object onto the current device now (hipFuncGetAttributes), so that no
+// first launch inside a batch does it while an in-process peer's persistent loop is running.
+hipError_t warm_kernels() {
+  hipFuncAttributes a;
+  const void* fs[] = {reinterpret_cast<const void*>(&k_filter_score<true>), reinterpret_cast<const void*>(&k_filter_score<false>),
+                      reinterpret_cast<const void*>(&k_select<true>),       reinterpret_cast<const void*>(&k_select<false>),
+                      reinterpret_cast<const void*>(&k_xpack_a),            reinterpret_cast<const void*>(&k_unpack_pts),
+                      reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
+                      reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
+                      reinterpret_cast<const void*>(&k_sched_loop)};
+  for (const void* f : fs) {
+    const hipError_t e = hipFuncGetAttributes(&a, f);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 #ifdef KSG_DIAG
 hipError_t set_diag(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &p, sizeof(p)); }

@@ -67,6 +67,11 @@ ksg_ctx* ksg_create(const char* config_json, size_t len) {
       return nullptr;
     }
     ctx->engine.reset(new Engine(ctx->cluster.get()));
+    if (!ctx->cluster->err.empty()) {  // the kernels' code object did not load
+      g_create_error = ctx->cluster->err;
+      delete ctx;
+      return nullptr;
+    }
     if (cfg.sharded()) {  // node-sharded: join the exchange group (collective across the ranks)
       std::string err;
       ctx->engine->comm = make_comm(cfg, &err);

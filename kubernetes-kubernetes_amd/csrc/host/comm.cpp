@@ -213,6 +213,15 @@ class LocalComm : public Comm {
     return KSG_OK;
   }
 
+  int launch_gate() override {
+    int sl = 0;
+    if (!rendezvous(nullptr, nullptr, 0, &sl)) {
+      err = "local exchange: launch rendezvous timed out";
+      return KSG_EDEVICE;
+    }
+    return KSG_OK;
+  }
+
   int batch_end() override {  // every rank's stream has drained: buffers may be reused/regrown
     int sl = 0;
     if (!rendezvous(nullptr, nullptr, 0, &sl)) {

@@ -34,6 +34,10 @@ class Comm {
   virtual int group_end() { return 0; }
   // end of a batch: every rank's stream has drained (already synchronised by the caller)
   virtual int batch_end() { return 0; }
+  // before a batch's first persistent-loop launch: in-process ranks share one device, and a rank
+  // still in a synchronising HIP call (allocation, first use) must not hold its loop back while
+  // a peer's loop is already spinning on it
+  virtual int launch_gate() { return 0; }
   // collective: every rank passes its device buffer; all[r] becomes rank r's buffer as mapped in
   // this process (in-process: the pointer itself; RCCL ranks: an IPC mapping of the peer's memory)
   virtual int share_buffers(void* mine, std::vector<void*>* all) = 0;

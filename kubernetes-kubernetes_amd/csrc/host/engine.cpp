@@ -39,6 +39,8 @@ hipError_t set_diag(unsigned long long* p);
 #endif
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
                              hipEvent_t t0, hipEvent_t t1);
+hipError_t warm_kernels();
+hipError_t warm_aggregate();
 
 #define HIPCHK(x)                                               \
   do {                                                          \
@@ -805,6 +807,9 @@ Engine::Engine(Cluster* cl) : c(cl) {
   (void)hipEventCreate(&ev1);
   if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, c->cfg.device) != hipSuccess)
     cu_count = 0;
+  // every kernel's code object loaded before the first batch (see warm_kernels)
+  if (c->err.empty() && (warm_kernels() != hipSuccess || warm_aggregate() != hipSuccess))
+    c->err = "cannot load the kernels' code object on HIP device " + std::to_string(c->cfg.device);
 }
 
 // A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
@@ -1168,6 +1173,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       lv.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr;
       lv.desc_bytes = (const uint32_t*)d_off.p + n;
       lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr;
+      // in-process ranks: every rank is past its allocations before any rank's first loop starts
+      if (runs.empty() && comm && comm->launch_gate()) {
+        c->err = comm->err;
+        return KSG_EDEVICE;
+      }
       HIPCHK(launch_sched_loop(m, bv, lv, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
       runs.push_back({i, j - i, rb});
       launches += j - i;

@@ -55,3 +55,30 @@ def test_config_errors_are_reported_before_device_probe():
     _ensure_built()
     with pytest.raises(KsgError):
         native.Scheduler({"nodeResourcesFit": {"scoringStrategy": {"type": "Bogus"}}})
+
+
+def _kernel_notes(tmp_path):
+    """The gfx950 code object's AMDHSA metadata, as llvm-readelf prints it."""
+    bin_dir = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(bin_dir, "llvm-readelf")):
+        pytest.skip("ROCm LLVM tools not present")
+    so = tmp_path / "lib.so"
+    so.write_bytes(open(_ensure_built(), "rb").read())
+    subprocess.check_call([os.path.join(bin_dir, "llvm-objdump"), "--offloading", str(so)],
+                          stdout=subprocess.DEVNULL, cwd=tmp_path)
+    cos = sorted(p for p in tmp_path.iterdir() if p.name.endswith("gfx950"))
+    assert cos, "no gfx950 code object in the library"
+    return "".join(subprocess.check_output([os.path.join(bin_dir, "llvm-readelf"), "--notes", str(p)], text=True)
+                   for p in cos)
+
+
+def test_no_kernel_uses_scratch(tmp_path):
+    """Every kernel runs without private (scratch) memory: a dispatch that needs scratch waits for the
+    runtime's scratch grant before its waves start, and the persistent loop's ranks must start together."""
+    notes = _kernel_notes(tmp_path)
+    kernels = re.findall(r"\.name:\s+(_Z\S+)", notes)
+    sizes = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+    assert kernels and len(kernels) == len(sizes)
+    assert any("k_sched_loop" in k for k in kernels)
+    used = {k: s for k, s in zip(kernels, sizes) if s}
+    assert not used, used
