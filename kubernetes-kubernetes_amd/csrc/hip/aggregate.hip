@@ -55,9 +55,8 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
       const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
       const uint32_t el = pts_eligible(m, base, d, cs, d.n_ptsf, i);
       for (int32_t c = 0; c < d.n_ptsf; ++c) {
-        if (!((el >> c) & 1u)) continue;
-        unsigned long long* pp = b.arena + cs[c].pres_base + node_label(m, cs[c].slot, i);
-        if (*pp == 0ull && atomicExch(pp, 1ull) == 0ull) atomicAdd(&ps->pts_ndom[c], 1u);
+        const bool on = ((el >> c) & 1u) != 0;
+        mark_domains(b.arena + cs[c].pres_base, on ? node_label(m, cs[c].slot, i) : 0, on, &ps->pts_ndom[c]);
       }
     }
   } else if (blk < nb_node + nb_pod) {

@@ -29,6 +29,29 @@ enum : int { P_UNSCHED = 0, P_NODENAME = 1, P_TAINT = 2, P_NA = 3, P_PORTS = 4, 
              P_IPA = 7, P_BAL = 8, P_IMG = 9 };
 enum : uint32_t { C_OK = 0, C_ERROR = 1, C_UNSCHED = 2, C_UU = 3 };
 
+// Domain presence: set flags[v] (0 -> 1) for every active lane with `want`, and add to *counter the
+// number of flags this call set first.  A few domains shared by many nodes (zones) would make every
+// lane exchange the same words: the first four distinct values of a wave are issued by one leader
+// lane each, the rest (hostname-like keys, all distinct) one exchange per lane.  One counter atomic
+// per wave.  Called by whole waves (inactive lanes simply do not take part).
+__device__ __forceinline__ void mark_domains(unsigned long long* flags, int v, bool want, uint32_t* counter) {
+  const int lane = threadIdx.x & 63;
+  const bool cand = want && flags[v] == 0ull;
+  unsigned long long todo = __ballot(cand);
+  bool lead = false;
+  for (int it = 0; it < 4 && todo; ++it) {
+    const int l = __builtin_ctzll(todo);
+    const int lv = __shfl(v, l, 64);
+    const unsigned long long same = __ballot(cand && v == lv);
+    lead |= lane == l;
+    todo &= ~same;
+  }
+  lead |= ((todo >> lane) & 1ull) != 0;
+  const bool won = lead && atomicExch(flags + v, 1ull) == 0ull;
+  const unsigned long long wb = __ballot(won);
+  if (wb && lane == __builtin_ctzll(wb)) atomicAdd(counter, (uint32_t)__popcll(wb));
+}
+
 // Go int64 `a / b` (truncating) without the ~60-instruction 64-bit division expansion on the
 // common path: operands that fit 32 bits use the 32-bit unit; non-negative operands below 2^52
 // divide in FP64 (exact inputs, correctly rounded quotient) and the truncated quotient is fixed

@@ -468,8 +468,7 @@ __device__ __forceinline__ NodeEval eval_node(const MirrorView& m, const BatchVi
       PodStats* ps = b.stats + pod;
       for (int32_t c = 0; c < d.n_ptss; ++c) {
         if (cs[c].hostname) continue;
-        unsigned long long* pp = b.arena + cs[c].pres_base + node_label(m, cs[c].slot, i);
-        if (*pp == 0ull && atomicExch(pp, 1ull) == 0ull) atomicAdd(&ps->pts_distinct[c], 1u);
+        mark_domains(b.arena + cs[c].pres_base, node_label(m, cs[c].slot, i), true, &ps->pts_distinct[c]);
       }
     }
   }
