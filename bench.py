@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--node-scaling", default=None, choices=["weak", "strong"],
                     help="sharded mode: grow the cluster with N (weak) or keep it fixed (strong)")
     ap.add_argument("--batch", type=int, default=1000)
+    ap.add_argument("--pct", type=int, default=100,
+                    help="percentageOfNodesToScore (100: the parity contract; 0: upstream's adaptive default)")
     ap.add_argument("--timing-stride", type=int, default=8, help="time every k-th filter kernel with HIP events")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -81,14 +83,17 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(nodes, init, pods, budget_s, threads=1):
+def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100):
     """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
     Filter / Score loops over nodes on a pool of that many threads (the reference's
     Parallelizer.Until with parallelism 16), results identical to the sequential oracle
     (tests/test_oracle_parallel.py)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_binding import oracle
-    o = oracle({"cpuThreads": threads} if threads > 1 else {})
+    cfg = {"cpuThreads": threads} if threads > 1 else {}
+    if pct != 100:  # the cut filter pass runs sequentially in the oracle (its Score loop stays parallel)
+        cfg["percentageOfNodesToScore"] = pct
+    o = oracle(cfg)
     for n in nodes:
         o.add_node(n)
     for p in init:
@@ -127,6 +132,8 @@ def main():
 
     c5 = a.workload == "c5"
     sharded = (world > 1 and a.mode == "sharded") or a.shard_single
+    if sharded and a.pct != 100:
+        sys.exit("--pct != 100 runs unsharded only (use --mode replicas for N > 1)")
     scaling = a.node_scaling or ("strong" if c5 else "weak")
     grow = world if (sharded and scaling == "weak") else 1
     n_nodes = (a.nodes or (100000 if c5 else 5000)) * grow
@@ -149,7 +156,7 @@ def main():
     def build(dev_exchange):
         """Scheduler with the cluster loaded, warm-up batches run (then forgotten, so the timed run
         starts from the config state); None if the warm-up failed on this rank."""
-        cfg = {"device": local, "kernelTimingStride": a.timing_stride}
+        cfg = {"device": local, "kernelTimingStride": a.timing_stride, "percentageOfNodesToScore": a.pct}
         if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
             obj = [comm_unique_id() if rank == 0 else None]
             if dist is not None:
@@ -236,13 +243,15 @@ def main():
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             # the reference's default parallelism (16 goroutines over nodes), then one thread
-            v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads)
-            v1, done1, cdt1 = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1)
+            v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads, pct=a.pct)
+            v1, done1, cdt1 = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct)
             cpu = {"value": round(v, 2), "unit": "pods/s", "cores": a.cpu_threads, "kind": "port",
                    "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
                              f"{cdt:.1f} s, oracle/ C++ restatement, Filter/Score over nodes on "
-                             f"{a.cpu_threads} threads ({cpu_model()}, {os.cpu_count()} logical CPUs visible)",
+                             f"{a.cpu_threads} threads ({cpu_model()}, {os.cpu_count()} logical CPUs visible)"
+                             + ("; percentageOfNodesToScore < 100: the cut Filter pass is sequential, Score "
+                                "on the pool" if a.pct != 100 else ""),
                    "single_thread": {"value": round(v1, 2), "cores": 1,
                                      "sample": f"first {done1} pods, {cdt1:.1f} s, 1 thread"}}
         out = {
@@ -263,7 +272,7 @@ def main():
                                    f"{n_meas} measured pods" + ("" if sharded else " per GPU")
                                    + (" (BASELINE configs[1])" if a.workload == "c2" and world == 1 else "")
                                    + (" (BASELINE configs[4])" if c5 else ""),
-                       "nodes": n_nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": 100,
+                       "nodes": n_nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": a.pct,
                        "plugins": "default",
                        "parallelism": (f"nodes-sharded{world}" if sharded
                                        else f"replicas{world}" if world > 1 else "single"),

@@ -146,6 +146,8 @@ enum DescFlags : uint32_t {
   DF_NODE_LIST = 1u << 13,         // plugin-eval mode: only the nodes in the bitmap at node_list_off are listed
   DF_AGGREGATE = 1u << 14,         // PTS/IPA counts: k_aggregate runs before the node pass
   DF_FAST = 1u << 15,              // default-plugin shape: straight-line cpu/mem Fit + BalancedAllocation (eval_node_fast)
+  DF_ROTDEV = 1u << 16,            // nextStartNodeIndex is device-resident: k_sample_find derives this pod's rotation
+  DF_SAMPLE = 1u << 17,            // numFeasibleNodesToFind < nodes: the feasible list is cut (k_sample_apply)
 };
 
 struct PodDesc {
@@ -200,6 +202,9 @@ struct PodDesc {
   int32_t n_exkeys, exkeys_off;      // KeyHist: existing anti-affinity counts (Filter)
   int32_t n_topokeys, topokeys_off;  // KeyHist: topology scores (Score)
   int32_t arena_words;               // arena entries this pod uses (zeroed again by k_select)
+  // ---- percentageOfNodesToScore (schedule_one.go:778-782,858-884), DF_ROTDEV / DF_SAMPLE
+  int32_t num_to_find;               // numFeasibleNodesToFind (or 1 without score plugins)
+  int32_t prev_pod;                  // previous launched pod of the batch (its rot_out), -1: PodStats::rot_in
   int32_t pad2;
 };
 
@@ -212,7 +217,8 @@ struct DevResult {
   int64_t total;
   uint64_t key;       // winning packed key (debug)
   uint32_t ipa_any;   // PodStats::ipa_any (PreFilter / PreScore Skip decisions taken on the device)
-  uint32_t pad[3];
+  uint32_t rot_next;  // DF_ROTDEV: nextStartNodeIndex after this pod
+  uint32_t pad[2];
 };
 
 // Per-pod scratch (zeroed by the host before each batch).
@@ -228,6 +234,12 @@ struct PodStats {
   uint32_t pts_ndom[kMaxCons];        // domains per DoNotSchedule constraint
   uint32_t pts_distinct[kMaxCons];    // feasible, non-ignored domains per ScheduleAnyway constraint
   uint32_t pts_nonignored;            // feasible nodes carrying every ScheduleAnyway key
+  // device-resident nextStartNodeIndex (DF_ROTDEV, k_sample_find)
+  uint32_t rot_in;                    // first launched pod of the batch: the host's nextStartNodeIndex
+  uint32_t rot;                       // this pod's rotation start (snapshot index)
+  uint32_t rot_out;                   // nextStartNodeIndex after this pod (schedule_one.go:686-687)
+  uint32_t processed;                 // nodes processed by findNodesThatPassFilters
+  int32_t samp_end;                   // snapshot index of the (K+1)-th feasible node in rotated order, -1: none
   uint32_t pad[3];
 };
 

@@ -466,7 +466,8 @@ __device__ __forceinline__ NodeEval eval_node(const MirrorView& m, const BatchVi
     if (!ignored) {
       r.pts = true;
       PodStats* ps = b.stats + pod;
-      for (int32_t c = 0; c < d.n_ptss; ++c) {
+      // a cut feasible list (DF_SAMPLE): k_sample_apply marks the kept nodes' domains instead
+      for (int32_t c = 0; c < ((d.flags & DF_SAMPLE) ? 0 : d.n_ptss); ++c) {
         if (cs[c].hostname) continue;
         mark_domains(b.arena + cs[c].pres_base, node_label(m, cs[c].slot, i), true, &ps->pts_distinct[c]);
       }
@@ -725,7 +726,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView
       in = s_min[w] < in ? s_min[w] : in;
     }
     b.blk_cnt[blk] = c;
-    if (c) {
+    if (c && !(d.flags & DF_SAMPLE)) {  // a cut feasible list: k_sample_apply reduces the kept nodes
       PodStats* ps = b.stats + pod;
       if ((sm >> P_TAINT) & 1u) atomicMax(&ps->max_raw[P_TAINT], a);
       if ((sm >> P_NA) & 1u) atomicMax(&ps->max_raw[P_NA], bb);
@@ -949,6 +950,10 @@ __device__ __forceinline__ bool commit_result(const MirrorView& m, const BatchVi
   r.key = best;
   r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
   r.ipa_any = ipa_any >= 0 ? (uint32_t)ipa_any : ps->ipa_any;
+  if (d.flags & DF_ROTDEV) {  // k_sample_find's rotation bookkeeping
+    r.evaluated = (int32_t)ps->processed;
+    r.rot_next = ps->rot_out;
+  }
   if (d.flags & DF_PREFILTER_REJECT) r.status = (int32_t)C_UNSCHED;
   if ((d.flags & DF_SCORE_ERROR) && F > 1) {  // prioritizeNodes error (schedule_one.go:600-603)
     r.status = (int32_t)C_ERROR;
@@ -1014,7 +1019,7 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
 
   // ---- global feasible count F, this block's exclusive prefix, and P(s) = feasible nodes
   // before the rotation start (nextStartNodeIndex, schedule_one.go:808) -- one strided pass
-  const int s = d.rot_start;
+  const int s = (d.flags & DF_ROTDEV) ? (int)ps->rot : d.rot_start;
   const int sb = s / kBlock;
   __shared__ uint32_t s_red[kBlock / 64][3];
   uint32_t pre = 0, tot = 0, pres = 0;
@@ -1066,6 +1071,154 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
   int node = -1;
   if (F > 0) node = find_rank_node(b, 0, nblocks, winner_rank(best, ps_before, F));
   if (threadIdx.x == 0) commit_result(m, b, base, d, ps, pod, F, node, best);
+}
+
+// ---- percentageOfNodesToScore: the cut feasible list (schedule_one.go:778-884) ---------------------
+// findNodesThatPassFilters checks nodes[(nextStartNodeIndex + i) % numAll] in order and stops at
+// the (K+1)-th feasible node, K = numFeasibleNodesToFind (schedule_one.go:809-824, sequential
+// Parallelizer semantics): the feasible list is the first K feasible nodes of the rotated order,
+// processedNodes = K + the failures before that (K+1)-th node = its rotated position, and
+// nextStartNodeIndex advances by it (:686-687).  Every node is still evaluated on the device (one
+// pass is cheaper than a serial walk); the cut is the cyclic snapshot-index range [rot, samp_end).
+__device__ __forceinline__ bool in_cyclic(int i, int lo, int hi) {  // lo != hi
+  return lo < hi ? (i >= lo && i < hi) : (i >= lo || i < hi);
+}
+
+// k_sample_find (1 block): this pod's rotation start from the device-resident nextStartNodeIndex,
+// the (K+1)-th feasible node of the rotated order, processedNodes and the next rotation.
+__global__ __launch_bounds__(kBlock) void k_sample_find(MirrorView m, BatchView b, int pod, int nblocks) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  const int N = m.n;
+  const uint32_t rot_in = d.prev_pod < 0 ? ps->rot_in : b.stats[d.prev_pod].rot_out;
+  if (d.flags & DF_PREFILTER_REJECT) {  // the cycle ends before findNodesThatPassFilters (:635-648)
+    if (threadIdx.x == 0) {
+      ps->rot = 0;
+      ps->rot_out = rot_in;
+      ps->processed = 0;
+      ps->samp_end = -1;
+    }
+    return;
+  }
+  const bool sub = (d.flags & DF_SUBSET) != 0;
+  const int32_t* subset = at<int32_t>(base, d.subset_off);
+  const int cnt = sub ? d.subset_cnt : N;  // numAllNodes = len(nodes)
+  // nodes[(nextStartNodeIndex + i) % numAll]: the PreFilterResult list is in snapshot order
+  const int s = cnt == 0 ? 0 : (sub ? subset[rot_in % (uint32_t)cnt] : (int)rot_in);
+  __shared__ uint32_t s_tot[kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t tot = 0;
+  for (int k = threadIdx.x; k < nblocks; k += kBlock) tot += b.blk_cnt[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  if (lane == 0) s_tot[wave] = tot;
+  __syncthreads();
+  uint32_t F = 0;
+  for (int w = 0; w < kBlock / 64; ++w) F += s_tot[w];
+  const uint32_t K = (uint32_t)d.num_to_find;
+  int end = -1;
+  uint32_t processed = (uint32_t)cnt;
+  if (F > K) {
+    const uint32_t below = s > 0 ? count_below(b, 0, nblocks, s) : 0u;  // feasible nodes before s
+    end = find_rank_node(b, 0, nblocks, (below + K) % F);               // rotated rank K
+    if (sub) {  // rotated position inside the PreFilterResult list
+      __shared__ int s_pos[2];
+      for (int q = threadIdx.x; q < cnt; q += kBlock) {
+        if (subset[q] == s) s_pos[0] = q;
+        if (subset[q] == end) s_pos[1] = q;
+      }
+      __syncthreads();
+      processed = (uint32_t)((s_pos[1] - s_pos[0] + cnt) % cnt);
+    } else {
+      processed = (uint32_t)((end - s + N) % N);
+    }
+  }
+  if (threadIdx.x == 0) {
+    ps->rot = (uint32_t)s;
+    ps->samp_end = end;
+    ps->processed = processed;
+    ps->rot_out = N > 0 ? (uint32_t)(((uint64_t)rot_in + processed) % (uint64_t)N) : 0u;
+  }
+}
+
+// k_sample_apply (node blocks): keep the feasible nodes in [rot, samp_end), rewrite this block's
+// mask words and count, and do the feasible-list reductions k_filter_score skipped for a cut list:
+// the normalising plugins' raw-score max/min, PodTopologySpread PreScore's ignored-node count and
+// domain presence (podtopologyspread/scoring.go:61-115).  Evaluation output: nodes past the cut
+// were never processed, so they carry no status (result[i] == nil, schedule_one.go:845-850).
+__global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView b, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  const int blk = (int)blockIdx.x;
+  const int i = blk * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cap = (size_t)m.cap;
+  const int end = ps->samp_end, s = (int)ps->rot;
+  const bool inproc = i < m.n && (end < 0 || in_cyclic(i, s, end));
+  const unsigned long long word = b.fmask[(size_t)blk * (kBlock / 64) + wave];
+  const bool kept = inproc && ((word >> lane) & 1ull);
+  if ((d.flags & DF_EVAL_OUT) && i < m.n && !inproc) b.status[i] = 0u;
+  const unsigned long long ballot = __ballot(kept);
+  if (lane == 0) b.fmask[(size_t)blk * (kBlock / 64) + wave] = ballot;
+  const uint32_t sm = d.score_mask;
+  unsigned long long mt = 0, mn = 0, mi = 0, ni = ~0ull;
+  if (kept) {
+    if ((sm >> P_TAINT) & 1u) mt = enc_i64(b.raw[P_TAINT * cap + i]);
+    if ((sm >> P_NA) & 1u) mn = enc_i64(b.raw[P_NA * cap + i]);
+    if ((sm >> P_IPA) & 1u) mi = ni = enc_i64(b.raw[P_IPA * cap + i]);
+  }
+  bool pts = false;
+  if ((sm >> P_PTS) & 1u) {
+    const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+    bool ignored = false;
+    if (kept)
+      for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
+    pts = kept && !ignored;
+    for (int32_t c = 0; c < d.n_ptss; ++c) {
+      if (cs[c].hostname) continue;
+      mark_domains(b.arena + cs[c].pres_base, pts ? node_label(m, cs[c].slot, i) : 0, pts, &ps->pts_distinct[c]);
+    }
+  }
+  mt = wave_max_u64(mt);
+  mn = wave_max_u64(mn);
+  mi = wave_max_u64(mi);
+  ni = wave_min_u64(ni);
+  const unsigned long long pball = __ballot(pts);
+  __shared__ uint32_t s_cnt[kBlock / 64], s_pts[kBlock / 64];
+  __shared__ unsigned long long s_max[3][kBlock / 64], s_min[kBlock / 64];
+  if (lane == 0) {
+    s_cnt[wave] = (uint32_t)__popcll(ballot);
+    s_pts[wave] = (uint32_t)__popcll(pball);
+    s_max[0][wave] = mt;
+    s_max[1][wave] = mn;
+    s_max[2][wave] = mi;
+    s_min[wave] = ni;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0, pc = 0;
+    unsigned long long a = 0, bb = 0, ia = 0, in = ~0ull;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      c += s_cnt[w];
+      pc += s_pts[w];
+      a = s_max[0][w] > a ? s_max[0][w] : a;
+      bb = s_max[1][w] > bb ? s_max[1][w] : bb;
+      ia = s_max[2][w] > ia ? s_max[2][w] : ia;
+      in = s_min[w] < in ? s_min[w] : in;
+    }
+    b.blk_cnt[blk] = c;
+    if (c) {
+      if ((sm >> P_TAINT) & 1u) atomicMax(&ps->max_raw[P_TAINT], a);
+      if ((sm >> P_NA) & 1u) atomicMax(&ps->max_raw[P_NA], bb);
+      if ((sm >> P_IPA) & 1u) {
+        atomicMax(&ps->max_raw[P_IPA], ia);
+        atomicMin(&ps->min_raw[P_IPA], in);
+      }
+      if (pc) atomicAdd(&ps->pts_nonignored, pc);
+    }
+  }
 }
 
 // ---- node-sharded path ----------------------------------------------------------------
@@ -1926,6 +2079,12 @@ hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipSt
     hipLaunchKernelGGL(k_select<false>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
   return hipGetLastError();
 }
+hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s) {
+  const int nb = (m.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_sample_find, dim3(1), dim3(kBlock), 0, s, m, b, pod, nb);
+  if (cut && nb > 0) hipLaunchKernelGGL(k_sample_apply, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
+  return hipGetLastError();
+}
 hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
   hipLaunchKernelGGL(k_xpack_a, dim3(1), dim3(kBlock), 0, s, b, sv, pod);
   return hipGetLastError();
@@ -1970,7 +2129,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_a),            reinterpret_cast<const void*>(&k_unpack_pts),
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
-                      reinterpret_cast<const void*>(&k_sched_loop)};
+                      reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
+                      reinterpret_cast<const void*>(&k_sample_apply)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
     if (e != hipSuccess) return e;

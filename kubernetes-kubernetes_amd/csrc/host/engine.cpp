@@ -26,6 +26,7 @@ namespace ksg {
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
                                hipEvent_t t1, int blk0, int nblk, bool lds);
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, bool lds);
+hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s);
 hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, const PodDesc& d, hipStream_t s);
 hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0 = 0,
                             int nblk = -1);
@@ -181,7 +182,9 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   if (noNA && !cfg.has_added_required && !p.has_node_selector) fmask &= ~(1u << P_NA);
   std::vector<int32_t> subset;
   bool restricted = false, conflict = false;
-  if (!noNA && !p.required_na.empty()) {
+  // (only when the profile runs NodeAffinity: a disabled plugin's PreFilter neither restricts
+  // the node list nor rejects, RunPreFilterPlugins framework.go:934-990)
+  if (cfg.enabled[P_NA] && !noNA && !p.required_na.empty()) {
     std::set<std::string> names;
     bool namesNil = true, allNodes = false;
     for (auto& t : p.required_na) {
@@ -467,13 +470,15 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
       if (!cfg.enabled[q]) { fmask &= ~(1u << q); smask &= ~(1u << q); }
     bool any_score = false;
     for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) any_score |= cfg.enabled[q];
-    if (!any_score) {
-      c->err = "a profile without score plugins (numNodesToFind = 1) is not supported";
-      return KSG_ENOTSUP;
-    }
-    if (N >= 100 && cfg.pct != 100) {
-      c->err = "percentageOfNodesToScore != 100 (sampling) is not supported on the device path";
-      return KSG_ENOTSUP;
+    // percentageOfNodesToScore / a profile without score plugins: nextStartNodeIndex then depends
+    // on where the filter pass stopped, so it lives on the device (DF_ROTDEV, k_sample_find)
+    if (!any_score) D.flags |= DF_NO_SCORE;
+    if (rotdev()) {
+      if (comm) {
+        c->err = "percentageOfNodesToScore != 100 (or no score plugins) is not supported on a node-sharded context";
+        return KSG_ENOTSUP;
+      }
+      D.flags |= DF_ROTDEV;
     }
     if (score_err) D.flags |= DF_SCORE_ERROR;
     if (conflict || (!out->prefilter_error && out->ipa_parse_error)) {
@@ -498,6 +503,17 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     } else {
       D.rot_start = N ? (int32_t)(c->next_start % N) : 0;
     }
+    // numFeasibleNodesToFind (schedule_one.go:778-782,858-884) over len(nodes)
+    const int32_t num_all = out->num_all;
+    int64_t k = num_all;
+    if (num_all >= 100) {
+      int64_t pct = cfg.pct;
+      if (pct == 0) pct = std::max<int64_t>(5, 50 - num_all / 125);
+      k = std::max<int64_t>(100, (int64_t)num_all * pct / 100);
+    }
+    if (!any_score) k = 1;
+    D.num_to_find = (int32_t)std::min<int64_t>(k, INT32_MAX);
+    if ((D.flags & DF_ROTDEV) && k < num_all && !(D.flags & DF_PREFILTER_REJECT)) D.flags |= DF_SAMPLE;
   } else if (mode == FILTER_ONE) {
     fmask &= 1u << plugin;
     if ((plugin == P_PTS && out->prefilter_error) || (plugin == P_IPA && out->ipa_parse_error)) {
@@ -546,7 +562,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     // no existing anti-affinity) leave their mask bits set but never reject: not a reason to leave
     const bool topo_filter = D.n_ptsf > 0 || D.n_raff > 0 || D.n_ranti > 0 || (D.ipa_flags & IPA_EXIST_FILTER);
     if (mode == CYCLE && shape && D.n_scalar == 0 && !topo_filter && !(smask & topo) &&
-        !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR)) &&
+        !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR | DF_ROTDEV)) &&
         c->alloc_bound < ((int64_t)1 << 52) / 100)
       D.flags |= DF_FAST;
   }
@@ -814,10 +830,16 @@ Engine::Engine(Cluster* cl) : c(cl) {
 
 // A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
 // PodTopologySpread / InterPodAffinity scores, no per-node evaluation output).
+bool Engine::rotdev() const {
+  bool any_score = false;
+  for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) any_score |= c->cfg.enabled[q];
+  return c->cfg.pct != 100 || !any_score;
+}
+
 bool Engine::loop_ok(const CompiledPod& p) const {
   if (p.error) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
-  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE)) return false;
+  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV)) return false;
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
   if (p.blob.size() > (size_t)kBlobLds) return false;
   // the exchange granules carry raw TaintToleration counts and raw NodeAffinity sums (+1) in 24
@@ -1019,7 +1041,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       return rc;
     }
     if (cp[i].prefilter_error) cp[i].error = true;  // PreFilter Error: status Error, no launch
-    if (!cp[i].prefilter_reject && !cp[i].prefilter_error) {
+    if (!cp[i].prefilter_reject && !cp[i].prefilter_error && !rotdev()) {
       // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
       const int64_t N = (int64_t)c->order().size();
       c->next_start = (c->next_start + cp[i].num_all) % N;
@@ -1057,6 +1079,18 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       hs[i].min_raw[q] = enc_i64(INT64_MAX);
     }
   }
+  // device-resident nextStartNodeIndex: each launched pod's k_sample_find reads the previous
+  // launched pod's rotation; the first reads the host's value
+  const bool rot_dev = rotdev();
+  int last_launched = -1;
+  if (rot_dev)
+    for (int i = 0; i < n; ++i) {
+      if (cp[i].error) continue;
+      PodDesc* pd = reinterpret_cast<PodDesc*>(hp + offs[i]);
+      pd->prev_pod = last_launched;
+      if (last_launched < 0) hs[i].rot_in = (uint32_t)c->next_start;
+      last_launched = i;
+    }
   hipStream_t s = c->stream;
   const MirrorView& m = c->view;
   HIPCHK(hipMemcpyAsync(d_descs.p, hp, o, hipMemcpyHostToDevice, s));
@@ -1199,6 +1233,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     } else {
       HIPCHK(launch_filter_score(m, bv, i, s, nullptr, nullptr, 0, -1, lds));
     }
+    if (hd.flags & DF_ROTDEV) HIPCHK(launch_sample(m, bv, i, (hd.flags & DF_SAMPLE) != 0, s));
     if (hd.score_mask & (1u << P_PTS)) HIPCHK(launch_pts_score(m, bv, i, s));
     HIPCHK(launch_select(m, bv, i, s, lds));
     bytes += algo_bytes(hd);
@@ -1234,6 +1269,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       r.node_index = d.node;
       r.feasible_nodes = d.feasible;
       r.evaluated_nodes = d.feasible > 0 ? cp[i].num_all : (cp[i].prefilter_reject ? 0 : cp[i].num_all);
+      if (rot_dev) {
+        if (!cp[i].prefilter_reject) r.evaluated_nodes = d.evaluated;
+        if (i == last_launched) c->next_start = d.rot_next;
+      }
       r.total_score = d.feasible > 1 ? d.total : 0;
       if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
       if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {

@@ -370,6 +370,9 @@ class Engine {
   bool loop_ok(const CompiledPod& p) const;
   // node-sharded evaluation (cfg.world > 1): this rank's block range + the exchange transport
   std::unique_ptr<Comm> comm;
+  // nextStartNodeIndex advances by a data-dependent count (percentageOfNodesToScore < 100, or
+  // numNodesToFind = 1 without score plugins): it is kept on the device across a batch
+  bool rotdev() const;
   int32_t shard_blk0 = 0, shard_nblk = -1;
   void shard_range(int32_t n, int32_t* blk0, int32_t* nblk) const;
 

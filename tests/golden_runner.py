@@ -18,11 +18,22 @@ def load_cases():
     return out
 
 
+def case_nodes(case):
+    """The case's nodes; `nodes_gen` expands {"count": n, "template": node} with "{i}" in the
+    template's name replaced by 0..n-1 (large all-identical clusters stay small on disk)."""
+    nodes = list(case["nodes"])
+    g = case.get("nodes_gen")
+    if g:
+        t = json.dumps(g["template"])
+        nodes += [json.loads(t.replace("{i}", str(i))) for i in range(g["count"])]
+    return nodes
+
+
 def build(make_backend, case):
     b = make_backend(case.get("config") or {})
     for ns in case.get("namespaces", []):
         b.upsert_namespace(ns)
-    for n in case["nodes"]:
+    for n in case_nodes(case):
         b.add_node(n)
     for p in case.get("existing", []):
         b.add_pod(p)
@@ -39,8 +50,12 @@ def run_case(make_backend, case):
         return ["config accepted but the reference rejects it"]
     b = build(make_backend, case)
     names = b.node_names()
+    if case["kind"] == "sequence":
+        errs = run_sequence_case(b, case, names)
+        b.close()
+        return errs
     h = b.compile(case["pod"])
-    want_names = [n["metadata"]["name"] for n in case["nodes"]]
+    want_names = [n["metadata"]["name"] for n in case_nodes(case)]
     errs = []
     e = case["expect"]
     if case["kind"] == "score":
@@ -95,4 +110,20 @@ def run_cycle_case(b, case, names):
         errs.append(f"feasible {r.feasible_nodes} != {e['feasible']}")
     if "evaluated" in e and r.evaluated_nodes != e["evaluated"]:
         errs.append(f"evaluated {r.evaluated_nodes} != {e['evaluated']}")
+    return errs
+
+
+def run_sequence_case(b, case, names):
+    """Scheduling cycles of the same pod without assume (findNodesThatFitPod called repeatedly,
+    schedule_one_test.go:4472-4485); step i's expectations hold after cycle i."""
+    errs = []
+    for i, e in enumerate(case["expect"]["steps"]):
+        r, _ = b.schedule_one(b.compile(case["pod"]), assume=False)
+        got = names[r.node_index] if r.node_index >= 0 else None
+        if "node" in e and got != e["node"]:
+            errs.append(f"step {i}: node {got} != {e['node']}")
+        if "feasible" in e and r.feasible_nodes != e["feasible"]:
+            errs.append(f"step {i}: feasible {r.feasible_nodes} != {e['feasible']}")
+        if "evaluated" in e and r.evaluated_nodes != e["evaluated"]:
+            errs.append(f"step {i}: evaluated {r.evaluated_nodes} != {e['evaluated']}")
     return errs

@@ -205,3 +205,52 @@ def test_persistent_loop_mixed_runs(native, seed):
     for k, p in enumerate(pods):
         ro, _ = o.schedule_one(o.compile(p), assume=True)
         assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"
+
+
+# ---- percentageOfNodesToScore: the cut feasible list and the device-resident nextStartNodeIndex
+# (schedule_one.go:778-884, 686-687).  Random clusters are >= 100 nodes so the cut is active; the
+# no-score profile takes numNodesToFind = 1 (schedule_one.go:780-782).
+NO_SCORE = {"disabledPlugins": ["TaintToleration", "NodeAffinity", "NodeResourcesFit", "PodTopologySpread",
+                                "InterPodAffinity", "NodeResourcesBalancedAllocation", "ImageLocality"]}
+SAMPLING = [(0, {}), (7, {}), (30, {}), (55, {"nodeResourcesFit": {"scoringStrategy": {"type": "MostAllocated"}}}),
+            (0, {"interPodAffinity": {"hardPodAffinityWeight": 5}}), (100, NO_SCORE), (20, NO_SCORE)]
+
+
+@pytest.mark.parametrize("k", range(len(SAMPLING)))
+@pytest.mark.parametrize("seed", range(3))
+def test_sampling_sequences_match_oracle(native, k, seed):
+    pct, extra = SAMPLING[k]
+    rng, _, nodes, existing, names = rand_cluster(5000 + 10 * k + seed, n_nodes=[130, 257, 600][seed], n_existing=60)
+    cfg = dict(extra, percentageOfNodesToScore=pct)
+    g, o = _pair(native, cfg, nodes, existing)
+    for q in range(30):
+        _cmp_cycle(g, o, rand_pod(rng, q, names), f"pct {pct} seed {seed} pod {q}")
+
+
+@pytest.mark.parametrize("k", range(len(SAMPLING)))
+def test_sampling_batch_matches_sequential_oracle(native, k):
+    """The rotation is carried pod to pod on the device inside one batch."""
+    pct, extra = SAMPLING[k]
+    rng, _, nodes, existing, names = rand_cluster(6000 + k, n_nodes=700, n_existing=80)
+    cfg = dict(extra, percentageOfNodesToScore=pct)
+    g, o = _pair(native, cfg, nodes, existing)
+    for rnd in range(2):  # two batches: the host picks the rotation up from the first
+        pods = [rand_pod(rng, 200 * rnd + q, names) for q in range(120)]
+        rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+        for q, p in enumerate(pods):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[q].as_tuple() == ro.as_tuple(), f"pct {pct} batch {rnd} pod {q}"
+
+
+def test_sampling_prefilter_subset_over_100_nodes(native):
+    """A PreFilterResult (matchFields metadata.name) of 150 nodes is itself sampled: the rotation
+    runs over the subset list and nextStartNodeIndex advances by the subset's processed count."""
+    from ksg.objects import PodW
+    rng, _, nodes, existing, names = rand_cluster(77, n_nodes=400, n_existing=40)
+    g, o = _pair(native, {"percentageOfNodesToScore": 10}, nodes, existing)
+    for q in range(12):
+        sub = rng.sample(names, 150)
+        p = PodW(f"s{q}", uid=f"s{q}").req({"cpu": "100m"}).node_affinity_required(
+            [{"matchFields": [{"key": "metadata.name", "operator": "In", "values": sub}]}]).obj()
+        _cmp_cycle(g, o, p, f"subset pod {q}")
+        _cmp_cycle(g, o, rand_pod(rng, q, names), f"pod {q}")
