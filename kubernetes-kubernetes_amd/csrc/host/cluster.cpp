@@ -264,7 +264,7 @@ void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo
 
 // node_override: the node an assumed pod was placed on (the spec itself is left unbound)
 int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done, int32_t slot,
-                     const std::string* node_override) {
+                     const std::string* node_override, const PodResources* res) {
   const std::string uid = uid_override.empty() ? p.uid : uid_override;
   const std::string& node_name = node_override ? *node_override : p.node_name;
   if (node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
@@ -274,7 +274,7 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   BoundPod bp;
   bp.uid = uid;
   bp.node = node_name;
-  bp.res = calc_resources(p);
+  bp.res = res ? *res : calc_resources(p);
   bp.with_affinity = p.has_pod_affinity || p.has_pod_anti;
   pods_with_affinity += bp.with_affinity ? 1 : 0;
   auto take = [&](const Container& c) {

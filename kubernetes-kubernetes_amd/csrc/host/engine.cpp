@@ -549,7 +549,8 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   out->score_mask = smask;
   if (assume) {
     D.flags |= DF_ASSUME;
-    D.slot = c->pod_table_put(p, -1);  // live once k_select's assume writes its node index
+    // live once k_select's assume writes its node index; a pipelined batch reserved it up front
+    D.slot = next_slot_ >= 0 ? next_slot_ : c->pod_table_put(p, -1);
     out->slot = D.slot;
   }
   if (eval) D.flags |= DF_EVAL_OUT;
@@ -830,6 +831,20 @@ Engine::Engine(Cluster* cl) : c(cl) {
 
 // A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
 // PodTopologySpread / InterPodAffinity scores, no per-node evaluation output).
+// No extended-resource requests anywhere in the pod (the batch pipeline's compile-cannot-fail test).
+static bool calc_scalar_free(const PodSpec& p) {
+  auto ok = [](const ResVec& v) {
+    for (auto& r : v)
+      if (r.name != "cpu" && r.name != "memory" && r.name != "ephemeral-storage") return false;
+    return true;
+  };
+  for (auto& k : p.containers)
+    if (!ok(k.req)) return false;
+  for (auto& k : p.init_containers)
+    if (!ok(k.req)) return false;
+  return ok(p.pod_requests) && ok(p.overhead);
+}
+
 bool Engine::rotdev() const {
   bool any_score = false;
   for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) any_score |= c->cfg.enabled[q];
@@ -891,6 +906,8 @@ Engine::~Engine() {
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
   for (hipEvent_t e : cev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : pev) (void)hipEventDestroy(e);
+  if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail})
     if (b->p) (void)hipFree(b->p);
@@ -1030,77 +1047,174 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   using clk = std::chrono::steady_clock;
   const auto T0 = clk::now();
-  // ---- compile every pod (may materialise label columns / relayout the mirror)
-  std::vector<CompiledPod> cp(n);
-  int64_t start = c->next_start;
-  for (int i = 0; i < n; ++i) {
-    int rc = compile(*pods[i], CYCLE, -1, assume, eval != nullptr, &cp[i]);
-    if (rc) {
-      c->next_start = start;
-      for (int j = 0; j < i; ++j) c->pod_table_drop(cp[j].slot);
-      return rc;
+  // ---- the chunk plan (needs the exchange mode of a sharded context)
+  const int W = comm ? c->cfg.world : 1;
+  // In-process ranks (localGroup, one device) need every rank's loop resident at once: each rank has
+  // its own stream, and streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, default 4)
+  // share queues and serialise.  Such groups keep the all-reduce path.
+  static const int hwq = [] {
+    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+    return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
+  }();
+  const bool rccl = !c->cfg.nccl_id.empty();
+  const bool dx = comm && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) && (rccl || W < hwq);
+  // Host/device pipeline: the batch runs as chunks.  While the device schedules chunk k the host
+  // compiles and stages chunk k+1, then mirrors the finished chunks' assumes into the cache.  Only
+  // chunk 0's compile and the last chunk's bookkeeping are exposed, so chunk 0 is short (64 pods),
+  // each next chunk at most 5x the previous (its compile, ~1 us per pod, hides under the previous
+  // chunk's device time, ~6 us per pod), and the tail shrinks geometrically (60 % of what is left)
+  // down to a last chunk of <= 32 pods.
+  std::vector<int> bnd;
+  if ((!comm || dx) && !eval && n >= 256)
+    for (int r = n, prev = 0; r > 32;) {
+      int take = prev == 0 ? 64 : std::min((r * 3 + 4) / 5, 5 * prev);
+      take = std::min(take, r);
+      bnd.push_back(n - r + take);
+      r -= take;
+      prev = take;
     }
-    if (cp[i].prefilter_error) cp[i].error = true;  // PreFilter Error: status Error, no launch
-    if (!cp[i].prefilter_reject && !cp[i].prefilter_error && !rotdev()) {
-      // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
-      const int64_t N = (int64_t)c->order().size();
-      c->next_start = (c->next_start + cp[i].num_all) % N;
+  if (bnd.empty() || bnd.back() != n) bnd.push_back(n);
+  auto chunk_end = [&](int i) {  // end of the chunk holding pod i
+    return *std::upper_bound(bnd.begin(), bnd.end(), i);
+  };
+  // Compiling a chunk after chunk 0 is launched needs every pod-table slot reserved and uploaded
+  // before the first launch: a later full upload would overwrite the pod_node entries the device
+  // assumes wrote.  A reservation adds the pod's (anti-)affinity terms to the key tables other pods'
+  // compiles read, so batches holding PodTopologySpread / InterPodAffinity / extended-resource pods
+  // (the compile paths that can also fail) compile everything before the first launch.
+  bool pipe = bnd.size() > 1;
+  for (int i = 0; i < n && pipe; ++i) {
+    const PodSpec& q = *pods[i];
+    pipe = !q.has_pod_affinity && !q.has_pod_anti && q.spreads.empty() && calc_scalar_free(q);
+  }
+  std::vector<int32_t> pre_slot;
+  if (pipe && assume) {
+    pre_slot.resize(n);
+    for (int i = 0; i < n; ++i) pre_slot[i] = c->pod_table_put(*pods[i], -1);
+  }
+  std::vector<CompiledPod> cp(n);
+  int compiled = 0;
+  // compile pods [compiled, b) against the cache (PreFilter / PreScore on the host)
+  auto compile_upto = [&](int b) -> int {
+    for (int i = compiled; i < b; ++i) {
+      next_slot_ = pre_slot.empty() ? -1 : pre_slot[i];
+      const int rc = compile(*pods[i], CYCLE, -1, assume, eval != nullptr, &cp[i]);
+      next_slot_ = -1;
+      if (rc) return rc;
+      if (cp[i].prefilter_error) cp[i].error = true;  // PreFilter Error: status Error, no launch
+      if (!cp[i].prefilter_reject && !cp[i].prefilter_error && !rotdev()) {
+        // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
+        const int64_t N = (int64_t)c->order().size();
+        c->next_start = (c->next_start + cp[i].num_all) % N;
+      }
+      compiled = i + 1;
+    }
+    return KSG_OK;
+  };
+  int rc;
+  {
+    const int64_t start = c->next_start;
+    if ((rc = compile_upto(pipe ? bnd[0] : n))) {  // nothing launched: the batch fails as a whole
+      c->next_start = start;
+      if (!pre_slot.empty())
+        for (int32_t sl : pre_slot) c->pod_table_drop(sl);
+      else
+        for (int j = 0; j < compiled; ++j) c->pod_table_drop(cp[j].slot);
+      return rc;
     }
   }
   const auto T1 = clk::now();
-  int rc = c->ensure_mirror();
-  if (rc) return rc;
-  // ---- stage descriptors + stats in pinned memory, one H2D
+  if ((rc = c->ensure_mirror())) return rc;
+  // ---- staging: [offsets n | program sizes n | PodStats n | DevResult n | give-up flags n | programs]
+  // in pinned memory; each chunk's programs, offsets and stats go up in their own H2D copies
   size_t desc_bytes = 0;
   int32_t arena_words = 0;
-  for (auto& x : cp) {
-    desc_bytes += x.blob.size();
-    arena_words = std::max(arena_words, x.arena_words);
+  for (int i = 0; i < compiled; ++i) {
+    desc_bytes += cp[i].blob.size();
+    arena_words = std::max(arena_words, cp[i].arena_words);
   }
+  if (compiled < n)  // room for the chunks still to be compiled (re-sized after a sync if they outgrow it)
+    desc_bytes = std::max(desc_bytes * 2 * (size_t)n / (size_t)compiled, (size_t)n * 1024);
   if ((rc = ensure_scratch(desc_bytes, n, eval != nullptr, arena_words))) return rc;
-  uint8_t* hp = (uint8_t*)h_pinned;
-  std::vector<uint32_t> offs(n);
-  size_t o = 0;
-  for (int i = 0; i < n; ++i) {
-    offs[i] = (uint32_t)o;
-    std::memcpy(hp + o, cp[i].blob.data(), cp[i].blob.size());
-    o += cp[i].blob.size();
-  }
-  std::memcpy(hp + o, offs.data(), (size_t)n * 4);
-  for (int i = 0; i < n; ++i) {  // program sizes follow the offsets (k_sched_loop's prefetch)
-    const uint32_t sz = (uint32_t)cp[i].blob.size();
-    std::memcpy(hp + o + (size_t)(n + i) * 4, &sz, 4);
-  }
-  PodStats* hs = (PodStats*)(hp + ((o + (size_t)n * 8 + 15) & ~size_t(15)));
-  for (int i = 0; i < n; ++i) {
-    std::memset(&hs[i], 0, sizeof(PodStats));
-    for (int q = 0; q < kNumPlugins; ++q) {
-      hs[i].max_raw[q] = enc_i64(INT64_MIN);
-      hs[i].min_raw[q] = enc_i64(INT64_MAX);
-    }
-  }
+  const size_t meta = ((size_t)n * 8 + 15) & ~size_t(15);
+  const size_t meta_all = meta + (((size_t)n * (sizeof(PodStats) + sizeof(DevResult) + 4) + 15) & ~size_t(15));
+  uint8_t* hp = nullptr;
+  uint32_t* h_offs = nullptr;
+  PodStats* hs = nullptr;
+  DevResult* hr = nullptr;
+  uint32_t* hfail = nullptr;
+  uint8_t* hdesc = nullptr;
+  size_t desc_cap = 0, o = 0;
+  auto map_pinned = [&]() {
+    hp = (uint8_t*)h_pinned;
+    h_offs = (uint32_t*)hp;
+    hs = (PodStats*)(hp + meta);
+    hr = (DevResult*)(hs + n);
+    hfail = (uint32_t*)(hr + n);
+    hdesc = hp + meta_all;
+    desc_cap = std::min(h_pinned_bytes - meta_all, d_descs.bytes);
+  };
+  map_pinned();
+  hipStream_t s = c->stream;
+  const MirrorView& m = c->view;
   // device-resident nextStartNodeIndex: each launched pod's k_sample_find reads the previous
   // launched pod's rotation; the first reads the host's value
   const bool rot_dev = rotdev();
   int last_launched = -1;
-  if (rot_dev)
-    for (int i = 0; i < n; ++i) {
-      if (cp[i].error) continue;
-      PodDesc* pd = reinterpret_cast<PodDesc*>(hp + offs[i]);
-      pd->prev_pod = last_launched;
-      if (last_launched < 0) hs[i].rot_in = (uint32_t)c->next_start;
-      last_launched = i;
+  // programs, offsets, stats of pods [a, b) into pinned memory, then their H2D copies
+  // chunks after the first go up on the copy stream while the device runs the chunk before them;
+  // the compute stream waits for them before the chunk's first launch
+  // (not for in-process rank groups: their streams already outnumber the hardware queues, and a
+  // copy stream's event wait sharing a queue with a peer's loop launch would hold that loop back)
+  const bool copy_stream = pipe && (!comm || rccl);
+  if (copy_stream && !cstream) HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+  while (pev.size() < 2 * bnd.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    pev.push_back(e);
+  }
+  int staged_chunks = 0;
+  auto stage = [&](int a, int b) -> int {
+    const bool async = copy_stream && a > 0;
+    hipStream_t st_ = async ? cstream : s;
+    const size_t o0 = o;
+    for (int i = a; i < b; ++i) {
+      h_offs[i] = (uint32_t)o;
+      h_offs[n + i] = (uint32_t)cp[i].blob.size();  // program sizes follow the offsets (k_sched_loop's prefetch)
+      std::memcpy(hdesc + o, cp[i].blob.data(), cp[i].blob.size());
+      PodStats& st = hs[i];
+      std::memset(&st, 0, sizeof(PodStats));
+      for (int q = 0; q < kNumPlugins; ++q) {
+        st.max_raw[q] = enc_i64(INT64_MIN);
+        st.min_raw[q] = enc_i64(INT64_MAX);
+      }
+      if (rot_dev && !cp[i].error) {
+        reinterpret_cast<PodDesc*>(hdesc + o)->prev_pod = last_launched;
+        if (last_launched < 0) st.rot_in = (uint32_t)c->next_start;
+        last_launched = i;
+      }
+      o += cp[i].blob.size();
     }
-  hipStream_t s = c->stream;
-  const MirrorView& m = c->view;
-  HIPCHK(hipMemcpyAsync(d_descs.p, hp, o, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d_off.p, hp + o, (size_t)n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(d_stats.p, hs, (size_t)n * sizeof(PodStats), hipMemcpyHostToDevice, s));
+    if (b > a) {
+      HIPCHK(hipMemcpyAsync((uint8_t*)d_descs.p + o0, hdesc + o0, o - o0, hipMemcpyHostToDevice, st_));
+      HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + a, h_offs + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice, st_));
+      HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + n + a, h_offs + n + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice, st_));
+      HIPCHK(hipMemcpyAsync((PodStats*)d_stats.p + a, hs + a, (size_t)(b - a) * sizeof(PodStats),
+                            hipMemcpyHostToDevice, st_));
+    }
+    if (async) {
+      HIPCHK(hipEventRecord(pev[2 * (size_t)staged_chunks], cstream));
+      HIPCHK(hipStreamWaitEvent(s, pev[2 * (size_t)staged_chunks], 0));
+    }
+    ++staged_chunks;
+    return KSG_OK;
+  };
+  if ((rc = stage(0, compiled))) return rc;
   if (eval) {
     HIPCHK(hipMemsetAsync(d_out.p, 0, (size_t)m.cap * 8 * kNumPlugins, s));
     HIPCHK(hipMemsetAsync(d_total.p, 0, (size_t)m.cap * 8, s));
   }
-  const BatchView bv = bview(n);
+  BatchView bv = bview(n);
   const int stride = c->cfg.timing_stride;
   const size_t npairs = stride > 0 ? (size_t)((n + stride - 1) / stride) : 0;
   while (tev.size() < 2 * npairs) {
@@ -1115,7 +1229,6 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // the rank's shard (k_sched_loop).  Sharded, every rank uses the same G (from the largest shard):
   // the exchange has world * G participants.
   const int NB = (m.n + kBlock - 1) / kBlock;
-  const int W = comm ? c->cfg.world : 1;
   int32_t sblk0 = 0, snblk = NB;
   if (comm) shard_range(m.n, &sblk0, &snblk);
   const int NBs = (NB + W - 1) / W;
@@ -1124,15 +1237,6 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const int max_wg = std::min(256 / W, comm && c->cfg.nccl_id.empty() ? cus / W : cus);
   int G = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
   G = std::min(std::max(G, (NBs + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NBs, 1), max_wg));
-  // In-process ranks (localGroup, one device) need every rank's loop resident at once: each rank has
-  // its own stream, and streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, default 4)
-  // share queues and serialise.  Such groups keep the all-reduce path.
-  static const int hwq = [] {
-    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
-    return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
-  }();
-  const bool rccl = !c->cfg.nccl_id.empty();
-  const bool dx = comm && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) && (rccl || W < hwq);
   const bool use_loop = (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
                         (int64_t)G * kLoopMaxBlk >= NBs && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   struct LoopRun { int first, count; double bytes; };
@@ -1150,33 +1254,113 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
 #endif
     }
   }
-  // Host/device pipeline: the batch is enqueued as up to four chunks, each followed by the D2H of
-  // its results (and of the loop's give-up flag) and an event, so the host's bookkeeping of chunk
-  // k (the cache's assumed pods) runs while the device schedules chunk k+1.  Every pod was compiled
-  // above, against the cache as it was when the batch started, so the order of host work does not
-  // change any result.
-  DevResult* hr = (DevResult*)(hs + n);
-  uint32_t* hfail = (uint32_t*)(hr + n);
-  const int CH = ((!comm || dx) && !eval && n >= 256) ? (n + 3) / 4 : n;
   struct Chunk { int a, b; };
   std::vector<Chunk> chunks;
-  while (cev.size() < (size_t)(n + CH - 1) / CH) {
+  while (cev.size() < bnd.size()) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     cev.push_back(e);
   }
   auto close_chunk = [&](int upto) -> int {
     const int a = chunks.empty() ? 0 : chunks.back().b;
+    hipStream_t ds = s;
+    if (copy_stream) {  // results come back on the copy stream, off the compute stream's path
+      HIPCHK(hipEventRecord(pev[2 * chunks.size() + 1], s));
+      HIPCHK(hipStreamWaitEvent(cstream, pev[2 * chunks.size() + 1], 0));
+      ds = cstream;
+    }
     HIPCHK(hipMemcpyAsync(hr + a, (DevResult*)d_results.p + a, (size_t)(upto - a) * sizeof(DevResult),
-                          hipMemcpyDeviceToHost, s));
-    if (use_loop) HIPCHK(hipMemcpyAsync(hfail + chunks.size(), d_fail.p, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipEventRecord(cev[chunks.size()], s));
+                          hipMemcpyDeviceToHost, ds));
+    if (use_loop) HIPCHK(hipMemcpyAsync(hfail + chunks.size(), d_fail.p, 4, hipMemcpyDeviceToHost, ds));
+    HIPCHK(hipEventRecord(cev[chunks.size()], ds));
     chunks.push_back({a, upto});
     return KSG_OK;
   };
+  // results + host shadow of the device-side assumes for pods [a, b)
+  auto settle = [&](int a, int b) -> int {
+    for (int i = a; i < b; ++i) {
+      ksg_result& r = results[i];
+      if (cp[i].error) {
+        r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
+        c->pod_table_drop(cp[i].slot);
+        continue;
+      }
+      const DevResult& d = hr[i];
+      r.status = d.status;
+      r.node_index = d.node;
+      r.feasible_nodes = d.feasible;
+      r.evaluated_nodes = d.feasible > 0 ? cp[i].num_all : (cp[i].prefilter_reject ? 0 : cp[i].num_all);
+      if (rot_dev) {
+        if (!cp[i].prefilter_reject) r.evaluated_nodes = d.evaluated;
+        if (!cp[i].error) c->next_start = d.rot_next;  // the last launched pod's wins
+      }
+      r.total_score = d.feasible > 1 ? d.total : 0;
+      if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
+      if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
+        static uint64_t seq = 0;
+        std::string uid = pods[i]->uid + "#a" + std::to_string(++seq);
+        int rc2 = c->add_pod(*pods[i], uid, /*device_done=*/true, cp[i].slot, &c->order()[r.node_index], &cp[i].res);
+        if (rc2) return rc2;
+        assumed[handles.empty() ? -1 : handles[i]] = uid;
+      } else {
+        c->pod_table_drop(cp[i].slot);  // not placed: the reserved pod-table slot never went live
+      }
+    }
+    return KSG_OK;
+  };
+  int settled = 0;  // chunks whose results are mirrored into the cache
+  auto settle_closed = [&]() -> int {  // after a stream sync: every closed chunk
+    for (; settled < (int)chunks.size(); ++settled) {
+      if (use_loop && hfail[settled]) {
+        c->err = "k_sched_loop: an exchange granule never arrived (spin limit)";
+        return KSG_EDEVICE;
+      }
+      const int r2 = settle(chunks[settled].a, chunks[settled].b);
+      if (r2) return r2;
+    }
+    return KSG_OK;
+  };
+  // compile + stage the chunk starting at pod i while the device runs the chunks before it
+  auto next_chunk = [&](int i) -> int {
+    const int b = chunk_end(i);
+    int r2 = compile_upto(b);
+    auto drain = [&]() -> int {  // close chunk k, wait for both streams
+      if ((chunks.empty() || chunks.back().b < i) && close_chunk(i)) return KSG_EDEVICE;
+      HIPCHK(hipStreamSynchronize(s));
+      if (cstream) HIPCHK(hipStreamSynchronize(cstream));
+      return KSG_OK;
+    };
+    if (r2) {  // the pods before i are scheduled: finish their bookkeeping, release the rest's slots
+      if (drain()) return KSG_EDEVICE;
+      const int r3 = settle_closed();
+      for (int j = i; j < (int)pre_slot.size(); ++j) c->pod_table_drop(pre_slot[j]);
+      return r3 ? r3 : r2;
+    }
+    size_t need = 0;
+    int32_t aw = 0;
+    for (int j = i; j < b; ++j) {
+      need += cp[j].blob.size();
+      aw = std::max(aw, cp[j].arena_words);
+    }
+    if (c->layout_dirty || c->pods_dirty || o + need > desc_cap || aw > arena_words) {
+      // the mirror must be re-laid out or the buffers grown: drain the device and mirror what it
+      // assumed first (the same state a batch boundary here would give)
+      if ((r2 = drain())) return r2;
+      if ((r2 = settle_closed())) return r2;
+      if ((r2 = c->ensure_mirror())) return r2;
+      arena_words = std::max(arena_words, aw);
+      o = 0;
+      if ((r2 = ensure_scratch(std::max(need, desc_bytes), n, false, arena_words))) return r2;
+      map_pinned();
+      bv = bview(n);
+    }
+    return stage(i, b);
+  };
   for (int i = 0; i < n && (!comm || dx);) {
-    if (i > 0 && i % CH == 0 && (chunks.empty() || chunks.back().b < i))
-      if ((rc = close_chunk(i))) return rc;
+    if (i > 0 && std::binary_search(bnd.begin(), bnd.end(), i) && (chunks.empty() || chunks.back().b < i)) {
+      if (i >= compiled && (rc = next_chunk(i))) return rc;  // its H2D does not wait for chunk k
+      if ((chunks.empty() || chunks.back().b < i) && (rc = close_chunk(i))) return rc;
+    }
     if (cp[i].error) {
       ++i;
       continue;
@@ -1184,7 +1368,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (use_loop && loop_ok(cp[i])) {  // a run of node-local pods: one k_sched_loop launch
       int j = i;
       double rb = 0;
-      const int cut = (i / CH + 1) * CH;
+      const int cut = chunk_end(i);
       while (j < n && j < cut && j - i < kLoopMaxPods && loop_ok(cp[j]))
         rb += algo_bytes(*reinterpret_cast<const PodDesc*>(cp[j++].blob.data())) *
               (comm && m.n > 0 ? std::min(1.0, (double)snblk * kBlock / (double)m.n) : 1.0);
@@ -1255,40 +1439,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     HIPCHK(hipMemcpyAsync(outs.data(), d_out.p, outs.size() * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
   }
-  // results + host shadow of the device-side assumes for pods [a, b)
-  auto settle = [&](int a, int b) -> int {
-    for (int i = a; i < b; ++i) {
-      ksg_result& r = results[i];
-      if (cp[i].error) {
-        r = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
-        c->pod_table_drop(cp[i].slot);
-        continue;
-      }
-      const DevResult& d = hr[i];
-      r.status = d.status;
-      r.node_index = d.node;
-      r.feasible_nodes = d.feasible;
-      r.evaluated_nodes = d.feasible > 0 ? cp[i].num_all : (cp[i].prefilter_reject ? 0 : cp[i].num_all);
-      if (rot_dev) {
-        if (!cp[i].prefilter_reject) r.evaluated_nodes = d.evaluated;
-        if (i == last_launched) c->next_start = d.rot_next;
-      }
-      r.total_score = d.feasible > 1 ? d.total : 0;
-      if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
-      if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
-        static uint64_t seq = 0;
-        std::string uid = pods[i]->uid + "#a" + std::to_string(++seq);
-        int rc2 = c->add_pod(*pods[i], uid, /*device_done=*/true, cp[i].slot, &c->order()[r.node_index]);
-        if (rc2) return rc2;
-        assumed[handles.empty() ? -1 : handles[i]] = uid;
-      } else {
-        c->pod_table_drop(cp[i].slot);  // not placed: the reserved pod-table slot never went live
-      }
-    }
-    return KSG_OK;
-  };
   if (chunks.size() > 1)  // pipelined: settle each chunk as soon as its results have landed
-    for (size_t k = 0; k < chunks.size(); ++k) {
+    for (size_t k = (size_t)settled; k < chunks.size(); ++k) {
       HIPCHK(hipEventSynchronize(cev[k]));
       if (use_loop && hfail[k]) {
         uint32_t f[4] = {0, 0, 0, 0};
@@ -1301,6 +1453,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       if ((rc = settle(chunks[k].a, chunks[k].b))) return rc;
     }
   HIPCHK(hipStreamSynchronize(s));
+  if (copy_stream) HIPCHK(hipStreamSynchronize(cstream));
   const auto T3 = clk::now();
   if (comm && comm->batch_end()) {
     c->err = comm->err;
@@ -1465,7 +1618,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
 
   // ---- results + host shadow of the device-side assumes
-  if (chunks.size() <= 1)
+  if (chunks.size() <= 1 && settled == 0)
     if ((rc = settle(0, n))) return rc;
   if (c->cfg.loop_stamps) {
     const auto T4 = clk::now();

@@ -232,8 +232,9 @@ class Cluster {
   int remove_node(const std::string& name);
   // device_done: the HBM mirror already holds the pod (device-side AssumePod)
   // slot: the pod-table slot reserved for an assumed pod at compile time (-1: allocate one)
+  // res: the pod's PodInfo.CalculateResource when the caller already has it (a compiled pod)
   int add_pod(const PodSpec& p, const std::string& uid_override = "", bool device_done = false, int32_t slot = -1,
-              const std::string* node_override = nullptr);
+              const std::string* node_override = nullptr, const PodResources* res = nullptr);
   int remove_pod(const std::string& uid);
   int32_t pods_with_affinity = 0;
 
@@ -253,7 +254,7 @@ class Cluster {
   std::vector<PortRec> ports;
   Interner scalar_ix;  // extended / scalar resource columns
   std::map<std::string, NamespaceSpec> namespaces;
-  std::map<std::string, BoundPod> pods;
+  std::unordered_map<std::string, BoundPod> pods;
 
   int32_t key_id(const std::string& k);
   Interner ns_ix;  // namespace names
@@ -370,6 +371,9 @@ class Engine {
   bool loop_ok(const CompiledPod& p) const;
   // node-sharded evaluation (cfg.world > 1): this rank's block range + the exchange transport
   std::unique_ptr<Comm> comm;
+  int32_t next_slot_ = -1;  // compile(): a pod-table slot reserved by run_batch's pipeline
+  hipStream_t cstream = nullptr;    // run_batch's copy stream (pipelined chunks' H2D / D2H)
+  std::vector<hipEvent_t> pev;      // its per-chunk staged / finished events
   // nextStartNodeIndex advances by a data-dependent count (percentageOfNodesToScore < 100, or
   // numNodesToFind = 1 without score plugins): it is kept on the device across a batch
   bool rotdev() const;
