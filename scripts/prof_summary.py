@@ -23,7 +23,9 @@ def main():
     tag = sys.argv[1]
     nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
     workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
-    loop_pods = int(sys.argv[4]) if len(sys.argv) > 4 else 1000
+    # pods per k_sched_loop dispatch, on average: a 1000-pod batch runs as 7 chunks (engine.cpp
+    # run_batch: 64, 320, 370, 148, 59, 24, 15), each one loop dispatch
+    loop_pods = float(sys.argv[4]) if len(sys.argv) > 4 else 1000.0 / 7.0
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     c = sqlite3.connect(os.path.join(PROF, "trace", "run_results.db"))
@@ -40,8 +42,8 @@ def main():
             lines.append(f"{kn} dispatch duration us: median {d[len(d) // 2] / 1e3:.3f} "
                          f"p10 {d[len(d) // 10] / 1e3:.3f} p90 {d[9 * len(d) // 10] / 1e3:.3f}")
             if kn == "k_sched_loop":
-                lines.append(f"k_sched_loop per pod us ({loop_pods} pods per dispatch): median "
-                             f"{d[len(d) // 2] / 1e3 / loop_pods:.3f}")
+                lines.append(f"k_sched_loop per pod us (mean dispatch / {loop_pods:.2f} pods per dispatch): "
+                             f"{sum(d) / len(d) / 1e3 / loop_pods:.3f}")
     open(os.path.join(out, f"{tag}_kernel_stats.txt"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
@@ -90,7 +92,7 @@ def main():
             avg = {k: sum(v) / len(v) for k, v in sq.items()}
             waves = avg.get("SQ_WAVES", 1.0) or 1.0
             sl = [f"# rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES "
-                  f"GRBM_GUI_ACTIVE GRBM_COUNT, k_sched_loop, per dispatch ({loop_pods} pods) (tag {tag})"]
+                  f"GRBM_GUI_ACTIVE GRBM_COUNT, k_sched_loop, per dispatch ({loop_pods:.2f} pods) (tag {tag})"]
             for k in sorted(avg):
                 sl.append(f"{k:20s} {avg[k]:16.1f}")
             for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
