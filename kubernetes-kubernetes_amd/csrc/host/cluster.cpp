@@ -471,7 +471,9 @@ int Cluster::ensure_label_slot(int32_t key) {
   keys[key].slot = slots_used_++;
   if (layout_dirty || slots_used_ > slots_cap_) {
     layout_dirty = true;  // regrow on the next ensure_mirror
-    return ensure_mirror();
+    // (deferred while a pipelined batch has pods in flight: the shadow lacks their assumes until
+    // the batch drains and mirrors them, engine.cpp run_batch)
+    return defer_relayout ? KSG_OK : ensure_mirror();
   }
   return upload_label_column(key);
 }

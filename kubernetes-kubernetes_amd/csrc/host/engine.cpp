@@ -1323,7 +1323,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // compile + stage the chunk starting at pod i while the device runs the chunks before it
   auto next_chunk = [&](int i) -> int {
     const int b = chunk_end(i);
+    c->defer_relayout = true;  // the earlier chunks' assumes are not in the shadow yet
     int r2 = compile_upto(b);
+    c->defer_relayout = false;
     auto drain = [&]() -> int {  // close chunk k, wait for both streams
       if ((chunks.empty() || chunks.back().b < i) && close_chunk(i)) return KSG_EDEVICE;
       HIPCHK(hipStreamSynchronize(s));
@@ -1346,6 +1348,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       // the mirror must be re-laid out or the buffers grown: drain the device and mirror what it
       // assumed first (the same state a batch boundary here would give)
       if ((r2 = drain())) return r2;
+      if (c->cfg.loop_stamps)
+        std::fprintf(stderr, "[host] pipeline drained before pod %d (%s)\n", i,
+                     c->layout_dirty || c->pods_dirty ? "mirror re-layout" : "staging grown");
       if ((r2 = settle_closed())) return r2;
       if ((r2 = c->ensure_mirror())) return r2;
       arena_words = std::max(arena_words, aw);

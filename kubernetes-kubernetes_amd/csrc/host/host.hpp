@@ -286,6 +286,7 @@ class Cluster {
   MirrorView view;
   hipStream_t stream = nullptr;
   bool layout_dirty = true;
+  bool defer_relayout = false;  // ensure_label_slot only marks layout_dirty (pods in flight)
   int ensure_mirror();                       // (re)build device arrays if dirty
   int ensure_label_slot(int32_t key);        // materialise a label column
   int upload_node_dynamic(int32_t idx);      // push one node's Requested/ports to HBM

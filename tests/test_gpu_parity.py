@@ -254,3 +254,46 @@ def test_sampling_prefilter_subset_over_100_nodes(native):
             [{"matchFields": [{"key": "metadata.name", "operator": "In", "values": sub}]}]).obj()
         _cmp_cycle(g, o, p, f"subset pod {q}")
         _cmp_cycle(g, o, rand_pod(rng, q, names), f"pod {q}")
+
+
+# ---- the host pipeline's fallbacks (engine.cpp run_batch): a later chunk whose compile references a
+# label key no node column holds yet (mirror re-layout mid-batch), or whose programs outgrow the
+# staging buffers sized from chunk 0, drains the device, mirrors the finished chunks and re-lays
+# out -- the results must still be the sequential oracle's.
+def _pipeline_cluster(n_nodes=900):
+    from ksg.objects import NodeW
+    nodes = []
+    for i in range(n_nodes):
+        w = NodeW(f"node-{i:05d}").capacity({"cpu": "8", "memory": "32Gi", "pods": "110"}) \
+            .label("kubernetes.io/hostname", f"node-{i:05d}").label("rack", f"r{i % 7}").label("tier", f"t{i % 3}")
+        for q in range(12):
+            w = w.label(f"k{q}", f"v{(i + q) % 4}")
+        nodes.append(w.obj())
+    return nodes
+
+
+def test_pipeline_relayout_mid_batch(native):
+    from ksg.objects import PodW
+    nodes = _pipeline_cluster()
+    pods = []
+    for k in range(700):
+        p = PodW(f"p{k}", uid=f"p{k}").req({"cpu": "100m", "memory": "200Mi"})
+        if k >= 300 and k % 5 == 0:  # first seen after chunk 0: new label columns mid-batch, more
+            # than the column capacity the mirror was laid out with (a full re-layout)
+            p = p.node_selector({f"k{(k // 10) % 12}": f"v{k % 4}"} if k % 2 else {"tier": f"t{k % 3}"})
+        pods.append(p.obj())
+    _stream(native, nodes, [], pods)
+
+
+def test_pipeline_staging_outgrown_mid_batch(native):
+    from ksg.objects import PodW
+    nodes = _pipeline_cluster()
+    pods = []
+    for k in range(700):
+        p = PodW(f"q{k}", uid=f"q{k}").req({"cpu": "50m", "memory": "100Mi"})
+        if k >= 200:  # far larger programs than chunk 0's: many preferred node-affinity terms
+            p = p.node_affinity_preferred([(1 + (j % 9), {"matchExpressions": [
+                {"key": "kubernetes.io/hostname", "operator": "In",
+                 "values": [f"node-{(k * 31 + j * 7 + v) % 900:05d}" for v in range(40)]}]}) for j in range(16)])
+        pods.append(p.obj())
+    _stream(native, nodes, [], pods)
