@@ -318,6 +318,21 @@ enum XaWord : int {
 enum XpWord : int { XP_MAX_PTS = 0, XP_NMIN_PTS = 1, XP_WORDS = 4 };
 enum XbWord : int { XB_KEY = 0, XB_NODE = kMaxShards, XB_WORDS = 2 * kMaxShards };
 struct RankPtrs { unsigned long long* p[kMaxShards]; };  // every rank's exchange vector (local transport)
+// One node's static columns (NodeInfo.node) for an in-place update of the mirror, flushed in bulk
+// at the next cycle (Cluster::flush_node_updates -> k_node_update).  Variable parts live in pools
+// after the records: taint / image ids (uint32) at id_off, label entries at lbl_off (lbl_cnt of
+// them: slot, value id, Gt/Lt integer, parse ok).
+struct NodeUpdate {
+  int32_t node, n_taint, n_img, lbl_cnt;
+  uint32_t taint_off, img_off;      // the node's CSR offsets on the device
+  uint32_t id_off, lbl_off;         // into the id / label pools of the flush
+  int64_t alloc_cpu, alloc_mem, alloc_eph;
+  int32_t alloc_pods;
+  uint32_t flags;
+  int64_t scalar[kMaxScalar];
+};
+struct LabelEntry { int32_t slot, value; int64_t num; int32_t ok, pad; };
+
 struct ShardView {
   int32_t world, rank;
   int32_t blk0, nblk;         // this rank's kBlock-node blocks [blk0, blk0 + nblk)

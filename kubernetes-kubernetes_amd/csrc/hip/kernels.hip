@@ -2079,6 +2079,38 @@ hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipSt
     hipLaunchKernelGGL(k_select<false>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
   return hipGetLastError();
 }
+// ---- incremental mirror ingestion (Cache.UpdateNode, cache.go UpdateNode + UpdateSnapshot's
+// generation diff): one thread per updated node writes its static columns in place.
+__global__ __launch_bounds__(kBlock) void k_node_update(MirrorView m, const NodeUpdate* u, const uint32_t* ids,
+                                                       const LabelEntry* lbl, int count) {
+  const int k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= count) return;
+  const NodeUpdate r = u[k];
+  const int i = r.node;
+  if (i < 0 || i >= m.n) return;
+  const size_t cap = (size_t)m.cap;
+  const_cast<int64_t*>(m.alloc_cpu)[i] = r.alloc_cpu;
+  const_cast<int64_t*>(m.alloc_mem)[i] = r.alloc_mem;
+  const_cast<int64_t*>(m.alloc_eph)[i] = r.alloc_eph;
+  const_cast<int32_t*>(m.alloc_pods)[i] = r.alloc_pods;
+  const_cast<uint32_t*>(m.flags)[i] = r.flags;
+  for (int q = 0; q < kMaxScalar; ++q) const_cast<int64_t*>(m.scalar_alloc)[(size_t)q * cap + i] = r.scalar[q];
+  for (int q = 0; q < r.n_taint; ++q) const_cast<uint32_t*>(m.taint_ids)[r.taint_off + q] = ids[r.id_off + q];
+  for (int q = 0; q < r.n_img; ++q) const_cast<uint32_t*>(m.img_ids)[r.img_off + q] = ids[r.id_off + r.n_taint + q];
+  for (int q = 0; q < r.lbl_cnt; ++q) {
+    const LabelEntry e = lbl[r.lbl_off + q];
+    const size_t o = (size_t)e.slot * cap + i;
+    const_cast<int32_t*>(m.labels)[o] = e.value;
+    const_cast<int64_t*>(m.label_num)[o] = e.num;
+    const_cast<uint8_t*>(m.label_num_ok)[o] = (uint8_t)e.ok;
+  }
+}
+hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const uint32_t* ids, const LabelEntry* lbl,
+                              int count, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_node_update, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, u, ids, lbl, count);
+  return hipGetLastError();
+}
 hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s) {
   const int nb = (m.n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_sample_find, dim3(1), dim3(kBlock), 0, s, m, b, pod, nb);
@@ -2130,7 +2162,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
                       reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
-                      reinterpret_cast<const void*>(&k_sample_apply)};
+                      reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_node_update)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
     if (e != hipSuccess) return e;

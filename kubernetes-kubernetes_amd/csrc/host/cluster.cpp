@@ -10,6 +10,8 @@
 #include "host.hpp"
 
 namespace ksg {
+hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const uint32_t* ids, const LabelEntry* lbl,
+                              int count, hipStream_t s);
 
 static const char* zone_key(const NodeSpec& n, std::string* out) {  // node/topology/helpers.go:31-58
   auto get = [&](const char* a, const char* b) -> std::string {
@@ -36,6 +38,7 @@ Cluster::~Cluster() {
   free_all();
   for (auto& b : pt_dev_)
     if (b.p) (void)hipFree(b.p);
+  if (upd_dev_.p) (void)hipFree(upd_dev_.p);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -221,9 +224,15 @@ int Cluster::update_node(NodeSpec&& n) {
     tree_remove(r.spec);
     tree_add(n);
   }
+  const size_t nt0 = r.taint_ids.size(), ni0 = r.image_ids.size();
   add_images(n);
   r.spec = std::move(n);
   intern_node(r);
+  // NodeInfo.SetNode (cache.go UpdateNode): a node that keeps its snapshot position (same zone)
+  // and its taint / image counts (same CSR ranges) is rewritten in place on the device; anything
+  // else (and a new extended resource or label column) takes the full re-layout
+  if (!layout_dirty && z0 == z1 && r.taint_ids.size() == nt0 && r.image_ids.size() == ni0)
+    return upload_node_static(index_of(r.spec.name));
   layout_dirty = true;
   return KSG_OK;
 }
@@ -329,7 +338,13 @@ int Cluster::remove_pod(const std::string& uid) {
 
 int Cluster::ensure_mirror() {
   order();
-  if (!layout_dirty) return upload_pod_table();
+  if (!layout_dirty) {
+    const int rc = flush_node_updates();
+    return rc ? rc : upload_pod_table();
+  }
+  for (int32_t i : static_dirty_)  // the re-layout below uploads every node
+    if ((size_t)i < static_queued_.size()) static_queued_[i] = 0;
+  static_dirty_.clear();
   HIPCHK(hipStreamSynchronize(stream));
   free_all();
   const int32_t n = (int32_t)order_.size();
@@ -398,6 +413,8 @@ int Cluster::ensure_mirror() {
     toff[i] = (uint32_t)tids.size();
     ioff[i] = (uint32_t)iids.size();
   }
+  node_toff_ = toff;  // CSR ranges of every node (upload_node_static rewrites a node's ids in place)
+  node_ioff_ = ioff;
   taint_ids_per_node = n ? (double)tids.size() / n : 0.0;
   taint_max_per_node = taint_max;
   img_ids_per_node = n ? (double)iids.size() / n : 0.0;
@@ -476,6 +493,85 @@ int Cluster::ensure_label_slot(int32_t key) {
     return defer_relayout ? KSG_OK : ensure_mirror();
   }
   return upload_label_column(key);
+}
+
+// The node's static columns (NodeInfo.node: allocatable, unschedulable, taints, images, the
+// materialised label columns) at snapshot position i are rewritten in place: the node is queued
+// and the queue goes to the device in one H2D + one k_node_update launch at the next cycle's
+// ensure_mirror -- the device-side counterpart of UpdateSnapshot's generation diff
+// (backend/cache/cache.go:223-265).
+int Cluster::upload_node_static(int32_t i) {
+  if (i < 0 || layout_dirty || (size_t)i + 1 >= node_toff_.size()) {
+    layout_dirty = true;
+    return KSG_OK;
+  }
+  if (static_queued_.size() < (size_t)view.n) static_queued_.resize((size_t)view.n, 0);
+  if (!static_queued_[i]) {
+    static_queued_[i] = 1;
+    static_dirty_.push_back(i);
+  }
+  return KSG_OK;
+}
+
+int Cluster::flush_node_updates() {
+  if (static_dirty_.empty()) return KSG_OK;
+  const size_t cnt = static_dirty_.size();
+  std::vector<NodeUpdate> rec(cnt);
+  std::vector<uint32_t> ids;
+  std::vector<LabelEntry> lbl;
+  std::vector<int64_t> vnum;
+  for (size_t q = 0; q < cnt; ++q) {
+    const int32_t i = static_dirty_[q];
+    static_queued_[i] = 0;
+    const NodeRec& r = *nodes_[order_[i]];
+    NodeUpdate& u = rec[q];
+    std::memset(&u, 0, sizeof(u));
+    u.node = i;
+    u.alloc_cpu = r.alloc_cpu;
+    u.alloc_mem = r.alloc_mem;
+    u.alloc_eph = r.alloc_eph;
+    u.alloc_pods = (int32_t)r.alloc_pods;
+    u.flags = r.spec.unschedulable ? 1u : 0u;
+    for (auto& kv : r.scalar_alloc) u.scalar[kv.first] = kv.second;
+    u.taint_off = node_toff_[i];
+    u.img_off = node_ioff_[i];
+    u.n_taint = (int32_t)r.taint_ids.size();
+    u.n_img = (int32_t)r.image_ids.size();
+    u.id_off = (uint32_t)ids.size();
+    ids.insert(ids.end(), r.taint_ids.begin(), r.taint_ids.end());
+    ids.insert(ids.end(), r.image_ids.begin(), r.image_ids.end());
+    u.lbl_off = (uint32_t)lbl.size();
+    for (int32_t k = 0; k < (int32_t)keys.size(); ++k) {  // labels.Requirement Gt/Lt parse (selector.go:265-289)
+      if (keys[k].slot < 0) continue;
+      LabelEntry e{keys[k].slot, -1, 0, 0, 0};
+      for (auto& kv : r.labels)
+        if (kv.first == k) e.value = kv.second;
+      if (e.value >= 0) e.ok = parse_go_int(keys[k].values.strs[e.value], &e.num) ? 1 : 0;
+      if (!e.ok) e.num = 0;
+      lbl.push_back(e);
+    }
+    u.lbl_cnt = (int32_t)(lbl.size() - u.lbl_off);
+  }
+  static_dirty_.clear();
+  const size_t b0 = cnt * sizeof(NodeUpdate), b1 = std::max<size_t>(ids.size(), 1) * 4,
+               b2 = std::max<size_t>(lbl.size(), 1) * sizeof(LabelEntry);
+  const size_t o1 = (b0 + 15) & ~size_t(15), o2 = (o1 + b1 + 15) & ~size_t(15), total = o2 + b2;
+  if (upd_dev_.bytes < total) {
+    if (upd_dev_.p) (void)hipFree(upd_dev_.p);
+    upd_dev_.p = nullptr;
+    HIPCHK(hipMalloc(&upd_dev_.p, total * 2));
+    upd_dev_.bytes = total * 2;
+  }
+  std::vector<uint8_t> host(total, 0);
+  std::memcpy(host.data(), rec.data(), b0);
+  if (!ids.empty()) std::memcpy(host.data() + o1, ids.data(), ids.size() * 4);
+  if (!lbl.empty()) std::memcpy(host.data() + o2, lbl.data(), lbl.size() * sizeof(LabelEntry));
+  uint8_t* d = (uint8_t*)upd_dev_.p;
+  HIPCHK(hipMemcpyAsync(d, host.data(), total, hipMemcpyHostToDevice, stream));
+  HIPCHK(launch_node_update(view, (const NodeUpdate*)d, (const uint32_t*)(d + o1), (const LabelEntry*)(d + o2),
+                            (int)cnt, stream));
+  HIPCHK(hipStreamSynchronize(stream));  // the host staging vector dies here
+  return KSG_OK;
 }
 
 int Cluster::upload_node_dynamic(int32_t i) {

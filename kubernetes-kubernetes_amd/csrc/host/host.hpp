@@ -287,6 +287,12 @@ class Cluster {
   hipStream_t stream = nullptr;
   bool layout_dirty = true;
   bool defer_relayout = false;  // ensure_label_slot only marks layout_dirty (pods in flight)
+  std::vector<uint32_t> node_toff_, node_ioff_;  // taint / image CSR offsets as laid out on the device
+  int upload_node_static(int32_t i);  // queue an in-place node update (flushed by ensure_mirror)
+  int flush_node_updates();
+  std::vector<int32_t> static_dirty_;
+  std::vector<uint8_t> static_queued_;
+  DevBuf upd_dev_;
   int ensure_mirror();                       // (re)build device arrays if dirty
   int ensure_label_slot(int32_t key);        // materialise a label column
   int upload_node_dynamic(int32_t idx);      // push one node's Requested/ports to HBM

@@ -297,3 +297,44 @@ def test_pipeline_staging_outgrown_mid_batch(native):
                  "values": [f"node-{(k * 31 + j * 7 + v) % 900:05d}" for v in range(40)]}]}) for j in range(16)])
         pods.append(p.obj())
     _stream(native, nodes, [], pods)
+
+
+# ---- incremental mirror ingestion: Cache.UpdateNode for a node that keeps
+# its snapshot position and its taint / image counts is rewritten in place on the device
+# (Cluster::upload_node_static); other updates take the full re-layout.  Both against the oracle.
+@pytest.mark.parametrize("seed", range(3))
+def test_node_updates_in_place(native, seed):
+    import copy
+    rng, cfg, nodes, existing, names = rand_cluster(900 + seed, n_nodes=[130, 300, 520][seed], n_existing=80)
+    g, o = _pair(native, cfg, nodes, existing)
+    cur = {n["metadata"]["name"]: n for n in nodes}
+    for rnd in range(10):
+        for _ in range(6):
+            nm = rng.choice(names)
+            n = copy.deepcopy(cur[nm])
+            st, md, sp = n["status"], n["metadata"], n.setdefault("spec", {})
+            r = rng.random()
+            if r < 0.3:  # allocatable
+                st["allocatable"]["cpu"] = rng.choice(["1", "4", "8", "16", "2500m"])
+                st["allocatable"]["memory"] = rng.choice(["2Gi", "8Gi", "32Gi"])
+            elif r < 0.45:
+                sp["unschedulable"] = not sp.get("unschedulable", False)
+            elif r < 0.65:  # label values of existing keys (zone kept: same snapshot position)
+                lb = md.setdefault("labels", {})
+                lb["gen"] = str(rng.randint(1, 9))
+                lb["disk"] = rng.choice(["ssd", "hdd", "nvme"])
+            elif r < 0.85 and sp.get("taints"):  # same taint count, other values / effects
+                for t in sp["taints"]:
+                    t["value"] = rng.choice(["", "x", "y", "z"])
+                    t["effect"] = rng.choice(["NoSchedule", "PreferNoSchedule", "NoExecute"])
+            else:  # a layout change: zone moved, or a taint added
+                if rng.random() < 0.5:
+                    md.setdefault("labels", {})["topology.kubernetes.io/zone"] = f"zone-x{rng.randint(0, 2)}"
+                else:
+                    sp.setdefault("taints", []).append({"key": "extra", "value": "", "effect": "PreferNoSchedule"})
+            cur[nm] = n
+            g.update_node(n)
+            o.update_node(n)
+        assert g.node_names() == o.node_names()
+        for q in range(8):
+            _cmp_cycle(g, o, rand_pod(rng, 100 * rnd + q, names), f"seed {seed} round {rnd} pod {q}")
