@@ -235,7 +235,7 @@ def test_sampling_batch_matches_sequential_oracle(native, k):
     cfg = dict(extra, percentageOfNodesToScore=pct)
     g, o = _pair(native, cfg, nodes, existing)
     for rnd in range(2):  # two batches: the host picks the rotation up from the first
-        pods = [rand_pod(rng, 200 * rnd + q, names) for q in range(120)]
+        pods = [rand_pod(rng, 400 * rnd + q, names) for q in range(300)]  # >= 256: the chunked pipeline
         rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
         for q, p in enumerate(pods):
             ro, _ = o.schedule_one(o.compile(p), assume=True)
@@ -338,3 +338,18 @@ def test_node_updates_in_place(native, seed):
         assert g.node_names() == o.node_names()
         for q in range(8):
             _cmp_cycle(g, o, rand_pod(rng, 100 * rnd + q, names), f"seed {seed} round {rnd} pod {q}")
+
+
+@pytest.mark.parametrize("pct", [0, 30])
+def test_sampling_pipelined_batch(native, pct):
+    """Default-plugin pods in 600-pod batches take the chunked pipeline; the device-resident
+    nextStartNodeIndex crosses the chunks (and the launch path replaces the persistent loop)."""
+    from ksg import synth
+    nodes, init, pods = synth.scheduling_basic(700, 100, 1200, hetero=True)
+    g, o = _pair(native, {"percentageOfNodesToScore": pct}, nodes, init)
+    for rnd in range(2):
+        part = pods[600 * rnd:600 * (rnd + 1)]
+        rs = g.schedule_batch([g.compile(p) for p in part], assume=True)
+        for q, p in enumerate(part):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[q].as_tuple() == ro.as_tuple(), f"pct {pct} batch {rnd} pod {q}"
