@@ -1559,8 +1559,6 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
           std::vector<double> late(G, 0.0);
           double wl = 0;
           int wn = 0, cntq = 0;
-          DevResult* hr0 = (DevResult*)((uint8_t*)h_pinned + 0);  // not yet copied: use stamps only
-          (void)hr0;
           for (auto& r : runs)
             for (int q = r.first + 1; q < r.first + r.count; ++q) {
               unsigned long long amin = ~0ull;
