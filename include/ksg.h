@@ -202,6 +202,11 @@ int ksg_shard_range(const ksg_ctx *ctx, int32_t *first_node, int32_t *num_nodes)
 int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
                                 double *bytes_per_launch, int32_t *launches, int32_t *kernel);
 
+/* Parity diagnostic (no device needed): fills out[k] = math.Log(float64(k)) for 0 <= k < n with
+ * the table PodTopologySpread's score kernel reads (topologyNormalizingWeight, podtopologyspread/
+ * scoring.go:287-299: log(size + 2)).  Returns n. */
+int ksg_debug_log_table(double *out, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

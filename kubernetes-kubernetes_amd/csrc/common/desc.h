@@ -332,6 +332,14 @@ struct NodeUpdate {
   int64_t scalar[kMaxScalar];
 };
 struct LabelEntry { int32_t slot, value; int64_t num; int32_t ok, pad; };
+// One node's dynamic columns (NodeInfo.Requested / NonZeroRequested / len(Pods) / UsedPorts)
+// after pod events, flushed in bulk at the next cycle (Cluster::flush_node_dynamic -> k_node_dyn).
+struct NodeDyn {
+  int32_t node, num_pods;
+  int64_t req_cpu, req_mem, req_eph, nz_cpu, nz_mem;
+  int64_t scalar[kMaxScalar];
+  uint32_t ports[kPortSlots];
+};
 
 struct ShardView {
   int32_t world, rank;

@@ -2111,6 +2111,29 @@ hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const ui
   hipLaunchKernelGGL(k_node_update, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, u, ids, lbl, count);
   return hipGetLastError();
 }
+// pod events (NodeInfo.update via AddPod / RemovePod / ForgetPod): one thread per queued node
+// writes its dynamic columns in place
+__global__ __launch_bounds__(kBlock) void k_node_dyn(MirrorView m, const NodeDyn* d, int count) {
+  const int k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= count) return;
+  const NodeDyn& r = d[k];
+  const int i = r.node;
+  if (i < 0 || i >= m.n) return;
+  const size_t cap = (size_t)m.cap;
+  m.req_cpu[i] = r.req_cpu;
+  m.req_mem[i] = r.req_mem;
+  m.req_eph[i] = r.req_eph;
+  m.nz_cpu[i] = r.nz_cpu;
+  m.nz_mem[i] = r.nz_mem;
+  m.num_pods[i] = r.num_pods;
+  for (int q = 0; q < kMaxScalar; ++q) m.scalar_req[(size_t)q * cap + i] = r.scalar[q];
+  for (int q = 0; q < kPortSlots; ++q) m.ports[(size_t)i * kPortSlots + q] = r.ports[q];
+}
+hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, int count, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_node_dyn, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, d, count);
+  return hipGetLastError();
+}
 hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s) {
   const int nb = (m.n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_sample_find, dim3(1), dim3(kBlock), 0, s, m, b, pod, nb);
@@ -2162,7 +2185,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
                       reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
-                      reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_node_update)};
+                      reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_node_update),
+                      reinterpret_cast<const void*>(&k_node_dyn)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
     if (e != hipSuccess) return e;

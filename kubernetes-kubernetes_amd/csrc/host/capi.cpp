@@ -286,4 +286,10 @@ int ksg_last_batch_kernel_stats(const ksg_ctx* ctx, double* avg_kernel_ms, doubl
   return KSG_OK;
 }
 
+int ksg_debug_log_table(double* out, int32_t n) {
+  if (!out || n < 0) return KSG_EINVAL;
+  for (int32_t k = 0; k < n; ++k) out[k] = ksg::go_log((double)k);  // as Cluster::upload_pod_table builds it
+  return n;
+}
+
 }  // extern "C"

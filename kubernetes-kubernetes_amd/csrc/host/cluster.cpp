@@ -1,9 +1,10 @@
 // cluster.cpp -- host cache shadow and the HBM mirror of the snapshot.
 //
 // Mirrors backend/cache/cache.go (AddNode/UpdateNode/RemoveNode :630-695, AddPod/RemovePod
-// :515-597, image states :712-759), NodeInfo.update (framework/types.go:445-468) and the
-// nodeTree zone round-robin order (node_tree.go:52-143).  Node add/remove re-lays the mirror
-// out (the snapshot list is rebuilt then too, cache.go:318-358); pod events touch one node.
+// :515-597, ghost nodes :442-446,666-689, image states :712-759), NodeInfo.update
+// (framework/types.go:445-468), the nodeTree zone round-robin order (node_tree.go:52-143) and
+// UpdateSnapshot's list rule (cache.go:190-296, 318-358).  Node add/remove re-lays the mirror
+// out; node updates are rewritten in place; pod events touch one node.
 #include <algorithm>
 #include <cstring>
 
@@ -12,6 +13,7 @@
 namespace ksg {
 hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const uint32_t* ids, const LabelEntry* lbl,
                               int count, hipStream_t s);
+hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, int count, hipStream_t s);
 
 static const char* zone_key(const NodeSpec& n, std::string* out) {  // node/topology/helpers.go:31-58
   auto get = [&](const char* a, const char* b) -> std::string {
@@ -39,6 +41,7 @@ Cluster::~Cluster() {
   for (auto& b : pt_dev_)
     if (b.p) (void)hipFree(b.p);
   if (upd_dev_.p) (void)hipFree(upd_dev_.p);
+  if (dyn_dev_.p) (void)hipFree(dyn_dev_.p);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -77,7 +80,7 @@ uint32_t Cluster::port_id(std::string ip, std::string proto, int32_t port) {  //
 }
 
 // ---- nodeTree ---------------------------------------------------------------------------------
-void Cluster::tree_add(const NodeSpec& n) {
+void Cluster::tree_add(const NodeSpec& n) {  // node_tree.go:51-67
   std::string z;
   zone_key(n, &z);
   auto it = tree_.find(z);
@@ -86,10 +89,12 @@ void Cluster::tree_add(const NodeSpec& n) {
     tree_[z] = {n.name};
   } else if (std::find(it->second.begin(), it->second.end(), n.name) == it->second.end()) {
     it->second.push_back(n.name);
+  } else {
+    return;  // already in the zone: not added again
   }
-  order_dirty_ = true;
+  ++tree_nodes_;
 }
-void Cluster::tree_remove(const NodeSpec& n) {
+void Cluster::tree_remove(const NodeSpec& n) {  // node_tree.go:70-99
   std::string z;
   zone_key(n, &z);
   auto it = tree_.find(z);
@@ -102,10 +107,29 @@ void Cluster::tree_remove(const NodeSpec& n) {
     tree_.erase(it);
     zones_.erase(std::find(zones_.begin(), zones_.end(), z));
   }
-  order_dirty_ = true;
+  --tree_nodes_;
 }
+
+// UpdateSnapshot's list rule (cache.go:223-290): nodeInfoList is re-created from nodeTree.list
+// only when a node changed since the last snapshot is new to the snapshot's map
+// (updateAllLists, :228-234), or when the map holds more names than the tree (deleted nodes,
+// :270-273).  Any other change -- a node moving to another zone included -- keeps every node at
+// its list position (the list holds pointers into the map, updated in place, :257-259).
 const std::vector<std::string>& Cluster::order() {
-  if (order_dirty_) {
+  bool rebuild = false;
+  for (auto& nm : snap_new_) {
+    auto it = nodes_.find(nm);
+    if (it != nodes_.end() && it->second->real && snap_names_.insert(nm).second) rebuild = true;
+  }
+  snap_new_.clear();
+  if (!snap_gone_.empty()) {  // removeDeletedNodesFromSnapshot (cache.go:361-372)
+    for (auto& nm : snap_gone_) {
+      auto it = nodes_.find(nm);
+      if ((it == nodes_.end() || !it->second->real) && snap_names_.erase(nm)) rebuild = true;
+    }
+    snap_gone_.clear();
+  }
+  if (rebuild) {  // updateNodeInfoSnapshotList(updateAll=true) over nodeTree.list (node_tree.go:119-143)
     order_.clear();
     size_t longest = 0;
     for (auto& z : zones_) longest = std::max(longest, tree_[z].size());
@@ -116,7 +140,6 @@ const std::vector<std::string>& Cluster::order() {
       }
     index_.clear();
     for (size_t i = 0; i < order_.size(); ++i) index_[order_[i]] = (int32_t)i;
-    order_dirty_ = false;
     layout_dirty = true;
   }
   return order_;
@@ -199,57 +222,80 @@ void Cluster::intern_node(NodeRec& r) {
   for (int64_t v : {r.alloc_cpu, r.alloc_mem}) alloc_bound = std::max(alloc_bound, v < 0 ? INT64_MAX : v);
 }
 
+void Cluster::set_node(NodeRec& r, NodeSpec&& n) {  // addNodeImageStates + NodeInfo.SetNode
+  add_images(n);
+  r.spec = std::move(n);
+  r.real = true;
+  intern_node(r);
+}
+
+// Cache.AddNode (cache.go:630-646).  A node the cache already holds as a ghost (pods that arrived
+// first, or a removed node whose pods remain) gets its Node object back, keeping those pods.
+// An AddNode for a node the cache holds with its Node object is taken as UpdateNode: upstream
+// would append the name to a second zone list if the zone changed (nodeTree.addNode does not
+// look in other zones), which the informer never asks for.
 int Cluster::add_node(NodeSpec&& n) {
   auto it = nodes_.find(n.name);
-  if (it != nodes_.end()) return update_node(std::move(n));
-  auto rec = std::make_unique<NodeRec>();
-  rec->spec = std::move(n);
-  tree_add(rec->spec);
-  add_images(rec->spec);
-  intern_node(*rec);
-  nodes_[rec->spec.name] = std::move(rec);
-  layout_dirty = true;
+  if (it != nodes_.end() && it->second->real) return update_node(std::move(n));
+  NodeRec* r;
+  if (it == nodes_.end()) {
+    auto rec = std::make_unique<NodeRec>();
+    r = rec.get();
+    nodes_[n.name] = std::move(rec);
+  } else {
+    r = it->second.get();
+  }
+  const std::string name = n.name;
+  tree_add(n);
+  set_node(*r, std::move(n));
+  snap_new_.insert(name);
+  snap_gone_.erase(name);
+  layout_dirty = true;  // the row appears (or returns with the ghost's pods)
+  // a ghost's pods join the pod table's node index at the next ensure_mirror
   return KSG_OK;
 }
 
+// Cache.UpdateNode (cache.go:648-664): nodeTree.updateNode moves the node between zone lists, but
+// the snapshot list keeps its position until the next rebuild (order()), so the mirror row is
+// rewritten in place whenever its taint / image CSR ranges keep their sizes.
 int Cluster::update_node(NodeSpec&& n) {
   auto it = nodes_.find(n.name);
-  if (it == nodes_.end()) return add_node(std::move(n));
+  if (it == nodes_.end() || !it->second->real) return add_node(std::move(n));
   NodeRec& r = *it->second;
   remove_images(r.spec);
   std::string z0, z1;
   zone_key(r.spec, &z0);
   zone_key(n, &z1);
-  if (z0 != z1) {
+  if (z0 != z1) {  // node_tree.go:102-115
     tree_remove(r.spec);
     tree_add(n);
   }
   const size_t nt0 = r.taint_ids.size(), ni0 = r.image_ids.size();
-  add_images(n);
-  r.spec = std::move(n);
-  intern_node(r);
-  // NodeInfo.SetNode (cache.go UpdateNode): a node that keeps its snapshot position (same zone)
-  // and its taint / image counts (same CSR ranges) is rewritten in place on the device; anything
-  // else (and a new extended resource or label column) takes the full re-layout
-  if (!layout_dirty && z0 == z1 && r.taint_ids.size() == nt0 && r.image_ids.size() == ni0)
+  set_node(r, std::move(n));
+  if (!layout_dirty && r.taint_ids.size() == nt0 && r.image_ids.size() == ni0)
     return upload_node_static(index_of(r.spec.name));
   layout_dirty = true;
   return KSG_OK;
 }
 
+// Cache.RemoveNode (cache.go:672-695): the node leaves the tree and the image states; while pods
+// remain on it, it stays in the cache as a ghost with their requests (their delete events may
+// still be on the way), skipped by snapshots and by the pod table's aggregation.
 int Cluster::remove_node(const std::string& name) {
   auto it = nodes_.find(name);
-  if (it == nodes_.end()) { err = "unknown node " + name; return KSG_ENOTFOUND; }
-  remove_images(it->second->spec);
-  tree_remove(it->second->spec);
-  for (auto& uid : it->second->pods) {
+  if (it == nodes_.end() || !it->second->real) { err = "node " + name + " is not found"; return KSG_ENOTFOUND; }
+  NodeRec& r = *it->second;
+  remove_images(r.spec);
+  tree_remove(r.spec);
+  r.real = false;
+  for (auto& uid : r.pods) {  // leave the aggregation (not in any snapshot list any more)
     auto pt = pods.find(uid);
-    if (pt == pods.end()) continue;
-    pods_with_affinity -= pt->second.with_affinity ? 1 : 0;
-    pod_table_drop(pt->second.slot);
-    pods.erase(pt);
+    if (pt != pods.end() && pt->second.slot >= 0) pt_node[pt->second.slot] = -1;
   }
-  nodes_.erase(it);
+  pods_dirty = true;
+  if (r.pods.empty()) nodes_.erase(it);  // removeNodeInfoFromList
+  snap_gone_.insert(name);
+  snap_new_.erase(name);
   layout_dirty = true;
   return KSG_OK;
 }
@@ -271,7 +317,8 @@ void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo
   }
 }
 
-// node_override: the node an assumed pod was placed on (the spec itself is left unbound)
+// Cache.addPod (cache.go:437-466).  node_override: the node an assumed pod was placed on (the spec
+// itself is left unbound).  A pod whose node the cache does not hold creates a ghost NodeInfo.
 int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool device_done, int32_t slot,
                      const std::string* node_override, const PodResources* res) {
   const std::string uid = uid_override.empty() ? p.uid : uid_override;
@@ -279,7 +326,13 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   if (node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
   if (pods.count(uid)) { err = "pod " + uid + " exists"; return KSG_EEXIST; }
   NodeRec* r = node(node_name);
-  if (!r) { err = "unknown node " + node_name; return KSG_ENOTFOUND; }
+  if (!r) {
+    auto rec = std::make_unique<NodeRec>();
+    rec->spec.name = node_name;
+    rec->real = false;
+    r = rec.get();
+    nodes_[node_name] = std::move(rec);
+  }
   BoundPod bp;
   bp.uid = uid;
   bp.node = node_name;
@@ -295,22 +348,24 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   for (auto& c : p.containers) take(c);
   apply_pod(*r, bp, +1);
   r->pods.push_back(uid);
-  order();
   // pod_table_put may materialise label columns (and relayout the mirror), so the node index is
   // taken afterwards; while the layout is dirty it is re-derived by the next ensure_mirror
   bp.slot = slot >= 0 ? slot : pod_table_put(p, -1);
-  pt_node[bp.slot] = layout_dirty ? -1 : index_of(r->spec.name);
+  const int32_t ix = r->real ? index_of(node_name) : -1;
+  pt_node[bp.slot] = layout_dirty ? -1 : ix;
   pods.emplace(uid, std::move(bp));
-  if (!layout_dirty && !device_done) return upload_node_dynamic(index_of(r->spec.name));
+  if (!layout_dirty && !device_done) return upload_node_dynamic(ix);
   return KSG_OK;
 }
 
+// Cache.removePod (cache.go:480-513): a ghost node goes once its last pod has gone
 int Cluster::remove_pod(const std::string& uid) {
   auto it = pods.find(uid);
   if (it == pods.end()) { err = "unknown pod " + uid; return KSG_ENOTFOUND; }
   NodeRec* r = node(it->second.node);
   pods_with_affinity -= it->second.with_affinity ? 1 : 0;
   pod_table_drop(it->second.slot);
+  int32_t ix = -1;
   if (r) {
     apply_pod(*r, it->second, -1);
     auto& v = r->pods;
@@ -319,10 +374,11 @@ int Cluster::remove_pod(const std::string& uid) {
       *jt = v.back();
       v.pop_back();
     }
+    if (r->real) ix = index_of(r->spec.name);
+    else if (v.empty()) nodes_.erase(it->second.node);
   }
   pods.erase(it);
-  order();
-  if (r && !layout_dirty) return upload_node_dynamic(index_of(r->spec.name));
+  if (!layout_dirty) return upload_node_dynamic(ix);
   return KSG_OK;
 }
 
@@ -339,12 +395,16 @@ int Cluster::remove_pod(const std::string& uid) {
 int Cluster::ensure_mirror() {
   order();
   if (!layout_dirty) {
-    const int rc = flush_node_updates();
+    int rc = flush_node_updates();
+    if (!rc) rc = flush_node_dynamic();
     return rc ? rc : upload_pod_table();
   }
   for (int32_t i : static_dirty_)  // the re-layout below uploads every node
     if ((size_t)i < static_queued_.size()) static_queued_[i] = 0;
   static_dirty_.clear();
+  for (int32_t i : dyn_dirty_)
+    if ((size_t)i < dyn_queued_.size()) dyn_queued_[i] = 0;
+  dyn_dirty_.clear();
   HIPCHK(hipStreamSynchronize(stream));
   free_all();
   const int32_t n = (int32_t)order_.size();
@@ -449,8 +509,11 @@ int Cluster::ensure_mirror() {
       if (rc) return rc;
     }
   // snapshot indices moved: re-derive every pod's node index in the pod table
-  for (auto& kv : pods)
-    if (kv.second.slot >= 0) pt_node[kv.second.slot] = index_of(kv.second.node);
+  for (auto& kv : pods)  // (pods on ghost nodes stay out of the aggregation)
+    if (kv.second.slot >= 0) {
+      const NodeRec* r = node(kv.second.node);
+      pt_node[kv.second.slot] = r && r->real ? index_of(kv.second.node) : -1;
+    }
   pods_dirty = true;
   return upload_pod_table();
 }
@@ -574,29 +637,60 @@ int Cluster::flush_node_updates() {
   return KSG_OK;
 }
 
+// A node's dynamic columns (NodeInfo.Requested / NonZeroRequested / len(Pods) / UsedPorts) after a
+// pod event are queued like the static ones and go up at the next cycle as one H2D of NodeDyn
+// records + one k_node_dyn launch (a cache fed thousands of pod events between cycles pays one
+// copy, not ~25 per event).
 int Cluster::upload_node_dynamic(int32_t i) {
   if (i < 0 || layout_dirty) return KSG_OK;
-  const NodeRec& r = *nodes_[order_[i]];
-  const int32_t cap = view.cap;
-  HIPCHK(hipMemcpyAsync(view.req_cpu + i, &r.req_cpu, 8, hipMemcpyHostToDevice, stream));
-  HIPCHK(hipMemcpyAsync(view.req_mem + i, &r.req_mem, 8, hipMemcpyHostToDevice, stream));
-  HIPCHK(hipMemcpyAsync(view.req_eph + i, &r.req_eph, 8, hipMemcpyHostToDevice, stream));
-  HIPCHK(hipMemcpyAsync(view.nz_cpu + i, &r.nz_cpu, 8, hipMemcpyHostToDevice, stream));
-  HIPCHK(hipMemcpyAsync(view.nz_mem + i, &r.nz_mem, 8, hipMemcpyHostToDevice, stream));
-  HIPCHK(hipMemcpyAsync(view.num_pods + i, &r.num_pods, 4, hipMemcpyHostToDevice, stream));
-  int64_t sv[kMaxScalar];
-  for (int s = 0; s < kMaxScalar; ++s) {
-    auto it = r.scalar_req.find(s);
-    sv[s] = it == r.scalar_req.end() ? 0 : it->second;
-    HIPCHK(hipMemcpyAsync(view.scalar_req + (size_t)s * cap + i, &sv[s], 8, hipMemcpyHostToDevice, stream));
+  if (dyn_queued_.size() < (size_t)view.n) dyn_queued_.resize((size_t)view.n, 0);
+  if (!dyn_queued_[i]) {
+    dyn_queued_[i] = 1;
+    dyn_dirty_.push_back(i);
   }
-  if (r.ports.size() > (size_t)kPortSlots) { err = "too many host ports on node"; return KSG_ENOTSUP; }
-  uint32_t slots[kPortSlots];
-  for (int q = 0; q < kPortSlots; ++q) slots[q] = 0xffffffffu;
-  int q = 0;
-  for (uint32_t p : r.ports) slots[q++] = p;
-  HIPCHK(hipMemcpyAsync(view.ports + (size_t)i * kPortSlots, slots, sizeof(slots), hipMemcpyHostToDevice, stream));
-  HIPCHK(hipStreamSynchronize(stream));
+  return KSG_OK;
+}
+
+int Cluster::flush_node_dynamic() {
+  if (dyn_dirty_.empty()) return KSG_OK;
+  const size_t cnt = dyn_dirty_.size();
+  std::vector<NodeDyn> rec(cnt);
+  for (size_t q = 0; q < cnt; ++q) {
+    const int32_t i = dyn_dirty_[q];
+    dyn_queued_[i] = 0;
+    const NodeRec& r = *nodes_[order_[i]];
+    if (r.ports.size() > (size_t)kPortSlots) {
+      err = "node " + r.spec.name + " uses more host ports than supported";
+      layout_dirty = true;  // the next cycle re-lays out (and reports the same)
+      dyn_dirty_.clear();
+      return KSG_ENOTSUP;
+    }
+    NodeDyn& d = rec[q];
+    std::memset(&d, 0, sizeof(d));
+    d.node = i;
+    d.num_pods = r.num_pods;
+    d.req_cpu = r.req_cpu;
+    d.req_mem = r.req_mem;
+    d.req_eph = r.req_eph;
+    d.nz_cpu = r.nz_cpu;
+    d.nz_mem = r.nz_mem;
+    for (auto& kv : r.scalar_req) d.scalar[kv.first] = kv.second;
+    for (int q2 = 0; q2 < kPortSlots; ++q2) d.ports[q2] = 0xffffffffu;
+    int k = 0;
+    for (uint32_t p : r.ports) d.ports[k++] = p;
+  }
+  dyn_dirty_.clear();
+  const size_t bytes = cnt * sizeof(NodeDyn);
+  if (dyn_dev_.bytes < bytes) {
+    if (dyn_dev_.p) (void)hipFree(dyn_dev_.p);
+    dyn_dev_.p = nullptr;
+    dyn_dev_.bytes = 0;
+    HIPCHK(hipMalloc(&dyn_dev_.p, bytes * 2));
+    dyn_dev_.bytes = bytes * 2;
+  }
+  HIPCHK(hipMemcpyAsync(dyn_dev_.p, rec.data(), bytes, hipMemcpyHostToDevice, stream));
+  HIPCHK(launch_node_dyn(view, (const NodeDyn*)dyn_dev_.p, (int)cnt, stream));
+  HIPCHK(hipStreamSynchronize(stream));  // the host records die here
   return KSG_OK;
 }
 

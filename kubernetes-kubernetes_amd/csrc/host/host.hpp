@@ -17,6 +17,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../common/desc.h"
@@ -118,6 +119,7 @@ struct PodResources {
 };
 ResVec pod_requests(const PodSpec& p, const ResVec* non_missing);
 PodResources calc_resources(const PodSpec& p);
+double go_log(double x);  // Go's math.Log (podtable.cpp)
 bool tolerates(const Tol& t, const std::string& key, const std::string& value, const std::string& effect,
                bool cmp_ops);
 
@@ -206,6 +208,9 @@ struct NodeRec {
   std::map<int32_t, int64_t> scalar_req;
   std::set<uint32_t> ports;
   std::vector<std::string> pods;  // uids in NodeInfo.Pods order
+  // false: a ghost NodeInfo (cache.go:442-446, 672-689) -- pods arrived before their node, or the
+  // node was removed while pods remained; it holds their requests but is skipped by snapshots
+  bool real = true;
 };
 
 struct TaintRec { std::string key, value, effect; };
@@ -238,7 +243,9 @@ class Cluster {
   int remove_pod(const std::string& uid);
   int32_t pods_with_affinity = 0;
 
-  // snapshot order (nodeTree.list)
+  // UpdateSnapshot (cache.go:190-296): the snapshot's nodeInfoList order, rebuilt from
+  // nodeTree.list only when a node new to the snapshot appears or one is gone; called at the start
+  // of every scheduling cycle (and by the node listing)
   const std::vector<std::string>& order();
   int32_t index_of(const std::string& node) const;
   NodeRec* node(const std::string& name);
@@ -295,7 +302,11 @@ class Cluster {
   DevBuf upd_dev_;
   int ensure_mirror();                       // (re)build device arrays if dirty
   int ensure_label_slot(int32_t key);        // materialise a label column
-  int upload_node_dynamic(int32_t idx);      // push one node's Requested/ports to HBM
+  int upload_node_dynamic(int32_t idx);      // queue one node's Requested/ports (flushed by ensure_mirror)
+  int flush_node_dynamic();
+  std::vector<int32_t> dyn_dirty_;
+  std::vector<uint8_t> dyn_queued_;
+  DevBuf dyn_dev_;
   int64_t next_start = 0;                    // Scheduler.nextStartNodeIndex
   double taint_ids_per_node = 0, img_ids_per_node = 0;  // CSR densities (algorithmic-bytes model)
   int64_t taint_max_per_node = 0;                        // bounds k_sched_loop's raw-score granules
@@ -305,9 +316,12 @@ class Cluster {
   std::vector<std::string> zones_;
   std::map<std::string, std::vector<std::string>> tree_;
   std::unordered_map<std::string, std::unique_ptr<NodeRec>> nodes_;
-  std::vector<std::string> order_;
+  std::vector<std::string> order_;  // snapshot.nodeInfoList (names)
   std::unordered_map<std::string, int32_t> index_;
-  bool order_dirty_ = true;
+  // snapshot.nodeInfoMap's names, and the events since the last UpdateSnapshot that can make it
+  // rebuild the list: names added (maybe new to the map) and names removed (maybe still in it)
+  std::unordered_set<std::string> snap_names_, snap_new_, snap_gone_;
+  int32_t tree_nodes_ = 0;  // nodeTree.numNodes
   int32_t slots_used_ = 0, slots_cap_ = 0;
   std::vector<DevBuf> bufs_;
   DevBuf pt_dev_[9];  // pod table / term table device arrays (own lifetime, grown geometrically)
@@ -315,6 +329,7 @@ class Cluster {
 
   void tree_add(const NodeSpec& n);
   void tree_remove(const NodeSpec& n);
+  void set_node(NodeRec& r, NodeSpec&& n);  // NodeInfo.SetNode + image states
   void intern_node(NodeRec& r);
   void add_images(const NodeSpec& n);
   void remove_images(const NodeSpec& n);

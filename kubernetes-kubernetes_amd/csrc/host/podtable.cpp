@@ -181,7 +181,7 @@ int Cluster::grow(DevBuf& b, size_t bytes) {
 // Go's math.Log (math/log.go: the FreeBSD e_log.c reduction and polynomial), evaluated without
 // fused multiply-adds (objects are built with -ffp-contract=off) -- the weights
 // PodTopologySpread multiplies domain counts by (scoring.go:287-299).
-static double go_log(double x) {
+double go_log(double x) {
   const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
   const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
                L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,

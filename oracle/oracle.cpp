@@ -261,6 +261,7 @@ using HostPorts = std::map<std::string, std::set<std::pair<std::string, int32_t>
 
 struct NodeInfoO {  // framework.NodeInfo (framework/types.go:172-220)
   int pos = -1;  // index in the snapshot list (set by rebuild_list; the result's node index)
+  bool hasNode = false;  // Node() != nil; false: a ghost (cache.go:442-446, 666-689)
   Node node;
   std::vector<PodInfo*> pods;
   std::vector<PodInfo*> podsWithAffinity, podsWithRequiredAntiAffinity;
@@ -447,15 +448,39 @@ struct ksgo_ctx {
   std::map<std::string, ImageState> imageStates;  // cache.imageStates
   std::map<std::string, std::unique_ptr<PodInfo>> pods;  // bound/assumed pods by uid
   std::vector<NodeInfoO*> list;  // snapshot nodeInfoList order
-  bool listDirty = true;
+  std::set<std::string> snapMap;  // snapshot.nodeInfoMap's names
+  std::vector<std::string> changed;  // nodes given a Node object since the last snapshot
+  int numNodes = 0;                  // nodeTree.numNodes
   int64_t nextStartNodeIndex = 0;
   uint64_t assumeSeq = 0;
   std::map<int32_t, std::unique_ptr<Pod>> queue;  // compiled pods
   int32_t nextHandle = 1;
   std::map<int32_t, std::string> assumedUid;  // handle -> assumed pod uid
 
-  void rebuild_list() {  // nodeTree.list (node_tree.go:119-143) -> updateNodeInfoSnapshotList
-    if (!listDirty) return;
+  // UpdateSnapshot (backend/cache/cache.go:190-296), its list part.  A NodeInfo object stays alive
+  // while its name is in snapMap (the snapshot owns copies upstream; here the list points at the
+  // cache's objects, so a removed node's object lives until the snapshot drops it).
+  void rebuild_list() {
+    bool updateAll = false;
+    for (auto& nm : changed) {  // the generation walk (:223-261): a node new to the map
+      auto it = nodes.find(nm);
+      if (it != nodes.end() && it->second->hasNode && snapMap.insert(nm).second) updateAll = true;
+    }
+    changed.clear();
+    if ((int)snapMap.size() > numNodes) {  // removeDeletedNodesFromSnapshot (:270-273, 361-372)
+      for (auto it = snapMap.begin(); it != snapMap.end();) {
+        auto n = nodes.find(*it);
+        if (n == nodes.end() || !n->second->hasNode) {
+          if (n != nodes.end() && n->second->pods.empty()) nodes.erase(n);  // removeNodeInfoFromList
+          it = snapMap.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      updateAll = true;
+    }
+    if (!updateAll) return;
+    // updateNodeInfoSnapshotList(updateAll) (:318-345) over nodeTree.list (node_tree.go:119-143)
     list.clear();
     size_t maxLen = 0;
     for (auto& z : zones) maxLen = std::max(maxLen, tree[z].size());
@@ -465,7 +490,12 @@ struct ksgo_ctx {
         if (idx < na.size()) list.push_back(nodes[na[idx]].get());
       }
     for (size_t i = 0; i < list.size(); ++i) list[i]->pos = (int)i;
-    listDirty = false;
+  }
+  // a node object with neither Node nor pods leaves the cache (cache.go:493-494, 685-686) unless
+  // the snapshot still lists it
+  void maybe_drop(const std::string& name) {
+    auto it = nodes.find(name);
+    if (it != nodes.end() && !it->second->hasNode && it->second->pods.empty() && !snapMap.count(name)) nodes.erase(it);
   }
   const Labels* ns_labels(const std::string& ns) const {  // GetNamespaceLabelsSnapshot (ipa plugin.go:150-159)
     auto it = namespaces.find(ns);
@@ -1528,6 +1558,7 @@ static void tree_add(ksgo_ctx* c, const Node& n) {  // node_tree.go:52-70
       if (nm == n.name) return;
     it->second.push_back(n.name);
   }
+  c->numNodes++;
 }
 static void tree_remove(ksgo_ctx* c, const Node& n) {  // node_tree.go:73-98
   std::string z = get_zone_key(n);
@@ -1541,11 +1572,16 @@ static void tree_remove(ksgo_ctx* c, const Node& n) {  // node_tree.go:73-98
         c->tree.erase(it);
         c->zones.erase(std::find(c->zones.begin(), c->zones.end(), z));
       }
+      c->numNodes--;
       return;
     }
 }
 
-int ksgo_add_node(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:630-646
+// Cache.AddNode (cache.go:630-646).  An AddNode for a node the cache holds with its Node object is
+// taken as UpdateNode (as the product does): upstream would append the name to a second zone list
+// when the zone changed, which the informer never asks for.
+int ksgo_update_node(ksgo_ctx* c, const char* json, size_t len);
+int ksgo_add_node(ksgo_ctx* c, const char* json, size_t len) {
   try {
     Node n;
     if (!decode_node(mj::parse(json, len), &n, &c->err)) return KSG_EINVAL;
@@ -1555,55 +1591,58 @@ int ksgo_add_node(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:630-
       auto up = std::make_unique<NodeInfoO>();
       ni = up.get();
       c->nodes[n.name] = std::move(up);
+    } else if (it->second->hasNode) {
+      return ksgo_update_node(c, json, len);
     } else {
-      ni = it->second.get();
-      remove_node_images(c, ni->node);
+      ni = it->second.get();  // a ghost: removeNodeImageStates(nil) is a no-op
     }
     tree_add(c, n);
     add_node_images(c, n);
     ni->node = n;
+    ni->hasNode = true;
     ni->allocatable = node_allocatable(n);
-    c->listDirty = true;
+    c->changed.push_back(n.name);
     return KSG_OK;
   } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
 }
 
-int ksgo_update_node(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:648-670
+int ksgo_update_node(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:648-664
   try {
     Node n;
     if (!decode_node(mj::parse(json, len), &n, &c->err)) return KSG_EINVAL;
     auto it = c->nodes.find(n.name);
-    if (it == c->nodes.end()) return ksgo_add_node(c, json, len);
+    if (it == c->nodes.end() || !it->second->hasNode) return ksgo_add_node(c, json, len);
     NodeInfoO* ni = it->second.get();
     remove_node_images(c, ni->node);
-    if (get_zone_key(ni->node) != get_zone_key(n)) { tree_remove(c, ni->node); tree_add(c, n); }
+    if (get_zone_key(ni->node) != get_zone_key(n)) { tree_remove(c, ni->node); tree_add(c, n); }  // node_tree.go:102-115
     add_node_images(c, n);
     ni->node = n;
     ni->allocatable = node_allocatable(n);
-    c->listDirty = true;
+    c->changed.push_back(n.name);
     return KSG_OK;
   } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
 }
 
 int ksgo_remove_node(ksgo_ctx* c, const char* name) {  // cache.go:672-695
   auto it = c->nodes.find(name);
-  if (it == c->nodes.end()) return KSG_ENOTFOUND;
-  remove_node_images(c, it->second->node);
-  tree_remove(c, it->second->node);
-  for (auto* p : it->second->pods) c->pods.erase(p->pod.uid);
-  c->nodes.erase(it);
-  c->listDirty = true;
+  if (it == c->nodes.end() || !it->second->hasNode) { c->err = "node not found"; return KSG_ENOTFOUND; }
+  NodeInfoO* ni = it->second.get();
+  tree_remove(c, ni->node);
+  remove_node_images(c, ni->node);
+  ni->hasNode = false;  // n.info.RemoveNode(); the pods stay until their delete events
+  c->maybe_drop(name);
   return KSG_OK;
 }
 
-int ksgo_add_pod(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:515-545 addPod
+int ksgo_add_pod(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:437-466 addPod
   try {
     Pod p;
     if (!decode_pod(mj::parse(json, len), &p, &c->err)) return KSG_EINVAL;
     if (p.nodeName.empty()) { c->err = "pod is not bound"; return KSG_EINVAL; }
     if (c->pods.count(p.uid)) { c->err = "pod exists"; return KSG_EEXIST; }
     auto it = c->nodes.find(p.nodeName);
-    if (it == c->nodes.end()) { c->err = "unknown node " + p.nodeName; return KSG_ENOTFOUND; }
+    if (it == c->nodes.end())  // a ghost NodeInfo (cache.go:442-446)
+      it = c->nodes.emplace(p.nodeName, std::make_unique<NodeInfoO>()).first;
     auto pi = std::make_unique<PodInfo>();
     new_pod_info(p, pi.get());
     node_add_pod(*it->second, pi.get());
@@ -1612,12 +1651,14 @@ int ksgo_add_pod(ksgo_ctx* c, const char* json, size_t len) {  // cache.go:515-5
   } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
 }
 
-int ksgo_remove_pod(ksgo_ctx* c, const char* uid) {
+int ksgo_remove_pod(ksgo_ctx* c, const char* uid) {  // cache.go:480-513 removePod
   auto it = c->pods.find(uid);
   if (it == c->pods.end()) return KSG_ENOTFOUND;
-  auto nt = c->nodes.find(it->second->pod.nodeName);
+  const std::string node = it->second->pod.nodeName;
+  auto nt = c->nodes.find(node);
   if (nt != c->nodes.end()) node_remove_pod(*nt->second, uid);
   c->pods.erase(it);
+  c->maybe_drop(node);
   return KSG_OK;
 }
 

@@ -49,6 +49,10 @@ def run_case(make_backend, case):
             return []
         return ["config accepted but the reference rejects it"]
     b = build(make_backend, case)
+    if case["kind"] == "events":
+        errs = run_events_case(b, case)
+        b.close()
+        return errs
     names = b.node_names()
     if case["kind"] == "sequence":
         errs = run_sequence_case(b, case, names)
@@ -126,4 +130,37 @@ def run_sequence_case(b, case, names):
             errs.append(f"step {i}: feasible {r.feasible_nodes} != {e['feasible']}")
         if "evaluated" in e and r.evaluated_nodes != e["evaluated"]:
             errs.append(f"step {i}: evaluated {r.evaluated_nodes} != {e['evaluated']}")
+    return errs
+
+
+def run_events_case(b, case):
+    """Cache events (informer / assume feed) with UpdateSnapshot steps: each "snapshot" op takes a
+    snapshot (the node listing does, as a scheduling cycle would) and checks its node order."""
+    errs = []
+    for i, op in enumerate(case["ops"]):
+        kind = op["op"]
+        if kind == "snapshot":
+            got = b.node_names()
+            if "want" in op and got != op["want"]:
+                errs.append(f"op {i}: snapshot {got} != {op['want']}")
+            continue
+        try:
+            if kind == "add_node":
+                b.add_node(op["node"])
+            elif kind == "update_node":
+                b.update_node(op["node"])
+            elif kind == "remove_node":
+                b.remove_node(op["name"])
+            elif kind == "add_pod":
+                b.add_pod(op["pod"])
+            elif kind == "remove_pod":
+                b.remove_pod(op["uid"])
+            else:
+                errs.append(f"op {i}: unknown op {kind}")
+                continue
+            if op.get("error"):
+                errs.append(f"op {i}: {kind} succeeded, the reference returns an error")
+        except KsgError as e:
+            if not op.get("error"):
+                errs.append(f"op {i}: {kind} failed: {e}")
     return errs

@@ -82,3 +82,21 @@ def test_no_kernel_uses_scratch(tmp_path):
     assert any("k_sched_loop" in k for k in kernels)
     used = {k: s for k, s in zip(kernels, sizes) if s}
     assert not used, used
+
+
+def test_log_table_matches_oracle_go_log_bit_for_bit():
+    """The table PodTopologySpread scores read on the device (Cluster::log_tab) against the
+    oracle's math.Log restatement, for every log(size + 2) a 100k-node cluster can need
+    (podtopologyspread/scoring.go:287-299).  Both are independent copies of Go's math/log.go."""
+    import struct
+
+    from oracle_binding import load as load_oracle
+    n = 100005
+    lib = C.CDLL(_ensure_built())
+    lib.ksg_debug_log_table.argtypes = [C.POINTER(C.c_double), C.c_int32]
+    buf = (C.c_double * n)()
+    assert lib.ksg_debug_log_table(buf, n) == n
+    ora = load_oracle()
+    bad = [k for k in range(2, n)
+           if struct.pack("<d", buf[k]) != struct.pack("<d", ora.ksgo_go_log(float(k)))]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"

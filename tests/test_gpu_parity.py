@@ -340,6 +340,84 @@ def test_node_updates_in_place(native, seed):
             _cmp_cycle(g, o, rand_pod(rng, 100 * rnd + q, names), f"seed {seed} round {rnd} pod {q}")
 
 
+# ---- cache churn: UpdateSnapshot keeps the snapshot list across zone
+# moves until a node is added or removed (cache.go:223-290); ghost NodeInfos hold the pods of nodes
+# that are not (or no longer) there (cache.go:442-446, 666-689).  Random event streams between
+# scheduling cycles and batches, against the oracle (which restates the same cache rules).
+@pytest.mark.parametrize("seed", range(4))
+def test_cache_churn_matches_oracle(native, seed):
+    import copy
+    from fuzz_gen import rand_node
+    rng, cfg, nodes, existing, names = rand_cluster(4400 + seed, n_nodes=[90, 260, 300, 700][seed], n_existing=50)
+    g, o = _pair(native, cfg, nodes, existing)
+    live = {n["metadata"]["name"]: n for n in nodes}
+    gone = {}   # removed nodes (their pods may still be in the cache: ghosts)
+    pods_on = {}  # uid -> node of the extra bound pods this test adds
+    nxt = 10000
+    both = (g, o)
+    for rnd in range(12):
+        for _ in range(rng.randint(2, 7)):
+            r = rng.random()
+            if r < 0.3 and live:  # zone move (or label change) of a live node
+                nm = rng.choice(sorted(live))
+                n = copy.deepcopy(live[nm])
+                n["metadata"].setdefault("labels", {})["topology.kubernetes.io/zone"] = rng.choice(
+                    ["zone-a", "zone-b", "zone-c", "zone-d"])
+                live[nm] = n
+                for b in both:
+                    b.update_node(n)
+            elif r < 0.45:  # a new node
+                n = rand_node(rng, nxt)
+                nxt += 1
+                live[n["metadata"]["name"]] = n
+                for b in both:
+                    b.add_node(n)
+            elif r < 0.6 and len(live) > 5:  # a node removed (its pods stay: a ghost)
+                nm = rng.choice(sorted(live))
+                gone[nm] = live.pop(nm)
+                for b in both:
+                    b.remove_node(nm)
+            elif r < 0.7 and gone:  # a removed node comes back (maybe in another zone)
+                nm = rng.choice(sorted(gone))
+                n = copy.deepcopy(gone.pop(nm))
+                n["metadata"].setdefault("labels", {})["topology.kubernetes.io/zone"] = rng.choice(["zone-a", "zone-e"])
+                live[nm] = n
+                for b in both:
+                    b.add_node(n)
+            elif r < 0.85:  # a bound pod, sometimes on a node the cache does not know (yet)
+                p = rand_pod(rng, 50000 + nxt, names, topology=True)
+                nxt += 1
+                p["spec"].get("affinity", {}).pop("nodeAffinity", None)
+                target = rng.choice(sorted(live) + sorted(gone) + [f"future-{rng.randint(0, 3)}"])
+                p["spec"]["nodeName"] = target
+                pods_on[p["metadata"]["uid"]] = target
+                for b in both:
+                    b.add_pod(p)
+            elif pods_on:  # a pod delete event
+                uid = rng.choice(sorted(pods_on))
+                del pods_on[uid]
+                for b in both:
+                    b.remove_pod(uid)
+        if rng.random() < 0.3:  # a "future" node arrives: its ghost pods join it
+            nm = f"future-{rng.randint(0, 3)}"
+            if nm not in live:
+                n = rand_node(rng, 0)
+                n["metadata"]["name"] = nm
+                n["metadata"]["labels"]["kubernetes.io/hostname"] = nm
+                live[nm] = n
+                gone.pop(nm, None)
+                for b in both:
+                    b.add_node(n)
+        assert g.node_names() == o.node_names(), f"seed {seed} round {rnd}: snapshot order"
+        for q in range(4):
+            _cmp_cycle(g, o, rand_pod(rng, 100 * rnd + q, sorted(live)), f"seed {seed} round {rnd} pod {q}")
+        batch = [rand_pod(rng, 7000 + 100 * rnd + q, sorted(live), topology=False) for q in range(20)]
+        rs = g.schedule_batch([g.compile(p) for p in batch], assume=True)
+        for q, p in enumerate(batch):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[q].as_tuple() == ro.as_tuple(), f"seed {seed} round {rnd} batch pod {q}"
+
+
 @pytest.mark.parametrize("pct", [0, 30])
 def test_sampling_pipelined_batch(native, pct):
     """Default-plugin pods in 600-pod batches take the chunked pipeline; the device-resident
