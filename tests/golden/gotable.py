@@ -303,7 +303,7 @@ class GoFile:
                 while p.peek()[1] != "{":
                     p.next()
                 body_start = p.i
-                if name.startswith("Test"):
+                if name.startswith("Test") or re.match(r"test[A-Z]", name):
                     self.tests[name] = body_start
                 else:
                     ret = self._single_return(body_start)
@@ -472,8 +472,31 @@ CONSTS = {
     "st.PodAffinityWithRequiredPreferredReq": "reqpref", "st.PodAntiAffinityWithRequiredReq": "req",
     "st.PodAntiAffinityWithPreferredReq": "pref", "st.PodAntiAffinityWithRequiredPreferredReq": "reqpref",
     "st.NilPodAffinity": "nil", "st.NodeSelectorTypeMatchExpressions": "expr", "st.NodeSelectorTypeMatchFields": "fields",
+    "v1.ResourceHugePagesPrefix": "hugepages-", "resource.DecimalSI": "DecimalSI", "resource.BinarySI": "BinarySI",
+    "v1.ContainerRestartPolicyAlways": "Always",
+    "config.LeastAllocated": "LeastAllocated", "config.MostAllocated": "MostAllocated",
+    "config.RequestedToCapacityRatio": "RequestedToCapacityRatio",
     "true": True, "false": False, "nil": None,
 }
+PAUSE = "registry.k8s.io/pause:3.10.2"  # imageutils.GetPauseImageName (test/utils/image/manifest.go:233)
+
+
+def go_sprintf(fmt, *args):
+    out, i = [], 0
+    k = 0
+    while k < len(fmt):
+        if fmt[k] == "%" and k + 1 < len(fmt):
+            verb = fmt[k + 1]
+            if verb == "%":
+                out.append("%")
+            else:
+                out.append(str(args[i]))
+                i += 1
+            k += 2
+        else:
+            out.append(fmt[k])
+            k += 1
+    return "".join(out)
 
 
 class Unknown(Exception):
@@ -496,11 +519,15 @@ class Status(dict):
     pass
 
 
+MAP_TYPES = {"v1.ResourceList"}  # named map types: keys are expressions, not field names
+
+
 class Evaluator:
-    def __init__(self, gofile, extra_consts=None):
+    def __init__(self, gofile, extra_consts=None, helpers=None):
         self.f = gofile
         self.consts = dict(CONSTS)
         self.consts.update(extra_consts or {})
+        self.helpers = dict(helpers or {})  # Python restatements of multi-statement test helpers
 
     def ev(self, e, env):
         k = e[0]
@@ -566,7 +593,9 @@ class Evaluator:
         if kind == "slice" or kind == "array":
             inner = typ[-1]
             return [self.composite(inner, v[1], env) if v[0] == "elided" else self.ev(v, env) for _, v in elems]
-        if kind == "map":
+        if kind == "map" or (kind == "named" and typ[1] in MAP_TYPES):
+            if kind == "named":
+                typ = ("map", None, ("named", "resource.Quantity"))
             out = {}
             for key, v in elems:
                 kk = self.ev(key, env)
@@ -607,8 +636,19 @@ class Evaluator:
                 return NodeB()
             if name in ("st.MakeLabelSelector",):
                 return LSB()
-            if name in ("ptr.To", "resource.MustParse", "int64", "int32", "int"):
+            if name in ("ptr.To", "resource.MustParse", "int64", "int32", "int", "v1.ResourceName", "string"):
                 return self.ev(args[0], env)
+            if name == "fmt.Sprintf":
+                vals = [self.ev(a, env) for a in args]
+                return go_sprintf(*vals)
+            if name == "resource.NewMilliQuantity":
+                return f"{self.ev(args[0], env)}m"
+            if name == "resource.NewQuantity":
+                return str(self.ev(args[0], env))
+            if name in ("framework.NewNodeInfo",):
+                return {"_nodeinfo_pods": [self.ev(a, env) for a in args]}
+            if name in self.helpers:
+                return self.helpers[name](*[self.ev(a, env) for a in args])
             if name in ("fwk.NewStatus", "framework.NewStatus"):
                 vals = [self.ev(a, env) for a in args]
                 return Status(code=vals[0], reasons=vals[1:])
@@ -627,6 +667,8 @@ class Evaluator:
                 return {}
             if name in ("int64", "int32", "int", "float64", "string"):
                 return self.ev(args[0], env)
+            if name in self.helpers:
+                return self.helpers[name](*[self.ev(a, env) for a in args])
             if name in self.f.funcs:
                 params, body = self.f.funcs[name]
                 sub = dict(env)
@@ -860,11 +902,50 @@ class PodB(Builder):
         self.o["spec"].setdefault("topologySpreadConstraints", []).append(c)
         return self
 
+    def m_Req(self, req):  # wrappers.go:814-822
+        if req:
+            n = len(self.o["spec"]["containers"])
+            self.o["spec"]["containers"].append({"name": f"con{n}", "image": PAUSE,
+                                                 "resources": {"requests": {k: str(v) for k, v in req.items()}}})
+        return self
+
+    def m_InitReq(self, req):  # :836-844 (Resources: requests and limits)
+        if req:
+            ic = self.o["spec"].setdefault("initContainers", [])
+            r = {k: str(v) for k, v in req.items()}
+            ic.append({"name": f"init-con{len(ic)}", "image": PAUSE, "resources": {"requests": r, "limits": dict(r)}})
+        return self
+
+    def m_SidecarReq(self, req):  # :847-855
+        if req:
+            ic = self.o["spec"].setdefault("initContainers", [])
+            r = {k: str(v) for k, v in req.items()}
+            ic.append({"name": f"sidecar-con{len(ic)}", "image": PAUSE, "restartPolicy": "Always",
+                       "resources": {"requests": r, "limits": dict(r)}})
+        return self
+
+    def m_Container(self, image):  # :366-370
+        n = len(self.o["spec"]["containers"])
+        self.o["spec"]["containers"].append({"name": f"con{n}", "image": image})
+        return self
+
+    def m_Containers(self, cs):
+        self.o["spec"]["containers"] = list(cs)
+        return self
+
+    def m_Overhead(self, rl):
+        self.o["spec"]["overhead"] = {k: str(v) for k, v in rl.items()}
+        return self
+
+    def m_Resources(self, rr):  # pod-level resources (:339-342)
+        self.o["spec"]["resources"] = rr
+        return self
+
     def m_Obj(self):
         return self.o
 
 
-def load_table(path, test, table="tests", extra_consts=None):
+def load_table(path, test, table="tests", extra_consts=None, helpers=None):
     """-> list of dicts (field name -> evaluated value or Unknown marker)."""
     import glob
     import os
@@ -877,7 +958,7 @@ def load_table(path, test, table="tests", extra_consts=None):
             for k, v in o.funcs.items():
                 gf.funcs.setdefault(k, v)
     local, tab = gf.test_locals_and_table(test, table)
-    ev = Evaluator(gf, extra_consts)
+    ev = Evaluator(gf, extra_consts, helpers)
     env = dict(local)
     assert tab[0] == "composite", tab[0]
     out = []

@@ -555,6 +555,8 @@ def main():
         pass
     groups = dict(GROUPS)
     groups.update(extra)
+    import make_fixtures_e  # fifth batch (Fit filter/scores, NodeAffinity score, NodeUnschedulable, NodeName)
+    groups.update(make_fixtures_e.GROUPS)
     for name, fn in groups.items():
         cases = fn()
         path = os.path.join(HERE, f"{name}.json")

@@ -114,6 +114,28 @@ def run_cycle_case(b, case, names):
         errs.append(f"feasible {r.feasible_nodes} != {e['feasible']}")
     if "evaluated" in e and r.evaluated_nodes != e["evaluated"]:
         errs.append(f"evaluated {r.evaluated_nodes} != {e['evaluated']}")
+    if "node_in" in e:  # the reference test accepts any of these hosts (random tie-break upstream)
+        got = names[r.node_index] if r.node_index >= 0 else None
+        if got not in e["node_in"]:
+            errs.append(f"node {got} not in {e['node_in']}")
+    if "plugin_scores" in e:  # NodePluginScores.Scores: weighted normalised score per plugin and node
+        from ksg.abi import PLUGIN_ID
+        for plugin, want in e["plugin_scores"].items():
+            row = ev["plugin_scores"][PLUGIN_ID[plugin]]
+            by = dict(zip(names, row))
+            for n, v in want.items():
+                if by[n] != v:
+                    errs.append(f"{plugin}[{n}] {by[n]} != {v}")
+            if not (ev["score_plugin_mask"] >> PLUGIN_ID[plugin]) & 1:
+                errs.append(f"{plugin} did not score (skipped)")
+    if "node_status" in e:  # Diagnosis.NodeToStatus: (code, plugin, reason bits) per node
+        from ksg.abi import PLUGIN_ID
+        for n, (code, plugin, reasons) in e["node_status"].items():
+            i = names.index(n)
+            got = (ev["node_code"][i], ev["node_plugin"][i], ev["node_reasons"][i])
+            want = (code, PLUGIN_ID[plugin] if plugin else 255, reasons)
+            if got != want:
+                errs.append(f"status[{n}] {got} != {want}")
     return errs
 
 
