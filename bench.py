@@ -42,11 +42,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c2-hetero", "c3", "c4", "c4-anti", "c5"],
-                    help="c2 SchedulingBasic (the metric's config); c3 SchedulingPodAffinity; c4 TopologySpreading; "
-                         "c5 100k-node mixed cluster")
-    ap.add_argument("--nodes", type=int, default=None, help="cluster nodes at N=1 (c2-c4: 5000, c5: 100000)")
-    ap.add_argument("--init-pods", type=int, default=None, help="bound pods at N=1 (c2-c4: 1000, c5: 10000)")
+    ap.add_argument("--workload", default="c2", choices=list(WORKLOADS),
+                    help="c2 SchedulingBasic (the metric's config); c3 SchedulingPodAffinity + NodeAffinity + "
+                         "taints; c4 TopologySpreading; c4-anti PreferredPodAntiAffinity; c5 100k-node mixed "
+                         "cluster; c2-hetero / c3-pa variants")
+    ap.add_argument("--nodes", type=int, default=None, help="cluster nodes at N=1 (default: the config's)")
+    ap.add_argument("--init-pods", type=int, default=None, help="bound pods at N=1 (default: the config's)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the oracle check of the timed stream's placements (the cpu_baseline sample)")
     ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"], help="multi-GPU mode (N>1)")
     ap.add_argument("--shard-single", action="store_true",
                     help="run the node-sharded pipeline (RCCL transport) even at N=1 -- a check of that path")
@@ -67,10 +70,18 @@ def parse():
     return ap.parse_args()
 
 
-WORKLOAD_NAMES = {"c2": "SchedulingBasic", "c2-hetero": "SchedulingBasic (heterogeneous nodes)",
-                  "c3": "SchedulingPodAffinity", "c4": "TopologySpreading", "c4-anti": "PreferredPodAntiAffinity",
-                  "c5": "Mixed 100k-node cluster (50% default, 10% each node-affinity / pod-affinity / "
-                        "anti-affinity / preferred anti-affinity / zone spread)"}
+# workload -> (name, default nodes, default init pods, BASELINE configs index)
+WORKLOADS = {
+    "c2": ("SchedulingBasic", 5000, 1000, 1),
+    "c2-hetero": ("SchedulingBasic (heterogeneous nodes)", 5000, 1000, None),
+    "c3": ("SchedulingPodAffinity + NodeAffinity + taints (1 in 5 nodes foo:NoSchedule; pod-affinity / "
+           "node-affinity / node-inclusion-policy spread pods in turn)", 5000, 5000, 2),
+    "c3-pa": ("SchedulingPodAffinity", 5000, 5000, None),
+    "c4": ("TopologySpreading", 15000, 15000, 3),
+    "c4-anti": ("PreferredPodAntiAffinity", 15000, 15000, 3),
+    "c5": ("Mixed 100k-node cluster (50% default, 10% each node-affinity / pod-affinity / anti-affinity / "
+           "preferred anti-affinity / zone spread)", 100000, 10000, 4),
+}
 
 
 def cpu_model():
@@ -100,14 +111,15 @@ def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100):
         o.add_pod(p)
     hs = [o.compile(p) for p in pods]
     done = 0
+    results = []
     t0 = time.perf_counter()
     chunk = 50
     while done < len(hs) and time.perf_counter() - t0 < budget_s:
-        o.schedule_batch(hs[done:done + chunk], assume=True)
+        results += [r.as_tuple() for r in o.schedule_batch(hs[done:done + chunk], assume=True)]
         done += min(chunk, len(hs) - done)
     dt = time.perf_counter() - t0
     o.close()
-    return done / dt, done, dt
+    return done / dt, done, dt, results
 
 
 def main():
@@ -136,13 +148,16 @@ def main():
         sys.exit("--pct != 100 runs unsharded only (use --mode replicas for N > 1)")
     scaling = a.node_scaling or ("strong" if c5 else "weak")
     grow = world if (sharded and scaling == "weak") else 1
-    n_nodes = (a.nodes or (100000 if c5 else 5000)) * grow
-    n_init = (a.init_pods if a.init_pods is not None else (10000 if c5 else 1000)) * grow
+    wname, d_nodes, d_init, cfg_ix = WORKLOADS[a.workload]
+    n_nodes = (a.nodes or d_nodes) * grow
+    n_init = (a.init_pods if a.init_pods is not None else d_init) * grow
     n_meas = a.steps * a.batch
     n_warm = max(a.warmup, 1 if sharded else 0) * a.batch
     if a.workload in ("c2", "c2-hetero"):
         nodes, init, pods = synth.scheduling_basic(n_nodes, n_init, n_warm + n_meas, hetero=a.workload == "c2-hetero")
     elif a.workload == "c3":
+        nodes, init, pods = synth.scheduling_c3(n_nodes, n_init, n_warm + n_meas)
+    elif a.workload == "c3-pa":
         nodes, init, pods = synth.scheduling_pod_affinity(n_nodes, n_init, n_warm + n_meas)
     elif c5:
         nodes, init, pods = synth.mixed_cluster(n_nodes, n_init, n_warm + n_meas)
@@ -243,8 +258,9 @@ def main():
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             # the reference's default parallelism (16 goroutines over nodes), then one thread
-            v, done, cdt = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads, pct=a.pct)
-            v1, done1, cdt1 = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct)
+            v, done, cdt, ores = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads,
+                                              pct=a.pct)
+            v1, done1, cdt1, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct)
             cpu = {"value": round(v, 2), "unit": "pods/s", "cores": a.cpu_threads, "kind": "port",
                    "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
@@ -254,6 +270,17 @@ def main():
                                 "on the pool" if a.pct != 100 else ""),
                    "single_thread": {"value": round(v1, 2), "cores": 1,
                                      "sample": f"first {done1} pods, {cdt1:.1f} s, 1 thread"}}
+        parity = None
+        if cpu is not None and not a.no_verify:
+            # the timed stream's results (ScheduleResult: status, node, evaluated, feasible, total score)
+            # against the oracle's over the same pods from the same initial state
+            gres = [r.as_tuple() for _, rs in arrays for r in rs][:len(ores)]
+            bad = [k for k, (x, y) in enumerate(zip(gres, ores)) if x != y]
+            parity = {"checked_pods": len(ores), "mismatches": len(bad), "first_mismatch": bad[0] if bad else None,
+                      "against": "oracle/ (same pods, same initial state)"}
+            if bad:
+                print(f"PARITY FAILURE: {len(bad)} of {len(ores)} timed pods differ from the oracle "
+                      f"(first: pod {bad[0]}: {gres[bad[0]]} vs {ores[bad[0]]})", file=sys.stderr, flush=True)
         out = {
             "metric": "pods scheduled/sec + node-evals/sec at 5k/100k nodes, 1/2/4/8 MI355X",
             "value": round(pods_s, 2),
@@ -268,10 +295,9 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (scheduler_perf node-default / pod-default templates, seeded)",
-            "config": {"workload": f"{WORKLOAD_NAMES[a.workload]} {n_nodes} nodes / {n_init} init pods / "
+            "config": {"workload": f"{wname} {n_nodes} nodes / {n_init} init pods / "
                                    f"{n_meas} measured pods" + ("" if sharded else " per GPU")
-                                   + (" (BASELINE configs[1])" if a.workload == "c2" and world == 1 else "")
-                                   + (" (BASELINE configs[4])" if c5 else ""),
+                                   + (f" (BASELINE configs[{cfg_ix}])" if cfg_ix is not None else ""),
                        "nodes": n_nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": a.pct,
                        "plugins": "default",
                        "parallelism": (f"nodes-sharded{world}" if sharded
@@ -284,6 +310,7 @@ def main():
                          "traffic": traffic, "avg_kernel_us": round(kms * 1e3, 3),
                          "algo_bytes_per_launch": round(kbytes, 1)},
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(out), flush=True)
     s.close()

@@ -119,6 +119,53 @@ def scheduling_pod_affinity(n_nodes, n_init, n_pods, seed=0x5EED):
     return nodes, init, pods
 
 
+def pod_with_node_inclusion_policy(name, ns):
+    """templates/pod-with-node-inclusion-policy.yaml: hostname spread, maxSkew 1, DoNotSchedule,
+    nodeAffinityPolicy / nodeTaintsPolicy Honor, selector foo=bar."""
+    p = _pause_pod(name, ns, {"foo": "bar"})
+    p.o["spec"]["topologySpreadConstraints"] = [{
+        "maxSkew": 1, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "DoNotSchedule",
+        "nodeAffinityPolicy": "Honor", "nodeTaintsPolicy": "Honor", "labelSelector": {"matchLabels": {"foo": "bar"}}}]
+    return p.obj()
+
+
+def scheduling_c3(n_nodes, n_init, n_pods, taint_every=5, seed=0x5EED):
+    """BASELINE C3 (configs[2]): SchedulingPodAffinity + NodeAffinity + taints.
+
+    Nodes: node-default in zone1 (affinity/performance-config.yaml:96-139, labelNodePrepareStrategy
+    zone1); every `taint_every`-th one is node-with-taint (foo:NoSchedule) -- 1000 of 5000, as in
+    SchedulingWithNodeInclusionPolicy (topology_spreading/performance-config.yaml:149-180).
+    Init pods: pod-with-pod-affinity in sched-0, bound round-robin to the untainted nodes (the
+    pods tolerate no taint).  Measured stream, in turn: pod-with-pod-affinity (sched-1),
+    pod-with-node-affinity (zone In [zone1, zone2], affinity/performance-config.yaml:222-259),
+    pod-with-node-inclusion-policy (hostname spread honouring affinity and taints)."""
+    nodes, plain = [], []
+    for i in range(n_nodes):
+        name = f"node-{i:06d}"
+        w = (NodeW(name).capacity({"cpu": "4", "memory": "32Gi", "pods": "110"})
+             .label("kubernetes.io/hostname", name).label("topology.kubernetes.io/zone", "zone1"))
+        if i % taint_every == taint_every - 1:
+            w.taints([{"key": "foo", "effect": "NoSchedule"}])
+        else:
+            plain.append(name)
+        nodes.append(w.obj())
+    init = []
+    for k in range(n_init):
+        p = pod_with_pod_affinity(f"init-{k}", "sched-0")
+        p["spec"]["nodeName"] = plain[k % len(plain)]
+        init.append(p)
+    pods = []
+    for k in range(n_pods):
+        kind = k % 3
+        if kind == 0:
+            pods.append(pod_with_pod_affinity(f"pod-{k}", "sched-1"))
+        elif kind == 1:
+            pods.append(pod_with_node_affinity(f"pod-{k}", "sched-1", ["zone1", "zone2"]))
+        else:
+            pods.append(pod_with_node_inclusion_policy(f"pod-{k}", "sched-1"))
+    return nodes, init, pods
+
+
 def topology_spreading(n_nodes, n_init, n_pods, preferred_anti=False, seed=0x5EED):
     """BASELINE C4 / TopologySpreading (topology_spreading/performance-config.yaml:20-59): zones
     moon-1/2/3 round-robin, init pod-default pods, measured pod-with-topology-spreading (or, with

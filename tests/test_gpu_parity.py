@@ -155,12 +155,28 @@ def test_empty_cluster_and_unschedulable(native):
     assert g.schedule_one(hg)[0].as_tuple() == o.schedule_one(ho)[0].as_tuple()
 
 
-def _stream(native, nodes, init, pods, cfg=None):
-    g, o = _pair(native, cfg or {}, nodes, init)
-    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
-    for k, p in enumerate(pods):
-        ro, _ = o.schedule_one(o.compile(p), assume=True)
-        assert rs[k].as_tuple() == ro.as_tuple(), f"pod {k}"
+def _stream(native, nodes, init, pods, cfg=None, ocfg=None, batch=None):
+    """The pods through ksg_schedule_batch (in batches of `batch`), each assume landing before the
+    next pod, against the oracle (ocfg: e.g. cpuThreads for the large clusters)."""
+    g = native(dict(cfg or {}))
+    o = oracle(dict(cfg or {}, **(ocfg or {})))
+    for b in (g, o):
+        for ns in namespaces():
+            b.upsert_namespace(ns)
+        for n in nodes:
+            b.add_node(n)
+        for p in init:
+            b.add_pod(p)
+    assert g.node_names() == o.node_names()
+    hs = [g.compile(p) for p in pods]
+    step = batch or len(pods)
+    rs = []
+    for i in range(0, len(hs), step):
+        rs += g.schedule_batch(hs[i:i + step], assume=True)
+    ors = o.schedule_batch([o.compile(p) for p in pods], assume=True)
+    for k in range(len(pods)):
+        assert rs[k].as_tuple() == ors[k].as_tuple(), f"pod {k}: {rs[k].as_tuple()} != oracle {ors[k].as_tuple()}"
+    return rs
 
 
 def test_c3_pod_affinity_1k(native):
@@ -176,6 +192,31 @@ def test_c4_topology_spreading_3k(native):
 def test_c4_preferred_anti_affinity_2k(native):
     from ksg.synth import topology_spreading
     _stream(native, *topology_spreading(2000, 2000, 120, preferred_anti=True))
+
+
+# ---- the BASELINE configs at their own sizes -----------------------------------------
+def test_c3_baseline_size(native):
+    """configs[2]: 5000 nodes in zone1 (1000 tainted foo:NoSchedule), 5000 pod-affinity init pods,
+    pod-affinity / node-affinity / node-inclusion-policy spread pods in turn."""
+    from ksg.synth import scheduling_c3
+    rs = _stream(native, *scheduling_c3(5000, 5000, 240), ocfg={"cpuThreads": 16}, batch=80)
+    assert sum(r.status == 0 for r in rs) == len(rs)
+
+
+@pytest.mark.parametrize("anti", [False, True])
+def test_c4_baseline_size(native, anti):
+    """configs[3]: 15000 nodes (zones moon-1/2/3), 15000 init pods, zone spread maxSkew 5 (or
+    preferred hostname anti-affinity)."""
+    from ksg.synth import topology_spreading
+    _stream(native, *topology_spreading(15000, 15000, 160, preferred_anti=anti), ocfg={"cpuThreads": 16}, batch=80)
+
+
+def test_c5_mixed_100k(native):
+    """configs[4] on one GPU: 100000 heterogeneous nodes in 10 zones (1 % tainted), 10000 bound pods,
+    the mixed stream (50 % default, 10 % each node-affinity / pod-affinity / anti-affinity /
+    preferred anti-affinity / zone spread)."""
+    from ksg.synth import mixed_cluster
+    _stream(native, *mixed_cluster(100000, 10000, 200), ocfg={"cpuThreads": 16}, batch=100)
 
 
 @pytest.mark.parametrize("wg", [1, 3, 7, 64, 256])

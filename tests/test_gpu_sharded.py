@@ -175,3 +175,13 @@ def test_rccl_transport_single_rank_matches_oracle():
     got = [r.as_tuple() for r in s.schedule_batch([s.compile(p) for p in pods], assume=True)]
     for k, p in enumerate(pods):
         assert got[k] == o.schedule_one(o.compile(p), assume=True)[0].as_tuple(), f"pod {k}"
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_c5_mixed_sharded_20k(world):
+    """configs[4]'s mixed stream on 20000 nodes split over W in-process ranks (the 8-GPU layout of
+    the 100k-node config, scaled to one device), against the oracle."""
+    from ksg.synth import mixed_cluster
+    nodes, init, pods = mixed_cluster(20000, 2000, 120)
+    ranks, o = _group(world, {}, nodes, init)
+    _check(ranks, o, pods, chunk=60)
