@@ -28,7 +28,8 @@ def main():
     loop_pods = float(sys.argv[4]) if len(sys.argv) > 4 else 1000.0 / 7.0
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    c = sqlite3.connect(os.path.join(PROF, "trace", "run_results.db"))
+    # KSG_PROF_TRACE: the kernel-trace directory under gpurun_out/prof (default "trace")
+    c = sqlite3.connect(os.path.join(PROF, os.environ.get("KSG_PROF_TRACE", "trace"), "run_results.db"))
     rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     lines = [f"# rocprofv3 --kernel-trace --stats -- python3 bench.py (tag {tag})",
              f"{'kernel':60s} {'calls':>8s} {'total_us':>12s} {'avg_us':>9s} {'pct':>6s}"]
