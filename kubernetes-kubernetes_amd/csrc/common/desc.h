@@ -98,7 +98,9 @@ struct PtsCons {
   int32_t hist_base;    // arena entries: per-domain (or per-node) matching pod counts
   int32_t pres_base;    // arena entries: domain presence flags
   int32_t nvals;        // domains (label values of the key)
-  int32_t pad;
+  int32_t lref;         // k_agg_loop: where hist_base's counts live (AggRef)
+  int32_t pref;         // k_agg_loop: where pres_base's flags live (AggRef; unused for node-local keys)
+  int32_t pad[3];
 };
 // an InterPodAffinity term of the incoming pod (interpodaffinity/filtering.go:246-283, scoring.go:81-125)
 struct IpaTerm {
@@ -108,9 +110,14 @@ struct IpaTerm {
   int32_t sel;          // selector program offset
   int32_t ns_off, ns_cnt;  // namespace ids (pod selector pool, int32 units)
   int32_t all_ns;       // namespaceSelector matches the empty label set
-  int32_t pad;
+  int32_t lref;         // k_agg_loop: where hist_base's counts live (AggRef)
 };
-struct KeyHist { int32_t slot; int32_t base; };
+struct KeyHist { int32_t slot; int32_t base; int32_t lref; int32_t pad; };
+// k_agg_loop's placement of one arena histogram ("AggRef"): >= 0, the histogram's first word in the
+// pod's compact shared region (a topology key whose values several nodes share: zones); < 0, the
+// node-local histogram -1 - lref, one count per node of the workgroup's range (a key whose every
+// value is on one node only, like kubernetes.io/hostname: the owner of the node holds every count).
+constexpr int kKeytabStride = 5;  // keytab entry: slot, existing-anti base, topology base, their AggRefs
 // an existing pod's affinity term (device term table, kube-scheduler/framework/types.go:380-396)
 enum TermKind : int32_t { T_DEAD = -1, T_REQ_AFF = 0, T_REQ_ANTI = 1, T_PREF_AFF = 2, T_PREF_ANTI = 3 };
 struct DTerm {
@@ -198,13 +205,19 @@ struct PodDesc {
   uint32_t ipa_flags;
   int32_t hard_weight;
   int32_t n_raff, raff_off, n_ranti, ranti_off, n_paff, paff_off, n_panti, panti_off;  // IpaTerm
-  int32_t n_keytab, keytab_off;      // int32 [key id][2]: existing-anti / topology-score arena base, -1 none
+  int32_t n_keytab, keytab_off;      // int32 [key id][kKeytabStride]: slot, existing-anti / topology-score arena base (-1 none), their AggRefs
   int32_t n_exkeys, exkeys_off;      // KeyHist: existing anti-affinity counts (Filter)
   int32_t n_topokeys, topokeys_off;  // KeyHist: topology scores (Score)
   int32_t arena_words;               // arena entries this pod uses (zeroed again by k_select)
   // ---- percentageOfNodesToScore (schedule_one.go:778-782,858-884), DF_ROTDEV / DF_SAMPLE
   int32_t num_to_find;               // numFeasibleNodesToFind (or 1 without score plugins)
   int32_t prev_pod;                  // previous launched pod of the batch (its rot_out), -1: PodStats::rot_in
+  // ---- k_agg_loop (the persistent loop for pods with pod-table aggregation)
+  int32_t n_own_terms, own_terms_off;  // int32 term-table entries of this pod's own affinity terms (the
+                                       // owner adds them to its term list when the pod is assumed)
+  int32_t agg_gwords;                  // words of the compact shared region (AggRef >= 0)
+  int32_t agg_nlocal;                  // node-local histograms (AggRef < 0)
+  int32_t agg_local_cons;              // bit c: DoNotSchedule constraint c counts on a node-local histogram
   int32_t pad2;
 };
 
@@ -367,6 +380,39 @@ struct LoopView {
 // exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
 // A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)
 constexpr int kGran = 4;
+
+// ---- persistent loop for pods with pod-table aggregation (k_agg_loop) ---------------
+// Same workgroup geometry as k_sched_loop (unsharded).  Each workgroup also owns the pod-table slots
+// and existing affinity terms of the pods bound to its nodes.
+constexpr int kAggLocal = 4;       // node-local histograms per pod
+constexpr int kAggGWords = 2048;   // compact shared-region words per pod (staged in LDS)
+constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local histograms per pod
+constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
+constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
+constexpr int kAGran = 8;          // granules per participant per pod
+enum AggGran : int {
+  AG_Z0 = 0,   // {InterPodAffinity "any" bits}: every count of the pod is in the shared region
+  AG_Z1 = 1,   // node-local DoNotSchedule constraint 0: {min count over my eligible nodes (24) | eligible nodes (20)}
+  AG_Z2 = 2,   // ... constraint 1
+  AG_A0 = 3,   // {feasible | feasible before nextStartNodeIndex}
+  AG_A1 = 4,   // {max raw TaintToleration + 1 | max raw NodeAffinity + 1}
+  AG_A2 = 5,   // max raw InterPodAffinity (biased, 0 = none)
+  AG_A3 = 6,   // min raw InterPodAffinity (biased and reversed, 0 = none)
+  AG_B = 7,    // packed (TotalScore, pre-order) key
+};
+constexpr int64_t kAggIpaBias = (int64_t)1 << 46;  // |raw InterPodAffinity| < 2^46 (host-checked)
+struct AggView {
+  int32_t first_pod, npods;   // pods [first_pod, first_pod + npods) of the batch
+  int32_t nwg;                // resident workgroups
+  int32_t blk0, nblk;         // node blocks [blk0, blk0 + nblk)
+  uint32_t tag;               // granule tag (1..65535)
+  int32_t gwords;             // region words per pod (max agg_gwords of the run)
+  unsigned long long* gran;   // [npods][nwg][kAGran]
+  unsigned long long* region; // [npods][gwords]: shared-region partial sums (zeroed by the host)
+  uint32_t* fail;             // set when a spin gives up
+  const uint32_t* desc_bytes; // [batch pods] program sizes
+  unsigned long long* stamps; // diagnostic: [npods][8] (nullptr)
+};
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)
 KSG_HD inline uint32_t pack_status(uint32_t code, uint32_t plugin, uint32_t reasons) {

@@ -23,11 +23,6 @@ namespace ksg {
 
 constexpr int kLdsArena = 2048;  // int64 entries staged in LDS (16 KiB)
 
-__device__ __forceinline__ bool term_matches_pod(const int32_t* sp, const IpaTerm& t, int32_t ns,
-                                                 const unsigned long long* lbl, int32_t n) {
-  // AffinityTerm.Matches(pod, nil) for the incoming pod's (namespace-merged) terms (types.go:391-396)
-  return (t.all_ns || id_in(sp + t.ns_off, t.ns_cnt, ns)) && lsel_match(sp + t.sel, lbl, n);
-}
 
 __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b, int pod, int nb_node, int nb_pod,
                                                         int nb_term) {
@@ -140,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
       const DTerm t = m.terms[j];
       const int n = t.kind >= 0 ? m.pod_node[t.owner] : -1;
       if (n >= 0 && t.key < d.n_keytab) {
-        const int32_t* kt = at<int32_t>(base, d.keytab_off) + (size_t)t.key * 3;
+        const int32_t* kt = at<int32_t>(base, d.keytab_off) + (size_t)t.key * kKeytabStride;
         const bool anti = t.kind == T_REQ_ANTI;
         const int32_t hb = anti ? ((d.ipa_flags & IPA_EXIST_FILTER) ? kt[1] : -1)
                                 : ((d.ipa_flags & IPA_EXIST_SCORE) ? kt[2] : -1);

@@ -170,4 +170,10 @@ __device__ __forceinline__ uint32_t pts_eligible(const MirrorView& m, const uint
   return bits;
 }
 
+__device__ __forceinline__ bool term_matches_pod(const int32_t* sp, const IpaTerm& t, int32_t ns,
+                                                 const unsigned long long* lbl, int32_t n) {
+  // AffinityTerm.Matches(pod, nil) for the incoming pod's (namespace-merged) terms (types.go:391-396)
+  return (t.all_ns || id_in(sp + t.ns_off, t.ns_cnt, ns)) && lsel_match(sp + t.sel, lbl, n);
+}
+
 }  // namespace ksg

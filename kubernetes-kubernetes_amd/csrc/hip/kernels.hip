@@ -209,11 +209,25 @@ __shared__ unsigned long long s_diag[24];  // stamps land in LDS (a global store
 #endif
 
 // ---- filters ------------------------------------------------------------------------------------
+// Where PodTopologySpread / InterPodAffinity read the pod's per-domain counts.  The launch path:
+// k_aggregate's arena in HBM and its PodStats reductions.  k_agg_loop: AggTopo (LDS).
+struct ArenaTopo {
+  const PodStats* ps;
+  const unsigned long long* arena;
+  __device__ __forceinline__ int64_t cnt(int32_t hist_base, int32_t, int32_t v, int) const {
+    return (int64_t)arena[hist_base + v];
+  }
+  __device__ __forceinline__ int64_t pmin(int c) const { return ps->pts_min[c]; }
+  __device__ __forceinline__ uint32_t pndom(int c) const { return ps->pts_ndom[c]; }
+  __device__ __forceinline__ uint32_t any() const { return ps->ipa_any; }
+};
+
 // Returns the packed Filter status of node i (0 = Success), first failing plugin in the
 // RunFilterPlugins order wins.  *raw_taint gets the PreferNoSchedule count while the taint
-// list is in registers.
+// list is in registers.  ls: node i's slot in the caller's topology view (k_agg_loop).
+template <typename Topo>
 __device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const uint8_t* base, const PodDesc& d, int i,
-                                int64_t* raw_taint, const PodStats* ps, const unsigned long long* arena) {
+                                int64_t* raw_taint, const Topo& tp, int ls) {
   const uint32_t fm = d.filter_mask;
   // NodeUnschedulable (node_unschedulable.go:125-143)
   if ((fm >> P_UNSCHED) & 1u)
@@ -289,8 +303,8 @@ __device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const u
     for (int32_t c = 0; c < d.n_ptsf; ++c) {
       const int32_t v = node_label(m, cs[c].slot, i);
       if (v < 0) return pack_status(C_UU, P_PTS, KSG_R_PTS_MISSING_LABEL);
-      const int64_t minMatch = (int64_t)ps->pts_ndom[c] < (int64_t)cs[c].min_domains ? 0 : ps->pts_min[c];
-      const int64_t matchNum = (int64_t)arena[cs[c].hist_base + v];
+      const int64_t minMatch = (int64_t)tp.pndom(c) < (int64_t)cs[c].min_domains ? 0 : tp.pmin(c);
+      const int64_t matchNum = tp.cnt(cs[c].hist_base, cs[c].lref, v, ls);
       if (matchNum + cs[c].self_match - minMatch > (int64_t)cs[c].max_skew)
         return pack_status(C_UNSCHED, P_PTS, KSG_R_PTS_SKEW);
     }
@@ -302,23 +316,24 @@ __device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const u
     for (int32_t k = 0; k < d.n_raff; ++k) {
       const int32_t v = node_label(m, ra[k].slot, i);
       if (v < 0) return pack_status(C_UU, P_IPA, KSG_R_IPA_AFFINITY);
-      if ((int64_t)arena[ra[k].hist_base + v] <= 0) podsExist = false;
+      if (tp.cnt(ra[k].hist_base, ra[k].lref, v, ls) <= 0) podsExist = false;
     }
-    if (!podsExist && !((ps->ipa_any & 1u) == 0 && (d.ipa_flags & IPA_SELF_ALL)))
+    const uint32_t any = tp.any();
+    if (!podsExist && !((any & 1u) == 0 && (d.ipa_flags & IPA_SELF_ALL)))
       return pack_status(C_UU, P_IPA, KSG_R_IPA_AFFINITY);
-    if (ps->ipa_any & 2u) {  // satisfyPodAntiAffinity :379-391
+    if (any & 2u) {  // satisfyPodAntiAffinity :379-391
       const IpaTerm* rn = at<IpaTerm>(base, d.ranti_off);
       for (int32_t k = 0; k < d.n_ranti; ++k) {
         const int32_t v = node_label(m, rn[k].slot, i);
-        if (v >= 0 && (int64_t)arena[rn[k].hist_base + v] > 0)
+        if (v >= 0 && tp.cnt(rn[k].hist_base, rn[k].lref, v, ls) > 0)
           return pack_status(C_UNSCHED, P_IPA, KSG_R_IPA_ANTI_AFFINITY);
       }
     }
-    if (ps->ipa_any & 4u) {  // satisfyExistingPodsAntiAffinity :364-376
+    if (any & 4u) {  // satisfyExistingPodsAntiAffinity :364-376
       const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
       for (int32_t k = 0; k < d.n_exkeys; ++k) {
         const int32_t v = node_label(m, ek[k].slot, i);
-        if (v >= 0 && (int64_t)arena[ek[k].base + v] > 0)
+        if (v >= 0 && tp.cnt(ek[k].base, ek[k].lref, v, ls) > 0)
           return pack_status(C_UNSCHED, P_IPA, KSG_R_IPA_EXISTING_ANTI);
       }
     }
@@ -404,7 +419,7 @@ __device__ __forceinline__ NodeEval eval_node(const MirrorView& m, const BatchVi
       st = in ? 0u : pack_status(C_UU, 15u, KSG_R_PREFILTER);
     }
     if (st == 0) {
-      uint32_t f = run_filters(m, nc, base, d, i, &raw_taint, b.stats + pod, b.arena);
+      uint32_t f = run_filters(m, nc, base, d, i, &raw_taint, ArenaTopo{b.stats + pod, b.arena}, 0);
       if (d.flags & DF_ALL_FEASIBLE)  // plugin-eval mode: the caller's node list is the feasible list
         f = ((d.flags & DF_NODE_LIST) && !bit(base, d.node_list_off, (uint32_t)i, (m.n + 31) / 32))
                 ? pack_status(C_UU, 15u, 0u)
@@ -2047,6 +2062,688 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   }
 }
 
+
+// =====================================================================================================
+// k_agg_loop -- the persistent loop for pods with pod-table aggregation
+// =====================================================================================================
+// PodTopologySpread / InterPodAffinity pods (SchedulingPodAffinity, TopologySpreading, the mixed
+// cluster) in one launch, instead of k_aggregate + k_filter_score + k_select per pod.  Geometry as
+// k_sched_loop: G resident workgroups, workgroup w owns the node blocks [k0, k1) for the whole run
+// and keeps their cores in LDS.  It also owns the pod-table slots and existing affinity terms of the
+// pods bound to those nodes (scanned once per launch; the owner of a chosen node appends the
+// assumed pod and its terms).  Per pod q, three granule exchanges (Z, A, B):
+//   aggregation  node role (DoNotSchedule eligibility, shared-domain presence), pod role (the
+//                pod's selectors against my pods), term role (my existing terms against the pod).
+//                Counts on a key whose values are each on one node (kubernetes.io/hostname) are
+//                complete here: they stay in LDS, one per node.  Counts on shared keys (zones)
+//                are partial: staged in LDS, added to the pod's compact region in HBM.
+//   xchg Z       {IPA any bits}, {min count | eligible nodes} of each node-local DoNotSchedule
+//                constraint over my nodes.  After it: the region's totals into LDS, and each
+//                shared DoNotSchedule constraint's minimum over its present domains.
+//   phase 1      RunFilterPlugins + raw scores of my nodes (LDS cores, LDS counts)
+//   xchg A       {feasible | before nextStartNodeIndex}, {max raw TT + 1 | max raw NA + 1},
+//                max and min raw InterPodAffinity (biased)
+//   phase 2      positions in the rotated feasible list, NormalizeScore + weights, best packed key
+//   xchg B       {key}; the owner of the maximum commits (AssumePod on the LDS core + mirror).
+struct AggTopo {
+  const unsigned long long* gh;  // shared-region totals of the pod
+  const int32_t* lh;             // node-local counts [histogram][kAggSlots]
+  const long long* mn;           // DoNotSchedule minimum per constraint
+  const uint32_t* nd;            // DoNotSchedule domains per constraint
+  uint32_t ipa_any;
+  __device__ __forceinline__ int64_t cnt(int32_t, int32_t lref, int32_t v, int ls) const;
+  __device__ __forceinline__ int64_t pmin(int c) const { return mn[c]; }
+  __device__ __forceinline__ uint32_t pndom(int c) const { return nd[c]; }
+  __device__ __forceinline__ uint32_t any() const { return ipa_any; }
+};
+constexpr int kAggSlots = kLoopMaxBlk * kBlock;  // node slots per workgroup
+__device__ __forceinline__ int64_t AggTopo::cnt(int32_t, int32_t lref, int32_t v, int ls) const {
+  return lref >= 0 ? (int64_t)gh[lref + v] : (int64_t)lh[(size_t)(-1 - lref) * kAggSlots + ls];
+}
+
+// RunFilterPlugins + raw scores of node i for the loop (eval_node's plugin set minus the
+// PodTopologySpread score, which the loop does not take)
+__device__ __forceinline__ NodeEval eval_agg(const MirrorView& m, const NodeCore& nc, const uint8_t* base,
+                                             const PodDesc& d, int i, const AggTopo& tp, int ls) {
+  NodeEval r{1u, false, 0, 0, 0, 0};
+  int64_t raw_taint = 0;
+  const uint32_t st = run_filters(m, nc, base, d, i, &raw_taint, tp, ls);
+  r.st = st;
+  if (st) return r;
+  const uint32_t sm = d.score_mask;
+  int64_t fixed = 0;
+  if ((sm >> P_TAINT) & 1u) r.rt = raw_taint;
+  if ((sm >> P_NA) & 1u) {
+    int64_t sc = 0;
+    if (d.flags & DF_HAS_ADDED_PREF) sc += prog_weight(m, base, d, d.na_added_pref, i);
+    if (d.flags & DF_HAS_PREF_NA) sc += prog_weight(m, base, d, d.na_preferred, i);
+    r.rna = sc;
+  }
+  if ((sm >> P_FIT) & 1u) fixed += fit_score(m, nc, base, d, i) * d.weight[P_FIT];
+  if ((sm >> P_BAL) & 1u) fixed += balanced_alloc_score(m, nc, base, d, i) * d.weight[P_BAL];
+  if ((sm >> P_IMG) & 1u) fixed += image_score_range(m, base, d, nc.ilo, nc.ihi) * d.weight[P_IMG];
+  if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.Score (interpodaffinity/scoring.go:240-255)
+    const KeyHist* tk = at<KeyHist>(base, d.topokeys_off);
+    int64_t sc = 0;
+    for (int32_t k = 0; k < d.n_topokeys; ++k) {
+      const int32_t v = node_label(m, tk[k].slot, i);
+      if (v >= 0) sc += tp.cnt(tk[k].base, tk[k].lref, v, ls);
+    }
+    r.ripa = sc;
+  }
+  r.fixed = fixed;
+  return r;
+}
+
+// NormalizeScore + weights (framework.go:1409-1452): node_total's arithmetic on the loop's values
+__device__ __forceinline__ int64_t agg_total(const PodDesc& d, int64_t fixed, int64_t rt, int64_t rn, int64_t ri,
+                                             int64_t mx_t, int64_t mx_n, int64_t mx_i, int64_t mn_i, uint32_t any) {
+  if (d.flags & DF_NO_SCORE) return 1;
+  int64_t total = loop_total(d, fixed, rt, rn, mx_t, mx_n);
+  if ((d.score_mask >> P_IPA) & 1u) {  // interpodaffinity/scoring.go:258-290
+    int64_t v = ri;
+    if (any & 8u) {
+      const int64_t diff = mx_i - mn_i;
+      double f = 0.0;
+      if (diff > 0) f = 100.0 * ((double)(ri - mn_i) / (double)diff);
+      v = (int64_t)f;
+    }
+    total += v * d.weight[P_IPA];
+  }
+  return total;
+}
+
+__device__ __forceinline__ void agran_put(const AggView& av, int q, int w, int slot, unsigned long long payload) {
+  __hip_atomic_store(av.gran + ((size_t)q * av.nwg + w) * kAGran + slot,
+                     ((unsigned long long)av.tag << 48) | (payload & kPayload), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// One wave: poll granules [slot0, slot0 + NS) of every workgroup for pod q until all tags match.
+template <int NS>
+__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep]) {
+  const int lane = threadIdx.x & 63;
+  const int P = av.nwg;
+  const unsigned long long* g = av.gran + (size_t)q * P * kAGran + slot0;
+  const unsigned long long want = (unsigned long long)av.tag;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kMaxSweep; ++r) {
+      const int v = lane + 64 * r;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        unsigned long long y = want << 48;
+        if (v < P) y = __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (y >> 48) == want;
+        x[k][r] = y & kPayload;
+      }
+    }
+    if (__all(ok)) return true;
+    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
+      const unsigned long long miss = __ballot(!ok);
+      if (lane == 0) {
+        __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+    if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
+  __shared__ __align__(16) uint8_t s_blob[2][kBlobLds];  // pod p's program in s_blob[p & 1]
+  __shared__ LoopCores s_core;
+  __shared__ int64_t s_fx[kAggSlots], s_ri[kAggSlots];  // phase-1 slots
+  __shared__ uint32_t s_rt[kAggSlots], s_rn[kAggSlots];
+  __shared__ unsigned long long s_ball[kLoopMaxBlk][kBlock / 64];
+  __shared__ int32_t s_lh[kAggLocal * kAggSlots];       // node-local histograms of the pod
+  __shared__ unsigned long long s_gh[kAggGWords];       // shared-region partials, then totals
+  __shared__ uint8_t s_elig[kAggSlots];                 // DoNotSchedule eligibility bits per node
+  __shared__ uint32_t s_pods[kAggPods], s_terms[kAggTerms];  // (slot | term) << 9 | node slot
+  __shared__ uint32_t s_np, s_nt;
+  __shared__ uint32_t s_off[kLoopMaxPods];
+  __shared__ long long s_pmin[kMaxCons];
+  __shared__ uint32_t s_pndom[kMaxCons];
+  __shared__ uint32_t s_any, s_ok, s_F, s_psb, s_acc;
+  __shared__ long long s_lmin[kAggLocalCons];
+  __shared__ uint32_t s_lcnt[kAggLocalCons];
+  __shared__ int64_t s_mx[4];  // mx_t, mx_n, mx_i, mn_i
+  __shared__ uint32_t s_wu[kBlock / 64][2];
+  __shared__ unsigned long long s_wx[kBlock / 64][4];
+  __shared__ unsigned long long s_wk[kBlock / 64];
+  __shared__ int s_wn[kBlock / 64];
+  __shared__ int s_win;
+  __shared__ unsigned long long s_best;
+  const int w = blockIdx.x, G = av.nwg;
+  const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
+  const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
+  const int nlo = k0 * kBlock, nhi = k1 * kBlock < m.n ? k1 * kBlock : m.n;
+  const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
+  auto stamp = [&](int q, int k) {
+    if (av.stamps && w == 0 && t == 0) av.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto fail = [&](uint32_t code) {
+    __hip_atomic_store(av.fail + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto stage_prog = [&](int q, int slot, int tid, int nthr) __attribute__((always_inline)) {
+    const uint4* src = reinterpret_cast<const uint4*>(b.descs + s_off[q]);
+    const uint32_t n16 = av.desc_bytes[av.first_pod + q] / 16u;
+    uint4* dst = reinterpret_cast<uint4*>(s_blob[slot]);
+    for (uint32_t o = (uint32_t)tid; o < n16; o += (uint32_t)nthr) dst[o] = src[o];
+  };
+
+  // ---- launch prologue: node cores, program offsets, my pods and terms
+#pragma unroll
+  for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+    const int i = (k0 + kk) * kBlock + t;
+    if (kk < nk && i < m.n) {
+      const NodeCore c = load_core(m, i);
+      s_core.acpu[kk][t] = c.acpu;
+      s_core.amem[kk][t] = c.amem;
+      s_core.aeph[kk][t] = c.aeph;
+      s_core.apods[kk][t] = c.apods;
+      s_core.flags[kk][t] = c.flags;
+      s_core.tlo[kk][t] = c.tlo;
+      s_core.thi[kk][t] = c.thi;
+      s_core.ilo[kk][t] = c.ilo;
+      s_core.ihi[kk][t] = c.ihi;
+      lds_put_dynamic(s_core, kk, t, c);
+    }
+  }
+  for (int k = t; k < av.npods; k += kBlock) s_off[k] = b.desc_off[av.first_pod + k];
+  if (t == 0) {
+    s_np = 0;
+    s_nt = 0;
+  }
+  __syncthreads();
+  for (int s = t; s < m.pods_hw; s += kBlock) {
+    const int n = m.pod_node[s];
+    if (n >= nlo && n < nhi) {
+      const uint32_t k = atomicAdd(&s_np, 1u);
+      if (k < (uint32_t)kAggPods) s_pods[k] = ((uint32_t)s << 9) | (uint32_t)(n - nlo);
+    }
+  }
+  for (int j = t; j < m.n_terms; j += kBlock) {
+    const DTerm tm = m.terms[j];
+    const int n = tm.kind >= 0 ? m.pod_node[tm.owner] : -1;
+    if (n >= nlo && n < nhi) {
+      const uint32_t k = atomicAdd(&s_nt, 1u);
+      if (k < (uint32_t)kAggTerms) s_terms[k] = ((uint32_t)j << 9) | (uint32_t)(n - nlo);
+    }
+  }
+  if (av.npods > 0) stage_prog(0, 0, t, kBlock);
+  __syncthreads();
+  if (s_np > (uint32_t)kAggPods || s_nt > (uint32_t)kAggTerms) {  // host-checked; never taken
+    if (t == 0) fail(0xfffffffeu);
+    return;
+  }
+
+  for (int q = 0; q < av.npods; ++q) {
+    const int pod = av.first_pod + q;
+    const uint8_t* base = s_blob[q & 1];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    PodStats* ps = b.stats + pod;
+    unsigned long long* region = av.region + (size_t)q * av.gwords;
+    const int gw = d.agg_gwords, nl = d.agg_nlocal;
+    const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
+    const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+    stamp(q, 0);
+
+    // ======== aggregation ========
+    for (int x = t; x < nl * kAggSlots; x += kBlock) s_lh[x] = 0;
+    for (int x = t; x < gw; x += kBlock) s_gh[x] = 0ull;
+    if (t == 0) s_any = 0;
+    __syncthreads();
+    // node role: DoNotSchedule eligibility (nodeLabelsMatchSpreadConstraints + inclusion policies,
+    // podtopologyspread/common.go:43-80) and the shared domains it makes present (filtering.go:255-311)
+#pragma unroll
+    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+      const int i = (k0 + kk) * kBlock + t;
+      uint32_t el = 0;
+      if (kk < nk && i < m.n && d.n_ptsf) {
+        el = pts_eligible(m, base, d, cf, d.n_ptsf, i);
+        for (int32_t c = 0; c < d.n_ptsf; ++c)
+          if (((el >> c) & 1u) && cf[c].lref >= 0) s_gh[cf[c].pref + node_label(m, cf[c].slot, i)] = 1ull;
+      }
+      s_elig[kk * kBlock + t] = (uint8_t)el;
+    }
+    __syncthreads();
+    uint32_t any = 0;
+    auto add = [&](int32_t lref, int32_t v, int ls, long long wt) __attribute__((always_inline)) {
+      if (lref >= 0) atomicAdd(&s_gh[lref + v], (unsigned long long)wt);
+      else atomicAdd(&s_lh[(-1 - lref) * kAggSlots + ls], (int32_t)wt);
+    };
+    // pod role: the pod's selectors against the pods on my nodes (k_aggregate's pod role)
+    for (uint32_t k = (uint32_t)t; k < s_np; k += kBlock) {
+      const uint32_t e = s_pods[k];
+      const int s = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
+      const int32_t pns = m.pod_ns[s];
+      const bool term = (m.pod_flags[s] & 1u) != 0;
+      const unsigned long long* pl = m.lbl_pool + m.pod_lbl_off[s];
+      const int32_t pn = (int32_t)m.pod_lbl_cnt[s];
+      if (!term && pns == d.ns_id && d.n_ptsf) {  // calPreFilterState counts (filtering.go:255-300)
+        const uint32_t el = s_elig[ls];
+        for (int32_t c = 0; c < d.n_ptsf; ++c)
+          if (((el >> c) & 1u) && !lsel_empty(sp + cf[c].sel) && lsel_match(sp + cf[c].sel, pl, pn))
+            add(cf[c].lref, node_label(m, cf[c].slot, n), ls, 1);
+      }
+      if (d.n_raff) {  // affinityCounts (filtering.go:256-266)
+        const IpaTerm* ts = at<IpaTerm>(base, d.raff_off);
+        bool all = true;
+        for (int32_t k2 = 0; k2 < d.n_raff; ++k2) all = all && term_matches_pod(sp, ts[k2], pns, pl, pn);
+        if (all)
+          for (int32_t k2 = 0; k2 < d.n_raff; ++k2) {
+            const int32_t v = node_label(m, ts[k2].slot, n);
+            if (v >= 0) {
+              add(ts[k2].lref, v, ls, 1);
+              any |= 1u;
+            }
+          }
+      }
+      if (d.n_ranti) {  // antiAffinityCounts (filtering.go:268-276)
+        const IpaTerm* ts = at<IpaTerm>(base, d.ranti_off);
+        for (int32_t k2 = 0; k2 < d.n_ranti; ++k2)
+          if (term_matches_pod(sp, ts[k2], pns, pl, pn)) {
+            const int32_t v = node_label(m, ts[k2].slot, n);
+            if (v >= 0) {
+              add(ts[k2].lref, v, ls, 1);
+              any |= 2u;
+            }
+          }
+      }
+      if (d.ipa_flags & IPA_PREF) {  // the incoming pod's soft terms (scoring.go:98-110)
+        const IpaTerm* ta = at<IpaTerm>(base, d.paff_off);
+        for (int32_t k2 = 0; k2 < d.n_paff; ++k2)
+          if (term_matches_pod(sp, ta[k2], pns, pl, pn)) {
+            const int32_t v = node_label(m, ta[k2].slot, n);
+            if (v >= 0) {
+              add(ta[k2].lref, v, ls, ta[k2].weight);
+              any |= 8u;
+            }
+          }
+        const IpaTerm* tn = at<IpaTerm>(base, d.panti_off);
+        for (int32_t k2 = 0; k2 < d.n_panti; ++k2)
+          if (term_matches_pod(sp, tn[k2], pns, pl, pn)) {
+            const int32_t v = node_label(m, tn[k2].slot, n);
+            if (v >= 0) {
+              add(tn[k2].lref, v, ls, -(long long)tn[k2].weight);
+              any |= 8u;
+            }
+          }
+      }
+    }
+    // term role: my pods' existing affinity terms against the incoming pod (k_aggregate's term role)
+    if (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE))
+      for (uint32_t k = (uint32_t)t; k < s_nt; k += kBlock) {
+        const uint32_t e = s_terms[k];
+        const int j = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
+        const DTerm tm = m.terms[j];
+        if (tm.key >= d.n_keytab) continue;
+        const int32_t* kt = at<int32_t>(base, d.keytab_off) + (size_t)tm.key * kKeytabStride;
+        const bool anti = tm.kind == T_REQ_ANTI;
+        const int32_t hb = anti ? ((d.ipa_flags & IPA_EXIST_FILTER) ? kt[1] : -1)
+                                : ((d.ipa_flags & IPA_EXIST_SCORE) ? kt[2] : -1);
+        long long wt = 0;
+        if (tm.kind == T_REQ_AFF) wt = d.hard_weight;  // HardPodAffinityWeight (scoring.go:112-117)
+        else if (tm.kind == T_PREF_AFF) wt = tm.weight;
+        else if (tm.kind == T_PREF_ANTI) wt = -(long long)tm.weight;
+        else wt = 1;
+        if (hb < 0 || wt == 0) continue;
+        const int32_t* tp = m.term_pool;
+        const unsigned long long* il = at<unsigned long long>(base, d.lbl_off);
+        const unsigned long long* nsl = at<unsigned long long>(base, d.nslbl_off);
+        // AffinityTerm.Matches(incoming pod, namespace labels) (types.go:391-396)
+        const bool match = (id_in(tp + tm.ns_off, tm.ns_cnt, d.ns_id) || lsel_match(tp + tm.nssel, nsl, d.n_nslbl)) &&
+                           lsel_match(tp + tm.sel, il, d.n_lbl);
+        const int32_t v = match ? node_label(m, kt[0], n) : -1;
+        if (v >= 0) {
+          add(anti ? kt[3] : kt[4], v, ls, wt);
+          any |= anti ? 4u : 8u;
+        }
+      }
+    if (any) atomicOr(&s_any, any);
+    __syncthreads();
+    // my partials of the shared region; node-local DoNotSchedule minima over my eligible nodes
+    for (int x = t; x < gw; x += kBlock)
+      if (s_gh[x]) atomicAdd(region + x, s_gh[x]);
+    {
+      int li = 0;
+      for (int32_t c = 0; c < d.n_ptsf && li < kAggLocalCons; ++c) {
+        if (!((d.agg_local_cons >> c) & 1)) continue;
+        long long mn = 0x7fffffffffffffffll;
+        uint32_t cnt = 0;
+        for (int kk = 0; kk < nk; ++kk)
+          if ((s_elig[kk * kBlock + t] >> c) & 1u) {
+            const long long x = s_lh[(size_t)(-1 - cf[c].lref) * kAggSlots + kk * kBlock + t];
+            mn = x < mn ? x : mn;
+            ++cnt;
+          }
+        mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
+        cnt = wave_sum_u32(cnt);
+        if (lane == 0) {
+          s_wx[wave][li] = (unsigned long long)mn;
+          s_wu[wave][li] = cnt;
+        }
+        ++li;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my region atomics performed before Z
+    __syncthreads();
+    if (t == 0) {  // every Z granule is published (zero for an absent constraint)
+      unsigned long long z1 = 0, z2 = 0;
+      int li = 0;
+      for (int32_t c = 0; c < d.n_ptsf && li < kAggLocalCons; ++c) {
+        if (!((d.agg_local_cons >> c) & 1)) continue;
+        long long mn = 0x7fffffffffffffffll;
+        uint32_t cnt = 0;
+        for (int v = 0; v < kBlock / 64; ++v) {
+          const long long x = (long long)s_wx[v][li];
+          mn = x < mn ? x : mn;
+          cnt += s_wu[v][li];
+        }
+        const unsigned long long m24 = mn > 0xffffffll ? 0xffffffull : (unsigned long long)mn;
+        const unsigned long long zz = ((unsigned long long)cnt << 24) | m24;  // no eligible node: min 2^24-1
+        if (li == 0) z1 = zz;
+        else z2 = zz;
+        ++li;
+      }
+      agran_put(av, q, w, AG_Z0, s_any);
+      agran_put(av, q, w, AG_Z1, z1);
+      agran_put(av, q, w, AG_Z2, z2);
+    }
+    stamp(q, 1);
+
+    // ======== exchange Z (wave 0), the next program's staging (waves 1-3) ========
+    if (wave == 0) {
+      unsigned long long z[3][kMaxSweep];
+      const bool ok = agran_sweep<3>(av, q, AG_Z0, z);
+      uint32_t a = 0, c1 = 0, c2 = 0;
+      unsigned long long m1 = 0xffffffull, m2 = 0xffffffull;
+#pragma unroll
+      for (int r = 0; r < kMaxSweep; ++r)
+        if (lane + 64 * r < G) {
+          a |= (uint32_t)z[0][r];
+          const unsigned long long x1 = z[1][r] & 0xffffffull, x2 = z[2][r] & 0xffffffull;
+          c1 += (uint32_t)(z[1][r] >> 24);
+          c2 += (uint32_t)(z[2][r] >> 24);
+          m1 = x1 < m1 ? x1 : m1;
+          m2 = x2 < m2 ? x2 : m2;
+        }
+      for (int o = 32; o > 0; o >>= 1) {
+        a |= (uint32_t)__shfl_xor((int)a, o, 64);
+        const unsigned long long y1 = __shfl_xor(m1, o, 64), y2 = __shfl_xor(m2, o, 64);
+        m1 = y1 < m1 ? y1 : m1;
+        m2 = y2 < m2 ? y2 : m2;
+      }
+      c1 = wave_sum_u32(c1);
+      c2 = wave_sum_u32(c2);
+      if (lane == 0) {
+        s_ok = ok ? 1u : 0u;
+        s_any = a;
+        s_lmin[0] = (long long)m1;
+        s_lmin[1] = (long long)m2;
+        s_lcnt[0] = c1;
+        s_lcnt[1] = c2;
+      }
+    } else if (q + 1 < av.npods) {
+      stage_prog(q + 1, (q + 1) & 1, t - 64, kBlock - 64);  // s_blob[(q + 1) & 1] held pod q-1
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    stamp(q, 2);
+    for (int x = t; x < gw; x += kBlock) s_gh[x] = __hip_atomic_load(region + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    // DoNotSchedule minima (criticalPaths, filtering.go:64-124): shared constraints over their
+    // present domains (one wave each), node-local ones from exchange Z
+    {
+      int li = 0;
+      for (int32_t c = 0; c < d.n_ptsf; ++c) {
+        if ((d.agg_local_cons >> c) & 1) {
+          if (t == 0) {
+            s_pmin[c] = li < kAggLocalCons ? s_lmin[li] : 0;
+            s_pndom[c] = li < kAggLocalCons ? s_lcnt[li] : 0;
+          }
+          ++li;
+          continue;
+        }
+        if (wave != (c & 3)) continue;
+        long long mn = 0x7fffffffffffffffll;
+        uint32_t cnt = 0;
+        for (int v = lane; v < cf[c].nvals; v += 64)
+          if (s_gh[cf[c].pref + v]) {
+            const long long x = (long long)s_gh[cf[c].lref + v];
+            mn = x < mn ? x : mn;
+            ++cnt;
+          }
+        mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
+        cnt = wave_sum_u32(cnt);
+        if (lane == 0) {
+          s_pmin[c] = mn;
+          s_pndom[c] = cnt;
+        }
+      }
+    }
+    __syncthreads();
+    stamp(q, 3);
+
+    // ======== phase 1: my nodes ========
+    const AggTopo tp{s_gh, s_lh, s_pmin, s_pndom, s_any};
+    uint32_t w_cnt = 0, w_below = 0;
+    unsigned long long t_mt = 0, t_mn = 0, t_mi = 0, t_ni = ~0ull;
+#pragma unroll
+    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+      if (kk < nk) {
+        const int i = (k0 + kk) * kBlock + t, ls = kk * kBlock + t;
+        NodeEval ne{1u, false, 0, 0, 0, 0};
+        if (i < m.n) ne = eval_agg(m, lds_core(s_core, kk, t), base, d, i, tp, ls);
+        const bool feas = ne.st == 0;
+        const unsigned long long ballot = __ballot(feas);
+        if (lane == 0) s_ball[kk][wave] = ballot;
+        const int lim = d.rot_start - ((k0 + kk) * kBlock + wave * 64);
+        const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+        w_cnt += (uint32_t)__popcll(ballot);
+        w_below += (uint32_t)__popcll(ballot & bm);
+        s_fx[ls] = ne.fixed;
+        s_rt[ls] = (uint32_t)ne.rt;
+        s_rn[ls] = (uint32_t)ne.rna;
+        s_ri[ls] = ne.ripa;
+        if (feas) {
+          const unsigned long long et = enc_i64(ne.rt), en = enc_i64(ne.rna), ei = enc_i64(ne.ripa);
+          t_mt = et > t_mt ? et : t_mt;
+          t_mn = en > t_mn ? en : t_mn;
+          t_mi = ei > t_mi ? ei : t_mi;
+          t_ni = ei < t_ni ? ei : t_ni;
+        }
+      }
+    }
+    t_mt = wave_max_u64(t_mt);
+    t_mn = wave_max_u64(t_mn);
+    t_mi = wave_max_u64(t_mi);
+    t_ni = ~wave_max_u64(~t_ni);
+    if (lane == 0) {
+      s_wu[wave][0] = w_cnt;
+      s_wu[wave][1] = w_below;
+      s_wx[wave][0] = t_mt;
+      s_wx[wave][1] = t_mn;
+      s_wx[wave][2] = t_mi;
+      s_wx[wave][3] = t_ni;
+    }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t c = 0, bl = 0;
+      unsigned long long a = 0, bb = 0, mi = 0, ni = ~0ull;
+      for (int v = 0; v < kBlock / 64; ++v) {
+        c += s_wu[v][0];
+        bl += s_wu[v][1];
+        a = s_wx[v][0] > a ? s_wx[v][0] : a;
+        bb = s_wx[v][1] > bb ? s_wx[v][1] : bb;
+        mi = s_wx[v][2] > mi ? s_wx[v][2] : mi;
+        ni = s_wx[v][3] < ni ? s_wx[v][3] : ni;
+      }
+      unsigned long long g0, g1;
+      a_granules(c, bl, a, bb, &g0, &g1);
+      // raw InterPodAffinity biased into [1, 2^47): max as is, min reversed (max of 2^47 - x)
+      const unsigned long long bi = c ? (unsigned long long)(dec_i64(mi) + kAggIpaBias) + 1ull : 0ull;
+      const unsigned long long bn = c ? (1ull << 47) - (unsigned long long)(dec_i64(ni) + kAggIpaBias) : 0ull;
+      agran_put(av, q, w, AG_A0, g0);
+      agran_put(av, q, w, AG_A1, g1);
+      agran_put(av, q, w, AG_A2, bi);
+      agran_put(av, q, w, AG_A3, bn);
+    }
+    stamp(q, 4);
+
+    // ======== exchange A (wave 0) ========
+    if (wave == 0) {
+      unsigned long long xa[4][kMaxSweep];
+      const bool ok = agran_sweep<4>(av, q, AG_A0, xa);
+      uint32_t F = 0, wp = 0, bf = 0;
+      unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
+#pragma unroll
+      for (int r = 0; r < kMaxSweep; ++r) {
+        const int v = lane + 64 * r;
+        if (v < G) {
+          const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
+          F += c;
+          if (v < w) wp += c;
+          bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
+          const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
+          tmax = tv > tmax ? tv : tmax;
+          nmax = nv > nmax ? nv : nmax;
+          imax = xa[2][r] > imax ? xa[2][r] : imax;
+          inmax = xa[3][r] > inmax ? xa[3][r] : inmax;
+        }
+      }
+      F = wave_sum_u32(F);
+      bf = wave_sum_u32(bf);
+      wp = wave_sum_u32(wp);
+      tmax = wave_max_u64(tmax);
+      nmax = wave_max_u64(nmax);
+      imax = wave_max_u64(imax);
+      inmax = wave_max_u64(inmax);
+      if (lane == 0) {
+        s_ok = ok ? 1u : 0u;
+        s_F = F;
+        s_psb = bf;
+        s_acc = wp;
+        s_mx[0] = tmax ? (int64_t)tmax - 1 : 0;
+        s_mx[1] = nmax ? (int64_t)nmax - 1 : 0;
+        s_mx[2] = imax ? (int64_t)(imax - 1ull) - kAggIpaBias : 0;
+        s_mx[3] = inmax ? (int64_t)((1ull << 47) - inmax) - kAggIpaBias : 0;
+      }
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    stamp(q, 5);
+
+    // ======== phase 2: positions, NormalizeScore + weights, my best packed key ========
+    const uint32_t F = s_F, ps_before = s_psb;
+    const int64_t mx_t = s_mx[0], mx_n = s_mx[1], mx_i = s_mx[2], mn_i = s_mx[3];
+    const uint32_t ipa_any = s_any;
+    unsigned long long key = 0;
+    int knode = -1;
+    {
+      uint32_t acc = s_acc;
+#pragma unroll
+      for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+        if (kk < nk) {
+          uint32_t pre = 0;
+          for (int v = 0; v < kBlock / 64; ++v) pre += v < wave ? (uint32_t)__popcll(s_ball[kk][v]) : 0u;
+          const unsigned long long ballot = s_ball[kk][wave];
+          const int ls = kk * kBlock + t;
+          if ((ballot >> lane) & 1ull) {
+            const uint32_t g = acc + pre + wave_prefix_count(ballot, lane);
+            const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
+            const int64_t total = agg_total(d, s_fx[ls], s_rt[ls], s_rn[ls], s_ri[ls], mx_t, mx_n, mx_i, mn_i, ipa_any);
+            const unsigned long long kv = pack_best(total, pos);
+            if (kv > key) {
+              key = kv;
+              knode = (k0 + kk) * kBlock + t;
+            }
+          }
+          for (int v = 0; v < kBlock / 64; ++v) acc += (uint32_t)__popcll(s_ball[kk][v]);
+        }
+      }
+    }
+    {
+      const unsigned long long wk = wave_max_u64(key);
+      const unsigned long long hold = __ballot(key == wk && key != 0ull);
+      const int wn = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
+      if (lane == 0) {
+        s_wk[wave] = wk;
+        s_wn[wave] = wn;
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      unsigned long long k = 0;
+      int kn = -1;
+      for (int v = 0; v < kBlock / 64; ++v)
+        if (s_wk[v] > k) {
+          k = s_wk[v];
+          kn = s_wn[v];
+        }
+      s_wk[0] = k;
+      s_wn[0] = kn;
+      agran_put(av, q, w, AG_B, k);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
+    }
+    stamp(q, 6);
+
+    // ======== exchange B (wave 0) ========
+    if (wave == 0) {
+      unsigned long long xb[1][kMaxSweep];
+      const bool ok = agran_sweep<1>(av, q, AG_B, xb);
+      unsigned long long bm = 0;
+#pragma unroll
+      for (int r = 0; r < kMaxSweep; ++r) {
+        const unsigned long long v = (lane + 64 * r) < G ? xb[0][r] : 0ull;
+        bm = v > bm ? v : bm;
+      }
+      bm = wave_max_u64(bm);
+      if (lane == 0) {
+        s_ok = ok ? 1u : 0u;
+        s_best = bm;
+        s_win = (F > 0 && s_wk[0] == bm && s_wn[0] >= 0) ? s_wn[0] : -1;
+      }
+    }
+    __syncthreads();
+    if (!s_ok) return;
+
+    // ======== commit: the chosen node's owner (AssumePod on the LDS core + the mirror; the pod
+    // and its affinity terms join my lists) ========
+    const int win = s_win;
+    if (F == 0) {
+      if (w == 0 && t == 0) commit_result(m, b, base, d, ps, pod, 0, -1, s_best, nullptr, (int)ipa_any);
+    } else if (win >= 0 && t == (win - nlo) % kBlock) {
+      const int ls = win - nlo, kw = ls / kBlock;
+      if (d.flags & DF_ASSUME) {
+        NodeCore c = lds_core(s_core, kw, t);
+        assume_core(c, d);
+        commit_result(m, b, base, d, ps, pod, F, win, s_best, &c, (int)ipa_any);
+        lds_put_dynamic(s_core, kw, t, c);
+        if (d.slot >= 0) {
+          const uint32_t np = s_np, nt = s_nt;
+          if (np < (uint32_t)kAggPods) s_pods[np] = ((uint32_t)d.slot << 9) | (uint32_t)ls;
+          const int32_t* own = at<int32_t>(base, d.own_terms_off);
+          uint32_t k2 = 0;
+          for (; k2 < (uint32_t)d.n_own_terms && nt + k2 < (uint32_t)kAggTerms; ++k2)
+            s_terms[nt + k2] = ((uint32_t)own[k2] << 9) | (uint32_t)ls;
+          s_np = np + 1;
+          s_nt = nt + k2;
+          if (np >= (uint32_t)kAggPods || k2 < (uint32_t)d.n_own_terms) fail(0xfffffffdu);  // host-checked
+        }
+      } else {
+        commit_result(m, b, base, d, ps, pod, F, win, s_best, nullptr, (int)ipa_any);
+      }
+    }
+    stamp(q, 7);
+    __syncthreads();  // my lists and cores are final; s_blob[q & 1] is free again
+  }
+}
 }  // namespace ksg
 
 // ---- host-side launchers (C++ linkage, called by the host library) ------------------------------
@@ -2175,6 +2872,14 @@ hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const Loop
     hipLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
   return hipGetLastError();
 }
+hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
+                           hipEvent_t t1) {
+  if (t0)
+    hipExtLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kBlock), 0, s, t0, t1, 0, m, b, av);
+  else
+    hipLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kBlock), 0, s, m, b, av);
+  return hipGetLastError();
+}
 // Loads the module's code object onto the current device now (hipFuncGetAttributes), so that no
 // first launch inside a batch does it while an in-process peer's persistent loop is running.
 hipError_t warm_kernels() {
@@ -2186,7 +2891,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
                       reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_node_update),
-                      reinterpret_cast<const void*>(&k_node_dyn)};
+                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
     if (e != hipSuccess) return e;

@@ -130,6 +130,7 @@ const std::vector<std::string>& Cluster::order() {
     snap_gone_.clear();
   }
   if (rebuild) {  // updateNodeInfoSnapshotList(updateAll=true) over nodeTree.list (node_tree.go:119-143)
+    ++node_gen_;
     order_.clear();
     size_t longest = 0;
     for (auto& z : zones_) longest = std::max(longest, tree_[z].size());
@@ -151,6 +152,24 @@ int32_t Cluster::index_of(const std::string& n) const {
 NodeRec* Cluster::node(const std::string& name) {
   auto it = nodes_.find(name);
   return it == nodes_.end() ? nullptr : it->second.get();
+}
+bool Cluster::key_unique(int32_t key) {
+  auto it = uniq_cache_.find(key);
+  if (it != uniq_cache_.end() && it->second.first == node_gen_) return it->second.second;
+  std::vector<uint8_t> seen(keys[key].values.strs.size(), 0);
+  bool ok = true;
+  for (auto& nm : order_) {
+    const NodeRec* r = node(nm);
+    if (!r) continue;
+    for (auto& kv : r->labels)
+      if (kv.first == key) {
+        ok = seen[(size_t)kv.second]++ == 0;
+        break;
+      }
+    if (!ok) break;
+  }
+  uniq_cache_[key] = {node_gen_, ok};
+  return ok;
 }
 
 // ---- cache events -------------------------------------------------------------------------------
@@ -235,6 +254,7 @@ void Cluster::set_node(NodeRec& r, NodeSpec&& n) {  // addNodeImageStates + Node
 // would append the name to a second zone list if the zone changed (nodeTree.addNode does not
 // look in other zones), which the informer never asks for.
 int Cluster::add_node(NodeSpec&& n) {
+  ++node_gen_;
   auto it = nodes_.find(n.name);
   if (it != nodes_.end() && it->second->real) return update_node(std::move(n));
   NodeRec* r;
@@ -259,6 +279,7 @@ int Cluster::add_node(NodeSpec&& n) {
 // the snapshot list keeps its position until the next rebuild (order()), so the mirror row is
 // rewritten in place whenever its taint / image CSR ranges keep their sizes.
 int Cluster::update_node(NodeSpec&& n) {
+  ++node_gen_;
   auto it = nodes_.find(n.name);
   if (it == nodes_.end() || !it->second->real) return add_node(std::move(n));
   NodeRec& r = *it->second;
@@ -282,6 +303,7 @@ int Cluster::update_node(NodeSpec&& n) {
 // remain on it, it stays in the cache as a ghost with their requests (their delete events may
 // still be on the way), skipped by snapshots and by the pod table's aggregation.
 int Cluster::remove_node(const std::string& name) {
+  ++node_gen_;
   auto it = nodes_.find(name);
   if (it == nodes_.end() || !it->second->real) { err = "node " + name + " is not found"; return KSG_ENOTFOUND; }
   NodeRec& r = *it->second;

@@ -40,6 +40,8 @@ hipError_t set_diag(unsigned long long* p);
 #endif
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
                              hipEvent_t t0, hipEvent_t t1);
+hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
+                           hipEvent_t t1);
 hipError_t warm_kernels();
 hipError_t warm_aggregate();
 
@@ -552,6 +554,11 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     // live once k_select's assume writes its node index; a pipelined batch reserved it up front
     D.slot = next_slot_ >= 0 ? next_slot_ : c->pod_table_put(p, -1);
     out->slot = D.slot;
+    // the pod's own affinity terms: k_agg_loop's owner of its node adds them when it is assumed
+    const std::vector<int32_t>& own = c->pt_terms[(size_t)D.slot];
+    D.n_own_terms = (int32_t)own.size();
+    D.own_terms_off = B.put(own);
+    out->own_terms = D.n_own_terms;
   }
   if (eval) D.flags |= DF_EVAL_OUT;
   // DF_FAST: the straight-line default-plugin evaluation (kernels.hip eval_node_fast)
@@ -601,9 +608,12 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
   smask = &sm;
   std::vector<int32_t> pool;  // selector programs + namespace id lists
   int32_t arena = 0;
-  auto alloc = [&](int32_t n) {
+  struct HistRec { int32_t base, n, key; bool pres; };
+  std::vector<HistRec> hists;  // every histogram of the arena (k_agg_loop's placement below)
+  auto alloc = [&](int32_t n, int32_t key, bool pres) {
     const int32_t b = arena;
     arena += n;
+    hists.push_back({b, n, key, pres});
     return b;
   };
   auto nvals = [&](int32_t key) { return (int32_t)c->keys[key].values.strs.size(); };
@@ -635,8 +645,8 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       pc.taint_honor = sp.taint_honor ? 1 : 0;
       pc.hostname = (score && sp.key == "kubernetes.io/hostname") ? 1 : 0;
       pc.nvals = pc.hostname ? N : nvals(key);
-      pc.hist_base = alloc(pc.nvals);
-      pc.pres_base = pc.hostname ? -1 : alloc(pc.nvals);
+      pc.hist_base = alloc(pc.nvals, key, false);
+      pc.pres_base = pc.hostname ? -1 : alloc(pc.nvals, key, true);
       cons->push_back(pc);
     }
     return true;
@@ -696,7 +706,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       const int32_t key = c->key_id(t.topo);
       it.slot = slot_of(key);
       auto b = bases->find(key);
-      if (b == bases->end()) b = bases->emplace(key, alloc(nvals(key))).first;
+      if (b == bases->end()) b = bases->emplace(key, alloc(nvals(key), key, false)).first;
       it.hist_base = b->second;
       (void)pref;
       o->push_back(it);
@@ -734,7 +744,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
     if (!ipa_f) { raff.clear(); ranti.clear(); }
     if (ipa_f && parse_ok && !c->exanti_keys.empty()) {
       D.ipa_flags |= IPA_EXIST_FILTER;
-      for (auto& kv : c->exanti_keys) exanti_base[kv.first] = alloc(nvals(kv.first));
+      for (auto& kv : c->exanti_keys) exanti_base[kv.first] = alloc(nvals(kv.first), kv.first, false);
     }
     // PreScore: IgnorePreferredTermsOfExistingPods && !hasConstraints -> Skip (scoring.go:152-156)
     if (ipa_s && cfg.ignore_pref_existing && !hasConstraints) *smask &= ~(1u << P_IPA);
@@ -747,7 +757,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       for (auto& kv : c->score_keys_pref) ekeys.insert(kv.first);
       if (!ekeys.empty() && parse_ok) D.ipa_flags |= IPA_EXIST_SCORE;
       for (int32_t k : ekeys)
-        if (!topo_base.count(k)) topo_base[k] = alloc(nvals(k));
+        if (!topo_base.count(k)) topo_base[k] = alloc(nvals(k), k, false);
       // Neither the pod's preferred terms nor any existing pod's scoring terms can add to
       // topologyScore, so it stays empty and PreScore returns Skip (scoring.go:207-209) -- known
       // here without counting anything on the device.
@@ -759,24 +769,58 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
   }
   D.hard_weight = cfg.hard_weight;
 
-  // key table for the existing-term pass: {label slot, existing-anti base, topology-score base}
+  // k_agg_loop's placement of every histogram (AggRef, desc.h): a key whose values are each on one
+  // node only keeps per-node counts with the node's owner workgroup (its presence flags are not
+  // needed: every eligible node is its own domain); any other key's histogram goes to the pod's
+  // compact shared region, summed over workgroups.  A pod that does not fit takes the launch path.
+  std::unordered_map<int32_t, int32_t> ref;  // arena base -> AggRef
+  int32_t gwords = 0, nlocal = 0;
+  for (auto& h : hists) {
+    const bool uniq = c->key_unique(h.key);
+    if (uniq && h.pres) ref[h.base] = -1 - kAggLocal;  // never read
+    else if (uniq) ref[h.base] = -1 - nlocal++;
+    else {
+      ref[h.base] = gwords;
+      gwords += h.n;
+    }
+  }
+  auto aref = [&](int32_t b) { return b < 0 ? 0 : ref.at(b); };
+  int32_t local_cons = 0, nlc = 0;
+  for (size_t k = 0; k < ptsf.size(); ++k) {
+    ptsf[k].lref = aref(ptsf[k].hist_base);
+    ptsf[k].pref = aref(ptsf[k].pres_base);
+    if (ptsf[k].lref < 0) {
+      local_cons |= 1 << k;
+      ++nlc;
+    }
+  }
+  for (auto* v : {&raff, &ranti, &paff, &panti})
+    for (auto& t : *v) t.lref = aref(t.hist_base);
+  D.agg_gwords = gwords;
+  D.agg_nlocal = nlocal;
+  D.agg_local_cons = local_cons;
+  out->agg_ok = ptss.empty() && nlocal <= kAggLocal && gwords <= kAggGWords && nlc <= kAggLocalCons;
+
+  // key table for the existing-term pass: {label slot, existing-anti base, topology-score base, AggRefs}
   std::vector<int32_t> keytab;
   if (!exanti_base.empty() || ((D.ipa_flags & IPA_EXIST_SCORE) != 0)) {
     const int32_t nk = (int32_t)c->label_keys.strs.size();
-    keytab.assign((size_t)nk * 3, -1);
+    keytab.assign((size_t)nk * kKeytabStride, -1);
     for (auto& kv : exanti_base) {
-      keytab[(size_t)kv.first * 3] = slot_of(kv.first);
-      keytab[(size_t)kv.first * 3 + 1] = kv.second;
+      keytab[(size_t)kv.first * kKeytabStride] = slot_of(kv.first);
+      keytab[(size_t)kv.first * kKeytabStride + 1] = kv.second;
+      keytab[(size_t)kv.first * kKeytabStride + 3] = aref(kv.second);
     }
     for (auto& kv : topo_base) {
-      keytab[(size_t)kv.first * 3] = slot_of(kv.first);
-      keytab[(size_t)kv.first * 3 + 2] = kv.second;
+      keytab[(size_t)kv.first * kKeytabStride] = slot_of(kv.first);
+      keytab[(size_t)kv.first * kKeytabStride + 2] = kv.second;
+      keytab[(size_t)kv.first * kKeytabStride + 4] = aref(kv.second);
     }
     D.n_keytab = nk;
   }
   std::vector<KeyHist> exkeys, topokeys;
-  for (auto& kv : exanti_base) exkeys.push_back({c->keys[kv.first].slot, kv.second});
-  for (auto& kv : topo_base) topokeys.push_back({c->keys[kv.first].slot, kv.second});
+  for (auto& kv : exanti_base) exkeys.push_back({c->keys[kv.first].slot, kv.second, aref(kv.second), 0});
+  for (auto& kv : topo_base) topokeys.push_back({c->keys[kv.first].slot, kv.second, aref(kv.second), 0});
 
   const bool agg = !ptsf.empty() || !ptss.empty() || !raff.empty() || !ranti.empty() || !exkeys.empty() ||
                    ((*smask >> P_IPA) & 1u);
@@ -856,6 +900,24 @@ bool Engine::loop_ok(const CompiledPod& p) const {
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
   if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV)) return false;
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
+  return loop_bounds_ok(p);
+}
+// A pod k_agg_loop takes: any CYCLE pod without PodTopologySpread scoring, evaluation output,
+// PreFilter outcomes or sampling, whose histograms fit the loop's placement (CompiledPod::agg_ok).
+bool Engine::agg_loop_ok(const CompiledPod& p) const {
+  if (p.error || !p.agg_ok) return false;
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
+  if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET))
+    return false;
+  if (d.score_mask & (1u << P_PTS)) return false;
+  // raw InterPodAffinity scores ride the granules biased by 2^46: every existing term and pod adds
+  // at most 100 per matching term of the pod
+  const double ipa_bound = ((double)c->tt.size() + (double)c->pt_node.size() + 1.0) * 100.0 * (4.0 * kMaxPodTerms + 1.0);
+  if (ipa_bound >= (double)kAggIpaBias) return false;
+  return loop_bounds_ok(p);
+}
+bool Engine::loop_bounds_ok(const CompiledPod& p) const {
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
   if (p.blob.size() > (size_t)kBlobLds) return false;
   // the exchange granules carry raw TaintToleration counts and raw NodeAffinity sums (+1) in 24
   // bits each and the packed key in 48: bound the pod's possible values
@@ -902,6 +964,20 @@ double Engine::algo_bytes(const PodDesc& d) const {
   return b * N;
 }
 
+// Algorithmic bytes of one pod's pod-table pass (k_aggregate / k_agg_loop's aggregation): every
+// existing pod's node, namespace, flags, label range and labels, every existing term's record.
+double Engine::agg_bytes(const PodDesc& d) const {
+  if (!(d.flags & DF_AGGREGATE)) return 0;
+  const bool pod_work = d.n_ptsf || d.n_ptss || d.n_raff || d.n_ranti || (d.ipa_flags & IPA_PREF);
+  const bool term_work = (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE)) != 0;
+  const double pods = (double)c->view.pods_hw;
+  const double lbl = pods > 0 ? (double)c->pt_pool.size() / pods : 0.0;
+  double b = 0;
+  if (pod_work) b += pods * (20.0 + 8.0 * lbl);
+  if (term_work) b += (double)c->view.n_terms * (double)sizeof(DTerm);
+  return b;
+}
+
 Engine::~Engine() {
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
@@ -909,7 +985,7 @@ Engine::~Engine() {
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
   if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail})
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -1239,10 +1315,37 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   G = std::min(std::max(G, (NBs + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NBs, 1), max_wg));
   const bool use_loop = (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
                         (int64_t)G * kLoopMaxBlk >= NBs && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
-  struct LoopRun { int first, count; double bytes; };
+  // k_agg_loop (unsharded): the same geometry; every workgroup's LDS lists must hold its nodes' pods
+  // and terms plus everything this batch can add (each pod, and its own terms, at most once)
+  bool use_agg = !comm && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 && G <= cus &&
+                 (int64_t)G * kLoopMaxBlk >= NB && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
+  if (use_agg) {
+    bool any = false;
+    int64_t own = 0;
+    for (int i = 0; i < compiled; ++i) {
+      any = any || agg_loop_ok(cp[i]);
+      own += cp[i].own_terms;
+    }
+    use_agg = any && c->pt_node.size() < ((size_t)1 << 23) && c->tt.size() < ((size_t)1 << 23);
+    if (use_agg) {
+      std::vector<int32_t> wg_of((size_t)NB), np((size_t)G, 0), nt((size_t)G, 0);
+      for (int w = 0; w < G; ++w)
+        for (int64_t k = (int64_t)NB * w / G; k < (int64_t)NB * (w + 1) / G; ++k) wg_of[(size_t)k] = w;
+      for (int32_t nd : c->pt_node)
+        if (nd >= 0 && nd < m.n) np[(size_t)wg_of[(size_t)(nd / kBlock)]]++;
+      for (const DTerm& tm : c->tt) {
+        const int32_t nd = tm.kind >= 0 && tm.owner >= 0 ? c->pt_node[(size_t)tm.owner] : -1;
+        if (nd >= 0 && nd < m.n) nt[(size_t)wg_of[(size_t)(nd / kBlock)]]++;
+      }
+      use_agg = *std::max_element(np.begin(), np.end()) + (int64_t)n <= kAggPods &&
+                *std::max_element(nt.begin(), nt.end()) + own <= kAggTerms;
+    }
+  }
+  struct LoopRun { int first, count; double bytes; bool agg; };
   std::vector<LoopRun> runs;
-  if (use_loop) {
-    if ((rc = gran_setup())) return rc;
+  if (use_agg && (rc = ensure(d_agran, (size_t)kLoopMaxPods * 256 * kAGran * 8))) return rc;
+  if (use_loop || use_agg) {
+    if (use_loop && (rc = gran_setup())) return rc;
     if ((rc = ensure(d_fail, 16))) return rc;
     HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
     if (c->cfg.loop_stamps) {
@@ -1271,7 +1374,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
     HIPCHK(hipMemcpyAsync(hr + a, (DevResult*)d_results.p + a, (size_t)(upto - a) * sizeof(DevResult),
                           hipMemcpyDeviceToHost, ds));
-    if (use_loop) HIPCHK(hipMemcpyAsync(hfail + chunks.size(), d_fail.p, 4, hipMemcpyDeviceToHost, ds));
+    if (use_loop || use_agg) HIPCHK(hipMemcpyAsync(hfail + chunks.size(), d_fail.p, 4, hipMemcpyDeviceToHost, ds));
     HIPCHK(hipEventRecord(cev[chunks.size()], ds));
     chunks.push_back({a, upto});
     return KSG_OK;
@@ -1311,8 +1414,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   int settled = 0;  // chunks whose results are mirrored into the cache
   auto settle_closed = [&]() -> int {  // after a stream sync: every closed chunk
     for (; settled < (int)chunks.size(); ++settled) {
-      if (use_loop && hfail[settled]) {
-        c->err = "k_sched_loop: an exchange granule never arrived (spin limit)";
+      if ((use_loop || use_agg) && hfail[settled]) {
+        c->err = "persistent loop: an exchange granule never arrived (spin limit)";
         return KSG_EDEVICE;
       }
       const int r2 = settle(chunks[settled].a, chunks[settled].b);
@@ -1402,7 +1505,49 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         return KSG_EDEVICE;
       }
       HIPCHK(launch_sched_loop(m, bv, lv, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
-      runs.push_back({i, j - i, rb});
+      runs.push_back({i, j - i, rb, false});
+      launches += j - i;
+      i = j;
+      continue;
+    }
+    if (use_agg && agg_loop_ok(cp[i])) {  // a run of pod-table pods: one k_agg_loop launch
+      int j = i;
+      double rb = 0;
+      int32_t gw = 1;
+      const int cut = chunk_end(i);
+      while (j < n && j < cut && j - i < kLoopMaxPods && agg_loop_ok(cp[j]) && !loop_ok(cp[j])) {
+        const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[j].blob.data());
+        rb += algo_bytes(hd) + agg_bytes(hd);
+        gw = std::max(gw, hd.agg_gwords);
+        ++j;
+      }
+      while (lev.size() < 2 * (runs.size() + 1)) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        lev.push_back(e);
+      }
+      const size_t rbytes = (size_t)(j - i) * (size_t)gw * 8;
+      if ((rc = ensure(d_region, rbytes))) return rc;
+      HIPCHK(hipMemsetAsync(d_region.p, 0, rbytes, s));
+      if (++agran_tag > 0xFFFFu) {
+        agran_tag = 1;
+        HIPCHK(hipMemsetAsync(d_agran.p, 0, d_agran.bytes, s));
+      }
+      AggView av{};
+      av.first_pod = i;
+      av.npods = j - i;
+      av.nwg = G;
+      av.blk0 = 0;
+      av.nblk = NB;
+      av.tag = agran_tag;
+      av.gwords = gw;
+      av.gran = (unsigned long long*)d_agran.p;
+      av.region = (unsigned long long*)d_region.p;
+      av.fail = (uint32_t*)d_fail.p;
+      av.desc_bytes = (const uint32_t*)d_off.p + n;
+      av.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr;
+      HIPCHK(launch_agg_loop(m, bv, av, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
+      runs.push_back({i, j - i, rb, true});
       launches += j - i;
       i = j;
       continue;
@@ -1468,7 +1613,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     uint32_t fail = 0;
     HIPCHK(hipMemcpy(&fail, d_fail.p, 4, hipMemcpyDeviceToHost));
     if (fail) {
-      c->err = "k_sched_loop: a workgroup never reached a per-pod arrival counter (spin limit)";
+      c->err = "persistent loop: a workgroup never reached a per-pod exchange (spin limit)";
       return KSG_EDEVICE;
     }
   }
@@ -1487,27 +1632,51 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   last_bytes = launches ? bytes / launches : 0;
   last_launches = launches;
   last_kernel = 0;
-  if (!runs.empty()) {  // the loop dominates: per-pod time inside k_sched_loop and bytes per pod
-    double lms = 0, lb = 0;
-    int lp = 0;
+  if (!runs.empty()) {  // a loop dominates: per-pod time inside k_sched_loop / k_agg_loop and bytes per pod
+    double lms[2] = {0, 0}, lb[2] = {0, 0};
+    int lp[2] = {0, 0};
     for (size_t r = 0; r < runs.size(); ++r) {
       float x = 0;
       HIPCHK(hipEventElapsedTime(&x, lev[2 * r], lev[2 * r + 1]));
-      lms += x;
-      lb += runs[r].bytes;
-      lp += runs[r].count;
+      const int k = runs[r].agg ? 1 : 0;
+      lms[k] += x;
+      lb[k] += runs[r].bytes;
+      lp[k] += runs[r].count;
     }
-    if (lp * 2 >= launches) {
-      last_kernel = 1;
-      last_kernel_ms = lms / lp;
-      last_bytes = lb / lp;
+    const int k = lp[1] > lp[0] ? 1 : 0;
+    if (lp[k] * 2 >= launches) {
+      last_kernel = 1 + k;
+      last_kernel_ms = lms[k] / lp[k];
+      last_bytes = lb[k] / lp[k];
     }
     if (c->cfg.loop_stamps) {  // mean per-phase time (us) of the looped pods, workgroup 0's view
+      std::vector<LoopRun> sruns, aruns;
+      for (auto& r : runs) (r.agg ? aruns : sruns).push_back(r);
+      {  // k_agg_loop: aggregation, Z, totals + minima, phase 1, A, phase 2, B + commit, gap to the next pod
+        std::vector<unsigned long long> st((size_t)n * 8);
+        HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+        double acc[9] = {0};
+        int cnt = 0;
+        for (auto& r : aruns)
+          for (int q = r.first; q + 1 < r.first + r.count; ++q) {
+            const unsigned long long* t = &st[(size_t)q * 8];
+            bool okq = true;
+            for (int k = 0; k < 8; ++k) okq = okq && t[k] != 0;
+            if (!okq || !st[(size_t)(q + 1) * 8]) continue;
+            for (int k = 1; k < 8; ++k) acc[k] += (double)(t[k] - t[k - 1]) / 100.0;
+            acc[8] += (double)(st[(size_t)(q + 1) * 8] - t[7]) / 100.0;
+            cnt++;
+          }
+        if (cnt)
+          std::fprintf(stderr, "[k_agg_loop stamps, %d pods, us] aggregation %.3f  Z %.3f  totals+minima %.3f  "
+                       "phase1 %.3f  A %.3f  phase2 %.3f  B+commit %.3f  gap %.3f\n", cnt, acc[1] / cnt, acc[2] / cnt,
+                       acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt, acc[7] / cnt, acc[8] / cnt);
+      }
       std::vector<unsigned long long> st((size_t)n * 8);
       HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
       double acc[9] = {0};
       int cnt = 0;
-      for (auto& r : runs)
+      for (auto& r : sruns)
         for (int q = r.first; q < r.first + r.count; ++q) {
           const unsigned long long* t = &st[(size_t)q * 8];
           const unsigned long long nxt = q + 1 < r.first + r.count ? st[(size_t)(q + 1) * 8] : 0;
@@ -1538,7 +1707,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                          hipMemcpyDeviceToHost));
         double ska = 0, skb = 0, ab = 0;
         int sc = 0;
-        for (auto& r : runs)
+        for (auto& r : sruns)
           for (int q = r.first; q + 1 < r.first + r.count; ++q) {
             unsigned long long amin = ~0ull, amax = 0, bmin = ~0ull, bmax = 0, an = ~0ull;
             for (int g = 0; g < G; ++g) {
@@ -1559,7 +1728,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
           std::vector<double> late(G, 0.0);
           double wl = 0;
           int wn = 0, cntq = 0;
-          for (auto& r : runs)
+          for (auto& r : sruns)
             for (int q = r.first + 1; q < r.first + r.count; ++q) {
               unsigned long long amin = ~0ull;
               for (int g = 0; g < G; ++g) amin = std::min(amin, ws[((size_t)q * G + g) * 8]);
@@ -1577,7 +1746,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
           double own = 0, ownlate = 0, ownx = 0, seg[5] = {0};
           int segn = 0;
           int on = 0;
-          for (auto& r : runs)
+          for (auto& r : sruns)
             for (int q = r.first; q + 1 < r.first + r.count; ++q)
               for (int g = 0; g < G; ++g) {
                 const unsigned long long c0 = ws[((size_t)q * G + g) * 8 + 2], c1 = ws[((size_t)q * G + g) * 8 + 3];

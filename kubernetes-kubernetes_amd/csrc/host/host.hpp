@@ -145,6 +145,7 @@ struct Config {
   int device = 0;
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
+  bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
   // sharded: the loop's per-pod exchange device-to-device (granules over xGMI).  Default on for RCCL
   // ranks (one process per GPU); in-process groups (localGroup, one device) only when asked: their
@@ -249,6 +250,9 @@ class Cluster {
   const std::vector<std::string>& order();
   int32_t index_of(const std::string& node) const;
   NodeRec* node(const std::string& name);
+  // every value of label key `key` is on one snapshot node at most (kubernetes.io/hostname): its
+  // per-domain counts are per-node counts (k_agg_loop keeps them with the node's owner)
+  bool key_unique(int32_t key);
 
   // interning used by the compiler
   Interner label_keys;
@@ -322,6 +326,8 @@ class Cluster {
   // rebuild the list: names added (maybe new to the map) and names removed (maybe still in it)
   std::unordered_set<std::string> snap_names_, snap_new_, snap_gone_;
   int32_t tree_nodes_ = 0;  // nodeTree.numNodes
+  uint64_t node_gen_ = 1;   // bumped by every node event (key_unique's cache)
+  std::unordered_map<int32_t, std::pair<uint64_t, bool>> uniq_cache_;
   int32_t slots_used_ = 0, slots_cap_ = 0;
   std::vector<DevBuf> bufs_;
   DevBuf pt_dev_[9];  // pod table / term table device arrays (own lifetime, grown geometrically)
@@ -358,6 +364,8 @@ struct CompiledPod {
   bool ipa_parse_error = false;  // IPA PreFilter: NewPodInfo failed -> UnschedulableAndUnresolvable
   bool topo_score_error = false; // PTS/IPA PreScore Error
   int32_t arena_words = 0;
+  bool agg_ok = false;        // fits k_agg_loop's histogram placement
+  int32_t own_terms = 0;      // the pod's own affinity terms (k_agg_loop's term-list bound)
 };
 struct Blob;
 class Comm;
@@ -386,11 +394,14 @@ class Engine {
   // measurement: average k_filter_score duration (sampled with events when cfg.timing_stride > 0,
   // else the batch's kernel time / launches) and its algorithmic bytes per launch
   double algo_bytes(const PodDesc& d) const;
+  double agg_bytes(const PodDesc& d) const;  // the pod-table pass of an aggregating pod
   double last_kernel_ms = 0, last_bytes = 0;
   int32_t last_launches = 0;
   int32_t last_kernel = 0;  // 0: k_filter_score figures; 1: k_sched_loop (per-pod time in the loop)
   int cu_count = 0;
   bool loop_ok(const CompiledPod& p) const;
+  bool loop_bounds_ok(const CompiledPod& p) const;  // the loops' granule payload bounds
+  bool agg_loop_ok(const CompiledPod& p) const;
   // node-sharded evaluation (cfg.world > 1): this rank's block range + the exchange transport
   std::unique_ptr<Comm> comm;
   int32_t next_slot_ = -1;  // compile(): a pod-table slot reserved by run_batch's pipeline
@@ -410,6 +421,8 @@ class Engine {
   DevBuf d_gran, d_fail, d_stamps;  // k_sched_loop: exchange granules (local), give-up flag, stamps
   std::vector<unsigned long long*> gran_all;  // every rank's granule array as mapped here ([rank] = d_gran)
   uint32_t gran_tag = 0;
+  DevBuf d_agran, d_region;  // k_agg_loop: exchange granules (own tag sequence), per-pod shared regions
+  uint32_t agran_tag = 0;
   int gran_setup();
   int next_gran_tag(uint32_t* tag);
   std::vector<hipEvent_t> lev;  // k_sched_loop timing events (pairs)

@@ -43,11 +43,11 @@ class Scheduler(Backend):
 
     def kernel_stats(self):
         """(avg ms, algorithmic bytes, pods, kernel name) of the last batch: per k_filter_score
-        launch, or per pod inside the persistent k_sched_loop when most pods ran there."""
+        launch, or per pod inside a persistent loop (k_sched_loop, k_agg_loop) when most pods ran there."""
         ms, by, n, k = C.c_double(), C.c_double(), C.c_int32(), C.c_int32()
         self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n), C.byref(k)),
                   "kernel_stats")
-        return ms.value, by.value, n.value, ("k_sched_loop" if k.value == 1 else "k_filter_score")
+        return ms.value, by.value, n.value, {1: "k_sched_loop", 2: "k_agg_loop"}.get(k.value, "k_filter_score")
 
     def shard_range(self):
         """(first snapshot index, node count) this rank evaluates (node-sharded contexts)."""

@@ -248,6 +248,23 @@ def test_persistent_loop_mixed_runs(native, seed):
         assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"
 
 
+@pytest.mark.parametrize("seed,wg", [(0, 0), (1, 0), (2, 1), (3, 5), (4, 0), (5, 64)])
+def test_agg_loop_matches_launch_path(native, seed, wg):
+    """k_agg_loop (PodTopologySpread / InterPodAffinity pods in one persistent launch): random pods
+    with hostname-keyed (node-local counts) and zone / disk-keyed (shared counts) constraints and
+    terms, in one batch, against the per-pod launch path (aggLoop off) and the oracle."""
+    rng, cfg, nodes, existing, names = rand_cluster(7000 + seed, n_nodes=[300, 700, 1100][seed % 3], n_existing=150)
+    base = dict(cfg, loopWorkgroups=wg) if wg else cfg
+    g, o = _pair(native, base, nodes, existing)
+    g2, _ = _pair(native, dict(base, aggLoop=False), nodes, existing)
+    pods = [rand_pod(rng, k, names) for k in range(160)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"
+
+
 # ---- percentageOfNodesToScore: the cut feasible list and the device-resident nextStartNodeIndex
 # (schedule_one.go:778-884, 686-687).  Random clusters are >= 100 nodes so the cut is active; the
 # no-score profile takes numNodesToFind = 1 (schedule_one.go:780-782).
