@@ -155,6 +155,9 @@ enum DescFlags : uint32_t {
   DF_FAST = 1u << 15,              // default-plugin shape: straight-line cpu/mem Fit + BalancedAllocation (eval_node_fast)
   DF_ROTDEV = 1u << 16,            // nextStartNodeIndex is device-resident: k_sample_find derives this pod's rotation
   DF_SAMPLE = 1u << 17,            // numFeasibleNodesToFind < nodes: the feasible list is cut (k_sample_apply)
+  DF_LFAST = 1u << 18,             // DF_FAST's shape for the node-local plugins (k_agg_loop: eval_core_fast + the
+                                   // PodTopologySpread / InterPodAffinity filters and score after it)
+  DF_TERMINATING = 1u << 19,       // the pod has a deletionTimestamp (its pod-table slot's flag)
 };
 
 struct PodDesc {
@@ -384,12 +387,13 @@ constexpr int kGran = 4;
 // ---- persistent loop for pods with pod-table aggregation (k_agg_loop) ---------------
 // Same workgroup geometry as k_sched_loop (unsharded).  Each workgroup also owns the pod-table slots
 // and existing affinity terms of the pods bound to its nodes.
+constexpr int kAggThreads = 512;   // one node slot per thread (8 waves)
 constexpr int kAggLocal = 4;       // node-local histograms per pod
-constexpr int kAggGWords = 2048;   // compact shared-region words per pod (staged in LDS)
+constexpr int kAggGWords = 1024;   // compact shared-region words per pod (staged in LDS)
 constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local histograms per pod
 constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
 constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
-constexpr int kAGran = 8;          // granules per participant per pod
+constexpr int kAGran = 9;          // granules per participant per pod
 enum AggGran : int {
   AG_Z0 = 0,   // {InterPodAffinity "any" bits}: every count of the pod is in the shared region
   AG_Z1 = 1,   // node-local DoNotSchedule constraint 0: {min count over my eligible nodes (24) | eligible nodes (20)}
@@ -399,19 +403,25 @@ enum AggGran : int {
   AG_A2 = 5,   // max raw InterPodAffinity (biased, 0 = none)
   AG_A3 = 6,   // min raw InterPodAffinity (biased and reversed, 0 = none)
   AG_B = 7,    // packed (TotalScore, pre-order) key
+  AG_BN = 8,   // the snapshot index + 1 of the workgroup's best node (every workgroup folds the
+               // chosen pod into the next pod's counts)
 };
 constexpr int64_t kAggIpaBias = (int64_t)1 << 46;  // |raw InterPodAffinity| < 2^46 (host-checked)
+constexpr int kAggStamps = 16;                     // diagnostic stamps per pod (AggView::stamps)
 struct AggView {
   int32_t first_pod, npods;   // pods [first_pod, first_pod + npods) of the batch
   int32_t nwg;                // resident workgroups
   int32_t blk0, nblk;         // node blocks [blk0, blk0 + nblk)
   uint32_t tag;               // granule tag (1..65535)
   int32_t gwords;             // region words per pod (max agg_gwords of the run)
+  int32_t debug;              // diagnostic: bit 0 never fold (gather every pod after the previous one is
+                              // placed), bit 1 never DF_LFAST (config "aggLoopDebug")
   unsigned long long* gran;   // [npods][nwg][kAGran]
   unsigned long long* region; // [npods][gwords]: shared-region partial sums (zeroed by the host)
   uint32_t* fail;             // set when a spin gives up
   const uint32_t* desc_bytes; // [batch pods] program sizes
-  unsigned long long* stamps; // diagnostic: [npods][8] (nullptr)
+  unsigned long long* stamps; // diagnostic: [npods][kAggStamps] (nullptr)
+  unsigned long long* wstamps;  // diagnostic: [npods][nwg][4] phase-1 start, A publish, B publish, commit end
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -222,6 +222,9 @@ struct ArenaTopo {
   __device__ __forceinline__ uint32_t any() const { return ps->ipa_any; }
 };
 
+template <typename Topo>
+__device__ __forceinline__ uint32_t topo_filters(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i,
+                                                 const Topo& tp, int ls);
 // Returns the packed Filter status of node i (0 = Success), first failing plugin in the
 // RunFilterPlugins order wins.  *raw_taint gets the PreferNoSchedule count while the taint
 // list is in registers.  ls: node i's slot in the caller's topology view (k_agg_loop).
@@ -297,6 +300,14 @@ __device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const u
     }
     if (reasons) return pack_status(unresolvable ? C_UU : C_UNSCHED, P_FIT, reasons);
   }
+  return topo_filters(m, base, d, i, tp, ls);
+}
+
+// PodTopologySpread + InterPodAffinity Filter of node i (the last two in the RunFilterPlugins order)
+template <typename Topo>
+__device__ __forceinline__ uint32_t topo_filters(const MirrorView& m, const uint8_t* base, const PodDesc& d, int i,
+                                                 const Topo& tp, int ls) {
+  const uint32_t fm = d.filter_mask;
   // PodTopologySpread (podtopologyspread/filtering.go:314-359) against k_aggregate's counts
   if ((fm >> P_PTS) & 1u) {
     const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
@@ -2103,25 +2114,34 @@ __device__ __forceinline__ int64_t AggTopo::cnt(int32_t, int32_t lref, int32_t v
 
 // RunFilterPlugins + raw scores of node i for the loop (eval_node's plugin set minus the
 // PodTopologySpread score, which the loop does not take)
-__device__ __forceinline__ NodeEval eval_agg(const MirrorView& m, const NodeCore& nc, const uint8_t* base,
-                                             const PodDesc& d, int i, const AggTopo& tp, int ls) {
+// DF_LFAST: the node-local plugins by eval_core_fast (bal_wo: the core's BalancedAllocation without
+// the pod), then the PodTopologySpread / InterPodAffinity filters.
+__device__ __forceinline__ NodeEval eval_agg(const MirrorView& m, const NodeCore& nc, int64_t bal_wo, const PodFast& pf,
+                                             const uint8_t* base, const PodDesc& d, int i, const AggTopo& tp, int ls) {
   NodeEval r{1u, false, 0, 0, 0, 0};
-  int64_t raw_taint = 0;
-  const uint32_t st = run_filters(m, nc, base, d, i, &raw_taint, tp, ls);
-  r.st = st;
-  if (st) return r;
   const uint32_t sm = d.score_mask;
-  int64_t fixed = 0;
-  if ((sm >> P_TAINT) & 1u) r.rt = raw_taint;
-  if ((sm >> P_NA) & 1u) {
-    int64_t sc = 0;
-    if (d.flags & DF_HAS_ADDED_PREF) sc += prog_weight(m, base, d, d.na_added_pref, i);
-    if (d.flags & DF_HAS_PREF_NA) sc += prog_weight(m, base, d, d.na_preferred, i);
-    r.rna = sc;
+  if (pf.flags & DF_LFAST) {
+    r = eval_core_fast(m, nc, bal_wo, pf, base, d, i);
+    if (r.st == 0) r.st = topo_filters(m, base, d, i, tp, ls);
+    if (r.st) return r;
+  } else {
+    int64_t raw_taint = 0;
+    const uint32_t st = run_filters(m, nc, base, d, i, &raw_taint, tp, ls);
+    r.st = st;
+    if (st) return r;
+    int64_t fixed = 0;
+    if ((sm >> P_TAINT) & 1u) r.rt = raw_taint;
+    if ((sm >> P_NA) & 1u) {
+      int64_t sc = 0;
+      if (d.flags & DF_HAS_ADDED_PREF) sc += prog_weight(m, base, d, d.na_added_pref, i);
+      if (d.flags & DF_HAS_PREF_NA) sc += prog_weight(m, base, d, d.na_preferred, i);
+      r.rna = sc;
+    }
+    if ((sm >> P_FIT) & 1u) fixed += fit_score(m, nc, base, d, i) * d.weight[P_FIT];
+    if ((sm >> P_BAL) & 1u) fixed += balanced_alloc_score(m, nc, base, d, i) * d.weight[P_BAL];
+    if ((sm >> P_IMG) & 1u) fixed += image_score_range(m, base, d, nc.ilo, nc.ihi) * d.weight[P_IMG];
+    r.fixed = fixed;
   }
-  if ((sm >> P_FIT) & 1u) fixed += fit_score(m, nc, base, d, i) * d.weight[P_FIT];
-  if ((sm >> P_BAL) & 1u) fixed += balanced_alloc_score(m, nc, base, d, i) * d.weight[P_BAL];
-  if ((sm >> P_IMG) & 1u) fixed += image_score_range(m, base, d, nc.ilo, nc.ihi) * d.weight[P_IMG];
   if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.Score (interpodaffinity/scoring.go:240-255)
     const KeyHist* tk = at<KeyHist>(base, d.topokeys_off);
     int64_t sc = 0;
@@ -2131,7 +2151,6 @@ __device__ __forceinline__ NodeEval eval_agg(const MirrorView& m, const NodeCore
     }
     r.ripa = sc;
   }
-  r.fixed = fixed;
   return r;
 }
 
@@ -2194,193 +2213,186 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
-  __shared__ __align__(16) uint8_t s_blob[2][kBlobLds];  // pod p's program in s_blob[p & 1]
+// One lane: poll granule `slot` of participant p for pod q (give-up as agran_sweep).
+__device__ __forceinline__ bool agran_poll1(const AggView& av, int q, int p, int slot, unsigned long long* out) {
+  const unsigned long long* g = av.gran + ((size_t)q * av.nwg + p) * kAGran + slot;
+  const unsigned long long want = (unsigned long long)av.tag;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t spins = 0;; ++spins) {
+    const unsigned long long y = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((y >> 48) == want) {
+      *out = y & kPayload;
+      return true;
+    }
+    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
+      __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(av.fail + 2, (uint32_t)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(av.fail + 3, (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
+  __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
   __shared__ int64_t s_fx[kAggSlots], s_ri[kAggSlots];  // phase-1 slots
   __shared__ uint32_t s_rt[kAggSlots], s_rn[kAggSlots];
-  __shared__ unsigned long long s_ball[kLoopMaxBlk][kBlock / 64];
-  __shared__ int32_t s_lh[kAggLocal * kAggSlots];       // node-local histograms of the pod
-  __shared__ unsigned long long s_gh[kAggGWords];       // shared-region partials, then totals
-  __shared__ uint8_t s_elig[kAggSlots];                 // DoNotSchedule eligibility bits per node
+  __shared__ unsigned long long s_ball[kAggThreads / 64];  // [wave] feasibility ballots
+  __shared__ int32_t s_lh[kAggLocal * kAggSlots];          // node-local histograms
+  __shared__ unsigned long long s_gh[kAggGWords];          // shared-region partials, then totals
+  __shared__ uint8_t s_elig[kAggSlots];                    // DoNotSchedule eligibility bits per node
   __shared__ uint32_t s_pods[kAggPods], s_terms[kAggTerms];  // (slot | term) << 9 | node slot
   __shared__ uint32_t s_np, s_nt;
   __shared__ uint32_t s_off[kLoopMaxPods];
   __shared__ long long s_pmin[kMaxCons];
   __shared__ uint32_t s_pndom[kMaxCons];
-  __shared__ uint32_t s_any, s_ok, s_F, s_psb, s_acc;
+  __shared__ uint32_t s_any, s_gany, s_ok, s_F, s_psb, s_acc, s_gbar;
   __shared__ long long s_lmin[kAggLocalCons];
   __shared__ uint32_t s_lcnt[kAggLocalCons];
-  __shared__ int64_t s_mx[4];  // mx_t, mx_n, mx_i, mn_i
-  __shared__ uint32_t s_wu[kBlock / 64][2];
-  __shared__ unsigned long long s_wx[kBlock / 64][4];
-  __shared__ unsigned long long s_wk[kBlock / 64];
-  __shared__ int s_wn[kBlock / 64];
-  __shared__ int s_win;
+  __shared__ unsigned long long s_wx[kAggThreads / 64][4];
+  __shared__ uint32_t s_wu[kAggThreads / 64][2];
+  __shared__ int s_gnode, s_pend_ls;  // the chosen node of the pod just decided; my pending list append
   __shared__ unsigned long long s_best;
+  // the fold plan of pod q into pod q+1 (built while pod q is decided): what q+1's aggregation would
+  // add for pod q at its node, keyed by the label slot it is counted under
+  struct FoldItem { int32_t lref, slot, cons, wt; uint32_t anyb, pad; };
+  constexpr int kFoldMax = 80;
+  __shared__ FoldItem s_fi[kFoldMax];
+  __shared__ int32_t s_fv[kFoldMax];  // the chosen node's value id of each item's slot
+  __shared__ uint32_t s_nfi;
+  __shared__ int s_pw;                // participant whose key won the pod just decided
+  __shared__ uint32_t s_el;           // the chosen node's DoNotSchedule eligibility for the next pod
   const int w = blockIdx.x, G = av.nwg;
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int nlo = k0 * kBlock, nhi = k1 * kBlock < m.n ? k1 * kBlock : m.n;
   const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int kk = t / kBlock, tt = t % kBlock;  // my node slot t = kk * kBlock + tt
+  const int my_i = (k0 + kk) * kBlock + tt;
+  const bool my_node = kk < nk && my_i < m.n;
   auto stamp = [&](int q, int k) {
-    if (av.stamps && w == 0 && t == 0) av.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    if (av.stamps && w == 0 && t == 0) av.stamps[(size_t)q * kAggStamps + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto wstamp = [&](int q, int k) {  // thread 0 of every workgroup
+    if (av.wstamps && t == 0) av.wstamps[((size_t)q * G + w) * 4 + k] = __builtin_amdgcn_s_memrealtime();
   };
   auto fail = [&](uint32_t code) {
     __hip_atomic_store(av.fail + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  auto stage_prog = [&](int q, int slot, int tid, int nthr) __attribute__((always_inline)) {
+  auto stage_prog = [&](int q, int tid, int nthr) __attribute__((always_inline)) {
     const uint4* src = reinterpret_cast<const uint4*>(b.descs + s_off[q]);
     const uint32_t n16 = av.desc_bytes[av.first_pod + q] / 16u;
-    uint4* dst = reinterpret_cast<uint4*>(s_blob[slot]);
+    uint4* dst = reinterpret_cast<uint4*>(s_blob[q % 3]);
     for (uint32_t o = (uint32_t)tid; o < n16; o += (uint32_t)nthr) dst[o] = src[o];
   };
+  // spec(q): pod q's counts may be gathered before pod q-1 is placed, and pod q-1 folded in after
+  // (no node-local DoNotSchedule minimum, which would need the chosen node's own count)
+  auto spec = [&](const PodDesc& dn) { return dn.agg_local_cons == 0 && !(av.debug & 1); };
 
-  // ---- launch prologue: node cores, program offsets, my pods and terms
-#pragma unroll
-  for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-    const int i = (k0 + kk) * kBlock + t;
-    if (kk < nk && i < m.n) {
-      const NodeCore c = load_core(m, i);
-      s_core.acpu[kk][t] = c.acpu;
-      s_core.amem[kk][t] = c.amem;
-      s_core.aeph[kk][t] = c.aeph;
-      s_core.apods[kk][t] = c.apods;
-      s_core.flags[kk][t] = c.flags;
-      s_core.tlo[kk][t] = c.tlo;
-      s_core.thi[kk][t] = c.thi;
-      s_core.ilo[kk][t] = c.ilo;
-      s_core.ihi[kk][t] = c.ihi;
-      lds_put_dynamic(s_core, kk, t, c);
-    }
-  }
-  for (int k = t; k < av.npods; k += kBlock) s_off[k] = b.desc_off[av.first_pod + k];
-  if (t == 0) {
-    s_np = 0;
-    s_nt = 0;
-  }
-  __syncthreads();
-  for (int s = t; s < m.pods_hw; s += kBlock) {
-    const int n = m.pod_node[s];
-    if (n >= nlo && n < nhi) {
-      const uint32_t k = atomicAdd(&s_np, 1u);
-      if (k < (uint32_t)kAggPods) s_pods[k] = ((uint32_t)s << 9) | (uint32_t)(n - nlo);
-    }
-  }
-  for (int j = t; j < m.n_terms; j += kBlock) {
-    const DTerm tm = m.terms[j];
-    const int n = tm.kind >= 0 ? m.pod_node[tm.owner] : -1;
-    if (n >= nlo && n < nhi) {
-      const uint32_t k = atomicAdd(&s_nt, 1u);
-      if (k < (uint32_t)kAggTerms) s_terms[k] = ((uint32_t)j << 9) | (uint32_t)(n - nlo);
-    }
-  }
-  if (av.npods > 0) stage_prog(0, 0, t, kBlock);
-  __syncthreads();
-  if (s_np > (uint32_t)kAggPods || s_nt > (uint32_t)kAggTerms) {  // host-checked; never taken
-    if (t == 0) fail(0xfffffffeu);
-    return;
-  }
-
-  for (int q = 0; q < av.npods; ++q) {
-    const int pod = av.first_pod + q;
-    const uint8_t* base = s_blob[q & 1];
+  // ---- aggregation of pod q by threads [0, nthr) of a group (tid = my index in it), meeting at
+  // gbar(): the pod's selectors against my pods, my pods' terms against the pod, my nodes'
+  // DoNotSchedule eligibility; partials of shared keys into the pod's region; Z published by tid 0.
+  auto aggregate = [&](int q, int tid, int nthr, auto&& gbar) __attribute__((always_inline)) {
+    const uint8_t* base = s_blob[q % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
-    PodStats* ps = b.stats + pod;
     unsigned long long* region = av.region + (size_t)q * av.gwords;
     const int gw = d.agg_gwords, nl = d.agg_nlocal;
     const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
     const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
-    stamp(q, 0);
-
-    // ======== aggregation ========
-    for (int x = t; x < nl * kAggSlots; x += kBlock) s_lh[x] = 0;
-    for (int x = t; x < gw; x += kBlock) s_gh[x] = 0ull;
-    if (t == 0) s_any = 0;
-    __syncthreads();
+    for (int x = tid; x < nl * kAggSlots; x += nthr) s_lh[x] = 0;
+    for (int x = tid; x < gw; x += nthr) s_gh[x] = 0ull;
+    if (tid == 0) {
+      s_gany = 0;
+      s_lmin[0] = s_lmin[1] = 0x7fffffffffffffffll;
+      s_lcnt[0] = s_lcnt[1] = 0;
+    }
+    gbar();
     // node role: DoNotSchedule eligibility (nodeLabelsMatchSpreadConstraints + inclusion policies,
     // podtopologyspread/common.go:43-80) and the shared domains it makes present (filtering.go:255-311)
-#pragma unroll
-    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-      const int i = (k0 + kk) * kBlock + t;
+    for (int ls = tid; ls < kAggSlots; ls += nthr) {
+      const int i = nlo + ls;
       uint32_t el = 0;
-      if (kk < nk && i < m.n && d.n_ptsf) {
+      if (ls < nk * kBlock && i < m.n && d.n_ptsf) {
         el = pts_eligible(m, base, d, cf, d.n_ptsf, i);
         for (int32_t c = 0; c < d.n_ptsf; ++c)
           if (((el >> c) & 1u) && cf[c].lref >= 0) s_gh[cf[c].pref + node_label(m, cf[c].slot, i)] = 1ull;
       }
-      s_elig[kk * kBlock + t] = (uint8_t)el;
+      s_elig[ls] = (uint8_t)el;
     }
-    __syncthreads();
+    gbar();
     uint32_t any = 0;
     auto add = [&](int32_t lref, int32_t v, int ls, long long wt) __attribute__((always_inline)) {
       if (lref >= 0) atomicAdd(&s_gh[lref + v], (unsigned long long)wt);
       else atomicAdd(&s_lh[(-1 - lref) * kAggSlots + ls], (int32_t)wt);
     };
-    // pod role: the pod's selectors against the pods on my nodes (k_aggregate's pod role)
-    for (uint32_t k = (uint32_t)t; k < s_np; k += kBlock) {
-      const uint32_t e = s_pods[k];
-      const int s = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
-      const int32_t pns = m.pod_ns[s];
-      const bool term = (m.pod_flags[s] & 1u) != 0;
-      const unsigned long long* pl = m.lbl_pool + m.pod_lbl_off[s];
-      const int32_t pn = (int32_t)m.pod_lbl_cnt[s];
-      if (!term && pns == d.ns_id && d.n_ptsf) {  // calPreFilterState counts (filtering.go:255-300)
-        const uint32_t el = s_elig[ls];
-        for (int32_t c = 0; c < d.n_ptsf; ++c)
-          if (((el >> c) & 1u) && !lsel_empty(sp + cf[c].sel) && lsel_match(sp + cf[c].sel, pl, pn))
-            add(cf[c].lref, node_label(m, cf[c].slot, n), ls, 1);
-      }
-      if (d.n_raff) {  // affinityCounts (filtering.go:256-266)
-        const IpaTerm* ts = at<IpaTerm>(base, d.raff_off);
-        bool all = true;
-        for (int32_t k2 = 0; k2 < d.n_raff; ++k2) all = all && term_matches_pod(sp, ts[k2], pns, pl, pn);
-        if (all)
-          for (int32_t k2 = 0; k2 < d.n_raff; ++k2) {
-            const int32_t v = node_label(m, ts[k2].slot, n);
-            if (v >= 0) {
-              add(ts[k2].lref, v, ls, 1);
-              any |= 1u;
+    const uint32_t np = s_np, nitems = s_np + ((d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE)) ? s_nt : 0u);
+    for (uint32_t k = (uint32_t)tid; k < nitems; k += (uint32_t)nthr) {
+      if (k < np) {
+        // pod role: the pod's selectors against one pod on my nodes (k_aggregate's pod role)
+        const uint32_t e = s_pods[k];
+        const int s = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
+        const int32_t pns = m.pod_ns[s];
+        const bool term = (m.pod_flags[s] & 1u) != 0;
+        const unsigned long long* pl = m.lbl_pool + m.pod_lbl_off[s];
+        const int32_t pn = (int32_t)m.pod_lbl_cnt[s];
+        if (!term && pns == d.ns_id && d.n_ptsf) {  // calPreFilterState counts (filtering.go:255-300)
+          const uint32_t el = s_elig[ls];
+          for (int32_t c = 0; c < d.n_ptsf; ++c)
+            if (((el >> c) & 1u) && !lsel_empty(sp + cf[c].sel) && lsel_match(sp + cf[c].sel, pl, pn))
+              add(cf[c].lref, node_label(m, cf[c].slot, n), ls, 1);
+        }
+        if (d.n_raff) {  // affinityCounts (filtering.go:256-266)
+          const IpaTerm* ts = at<IpaTerm>(base, d.raff_off);
+          bool all = true;
+          for (int32_t k2 = 0; k2 < d.n_raff; ++k2) all = all && term_matches_pod(sp, ts[k2], pns, pl, pn);
+          if (all)
+            for (int32_t k2 = 0; k2 < d.n_raff; ++k2) {
+              const int32_t v = node_label(m, ts[k2].slot, n);
+              if (v >= 0) {
+                add(ts[k2].lref, v, ls, 1);
+                any |= 1u;
+              }
             }
-          }
-      }
-      if (d.n_ranti) {  // antiAffinityCounts (filtering.go:268-276)
-        const IpaTerm* ts = at<IpaTerm>(base, d.ranti_off);
-        for (int32_t k2 = 0; k2 < d.n_ranti; ++k2)
-          if (term_matches_pod(sp, ts[k2], pns, pl, pn)) {
-            const int32_t v = node_label(m, ts[k2].slot, n);
-            if (v >= 0) {
-              add(ts[k2].lref, v, ls, 1);
-              any |= 2u;
+        }
+        if (d.n_ranti) {  // antiAffinityCounts (filtering.go:268-276)
+          const IpaTerm* ts = at<IpaTerm>(base, d.ranti_off);
+          for (int32_t k2 = 0; k2 < d.n_ranti; ++k2)
+            if (term_matches_pod(sp, ts[k2], pns, pl, pn)) {
+              const int32_t v = node_label(m, ts[k2].slot, n);
+              if (v >= 0) {
+                add(ts[k2].lref, v, ls, 1);
+                any |= 2u;
+              }
             }
-          }
-      }
-      if (d.ipa_flags & IPA_PREF) {  // the incoming pod's soft terms (scoring.go:98-110)
-        const IpaTerm* ta = at<IpaTerm>(base, d.paff_off);
-        for (int32_t k2 = 0; k2 < d.n_paff; ++k2)
-          if (term_matches_pod(sp, ta[k2], pns, pl, pn)) {
-            const int32_t v = node_label(m, ta[k2].slot, n);
-            if (v >= 0) {
-              add(ta[k2].lref, v, ls, ta[k2].weight);
-              any |= 8u;
+        }
+        if (d.ipa_flags & IPA_PREF) {  // the incoming pod's soft terms (scoring.go:98-110)
+          const IpaTerm* ta = at<IpaTerm>(base, d.paff_off);
+          for (int32_t k2 = 0; k2 < d.n_paff; ++k2)
+            if (term_matches_pod(sp, ta[k2], pns, pl, pn)) {
+              const int32_t v = node_label(m, ta[k2].slot, n);
+              if (v >= 0) {
+                add(ta[k2].lref, v, ls, ta[k2].weight);
+                any |= 8u;
+              }
             }
-          }
-        const IpaTerm* tn = at<IpaTerm>(base, d.panti_off);
-        for (int32_t k2 = 0; k2 < d.n_panti; ++k2)
-          if (term_matches_pod(sp, tn[k2], pns, pl, pn)) {
-            const int32_t v = node_label(m, tn[k2].slot, n);
-            if (v >= 0) {
-              add(tn[k2].lref, v, ls, -(long long)tn[k2].weight);
-              any |= 8u;
+          const IpaTerm* tn = at<IpaTerm>(base, d.panti_off);
+          for (int32_t k2 = 0; k2 < d.n_panti; ++k2)
+            if (term_matches_pod(sp, tn[k2], pns, pl, pn)) {
+              const int32_t v = node_label(m, tn[k2].slot, n);
+              if (v >= 0) {
+                add(tn[k2].lref, v, ls, -(long long)tn[k2].weight);
+                any |= 8u;
+              }
             }
-          }
-      }
-    }
-    // term role: my pods' existing affinity terms against the incoming pod (k_aggregate's term role)
-    if (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE))
-      for (uint32_t k = (uint32_t)t; k < s_nt; k += kBlock) {
-        const uint32_t e = s_terms[k];
+        }
+      } else {
+        // term role: one existing affinity term of a pod on my nodes against the incoming pod
+        const uint32_t e = s_terms[k - np];
         const int j = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
         const DTerm tm = m.terms[j];
         if (tm.key >= d.n_keytab) continue;
@@ -2406,201 +2418,369 @@ __global__ __launch_bounds__(kBlock) void k_agg_loop(MirrorView m, BatchView b, 
           any |= anti ? 4u : 8u;
         }
       }
-    if (any) atomicOr(&s_any, any);
-    __syncthreads();
+    }
+    if (any) atomicOr(&s_gany, any);
+    gbar();
     // my partials of the shared region; node-local DoNotSchedule minima over my eligible nodes
-    for (int x = t; x < gw; x += kBlock)
+    for (int x = tid; x < gw; x += nthr)
       if (s_gh[x]) atomicAdd(region + x, s_gh[x]);
-    {
+    if (d.agg_local_cons) {
       int li = 0;
       for (int32_t c = 0; c < d.n_ptsf && li < kAggLocalCons; ++c) {
         if (!((d.agg_local_cons >> c) & 1)) continue;
         long long mn = 0x7fffffffffffffffll;
         uint32_t cnt = 0;
-        for (int kk = 0; kk < nk; ++kk)
-          if ((s_elig[kk * kBlock + t] >> c) & 1u) {
-            const long long x = s_lh[(size_t)(-1 - cf[c].lref) * kAggSlots + kk * kBlock + t];
+        for (int ls = tid; ls < kAggSlots; ls += nthr)
+          if ((s_elig[ls] >> c) & 1u) {
+            const long long x = s_lh[(size_t)(-1 - cf[c].lref) * kAggSlots + ls];
             mn = x < mn ? x : mn;
             ++cnt;
           }
-        mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
-        cnt = wave_sum_u32(cnt);
-        if (lane == 0) {
-          s_wx[wave][li] = (unsigned long long)mn;
-          s_wu[wave][li] = cnt;
+        if (cnt) {
+          atomicMin(&s_lmin[li], mn);
+          atomicAdd(&s_lcnt[li], cnt);
         }
         ++li;
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my region atomics performed before Z
-    __syncthreads();
-    if (t == 0) {  // every Z granule is published (zero for an absent constraint)
-      unsigned long long z1 = 0, z2 = 0;
-      int li = 0;
-      for (int32_t c = 0; c < d.n_ptsf && li < kAggLocalCons; ++c) {
-        if (!((d.agg_local_cons >> c) & 1)) continue;
-        long long mn = 0x7fffffffffffffffll;
-        uint32_t cnt = 0;
-        for (int v = 0; v < kBlock / 64; ++v) {
-          const long long x = (long long)s_wx[v][li];
-          mn = x < mn ? x : mn;
-          cnt += s_wu[v][li];
-        }
+    gbar();
+    if (tid == 0) {  // every Z granule is published (zero for an absent constraint)
+      unsigned long long z[2] = {0, 0};
+      for (int li = 0; li < kAggLocalCons; ++li) {
+        const long long mn = s_lmin[li];
         const unsigned long long m24 = mn > 0xffffffll ? 0xffffffull : (unsigned long long)mn;
-        const unsigned long long zz = ((unsigned long long)cnt << 24) | m24;  // no eligible node: min 2^24-1
-        if (li == 0) z1 = zz;
-        else z2 = zz;
-        ++li;
+        z[li] = ((unsigned long long)s_lcnt[li] << 24) | m24;  // no eligible node: min 2^24-1
       }
-      agran_put(av, q, w, AG_Z0, s_any);
-      agran_put(av, q, w, AG_Z1, z1);
-      agran_put(av, q, w, AG_Z2, z2);
+      agran_put(av, q, w, AG_Z0, s_gany);
+      agran_put(av, q, w, AG_Z1, z[0]);
+      agran_put(av, q, w, AG_Z2, z[1]);
     }
-    stamp(q, 1);
-
-    // ======== exchange Z (wave 0), the next program's staging (waves 1-3) ========
-    if (wave == 0) {
-      unsigned long long z[3][kMaxSweep];
-      const bool ok = agran_sweep<3>(av, q, AG_Z0, z);
-      uint32_t a = 0, c1 = 0, c2 = 0;
-      unsigned long long m1 = 0xffffffull, m2 = 0xffffffull;
+  };
+  // exchange Z of pod q (wave 0): OR of the any bits, node-local minima and domain counts
+  auto sweep_z = [&](int q) __attribute__((always_inline)) {
+    unsigned long long z[3][kMaxSweep];
+    const bool ok = agran_sweep<3>(av, q, AG_Z0, z);
+    uint32_t a = 0, c1 = 0, c2 = 0;
+    unsigned long long m1 = 0xffffffull, m2 = 0xffffffull;
 #pragma unroll
-      for (int r = 0; r < kMaxSweep; ++r)
-        if (lane + 64 * r < G) {
-          a |= (uint32_t)z[0][r];
-          const unsigned long long x1 = z[1][r] & 0xffffffull, x2 = z[2][r] & 0xffffffull;
-          c1 += (uint32_t)(z[1][r] >> 24);
-          c2 += (uint32_t)(z[2][r] >> 24);
-          m1 = x1 < m1 ? x1 : m1;
-          m2 = x2 < m2 ? x2 : m2;
-        }
-      for (int o = 32; o > 0; o >>= 1) {
-        a |= (uint32_t)__shfl_xor((int)a, o, 64);
-        const unsigned long long y1 = __shfl_xor(m1, o, 64), y2 = __shfl_xor(m2, o, 64);
-        m1 = y1 < m1 ? y1 : m1;
-        m2 = y2 < m2 ? y2 : m2;
+    for (int r = 0; r < kMaxSweep; ++r)
+      if (lane + 64 * r < G) {
+        a |= (uint32_t)z[0][r];
+        const unsigned long long x1 = z[1][r] & 0xffffffull, x2 = z[2][r] & 0xffffffull;
+        c1 += (uint32_t)(z[1][r] >> 24);
+        c2 += (uint32_t)(z[2][r] >> 24);
+        m1 = x1 < m1 ? x1 : m1;
+        m2 = x2 < m2 ? x2 : m2;
       }
-      c1 = wave_sum_u32(c1);
-      c2 = wave_sum_u32(c2);
-      if (lane == 0) {
-        s_ok = ok ? 1u : 0u;
-        s_any = a;
-        s_lmin[0] = (long long)m1;
-        s_lmin[1] = (long long)m2;
-        s_lcnt[0] = c1;
-        s_lcnt[1] = c2;
-      }
-    } else if (q + 1 < av.npods) {
-      stage_prog(q + 1, (q + 1) & 1, t - 64, kBlock - 64);  // s_blob[(q + 1) & 1] held pod q-1
+    for (int o = 32; o > 0; o >>= 1) {
+      a |= (uint32_t)__shfl_xor((int)a, o, 64);
+      const unsigned long long y1 = __shfl_xor(m1, o, 64), y2 = __shfl_xor(m2, o, 64);
+      m1 = y1 < m1 ? y1 : m1;
+      m2 = y2 < m2 ? y2 : m2;
     }
+    c1 = wave_sum_u32(c1);
+    c2 = wave_sum_u32(c2);
+    if (lane == 0) {
+      if (!ok) s_ok = 0u;
+      s_any = a;
+      s_lmin[0] = (long long)m1;
+      s_lmin[1] = (long long)m2;
+      s_lcnt[0] = c1;
+      s_lcnt[1] = c2;
+    }
+  };
+  // the region's totals into LDS (all threads; then a barrier)
+  auto load_totals = [&](int q, int tid, int nthr) __attribute__((always_inline)) {
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(s_blob[q % 3]);
+    const unsigned long long* region = av.region + (size_t)q * av.gwords;
+    for (int x = tid; x < d.agg_gwords; x += nthr)
+      s_gh[x] = __hip_atomic_load(region + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // DoNotSchedule minima (criticalPaths, filtering.go:64-124): shared constraints over their present
+  // domains (one wave each), node-local ones from exchange Z (all threads; then a barrier)
+  auto minima = [&](int q) __attribute__((always_inline)) {
+    const uint8_t* base = s_blob[q % 3];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
+    int li = 0;
+    for (int32_t c = 0; c < d.n_ptsf; ++c) {
+      if ((d.agg_local_cons >> c) & 1) {
+        if (t == 0) {
+          s_pmin[c] = li < kAggLocalCons ? s_lmin[li] : 0;
+          s_pndom[c] = li < kAggLocalCons ? s_lcnt[li] : 0;
+        }
+        ++li;
+        continue;
+      }
+      if (wave != (c & 7)) continue;
+      long long mn = 0x7fffffffffffffffll;
+      uint32_t cnt = 0;
+      for (int v = lane; v < cf[c].nvals; v += 64)
+        if (s_gh[cf[c].pref + v]) {
+          const long long x = (long long)s_gh[cf[c].lref + v];
+          mn = x < mn ? x : mn;
+          ++cnt;
+        }
+      mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
+      cnt = wave_sum_u32(cnt);
+      if (lane == 0) {
+        s_pmin[c] = mn;
+        s_pndom[c] = cnt;
+      }
+    }
+  };
+  // minima() by wave 0 alone, for a pod without node-local constraints (the folded path)
+  auto minima_w0 = [&](int q) __attribute__((always_inline)) {
+    const uint8_t* base = s_blob[q % 3];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
+    for (int32_t c = 0; c < d.n_ptsf; ++c) {
+      long long mn = 0x7fffffffffffffffll;
+      uint32_t cnt = 0;
+      for (int v = lane; v < cf[c].nvals; v += 64)
+        if (s_gh[cf[c].pref + v]) {
+          const long long x = (long long)s_gh[cf[c].lref + v];
+          mn = x < mn ? x : mn;
+          ++cnt;
+        }
+      mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
+      cnt = wave_sum_u32(cnt);
+      if (lane == 0) {
+        s_pmin[c] = mn;
+        s_pndom[c] = cnt;
+      }
+    }
+  };
+  // The fold plan of pod q into pod q + 1 (one wave, lanes gl): pod q as an existing pod of q+1 --
+  // its labels against q+1's selectors, its own terms against q+1 -- exactly what q+1's aggregation
+  // would count for it, less the chosen node's label values (looked up once the node is known).
+  auto plan_fold = [&](int q, int gl) __attribute__((always_inline)) {
+    const uint8_t* bp = s_blob[q % 3];
+    const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
+    const uint8_t* base = s_blob[(q + 1) % 3];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+    const unsigned long long* pl = at<unsigned long long>(bp, dp.lbl_off);
+    const int32_t pn = dp.n_lbl, pns = dp.ns_id;
+    const bool term = (dp.flags & DF_TERMINATING) != 0;
+    // (s_nfi was reset after the previous fold: a reset here by one lane would race the others' pushes)
+    auto push = [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb) __attribute__((always_inline)) {
+      const uint32_t k = atomicAdd(&s_nfi, 1u);
+      if (k < (uint32_t)kFoldMax) s_fi[k] = FoldItem{lref, slot, cons, wt, anyb, 0u};
+    };
+    // lane 0: PodTopologySpread + required affinity; 1..8 ranti; 9..16 paff; 17..24 panti; 32.. own terms
+    if (gl == 0) {
+      if (!term && pns == d.ns_id && d.n_ptsf) {
+        const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
+        for (int32_t c = 0; c < d.n_ptsf; ++c)
+          if (!lsel_empty(sp + cf[c].sel) && lsel_match(sp + cf[c].sel, pl, pn)) push(cf[c].lref, cf[c].slot, c, 1, 0u);
+      }
+      if (d.n_raff) {
+        const IpaTerm* ts = at<IpaTerm>(base, d.raff_off);
+        bool all = true;
+        for (int32_t k2 = 0; k2 < d.n_raff; ++k2) all = all && term_matches_pod(sp, ts[k2], pns, pl, pn);
+        if (all)
+          for (int32_t k2 = 0; k2 < d.n_raff; ++k2) push(ts[k2].lref, ts[k2].slot, -1, 1, 1u);
+      }
+    } else if (gl <= 8) {
+      const int k2 = gl - 1;
+      const IpaTerm* ts = at<IpaTerm>(base, d.ranti_off);
+      if (k2 < d.n_ranti && term_matches_pod(sp, ts[k2], pns, pl, pn)) push(ts[k2].lref, ts[k2].slot, -1, 1, 2u);
+    } else if (gl <= 24) {
+      const bool aff = gl <= 16;
+      const int k2 = aff ? gl - 9 : gl - 17;
+      const IpaTerm* ts = at<IpaTerm>(base, aff ? d.paff_off : d.panti_off);
+      if ((d.ipa_flags & IPA_PREF) && k2 < (aff ? d.n_paff : d.n_panti) && term_matches_pod(sp, ts[k2], pns, pl, pn))
+        push(ts[k2].lref, ts[k2].slot, -1, aff ? ts[k2].weight : -ts[k2].weight, 8u);
+    } else if (gl >= 32 && (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE))) {
+      const int32_t* own = at<int32_t>(bp, dp.own_terms_off);
+      for (int k2 = gl - 32; k2 < dp.n_own_terms; k2 += 32) {
+        const DTerm tm = m.terms[own[k2]];
+        if (tm.key >= d.n_keytab) continue;
+        const int32_t* kt = at<int32_t>(base, d.keytab_off) + (size_t)tm.key * kKeytabStride;
+        const bool anti = tm.kind == T_REQ_ANTI;
+        const int32_t hb = anti ? ((d.ipa_flags & IPA_EXIST_FILTER) ? kt[1] : -1)
+                                : ((d.ipa_flags & IPA_EXIST_SCORE) ? kt[2] : -1);
+        int32_t wt = 0;
+        if (tm.kind == T_REQ_AFF) wt = d.hard_weight;
+        else if (tm.kind == T_PREF_AFF) wt = tm.weight;
+        else if (tm.kind == T_PREF_ANTI) wt = -tm.weight;
+        else wt = 1;
+        if (hb < 0 || wt == 0) continue;
+        const int32_t* tp = m.term_pool;
+        const unsigned long long* il = at<unsigned long long>(base, d.lbl_off);
+        const unsigned long long* nsl = at<unsigned long long>(base, d.nslbl_off);
+        if ((id_in(tp + tm.ns_off, tm.ns_cnt, d.ns_id) || lsel_match(tp + tm.nssel, nsl, d.n_nslbl)) &&
+            lsel_match(tp + tm.sel, il, d.n_lbl))
+          push(anti ? kt[3] : kt[4], kt[0], -1, wt, anti ? 4u : 8u);
+      }
+    }
+  };
+  // the owner of pod q's node adds it (and its own terms) to my lists: one thread
+  auto append = [&](int q, int lq) __attribute__((always_inline)) {
+    const uint8_t* bp = s_blob[q % 3];
+    const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
+    const uint32_t np = s_np, nt = s_nt;
+    if (np < (uint32_t)kAggPods) s_pods[np] = ((uint32_t)dp.slot << 9) | (uint32_t)lq;
+    const int32_t* own = at<int32_t>(bp, dp.own_terms_off);
+    uint32_t k2 = 0;
+    for (; k2 < (uint32_t)dp.n_own_terms && nt + k2 < (uint32_t)kAggTerms; ++k2)
+      s_terms[nt + k2] = ((uint32_t)own[k2] << 9) | (uint32_t)lq;
+    s_np = np + 1;
+    s_nt = nt + k2;
+    if (np >= (uint32_t)kAggPods || k2 < (uint32_t)dp.n_own_terms) fail(0xfffffffdu);  // host-checked
+  };
+  auto wg_bar = [&]() __attribute__((always_inline)) { __syncthreads(); };
+
+  // ---- launch prologue: node cores, program offsets, my pods and terms, the first pod's counts
+  if (my_node) {
+    const NodeCore c = load_core(m, my_i);
+    s_core.acpu[kk][tt] = c.acpu;
+    s_core.amem[kk][tt] = c.amem;
+    s_core.aeph[kk][tt] = c.aeph;
+    s_core.apods[kk][tt] = c.apods;
+    s_core.flags[kk][tt] = c.flags;
+    s_core.tlo[kk][tt] = c.tlo;
+    s_core.thi[kk][tt] = c.thi;
+    s_core.ilo[kk][tt] = c.ilo;
+    s_core.ihi[kk][tt] = c.ihi;
+    lds_put_dynamic(s_core, kk, tt, c);
+  }
+  for (int k = t; k < av.npods; k += kAggThreads) s_off[k] = b.desc_off[av.first_pod + k];
+  if (t == 0) {
+    s_np = 0;
+    s_nt = 0;
+    s_gbar = 0;
+    s_ok = 1;
+    s_pend_ls = -1;
+    s_nfi = 0;
+  }
+  __syncthreads();
+  for (int s = t; s < m.pods_hw; s += kAggThreads) {
+    const int n = m.pod_node[s];
+    if (n >= nlo && n < nhi) {
+      const uint32_t k = atomicAdd(&s_np, 1u);
+      if (k < (uint32_t)kAggPods) s_pods[k] = ((uint32_t)s << 9) | (uint32_t)(n - nlo);
+    }
+  }
+  for (int j = t; j < m.n_terms; j += kAggThreads) {
+    const DTerm tm = m.terms[j];
+    const int n = tm.kind >= 0 ? m.pod_node[tm.owner] : -1;
+    if (n >= nlo && n < nhi) {
+      const uint32_t k = atomicAdd(&s_nt, 1u);
+      if (k < (uint32_t)kAggTerms) s_terms[k] = ((uint32_t)j << 9) | (uint32_t)(n - nlo);
+    }
+  }
+  if (av.npods > 0) stage_prog(0, t, kAggThreads);
+  if (av.npods > 1) stage_prog(1, t, kAggThreads);
+  __syncthreads();
+  if (s_np > (uint32_t)kAggPods || s_nt > (uint32_t)kAggTerms) {  // host-checked; never taken
+    if (t == 0) fail(0xfffffffeu);
+    return;
+  }
+  if (av.npods > 0) {
+    aggregate(0, t, kAggThreads, wg_bar);
+    if (wave == 0) sweep_z(0);
     __syncthreads();
     if (!s_ok) return;
-    stamp(q, 2);
-    for (int x = t; x < gw; x += kBlock) s_gh[x] = __hip_atomic_load(region + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    load_totals(0, t, kAggThreads);
     __syncthreads();
-    // DoNotSchedule minima (criticalPaths, filtering.go:64-124): shared constraints over their
-    // present domains (one wave each), node-local ones from exchange Z
+    minima(0);
+    __syncthreads();
+  }
+  uint32_t gtarget = 0;  // waves 1..7: arrivals their group barrier waits for (s_gbar is monotonic)
+  auto grp_bar = [&]() __attribute__((always_inline)) {
+    gtarget += kAggThreads / 64 - 1;
+    if (lane == 0) __hip_atomic_fetch_add(&s_gbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&s_gbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gtarget)
+      __builtin_amdgcn_s_sleep(1);
+  };
+
+  for (int q = 0; q < av.npods; ++q) {
+    const int pod = av.first_pod + q;
+    const uint8_t* base = s_blob[q % 3];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    PodStats* ps = b.stats + pod;
+    const bool more = q + 1 < av.npods;
+    const bool sp1 = more && spec(*reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3]));
+    stamp(q, 0);
+    wstamp(q, 0);
+
+    // ======== phase 1: my node (LDS core, LDS counts) ========
     {
-      int li = 0;
-      for (int32_t c = 0; c < d.n_ptsf; ++c) {
-        if ((d.agg_local_cons >> c) & 1) {
-          if (t == 0) {
-            s_pmin[c] = li < kAggLocalCons ? s_lmin[li] : 0;
-            s_pndom[c] = li < kAggLocalCons ? s_lcnt[li] : 0;
-          }
-          ++li;
-          continue;
-        }
-        if (wave != (c & 3)) continue;
-        long long mn = 0x7fffffffffffffffll;
-        uint32_t cnt = 0;
-        for (int v = lane; v < cf[c].nvals; v += 64)
-          if (s_gh[cf[c].pref + v]) {
-            const long long x = (long long)s_gh[cf[c].lref + v];
-            mn = x < mn ? x : mn;
-            ++cnt;
-          }
-        mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
-        cnt = wave_sum_u32(cnt);
-        if (lane == 0) {
-          s_pmin[c] = mn;
-          s_pndom[c] = cnt;
-        }
+      const AggTopo tp{s_gh, s_lh, s_pmin, s_pndom, s_any};
+      NodeEval ne{1u, false, 0, 0, 0, 0};
+      PodFast pf;
+      if ((d.flags & DF_LFAST) && !(av.debug & 2)) pf = load_fast(base, d);
+      else pf.flags = d.flags & ~DF_LFAST;
+      if (my_node) ne = eval_agg(m, lds_core(s_core, kk, tt), s_core.bwo[kk][tt], pf, base, d, my_i, tp, t);
+      const bool feas = ne.st == 0;
+      const unsigned long long ballot = __ballot(feas);
+      const int lim = d.rot_start - (nlo + wave * 64);
+      const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+      s_fx[t] = ne.fixed;
+      s_rt[t] = (uint32_t)ne.rt;
+      s_rn[t] = (uint32_t)ne.rna;
+      s_ri[t] = ne.ripa;
+      unsigned long long et = 0, en = 0, ei = 0, ni = ~0ull;
+      if (feas) {
+        et = enc_i64(ne.rt);
+        en = enc_i64(ne.rna);
+        ei = enc_i64(ne.ripa);
+        ni = ei;
+      }
+      et = wave_max_u64(et);
+      en = wave_max_u64(en);
+      ei = wave_max_u64(ei);
+      ni = ~wave_max_u64(~ni);
+      if (lane == 0) {
+        s_ball[wave] = ballot;
+        s_wu[wave][0] = (uint32_t)__popcll(ballot);
+        s_wu[wave][1] = (uint32_t)__popcll(ballot & bm);
+        s_wx[wave][0] = et;
+        s_wx[wave][1] = en;
+        s_wx[wave][2] = ei;
+        s_wx[wave][3] = ni;
       }
     }
     __syncthreads();
-    stamp(q, 3);
-
-    // ======== phase 1: my nodes ========
-    const AggTopo tp{s_gh, s_lh, s_pmin, s_pndom, s_any};
-    uint32_t w_cnt = 0, w_below = 0;
-    unsigned long long t_mt = 0, t_mn = 0, t_mi = 0, t_ni = ~0ull;
-#pragma unroll
-    for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-      if (kk < nk) {
-        const int i = (k0 + kk) * kBlock + t, ls = kk * kBlock + t;
-        NodeEval ne{1u, false, 0, 0, 0, 0};
-        if (i < m.n) ne = eval_agg(m, lds_core(s_core, kk, t), base, d, i, tp, ls);
-        const bool feas = ne.st == 0;
-        const unsigned long long ballot = __ballot(feas);
-        if (lane == 0) s_ball[kk][wave] = ballot;
-        const int lim = d.rot_start - ((k0 + kk) * kBlock + wave * 64);
-        const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
-        w_cnt += (uint32_t)__popcll(ballot);
-        w_below += (uint32_t)__popcll(ballot & bm);
-        s_fx[ls] = ne.fixed;
-        s_rt[ls] = (uint32_t)ne.rt;
-        s_rn[ls] = (uint32_t)ne.rna;
-        s_ri[ls] = ne.ripa;
-        if (feas) {
-          const unsigned long long et = enc_i64(ne.rt), en = enc_i64(ne.rna), ei = enc_i64(ne.ripa);
-          t_mt = et > t_mt ? et : t_mt;
-          t_mn = en > t_mn ? en : t_mn;
-          t_mi = ei > t_mi ? ei : t_mi;
-          t_ni = ei < t_ni ? ei : t_ni;
-        }
+    stamp(q, 1);
+    const uint32_t ipa_any = s_any;
+    if (av.debug & 32) {  // diagnostic: the speculative gathering first, not beside wave 0's work
+      if (wave != 0 && sp1) {
+        aggregate(q + 1, t - 64, kAggThreads - 64, grp_bar);
+        if (wave == 1) plan_fold(q, lane);
       }
+      __syncthreads();
     }
-    t_mt = wave_max_u64(t_mt);
-    t_mn = wave_max_u64(t_mn);
-    t_mi = wave_max_u64(t_mi);
-    t_ni = ~wave_max_u64(~t_ni);
-    if (lane == 0) {
-      s_wu[wave][0] = w_cnt;
-      s_wu[wave][1] = w_below;
-      s_wx[wave][0] = t_mt;
-      s_wx[wave][1] = t_mn;
-      s_wx[wave][2] = t_mi;
-      s_wx[wave][3] = t_ni;
-    }
-    __syncthreads();
-    if (t == 0) {
-      uint32_t c = 0, bl = 0;
-      unsigned long long a = 0, bb = 0, mi = 0, ni = ~0ull;
-      for (int v = 0; v < kBlock / 64; ++v) {
-        c += s_wu[v][0];
-        bl += s_wu[v][1];
-        a = s_wx[v][0] > a ? s_wx[v][0] : a;
-        bb = s_wx[v][1] > bb ? s_wx[v][1] : bb;
-        mi = s_wx[v][2] > mi ? s_wx[v][2] : mi;
-        ni = s_wx[v][3] < ni ? s_wx[v][3] : ni;
-      }
-      unsigned long long g0, g1;
-      a_granules(c, bl, a, bb, &g0, &g1);
-      // raw InterPodAffinity biased into [1, 2^47): max as is, min reversed (max of 2^47 - x)
-      const unsigned long long bi = c ? (unsigned long long)(dec_i64(mi) + kAggIpaBias) + 1ull : 0ull;
-      const unsigned long long bn = c ? (1ull << 47) - (unsigned long long)(dec_i64(ni) + kAggIpaBias) : 0ull;
-      agran_put(av, q, w, AG_A0, g0);
-      agran_put(av, q, w, AG_A1, g1);
-      agran_put(av, q, w, AG_A2, bi);
-      agran_put(av, q, w, AG_A3, bn);
-    }
-    stamp(q, 4);
 
-    // ======== exchange A (wave 0) ========
     if (wave == 0) {
+      // ======== wave 0: exchange A, phase 2, exchange B, commit ========
+      if (lane == 0) {
+        uint32_t c = 0, bl = 0;
+        unsigned long long a = 0, bb = 0, mi = 0, ni = ~0ull;
+        for (int v = 0; v < kAggThreads / 64; ++v) {
+          c += s_wu[v][0];
+          bl += s_wu[v][1];
+          a = s_wx[v][0] > a ? s_wx[v][0] : a;
+          bb = s_wx[v][1] > bb ? s_wx[v][1] : bb;
+          mi = s_wx[v][2] > mi ? s_wx[v][2] : mi;
+          ni = s_wx[v][3] < ni ? s_wx[v][3] : ni;
+        }
+        unsigned long long g0, g1;
+        a_granules(c, bl, a, bb, &g0, &g1);
+        // raw InterPodAffinity biased into [1, 2^47): max as is, min reversed (max of 2^47 - x)
+        const unsigned long long bi = c ? (unsigned long long)(dec_i64(mi) + kAggIpaBias) + 1ull : 0ull;
+        const unsigned long long bn = c ? (1ull << 47) - (unsigned long long)(dec_i64(ni) + kAggIpaBias) : 0ull;
+        agran_put(av, q, w, AG_A0, g0);
+        agran_put(av, q, w, AG_A1, g1);
+        agran_put(av, q, w, AG_A2, bi);
+        agran_put(av, q, w, AG_A3, bn);
+        wstamp(q, 1);
+      }
       unsigned long long xa[4][kMaxSweep];
-      const bool ok = agran_sweep<4>(av, q, AG_A0, xa);
+      bool ok = agran_sweep<4>(av, q, AG_A0, xa);
       uint32_t F = 0, wp = 0, bf = 0;
       unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
 #pragma unroll
@@ -2619,131 +2799,194 @@ __global__ __launch_bounds__(kBlock) void k_agg_loop(MirrorView m, BatchView b, 
         }
       }
       F = wave_sum_u32(F);
-      bf = wave_sum_u32(bf);
-      wp = wave_sum_u32(wp);
+      const uint32_t ps_before = wave_sum_u32(bf);
+      uint32_t acc = wave_sum_u32(wp);
       tmax = wave_max_u64(tmax);
       nmax = wave_max_u64(nmax);
       imax = wave_max_u64(imax);
       inmax = wave_max_u64(inmax);
-      if (lane == 0) {
-        s_ok = ok ? 1u : 0u;
-        s_F = F;
-        s_psb = bf;
-        s_acc = wp;
-        s_mx[0] = tmax ? (int64_t)tmax - 1 : 0;
-        s_mx[1] = nmax ? (int64_t)nmax - 1 : 0;
-        s_mx[2] = imax ? (int64_t)(imax - 1ull) - kAggIpaBias : 0;
-        s_mx[3] = inmax ? (int64_t)((1ull << 47) - inmax) - kAggIpaBias : 0;
-      }
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    stamp(q, 5);
-
-    // ======== phase 2: positions, NormalizeScore + weights, my best packed key ========
-    const uint32_t F = s_F, ps_before = s_psb;
-    const int64_t mx_t = s_mx[0], mx_n = s_mx[1], mx_i = s_mx[2], mn_i = s_mx[3];
-    const uint32_t ipa_any = s_any;
-    unsigned long long key = 0;
-    int knode = -1;
-    {
-      uint32_t acc = s_acc;
+      const int64_t mx_t = tmax ? (int64_t)tmax - 1 : 0, mx_n = nmax ? (int64_t)nmax - 1 : 0;
+      const int64_t mx_i = imax ? (int64_t)(imax - 1ull) - kAggIpaBias : 0;
+      const int64_t mn_i = inmax ? (int64_t)((1ull << 47) - inmax) - kAggIpaBias : 0;
+      stamp(q, 2);
+      // phase 2 over my 512 slots: positions, NormalizeScore + weights, the best packed key
+      unsigned long long key = 0;
+      int knode = -1;
+      if (ok) {
 #pragma unroll
-      for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-        if (kk < nk) {
-          uint32_t pre = 0;
-          for (int v = 0; v < kBlock / 64; ++v) pre += v < wave ? (uint32_t)__popcll(s_ball[kk][v]) : 0u;
-          const unsigned long long ballot = s_ball[kk][wave];
-          const int ls = kk * kBlock + t;
+        for (int v = 0; v < kAggThreads / 64; ++v) {
+          const unsigned long long ballot = s_ball[v];
+          const int ls = v * 64 + lane;
           if ((ballot >> lane) & 1ull) {
-            const uint32_t g = acc + pre + wave_prefix_count(ballot, lane);
+            const uint32_t g = acc + wave_prefix_count(ballot, lane);
             const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
             const int64_t total = agg_total(d, s_fx[ls], s_rt[ls], s_rn[ls], s_ri[ls], mx_t, mx_n, mx_i, mn_i, ipa_any);
             const unsigned long long kv = pack_best(total, pos);
             if (kv > key) {
               key = kv;
-              knode = (k0 + kk) * kBlock + t;
+              knode = nlo + ls;
             }
           }
-          for (int v = 0; v < kBlock / 64; ++v) acc += (uint32_t)__popcll(s_ball[kk][v]);
+          acc += (uint32_t)__popcll(ballot);
         }
       }
-    }
-    {
       const unsigned long long wk = wave_max_u64(key);
       const unsigned long long hold = __ballot(key == wk && key != 0ull);
       const int wn = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
       if (lane == 0) {
-        s_wk[wave] = wk;
-        s_wn[wave] = wn;
+        agran_put(av, q, w, AG_B, wk);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
+        wstamp(q, 2);
       }
-    }
-    __syncthreads();
-    if (t == 0) {
-      unsigned long long k = 0;
-      int kn = -1;
-      for (int v = 0; v < kBlock / 64; ++v)
-        if (s_wk[v] > k) {
-          k = s_wk[v];
-          kn = s_wn[v];
-        }
-      s_wk[0] = k;
-      s_wn[0] = kn;
-      agran_put(av, q, w, AG_B, k);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
-    }
-    stamp(q, 6);
-
-    // ======== exchange B (wave 0) ========
-    if (wave == 0) {
+      stamp(q, 3);
       unsigned long long xb[1][kMaxSweep];
-      const bool ok = agran_sweep<1>(av, q, AG_B, xb);
-      unsigned long long bm = 0;
+      ok = ok && agran_sweep<1>(av, q, AG_B, xb);
+      unsigned long long bmx = 0;
+      int bpart = -1;
 #pragma unroll
       for (int r = 0; r < kMaxSweep; ++r) {
         const unsigned long long v = (lane + 64 * r) < G ? xb[0][r] : 0ull;
-        bm = v > bm ? v : bm;
+        if (v > bmx) {
+          bmx = v;
+          bpart = lane + 64 * r;
+        }
       }
-      bm = wave_max_u64(bm);
+      const unsigned long long gbest = wave_max_u64(bmx);
+      const unsigned long long bh = __ballot(bmx == gbest && gbest != 0ull);  // keys are unique
+      const int pw = (F > 0 && bh) ? __builtin_amdgcn_readlane(bpart, (int)__builtin_ctzll(bh)) : -1;
+      const int gnode = (F > 0 && pw == w) ? wn : -1;  // the chosen node, if it is mine
+      if (lane == 0 && gnode >= 0 && sp1) {
+        // the chosen node and its DoNotSchedule eligibility for pod q+1: every workgroup folds pod q
+        // into q+1's counts at that node
+        uint32_t el = 0;
+        const uint8_t* bn = s_blob[(q + 1) % 3];
+        const PodDesc& dn = *reinterpret_cast<const PodDesc*>(bn);
+        if (dn.n_ptsf) el = pts_eligible(m, bn, dn, at<PtsCons>(bn, dn.ptsf_off), dn.n_ptsf, gnode);
+        agran_put(av, q, w, AG_BN, (unsigned long long)(uint32_t)(gnode + 1) | ((unsigned long long)el << 32));
+      }
+      // ======== commit (lane 0): the owner of the chosen node applies AssumePod to its LDS core and
+      // the mirror; the pod joins my lists before the next pod that counts it ========
       if (lane == 0) {
-        s_ok = ok ? 1u : 0u;
-        s_best = bm;
-        s_win = (F > 0 && s_wk[0] == bm && s_wn[0] >= 0) ? s_wn[0] : -1;
+        if (!ok) s_ok = 0u;
+        s_best = gbest;
+        s_F = F;
+        s_gnode = gnode;
+        s_pw = pw;
+        s_pend_ls = -1;
+        if (ok) {
+          if (F == 0) {
+            if (w == 0) commit_result(m, b, base, d, ps, pod, 0, -1, gbest, nullptr, (int)ipa_any);
+          } else if (gnode >= nlo && gnode < nhi) {
+            const int ls = gnode - nlo;
+            if (d.flags & DF_ASSUME) {
+              NodeCore c = lds_core(s_core, ls / kBlock, ls % kBlock);
+              assume_core(c, d);
+              commit_result(m, b, base, d, ps, pod, F, gnode, gbest, &c, (int)ipa_any);
+              lds_put_dynamic(s_core, ls / kBlock, ls % kBlock, c);
+              if (d.slot >= 0) s_pend_ls = ls;
+            } else {
+              commit_result(m, b, base, d, ps, pod, F, gnode, gbest, nullptr, (int)ipa_any);
+            }
+          }
+        }
       }
+      stamp(q, 4);
+      if (lane == 0) wstamp(q, 3);
+    } else {
+      // ======== waves 1..7: pod q+1's counts before pod q is placed (folded in below), then the
+      // program of pod q+2 ========
+      if (sp1 && !(av.debug & 40)) {
+        aggregate(q + 1, t - 64, kAggThreads - 64, grp_bar);
+        if (wave == 1) {
+          plan_fold(q, lane);
+          sweep_z(q + 1);  // every workgroup's counts of q+1 (without pod q) are in the region
+        }
+        grp_bar();
+        load_totals(q + 1, t - 64, kAggThreads - 64);
+      }
+      if (q + 2 < av.npods) stage_prog(q + 2, t - 64, kAggThreads - 64);  // s_blob[(q+2)%3] held pod q-1
     }
     __syncthreads();
     if (!s_ok) return;
+    stamp(q, 5);
 
-    // ======== commit: the chosen node's owner (AssumePod on the LDS core + the mirror; the pod
-    // and its affinity terms join my lists) ========
-    const int win = s_win;
-    if (F == 0) {
-      if (w == 0 && t == 0) commit_result(m, b, base, d, ps, pod, 0, -1, s_best, nullptr, (int)ipa_any);
-    } else if (win >= 0 && t == (win - nlo) % kBlock) {
-      const int ls = win - nlo, kw = ls / kBlock;
-      if (d.flags & DF_ASSUME) {
-        NodeCore c = lds_core(s_core, kw, t);
-        assume_core(c, d);
-        commit_result(m, b, base, d, ps, pod, F, win, s_best, &c, (int)ipa_any);
-        lds_put_dynamic(s_core, kw, t, c);
-        if (d.slot >= 0) {
-          const uint32_t np = s_np, nt = s_nt;
-          if (np < (uint32_t)kAggPods) s_pods[np] = ((uint32_t)d.slot << 9) | (uint32_t)ls;
-          const int32_t* own = at<int32_t>(base, d.own_terms_off);
-          uint32_t k2 = 0;
-          for (; k2 < (uint32_t)d.n_own_terms && nt + k2 < (uint32_t)kAggTerms; ++k2)
-            s_terms[nt + k2] = ((uint32_t)own[k2] << 9) | (uint32_t)ls;
-          s_np = np + 1;
-          s_nt = nt + k2;
-          if (np >= (uint32_t)kAggPods || k2 < (uint32_t)d.n_own_terms) fail(0xfffffffdu);  // host-checked
+    // ======== pod q+1's counts, final ========
+    if (more) {
+      const bool placed = s_F > 0 && s_pw >= 0 && (d.flags & DF_ASSUME) && d.slot >= 0 && !(av.debug & 12);
+      const int lq = s_pend_ls;
+      if (sp1 && (av.debug & 8)) {  // diagnostic: the group gathers after the placement (no fold)
+        if (t == 0 && lq >= 0) append(q, lq);
+        __syncthreads();
+        if (wave != 0) aggregate(q + 1, t - 64, kAggThreads - 64, grp_bar);
+        __syncthreads();
+      }
+      if (sp1) {
+        if (wave == 0) {
+          if (av.debug & 40) sweep_z(q + 1);
+          stamp(q, 6);
+          if (placed) {  // the chosen node and its eligibility, from the winner's node granule
+            unsigned long long bn = 0;
+            if (lane == 0 && !agran_poll1(av, q, s_pw, AG_BN, &bn)) s_ok = 0u;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bn, 0);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bn >> 32), 0);
+            const int nq = (int)lo - 1;
+            const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+            for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
+            if (lane == 0) {
+              s_gnode = nq;
+              s_el = hi;
+            }
+          }
+          if (lane == 0 && lq >= 0 && !(av.debug & 8)) append(q, lq);
         }
+        __syncthreads();
+        if (!s_ok) return;
+        if (av.debug & 40) {
+          load_totals(q + 1, t, kAggThreads);
+          __syncthreads();
+        }
+        stamp(q, 7);
+        if (wave == 0) {
+          if (placed) {  // fold pod q into q+1's counts: shared ones everywhere, node-local ones at the owner
+            const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+            const uint32_t el = s_el;
+            uint32_t any = 0;
+            for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) {
+              const FoldItem it = s_fi[k];
+              const int32_t v = s_fv[k];
+              if (v < 0 || (it.cons >= 0 && !((el >> it.cons) & 1u))) continue;
+              if (it.lref >= 0) atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
+              else if (lq >= 0) atomicAdd(&s_lh[(-1 - it.lref) * kAggSlots + lq], it.wt);
+              any |= it.anyb;
+            }
+            for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
+            if (lane == 0) s_any |= any;
+          }
+          if (av.stamps && lane == 0) {  // diagnostic: the fold of pod q as each workgroup saw it
+            av.stamps[(size_t)q * kAggStamps + 9 + (w & 3)] =
+                ((unsigned long long)s_nfi << 48) | ((unsigned long long)(uint32_t)(s_gnode + 1) << 16) |
+                ((unsigned long long)(placed ? 1u : 0u) << 8) | (unsigned long long)(lq >= 0 ? 1u : 0u);
+          }
+          minima_w0(q + 1);
+          if (lane == 0) s_nfi = 0;  // the next plan starts empty
+        }
+        __syncthreads();
       } else {
-        commit_result(m, b, base, d, ps, pod, F, win, s_best, nullptr, (int)ipa_any);
+        if (t == 0 && lq >= 0) append(q, lq);
+        __syncthreads();
+        aggregate(q + 1, t, kAggThreads, wg_bar);
+        if (wave == 0) sweep_z(q + 1);
+        __syncthreads();
+        if (!s_ok) return;
+        load_totals(q + 1, t, kAggThreads);
+        __syncthreads();
+        minima(q + 1);
+        __syncthreads();
       }
     }
-    stamp(q, 7);
-    __syncthreads();  // my lists and cores are final; s_blob[q & 1] is free again
+    stamp(q, 8);
   }
 }
+
 }  // namespace ksg
 
 // ---- host-side launchers (C++ linkage, called by the host library) ------------------------------
@@ -2875,9 +3118,9 @@ hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const Loop
 hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
                            hipEvent_t t1) {
   if (t0)
-    hipExtLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kBlock), 0, s, t0, t1, 0, m, b, av);
+    hipExtLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
   else
-    hipLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kBlock), 0, s, m, b, av);
+    hipLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
   return hipGetLastError();
 }
 // Loads the module's code object onto the current device now (hipFuncGetAttributes), so that no

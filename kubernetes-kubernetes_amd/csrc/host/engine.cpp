@@ -573,7 +573,12 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
         !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR | DF_ROTDEV)) &&
         c->alloc_bound < ((int64_t)1 << 52) / 100)
       D.flags |= DF_FAST;
+    if (mode == CYCLE && shape && D.n_scalar == 0 &&
+        !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_SCORE_ERROR | DF_ROTDEV)) &&
+        c->alloc_bound < ((int64_t)1 << 52) / 100)
+      D.flags |= DF_LFAST;
   }
+  if (p.terminating) D.flags |= DF_TERMINATING;
   B.finish();
   out->blob = std::move(B.b);
   return KSG_OK;
@@ -985,7 +990,7 @@ Engine::~Engine() {
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
   if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region})
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -1541,11 +1546,19 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       av.nblk = NB;
       av.tag = agran_tag;
       av.gwords = gw;
+      av.debug = c->cfg.agg_debug;
       av.gran = (unsigned long long*)d_agran.p;
       av.region = (unsigned long long*)d_region.p;
       av.fail = (uint32_t*)d_fail.p;
       av.desc_bytes = (const uint32_t*)d_off.p + n;
-      av.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr;
+      if (c->cfg.loop_stamps) {
+        const size_t sb = ((size_t)n * kAggStamps + (size_t)n * G * 4) * 8;
+        if ((rc = ensure(d_astamps, sb))) return rc;
+        if (runs.empty() || !runs.back().agg) HIPCHK(hipMemsetAsync(d_astamps.p, 0, sb, s));
+      }
+      av.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)i * kAggStamps : nullptr;
+      av.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)n * kAggStamps + (size_t)i * G * 4
+                                      : nullptr;
       HIPCHK(launch_agg_loop(m, bv, av, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
       runs.push_back({i, j - i, rb, true});
       launches += j - i;
@@ -1652,25 +1665,86 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (c->cfg.loop_stamps) {  // mean per-phase time (us) of the looped pods, workgroup 0's view
       std::vector<LoopRun> sruns, aruns;
       for (auto& r : runs) (r.agg ? aruns : sruns).push_back(r);
-      {  // k_agg_loop: aggregation, Z, totals + minima, phase 1, A, phase 2, B + commit, gap to the next pod
-        std::vector<unsigned long long> st((size_t)n * 8);
-        HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
-        double acc[9] = {0};
-        int cnt = 0;
+      {  // k_agg_loop (workgroup 0, wave 0): phase 1, A, phase 2 + B publish, B + commit, wait for the
+         // next pod's gathering; then (folded pods) Z, chosen node + totals, fold + minima; gap
+        std::vector<unsigned long long> st((size_t)n * kAggStamps);
+        if (!aruns.empty())
+          HIPCHK(hipMemcpy(st.data(), d_astamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+        double acc[10] = {0}, ns_prep = 0;
+        int cnt = 0, cspec = 0, cns = 0;
         for (auto& r : aruns)
           for (int q = r.first; q + 1 < r.first + r.count; ++q) {
-            const unsigned long long* t = &st[(size_t)q * 8];
-            bool okq = true;
-            for (int k = 0; k < 8; ++k) okq = okq && t[k] != 0;
-            if (!okq || !st[(size_t)(q + 1) * 8]) continue;
-            for (int k = 1; k < 8; ++k) acc[k] += (double)(t[k] - t[k - 1]) / 100.0;
-            acc[8] += (double)(st[(size_t)(q + 1) * 8] - t[7]) / 100.0;
+            const unsigned long long* t = &st[(size_t)q * kAggStamps];
+            const unsigned long long nx = st[(size_t)(q + 1) * kAggStamps];
+            bool okq = nx != 0;
+            for (int k : {0, 1, 2, 3, 4, 5, 8}) okq = okq && t[k] != 0;
+            if (!okq) continue;
+            for (int k = 1; k <= 5; ++k) acc[k] += (double)(t[k] - t[k - 1]) / 100.0;
+            if (t[6] && t[7]) {
+              acc[6] += (double)(t[6] - t[5]) / 100.0;
+              acc[7] += (double)(t[7] - t[6]) / 100.0;
+              acc[8] += (double)(t[8] - t[7]) / 100.0;
+              cspec++;
+            } else {
+              ns_prep += (double)(t[8] - t[5]) / 100.0;
+              cns++;
+            }
+            acc[9] += (double)(nx - t[8]) / 100.0;
             cnt++;
           }
+        {  // per-workgroup skew: spread of phase-1 start, A publish, B publish; who is last
+          std::vector<unsigned long long> ws((size_t)n * G * 4);
+          if (!aruns.empty())
+            HIPCHK(hipMemcpy(ws.data(), (unsigned long long*)d_astamps.p + (size_t)n * kAggStamps, ws.size() * 8,
+                             hipMemcpyDeviceToHost));
+          double sk[4] = {0}, ph1max = 0, ph1min = 0, lastA_hop = 0;
+          int sc = 0;
+          for (auto& r : aruns)
+            for (int q = r.first; q < r.first + r.count; ++q) {
+              unsigned long long mn[4], mx[4];
+              bool okq = true;
+              for (int k = 0; k < 4; ++k) { mn[k] = ~0ull; mx[k] = 0; }
+              double p1mx = 0, p1mn = 1e30;
+              for (int g = 0; g < G; ++g)
+                for (int k = 0; k < 4; ++k) {
+                  const unsigned long long v = ws[((size_t)q * G + g) * 4 + k];
+                  okq = okq && v != 0;
+                  mn[k] = std::min(mn[k], v);
+                  mx[k] = std::max(mx[k], v);
+                }
+              if (!okq) continue;
+              for (int g = 0; g < G; ++g) {
+                const double p1 = (double)(ws[((size_t)q * G + g) * 4 + 1] - ws[((size_t)q * G + g) * 4]) / 100.0;
+                p1mx = std::max(p1mx, p1);
+                p1mn = std::min(p1mn, p1);
+              }
+              for (int k = 0; k < 4; ++k) sk[k] += (double)(mx[k] - mn[k]) / 100.0;
+              ph1max += p1mx;
+              ph1min += p1mn;
+              lastA_hop += (double)(mn[2] - mx[1]) / 100.0;  // last A publish -> first B publish
+              sc++;
+            }
+          if (sc)
+            std::fprintf(stderr, "[k_agg_loop skew over workgroups, us] phase-1 start %.3f  A publish %.3f  B publish %.3f  "
+                         "commit end %.3f | phase 1 max %.3f min %.3f | last A -> first B %.3f\n", sk[0] / sc, sk[1] / sc,
+                         sk[2] / sc, sk[3] / sc, ph1max / sc, ph1min / sc, lastA_hop / sc);
+        }
+        if (std::getenv("KSG_AGG_DUMP"))
+          for (auto& r : aruns)
+            for (int q = r.first; q < r.first + r.count && q < r.first + 64; ++q) {
+              const unsigned long long* t = &st[(size_t)q * kAggStamps];
+              std::fprintf(stderr, "[agg dump] pod %d:", q);
+              for (int k = 9; k < 13; ++k)
+                std::fprintf(stderr, " wg%d nfi %llu node %lld placed %llu owner %llu |", k - 9, t[k] >> 48,
+                             (long long)((t[k] >> 16) & 0xffffffffull) - 1, (t[k] >> 8) & 1, t[k] & 1);
+              std::fprintf(stderr, "\n");
+            }
         if (cnt)
-          std::fprintf(stderr, "[k_agg_loop stamps, %d pods, us] aggregation %.3f  Z %.3f  totals+minima %.3f  "
-                       "phase1 %.3f  A %.3f  phase2 %.3f  B+commit %.3f  gap %.3f\n", cnt, acc[1] / cnt, acc[2] / cnt,
-                       acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt, acc[7] / cnt, acc[8] / cnt);
+          std::fprintf(stderr, "[k_agg_loop stamps, %d pods, us] phase1 %.3f  A %.3f  phase2+B publish %.3f  "
+                       "B+commit %.3f  wait gather %.3f | folded (%d): Z %.3f  node+totals %.3f  fold+minima %.3f | "
+                       "unfolded (%d): counts %.3f | gap %.3f\n", cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt,
+                       acc[4] / cnt, acc[5] / cnt, cspec, cspec ? acc[6] / cspec : 0.0, cspec ? acc[7] / cspec : 0.0,
+                       cspec ? acc[8] / cspec : 0.0, cns, cns ? ns_prep / cns : 0.0, acc[9] / cnt);
       }
       std::vector<unsigned long long> st((size_t)n * 8);
       HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));

@@ -146,6 +146,7 @@ struct Config {
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
+  int agg_debug = 0;            // AggView::debug (diagnostic)
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
   // sharded: the loop's per-pod exchange device-to-device (granules over xGMI).  Default on for RCCL
   // ranks (one process per GPU); in-process groups (localGroup, one device) only when asked: their
@@ -422,6 +423,7 @@ class Engine {
   std::vector<unsigned long long*> gran_all;  // every rank's granule array as mapped here ([rank] = d_gran)
   uint32_t gran_tag = 0;
   DevBuf d_agran, d_region;  // k_agg_loop: exchange granules (own tag sequence), per-pod shared regions
+  DevBuf d_astamps;          // k_agg_loop diagnostic stamps
   uint32_t agran_tag = 0;
   int gran_setup();
   int next_gran_tag(uint32_t* tag);

@@ -493,6 +493,7 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     if (const JVal* pl = d.get(r, "persistentLoop")) c->persistent_loop = pl->type == JVal::BOOL && pl->b;
     c->loop_wg = (int)d.num(r, "loopWorkgroups", 0);
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
+    c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);
     if (const JVal* dx = d.get(r, "deviceExchange")) c->dev_exchange = dx->type == JVal::BOOL && dx->b ? 1 : 0;
     c->loop_stamps = d.boolean(r, "loopStamps");
     if (const JVal* ds = d.get(r, "distributed")) {  // node-sharded evaluation
