@@ -203,6 +203,15 @@ int ksg_shard_range(const ksg_ctx *ctx, int32_t *first_node, int32_t *num_nodes)
 int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
                                 double *bytes_per_launch, int32_t *launches, int32_t *kernel);
 
+/* Recovery diagnostic: diffs the device mirror -- every node's Requested, NonZeroRequested, pod
+ * count, allocatable, unschedulable flag and host ports, and the pod table's node index per slot --
+ * against the host cache shadow it is uploaded from (the NodeInfo fields of framework/types.go:
+ * 172-220 that AssumePod changes, cache.go:365-380).  sync != 0 first does what the next scheduling
+ * cycle does (re-upload a mirror marked stale, e.g. after a persistent-loop give-up returned
+ * KSG_EDEVICE).  *ndiff: differing nodes + pod-table slots, -1 if no mirror is laid out for the
+ * current snapshot; *first: the first differing snapshot index (n + slot for a pod-table slot), -1. */
+int ksg_debug_compare_mirror(ksg_ctx *ctx, int32_t sync, int32_t *ndiff, int32_t *first);
+
 /* Parity diagnostic (no device needed): fills out[k] = math.Log(float64(k)) for 0 <= k < n with
  * the table PodTopologySpread's score kernel reads (topologyNormalizingWeight, podtopologyspread/
  * scoring.go:287-299: log(size + 2)).  Returns n. */

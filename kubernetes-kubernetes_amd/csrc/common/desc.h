@@ -379,6 +379,8 @@ struct LoopView {
   unsigned long long* stamps;  // diagnostic: [npods][8] s_memrealtime per phase (nullptr)
   const uint32_t* desc_bytes;  // [batch pods] program sizes (indexed like BatchView::desc_off)
   unsigned long long* wstamps;  // diagnostic: [npods][nwg][8] exchange / owner times (nullptr)
+  int32_t give_up_at;        // diagnostic: every workgroup gives up at this pod of the run (-1: never)
+  int32_t pad_;
 };
 // exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
 // A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)
@@ -422,6 +424,8 @@ struct AggView {
   const uint32_t* desc_bytes; // [batch pods] program sizes
   unsigned long long* stamps; // diagnostic: [npods][kAggStamps] (nullptr)
   unsigned long long* wstamps;  // diagnostic: [npods][nwg][4] phase-1 start, A publish, B publish, commit end
+  int32_t give_up_at;         // diagnostic: every workgroup gives up at this pod of the run (-1: never)
+  int32_t pad_;
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -1796,6 +1796,13 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   if (threadIdx.x == kBlock && lv.npods > 0) publish_a(0, 0);
 
   for (int q = 0; q < lv.npods; ++q) {
+    if (q == lv.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(lv.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
     const int pod = lv.first_pod + q, par = q & 1, npar = par ^ 1;
     const int bq = q % 3, bn = (q + 1) % 3, bs = (q + 2) % 3;
     const bool more = q + 1 < lv.npods;
@@ -2213,6 +2220,45 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
   }
 }
 
+// agran_sweep without holding every participant's granules: each pass visits participant groups of
+// 64 one after another (visit(v, x) per lane, after reset()), and is kept only if every tag matched.
+template <int NS, typename Reset, typename Visit>
+__device__ __forceinline__ bool agran_sweep_visit(const AggView& av, int q, int slot0, Reset&& reset, Visit&& visit) {
+  const int lane = threadIdx.x & 63;
+  const int P = av.nwg;
+  const unsigned long long* g = av.gran + (size_t)q * P * kAGran + slot0;
+  const unsigned long long want = (unsigned long long)av.tag;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t spins = 0;; ++spins) {
+    bool ok = true;
+    reset();
+#pragma unroll 1
+    for (int r = 0; r < kMaxSweep && 64 * r < P; ++r) {
+      const int v = lane + 64 * r;
+      unsigned long long x[NS];
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const unsigned long long y =
+            v < P ? __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : want << 48;
+        ok &= (y >> 48) == want;
+        x[k] = y & kPayload;
+      }
+      if (v < P) visit(v, x);
+    }
+    if (__all(ok)) return true;
+    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
+      if (lane == 0) {
+        __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+    if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // One lane: poll granule `slot` of participant p for pod q (give-up as agran_sweep).
 __device__ __forceinline__ bool agran_poll1(const AggView& av, int q, int p, int slot, unsigned long long* out) {
   const unsigned long long* g = av.gran + ((size_t)q * av.nwg + p) * kAGran + slot;
@@ -2239,8 +2285,11 @@ __device__ __forceinline__ bool agran_poll1(const AggView& av, int q, int p, int
 __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
-  __shared__ int64_t s_fx[kAggSlots], s_ri[kAggSlots];  // phase-1 slots
-  __shared__ uint32_t s_rt[kAggSlots], s_rn[kAggSlots];
+  // phase-1 slots: {weighted fixed score, raw TaintToleration, raw NodeAffinity} in one 16-byte
+  // record (one LDS read in phase 2), raw InterPodAffinity apart (read only when it scores)
+  struct SlotVal { int64_t fixed; uint32_t rt, rn; };
+  __shared__ __align__(16) SlotVal s_sv[kAggSlots];
+  __shared__ int64_t s_ri[kAggSlots];
   __shared__ unsigned long long s_ball[kAggThreads / 64];  // [wave] feasibility ballots
   __shared__ int32_t s_lh[kAggLocal * kAggSlots];          // node-local histograms
   __shared__ unsigned long long s_gh[kAggGWords];          // shared-region partials, then totals
@@ -2266,6 +2315,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ uint32_t s_nfi;
   __shared__ int s_pw;                // participant whose key won the pod just decided
   __shared__ uint32_t s_el;           // the chosen node's DoNotSchedule eligibility for the next pod
+  __shared__ int s_bn_q;              // the pod whose chosen node (s_gnode, s_el) wave 0 has resolved
+  __shared__ int s_a_q, s_p2_q;       // wave 0 -> 1: exchange A of pod q swept; wave 1 -> 0: its phase-2 half done
+  __shared__ int s_elig_q;            // the pod whose DoNotSchedule eligibility s_elig holds
+  __shared__ unsigned long long s_p2k;
+  __shared__ int s_p2n;
+  __shared__ int64_t s_mx[4];
+  __shared__ uint32_t s_pmult[kMaxCons];  // DoNotSchedule: present domains at the minimum
   const int w = blockIdx.x, G = av.nwg;
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
@@ -2325,6 +2381,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       s_elig[ls] = (uint8_t)el;
     }
     gbar();
+    if (tid == 0) __hip_atomic_store(&s_elig_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     uint32_t any = 0;
     auto add = [&](int32_t lref, int32_t v, int ls, long long wt) __attribute__((always_inline)) {
       if (lref >= 0) atomicAdd(&s_gh[lref + v], (unsigned long long)wt);
@@ -2530,12 +2587,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     }
   };
-  // minima() by wave 0 alone, for a pod without node-local constraints (the folded path)
-  auto minima_w0 = [&](int q) __attribute__((always_inline)) {
+  // minima() for a folded pod, by the gathering group's waves (wave index gw of gnw): per shared
+  // DoNotSchedule constraint its minimum, present domains and how many of them sit at the minimum
+  auto minima_grp = [&](int q, int gwv, int gnw) __attribute__((always_inline)) {
     const uint8_t* base = s_blob[q % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
     const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
-    for (int32_t c = 0; c < d.n_ptsf; ++c) {
+    for (int32_t c = gwv; c < d.n_ptsf; c += gnw) {
       long long mn = 0x7fffffffffffffffll;
       uint32_t cnt = 0;
       for (int v = lane; v < cf[c].nvals; v += 64)
@@ -2546,9 +2604,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         }
       mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
       cnt = wave_sum_u32(cnt);
+      uint32_t mult = 0;
+      for (int v = lane; v < cf[c].nvals; v += 64)
+        if (s_gh[cf[c].pref + v] && (long long)s_gh[cf[c].lref + v] == mn) ++mult;
+      mult = wave_sum_u32(mult);
       if (lane == 0) {
         s_pmin[c] = mn;
         s_pndom[c] = cnt;
+        s_pmult[c] = mult;
       }
     }
   };
@@ -2556,6 +2619,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   // its labels against q+1's selectors, its own terms against q+1 -- exactly what q+1's aggregation
   // would count for it, less the chosen node's label values (looked up once the node is known).
   auto plan_fold = [&](int q, int gl) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(gl));  // lane-dependent item selection stays in the loop (register pressure)
     const uint8_t* bp = s_blob[q % 3];
     const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
     const uint8_t* base = s_blob[(q + 1) % 3];
@@ -2655,6 +2719,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_ok = 1;
     s_pend_ls = -1;
     s_nfi = 0;
+    s_bn_q = -1;
+    s_a_q = -1;
+    s_p2_q = -1;
+    s_elig_q = -1;
   }
   __syncthreads();
   for (int s = t; s < m.pods_hw; s += kAggThreads) {
@@ -2691,13 +2759,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   }
   uint32_t gtarget = 0;  // waves 1..7: arrivals their group barrier waits for (s_gbar is monotonic)
   auto grp_bar = [&]() __attribute__((always_inline)) {
-    gtarget += kAggThreads / 64 - 1;
+    gtarget += kAggThreads / 64 - 2;  // waves 2..7
     if (lane == 0) __hip_atomic_fetch_add(&s_gbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (__hip_atomic_load(&s_gbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gtarget)
       __builtin_amdgcn_s_sleep(1);
   };
 
   for (int q = 0; q < av.npods; ++q) {
+    if (q == av.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
+      if (t == 0) fail((uint32_t)q);
+      return;
+    }
     const int pod = av.first_pod + q;
     const uint8_t* base = s_blob[q % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
@@ -2714,14 +2786,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       PodFast pf;
       if ((d.flags & DF_LFAST) && !(av.debug & 2)) pf = load_fast(base, d);
       else pf.flags = d.flags & ~DF_LFAST;
-      if (my_node) ne = eval_agg(m, lds_core(s_core, kk, tt), s_core.bwo[kk][tt], pf, base, d, my_i, tp, t);
+      // opaque per pod: keeps the compiler from hoisting my node's column addresses out of the pod
+      // loop, where they would stay live (and spill) across the exchanges
+      int my_iq = my_i;
+      asm volatile("" : "+v"(my_iq));
+      if (my_node) ne = eval_agg(m, lds_core(s_core, kk, tt), s_core.bwo[kk][tt], pf, base, d, my_iq, tp, t);
       const bool feas = ne.st == 0;
       const unsigned long long ballot = __ballot(feas);
       const int lim = d.rot_start - (nlo + wave * 64);
       const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
-      s_fx[t] = ne.fixed;
-      s_rt[t] = (uint32_t)ne.rt;
-      s_rn[t] = (uint32_t)ne.rna;
+      s_sv[t] = SlotVal{ne.fixed, (uint32_t)ne.rt, (uint32_t)ne.rna};
       s_ri[t] = ne.ripa;
       unsigned long long et = 0, en = 0, ei = 0, ni = ~0ull;
       if (feas) {
@@ -2747,163 +2821,228 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     __syncthreads();
     stamp(q, 1);
     const uint32_t ipa_any = s_any;
-    if (av.debug & 32) {  // diagnostic: the speculative gathering first, not beside wave 0's work
-      if (wave != 0 && sp1) {
-        aggregate(q + 1, t - 64, kAggThreads - 64, grp_bar);
-        if (wave == 1) plan_fold(q, lane);
-      }
-      __syncthreads();
-    }
 
-    if (wave == 0) {
-      // ======== wave 0: exchange A, phase 2, exchange B, commit ========
-      if (lane == 0) {
-        uint32_t c = 0, bl = 0;
-        unsigned long long a = 0, bb = 0, mi = 0, ni = ~0ull;
-        for (int v = 0; v < kAggThreads / 64; ++v) {
-          c += s_wu[v][0];
-          bl += s_wu[v][1];
-          a = s_wx[v][0] > a ? s_wx[v][0] : a;
-          bb = s_wx[v][1] > bb ? s_wx[v][1] : bb;
-          mi = s_wx[v][2] > mi ? s_wx[v][2] : mi;
-          ni = s_wx[v][3] < ni ? s_wx[v][3] : ni;
+    if (wave <= 1) {
+      // ======== waves 0-1: exchange A (wave 0), phase 2 (both halves), exchange B + commit (wave 0) ========
+      if (wave == 0) {
+        if (lane == 0) {
+          uint32_t c = 0, bl = 0;
+          unsigned long long a = 0, bb = 0, mi = 0, ni = ~0ull;
+          for (int v = 0; v < kAggThreads / 64; ++v) {
+            c += s_wu[v][0];
+            bl += s_wu[v][1];
+            a = s_wx[v][0] > a ? s_wx[v][0] : a;
+            bb = s_wx[v][1] > bb ? s_wx[v][1] : bb;
+            mi = s_wx[v][2] > mi ? s_wx[v][2] : mi;
+            ni = s_wx[v][3] < ni ? s_wx[v][3] : ni;
+          }
+          unsigned long long g0, g1;
+          a_granules(c, bl, a, bb, &g0, &g1);
+          // raw InterPodAffinity biased into [1, 2^47): max as is, min reversed (max of 2^47 - x)
+          const unsigned long long bi = c ? (unsigned long long)(dec_i64(mi) + kAggIpaBias) + 1ull : 0ull;
+          const unsigned long long bn = c ? (1ull << 47) - (unsigned long long)(dec_i64(ni) + kAggIpaBias) : 0ull;
+          agran_put(av, q, w, AG_A0, g0);
+          agran_put(av, q, w, AG_A1, g1);
+          agran_put(av, q, w, AG_A2, bi);
+          agran_put(av, q, w, AG_A3, bn);
+          wstamp(q, 1);
         }
-        unsigned long long g0, g1;
-        a_granules(c, bl, a, bb, &g0, &g1);
-        // raw InterPodAffinity biased into [1, 2^47): max as is, min reversed (max of 2^47 - x)
-        const unsigned long long bi = c ? (unsigned long long)(dec_i64(mi) + kAggIpaBias) + 1ull : 0ull;
-        const unsigned long long bn = c ? (1ull << 47) - (unsigned long long)(dec_i64(ni) + kAggIpaBias) : 0ull;
-        agran_put(av, q, w, AG_A0, g0);
-        agran_put(av, q, w, AG_A1, g1);
-        agran_put(av, q, w, AG_A2, bi);
-        agran_put(av, q, w, AG_A3, bn);
-        wstamp(q, 1);
-      }
-      unsigned long long xa[4][kMaxSweep];
-      bool ok = agran_sweep<4>(av, q, AG_A0, xa);
-      uint32_t F = 0, wp = 0, bf = 0;
-      unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
+        unsigned long long xa[4][kMaxSweep];
+        const bool ok = agran_sweep<4>(av, q, AG_A0, xa);
+        uint32_t F = 0, wp = 0, bf = 0;
+        unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
 #pragma unroll
-      for (int r = 0; r < kMaxSweep; ++r) {
-        const int v = lane + 64 * r;
-        if (v < G) {
-          const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
-          F += c;
-          if (v < w) wp += c;
-          bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
-          const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
-          tmax = tv > tmax ? tv : tmax;
-          nmax = nv > nmax ? nv : nmax;
-          imax = xa[2][r] > imax ? xa[2][r] : imax;
-          inmax = xa[3][r] > inmax ? xa[3][r] : inmax;
+        for (int r = 0; r < kMaxSweep; ++r) {
+          const int v = lane + 64 * r;
+          if (v < G) {
+            const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
+            F += c;
+            if (v < w) wp += c;
+            bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
+            const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
+            tmax = tv > tmax ? tv : tmax;
+            nmax = nv > nmax ? nv : nmax;
+            imax = xa[2][r] > imax ? xa[2][r] : imax;
+            inmax = xa[3][r] > inmax ? xa[3][r] : inmax;
+          }
         }
+        F = wave_sum_u32(F);
+        bf = wave_sum_u32(bf);
+        wp = wave_sum_u32(wp);
+        tmax = wave_max_u64(tmax);
+        nmax = wave_max_u64(nmax);
+        imax = wave_max_u64(imax);
+        inmax = wave_max_u64(inmax);
+        if (lane == 0) {
+          s_F = F;
+          s_psb = bf;
+          s_acc = wp;
+          s_mx[0] = tmax ? (int64_t)tmax - 1 : 0;
+          s_mx[1] = nmax ? (int64_t)nmax - 1 : 0;
+          s_mx[2] = imax ? (int64_t)(imax - 1ull) - kAggIpaBias : 0;
+          s_mx[3] = inmax ? (int64_t)((1ull << 47) - inmax) - kAggIpaBias : 0;
+          if (!ok) s_ok = 0u;
+          __hip_atomic_store(&s_a_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        stamp(q, 2);
+      } else {
+        while (__hip_atomic_load(&s_a_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+          __builtin_amdgcn_s_sleep(1);
       }
-      F = wave_sum_u32(F);
-      const uint32_t ps_before = wave_sum_u32(bf);
-      uint32_t acc = wave_sum_u32(wp);
-      tmax = wave_max_u64(tmax);
-      nmax = wave_max_u64(nmax);
-      imax = wave_max_u64(imax);
-      inmax = wave_max_u64(inmax);
-      const int64_t mx_t = tmax ? (int64_t)tmax - 1 : 0, mx_n = nmax ? (int64_t)nmax - 1 : 0;
-      const int64_t mx_i = imax ? (int64_t)(imax - 1ull) - kAggIpaBias : 0;
-      const int64_t mn_i = inmax ? (int64_t)((1ull << 47) - inmax) - kAggIpaBias : 0;
-      stamp(q, 2);
-      // phase 2 over my 512 slots: positions, NormalizeScore + weights, the best packed key
+      // ---- phase 2 over my half of the slots (wave v: ballots [4v, 4v + 4)): positions in the rotated
+      // feasible list, NormalizeScore + weights, the best packed key
+      const bool ok = s_ok != 0u;
+      const uint32_t F = s_F, ps_before = s_psb;
+      const int64_t mx_t = s_mx[0], mx_n = s_mx[1], mx_i = s_mx[2], mn_i = s_mx[3];
+      uint32_t acc = s_acc;
+      if (wave == 1)
+        for (int v = 0; v < kAggThreads / 128; ++v) acc += (uint32_t)__popcll(s_ball[v]);
       unsigned long long key = 0;
       int knode = -1;
       if (ok) {
+        // every LDS read of my half issued up front, then the arithmetic
+        constexpr int kH = kAggThreads / 128;
+        unsigned long long ballot[kH];
+        SlotVal sv[kH];
+        int64_t ri[kH];
+        const bool ipa = ((d.score_mask >> P_IPA) & 1u) != 0;
 #pragma unroll
-        for (int v = 0; v < kAggThreads / 64; ++v) {
-          const unsigned long long ballot = s_ball[v];
-          const int ls = v * 64 + lane;
-          if ((ballot >> lane) & 1ull) {
-            const uint32_t g = acc + wave_prefix_count(ballot, lane);
+        for (int vv = 0; vv < kH; ++vv) {
+          const int v = wave * kH + vv;
+          ballot[vv] = s_ball[v];
+          sv[vv] = s_sv[v * 64 + lane];
+          ri[vv] = ipa ? s_ri[v * 64 + lane] : 0;
+        }
+#pragma unroll
+        for (int vv = 0; vv < kH; ++vv) {
+          const int ls = (wave * kH + vv) * 64 + lane;
+          if ((ballot[vv] >> lane) & 1ull) {
+            const uint32_t g = acc + wave_prefix_count(ballot[vv], lane);
             const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-            const int64_t total = agg_total(d, s_fx[ls], s_rt[ls], s_rn[ls], s_ri[ls], mx_t, mx_n, mx_i, mn_i, ipa_any);
+            const int64_t total = agg_total(d, sv[vv].fixed, sv[vv].rt, sv[vv].rn, ri[vv], mx_t, mx_n, mx_i, mn_i, ipa_any);
             const unsigned long long kv = pack_best(total, pos);
             if (kv > key) {
               key = kv;
               knode = nlo + ls;
             }
           }
-          acc += (uint32_t)__popcll(ballot);
+          acc += (uint32_t)__popcll(ballot[vv]);
         }
       }
-      const unsigned long long wk = wave_max_u64(key);
+      unsigned long long wk = wave_max_u64(key);
       const unsigned long long hold = __ballot(key == wk && key != 0ull);
-      const int wn = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
-      if (lane == 0) {
-        agran_put(av, q, w, AG_B, wk);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
-        wstamp(q, 2);
-      }
-      stamp(q, 3);
-      unsigned long long xb[1][kMaxSweep];
-      ok = ok && agran_sweep<1>(av, q, AG_B, xb);
-      unsigned long long bmx = 0;
-      int bpart = -1;
-#pragma unroll
-      for (int r = 0; r < kMaxSweep; ++r) {
-        const unsigned long long v = (lane + 64 * r) < G ? xb[0][r] : 0ull;
-        if (v > bmx) {
-          bmx = v;
-          bpart = lane + 64 * r;
+      int wn = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
+      stamp(q, 10);
+      if (wave == 1) {
+        if (lane == 0) {
+          s_p2k = wk;
+          s_p2n = wn;
+          __hip_atomic_store(&s_p2_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-      }
-      const unsigned long long gbest = wave_max_u64(bmx);
-      const unsigned long long bh = __ballot(bmx == gbest && gbest != 0ull);  // keys are unique
-      const int pw = (F > 0 && bh) ? __builtin_amdgcn_readlane(bpart, (int)__builtin_ctzll(bh)) : -1;
-      const int gnode = (F > 0 && pw == w) ? wn : -1;  // the chosen node, if it is mine
-      if (lane == 0 && gnode >= 0 && sp1) {
-        // the chosen node and its DoNotSchedule eligibility for pod q+1: every workgroup folds pod q
-        // into q+1's counts at that node
-        uint32_t el = 0;
-        const uint8_t* bn = s_blob[(q + 1) % 3];
-        const PodDesc& dn = *reinterpret_cast<const PodDesc*>(bn);
-        if (dn.n_ptsf) el = pts_eligible(m, bn, dn, at<PtsCons>(bn, dn.ptsf_off), dn.n_ptsf, gnode);
-        agran_put(av, q, w, AG_BN, (unsigned long long)(uint32_t)(gnode + 1) | ((unsigned long long)el << 32));
-      }
-      // ======== commit (lane 0): the owner of the chosen node applies AssumePod to its LDS core and
-      // the mirror; the pod joins my lists before the next pod that counts it ========
-      if (lane == 0) {
-        if (!ok) s_ok = 0u;
-        s_best = gbest;
-        s_F = F;
-        s_gnode = gnode;
-        s_pw = pw;
-        s_pend_ls = -1;
-        if (ok) {
-          if (F == 0) {
-            if (w == 0) commit_result(m, b, base, d, ps, pod, 0, -1, gbest, nullptr, (int)ipa_any);
-          } else if (gnode >= nlo && gnode < nhi) {
-            const int ls = gnode - nlo;
-            if (d.flags & DF_ASSUME) {
-              NodeCore c = lds_core(s_core, ls / kBlock, ls % kBlock);
-              assume_core(c, d);
-              commit_result(m, b, base, d, ps, pod, F, gnode, gbest, &c, (int)ipa_any);
-              lds_put_dynamic(s_core, ls / kBlock, ls % kBlock, c);
-              if (d.slot >= 0) s_pend_ls = ls;
-            } else {
-              commit_result(m, b, base, d, ps, pod, F, gnode, gbest, nullptr, (int)ipa_any);
+      } else {
+        while (__hip_atomic_load(&s_p2_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+          __builtin_amdgcn_s_sleep(1);
+        stamp(q, 11);
+        if (s_p2k > wk) {  // keys are unique
+          wk = s_p2k;
+          wn = s_p2n;
+        }
+        if (lane == 0) {
+          agran_put(av, q, w, AG_B, wk);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
+          wstamp(q, 2);
+          stamp(q, 12);
+          // my candidate and its DoNotSchedule eligibility for pod q+1 (the gathering group's node
+          // role computed it for all my nodes): if it wins, every workgroup folds pod q in there
+          uint32_t el = 0;
+          if (sp1 && wn >= 0) {
+            const PodDesc& dn = *reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3]);
+            if (dn.n_ptsf) {
+              while (__hip_atomic_load(&s_elig_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q + 1)
+                __builtin_amdgcn_s_sleep(1);
+              el = s_elig[wn - nlo];
             }
           }
+          agran_put(av, q, w, AG_BN, (unsigned long long)(uint32_t)(wn + 1) | ((unsigned long long)el << 32));
         }
+        stamp(q, 3);
+        unsigned long long xb[2][kMaxSweep];
+        const bool okb = ok && agran_sweep<2>(av, q, AG_B, xb);
+        unsigned long long bmx = 0, bnx = 0;
+        int bpart = -1;
+#pragma unroll
+        for (int r = 0; r < kMaxSweep; ++r) {
+          const unsigned long long v = (lane + 64 * r) < G ? xb[0][r] : 0ull;
+          if (v > bmx) {
+            bmx = v;
+            bnx = xb[1][r];
+            bpart = lane + 64 * r;
+          }
+        }
+        const unsigned long long gbest = wave_max_u64(bmx);
+        const unsigned long long bh = __ballot(bmx == gbest && gbest != 0ull);
+        const int hl = bh ? (int)__builtin_ctzll(bh) : 0;
+        const int pw = (F > 0 && bh) ? __builtin_amdgcn_readlane(bpart, hl) : -1;
+        const uint32_t bnlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bnx, hl);
+        const uint32_t bnhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bnx >> 32), hl);
+        const int gnode = (F > 0 && pw == w) ? wn : -1;  // the chosen node, if it is mine
+        // ======== commit (lane 0): the owner of the chosen node applies AssumePod to its LDS core and
+        // the mirror; the pod joins my lists before the next pod that counts it ========
+        if (lane == 0) {
+          if (!okb) s_ok = 0u;
+          s_best = gbest;
+          s_pw = pw;
+          s_pend_ls = -1;
+          if (okb) {
+            if (F == 0) {
+              if (w == 0) commit_result(m, b, base, d, ps, pod, 0, -1, gbest, nullptr, (int)ipa_any);
+            } else if (gnode >= nlo && gnode < nhi) {
+              const int ls = gnode - nlo;
+              if (d.flags & DF_ASSUME) {
+                NodeCore c = lds_core(s_core, ls / kBlock, ls % kBlock);
+                assume_core(c, d);
+                commit_result(m, b, base, d, ps, pod, F, gnode, gbest, &c, (int)ipa_any);
+                lds_put_dynamic(s_core, ls / kBlock, ls % kBlock, c);
+                if (d.slot >= 0) s_pend_ls = ls;
+              } else {
+                commit_result(m, b, base, d, ps, pod, F, gnode, gbest, nullptr, (int)ipa_any);
+              }
+            }
+          }
+          // the chosen node and its eligibility for the fold, to the gathering group
+          if (sp1) {
+            const bool placed = okb && F > 0 && pw >= 0 && (d.flags & DF_ASSUME) && d.slot >= 0;
+            s_gnode = placed ? (int)bnlo - 1 : -1;
+            s_el = placed ? bnhi : 0u;
+            __hip_atomic_store(&s_bn_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        stamp(q, 4);
+        if (lane == 0) wstamp(q, 3);
       }
-      stamp(q, 4);
-      if (lane == 0) wstamp(q, 3);
     } else {
-      // ======== waves 1..7: pod q+1's counts before pod q is placed (folded in below), then the
-      // program of pod q+2 ========
-      if (sp1 && !(av.debug & 40)) {
-        aggregate(q + 1, t - 64, kAggThreads - 64, grp_bar);
-        if (wave == 1) {
+      // ======== waves 2..7: pod q+1's counts before pod q is placed (folded in below), its
+      // DoNotSchedule minima, then the program of pod q+2 ========
+      const int gt = t - 128, gn = kAggThreads - 128;
+      if (sp1) {
+        aggregate(q + 1, gt, gn, grp_bar);
+        if (wave == 2) {
           plan_fold(q, lane);
           sweep_z(q + 1);  // every workgroup's counts of q+1 (without pod q) are in the region
         }
         grp_bar();
-        load_totals(q + 1, t - 64, kAggThreads - 64);
+        load_totals(q + 1, gt, gn);
+        grp_bar();
+        minima_grp(q + 1, wave - 2, kAggThreads / 64 - 2);
+        if (wave == 2) {
+          // the chosen node's value of every fold item's label (once wave 0 has resolved the node)
+          while (__hip_atomic_load(&s_bn_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+            __builtin_amdgcn_s_sleep(1);
+          const int nq = s_gnode;
+          const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+          for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
+        }
       }
-      if (q + 2 < av.npods) stage_prog(q + 2, t - 64, kAggThreads - 64);  // s_blob[(q+2)%3] held pod q-1
+      if (q + 2 < av.npods) stage_prog(q + 2, gt, gn);  // s_blob[(q+2)%3] held pod q-1
     }
     __syncthreads();
     if (!s_ok) return;
@@ -2911,42 +3050,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
 
     // ======== pod q+1's counts, final ========
     if (more) {
-      const bool placed = s_F > 0 && s_pw >= 0 && (d.flags & DF_ASSUME) && d.slot >= 0 && !(av.debug & 12);
       const int lq = s_pend_ls;
-      if (sp1 && (av.debug & 8)) {  // diagnostic: the group gathers after the placement (no fold)
-        if (t == 0 && lq >= 0) append(q, lq);
-        __syncthreads();
-        if (wave != 0) aggregate(q + 1, t - 64, kAggThreads - 64, grp_bar);
-        __syncthreads();
-      }
       if (sp1) {
-        if (wave == 0) {
-          if (av.debug & 40) sweep_z(q + 1);
-          stamp(q, 6);
-          if (placed) {  // the chosen node and its eligibility, from the winner's node granule
-            unsigned long long bn = 0;
-            if (lane == 0 && !agran_poll1(av, q, s_pw, AG_BN, &bn)) s_ok = 0u;
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bn, 0);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bn >> 32), 0);
-            const int nq = (int)lo - 1;
-            const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
-            for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
-            if (lane == 0) {
-              s_gnode = nq;
-              s_el = hi;
-            }
-          }
-          if (lane == 0 && lq >= 0 && !(av.debug & 8)) append(q, lq);
-        }
-        __syncthreads();
-        if (!s_ok) return;
-        if (av.debug & 40) {
-          load_totals(q + 1, t, kAggThreads);
-          __syncthreads();
-        }
+        stamp(q, 6);
         stamp(q, 7);
         if (wave == 0) {
-          if (placed) {  // fold pod q into q+1's counts: shared ones everywhere, node-local ones at the owner
+          const int nq = s_gnode;
+          if (nq >= 0) {  // fold pod q into q+1's counts: shared ones everywhere, node-local ones at the owner
             const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
             const uint32_t el = s_el;
             uint32_t any = 0;
@@ -2954,20 +3064,27 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
               const FoldItem it = s_fi[k];
               const int32_t v = s_fv[k];
               if (v < 0 || (it.cons >= 0 && !((el >> it.cons) & 1u))) continue;
-              if (it.lref >= 0) atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
-              else if (lq >= 0) atomicAdd(&s_lh[(-1 - it.lref) * kAggSlots + lq], it.wt);
+              if (it.lref >= 0) {
+                const unsigned long long old = atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
+                if (it.cons >= 0) {  // a DoNotSchedule domain count went up by one: its minimum moves
+                  const int c = it.cons;  // only if this was the minimum's one domain (one item per constraint)
+                  if ((long long)old == s_pmin[c]) {
+                    if (s_pmult[c] == 1u) s_pmin[c] = (long long)old + 1;
+                    else s_pmult[c] -= 1u;
+                  }
+                }
+              } else if (lq >= 0) {
+                atomicAdd(&s_lh[(-1 - it.lref) * kAggSlots + lq], it.wt);
+              }
               any |= it.anyb;
             }
             for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
             if (lane == 0) s_any |= any;
           }
-          if (av.stamps && lane == 0) {  // diagnostic: the fold of pod q as each workgroup saw it
-            av.stamps[(size_t)q * kAggStamps + 9 + (w & 3)] =
-                ((unsigned long long)s_nfi << 48) | ((unsigned long long)(uint32_t)(s_gnode + 1) << 16) |
-                ((unsigned long long)(placed ? 1u : 0u) << 8) | (unsigned long long)(lq >= 0 ? 1u : 0u);
+          if (lane == 0) {
+            if (lq >= 0) append(q, lq);
+            s_nfi = 0;  // the next plan starts empty
           }
-          minima_w0(q + 1);
-          if (lane == 0) s_nfi = 0;  // the next plan starts empty
         }
         __syncthreads();
       } else {

@@ -286,6 +286,11 @@ int ksg_last_batch_kernel_stats(const ksg_ctx* ctx, double* avg_kernel_ms, doubl
   return KSG_OK;
 }
 
+int ksg_debug_compare_mirror(ksg_ctx* ctx, int32_t sync, int32_t* ndiff, int32_t* first) {
+  if (!ctx || !ndiff || !first) return KSG_EINVAL;
+  GUARD(return with_err(ctx, ctx->cluster->compare_mirror(sync != 0, ndiff, first));)
+}
+
 int ksg_debug_log_table(double* out, int32_t n) {
   if (!out || n < 0) return KSG_EINVAL;
   for (int32_t k = 0; k < n; ++k) out[k] = ksg::go_log((double)k);  // as Cluster::upload_pod_table builds it

@@ -716,4 +716,65 @@ int Cluster::flush_node_dynamic() {
   return KSG_OK;
 }
 
+
+// Parity diagnostic (ksg_debug_compare_mirror): the device mirror's node columns and pod table
+// against the host shadow they are uploaded from.  A difference means a device-side AssumePod the
+// cache does not hold (or the reverse) -- what a loop give-up leaves until the mirror is rebuilt.
+int Cluster::compare_mirror(bool sync, int32_t* ndiff, int32_t* first) {
+  order();
+  if (sync) {
+    const int rc = ensure_mirror();
+    if (rc) return rc;
+  }
+  *ndiff = 0;
+  *first = -1;
+  const int32_t n = view.n;
+  if (!view.req_cpu || n != (int32_t)order_.size()) {  // no mirror laid out for this order: nothing to compare
+    *ndiff = -1;
+    return KSG_OK;
+  }
+  HIPCHK(hipStreamSynchronize(stream));
+  std::vector<int64_t> rc_((size_t)n), rm((size_t)n), re((size_t)n), zc((size_t)n), zm((size_t)n), ac((size_t)n), am((size_t)n);
+  std::vector<int32_t> np((size_t)n), ap((size_t)n);
+  std::vector<uint32_t> fl((size_t)n), pt((size_t)n * kPortSlots);
+  auto down = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (!bytes) return KSG_OK;
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return KSG_OK;
+  };
+  int rc;
+  if ((rc = down(rc_.data(), view.req_cpu, (size_t)n * 8)) || (rc = down(rm.data(), view.req_mem, (size_t)n * 8)) ||
+      (rc = down(re.data(), view.req_eph, (size_t)n * 8)) || (rc = down(zc.data(), view.nz_cpu, (size_t)n * 8)) ||
+      (rc = down(zm.data(), view.nz_mem, (size_t)n * 8)) || (rc = down(ac.data(), view.alloc_cpu, (size_t)n * 8)) ||
+      (rc = down(am.data(), view.alloc_mem, (size_t)n * 8)) || (rc = down(np.data(), view.num_pods, (size_t)n * 4)) ||
+      (rc = down(ap.data(), view.alloc_pods, (size_t)n * 4)) || (rc = down(fl.data(), view.flags, (size_t)n * 4)) ||
+      (rc = down(pt.data(), view.ports, (size_t)n * kPortSlots * 4)))
+    return rc;
+  auto bad = [&](int32_t where) {
+    if (*first < 0) *first = where;
+    ++*ndiff;
+  };
+  for (int32_t i = 0; i < n; ++i) {
+    const NodeRec* r = node(order_[(size_t)i]);
+    if (!r) {
+      bad(i);
+      continue;
+    }
+    std::set<uint32_t> dp;
+    for (int k = 0; k < kPortSlots; ++k)
+      if (pt[(size_t)i * kPortSlots + k] != 0xffffffffu) dp.insert(pt[(size_t)i * kPortSlots + k]);
+    if (rc_[i] != r->req_cpu || rm[i] != r->req_mem || re[i] != r->req_eph || zc[i] != r->nz_cpu || zm[i] != r->nz_mem ||
+        np[i] != r->num_pods || ac[i] != r->alloc_cpu || am[i] != r->alloc_mem || ap[i] != (int32_t)r->alloc_pods ||
+        (fl[i] & 1u) != (r->spec.unschedulable ? 1u : 0u) || dp != r->ports)
+      bad(i);
+  }
+  if (!pods_dirty && view.pods_hw > 0) {  // the pod table as uploaded: every slot's node
+    std::vector<int32_t> pn((size_t)view.pods_hw);
+    if ((rc = down(pn.data(), view.pod_node, (size_t)view.pods_hw * 4))) return rc;
+    for (int32_t sl = 0; sl < view.pods_hw && (size_t)sl < pt_node.size(); ++sl)
+      if (pn[(size_t)sl] != pt_node[(size_t)sl]) bad(n + sl);
+  }
+  return KSG_OK;
+}
+
 }  // namespace ksg

@@ -1176,8 +1176,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   std::vector<CompiledPod> cp(n);
   int compiled = 0;
   // compile pods [compiled, b) against the cache (PreFilter / PreScore on the host)
+  std::vector<int64_t> ns_before((size_t)n, 0);  // Scheduler.nextStartNodeIndex before each pod's compile
   auto compile_upto = [&](int b) -> int {
     for (int i = compiled; i < b; ++i) {
+      ns_before[(size_t)i] = c->next_start;
       next_slot_ = pre_slot.empty() ? -1 : pre_slot[i];
       const int rc = compile(*pods[i], CYCLE, -1, assume, eval != nullptr, &cp[i]);
       next_slot_ = -1;
@@ -1416,13 +1418,34 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
     return KSG_OK;
   };
+  // A persistent loop gave up (a workgroup never reached an exchange): pods [first, n) are not
+  // scheduled -- their results say Error, their pod-table slots are released, nextStartNodeIndex is
+  // rewound to before them -- and the device mirror, which may hold some of their assumes, is
+  // rebuilt from the cache shadow at the next cycle.  The context stays usable.
+  auto loop_fault = [&](int first, const std::string& why) -> int {
+    (void)hipStreamSynchronize(s);
+    if (cstream) (void)hipStreamSynchronize(cstream);
+    for (int j = first; j < n; ++j) {
+      results[j] = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
+      c->pod_table_drop(j < compiled ? cp[j].slot : (pre_slot.empty() ? -1 : pre_slot[j]));
+    }
+    if (first < n && !rot_dev) c->next_start = ns_before[(size_t)first];
+    c->layout_dirty = true;
+    c->pods_dirty = true;
+    c->err = why + ": pods " + std::to_string(first) + ".." + std::to_string(n - 1) +
+             " of the batch were not scheduled (status Error); the device mirror is rebuilt from the cache";
+    return KSG_EDEVICE;
+  };
+  auto fault_detail = [&]() -> std::string {
+    uint32_t f[4] = {0, 0, 0, 0};
+    (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
+    return "persistent loop gave up (an exchange granule never arrived): pod " + std::to_string(f[1]) +
+           " of its run, granule " + std::to_string(f[2]) + ", participant " + std::to_string(f[3]);
+  };
   int settled = 0;  // chunks whose results are mirrored into the cache
   auto settle_closed = [&]() -> int {  // after a stream sync: every closed chunk
     for (; settled < (int)chunks.size(); ++settled) {
-      if ((use_loop || use_agg) && hfail[settled]) {
-        c->err = "persistent loop: an exchange granule never arrived (spin limit)";
-        return KSG_EDEVICE;
-      }
+      if ((use_loop || use_agg) && hfail[settled]) return loop_fault(chunks[settled].a, fault_detail());
       const int r2 = settle(chunks[settled].a, chunks[settled].b);
       if (r2) return r2;
     }
@@ -1443,8 +1466,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (r2) {  // the pods before i are scheduled: finish their bookkeeping, release the rest's slots
       if (drain()) return KSG_EDEVICE;
       const int r3 = settle_closed();
+      if (r3) return r3;
       for (int j = i; j < (int)pre_slot.size(); ++j) c->pod_table_drop(pre_slot[j]);
-      return r3 ? r3 : r2;
+      if (!rot_dev) c->next_start = ns_before[(size_t)i];  // pods [i, b) were compiled, never launched
+      return r2;
     }
     size_t need = 0;
     int32_t aw = 0;
@@ -1503,6 +1528,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       lv.fail = (uint32_t*)d_fail.p;
       lv.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr;
       lv.desc_bytes = (const uint32_t*)d_off.p + n;
+      lv.give_up_at = c->cfg.debug_give_up_at;
       lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr;
       // in-process ranks: every rank is past its allocations before any rank's first loop starts
       if (runs.empty() && comm && comm->launch_gate()) {
@@ -1547,6 +1573,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       av.tag = agran_tag;
       av.gwords = gw;
       av.debug = c->cfg.agg_debug;
+      av.give_up_at = c->cfg.debug_give_up_at;
       av.gran = (unsigned long long*)d_agran.p;
       av.region = (unsigned long long*)d_region.p;
       av.fail = (uint32_t*)d_fail.p;
@@ -1605,14 +1632,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (chunks.size() > 1)  // pipelined: settle each chunk as soon as its results have landed
     for (size_t k = (size_t)settled; k < chunks.size(); ++k) {
       HIPCHK(hipEventSynchronize(cev[k]));
-      if (use_loop && hfail[k]) {
-        uint32_t f[4] = {0, 0, 0, 0};
-        (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
-        c->err = "k_sched_loop: an exchange granule never arrived (spin limit): pod " + std::to_string(f[1]) +
-                 " of its run, granule " + std::to_string(f[2]) + ", lane of the first missing participant " +
-                 std::to_string(f[3]);
-        return KSG_EDEVICE;
-      }
+      if ((use_loop || use_agg) && hfail[k]) return loop_fault(chunks[k].a, fault_detail());
       if ((rc = settle(chunks[k].a, chunks[k].b))) return rc;
     }
   HIPCHK(hipStreamSynchronize(s));
@@ -1625,10 +1645,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (!runs.empty()) {
     uint32_t fail = 0;
     HIPCHK(hipMemcpy(&fail, d_fail.p, 4, hipMemcpyDeviceToHost));
-    if (fail) {
-      c->err = "persistent loop: a workgroup never reached a per-pod exchange (spin limit)";
-      return KSG_EDEVICE;
-    }
+    if (fail) return loop_fault(n, fault_detail());
   }
   float ms = 0;
   (void)hipEventElapsedTime(&ms, ev0, ev1);
@@ -1729,16 +1746,28 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                          "commit end %.3f | phase 1 max %.3f min %.3f | last A -> first B %.3f\n", sk[0] / sc, sk[1] / sc,
                          sk[2] / sc, sk[3] / sc, ph1max / sc, ph1min / sc, lastA_hop / sc);
         }
-        if (std::getenv("KSG_AGG_DUMP"))
+        {  // wave 0 inside "phase2+B publish": my half, wave 1's half, B publish, BN publish
+          double p2[4] = {0}, ns_half = 0;
+          int c2 = 0, cns2 = 0;
           for (auto& r : aruns)
-            for (int q = r.first; q < r.first + r.count && q < r.first + 64; ++q) {
+            for (int q = r.first; q < r.first + r.count; ++q) {
               const unsigned long long* t = &st[(size_t)q * kAggStamps];
-              std::fprintf(stderr, "[agg dump] pod %d:", q);
-              for (int k = 9; k < 13; ++k)
-                std::fprintf(stderr, " wg%d nfi %llu node %lld placed %llu owner %llu |", k - 9, t[k] >> 48,
-                             (long long)((t[k] >> 16) & 0xffffffffull) - 1, (t[k] >> 8) & 1, t[k] & 1);
-              std::fprintf(stderr, "\n");
+              if (!t[2] || !t[10] || !t[11] || !t[12] || !t[3]) continue;
+              if (!t[6]) {  // no gathering beside this phase 2 (the next pod is gathered after the barrier)
+                ns_half += (double)(t[10] - t[2]) / 100.0;
+                cns2++;
+              }
+              p2[0] += (double)(t[10] - t[2]) / 100.0;
+              p2[1] += (double)(t[11] - t[10]) / 100.0;
+              p2[2] += (double)(t[12] - t[11]) / 100.0;
+              p2[3] += (double)(t[3] - t[12]) / 100.0;
+              c2++;
             }
+          if (c2)
+            std::fprintf(stderr, "[k_agg_loop phase 2, us] my half %.3f (without a gathering beside it: %.3f, %d pods)  "
+                         "wait wave 1 %.3f  B publish %.3f  eligibility + BN publish %.3f\n", p2[0] / c2,
+                         cns2 ? ns_half / cns2 : 0.0, cns2, p2[1] / c2, p2[2] / c2, p2[3] / c2);
+        }
         if (cnt)
           std::fprintf(stderr, "[k_agg_loop stamps, %d pods, us] phase1 %.3f  A %.3f  phase2+B publish %.3f  "
                        "B+commit %.3f  wait gather %.3f | folded (%d): Z %.3f  node+totals %.3f  fold+minima %.3f | "

@@ -147,6 +147,7 @@ struct Config {
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int agg_debug = 0;            // AggView::debug (diagnostic)
+  int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
   // sharded: the loop's per-pod exchange device-to-device (granules over xGMI).  Default on for RCCL
   // ranks (one process per GPU); in-process groups (localGroup, one device) only when asked: their
@@ -306,6 +307,9 @@ class Cluster {
   std::vector<uint8_t> static_queued_;
   DevBuf upd_dev_;
   int ensure_mirror();                       // (re)build device arrays if dirty
+  // diff the device mirror (dynamic + static node columns, pod table) against the host shadow;
+  // sync: run ensure_mirror first (what the next cycle does)
+  int compare_mirror(bool sync, int32_t* ndiff, int32_t* first);
   int ensure_label_slot(int32_t key);        // materialise a label column
   int upload_node_dynamic(int32_t idx);      // queue one node's Requested/ports (flushed by ensure_mirror)
   int flush_node_dynamic();

@@ -494,6 +494,7 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     c->loop_wg = (int)d.num(r, "loopWorkgroups", 0);
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
     c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);
+    c->debug_give_up_at = (int)d.num(r, "debugLoopGiveUpAt", -1);
     if (const JVal* dx = d.get(r, "deviceExchange")) c->dev_exchange = dx->type == JVal::BOOL && dx->b ? 1 : 0;
     c->loop_stamps = d.boolean(r, "loopStamps");
     if (const JVal* ds = d.get(r, "distributed")) {  // node-sharded evaluation

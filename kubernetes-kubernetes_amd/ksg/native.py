@@ -31,6 +31,8 @@ def load():
         lib.ksg_create_error.restype = C.c_char_p
         lib.ksg_shard_range.restype = C.c_int
         lib.ksg_shard_range.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.ksg_debug_compare_mirror.restype = C.c_int
+        lib.ksg_debug_compare_mirror.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         _lib = lib
     return _lib
 
@@ -48,6 +50,14 @@ class Scheduler(Backend):
         self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n), C.byref(k)),
                   "kernel_stats")
         return ms.value, by.value, n.value, {1: "k_sched_loop", 2: "k_agg_loop"}.get(k.value, "k_filter_score")
+
+    def compare_mirror(self, sync=False):
+        """(differing nodes + pod-table slots, first difference) between the device mirror and the
+        host cache shadow (ksg_debug_compare_mirror); sync: rebuild a stale mirror first."""
+        nd, first = C.c_int32(), C.c_int32()
+        self._chk(self.lib.ksg_debug_compare_mirror(self.ctx, 1 if sync else 0, C.byref(nd), C.byref(first)),
+                  "compare_mirror")
+        return nd.value, first.value
 
     def shard_range(self):
         """(first snapshot index, node count) this rank evaluates (node-sharded contexts)."""

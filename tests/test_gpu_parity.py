@@ -263,6 +263,41 @@ def test_agg_loop_matches_launch_path(native, seed, wg):
     for k, p in enumerate(pods):
         ro, _ = o.schedule_one(o.compile(p), assume=True)
         assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"
+    assert g.compare_mirror(sync=False) == (0, -1), "device mirror differs from the cache after the batch"
+
+
+@pytest.mark.parametrize("agg", [False, True])
+def test_loop_give_up_recovers(native, agg):
+    """A persistent loop that gives up (forced with debugLoopGiveUpAt: every workgroup stops at the
+    6th pod of a run, as if one never arrived) fails the batch with KSG_EDEVICE and schedules none of
+    its pods; the device mirror, which holds the first pods' assumes, differs from the cache until
+    the next cycle rebuilds it (ksg_debug_compare_mirror), and scheduling then continues exactly as
+    the oracle's, which never saw the failed batch."""
+    from ksg.abi import KsgError
+    from ksg.synth import scheduling_basic, topology_spreading
+    nodes, init, pods = topology_spreading(600, 600, 60) if agg else scheduling_basic(600, 100, 60, hetero=True)
+    g = native({"debugLoopGiveUpAt": 5})
+    o = oracle({})
+    for b in (g, o):
+        for n in nodes:
+            b.add_node(n)
+        for p in init:
+            b.add_pod(p)
+    assert g.compare_mirror(sync=True) == (0, -1)
+    hs = [g.compile(p) for p in pods[:40]]
+    with pytest.raises(KsgError, match="not scheduled"):
+        g.schedule_batch(hs, assume=True)
+    nd, first = g.compare_mirror(sync=False)
+    assert nd > 0 and first >= 0, "the device assumes of the failed run should still be in the mirror"
+    assert g.compare_mirror(sync=True) == (0, -1)
+    hs = [g.compile(p) for p in pods]  # the same pods again, in runs shorter than the give-up point
+    rs = []
+    for i in range(0, len(hs), 5):
+        rs += g.schedule_batch(hs[i:i + 5], assume=True)
+    ors = o.schedule_batch([o.compile(p) for p in pods], assume=True)
+    for k in range(len(pods)):
+        assert rs[k].as_tuple() == ors[k].as_tuple(), f"pod {k}"
+    assert g.compare_mirror(sync=False) == (0, -1)
 
 
 # ---- percentageOfNodesToScore: the cut feasible list and the device-resident nextStartNodeIndex
