@@ -1743,15 +1743,14 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
           }
         }
 #pragma unroll
-        for (int v = 0; v < kBlock / 64; ++v) {
-          if (v >= vlo && v < vhi && ((ballot[v] >> lane) & 1ull)) {
+        for (int v = 0; v < kBlock / 64; ++v) {  // branch-free: independent chains interleave
+          if (v >= vlo && v < vhi) {
+            const bool f = ((ballot[v] >> lane) & 1ull) != 0;
             const uint32_t g = acc + wave_prefix_count(ballot[v], lane);
             const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-            const unsigned long long kv = pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos);
-            if (kv > *key) {
-              *key = kv;
-              *knode = (k0 + kk) * kBlock + v * 64 + lane;
-            }
+            const unsigned long long kv = f ? pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos) : 0ull;
+            *knode = kv > *key ? (k0 + kk) * kBlock + v * 64 + lane : *knode;
+            *key = kv > *key ? kv : *key;
           }
           acc += (uint32_t)__popcll(ballot[v]);
         }
@@ -2913,19 +2912,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           sv[vv] = s_sv[v * 64 + lane];
           ri[vv] = ipa ? s_ri[v * 64 + lane] : 0;
         }
+        // branch-free: the four chains are independent, so the compiler interleaves them
 #pragma unroll
         for (int vv = 0; vv < kH; ++vv) {
           const int ls = (wave * kH + vv) * 64 + lane;
-          if ((ballot[vv] >> lane) & 1ull) {
-            const uint32_t g = acc + wave_prefix_count(ballot[vv], lane);
-            const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-            const int64_t total = agg_total(d, sv[vv].fixed, sv[vv].rt, sv[vv].rn, ri[vv], mx_t, mx_n, mx_i, mn_i, ipa_any);
-            const unsigned long long kv = pack_best(total, pos);
-            if (kv > key) {
-              key = kv;
-              knode = nlo + ls;
-            }
-          }
+          const bool f = ((ballot[vv] >> lane) & 1ull) != 0;
+          const uint32_t g = acc + wave_prefix_count(ballot[vv], lane);
+          const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
+          const int64_t total = agg_total(d, sv[vv].fixed, sv[vv].rt, sv[vv].rn, ri[vv], mx_t, mx_n, mx_i, mn_i, ipa_any);
+          const unsigned long long kv = f ? pack_best(total, pos) : 0ull;
+          knode = kv > key ? nlo + ls : knode;
+          key = kv > key ? kv : key;
           acc += (uint32_t)__popcll(ballot[vv]);
         }
       }

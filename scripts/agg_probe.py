@@ -11,13 +11,14 @@ from ksg import synth  # noqa: E402
 
 wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
 wg = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+dbg = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 if wl == "c3":
     nodes, init, pods = synth.scheduling_c3(5000, 5000, 2000)
 elif wl in ("c4", "c4-anti"):
     nodes, init, pods = synth.topology_spreading(15000, 15000, 2000, preferred_anti=wl == "c4-anti")
 else:
     nodes, init, pods = synth.mixed_cluster(100000, 10000, 2000)
-s = Scheduler({"device": 0, "loopWorkgroups": wg, "loopStamps": True})
+s = Scheduler({"device": 0, "loopWorkgroups": wg, "loopStamps": True, "aggLoopDebug": dbg})
 for ns in synth.namespaces() if hasattr(synth, "namespaces") else []:
     s.upsert_namespace(ns)
 for n in nodes:
