@@ -212,6 +212,11 @@ int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
  * current snapshot; *first: the first differing snapshot index (n + slot for a pod-table slot), -1. */
 int ksg_debug_compare_mirror(ksg_ctx *ctx, int32_t sync, int32_t *ndiff, int32_t *first);
 
+/* Mirror-ingestion diagnostic: how many times the HBM mirror was rebuilt from the cache (*full) and
+ * how many node adds / removes / zone moves were applied by moving the unchanged nodes' columns on
+ * the device instead (*gather; UpdateSnapshot's list rebuild, cache.go:273-283). */
+int ksg_debug_relayouts(const ksg_ctx *ctx, uint64_t *full, uint64_t *gather);
+
 /* Parity diagnostic (no device needed): fills out[k] = math.Log(float64(k)) for 0 <= k < n with
  * the table PodTopologySpread's score kernel reads (topologyNormalizingWeight, podtopologyspread/
  * scoring.go:287-299: log(size + 2)).  Returns n. */

@@ -3165,6 +3165,53 @@ hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const ui
   hipLaunchKernelGGL(k_node_update, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, u, ids, lbl, count);
   return hipGetLastError();
 }
+// ---- node add / remove without a full re-layout (Cluster::relayout_gather): every surviving node's
+// columns move to its new snapshot index in one gather per column block; new or changed nodes are
+// then written by k_node_update / k_node_dyn.  dst[r][i] = src[r][idx[i]] for idx[i] >= 0
+// (rows x cap elements of esz bytes, row stride cap elements).
+__global__ __launch_bounds__(kBlock) void k_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* idx, int n,
+                                                        int cap, int esz) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const int r = blockIdx.y;
+  if (i >= n) return;
+  const int s = idx[i];
+  if (s < 0) return;
+  const size_t ro = (size_t)r * (size_t)cap;
+  if (esz == 8) {
+    reinterpret_cast<uint64_t*>(dst)[ro + i] = reinterpret_cast<const uint64_t*>(src)[ro + s];
+  } else if (esz == 4) {
+    reinterpret_cast<uint32_t*>(dst)[ro + i] = reinterpret_cast<const uint32_t*>(src)[ro + s];
+  } else if (esz == 1) {
+    dst[ro + i] = src[ro + s];
+  } else {  // ports: kPortSlots uint32 per node
+    for (int k = 0; k < esz / 4; ++k)
+      reinterpret_cast<uint32_t*>(dst)[(ro + i) * (size_t)(esz / 4) + k] =
+          reinterpret_cast<const uint32_t*>(src)[(ro + s) * (size_t)(esz / 4) + k];
+  }
+}
+// CSR ids (taints, images): node i's run moves from old_off[idx[i]] to new_off[i]
+__global__ __launch_bounds__(kBlock) void k_gather_csr(uint32_t* dst, const uint32_t* src, const int32_t* idx,
+                                                       const uint32_t* old_off, const uint32_t* new_off, int n) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int s = idx[i];
+  if (s < 0) return;
+  const uint32_t lo = old_off[s], cnt = old_off[s + 1] - lo, to = new_off[i];
+  for (uint32_t k = 0; k < cnt; ++k) dst[to + k] = src[lo + k];
+}
+hipError_t launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* idx, int n, int cap, int rows, int esz,
+                              hipStream_t s) {
+  if (n <= 0 || rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_rows, dim3((n + kBlock - 1) / kBlock, rows), dim3(kBlock), 0, s, dst, src, idx, n, cap, esz);
+  return hipGetLastError();
+}
+hipError_t launch_gather_csr(uint32_t* dst, const uint32_t* src, const int32_t* idx, const uint32_t* old_off,
+                             const uint32_t* new_off, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_csr, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, dst, src, idx, old_off, new_off, n);
+  return hipGetLastError();
+}
+
 // pod events (NodeInfo.update via AddPod / RemovePod / ForgetPod): one thread per queued node
 // writes its dynamic columns in place
 __global__ __launch_bounds__(kBlock) void k_node_dyn(MirrorView m, const NodeDyn* d, int count) {
@@ -3248,7 +3295,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
                       reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_node_update),
-                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop)};
+                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop),
+                      reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
     if (e != hipSuccess) return e;

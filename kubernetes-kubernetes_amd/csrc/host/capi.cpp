@@ -291,6 +291,13 @@ int ksg_debug_compare_mirror(ksg_ctx* ctx, int32_t sync, int32_t* ndiff, int32_t
   GUARD(return with_err(ctx, ctx->cluster->compare_mirror(sync != 0, ndiff, first));)
 }
 
+int ksg_debug_relayouts(const ksg_ctx* ctx, uint64_t* full, uint64_t* gather) {
+  if (!ctx || !full || !gather) return KSG_EINVAL;
+  *full = ctx->cluster->relayouts_full;
+  *gather = ctx->cluster->relayouts_gather;
+  return KSG_OK;
+}
+
 int ksg_debug_log_table(double* out, int32_t n) {
   if (!out || n < 0) return KSG_EINVAL;
   for (int32_t k = 0; k < n; ++k) out[k] = ksg::go_log((double)k);  // as Cluster::upload_pod_table builds it

@@ -140,7 +140,8 @@ const std::vector<std::string>& Cluster::order() {
         if (k < v.size()) order_.push_back(v[k]);
       }
     index_.clear();
-    for (size_t i = 0; i < order_.size(); ++i) index_[order_[i]] = (int32_t)i;
+    index_.reserve(order_.size() * 2);
+    for (size_t i = 0; i < order_.size(); ++i) index_.emplace(order_[i], (int32_t)i);
     layout_dirty = true;
   }
   return order_;
@@ -204,6 +205,7 @@ void Cluster::remove_images(const NodeSpec& n) {
 }
 
 void Cluster::intern_node(NodeRec& r) {
+  r.stale = true;
   r.labels.clear();
   for (auto& kv : r.spec.labels) {
     int32_t k = key_id(kv.first);
@@ -323,6 +325,7 @@ int Cluster::remove_node(const std::string& name) {
 }
 
 void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo.update
+  r.stale = true;
   r.req_cpu += sign * bp.res.cpu;
   r.req_mem += sign * bp.res.mem;
   r.req_eph += sign * bp.res.eph;
@@ -421,6 +424,11 @@ int Cluster::ensure_mirror() {
     if (!rc) rc = flush_node_dynamic();
     return rc ? rc : upload_pod_table();
   }
+  if (!defer_relayout && !mirror_suspect) {  // node adds / removes / zone moves: move the unchanged nodes' columns
+    bool done = false;
+    const int rc = relayout_gather(&done);
+    if (rc || done) return rc;
+  }
   for (int32_t i : static_dirty_)  // the re-layout below uploads every node
     if ((size_t)i < static_queued_.size()) static_queued_[i] = 0;
   static_dirty_.clear();
@@ -500,8 +508,10 @@ int Cluster::ensure_mirror() {
   taint_ids_per_node = n ? (double)tids.size() / n : 0.0;
   taint_max_per_node = taint_max;
   img_ids_per_node = n ? (double)iids.size() / n : 0.0;
-  view.taint_ids = (uint32_t*)dalloc(std::max<size_t>(tids.size(), 1) * 4);
-  view.img_ids = (uint32_t*)dalloc(std::max<size_t>(iids.size(), 1) * 4);
+  taint_cap_ = tids.size() + tids.size() / 2 + 1024;  // room for nodes added by relayout_gather
+  img_cap_ = iids.size() + iids.size() / 2 + 1024;
+  view.taint_ids = (uint32_t*)dalloc(taint_cap_ * 4);
+  view.img_ids = (uint32_t*)dalloc(img_cap_ * 4);
   auto up = [&](const void* dst, const void* src, size_t bytes) {
     return hipMemcpyAsync(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice, stream);
   };
@@ -530,6 +540,16 @@ int Cluster::ensure_mirror() {
       int rc = upload_label_column(k);
       if (rc) return rc;
     }
+  ++laid_epoch_;
+  for (int32_t i = 0; i < n; ++i) {
+    NodeRec& r = *nodes_[order_[(size_t)i]];
+    r.stale = false;
+    r.laid_ix = i;
+    r.laid_epoch = laid_epoch_;
+  }
+  laid_slots_ = slots_used_;
+  mirror_suspect = false;
+  ++relayouts_full;
   // snapshot indices moved: re-derive every pod's node index in the pod table
   for (auto& kv : pods)  // (pods on ghost nodes stay out of the aggregation)
     if (kv.second.slot >= 0) {
@@ -537,6 +557,131 @@ int Cluster::ensure_mirror() {
       pt_node[kv.second.slot] = r && r->real ? index_of(kv.second.node) : -1;
     }
   pods_dirty = true;
+  return upload_pod_table();
+}
+
+hipError_t launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* idx, int n, int cap, int rows, int esz,
+                              hipStream_t s);
+hipError_t launch_gather_csr(uint32_t* dst, const uint32_t* src, const int32_t* idx, const uint32_t* old_off,
+                             const uint32_t* new_off, int n, hipStream_t s);
+
+// Cache.AddNode / RemoveNode / a zone move between two cycles: UpdateSnapshot rebuilds the list
+// (cache.go:273-283) and snapshot indices shift.  Every node whose shadow did not change keeps its
+// device columns: one gather per column block moves them to the new index; new and changed nodes go
+// up as NodeUpdate / NodeDyn records.  The capacities (cap, label slots, CSR ids) must still fit.
+int Cluster::relayout_gather(bool* done) {
+  *done = false;
+  const int32_t n = (int32_t)order_.size();
+  const int32_t cap = view.cap;
+  if (!view.req_cpu || laid_epoch_ == 0 || n == 0 || n + 1 > cap || slots_used_ > slots_cap_) return KSG_OK;
+  std::vector<NodeRec*> recs((size_t)n);
+  for (int32_t i = 0; i < n; ++i) recs[(size_t)i] = nodes_[order_[(size_t)i]].get();
+  std::vector<int32_t> src((size_t)n, -1);
+  std::vector<uint32_t> toff((size_t)cap + 1, 0), ioff((size_t)cap + 1, 0);
+  size_t nt = 0, ni = 0;
+  int64_t taint_max = 0;
+  int32_t fresh = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const NodeRec& r = *recs[(size_t)i];
+    if (r.ports.size() > (size_t)kPortSlots) return KSG_OK;  // the full path reports it
+    src[(size_t)i] = (r.laid_epoch == laid_epoch_ && !r.stale) ? r.laid_ix : -1;
+    fresh += src[(size_t)i] < 0;
+    toff[(size_t)i] = (uint32_t)nt;
+    ioff[(size_t)i] = (uint32_t)ni;
+    nt += r.taint_ids.size();
+    ni += r.image_ids.size();
+    taint_max = std::max<int64_t>(taint_max, (int64_t)r.taint_ids.size());
+  }
+  for (int32_t i = n; i <= cap; ++i) {
+    toff[(size_t)i] = (uint32_t)nt;
+    ioff[(size_t)i] = (uint32_t)ni;
+  }
+  if (nt > taint_cap_ || ni > img_cap_) return KSG_OK;
+  if (fresh * 2 > n) return KSG_OK;  // mostly new columns: the full path is as cheap
+  // device scratch: the index map, the new CSR offsets, one column block
+  const size_t blk = (size_t)cap * 8 * (size_t)std::max(kMaxScalar, std::max(slots_used_, 1));
+  const size_t o_src = 0, o_toff = ((size_t)n * 4 + 255) & ~size_t(255),
+               o_ioff = o_toff + (((size_t)(cap + 1) * 4 + 255) & ~size_t(255)),
+               o_blk = o_ioff + (((size_t)(cap + 1) * 4 + 255) & ~size_t(255));
+  const size_t o_ids = o_blk + blk, need = o_ids + std::max(taint_cap_, img_cap_) * 4 + 256;
+  if (gather_dev_.bytes < need) {
+    if (gather_dev_.p) (void)hipFree(gather_dev_.p);
+    gather_dev_.p = nullptr;
+    gather_dev_.bytes = 0;
+    HIPCHK(hipMalloc(&gather_dev_.p, need));
+    gather_dev_.bytes = need;
+  }
+  uint8_t* g = (uint8_t*)gather_dev_.p;
+  const int32_t* d_src = (const int32_t*)(g + o_src);
+  HIPCHK(hipMemcpyAsync(g + o_src, src.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(g + o_toff, toff.data(), toff.size() * 4, hipMemcpyHostToDevice, stream));
+  HIPCHK(hipMemcpyAsync(g + o_ioff, ioff.data(), ioff.size() * 4, hipMemcpyHostToDevice, stream));
+  auto col = [&](const void* p, int rows, int esz) -> int {  // gather into the scratch block, copy back
+    if (rows <= 0) return KSG_OK;
+    HIPCHK(launch_gather_rows(g + o_blk, (const uint8_t*)p, d_src, n, cap, rows, esz, stream));
+    HIPCHK(hipMemcpyAsync(const_cast<void*>(p), g + o_blk, (size_t)rows * cap * (esz > 8 ? esz : esz), hipMemcpyDeviceToDevice,
+                          stream));
+    return KSG_OK;
+  };
+  int rc;
+  for (const void* p : {(const void*)view.alloc_cpu, (const void*)view.alloc_mem, (const void*)view.alloc_eph,
+                        (const void*)view.req_cpu, (const void*)view.req_mem, (const void*)view.req_eph,
+                        (const void*)view.nz_cpu, (const void*)view.nz_mem})
+    if ((rc = col(p, 1, 8))) return rc;
+  for (const void* p : {(const void*)view.alloc_pods, (const void*)view.num_pods, (const void*)view.flags})
+    if ((rc = col(p, 1, 4))) return rc;
+  if ((rc = col(view.scalar_alloc, kMaxScalar, 8)) || (rc = col(view.scalar_req, kMaxScalar, 8)) ||
+      (rc = col(view.ports, 1, 4 * kPortSlots)) || (rc = col(view.labels, laid_slots_, 4)) ||
+      (rc = col(view.label_num, laid_slots_, 8)) || (rc = col(view.label_num_ok, laid_slots_, 1)))
+    return rc;
+  // CSR ids, then the new offsets
+  HIPCHK(launch_gather_csr((uint32_t*)(g + o_ids), view.taint_ids, d_src, view.taint_off, (const uint32_t*)(g + o_toff), n,
+                           stream));
+  HIPCHK(hipMemcpyAsync(const_cast<uint32_t*>(view.taint_ids), g + o_ids, std::max<size_t>(nt, 1) * 4,
+                        hipMemcpyDeviceToDevice, stream));
+  HIPCHK(launch_gather_csr((uint32_t*)(g + o_ids), view.img_ids, d_src, view.img_off, (const uint32_t*)(g + o_ioff), n,
+                           stream));
+  HIPCHK(hipMemcpyAsync(const_cast<uint32_t*>(view.img_ids), g + o_ids, std::max<size_t>(ni, 1) * 4,
+                        hipMemcpyDeviceToDevice, stream));
+  HIPCHK(hipMemcpyAsync(const_cast<uint32_t*>(view.taint_off), g + o_toff, toff.size() * 4, hipMemcpyDeviceToDevice, stream));
+  HIPCHK(hipMemcpyAsync(const_cast<uint32_t*>(view.img_off), g + o_ioff, ioff.size() * 4, hipMemcpyDeviceToDevice, stream));
+  view.n = n;
+  node_toff_ = toff;
+  node_ioff_ = ioff;
+  taint_ids_per_node = (double)nt / n;
+  taint_max_per_node = taint_max;
+  img_ids_per_node = (double)ni / n;
+  layout_dirty = false;
+  // label columns materialised since the last layout: whole columns from the shadow
+  for (int32_t k = 0; k < (int32_t)keys.size(); ++k)
+    if (keys[k].slot >= laid_slots_ && (rc = upload_label_column(k))) return rc;
+  // new and changed nodes: their static and dynamic columns as records
+  static_queued_.assign((size_t)n, 0);
+  dyn_queued_.assign((size_t)n, 0);
+  static_dirty_.clear();
+  dyn_dirty_.clear();
+  for (int32_t i = 0; i < n; ++i)
+    if (src[(size_t)i] < 0) {
+      static_queued_[(size_t)i] = dyn_queued_[(size_t)i] = 1;
+      static_dirty_.push_back(i);
+      dyn_dirty_.push_back(i);
+    }
+  if ((rc = flush_node_updates()) || (rc = flush_node_dynamic())) return rc;
+  ++laid_epoch_;
+  for (int32_t i = 0; i < n; ++i) {
+    recs[(size_t)i]->stale = false;
+    recs[(size_t)i]->laid_ix = i;
+    recs[(size_t)i]->laid_epoch = laid_epoch_;
+  }
+  laid_slots_ = slots_used_;
+  ++relayouts_gather;
+  for (auto& kv : pods)  // snapshot indices moved: every pod's node index in the pod table
+    if (kv.second.slot >= 0) {
+      const NodeRec* r = node(kv.second.node);
+      pt_node[kv.second.slot] = r && r->real ? index_of(kv.second.node) : -1;
+    }
+  pods_dirty = true;
+  *done = true;
   return upload_pod_table();
 }
 
@@ -608,7 +753,7 @@ int Cluster::flush_node_updates() {
   for (size_t q = 0; q < cnt; ++q) {
     const int32_t i = static_dirty_[q];
     static_queued_[i] = 0;
-    const NodeRec& r = *nodes_[order_[i]];
+    NodeRec& r = *nodes_[order_[i]];
     NodeUpdate& u = rec[q];
     std::memset(&u, 0, sizeof(u));
     u.node = i;
@@ -636,6 +781,7 @@ int Cluster::flush_node_updates() {
       lbl.push_back(e);
     }
     u.lbl_cnt = (int32_t)(lbl.size() - u.lbl_off);
+    r.stale = false;  // (a queued node's dynamic columns are flushed right after, in ensure_mirror)
   }
   static_dirty_.clear();
   const size_t b0 = cnt * sizeof(NodeUpdate), b1 = std::max<size_t>(ids.size(), 1) * 4,
@@ -680,7 +826,7 @@ int Cluster::flush_node_dynamic() {
   for (size_t q = 0; q < cnt; ++q) {
     const int32_t i = dyn_dirty_[q];
     dyn_queued_[i] = 0;
-    const NodeRec& r = *nodes_[order_[i]];
+    NodeRec& r = *nodes_[order_[i]];
     if (r.ports.size() > (size_t)kPortSlots) {
       err = "node " + r.spec.name + " uses more host ports than supported";
       layout_dirty = true;  // the next cycle re-lays out (and reports the same)
@@ -700,6 +846,7 @@ int Cluster::flush_node_dynamic() {
     for (int q2 = 0; q2 < kPortSlots; ++q2) d.ports[q2] = 0xffffffffu;
     int k = 0;
     for (uint32_t p : r.ports) d.ports[k++] = p;
+    r.stale = false;
   }
   dyn_dirty_.clear();
   const size_t bytes = cnt * sizeof(NodeDyn);

@@ -1431,6 +1431,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
     if (first < n && !rot_dev) c->next_start = ns_before[(size_t)first];
     c->layout_dirty = true;
+    c->mirror_suspect = true;  // not a gather re-layout: unchanged nodes' device columns are suspect too
     c->pods_dirty = true;
     c->err = why + ": pods " + std::to_string(first) + ".." + std::to_string(n - 1) +
              " of the batch were not scheduled (status Error); the device mirror is rebuilt from the cache";

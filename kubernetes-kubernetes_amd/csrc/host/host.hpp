@@ -214,6 +214,11 @@ struct NodeRec {
   // false: a ghost NodeInfo (cache.go:442-446, 672-689) -- pods arrived before their node, or the
   // node was removed while pods remained; it holds their requests but is skipped by snapshots
   bool real = true;
+  // the shadow changed since the device columns were last written (a re-layout by gather keeps a
+  // node's device columns only if it is not stale, Cluster::relayout_gather)
+  bool stale = true;
+  int32_t laid_ix = -1;     // the node's index in the device layout of epoch laid_epoch
+  uint64_t laid_epoch = 0;
 };
 
 struct TaintRec { std::string key, value, effect; };
@@ -300,6 +305,7 @@ class Cluster {
   hipStream_t stream = nullptr;
   bool layout_dirty = true;
   bool defer_relayout = false;  // ensure_label_slot only marks layout_dirty (pods in flight)
+  bool mirror_suspect = false;  // device columns may hold assumes the cache lacks: rebuild all of them
   std::vector<uint32_t> node_toff_, node_ioff_;  // taint / image CSR offsets as laid out on the device
   int upload_node_static(int32_t i);  // queue an in-place node update (flushed by ensure_mirror)
   int flush_node_updates();
@@ -348,6 +354,16 @@ class Cluster {
   void* dalloc(size_t bytes);
   void free_all();
   int upload_label_column(int32_t key);
+  // node add / remove / zone move: move every unchanged node's device columns to its new index
+  // (one gather per column block) instead of rebuilding the mirror; false if the layout must be
+  // rebuilt (capacity grown, first layout)
+  int relayout_gather(bool* done);
+  uint64_t laid_epoch_ = 0;              // the device layout's epoch (NodeRec::laid_epoch)
+  int32_t laid_slots_ = 0;               // label slots laid out
+  size_t taint_cap_ = 0, img_cap_ = 0;   // device CSR id capacities
+  DevBuf gather_dev_;                    // relayout_gather scratch
+ public:
+  uint64_t relayouts_full = 0, relayouts_gather = 0;  // diagnostics
 };
 
 // ===================================================================================

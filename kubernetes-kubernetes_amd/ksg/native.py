@@ -31,6 +31,8 @@ def load():
         lib.ksg_create_error.restype = C.c_char_p
         lib.ksg_shard_range.restype = C.c_int
         lib.ksg_shard_range.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.ksg_debug_relayouts.restype = C.c_int
+        lib.ksg_debug_relayouts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib.ksg_debug_compare_mirror.restype = C.c_int
         lib.ksg_debug_compare_mirror.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         _lib = lib
@@ -58,6 +60,12 @@ class Scheduler(Backend):
         self._chk(self.lib.ksg_debug_compare_mirror(self.ctx, 1 if sync else 0, C.byref(nd), C.byref(first)),
                   "compare_mirror")
         return nd.value, first.value
+
+    def relayouts(self):
+        """(full mirror rebuilds, gather re-layouts) so far (ksg_debug_relayouts)."""
+        f, g = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.ksg_debug_relayouts(self.ctx, C.byref(f), C.byref(g)), "relayouts")
+        return f.value, g.value
 
     def shard_range(self):
         """(first snapshot index, node count) this rank evaluates (node-sharded contexts)."""

@@ -300,6 +300,48 @@ def test_loop_give_up_recovers(native, agg):
     assert g.compare_mirror(sync=False) == (0, -1)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_node_add_remove_by_gather(native, seed):
+    """Node adds, removes and zone moves between cycles move the unchanged nodes' device columns to
+    their new snapshot index (relayout_gather) instead of rebuilding the mirror: the mirror equals
+    the cache after every cycle, the scheduling equals the oracle's, and the gather path is taken."""
+    rng, cfg, nodes, existing, names = rand_cluster(9100 + seed, n_nodes=700, n_existing=120)
+    g, o = _pair(native, cfg, nodes, existing)
+    _cmp_cycle(g, o, rand_pod(rng, 0, names), "warm-up", evaluate=False)
+    full0, gat0 = g.relayouts()
+    k = 1
+    for step in range(12):
+        kind = step % 3
+        if kind == 0:  # add two nodes (zones drawn as the generator does)
+            for j in range(2):
+                extra = dict(nodes[rng.randrange(len(nodes))])
+                extra["metadata"] = dict(extra["metadata"], name=f"add-{seed}-{step}-{j}",
+                                         labels=dict(extra["metadata"].get("labels", {}),
+                                                     **{"kubernetes.io/hostname": f"add-{seed}-{step}-{j}"}))
+                g.add_node(extra)
+                o.add_node(extra)
+        elif kind == 1:  # remove a node (its pods become a ghost's)
+            victim = g.node_names()[rng.randrange(len(g.node_names()))]
+            g.remove_node(victim)
+            o.remove_node(victim)
+        else:  # a zone move
+            nm = g.node_names()[rng.randrange(len(g.node_names()))]
+            src = next(n for n in nodes if n["metadata"]["name"] == nm) if any(
+                n["metadata"]["name"] == nm for n in nodes) else None
+            if src is not None:
+                upd = dict(src)
+                upd["metadata"] = dict(src["metadata"], labels=dict(src["metadata"].get("labels", {}),
+                                                                    **{"topology.kubernetes.io/zone": "zone-b"}))
+                g.update_node(upd)
+                o.update_node(upd)
+        for _ in range(4):
+            _cmp_cycle(g, o, rand_pod(rng, k, names), f"seed {seed} step {step} pod {k}", evaluate=False)
+            k += 1
+        assert g.compare_mirror(sync=False) == (0, -1), f"mirror differs from the cache after step {step}"
+    full1, gat1 = g.relayouts()
+    assert gat1 - gat0 >= 6, f"node events re-laid out by gather only {gat1 - gat0} times (full {full1 - full0})"
+
+
 # ---- percentageOfNodesToScore: the cut feasible list and the device-resident nextStartNodeIndex
 # (schedule_one.go:778-884, 686-687).  Random clusters are >= 100 nodes so the cut is active; the
 # no-score profile takes numNodesToFind = 1 (schedule_one.go:780-782).
