@@ -162,6 +162,14 @@ static bool empty_term(const NSTerm& t) { return t.exprs.empty() && t.fields.emp
 int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
                     const uint8_t* node_list) {
   const Config& cfg = c->cfg;
+  using pclk = std::chrono::steady_clock;
+  pclk::time_point pt = cfg.loop_stamps ? pclk::now() : pclk::time_point{};
+  auto mark = [&](int k) {
+    if (!cfg.loop_stamps) return;
+    const pclk::time_point t = pclk::now();
+    cprof_[k] += std::chrono::duration<double, std::micro>(t - pt).count();
+    pt = t;
+  };
   const int32_t N = (int32_t)c->order().size();
   Blob B;
   PodDesc& D = B.d();
@@ -278,6 +286,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   if (!p.has_preferred_na && !cfg.has_added_pref) smask &= ~(1u << P_NA);
   if (sb.rc) return sb.rc;
 
+  mark(0);
   // NodeName (node_name.go:67-83)
   if (!p.node_name.empty()) {
     int32_t ix = c->index_of(p.node_name);
@@ -345,6 +354,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     D.pod_ports_off = B.put(own);
   }
 
+  mark(1);
   // NodeResourcesFit PreFilter + assume payload (fit.go:317-335; framework/types.go:1035-1076)
   const PodResources res = calc_resources(p);
   out->res = res;
@@ -449,11 +459,13 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     D.img_count = (int64_t)names.size();
   }
 
+  mark(2);
   // PodTopologySpread / InterPodAffinity: per-domain aggregation programs
   {
     const int rc = compile_topology(p, mode, plugin, N, &B, &D, &fmask, &smask, out);
     if (rc) return rc;
   }
+  mark(3);
 
   // selector program pools
   D.req_off = B.put(sb.reqs);
@@ -581,6 +593,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   if (p.terminating) D.flags |= DF_TERMINATING;
   B.finish();
   out->blob = std::move(B.b);
+  mark(4);
   return KSG_OK;
 }
 
@@ -594,6 +607,14 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
   Blob& B = *Bp;
   PodDesc& D = *Dp;
   const Config& cfg = c->cfg;
+  using pclk = std::chrono::steady_clock;
+  pclk::time_point pt = cfg.loop_stamps ? pclk::now() : pclk::time_point{};
+  auto mark = [&](int k) {
+    if (!cfg.loop_stamps) return;
+    const pclk::time_point t = pclk::now();
+    cprof_[k] += std::chrono::duration<double, std::micro>(t - pt).count();
+    pt = t;
+  };
   // the plugins this evaluation actually runs (profile in CYCLE mode, the one plugin otherwise)
   uint32_t* const fmask_caller = fmask;
   uint32_t* const smask_caller = smask;
@@ -677,6 +698,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
     return KSG_ENOTSUP;
   }
 
+  mark(5);
   // ---------------- InterPodAffinity (framework.NewPodInfo for the incoming pod)
   const bool ipa_f = (*fmask >> P_IPA) & 1u, ipa_s = (*smask >> P_IPA) & 1u;
   std::vector<IpaTerm> raff, ranti, paff, panti;
@@ -773,6 +795,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
     }
   }
   D.hard_weight = cfg.hard_weight;
+  mark(6);
 
   // k_agg_loop's placement of every histogram (AggRef, desc.h): a key whose values are each on one
   // node only keeps per-node counts with the node's owner workgroup (its presence flags are not
@@ -864,6 +887,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
     if (((fm_in >> q) & 1u) && !((fm >> q) & 1u)) *fmask_caller &= ~(1u << q);
     if (((sm_in >> q) & 1u) && !((sm >> q) & 1u)) *smask_caller &= ~(1u << q);
   }
+  mark(7);
   return KSG_OK;
 }
 
@@ -1901,6 +1925,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     std::fprintf(stderr, "[host, us per pod] compile %.3f  stage+launch %.3f  wait %.3f  results+assume %.3f\n",
                  us(T0, T1) / n, us(T1, T2) / n, us(T2, T3) / n, us(T3, T4) / n);
+    std::fprintf(stderr, "[compile sections, us per pod] node-affinity %.3f  taints+ports %.3f  resources+images %.3f  "
+                 "topology %.3f (spread %.3f  affinity %.3f  placement+tables %.3f)  masks+assume %.3f\n", cprof_[0] / n,
+                 cprof_[1] / n, cprof_[2] / n, cprof_[3] / n, cprof_[5] / n, cprof_[6] / n, cprof_[7] / n, cprof_[4] / n);
+    for (double& v : cprof_) v = 0;
   }
   if (eval) {
     const int32_t N = m.n;

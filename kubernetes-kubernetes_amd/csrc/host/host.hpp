@@ -404,6 +404,7 @@ class Engine {
   // compile `p` for the current cluster; rot_start from Cluster::next_start
   int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
               const uint8_t* node_list = nullptr);
+  double cprof_[8] = {};  // loopStamps: compile time per section (us), reported with the host line
   int compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* B, PodDesc* D, uint32_t* fmask,
                        uint32_t* smask, CompiledPod* out);
   // run a batch of cycles (device-resident, sequential semantics)

@@ -36,14 +36,14 @@ def main():
     for n, calls, tot, avg, pct in rows:  # top_kernels is in us; kernels.duration is ns
         lines.append(f"{short(n):60s} {calls:8d} {tot:12.1f} {avg:9.3f} {pct:6.2f}")
     # per-dispatch durations of the roofline kernel
-    for kn in ("k_filter_score", "k_sched_loop"):
+    for kn in ("k_filter_score", "k_sched_loop", "k_agg_loop"):
         d = [r[0] for r in c.execute(f"select duration from kernels where name like '%{kn}%'")]
         if d:
             d.sort()
             lines.append(f"{kn} dispatch duration us: median {d[len(d) // 2] / 1e3:.3f} "
                          f"p10 {d[len(d) // 10] / 1e3:.3f} p90 {d[9 * len(d) // 10] / 1e3:.3f}")
-            if kn == "k_sched_loop":
-                lines.append(f"k_sched_loop per pod us (mean dispatch / {loop_pods:.2f} pods per dispatch): "
+            if kn in ("k_sched_loop", "k_agg_loop"):
+                lines.append(f"{kn} per pod us (mean dispatch / {loop_pods:.2f} pods per dispatch): "
                              f"{sum(d) / len(d) / 1e3 / loop_pods:.3f}")
     open(os.path.join(out, f"{tag}_kernel_stats.txt"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
@@ -67,7 +67,7 @@ def main():
         fa = sum(f) / len(f) if f else 0.0
         wa = sum(w) / len(w) if w else 0.0
         pl.append(f"{k:60s} dispatches {len(f):6d} FETCH_KiB {fa:10.2f} (x2 {2 * fa:10.2f}) WRITE_KiB {wa:10.2f}")
-        for kn, per_unit in (("k_filter_score", 1), ("k_sched_loop", loop_pods)):
+        for kn, per_unit in (("k_filter_score", 1), ("k_sched_loop", loop_pods), ("k_agg_loop", loop_pods)):
             if k.endswith(kn):
                 traffic[kn] = {"kernel": kn, "nodes": nodes, "workload": workload, "fetch_kib_raw": fa / per_unit,
                                "write_kib": wa / per_unit,
