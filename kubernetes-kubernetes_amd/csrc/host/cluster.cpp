@@ -117,17 +117,24 @@ void Cluster::tree_remove(const NodeSpec& n) {  // node_tree.go:70-99
 // its list position (the list holds pointers into the map, updated in place, :257-259).
 const std::vector<std::string>& Cluster::order() {
   bool rebuild = false;
-  for (auto& nm : snap_new_) {
-    auto it = nodes_.find(nm);
-    if (it != nodes_.end() && it->second->real && snap_names_.insert(nm).second) rebuild = true;
+  // (an unordered_set's clear() zeroes its whole bucket array, ~1 MB after a 100k-node load: once
+  // per pod that was the largest host cost of a 100k-node batch, so it runs only when there was
+  // something to take, and a large set gives its buckets back)
+  if (!snap_new_.empty()) {
+    for (auto& nm : snap_new_) {
+      auto it = nodes_.find(nm);
+      if (it != nodes_.end() && it->second->real && snap_names_.insert(nm).second) rebuild = true;
+    }
+    if (snap_new_.bucket_count() > 1024) std::unordered_set<std::string>().swap(snap_new_);
+    else snap_new_.clear();
   }
-  snap_new_.clear();
   if (!snap_gone_.empty()) {  // removeDeletedNodesFromSnapshot (cache.go:361-372)
     for (auto& nm : snap_gone_) {
       auto it = nodes_.find(nm);
       if ((it == nodes_.end() || !it->second->real) && snap_names_.erase(nm)) rebuild = true;
     }
-    snap_gone_.clear();
+    if (snap_gone_.bucket_count() > 1024) std::unordered_set<std::string>().swap(snap_gone_);
+    else snap_gone_.clear();
   }
   if (rebuild) {  // updateNodeInfoSnapshotList(updateAll=true) over nodeTree.list (node_tree.go:119-143)
     ++node_gen_;
