@@ -1185,13 +1185,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // Compiling a chunk after chunk 0 is launched needs every pod-table slot reserved and uploaded
   // before the first launch: a later full upload would overwrite the pod_node entries the device
   // assumes wrote.  A reservation adds the pod's (anti-)affinity terms to the key tables other pods'
-  // compiles read, so batches holding PodTopologySpread / InterPodAffinity / extended-resource pods
-  // (the compile paths that can also fail) compile everything before the first launch.
+  // compiles read (existing-pod keys: InterPodAffinity then keeps histograms for keys no placed pod
+  // has yet -- all-zero counts, the same filter outcome and a zero normalised score, as the
+  // sequential compile already gives for the earlier pods of a batch that end up unplaced).
+  // Batches with extended-resource pods (a compile path that can add a column) compile everything
+  // before the first launch.
   bool pipe = bnd.size() > 1;
-  for (int i = 0; i < n && pipe; ++i) {
-    const PodSpec& q = *pods[i];
-    pipe = !q.has_pod_affinity && !q.has_pod_anti && q.spreads.empty() && calc_scalar_free(q);
-  }
+  for (int i = 0; i < n && pipe; ++i) pipe = calc_scalar_free(*pods[i]);
   std::vector<int32_t> pre_slot;
   if (pipe && assume) {
     pre_slot.resize(n);
@@ -1353,10 +1353,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (use_agg) {
     bool any = false;
     int64_t own = 0;
-    for (int i = 0; i < compiled; ++i) {
-      any = any || agg_loop_ok(cp[i]);
-      own += cp[i].own_terms;
-    }
+    for (int i = 0; i < compiled; ++i) any = any || agg_loop_ok(cp[i]);
+    if (!pre_slot.empty())  // pods compiled later: their own terms are reserved already
+      for (int32_t sl : pre_slot) own += (int64_t)c->pt_terms[(size_t)sl].size();
+    else
+      for (int i = 0; i < compiled; ++i) own += cp[i].own_terms;
     use_agg = any && c->pt_node.size() < ((size_t)1 << 23) && c->tt.size() < ((size_t)1 << 23);
     if (use_agg) {
       std::vector<int32_t> wg_of((size_t)NB), np((size_t)G, 0), nt((size_t)G, 0);
