@@ -258,7 +258,9 @@ def main():
     kname = max(set(k[3] for k in kstats), key=lambda nm: sum(1 for k in kstats if k[3] == nm))
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
-    tpath = a.traffic or os.path.join(ROOT, "profiles", f"traffic_{kname}.json")
+    tpath = a.traffic or os.path.join(ROOT, "profiles", f"traffic_{kname}_{a.workload}.json")
+    if not os.path.exists(tpath):
+        tpath = os.path.join(ROOT, "profiles", f"traffic_{kname}.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))

@@ -49,7 +49,8 @@ def main():
     print("\n".join(lines))
 
     per = {}
-    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+    sfx = os.environ.get("KSG_PROF_PMC_SUFFIX", "")  # e.g. "_c4": gpurun_out/prof/pmc_fetch_c4
+    for counter, sub in (("FETCH_SIZE", "pmc_fetch" + sfx), ("WRITE_SIZE", "pmc_write" + sfx)):
         p = os.path.join(PROF, sub, "run_results.db")
         if not os.path.exists(p):
             continue
@@ -78,8 +79,9 @@ def main():
                                        + ", separate PMC passes (tag " + tag + ")"}
     open(os.path.join(out, f"{tag}_pmc.txt"), "w").write("\n".join(pl) + "\n")
     print("\n".join(pl))
-    for kn, t in traffic.items():
-        json.dump(t, open(os.path.join(out, f"traffic_{kn}.json"), "w"), indent=1)
+    for kn, t in traffic.items():  # k_agg_loop runs on several workloads: one file per workload
+        fn = f"traffic_{kn}_{workload}.json" if kn == "k_agg_loop" else f"traffic_{kn}.json"
+        json.dump(t, open(os.path.join(out, fn), "w"), indent=1)
 
     # shader-counter pass (scripts/gpu_prof_sq.sh): instruction mix per wave and per pod, clock
     p = os.path.join(PROF, "pmc_sq", "run_results.db")
