@@ -23,8 +23,10 @@ constexpr int kNumPlugins = 10;  // KSG_NUM_PLUGINS
 constexpr int kBlock = 256;      // threads per block of the per-node kernels (4 waves)
 constexpr int kMaxScalar = 16;   // interned extended/scalar resource columns
 constexpr int kPortSlots = 8;    // used-port slots per node (grown by the host if exceeded)
-constexpr int kMaxCons = 8;      // PodTopologySpread constraints per kind per pod
-constexpr int kMaxPodTerms = 8;  // InterPodAffinity terms per kind per pod
+constexpr int kMaxCons = 32;      // PodTopologySpread constraints per kind per pod (eligibility is a 32-bit mask)
+constexpr int kMaxPodTerms = 64;  // InterPodAffinity terms per kind per pod
+constexpr int kAggMaxCons = 8;    // k_agg_loop: constraints / terms per kind of a looped pod (LDS minima, the
+constexpr int kAggMaxTerms = 8;   // fold plan's lane layout); pods with more take the launch path
 constexpr int kMaxShards = 8;    // node shards (GPUs) of one node-sharded scheduler
 constexpr int kBlobLds = 16384;  // pod programs up to this size are staged in LDS by the kernels
 constexpr int kLoopMaxPods = 1024;  // k_sched_loop: pods per launch (their program offsets are staged in LDS)

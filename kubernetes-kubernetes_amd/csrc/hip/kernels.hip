@@ -2296,8 +2296,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ uint32_t s_pods[kAggPods], s_terms[kAggTerms];  // (slot | term) << 9 | node slot
   __shared__ uint32_t s_np, s_nt;
   __shared__ uint32_t s_off[kLoopMaxPods];
-  __shared__ long long s_pmin[kMaxCons];
-  __shared__ uint32_t s_pndom[kMaxCons];
+  __shared__ long long s_pmin[kAggMaxCons];
+  __shared__ uint32_t s_pndom[kAggMaxCons];
   __shared__ uint32_t s_any, s_gany, s_ok, s_F, s_psb, s_acc, s_gbar;
   __shared__ long long s_lmin[kAggLocalCons];
   __shared__ uint32_t s_lcnt[kAggLocalCons];
@@ -2320,7 +2320,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ unsigned long long s_p2k;
   __shared__ int s_p2n;
   __shared__ int64_t s_mx[4];
-  __shared__ uint32_t s_pmult[kMaxCons];  // DoNotSchedule: present domains at the minimum
+  __shared__ uint32_t s_pmult[kAggMaxCons];  // DoNotSchedule: present domains at the minimum
   const int w = blockIdx.x, G = av.nwg;
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)

@@ -827,7 +827,10 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
   D.agg_gwords = gwords;
   D.agg_nlocal = nlocal;
   D.agg_local_cons = local_cons;
-  out->agg_ok = ptss.empty() && nlocal <= kAggLocal && gwords <= kAggGWords && nlc <= kAggLocalCons;
+  out->agg_ok = ptss.empty() && nlocal <= kAggLocal && gwords <= kAggGWords && nlc <= kAggLocalCons &&
+                ptsf.size() <= (size_t)kAggMaxCons && raff.size() <= (size_t)kAggMaxTerms &&
+                ranti.size() <= (size_t)kAggMaxTerms && paff.size() <= (size_t)kAggMaxTerms &&
+                panti.size() <= (size_t)kAggMaxTerms;
 
   // key table for the existing-term pass: {label slot, existing-anti base, topology-score base, AggRefs}
   std::vector<int32_t> keytab;
@@ -939,9 +942,12 @@ bool Engine::agg_loop_ok(const CompiledPod& p) const {
   if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET))
     return false;
   if (d.score_mask & (1u << P_PTS)) return false;
+  // the fold plan holds <= 8 items per kind of the next pod's constraints / terms plus one per own
+  // term of the pod just placed (kFoldMax = 80 in k_agg_loop)
+  if (d.n_own_terms > 4 * kAggMaxTerms) return false;
   // raw InterPodAffinity scores ride the granules biased by 2^46: every existing term and pod adds
   // at most 100 per matching term of the pod
-  const double ipa_bound = ((double)c->tt.size() + (double)c->pt_node.size() + 1.0) * 100.0 * (4.0 * kMaxPodTerms + 1.0);
+  const double ipa_bound = ((double)c->tt.size() + (double)c->pt_node.size() + 1.0) * 100.0 * (4.0 * kAggMaxTerms + 1.0);
   if (ipa_bound >= (double)kAggIpaBias) return false;
   return loop_bounds_ok(p);
 }

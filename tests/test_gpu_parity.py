@@ -266,6 +266,78 @@ def test_agg_loop_matches_launch_path(native, seed, wg):
     assert g.compare_mirror(sync=False) == (0, -1), "device mirror differs from the cache after the batch"
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_agg_loop_pipelined_batch(native, seed):
+    """400 random pods in one batch: chunks after the first are compiled while k_agg_loop runs, with
+    every pod's slot (and its affinity terms) reserved up front -- identical to the sequential oracle
+    and to the per-pod launch path, unplaced pods included."""
+    rng, cfg, nodes, existing, names = rand_cluster(7100 + seed, n_nodes=[400, 900, 260][seed], n_existing=150)
+    g, o = _pair(native, cfg, nodes, existing)
+    g2, _ = _pair(native, dict(cfg, aggLoop=False), nodes, existing)
+    pods = [rand_pod(rng, k, names) for k in range(400)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"
+    assert g.compare_mirror(sync=False) == (0, -1)
+
+
+def _crowd(rng, pod, n_cons, n_terms):
+    """More PodTopologySpread constraints / pod (anti-)affinity terms than k_agg_loop takes (8 per
+    kind): the launch path evaluates them (the limit is 32 constraints, 64 terms per kind)."""
+    from fuzz_gen import rand_label_selector, rand_pa_term, TOPO_KEYS
+    spec = pod.o["spec"] if hasattr(pod, "o") else pod["spec"]
+    cs = spec.setdefault("topologySpreadConstraints", [])
+    for _ in range(n_cons):
+        c = {"maxSkew": rng.randint(1, 12), "topologyKey": rng.choice(TOPO_KEYS),
+             "whenUnsatisfiable": "DoNotSchedule" if rng.random() < 0.3 else "ScheduleAnyway"}
+        sel = rand_label_selector(rng)
+        if sel is not None:
+            c["labelSelector"] = sel
+        cs.append(c)
+    if n_terms:
+        aff = spec.setdefault("affinity", {})
+        for kind in ("podAffinity", "podAntiAffinity"):
+            a = aff.setdefault(kind, {})
+            if rng.random() < 0.5:  # required terms: most select pods that do not exist (a feasible rest)
+                ts = [rand_pa_term(rng) for _ in range(n_terms)]
+                for t in ts:
+                    if rng.random() < (0.85 if kind == "podAntiAffinity" else 0.0):
+                        t["labelSelector"] = {"matchLabels": {"app": "absent"}}
+                    elif kind == "podAffinity":
+                        t["labelSelector"] = {}
+                        t.pop("namespaceSelector", None)
+                a["requiredDuringSchedulingIgnoredDuringExecution"] = ts
+            a["preferredDuringSchedulingIgnoredDuringExecution"] = [
+                {"weight": rng.randint(1, 100), "podAffinityTerm": rand_pa_term(rng)} for _ in range(n_terms)]
+    return pod
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_many_constraints_and_terms(native, seed):
+    """Pods with 9..32 spread constraints and 9..20 affinity terms per kind (formerly KSG_ENOTSUP):
+    per-cycle results and per-node evaluations, then a pipelined batch mixing them with random pods,
+    against the oracle."""
+    rng, cfg, nodes, existing, names = rand_cluster(7200 + seed, n_nodes=[150, 333, 600][seed], n_existing=120)
+    g, o = _pair(native, cfg, nodes, existing)
+    for k in range(16):
+        pod = rand_pod(rng, k, names, topology=False)
+        _crowd(rng, pod.o if hasattr(pod, "o") else pod, rng.randint(9, 32) if k % 2 == 0 else rng.randint(0, 3),
+               rng.randint(9, 20) if k % 4 < 2 else 0)
+        _cmp_cycle(g, o, pod, f"seed {seed} pod {k}")
+    pods = []
+    for k in range(300):
+        pod = rand_pod(rng, 100 + k, names)
+        if k % 5 == 0:
+            _crowd(rng, pod.o if hasattr(pod, "o") else pod, rng.randint(9, 12), rng.randint(0, 10))
+        pods.append(pod)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"seed {seed} batch pod {k}"
+
+
 @pytest.mark.parametrize("agg", [False, True])
 def test_loop_give_up_recovers(native, agg):
     """A persistent loop that gives up (forced with debugLoopGiveUpAt: every workgroup stops at the
