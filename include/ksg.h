@@ -180,6 +180,44 @@ int ksg_run_filter_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, int32_t 
 int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uint8_t *nodes,
                          int32_t *status_code, int64_t *raw, int64_t *normalized);
 
+/* ---- DefaultPreemption PostFilter ------------------------------------------
+ * Replaces Evaluator.Preempt (framework/preemption/preemption.go:103-170) for a pod whose cycle
+ * ended in a FitError: PodEligibleToPreemptOthers (default_preemption.go:364-388), findCandidates
+ * (preemption.go:174-196), DryRunPreemption -- SelectVictimsOnNode (default_preemption.go:252-354)
+ * per node, on the device -- and SelectCandidate / pickOneNodeForPreemption (preemption.go:262-397).
+ * The call only selects: deleting the victims and setting status.nominatedNodeName (executor.go)
+ * stay with the caller, whose informer events later remove the victims (ksg_remove_pod).
+ * args_json (NULL: defaults):
+ *   {"offset": <int>,        GetOffsetAndNumCandidates' random offset (rand.Int31n upstream), taken
+ *                            modulo the number of potential nodes
+ *    "minCandidateNodesPercentage": 10, "minCandidateNodesAbsolute": 100,   (DefaultPreemptionArgs)
+ *    "now": <unix ns>,       GetPodStartTime's clock for pods without status.startTime (utils.go:52-58)
+ *    "allNodes": false,      true: every snapshot node is a potential node (DryRunPreemption over
+ *                            the node list, as the reference's unit tests call it)
+ *    "pdbs": [<policy/v1 PodDisruptionBudget JSON>, ...]}
+ * Potential nodes are taken in snapshot order (the reference iterates a map there) and checked with
+ * Parallelizer parallelism 1 semantics; victims of equal priority and start time keep NodeInfo.Pods
+ * order; candidates tied on every criterion resolve to the earliest in candidate-list order.
+ * Pods whose victims would change their PodTopologySpread or InterPodAffinity counts return
+ * KSG_ENOTSUP.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
+ * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}],
+ * "selected": <node|null>, "victims": [uid...]}; *detail_len gets its length (KSG_ENOMEM if cap is
+ * too small; the result is still filled). */
+#define KSG_PREEMPT_OK 0            /* a node was nominated */
+#define KSG_PREEMPT_NOT_ELIGIBLE 1  /* PodEligibleToPreemptOthers said no (PreemptionPolicy, terminating victims) */
+#define KSG_PREEMPT_NO_CANDIDATES 2 /* "preemption is not helpful for scheduling" */
+typedef struct ksg_preempt_result {
+  int32_t status;             /* KSG_CODE_SUCCESS (a node was nominated) or KSG_CODE_UNSCHEDULABLE */
+  int32_t reason;             /* KSG_PREEMPT_* */
+  int32_t node_index;         /* snapshot index of the nominated node, -1 if none */
+  int32_t num_potential;      /* nodes findCandidates passed to DryRunPreemption */
+  int32_t num_candidates;     /* candidates DryRunPreemption returned */
+  int32_t num_victims;        /* victims on the nominated node */
+  int64_t num_pdb_violations; /* Victims.NumPDBViolations of the nominated node */
+} ksg_preempt_result;
+int ksg_preempt(ksg_ctx *ctx, int32_t handle, const char *args_json, size_t args_len, ksg_preempt_result *result,
+                char *detail, size_t detail_cap, size_t *detail_len);
+
 /* ---- node-sharded evaluation ---------------------------------------------
  * A context created with {"distributed": {"worldSize": W, "rank": r, "ncclId": "<hex>"}}
  * holds the whole cluster mirror (every rank is fed the same informer events) and evaluates

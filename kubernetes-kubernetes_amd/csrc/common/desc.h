@@ -226,6 +226,39 @@ struct PodDesc {
   int32_t pad2;
 };
 
+// ---- DefaultPreemption: SelectVictimsOnNode per node, one thread each ----------
+// The host lays out, per snapshot node, the pods isPreemptionAllowed admits (lower priority than the
+// preemptor) in reprieve order: sorted by MoreImportantPod, the PDB-violating group first
+// (default_preemption.go:280-343).  k_preempt removes them all, re-runs the filters the removal can
+// change (NodePorts, NodeResourcesFit, then PodTopologySpread / InterPodAffinity on the cycle's
+// counts, which the host guarantees no victim changes), and reprieves them one by one.
+constexpr int kPreemptScalar = 4;  // scalar resources of the preemptor whose victim deltas are tracked
+enum PVFlags : uint32_t {
+  PV_PORT = 1u,  // the victim holds a host port the preemptor's ports conflict with
+  PV_VIOL = 2u,  // the victim is in the PDB-violating group (filterPodsWithPDBViolation)
+};
+struct PVictim {
+  int64_t cpu, mem, eph;          // Resource it adds to NodeInfo.Requested (PodInfo.CalculateResource)
+  int64_t sc[kPreemptScalar];     // its request of the preemptor's scalar resources, PodDesc scalar order
+  uint32_t flags;                 // PVFlags
+  uint32_t pad;
+};
+enum PNFlags : uint32_t {
+  PN_BASE_PORT = 1u,  // a conflicting host port stays on the node with every victim removed
+};
+struct PNode {
+  int32_t voff, vcnt;  // the node's victims in the PVictim array
+  uint32_t flags;      // PNFlags
+  int32_t pad;
+};
+enum PStat : uint32_t { PS_NOT_CHECKED = 0xffffffffu, PS_NO_VICTIMS = 0xfffffffeu };
+struct POut {
+  uint32_t st;         // packed Filter status with the victims removed (0: fits), or a PStat
+  int32_t nvictims;    // victims that stay removed (flag 1 in the per-victim output)
+  int32_t nviolating;  // of them, from the PDB-violating group (numViolatingVictim)
+  int32_t pad;
+};
+
 // Per-pod device result (ScheduleResult + diagnostics), written by the select kernel.
 struct DevResult {
   int32_t status;     // KSG_CODE_*

@@ -3306,4 +3306,139 @@ hipError_t warm_kernels() {
 #ifdef KSG_DIAG
 hipError_t set_diag(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &p, sizeof(p)); }
 #endif
+
+// =====================================================================================================
+// k_preempt: DefaultPreemption.SelectVictimsOnNode (default_preemption.go:252-354) for every node the
+// dry run may check (findCandidates' NodesForStatusCode(Unschedulable), preemption.go:174-196, or every
+// node), one thread per node, the preemptor's cycle status in b.status (k_filter_score, evaluation
+// output).  The node's state is the mirror minus the victims: the filters a removal can change run on
+// it -- NodePorts, NodeResourcesFit (the static filters before them passed or fail unchanged), then
+// PodTopologySpread / InterPodAffinity against the cycle's counts, which no victim of this call changes
+// (the host checked) -- and the victims are added back one at a time in reprieve order, each kept
+// removed only when the preemptor no longer fits with it (reprievePod, :316-330).
+// =====================================================================================================
+__device__ __forceinline__ uint32_t preempt_node_filters(const MirrorView& m, const NodeCore& nc, const int64_t* sreq,
+                                                         const uint8_t* base, const PodDesc& d, int i, bool port) {
+  const uint32_t fm = d.filter_mask;
+  if (((fm >> P_PORTS) & 1u) && port) return pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
+  if ((fm >> P_FIT) & 1u) {  // fit.go:593-734, as run_filters with the node's Requested less the victims
+    uint32_t reasons = 0;
+    bool unresolvable = false;
+    if ((int64_t)nc.npods + 1 > (int64_t)nc.apods) reasons |= KSG_R_TOO_MANY_PODS;
+    if (d.fit_any) {
+      if (d.req_cpu > 0 && d.req_cpu > nc.acpu - nc.rcpu) {
+        reasons |= KSG_R_INSUFFICIENT_CPU;
+        unresolvable |= d.req_cpu > nc.acpu;
+      }
+      if (d.req_mem > 0 && d.req_mem > nc.amem - nc.rmem) {
+        reasons |= KSG_R_INSUFFICIENT_MEMORY;
+        unresolvable |= d.req_mem > nc.amem;
+      }
+      if (d.req_eph > 0 && d.req_eph > nc.aeph - nc.reph) {
+        reasons |= KSG_R_INSUFFICIENT_EPHEMERAL;
+        unresolvable |= d.req_eph > nc.aeph;
+      }
+      const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
+#pragma unroll
+      for (int k = 0; k < kPreemptScalar; ++k) {  // unrolled: sreq stays in registers (no scratch)
+        if (k >= d.n_scalar) break;
+        const int64_t a = m.scalar_alloc[(size_t)sr[k].slot * (size_t)m.cap + (size_t)i];
+        if (sr[k].qty > a - sreq[k]) {
+          reasons |= KSG_R_INSUFFICIENT_SCALAR;
+          unresolvable |= sr[k].qty > a;
+        }
+      }
+    }
+    if (reasons) return pack_status(unresolvable ? C_UU : C_UNSCHED, P_FIT, reasons);
+  }
+  return 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, int pod, const PNode* pn,
+                                                    const PVictim* pv, uint8_t* vout, POut* out, int all_nodes) {
+  const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+  if (i >= m.n) return;
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  POut o{PS_NOT_CHECKED, 0, 0, 0};
+  const uint32_t st0 = b.status[i];
+  const PNode nd = pn[i];
+  if (!all_nodes && status_code(st0) != C_UNSCHED) {
+    out[i] = o;
+    return;
+  }
+  if (nd.vcnt == 0) {  // "No preemption victims found for incoming pod" (:291-294)
+    o.st = PS_NO_VICTIMS;
+    out[i] = o;
+    return;
+  }
+  // a status from a filter that reads no pod (or a PreFilter rejection) holds with the victims removed too
+  const uint32_t p0 = status_plugin(st0);
+  if (st0 != 0 && (p0 == P_UNSCHED || p0 == P_NODENAME || p0 == P_TAINT || p0 == P_NA || p0 == 15u)) {
+    o.st = st0;
+    out[i] = o;
+    return;
+  }
+  NodeCore nc = load_core(m, i);
+  int64_t sreq[kPreemptScalar];
+  const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
+  const int ns = d.n_scalar < kPreemptScalar ? d.n_scalar : kPreemptScalar;  // host-checked: n_scalar <= 4
+#pragma unroll
+  for (int k = 0; k < kPreemptScalar; ++k)
+    sreq[k] = k < ns ? m.scalar_req[(size_t)sr[k].slot * (size_t)m.cap + (size_t)i] : 0;
+  const PVictim* v = pv + nd.voff;
+  for (int q = 0; q < nd.vcnt; ++q) {  // removePod of every potential victim (:285-289)
+    nc.rcpu -= v[q].cpu;
+    nc.rmem -= v[q].mem;
+    nc.reph -= v[q].eph;
+#pragma unroll
+    for (int k = 0; k < kPreemptScalar; ++k) sreq[k] -= v[q].sc[k];
+  }
+  nc.npods -= nd.vcnt;
+  bool port = (nd.flags & PN_BASE_PORT) != 0;
+  uint32_t st = preempt_node_filters(m, nc, sreq, base, d, i, port);
+  if (st == 0) {
+    int64_t raw_taint = 0;
+    (void)raw_taint;
+    st = topo_filters(m, base, d, i, ArenaTopo{b.stats + pod, b.arena}, 0);
+  }
+  o.st = st;
+  if (st == 0) {
+    // reprieve in order (:331-343); PodTopologySpread / InterPodAffinity cannot change (host-checked)
+    for (int q = 0; q < nd.vcnt; ++q) {
+      const PVictim x = v[q];
+      NodeCore t = nc;
+      t.rcpu += x.cpu;
+      t.rmem += x.mem;
+      t.reph += x.eph;
+      t.npods += 1;
+      int64_t ts[kPreemptScalar];
+#pragma unroll
+      for (int k = 0; k < kPreemptScalar; ++k) ts[k] = sreq[k] + x.sc[k];
+      const bool tp = port || (x.flags & PV_PORT) != 0;
+      const bool fits = preempt_node_filters(m, t, ts, base, d, i, tp) == 0;
+      if (fits) {
+        nc = t;
+#pragma unroll
+        for (int k = 0; k < kPreemptScalar; ++k) sreq[k] = ts[k];
+        port = tp;
+        vout[nd.voff + q] = 0;
+      } else {
+        vout[nd.voff + q] = 1;
+        o.nvictims += 1;
+        o.nviolating += (x.flags & PV_VIOL) ? 1 : 0;
+      }
+    }
+  }
+  out[i] = o;
+}
+
+hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, const PNode* pn, const PVictim* pv,
+                          uint8_t* vout, POut* out, int all_nodes, hipStream_t s) {
+  const int nb = (m.n + kBlock - 1) / kBlock;
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_preempt, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pn, pv, vout, out, all_nodes);
+  return hipGetLastError();
+}
+
 }  // namespace ksg

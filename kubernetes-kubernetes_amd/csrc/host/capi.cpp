@@ -232,6 +232,31 @@ int ksg_run_filter_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t*
   })
 }
 
+int ksg_preempt(ksg_ctx* ctx, int32_t handle, const char* args_json, size_t args_len, ksg_preempt_result* result,
+                char* detail, size_t detail_cap, size_t* detail_len) {
+  if (!ctx || !result) return KSG_EINVAL;
+  GUARD({
+    auto it = ctx->engine->queue.find(handle);
+    if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    if (ctx->cluster->cfg.sharded()) {
+      ctx->err = "preemption on a node-sharded context is not supported";
+      return KSG_ENOTSUP;
+    }
+    std::string d;
+    const int rc = ctx->engine->preempt(it->second, args_json, args_len, result, detail ? &d : nullptr);
+    if (rc) return with_err(ctx, rc);
+    if (detail_len) *detail_len = d.size();
+    if (detail) {
+      if (d.size() + 1 > detail_cap) {
+        ctx->err = "detail buffer too small";
+        return KSG_ENOMEM;
+      }
+      std::memcpy(detail, d.c_str(), d.size() + 1);
+    }
+    return KSG_OK;
+  })
+}
+
 int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, const uint8_t* nodes, int32_t* status_code,
                          int64_t* raw, int64_t* normalized) {
   if (!ctx || !status_code) return KSG_EINVAL;

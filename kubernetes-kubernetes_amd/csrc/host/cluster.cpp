@@ -370,6 +370,12 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   bp.node = node_name;
   bp.res = res ? *res : calc_resources(p);
   bp.with_affinity = p.has_pod_affinity || p.has_pod_anti;
+  bp.name = p.name;
+  bp.priority = p.priority;
+  bp.has_start = p.has_start;
+  bp.start_ns = p.start_ns;
+  bp.preempt_terminating = p.preempt_terminating;
+  bp.req_anti = !p.anti_req.empty();
   pods_with_affinity += bp.with_affinity ? 1 : 0;
   auto take = [&](const Container& c) {
     for (auto& hp : c.ports)

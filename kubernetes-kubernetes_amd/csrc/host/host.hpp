@@ -40,6 +40,7 @@ using ResVec = std::vector<ResAmount>;
 bool parse_quantity(const std::string& s, int64_t* milli);
 int64_t milli_ceil(int64_t m);  // Quantity.Value() from milli-units (rounds up)
 bool parse_go_int(const std::string& s, int64_t* v);  // strconv.ParseInt(s, 10, 64)
+bool parse_rfc3339(const std::string& s, int64_t* unix_ns);  // metav1.Time (RFC 3339, optional fraction)
 bool valid_label_key(const std::string& k);            // validation.IsQualifiedName
 bool valid_label_value(const std::string& v);          // validation.IsValidLabelValue
 bool scalar_resource(const std::string& n);            // scheduler/util/utils.go:200-203
@@ -94,6 +95,13 @@ struct PodSpec {
   ResVec overhead, pod_requests;
   std::vector<Spread> spreads;
   std::vector<std::string> image_volumes;
+  // DefaultPreemption inputs (corev1helpers.PodPriority, util.GetPodStartTime, preemption/util.go:23-35)
+  int32_t priority = 0;          // spec.priority (0 when nil)
+  bool has_start = false;        // status.startTime != nil
+  int64_t start_ns = 0;          // status.startTime, Unix nanoseconds
+  bool preempt_never = false;    // spec.preemptionPolicy == Never
+  std::string nominated_node;    // status.nominatedNodeName
+  bool preempt_terminating = false;  // PodTerminatingByPreemption
 };
 struct NodeImage { std::vector<std::string> names; int64_t size; };
 struct NodeSpec {
@@ -196,6 +204,11 @@ struct BoundPod {  // a pod in the cache (added bound or assumed)
   std::vector<uint32_t> port_ids;
   bool with_affinity = false;  // podWithAffinity (framework/types.go:386-389)
   int32_t slot = -1;           // pod-table slot (PTS/IPA aggregation)
+  // DefaultPreemption (victim order, PDB matching, nominated-node eligibility)
+  std::string name;
+  int32_t priority = 0;
+  bool has_start = false, preempt_terminating = false, req_anti = false;
+  int64_t start_ns = 0;
 };
 
 struct NodeRec {
@@ -412,6 +425,8 @@ class Engine {
                 ksg_result* results, ksg_eval_out* eval);
   int run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* nodes, int32_t* code, uint8_t* codes,
                  uint32_t* reasons, int64_t* raw, int64_t* norm);
+  // DefaultPreemption's PostFilter for a pod that failed its cycle (preempt.cpp)
+  int preempt(const PodSpec& p, const char* args_json, size_t args_len, ksg_preempt_result* res, std::string* detail);
 
   // measurement: average k_filter_score duration (sampled with events when cfg.timing_stride > 0,
   // else the batch's kernel time / launches) and its algorithmic bytes per launch
@@ -445,6 +460,7 @@ class Engine {
   uint32_t gran_tag = 0;
   DevBuf d_agran, d_region;  // k_agg_loop: exchange granules (own tag sequence), per-pod shared regions
   DevBuf d_astamps;          // k_agg_loop diagnostic stamps
+  DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   uint32_t agran_tag = 0;
   int gran_setup();
   int next_gran_tag(uint32_t* tag);

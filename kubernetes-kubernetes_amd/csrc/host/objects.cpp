@@ -195,6 +195,56 @@ static bool container(const JDoc& d, const JVal& c, Container* out, std::string*
   return true;
 }
 
+// metav1.Time's RFC 3339 text ("2006-01-02T15:04:05Z", optional fraction up to 9 digits, Z or
+// +hh:mm / -hh:mm) to Unix nanoseconds; days from the civil date by the proleptic Gregorian rule
+bool parse_rfc3339(const std::string& s, int64_t* unix_ns) {
+  auto dig = [&](size_t at, int n, int64_t* v) {
+    if (at + n > s.size()) return false;
+    int64_t x = 0;
+    for (int k = 0; k < n; ++k) {
+      const char ch = s[at + k];
+      if (ch < '0' || ch > '9') return false;
+      x = x * 10 + (ch - '0');
+    }
+    *v = x;
+    return true;
+  };
+  int64_t Y, M, D, h, mi, sec;
+  if (!dig(0, 4, &Y) || s.size() < 20 || s[4] != '-' || !dig(5, 2, &M) || s[7] != '-' || !dig(8, 2, &D) ||
+      (s[10] != 'T' && s[10] != 't') || !dig(11, 2, &h) || s[13] != ':' || !dig(14, 2, &mi) || s[16] != ':' ||
+      !dig(17, 2, &sec))
+    return false;
+  size_t q = 19;
+  int64_t frac = 0;
+  if (q < s.size() && s[q] == '.') {
+    int nd = 0;
+    for (++q; q < s.size() && s[q] >= '0' && s[q] <= '9'; ++q, ++nd)
+      if (nd < 9) frac = frac * 10 + (s[q] - '0');
+    if (nd == 0) return false;
+    for (int k = nd; k < 9; ++k) frac *= 10;
+  }
+  int64_t off = 0;
+  if (q < s.size() && (s[q] == 'Z' || s[q] == 'z')) {
+    ++q;
+  } else if (q < s.size() && (s[q] == '+' || s[q] == '-')) {
+    int64_t oh, om;
+    if (!dig(q + 1, 2, &oh) || q + 3 >= s.size() || s[q + 3] != ':' || !dig(q + 4, 2, &om)) return false;
+    off = (s[q] == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+    q += 6;
+  } else {
+    return false;
+  }
+  if (q != s.size() || M < 1 || M > 12 || D < 1 || D > 31 || h > 23 || mi > 59 || sec > 60) return false;
+  const int64_t y = Y - (M <= 2);  // days_from_civil
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (M + (M > 2 ? -3 : 9)) + 2) / 5 + D - 1;
+  const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  const int64_t days = era * 146097 + doe - 719468;
+  *unix_ns = ((days * 86400 + h * 3600 + mi * 60 + sec) - off) * 1000000000LL + frac;
+  return true;
+}
+
 bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
   try {
     JDoc d(p, n);
@@ -208,8 +258,26 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
     if (out->uid.empty()) out->uid = out->ns + "/" + out->name;
     out->labels = kv_map(d, d.get(*md, "labels"));
     out->terminating = d.present(*md, "deletionTimestamp");
+    if (const JVal* st = d.get(r, "status")) {
+      const std::string t = d.str(*st, "startTime");
+      if (!t.empty()) {
+        if (!parse_rfc3339(t, &out->start_ns)) { *err = "bad status.startTime " + t; return false; }
+        out->has_start = true;
+      }
+      out->nominated_node = d.str(*st, "nominatedNodeName");
+      // PodTerminatingByPreemption (preemption/util.go:23-35): the first DisruptionTarget condition decides
+      bool seen = false;
+      d.each(d.get(*st, "conditions"), [&](const JVal& c) {
+        if (seen || d.str(c, "type") != "DisruptionTarget") return;
+        seen = true;
+        out->preempt_terminating =
+            out->terminating && d.str(c, "status") == "True" && d.str(c, "reason") == "PreemptionByScheduler";
+      });
+    }
     const JVal* sp = d.get(r, "spec");
     if (!sp) return true;
+    out->priority = (int32_t)d.num(*sp, "priority", 0);
+    out->preempt_never = d.str(*sp, "preemptionPolicy") == "Never";
     out->node_name = d.str(*sp, "nodeName");
     if (const JVal* ns = d.get(*sp, "nodeSelector")) {
       out->has_node_selector = true;

@@ -59,6 +59,25 @@ class Result(C.Structure):
         return (self.status, self.node_index, self.evaluated_nodes, self.feasible_nodes, self.total_score)
 
 
+PREEMPT_OK, PREEMPT_NOT_ELIGIBLE, PREEMPT_NO_CANDIDATES = 0, 1, 2
+
+
+class PreemptResult(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("reason", C.c_int32),
+        ("node_index", C.c_int32),
+        ("num_potential", C.c_int32),
+        ("num_candidates", C.c_int32),
+        ("num_victims", C.c_int32),
+        ("num_pdb_violations", C.c_int64),
+    ]
+
+    def as_tuple(self):
+        return (self.status, self.reason, self.node_index, self.num_potential, self.num_candidates,
+                self.num_victims, self.num_pdb_violations)
+
+
 class EvalOut(C.Structure):
     _fields_ = [
         ("prefilter_code", C.c_int32),
@@ -102,6 +121,7 @@ def _sig(lib, prefix):
     d("run_filter_plugin", C.c_int, vp, i32, i32, C.POINTER(i32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint32))
     d("run_score_plugin", C.c_int, vp, i32, i32, C.POINTER(C.c_uint8), C.POINTER(i32), C.POINTER(C.c_int64),
       C.POINTER(C.c_int64))
+    d("preempt", C.c_int, vp, i32, cp, sz, C.POINTER(PreemptResult), C.c_char_p, sz, C.POINTER(sz))
     return f
 
 
@@ -122,6 +142,7 @@ class Backend:
 
     def __init__(self, lib, prefix, config=None):
         self.lib = lib
+        self.prefix = prefix
         self.f = _sig(lib, prefix)
         cfg = _js(config or {})
         self.ctx = self.f["create"](cfg, len(cfg))
@@ -271,3 +292,12 @@ class Backend:
                 mask[i] = 1
         self._chk(self.f["run_score_plugin"](self.ctx, handle, pid, mask, C.byref(st), raw, nrm), "run_score_plugin")
         return st.value, list(raw[:n]), list(nrm[:n])
+
+    def preempt(self, handle, args=None, detail_cap=1 << 20):
+        """DefaultPreemption PostFilter for a compiled pod: (PreemptResult, detail dict)."""
+        a = _js(args or {})
+        r = PreemptResult()
+        buf = C.create_string_buffer(detail_cap)
+        dl = C.c_size_t(0)
+        self._chk(self.f["preempt"](self.ctx, handle, a, len(a), C.byref(r), buf, detail_cap, C.byref(dl)), "preempt")
+        return r, json.loads(buf.value.decode())

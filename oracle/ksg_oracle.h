@@ -41,6 +41,10 @@ int ksgo_run_filter_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, int32_
 int ksgo_run_score_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, const uint8_t *nodes,
                           int32_t *status_code, int64_t *raw, int64_t *normalized);
 
+/* DefaultPreemption PostFilter, same contract as ksg_preempt (include/ksg.h). */
+int ksgo_preempt(ksgo_ctx *ctx, int32_t handle, const char *args_json, size_t args_len, ksg_preempt_result *result,
+                 char *detail, size_t detail_cap, size_t *detail_len);
+
 /* Go math.Log restatement (exposed so tests can compare it with libm). */
 double ksgo_go_log(double x);
 /* container/heap Init over (score) with nodeScoreHeap.Less, returns index of the root. */

@@ -1806,6 +1806,338 @@ int ksgo_run_score_plugin(ksgo_ctx* c, int32_t handle, int32_t plugin, const uin
   return KSG_OK;
 }
 
+// ---- DefaultPreemption PostFilter (plugins/defaultpreemption/default_preemption.go,
+// framework/preemption/preemption.go) -------------------------------------------------------
+// PreFilter once, as the failed cycle ran it (framework.go:934-995); the cycle's state is cloned per
+// node for the dry run (preemption.go:420-424).
+static bool preempt_prefilter(ksgo_ctx* c, Cycle& cy) {
+  for (int p : prefilter_order()) {
+    if (!c->cfg.enabled[p]) { cy.skipFilter[p] = true; continue; }
+    bool skip = false, restricts = false;
+    std::vector<std::string> names;
+    Status s = run_prefilter_plugin(cy, p, &skip, &names, &restricts);
+    if (skip) { cy.skipFilter[p] = true; continue; }
+    if (!s.ok()) return false;
+  }
+  for (int p = 0; p < KSG_NUM_PLUGINS; ++p)
+    if (!c->cfg.enabled[p]) cy.skipFilter[p] = true;
+  return true;
+}
+static Status preempt_filter_node(Cycle& cy, NodeInfoO* ni) {  // RunFilterPluginsWithNominatedPods (no nominated pods)
+  Status st;
+  for (int p : kFilterOrder) {
+    if (cy.skipFilter[p]) continue;
+    st = run_filter(cy, p, ni);
+    if (!st.ok()) { st.plugin = p; break; }
+  }
+  return st;
+}
+// criticalPaths (podtopologyspread/filtering.go:84-136), the two smallest (value, count) of a constraint
+struct CritPaths { std::string v[2]; int64_t n[2] = {INT32_MAX, INT32_MAX}; };
+static void crit_update(CritPaths& p, const std::string& tv, int64_t num) {  // :108-136
+  int i = -1;
+  if (tv == p.v[0]) i = 0;
+  else if (tv == p.v[1]) i = 1;
+  if (i >= 0) {
+    p.n[i] = num;
+    if (p.n[0] > p.n[1]) { std::swap(p.v[0], p.v[1]); std::swap(p.n[0], p.n[1]); }
+  } else if (num < p.n[0]) {
+    p.v[1] = p.v[0]; p.n[1] = p.n[0];
+    p.v[0] = tv; p.n[0] = num;
+  } else if (num < p.n[1]) {
+    p.v[1] = tv; p.n[1] = num;
+  }
+}
+static void pair_update(PairCounts& m, const Node& n, const std::string& tk, int64_t v) {  // filtering.go:111-120
+  auto it = n.labels.find(tk);
+  if (it == n.labels.end()) return;
+  auto& x = m[{tk, it->second}];
+  x += v;
+  if (x == 0) m.erase({tk, it->second});
+}
+// the PreFilter extensions' AddPod / RemovePod (PodTopologySpread filtering.go:157-212,
+// InterPodAffinity filtering.go:75-85,329-346) on a cloned state
+static void preempt_update(Cycle& cy, std::vector<CritPaths>& crit, const PodInfo* pi, const Node& node, int64_t d) {
+  const Pod& pod = *cy.pod;
+  if (!cy.skipFilter[KSG_PLUGIN_POD_TOPOLOGY_SPREAD] && pi->pod.ns == pod.ns &&
+      node_labels_match_spread(node.labels, cy.ptsF)) {
+    for (size_t i = 0; i < cy.ptsF.size(); ++i) {
+      auto& con = cy.ptsF[i];
+      if (!selector_matches(con.sel, pi->pod.labels)) continue;
+      if (!match_inclusion(cy, con, node)) continue;
+      const std::string& v = node.labels.at(con.key);
+      int64_t& x = cy.tpMatch[i][v];
+      x += d;
+      crit_update(crit[i], v, x);
+      cy.critMin[i] = crit[i].n[0];
+    }
+  }
+  if (!cy.skipFilter[KSG_PLUGIN_INTER_POD_AFFINITY]) {
+    for (auto& t : pi->reqAnti)
+      if (t.matches(pod, cy.nsLabels)) pair_update(cy.existingAnti, node, t.topologyKey, d);
+    if (pod_matches_all_terms(cy.ipaReqAff, pi->pod))
+      for (auto& t : cy.ipaReqAff) pair_update(cy.affCounts, node, t.topologyKey, d);
+    for (auto& t : cy.ipaReqAnti)
+      if (t.matches(pi->pod, nullptr)) pair_update(cy.antiCounts, node, t.topologyKey, d);
+  }
+}
+
+struct OPdb { std::string ns; Selector sel; bool ok = false; int32_t allowed = 0; std::set<std::string> disrupted; };
+struct OVictims { std::vector<PodInfo*> pods; int64_t viol = 0; };
+
+// SelectVictimsOnNode (default_preemption.go:252-354); returns the status code (0: victims found)
+static int select_victims(ksgo_ctx* c, const Cycle& cy0, const std::vector<CritPaths>& crit0, const Pod& pod,
+                          NodeInfoO* orig, const std::vector<OPdb>& pdbs, int64_t now, OVictims* out) {
+  NodeInfoO ni = *orig;  // nodeInfo.Snapshot()
+  Cycle cy = cy0;        // state.Clone()
+  std::vector<CritPaths> crit = crit0;
+  auto start = [&](const PodInfo* p) { return p->pod.hasStartTime ? p->pod.startTimeNs : now; };
+  auto more_important = [&](const PodInfo* a, const PodInfo* b) {  // util.MoreImportantPod
+    if (a->pod.priority != b->pod.priority) return a->pod.priority > b->pod.priority;
+    return start(a) < start(b);
+  };
+  std::vector<PodInfo*> pot;
+  for (auto* pi : ni.pods)
+    if (pi->pod.priority < pod.priority) pot.push_back(pi);  // isPreemptionAllowed
+  for (auto* pi : pot) {
+    node_remove_pod(ni, pi->pod.uid);
+    preempt_update(cy, crit, pi, ni.node, -1);
+  }
+  if (pot.empty()) return KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;  // "No preemption victims found"
+  Status st = preempt_filter_node(cy, &ni);
+  if (!st.ok()) return st.code;
+  // sort.Slice: an insertion sort (stable) up to 12 elements; equal keys keep NodeInfo.Pods order
+  std::stable_sort(pot.begin(), pot.end(), more_important);
+  // filterPodsWithPDBViolation (:406-452)
+  std::vector<int32_t> allowed;
+  for (auto& b : pdbs) allowed.push_back(b.allowed);
+  std::vector<PodInfo*> violating, nonViolating;
+  for (auto* pi : pot) {
+    bool v = false;
+    if (!pi->pod.labels.empty())
+      for (size_t i = 0; i < pdbs.size(); ++i) {
+        const OPdb& b = pdbs[i];
+        if (b.ns != pi->pod.ns || !b.ok || !selector_matches(b.sel, pi->pod.labels)) continue;
+        if (b.disrupted.count(pi->pod.name)) continue;
+        if (--allowed[i] < 0) v = true;
+      }
+    (v ? violating : nonViolating).push_back(pi);
+  }
+  std::vector<PodInfo*> victims;
+  int64_t numViol = 0;
+  auto reprieve = [&](PodInfo* pi) {  // :316-330
+    node_add_pod(ni, pi);
+    preempt_update(cy, crit, pi, ni.node, +1);
+    bool fits = preempt_filter_node(cy, &ni).ok();
+    if (!fits) {
+      node_remove_pod(ni, pi->pod.uid);
+      preempt_update(cy, crit, pi, ni.node, -1);
+      victims.push_back(pi);
+    }
+    return fits;
+  };
+  for (auto* pi : violating)
+    if (!reprieve(pi)) ++numViol;
+  for (auto* pi : nonViolating) reprieve(pi);
+  if (!violating.empty() && !nonViolating.empty()) std::stable_sort(victims.begin(), victims.end(), more_important);
+  if (victims.empty()) return KSG_CODE_ERROR;  // "expected at least one victim pod on node"
+  out->pods = victims;
+  out->viol = numViol;
+  return KSG_CODE_SUCCESS;
+}
+
+static void ojson_str(std::string& o, const std::string& s) {
+  o += '"';
+  for (char ch : s) {
+    if (ch == '"' || ch == '\\') { o += '\\'; o += ch; }
+    else o += ch;
+  }
+  o += '"';
+}
+
+int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args_len, ksg_preempt_result* res,
+                 char* detail, size_t detail_cap, size_t* detail_len) {
+  auto it = c->queue.find(handle);
+  if (it == c->queue.end()) return KSG_ENOTFOUND;
+  const Pod& pod = *it->second;
+  *res = ksg_preempt_result{};
+  res->status = KSG_CODE_UNSCHEDULABLE;
+  res->node_index = -1;
+  int64_t offsetIn = 0, now = 0;
+  int64_t pct = 10, absn = 100;
+  bool allNodes = false;
+  std::vector<OPdb> pdbs;
+  try {
+    mj::Value a = (args_json && args_len) ? mj::parse(args_json, args_len) : mj::Value{};
+    offsetIn = a.i64("offset", 0);
+    now = a.i64("now", 0);
+    pct = a.i64("minCandidateNodesPercentage", 10);
+    absn = a.i64("minCandidateNodesAbsolute", 100);
+    if (const mj::Value* b = a.has("allNodes")) allNodes = b->kind == mj::Value::Bool && b->b;
+    if (const mj::Value* ps = a.has("pdbs"))
+      for (auto& v : ps->arr) {
+        OPdb b;
+        if (const mj::Value* md = v.has("metadata")) b.ns = md->str("namespace", "default");
+        if (b.ns.empty()) b.ns = "default";
+        LabelSelectorSpec ls;
+        if (const mj::Value* sp = v.has("spec")) ls = decode_label_selector(sp->has("selector"));
+        // LabelSelectorAsSelector: an error, nil (Nothing) or empty (Empty()) selector matches nothing
+        b.ok = label_selector_as_selector(ls, &b.sel) && ls.present && !(ls.matchLabels.empty() && ls.matchExpressions.empty());
+        if (const mj::Value* st = v.has("status")) {
+          b.allowed = (int32_t)st->i64("disruptionsAllowed", 0);
+          if (const mj::Value* dp = st->has("disruptedPods"))
+            for (auto& kv : dp->obj) b.disrupted.insert(kv.first);
+        }
+        pdbs.push_back(std::move(b));
+      }
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+  if (pct < 0 || pct > 100 || absn < 0 || (pct == 0 && absn == 0)) { c->err = "bad DefaultPreemptionArgs"; return KSG_EINVAL; }
+  std::string msg, dj;
+  auto finish = [&]() {
+    if (detail_len) *detail_len = dj.size();
+    if (detail) {
+      if (dj.size() + 1 > detail_cap) return KSG_ENOMEM;
+      std::memcpy(detail, dj.c_str(), dj.size() + 1);
+    }
+    return KSG_OK;
+  };
+  // 1) PodEligibleToPreemptOthers (default_preemption.go:364-388)
+  if (pod.preemptionPolicy == "Never") {
+    res->reason = KSG_PREEMPT_NOT_ELIGIBLE;
+    dj = "{\"message\":\"not eligible due to preemptionPolicy=Never.\",\"candidates\":[]}";
+    return finish();
+  }
+  // the failed cycle's Diagnosis.NodeToStatus
+  c->rebuild_list();
+  const int N = (int)c->list.size();
+  std::vector<uint8_t> code(std::max(N, 1));
+  ksg_eval_out ev{};
+  ev.node_code = code.data();
+  ksg_result cr;
+  int rc = run_cycle(c, pod, &cr, &ev);
+  if (rc) return rc;
+  if (!pod.nominatedNodeName.empty()) {
+    NodeInfoO* nn = nullptr;
+    for (auto* ni : c->list)
+      if (ni->node.name == pod.nominatedNodeName) nn = ni;
+    if (nn && code[nn->pos] != KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE)
+      for (auto* pi : nn->pods)
+        if (pi->pod.priority < pod.priority && pi->pod.terminatingByPreemption) {
+          res->reason = KSG_PREEMPT_NOT_ELIGIBLE;
+          dj = "{\"message\":\"not eligible due to a terminating pod on the nominated node.\",\"candidates\":[]}";
+          return finish();
+        }
+  }
+  // 2) findCandidates (preemption.go:174-196): NodesForStatusCode(Unschedulable), snapshot order
+  std::vector<NodeInfoO*> pot;
+  for (auto* ni : c->list)
+    if (allNodes || code[ni->pos] == KSG_CODE_UNSCHEDULABLE) pot.push_back(ni);
+  const int64_t P = (int64_t)pot.size();
+  res->num_potential = (int32_t)P;
+  Cycle cy;
+  cy.c = c;
+  cy.pod = &pod;
+  cy.reqNA = get_required_node_affinity(pod);
+  std::vector<CritPaths> crit;
+  std::vector<std::pair<NodeInfoO*, OVictims>> nv, vl;
+  int64_t offset = 0, ncand = 0;
+  if (P > 0 && preempt_prefilter(c, cy)) {
+    for (auto& m : cy.tpMatch) {  // initial criticalPaths over the domains (map order)
+      CritPaths p;
+      for (auto& kv : m) crit_update(p, kv.first, kv.second);
+      crit.push_back(p);
+    }
+    offset = ((offsetIn % P) + P) % P;
+    ncand = P * pct / 100;  // calculateNumCandidates (default_preemption.go:219-228)
+    if (ncand < absn) ncand = absn;
+    if (ncand > P) ncand = P;
+    // DryRunPreemption (preemption.go:404-457), Parallelizer with parallelism 1
+    for (int64_t i = 0; i < P; ++i) {
+      NodeInfoO* ni = pot[(offset + i) % P];
+      OVictims v;
+      if (select_victims(c, cy, crit, pod, ni, pdbs, now, &v) != KSG_CODE_SUCCESS) continue;
+      auto& l = v.viol == 0 ? nv : vl;
+      if ((int64_t)l.size() < ncand) l.push_back({ni, v});  // candidateList.add drops past capacity
+      if (!nv.empty() && (int64_t)(nv.size() + vl.size()) >= ncand) break;
+    }
+  }
+  std::vector<std::pair<NodeInfoO*, OVictims>> cands = nv;
+  cands.insert(cands.end(), vl.begin(), vl.end());
+  res->num_candidates = (int32_t)cands.size();
+  // 4) SelectCandidate -> pickOneNodeForPreemption (preemption.go:262-397)
+  int best = -1;
+  if (cands.size() == 1) best = 0;
+  else if (!cands.empty()) {
+    auto startOf = [&](const PodInfo* p) { return p->pod.hasStartTime ? p->pod.startTimeNs : now; };
+    std::vector<std::function<int64_t(int)>> fs = {
+        [&](int k) { return -cands[k].second.viol; },
+        [&](int k) { return -(int64_t)cands[k].second.pods[0]->pod.priority; },
+        [&](int k) {
+          int64_t s = 0;
+          for (auto* p : cands[k].second.pods) s += (int64_t)p->pod.priority + (int64_t)INT32_MAX + 1;
+          return -s;
+        },
+        [&](int k) { return -(int64_t)cands[k].second.pods.size(); },
+        [&](int k) {  // util.GetEarliestPodStartTime
+          auto& ps = cands[k].second.pods;
+          int64_t t = startOf(ps[0]);
+          int32_t mp = ps[0]->pod.priority;
+          for (auto* p : ps) {
+            if (p->pod.priority == mp) { if (startOf(p) < t) t = startOf(p); }
+            else if (p->pod.priority > mp) { mp = p->pod.priority; t = startOf(p); }
+          }
+          return t;
+        }};
+    std::vector<int> all;
+    for (size_t k = 0; k < cands.size(); ++k) all.push_back((int)k);
+    for (auto& f : fs) {
+      std::vector<int> sel;
+      int64_t mx = INT64_MIN;
+      for (int k : all) {
+        int64_t s = f(k);
+        if (s > mx) { mx = s; sel.clear(); }
+        if (s == mx) sel.push_back(k);
+      }
+      all = sel;
+      if (all.size() == 1) break;
+    }
+    best = all[0];
+  }
+  if (best >= 0) {
+    res->status = KSG_CODE_SUCCESS;
+    res->reason = KSG_PREEMPT_OK;
+    res->node_index = cands[best].first->pos;
+    res->num_victims = (int32_t)cands[best].second.pods.size();
+    res->num_pdb_violations = cands[best].second.viol;
+  } else {
+    res->reason = KSG_PREEMPT_NO_CANDIDATES;
+    msg = "0/" + std::to_string(N) + " nodes are available: preemption is not helpful for scheduling.";
+  }
+  dj = "{\"offset\":" + std::to_string(offset) + ",\"numCandidates\":" + std::to_string(ncand) +
+       ",\"potential\":" + std::to_string(P) + ",\"message\":";
+  ojson_str(dj, msg);
+  dj += ",\"candidates\":[";
+  auto vlist = [&](const OVictims& v) {
+    std::string o = "[";
+    for (size_t q = 0; q < v.pods.size(); ++q) {
+      if (q) o += ",";
+      ojson_str(o, v.pods[q]->pod.uid);
+    }
+    return o + "]";
+  };
+  for (size_t k = 0; k < cands.size(); ++k) {
+    if (k) dj += ",";
+    dj += "{\"node\":";
+    ojson_str(dj, cands[k].first->node.name);
+    dj += ",\"numPDBViolations\":" + std::to_string(cands[k].second.viol) + ",\"victims\":" + vlist(cands[k].second) + "}";
+  }
+  dj += "],\"selected\":";
+  if (best >= 0) ojson_str(dj, cands[best].first->node.name);
+  else dj += "null";
+  dj += ",\"victims\":" + (best >= 0 ? vlist(cands[best].second) : std::string("[]")) + "}";
+  return finish();
+}
+
 double ksgo_go_log(double x) { return go_log(x); }
 
 int32_t ksgo_heap_root(const int64_t* scores, int32_t n) {

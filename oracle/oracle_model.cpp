@@ -2,6 +2,8 @@
 #include "oracle_model.hpp"
 
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
 #include <climits>
 
 namespace oracle {
@@ -251,7 +253,7 @@ static bool decode_reslist(const mj::Value* v, ResList* out, std::string* err) {
   }
   return true;
 }
-static LabelSelectorSpec decode_label_selector(const mj::Value* v) {
+LabelSelectorSpec decode_label_selector(const mj::Value* v) {
   LabelSelectorSpec ls;
   if (!v || v->is_null()) return ls;
   ls.present = true;
@@ -329,6 +331,42 @@ bool decode_namespace(const mj::Value& v, Namespace* out, std::string* err) {
   return true;
 }
 
+// metav1.Time text (RFC 3339 with an optional fraction) -> Unix nanoseconds
+static bool rfc3339_ns(const std::string& t, int64_t* out) {
+  int Y, M, D, h, m, s, n = 0;
+  if (std::sscanf(t.c_str(), "%4d-%2d-%2dT%2d:%2d:%2d%n", &Y, &M, &D, &h, &m, &s, &n) != 6 || n != 19) return false;
+  size_t i = 19;
+  int64_t frac = 0, scale = 1000000000;
+  if (i < t.size() && t[i] == '.') {
+    ++i;
+    size_t d0 = i;
+    while (i < t.size() && isdigit((unsigned char)t[i])) {
+      if (scale > 1) { scale /= 10; frac += (t[i] - '0') * scale; }
+      ++i;
+    }
+    if (i == d0) return false;
+  }
+  int64_t off = 0;
+  if (i < t.size() && t[i] == 'Z') ++i;
+  else if (i + 6 == t.size() && (t[i] == '+' || t[i] == '-')) {
+    int oh, om;
+    if (std::sscanf(t.c_str() + i + 1, "%2d:%2d", &oh, &om) != 2) return false;
+    off = (t[i] == '+' ? 1 : -1) * (oh * 3600 + om * 60);
+    i += 6;
+  } else return false;
+  if (i != t.size()) return false;
+  // days since 1970-01-01 (Howard Hinnant's civil-from-days inverse)
+  int64_t y = Y - (M <= 2 ? 1 : 0);
+  int64_t era = (y >= 0 ? y : y - 399) / 400;
+  int64_t yoe = y - era * 400;
+  int64_t mp = (M + 9) % 12;
+  int64_t doy = (153 * mp + 2) / 5 + D - 1;
+  int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  int64_t days = era * 146097 + doe - 719468;
+  *out = (days * 86400 + h * 3600 + m * 60 + s - off) * 1000000000LL + frac;
+  return true;
+}
+
 bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
   *out = Pod{};
   const mj::Value* md = v.has("metadata");
@@ -340,9 +378,26 @@ bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
   if (out->uid.empty()) out->uid = out->ns + "/" + out->name;
   out->labels = decode_labels(md->get("labels"));
   out->terminating = md->has("deletionTimestamp") != nullptr;
+  if (const mj::Value* st = v.has("status")) {
+    std::string t = st->str("startTime");
+    if (!t.empty()) {
+      if (!rfc3339_ns(t, &out->startTimeNs)) { *err = "bad startTime"; return false; }
+      out->hasStartTime = true;
+    }
+    out->nominatedNodeName = st->str("nominatedNodeName");
+    if (const mj::Value* cs = st->has("conditions"))
+      for (auto& c : cs->arr)
+        if (c.str("type") == "DisruptionTarget") {
+          out->terminatingByPreemption =
+              out->terminating && c.str("status") == "True" && c.str("reason") == "PreemptionByScheduler";
+          break;
+        }
+  }
   const mj::Value* sp = v.has("spec");
   if (!sp) return true;
   out->nodeName = sp->str("nodeName");
+  out->priority = (int32_t)sp->i64("priority", 0);
+  out->preemptionPolicy = sp->str("preemptionPolicy");
   if (auto ns = sp->has("nodeSelector")) { out->hasNodeSelector = true; out->nodeSelector = decode_labels(ns); }
   if (auto af = sp->has("affinity")) {
     if (auto na = af->has("nodeAffinity")) {

@@ -55,6 +55,7 @@ struct LabelSelectorSpec {
 };
 // metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:36-71)
 bool label_selector_as_selector(const LabelSelectorSpec& ls, Selector* out);
+LabelSelectorSpec decode_label_selector(const mj::Value* v);  // nullptr -> nil
 
 // ---- v1 objects ----------------------------------------------------------------------
 struct NSRequirement { std::string key, op; std::vector<std::string> values; };
@@ -119,6 +120,13 @@ struct Pod {
   ResList podRequests;  // spec.resources.requests (pod-level resources)
   std::vector<TopologySpreadConstraint> tsc;
   std::vector<std::string> imageVolumes;  // volumes[].image.reference
+  // DefaultPreemption
+  int32_t priority = 0;           // corev1helpers.PodPriority: spec.priority, 0 when nil
+  bool hasStartTime = false;      // status.startTime != nil
+  int64_t startTimeNs = 0;
+  std::string preemptionPolicy;   // spec.preemptionPolicy
+  std::string nominatedNodeName;  // status.nominatedNodeName
+  bool terminatingByPreemption = false;  // preemption.PodTerminatingByPreemption (preemption/util.go:23-35)
 };
 
 struct Namespace { std::string name; Labels labels; };

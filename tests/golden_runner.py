@@ -58,6 +58,10 @@ def run_case(make_backend, case):
         errs = run_sequence_case(b, case, names)
         b.close()
         return errs
+    if case["kind"] == "preempt":
+        errs = run_preempt_case(b, case, names)
+        b.close()
+        return errs
     h = b.compile(case["pod"])
     want_names = [n["metadata"]["name"] for n in case_nodes(case)]
     errs = []
@@ -136,6 +140,32 @@ def run_cycle_case(b, case, names):
             want = (code, PLUGIN_ID[plugin] if plugin else 255, reasons)
             if got != want:
                 errs.append(f"status[{n}] {got} != {want}")
+    return errs
+
+
+def run_preempt_case(b, case, names):
+    """DefaultPreemption PostFilter: the DryRunPreemption candidates (victims and NumPDBViolations, compared
+    as sets, as the reference test sorts them), the selected node, PodEligibleToPreemptOthers."""
+    from ksg.abi import KSG_ENOTSUP
+    errs = []
+    e = case["expect"]
+    try:
+        r, d = b.preempt(b.compile(case["pod"]), case.get("args") or {})
+    except KsgError as ex:
+        if case.get("device") == "ENOTSUP" and getattr(b, "prefix", "") == "ksg_" and f"rc={KSG_ENOTSUP}" in str(ex):
+            return []
+        return [f"preempt failed: {ex}"]
+    if case.get("device") == "ENOTSUP" and getattr(b, "prefix", "") == "ksg_":
+        errs.append("device path was expected to decline this case (KSG_ENOTSUP)")
+    if "candidates" in e:
+        got = {c["node"]: {"victims": sorted(c["victims"]), "numPDBViolations": c["numPDBViolations"]}
+               for c in d["candidates"]}
+        if got != e["candidates"]:
+            errs.append(f"candidates {got} != {e['candidates']}")
+    if "selected_in" in e and d.get("selected") not in e["selected_in"]:
+        errs.append(f"selected {d.get('selected')} not in {e['selected_in']}")
+    if "reason" in e and r.reason != e["reason"]:
+        errs.append(f"reason {r.reason} != {e['reason']}")
     return errs
 
 

@@ -1,0 +1,186 @@
+"""DefaultPreemption on the device (k_preempt through ksg_preempt) against the CPU oracle's restatement
+of default_preemption.go / preemption.go.
+
+Bar: the identical PostFilter outcome -- reason, nominated node, every DryRunPreemption candidate with
+its victims (in order) and NumPDBViolations, the selected node's victims -- over random clusters with
+mixed priorities, start times (some pods without one: the caller's clock), PodDisruptionBudgets, host
+ports, extended resources, pod counts, and every potential-node / offset / numCandidates regime.
+"""
+import random
+
+import pytest
+
+from oracle_binding import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from ksg.native import Scheduler
+    return Scheduler
+
+
+ZONES = ["z1", "z2", "z3"]
+
+
+def mk_node(i, rng):
+    alloc = {"cpu": f"{rng.choice([1000, 2000, 4000])}m", "memory": str(rng.choice([2, 4, 8]) * 1024 ** 3),
+             "pods": str(rng.choice([4, 6, 110]))}
+    if rng.random() < 0.3:
+        alloc["example.com/gpu"] = str(rng.choice([1, 2, 4]))
+    n = {"apiVersion": "v1", "kind": "Node",
+         "metadata": {"name": f"n{i:04d}", "labels": {"kubernetes.io/hostname": f"n{i:04d}",
+                                                      "topology.kubernetes.io/zone": rng.choice(ZONES)}},
+         "spec": {}, "status": {"allocatable": alloc, "capacity": alloc}}
+    if rng.random() < 0.1:
+        n["spec"]["taints"] = [{"key": "dedicated", "value": "x", "effect": "NoSchedule"}]
+    if rng.random() < 0.05:
+        n["spec"]["unschedulable"] = True
+    return n
+
+
+def mk_pod(name, rng, node=None, prio=None, big=False):
+    req = {"cpu": f"{rng.choice([100, 250, 500, 900]) * (3 if big else 1)}m",
+           "memory": str(rng.choice([128, 512, 1024]) * (3 if big else 1) * 1024 ** 2)}
+    if rng.random() < (0.3 if big else 0.15):
+        req["example.com/gpu"] = "1"
+    c = {"name": "c", "image": "img", "resources": {"requests": req}}
+    if rng.random() < 0.15:
+        c["ports"] = [{"containerPort": 80, "hostPort": rng.choice([8080, 8081]), "protocol": "TCP"}]
+    p = {"apiVersion": "v1", "kind": "Pod",
+         "metadata": {"name": name, "namespace": rng.choice(["default", "team"]), "uid": name,
+                      "labels": {"app": rng.choice(["a", "b", "c"])}},
+         "spec": {"containers": [c], "priority": prio if prio is not None else rng.choice([-100, 0, 0, 100, 500])},
+         "status": {}}
+    if rng.random() < 0.7:
+        p["status"]["startTime"] = f"2024-01-01T00:{rng.randrange(60):02d}:{rng.randrange(60):02d}Z"
+    if rng.random() < 0.1:
+        p["spec"]["tolerations"] = [{"key": "dedicated", "operator": "Exists", "effect": "NoSchedule"}]
+    if node:
+        p["spec"]["nodeName"] = node
+    return p
+
+
+def pdbs(rng):
+    out = []
+    for k in range(rng.randrange(0, 4)):
+        sel = rng.choice([{"matchLabels": {"app": rng.choice(["a", "b"])}},
+                          {"matchExpressions": [{"key": "app", "operator": "In", "values": ["a", "c"]}]},
+                          {}])
+        out.append({"metadata": {"namespace": rng.choice(["default", "team"])}, "spec": {"selector": sel},
+                    "status": {"disruptionsAllowed": rng.randrange(0, 3),
+                               "disruptedPods": {f"e{rng.randrange(40)}": "2024-01-01T00:00:00Z"}}})
+    return out
+
+
+def build(make, nodes, existing):
+    b = make({})
+    b.upsert_namespace({"metadata": {"name": "default"}})
+    b.upsert_namespace({"metadata": {"name": "team"}})
+    for n in nodes:
+        b.add_node(n)
+    for p in existing:
+        b.add_pod(p)
+    return b
+
+
+def cluster(seed, n_nodes, per_node):
+    rng = random.Random(seed)
+    nodes = [mk_node(i, rng) for i in range(n_nodes)]
+    existing = []
+    for i, n in enumerate(nodes):
+        for k in range(rng.randrange(per_node + 1)):
+            existing.append(mk_pod(f"e{i}-{k}", rng, node=n["metadata"]["name"]))
+    return rng, nodes, existing
+
+
+def compare(dev, orc, pod, args):
+    r1, d1 = dev.preempt(dev.compile(pod), args)
+    r2, d2 = orc.preempt(orc.compile(pod), args)
+    assert r1.as_tuple() == r2.as_tuple(), (r1.as_tuple(), r2.as_tuple(), d1, d2)
+    assert d1 == d2
+    return r1, d1
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_preempt_matches_oracle_random(native, seed):
+    rng, nodes, existing = cluster(seed, 60 + 40 * seed, 6)
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    found = 0
+    for q in range(12):
+        pod = mk_pod(f"pre{q}", rng, prio=rng.choice([100, 500, 1000]), big=True)
+        args = {"offset": rng.randrange(1000), "now": 1704067200 * 10 ** 9 + rng.randrange(3600) * 10 ** 9,
+                "pdbs": pdbs(rng), "allNodes": rng.random() < 0.3,
+                "minCandidateNodesPercentage": rng.choice([0, 10, 40, 100]),
+                "minCandidateNodesAbsolute": rng.choice([1, 3, 100])}
+        if args["minCandidateNodesPercentage"] == 0 and args["minCandidateNodesAbsolute"] == 0:
+            args["minCandidateNodesAbsolute"] = 1
+        r, _ = compare(dev, orc, pod, args)
+        found += r.status == 0
+    assert found > 0  # the streams do exercise a nomination
+
+
+def test_preempt_policy_never_and_terminating_victims(native):
+    rng, nodes, existing = cluster(11, 40, 5)
+    # a victim on the nominated node terminating by preemption blocks a new preemption
+    victim = mk_pod("vt", rng, node=nodes[0]["metadata"]["name"], prio=-100)
+    victim["metadata"]["deletionTimestamp"] = "2024-01-01T00:00:00Z"
+    victim["status"]["conditions"] = [{"type": "DisruptionTarget", "status": "True", "reason": "PreemptionByScheduler"}]
+    existing.append(victim)
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    pod = mk_pod("pre", rng, prio=1000, big=True)
+    pod["status"]["nominatedNodeName"] = nodes[0]["metadata"]["name"]
+    r, _ = compare(dev, orc, pod, {})
+    never = mk_pod("never", rng, prio=1000, big=True)
+    never["spec"]["preemptionPolicy"] = "Never"
+    r, _ = compare(dev, orc, never, {})
+    assert r.reason == 1
+
+
+def test_preempt_large_cluster(native):
+    """5000 nodes, ~40k bound pods, full nodes: the PreemptionBasic shape (scheduler_perf
+    misc/performance-config.yaml) at the C2 node count."""
+    rng = random.Random(5)
+    nodes = []
+    for i in range(5000):
+        alloc = {"cpu": "4000m", "memory": str(16 * 1024 ** 3), "pods": "110"}
+        nodes.append({"apiVersion": "v1", "kind": "Node",
+                      "metadata": {"name": f"n{i:05d}", "labels": {"topology.kubernetes.io/zone": ZONES[i % 3]}},
+                      "spec": {}, "status": {"allocatable": alloc, "capacity": alloc}})
+    existing = []
+    for i in range(5000):
+        for k in range(8):
+            existing.append({"apiVersion": "v1", "kind": "Pod",
+                             "metadata": {"name": f"low-{i}-{k}", "namespace": "default", "uid": f"low-{i}-{k}",
+                                          "labels": {"app": "low"}},
+                             "spec": {"nodeName": f"n{i:05d}", "priority": rng.choice([0, 10]),
+                                      "containers": [{"name": "c", "image": "i", "resources": {"requests": {
+                                          "cpu": "500m", "memory": str(2 * 1024 ** 3)}}}]},
+                             "status": {"startTime": f"2024-01-01T00:00:{rng.randrange(60):02d}Z"}})
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    for q in range(3):
+        pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"hi{q}", "namespace": "default", "uid": f"hi{q}"},
+               "spec": {"priority": 1000, "containers": [{"name": "c", "image": "i", "resources": {"requests": {
+                   "cpu": "1200m", "memory": str(3 * 1024 ** 3)}}}]}, "status": {}}
+        r, d = compare(dev, orc, pod, {"offset": 1234 + q, "pdbs": [
+            {"metadata": {"namespace": "default"}, "spec": {"selector": {"matchLabels": {"app": "low"}}},
+             "status": {"disruptionsAllowed": 2}}]})
+        assert r.status == 0 and r.num_potential == 5000 and r.num_candidates >= 100
+
+
+def test_preempt_declines_topology_victims(native):
+    """Victims that change the pod's PodTopologySpread counts are outside the device contract."""
+    rng, nodes, existing = cluster(3, 30, 6)
+    for p in existing:
+        p["metadata"]["labels"]["app"] = "a"
+        p["metadata"]["namespace"] = "default"
+    dev = build(native, nodes, existing)
+    pod = mk_pod("pre", rng, prio=1000, big=True)
+    pod["metadata"]["namespace"] = "default"
+    pod["spec"]["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone",
+                                                 "whenUnsatisfiable": "DoNotSchedule",
+                                                 "labelSelector": {"matchLabels": {"app": "a"}}}]
+    from ksg.abi import KsgError
+    with pytest.raises(KsgError, match="rc=-5"):
+        dev.preempt(dev.compile(pod), {})
