@@ -194,13 +194,14 @@ int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uin
  *    "now": <unix ns>,       GetPodStartTime's clock for pods without status.startTime (utils.go:52-58)
  *    "allNodes": false,      true: every snapshot node is a potential node (DryRunPreemption over
  *                            the node list, as the reference's unit tests call it)
+ *    "listCandidates": false, true: detail lists every candidate (else "candidates" is empty)
  *    "pdbs": [<policy/v1 PodDisruptionBudget JSON>, ...]}
  * Potential nodes are taken in snapshot order (the reference iterates a map there) and checked with
  * Parallelizer parallelism 1 semantics; victims of equal priority and start time keep NodeInfo.Pods
  * order; candidates tied on every criterion resolve to the earliest in candidate-list order.
  * Pods whose victims would change their PodTopologySpread or InterPodAffinity counts return
  * KSG_ENOTSUP.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
- * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}],
+ * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}] (listCandidates),
  * "selected": <node|null>, "victims": [uid...]}; *detail_len gets its length (KSG_ENOMEM if cap is
  * too small; the result is still filled). */
 #define KSG_PREEMPT_OK 0            /* a node was nominated */

@@ -259,6 +259,51 @@ struct POut {
   int32_t pad;
 };
 
+// The device-resident form (k_preempt_seg): every node's pods as an importance-ordered segment of
+// kSegCap records, kept up to date by the cache events (only the nodes whose pods changed are
+// re-sorted and re-uploaded).  The pods isPreemptionAllowed admits are then the segment's suffix with
+// priority below the preemptor's, and the PDB grouping runs on the device against the pod table's labels.
+constexpr int kSegCap = 128;  // records per node segment (a node with more pods takes the host-staged path)
+constexpr int kMaxPdb = 8;    // PodDisruptionBudgets the device groups by (more: host-staged path)
+enum PRFlags : uint32_t { PR_MANY_PORTS = 1u, PR_SCALAR = 2u };
+struct PRec {
+  int64_t cpu, mem, eph;  // PodInfo.CalculateResource
+  int64_t start;          // status.startTime (Unix ns), INT64_MAX without one (the call's clock)
+  int32_t prio, slot;     // corev1helpers.PodPriority; pod-table slot (namespace, labels)
+  uint32_t port[2];       // host port ids (0xffffffff: none)
+  uint32_t flags;         // PRFlags
+  int32_t pad;
+};
+struct PdbDev { int32_t ns, sel, allowed, ok; };  // namespace id, selector program offset, DisruptionsAllowed
+struct PSegOut {
+  uint32_t st;                  // as POut
+  int32_t nvictims, nviolating;
+  uint32_t flags;               // bit 0: a potential victim matches a DoNotSchedule spread selector (unsupported)
+  unsigned long long vmask[2];  // segment positions kept removed (victims)
+  unsigned long long violmask[2];  // segment positions in the PDB-violating group
+  // pickOneNodeForPreemption's criteria over the victims (preemption.go:322-357)
+  int32_t hiprio;               // priority of the most important victim
+  int32_t pad;
+  int64_t sumprio;              // sum of (priority + MaxInt32 + 1)
+  int64_t earliest;             // GetEarliestPodStartTime: earliest start among the highest-priority victims
+};
+// k_preempt_pick's answer: DryRunPreemption's cut and SelectCandidate over the per-node results
+struct PickOut {
+  int32_t potential, ncand, ncandidates, best;  // best: snapshot index, -1 if no candidate
+  int32_t offset, unsupported, pad[2];          // unsupported: some node's PSegOut flag bit 0
+  PSegOut best_out;                             // the chosen node's result (victim masks)
+};
+struct PreemptView {
+  const PRec* seg;           // [n][kSegCap]
+  const int32_t* cnt;        // [n] records in use
+  const PdbDev* pdb;         // [npdb]
+  const int32_t* pdb_pool;   // their selector programs
+  const uint8_t* disrupted;  // [slot] bit k: the pod is in PDB k's DisruptedPods (nullptr: none)
+  PSegOut* out;              // [n]
+  int32_t npdb, prio, all_nodes, pts_check;
+  int64_t now;               // GetPodStartTime for pods without a start time
+};
+
 // Per-pod device result (ScheduleResult + diagnostics), written by the select kernel.
 struct DevResult {
   int32_t status;     // KSG_CODE_*

@@ -3441,4 +3441,324 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
   return hipGetLastError();
 }
 
+
+// k_preempt_seg: k_preempt over the device-resident pod segments (PreemptView).  The filter re-runs and
+// the reprieve are k_preempt's; what the host staged per call there is derived here: the potential
+// victims (the segment suffix below the preemptor's priority), filterPodsWithPDBViolation
+// (default_preemption.go:406-452: selector programs against the pod table's labels, budgets in
+// registers), the victims' host-port conflicts and the node's remaining conflicting ports.
+__global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView b, int pod, PreemptView pv) {
+  const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+  if (i >= m.n) return;
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PSegOut o{};
+  o.st = PS_NOT_CHECKED;
+  const uint32_t st0 = b.status[i];
+  if (!pv.all_nodes && status_code(st0) != C_UNSCHED) {
+    pv.out[i] = o;
+    return;
+  }
+  const int cnt = pv.cnt[i];
+  const PRec* r = pv.seg + (size_t)i * kSegCap;
+  int first = cnt;
+  for (int q = 0; q < cnt; ++q)
+    if (r[q].prio < pv.prio) {
+      first = q;
+      break;
+    }
+  if (first == cnt) {  // "No preemption victims found for incoming pod"
+    o.st = PS_NO_VICTIMS;
+    pv.out[i] = o;
+    return;
+  }
+  const uint32_t p0 = status_plugin(st0);
+  if (st0 != 0 && (p0 == P_UNSCHED || p0 == P_NODENAME || p0 == P_TAINT || p0 == P_NA || p0 == 15u)) {
+    o.st = st0;
+    pv.out[i] = o;
+    return;
+  }
+  if (pv.pts_check) {  // a victim counted by a DoNotSchedule constraint would move the pod's spread counts
+    const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+    const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
+    for (int q = first; q < cnt; ++q) {
+      const int32_t slot = r[q].slot;
+      if (m.pod_ns[slot] != d.ns_id) continue;
+      const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+      const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+      for (int32_t c = 0; c < d.n_ptsf; ++c)
+        if (lsel_match(sp + cs[c].sel, lb, ln)) o.flags |= 1u;
+    }
+  }
+  // filterPodsWithPDBViolation over the importance-ordered potential victims
+  unsigned long long viol0 = 0ull, viol1 = 0ull;  // two words, no dynamically indexed array (scratch)
+  if (pv.npdb > 0) {
+    int32_t allowed[kMaxPdb];
+#pragma unroll
+    for (int k = 0; k < kMaxPdb; ++k) allowed[k] = k < pv.npdb ? pv.pdb[k].allowed : 0;
+    for (int q = first; q < cnt; ++q) {
+      const int32_t slot = r[q].slot;
+      const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+      if (ln == 0) continue;  // a pod with no labels matches no PDB
+      const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+      const int32_t ns = m.pod_ns[slot];
+      const uint32_t dis = pv.disrupted ? pv.disrupted[slot] : 0u;
+      bool v = false;
+#pragma unroll
+      for (int k = 0; k < kMaxPdb; ++k) {
+        if (k >= pv.npdb) break;
+        const PdbDev pb = pv.pdb[k];
+        if (!pb.ok || pb.ns != ns || !lsel_match(pv.pdb_pool + pb.sel, lb, ln) || ((dis >> k) & 1u)) continue;
+        if (--allowed[k] < 0) v = true;
+      }
+      if (v) (q < 64 ? viol0 : viol1) |= 1ull << (q & 63);
+    }
+  }
+  const bool ports_on = ((d.filter_mask >> P_PORTS) & 1u) != 0;
+  auto conf = [&](uint32_t pid) {
+    return ports_on && pid != 0xffffffffu && bit(base, d.port_conflict_off, pid, d.n_port_words);
+  };
+  bool port = false;  // a conflicting port no potential victim holds (NodeInfo.RemovePod drops shared ones too)
+  if (ports_on)
+    for (int s = 0; s < kPortSlots; ++s) {
+      const uint32_t pid = m.ports[(size_t)i * kPortSlots + s];
+      if (!conf(pid)) continue;
+      bool held = false;
+      for (int q = first; q < cnt; ++q) held |= r[q].port[0] == pid || r[q].port[1] == pid;
+      port |= !held;
+    }
+  NodeCore nc = load_core(m, i);
+  for (int q = first; q < cnt; ++q) {
+    nc.rcpu -= r[q].cpu;
+    nc.rmem -= r[q].mem;
+    nc.reph -= r[q].eph;
+  }
+  nc.npods -= cnt - first;
+  int64_t sreq[kPreemptScalar] = {0, 0, 0, 0};  // the host takes this path only for pods without scalar requests
+  uint32_t st = preempt_node_filters(m, nc, sreq, base, d, i, port);
+  if (st == 0) st = topo_filters(m, base, d, i, ArenaTopo{b.stats + pod, b.arena}, 0);
+  o.st = st;
+  unsigned long long vm0 = 0ull, vm1 = 0ull, vv0 = 0ull, vv1 = 0ull;
+  if (st == 0) {
+    for (int pass = 0; pass < 2; ++pass)  // the violating group first, then the others (:331-343)
+      for (int q = first; q < cnt; ++q) {
+        const bool isv = (((q < 64 ? viol0 : viol1) >> (q & 63)) & 1ull) != 0;
+        if (isv != (pass == 0)) continue;
+        const PRec x = r[q];
+        NodeCore t = nc;
+        t.rcpu += x.cpu;
+        t.rmem += x.mem;
+        t.reph += x.eph;
+        t.npods += 1;
+        const bool tp = port || conf(x.port[0]) || conf(x.port[1]);
+        if (preempt_node_filters(m, t, sreq, base, d, i, tp) == 0) {
+          nc = t;
+          port = tp;
+        } else {
+          (q < 64 ? vm0 : vm1) |= 1ull << (q & 63);
+          o.nvictims += 1;
+          if (isv) {
+            (q < 64 ? vv0 : vv1) |= 1ull << (q & 63);
+            o.nviolating += 1;
+          }
+        }
+      }
+  }
+  o.vmask[0] = vm0;
+  o.vmask[1] = vm1;
+  o.violmask[0] = vv0;
+  o.violmask[1] = vv1;
+  // the selection criteria: the victims' most important member leads either victim order (importance
+  // order, or reprieve order within one PDB group, both led by the segment's earliest victim)
+  o.hiprio = INT32_MIN;
+  o.sumprio = 0;
+  o.earliest = INT64_MAX;
+  for (int q = first; q < cnt; ++q) {
+    if (!((((q < 64 ? vm0 : vm1) >> (q & 63)) & 1ull))) continue;
+    const int64_t t = r[q].start == INT64_MAX ? pv.now : r[q].start;
+    if (o.hiprio == INT32_MIN || r[q].prio > o.hiprio) {
+      o.hiprio = r[q].prio;
+      o.earliest = t;
+    } else if (r[q].prio == o.hiprio && t < o.earliest) {
+      o.earliest = t;
+    }
+    o.sumprio += (int64_t)r[q].prio + 2147483648LL;
+  }
+  pv.out[i] = o;
+}
+
+// DryRunPreemption's candidate cut with sequential Parallelizer semantics (preemption.go:404-457) and
+// SelectCandidate / pickOneNodeForPreemption (:262-397) over k_preempt_seg's per-node results, in one
+// workgroup: the potential nodes (snapshot order) are ranked by a block scan, walked from the offset in
+// rotated order with running non-violating / violating candidate counts (each list capped at
+// numCandidates, candidateList.add), cut where a non-violating candidate is held and the two reach
+// numCandidates, and the candidates reduced by the five criteria (ties: earliest in candidate order,
+// non-violating list first).
+constexpr int kPickThreads = 1024;
+__device__ __forceinline__ int block_excl_scan(int v, int* tot, int* s_w) {  // kPickThreads, returns exclusive prefix
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int k = 0; k < kPickThreads / 64; ++k) {
+      const int t = s_w[k];
+      s_w[k] = acc;
+      acc += t;
+    }
+    s_w[kPickThreads / 64] = acc;
+  }
+  __syncthreads();
+  const int r = s_w[w] + x - v;
+  *tot = s_w[kPickThreads / 64];
+  __syncthreads();
+  return r;
+}
+struct PickKey {  // larger is better, lexicographic
+  int64_t a, b, c, d, e;
+  int32_t idx;  // candidate-order index (smaller wins a full tie)
+  int32_t node;
+};
+__device__ __forceinline__ bool pick_better(const PickKey& x, const PickKey& y) {
+  if (x.node < 0) return false;
+  if (y.node < 0) return true;
+  if (x.a != y.a) return x.a > y.a;
+  if (x.b != y.b) return x.b > y.b;
+  if (x.c != y.c) return x.c > y.c;
+  if (x.d != y.d) return x.d > y.d;
+  if (x.e != y.e) return x.e > y.e;
+  return x.idx < y.idx;
+}
+__global__ __launch_bounds__(kPickThreads) void k_preempt_pick(const PSegOut* out, int n, int64_t offset_in, int64_t pct,
+                                                               int64_t absn, int32_t* pot, PickOut* res) {
+  __shared__ int s_w[kPickThreads / 64 + 1];
+  __shared__ int s_cut, s_unsup;
+  __shared__ PickKey s_k[kPickThreads];
+  const int t = threadIdx.x;
+  if (t == 0) s_unsup = 0;
+  __syncthreads();
+  // potential ranks (snapshot order) -> pot[rank] = node
+  int P = 0;
+  for (int b0 = 0; b0 < n; b0 += kPickThreads) {
+    const int i = b0 + t;
+    const int f = (i < n && out[i].st != PS_NOT_CHECKED) ? 1 : 0;
+    if (i < n && (out[i].flags & 1u)) s_unsup = 1;
+    int tot;
+    const int r = block_excl_scan(f, &tot, s_w);
+    if (f) pot[P + r] = i;
+    P += tot;
+  }
+  __syncthreads();
+  if (P == 0) {
+    if (t == 0) {
+      res->potential = res->ncand = res->ncandidates = 0;
+      res->best = -1;
+      res->offset = 0;
+      res->unsupported = s_unsup;
+    }
+    return;
+  }
+  const int offset = (int)(((offset_in % P) + P) % P);
+  int64_t nc = (int64_t)P * pct / 100;
+  if (nc < absn) nc = absn;
+  if (nc > P) nc = P;
+  const int ncand = (int)nc;
+  // the cut: first rotated position j whose candidate brings (min(NV, nc) >= 1, min(NV, nc) + min(VV, nc) >= nc)
+  auto cls = [&](int j) {  // 1: non-violating candidate, 2: violating candidate, 0: neither
+    const PSegOut& o = out[pot[(offset + j) % P]];
+    if (o.st != 0 || o.nvictims == 0) return 0;
+    return o.nviolating == 0 ? 1 : 2;
+  };
+  if (t == 0) s_cut = INT32_MAX;
+  __syncthreads();
+  int NV = 0, VV = 0;
+  for (int b0 = 0; b0 < P; b0 += kPickThreads) {
+    const int j = b0 + t;
+    const int c = j < P ? cls(j) : 0;
+    int tn, tv;
+    const int en = block_excl_scan(c == 1 ? 1 : 0, &tn, s_w);
+    const int ev = block_excl_scan(c == 2 ? 1 : 0, &tv, s_w);
+    int64_t nvc = (int64_t)(NV + en + (c == 1 ? 1 : 0)), vvc = (int64_t)(VV + ev + (c == 2 ? 1 : 0));
+    nvc = nvc < nc ? nvc : nc;
+    vvc = vvc < nc ? vvc : nc;
+    if (c != 0 && nvc >= 1 && nvc + vvc >= nc) atomicMin(&s_cut, j);
+    __syncthreads();
+    NV += tn;
+    VV += tv;
+    if (s_cut != INT32_MAX) break;  // uniform: every lane reads the shared value after the barrier
+  }
+  __syncthreads();
+  const int cut = s_cut == INT32_MAX ? P - 1 : s_cut;
+  // candidates over [0, cut]; the non-violating list's size decides the violating candidates' order
+  NV = 0;
+  VV = 0;
+  int nvtot = 0;
+  for (int b0 = 0; b0 <= cut; b0 += kPickThreads) {
+    const int j = b0 + t;
+    const int c = j <= cut ? cls(j) : 0;
+    int tn, tv;
+    block_excl_scan(c == 1 ? 1 : 0, &tn, s_w);
+    block_excl_scan(c == 2 ? 1 : 0, &tv, s_w);
+    NV += tn;
+    VV += tv;
+  }
+  nvtot = NV < ncand ? NV : ncand;
+  const int vvtot = VV < ncand ? VV : ncand;
+  PickKey best{0, 0, 0, 0, 0, 0, -1};
+  NV = 0;
+  VV = 0;
+  for (int b0 = 0; b0 <= cut; b0 += kPickThreads) {
+    const int j = b0 + t;
+    const int c = j <= cut ? cls(j) : 0;
+    int tn, tv;
+    const int en = block_excl_scan(c == 1 ? 1 : 0, &tn, s_w);
+    const int ev = block_excl_scan(c == 2 ? 1 : 0, &tv, s_w);
+    int idx = -1;
+    if (c == 1 && NV + en < ncand) idx = NV + en;
+    if (c == 2 && VV + ev < ncand) idx = nvtot + VV + ev;
+    if (idx >= 0) {
+      const int node = pot[(offset + j) % P];
+      const PSegOut& o = out[node];
+      PickKey k{-(int64_t)o.nviolating, -(int64_t)o.hiprio, -o.sumprio, -(int64_t)o.nvictims, o.earliest, idx, node};
+      if (pick_better(k, best)) best = k;
+    }
+    NV += tn;
+    VV += tv;
+  }
+  s_k[t] = best;
+  __syncthreads();
+  for (int w = kPickThreads / 2; w > 0; w >>= 1) {
+    if (t < w && pick_better(s_k[t + w], s_k[t])) s_k[t] = s_k[t + w];
+    __syncthreads();
+  }
+  if (t == 0) {
+    res->potential = P;
+    res->ncand = ncand;
+    res->ncandidates = nvtot + vvtot;
+    res->best = s_k[0].node;
+    res->offset = offset;
+    res->unsupported = s_unsup;
+    if (s_k[0].node >= 0) res->best_out = out[s_k[0].node];
+  }
+}
+
+hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_t pct, int64_t absn, int32_t* pot,
+                               PickOut* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_preempt_pick, dim3(1), dim3(kPickThreads), 0, s, out, n, offset, pct, absn, pot, res);
+  return hipGetLastError();
+}
+
+hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s) {
+  const int nb = (m.n + kBlock - 1) / kBlock;
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_preempt_seg, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pv);
+  return hipGetLastError();
+}
+
 }  // namespace ksg

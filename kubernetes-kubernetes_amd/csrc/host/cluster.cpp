@@ -376,6 +376,10 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   bp.start_ns = p.start_ns;
   bp.preempt_terminating = p.preempt_terminating;
   bp.req_anti = !p.anti_req.empty();
+  req_anti_pods += bp.req_anti ? 1 : 0;
+  if (p.has_start) max_start_ns = std::max(max_start_ns, p.start_ns);
+  else ++nostart_pods;
+  mark_pre_dirty(*r);
   pods_with_affinity += bp.with_affinity ? 1 : 0;
   auto take = [&](const Container& c) {
     for (auto& hp : c.ports)
@@ -402,6 +406,9 @@ int Cluster::remove_pod(const std::string& uid) {
   if (it == pods.end()) { err = "unknown pod " + uid; return KSG_ENOTFOUND; }
   NodeRec* r = node(it->second.node);
   pods_with_affinity -= it->second.with_affinity ? 1 : 0;
+  req_anti_pods -= it->second.req_anti ? 1 : 0;
+  nostart_pods -= it->second.has_start ? 0 : 1;
+  if (r) mark_pre_dirty(*r);
   pod_table_drop(it->second.slot);
   int32_t ix = -1;
   if (r) {

@@ -227,6 +227,7 @@ struct NodeRec {
   // false: a ghost NodeInfo (cache.go:442-446, 672-689) -- pods arrived before their node, or the
   // node was removed while pods remained; it holds their requests but is skipped by snapshots
   bool real = true;
+  bool pre_dirty = true;  // k_preempt_seg: the node's pod segment must be rebuilt (Engine::preempt)
   // the shadow changed since the device columns were last written (a re-layout by gather keeps a
   // node's device columns only if it is not stale, Cluster::relayout_gather)
   bool stale = true;
@@ -263,6 +264,19 @@ class Cluster {
               const std::string* node_override = nullptr, const PodResources* res = nullptr);
   int remove_pod(const std::string& uid);
   int32_t pods_with_affinity = 0;
+  // DefaultPreemption's device-resident pod segments (Engine::preempt): nodes whose pods changed since
+  // the segments were last built, and what decides whether the cached importance order still holds
+  std::vector<std::string> pre_dirty_nodes;
+  int64_t req_anti_pods = 0;              // pods with required anti-affinity terms
+  int64_t nostart_pods = 0;               // pods without status.startTime (GetPodStartTime's clock)
+  int64_t max_start_ns = INT64_MIN;       // latest startTime ever seen (never lowered)
+  uint64_t layout_epoch() const { return laid_epoch_; }
+  void mark_pre_dirty(NodeRec& r) {
+    if (!r.pre_dirty) {
+      r.pre_dirty = true;
+      pre_dirty_nodes.push_back(r.spec.name);
+    }
+  }
 
   // UpdateSnapshot (cache.go:190-296): the snapshot's nodeInfoList order, rebuilt from
   // nodeTree.list only when a node new to the snapshot appears or one is gone; called at the start
@@ -461,6 +475,16 @@ class Engine {
   DevBuf d_agran, d_region;  // k_agg_loop: exchange granules (own tag sequence), per-pod shared regions
   DevBuf d_astamps;          // k_agg_loop diagnostic stamps
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
+  // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)
+  DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick;
+  std::vector<PRec> h_seg;
+  std::vector<int32_t> h_segcnt;
+  std::vector<std::vector<const BoundPod*>> seg_pods;
+  uint64_t seg_epoch = ~0ull;
+  std::vector<uint8_t> seg_flags;  // per node: bit 0 more than kSegCap pods, bit 1 a pod with > 2 host ports
+  int32_t seg_n = -1, seg_overflow = 0, seg_many_ports = 0;
+  void seg_build(int32_t i, NodeRec& r);
+  int seg_refresh();
   uint32_t agran_tag = 0;
   int gran_setup();
   int next_gran_tag(uint32_t* tag);

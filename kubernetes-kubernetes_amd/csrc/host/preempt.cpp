@@ -28,6 +28,9 @@ hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod,
                                hipEvent_t t1, int blk0, int nblk, bool lds);
 hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, const PNode* pn, const PVictim* pv,
                           uint8_t* vout, POut* out, int all_nodes, hipStream_t s);
+hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s);
+hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_t pct, int64_t absn, int32_t* pot,
+                               PickOut* res, hipStream_t s);
 
 #define PCHK(x)                                                         \
   do {                                                                  \
@@ -120,7 +123,7 @@ LabelSel decode_lsel(const JDoc& d, const JVal* v) {
 }
 
 struct Victim {
-  std::string uid;
+  const std::string* uid;
   const BoundPod* bp;
   int64_t start;
   bool viol = false;
@@ -151,6 +154,90 @@ void json_str(std::string& o, const std::string& s) {
 
 }  // namespace
 
+// One node's importance-ordered segment (k_preempt_seg).  The order is util.MoreImportantPod's with the
+// pods that have no status.startTime last among their priority: GetPodStartTime gives them the call's
+// clock, later than every start time the cache holds when now > Cluster::max_start_ns (the condition
+// Engine::preempt checks before using the segments).  Equal keys keep NodeInfo.Pods order.
+void Engine::seg_build(int32_t i, NodeRec& r) {
+  auto& v = seg_pods[i];
+  v.clear();
+  for (const std::string& uid : r.pods) v.push_back(&c->pods.at(uid));
+  std::stable_sort(v.begin(), v.end(), [](const BoundPod* a, const BoundPod* b) {
+    if (a->priority != b->priority) return a->priority > b->priority;
+    const int64_t ta = a->has_start ? a->start_ns : INT64_MAX, tb = b->has_start ? b->start_ns : INT64_MAX;
+    return ta < tb;
+  });
+  const int32_t n = (int32_t)std::min<size_t>(v.size(), (size_t)kSegCap);
+  uint8_t fl = v.size() > (size_t)kSegCap ? 1u : 0u;
+  PRec* out = h_seg.data() + (size_t)i * kSegCap;
+  for (int32_t q = 0; q < n; ++q) {
+    const BoundPod& bp = *v[q];
+    PRec x{};
+    x.cpu = bp.res.cpu;
+    x.mem = bp.res.mem;
+    x.eph = bp.res.eph;
+    x.start = bp.has_start ? bp.start_ns : INT64_MAX;
+    x.prio = bp.priority;
+    x.slot = bp.slot;
+    x.port[0] = x.port[1] = 0xffffffffu;
+    for (size_t k = 0; k < bp.port_ids.size() && k < 2; ++k) x.port[k] = bp.port_ids[k];
+    if (bp.port_ids.size() > 2) {
+      x.flags |= PR_MANY_PORTS;
+      fl |= 2u;
+    }
+    if (!bp.res.scalar.empty()) x.flags |= PR_SCALAR;
+    out[q] = x;
+  }
+  h_segcnt[i] = n;
+  seg_overflow += (fl & 1u) - (seg_flags[i] & 1u);
+  seg_many_ports += ((fl >> 1) & 1u) - ((seg_flags[i] >> 1) & 1u);
+  seg_flags[i] = fl;
+  r.pre_dirty = false;
+}
+
+// Brings the device segments up to the cache: every node after a re-layout (node order changed),
+// otherwise only the nodes whose pods changed since the last call (Cluster::pre_dirty_nodes).
+int Engine::seg_refresh() {
+  const std::vector<std::string>& order = c->order();
+  const int32_t N = (int32_t)order.size();
+  hipStream_t s = c->stream;
+  int rc;
+  if (seg_epoch != c->layout_epoch() || seg_n != N) {
+    h_seg.assign((size_t)N * kSegCap, PRec{});
+    h_segcnt.assign((size_t)N, 0);
+    seg_pods.assign((size_t)N, {});
+    seg_flags.assign((size_t)N, 0);
+    seg_overflow = seg_many_ports = 0;
+    for (int32_t i = 0; i < N; ++i) seg_build(i, *c->node(order[i]));
+    if ((rc = ensure(d_seg, sizeof(PRec) * (size_t)std::max(N, 1) * kSegCap))) return rc;
+    if ((rc = ensure(d_segcnt, 4 * (size_t)std::max(N, 1)))) return rc;
+    PCHK(hipMemcpyAsync(d_seg.p, h_seg.data(), sizeof(PRec) * h_seg.size(), hipMemcpyHostToDevice, s));
+    PCHK(hipMemcpyAsync(d_segcnt.p, h_segcnt.data(), 4 * h_segcnt.size(), hipMemcpyHostToDevice, s));
+    PCHK(hipStreamSynchronize(s));  // pageable sources
+    seg_epoch = c->layout_epoch();
+    seg_n = N;
+    c->pre_dirty_nodes.clear();
+    return KSG_OK;
+  }
+  bool any = false;
+  for (const std::string& name : c->pre_dirty_nodes) {
+    NodeRec* r = c->node(name);
+    if (!r || !r->real || !r->pre_dirty) continue;
+    const int32_t i = c->index_of(name);
+    if (i < 0) continue;
+    seg_build(i, *r);
+    PRec* dseg = (PRec*)d_seg.p + (size_t)i * kSegCap;
+    if (h_segcnt[i])
+      PCHK(hipMemcpyAsync(dseg, h_seg.data() + (size_t)i * kSegCap, sizeof(PRec) * (size_t)h_segcnt[i],
+                          hipMemcpyHostToDevice, s));
+    PCHK(hipMemcpyAsync((int32_t*)d_segcnt.p + i, &h_segcnt[i], 4, hipMemcpyHostToDevice, s));
+    any = true;
+  }
+  c->pre_dirty_nodes.clear();
+  if (any) PCHK(hipStreamSynchronize(s));  // pageable sources
+  return KSG_OK;
+}
+
 int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ksg_preempt_result* res,
                     std::string* detail) {
   *res = ksg_preempt_result{};
@@ -159,7 +246,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   // ---- DefaultPreemptionArgs + the call's inputs (validation_pluginargs.go:113-125)
   int64_t offset_in = 0, now = 0;
   int32_t pct = 10, absn = 100;
-  bool all_nodes = false;
+  bool all_nodes = false, staged = false, list = false;
   std::vector<Pdb> pdbs;
   try {
     JDoc d(args_json && args_len ? args_json : "{}", args_json && args_len ? args_len : 2);
@@ -169,6 +256,8 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     pct = (int32_t)d.num(r, "minCandidateNodesPercentage", 10);
     absn = (int32_t)d.num(r, "minCandidateNodesAbsolute", 100);
     all_nodes = d.boolean(r, "allNodes");
+    staged = d.boolean(r, "debugHostStaged");
+    list = d.boolean(r, "listCandidates");  // detail lists every DryRunPreemption candidate  // diagnostic: force the host-staged victim records
     d.each(d.get(r, "pdbs"), [&](const JVal& v) {
       Pdb b;
       if (const JVal* md = d.get(v, "metadata")) b.ns = d.str(*md, "namespace", "default");
@@ -208,105 +297,39 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     return KSG_ENOTSUP;
   }
 
-  // ---- the potential victims of every node, in reprieve order
-  std::vector<PNode> pn((size_t)std::max(N, 1));
-  std::vector<PVictim> pv;
-  std::vector<Victim> all;  // parallel to pv
-  const uint32_t* conflict = reinterpret_cast<const uint32_t*>(cp.blob.data() + D.port_conflict_off);
-  auto conflicts = [&](uint32_t pid) {
-    return (D.filter_mask >> P_PORTS & 1u) && (int32_t)(pid >> 5) < D.n_port_words &&
-           ((conflict[pid >> 5] >> (pid & 31u)) & 1u);
-  };
-  const int32_t pns = c->ns_id(p.ns);
-  std::vector<std::pair<std::string, int32_t>> scal;  // the preemptor's scalar resources in PodDesc order
-  {
-    const ScalarReq* sr = reinterpret_cast<const ScalarReq*>(cp.blob.data() + D.scalar_off);
-    for (int k = 0; k < D.n_scalar; ++k) scal.push_back({c->scalar_ix.strs[sr[k].slot], sr[k].slot});
-  }
   const bool pts_on = (D.filter_mask >> P_PTS & 1u) && D.n_ptsf > 0;
   const bool ipa_req = !p.aff_req.empty() || !p.anti_req.empty();
-  std::vector<Victim> vs;
-  for (int32_t i = 0; i < N; ++i) {
-    NodeRec* r = c->node(order[i]);
-    PNode& nd = pn[i];
-    nd = PNode{(int32_t)pv.size(), 0, 0u, 0};
-    vs.clear();
-    for (const std::string& uid : r->pods) {  // isPreemptionAllowed (:396-399): lower priority
-      const BoundPod& bp = c->pods.at(uid);
-      if (bp.priority < p.priority) vs.push_back(Victim{uid, &bp, bp.has_start ? bp.start_ns : now, false});
-    }
-    if (vs.empty()) continue;
-    // PodTopologySpread / InterPodAffinity counts a victim could change (their RemovePod/AddPod
-    // extensions) are outside what k_preempt re-evaluates: refuse rather than approximate
-    for (const Victim& v : vs) {
-      if (pts_on && c->pt_ns[v.bp->slot] == pns)
-        for (auto& sp : p.spreads)
-          if (sp.when == "DoNotSchedule" && sp.sel.present && lsel_match_slot(*c, sp.sel, v.bp->slot)) {
-            c->err = "preemption: a victim changes the pod's PodTopologySpread counts (not supported on the device)";
-            return KSG_ENOTSUP;
-          }
-      if (ipa_req || v.bp->req_anti) {
-        c->err = "preemption: InterPodAffinity terms between the pod and a victim (not supported on the device)";
-        return KSG_ENOTSUP;
-      }
-    }
-    std::stable_sort(vs.begin(), vs.end(), more_important);  // sort.Slice (:309-311), see header
-    // filterPodsWithPDBViolation (:406-452) over the sorted list
-    std::vector<int32_t> allowed(pdbs.size());
-    for (size_t k = 0; k < pdbs.size(); ++k) allowed[k] = pdbs[k].allowed;
-    const std::string* vns = nullptr;
-    for (Victim& v : vs) {
-      if (c->pt_lbl_cnt[v.bp->slot] == 0) continue;  // a pod with no labels matches no PDB
-      for (size_t k = 0; k < pdbs.size(); ++k) {
-        const Pdb& b = pdbs[k];
-        vns = &c->ns_ix.strs[c->pt_ns[v.bp->slot]];
-        if (b.ns != *vns || !b.sel_ok || !lsel_match_slot(*c, b.sel, v.bp->slot)) continue;
-        if (b.disrupted.count(v.bp->name)) continue;
-        if (--allowed[k] < 0) v.viol = true;
-      }
-    }
-    std::stable_partition(vs.begin(), vs.end(), [](const Victim& v) { return v.viol; });
-    std::set<uint32_t> vports;
-    for (const Victim& v : vs) {
-      PVictim x{};
-      x.cpu = v.bp->res.cpu;
-      x.mem = v.bp->res.mem;
-      x.eph = v.bp->res.eph;
-      for (size_t k = 0; k < scal.size(); ++k)
-        for (auto& sv : v.bp->res.scalar)
-          if (sv.first == scal[k].first) x.sc[k] += sv.second;
-      for (uint32_t pid : v.bp->port_ids) {
-        vports.insert(pid);
-        if (conflicts(pid)) x.flags |= PV_PORT;
-      }
-      if (v.viol) x.flags |= PV_VIOL;
-      pv.push_back(x);
-      all.push_back(v);
-    }
-    nd.vcnt = (int32_t)vs.size();
-    // NodeInfo.RemovePod drops a victim's ports from the node's set even if another pod holds them too
-    for (uint32_t pid : r->ports)
-      if (!vports.count(pid) && conflicts(pid)) nd.flags |= PN_BASE_PORT;
-  }
-  const int32_t V = (int32_t)pv.size();
-
-  // ---- device: the cycle's statuses, then SelectVictimsOnNode per node
-  std::vector<POut> po((size_t)std::max(N, 1));
-  std::vector<uint8_t> vo((size_t)std::max(V, 1));
-  uint32_t nom_status = 0;
+  const bool ports_on = (D.filter_mask >> P_PORTS) & 1u;
   int32_t nom_ix = p.nominated_node.empty() ? -1 : c->index_of(p.nominated_node);
-  if (N > 0) {
-    if ((rc = c->ensure_mirror())) return rc;
+  if (N > 0 && (rc = c->ensure_mirror())) return rc;
+  // The device-resident segments serve every pod whose victims' order the cache already knows (no pod
+  // sorted by the call's clock, see seg_build) and that the device groups itself: no scalar requests,
+  // no required InterPodAffinity terms on either side, at most kMaxPdb budgets.  The rest take the
+  // host-staged records (same kernel core).
+  bool seg = N > 0 && !staged && D.n_scalar == 0 && !ipa_req && c->req_anti_pods == 0 && pdbs.size() <= (size_t)kMaxPdb &&
+             (c->nostart_pods == 0 || now > c->max_start_ns);
+  if (seg && (rc = seg_refresh())) return rc;
+  seg = seg && seg_overflow == 0 && (!ports_on || seg_many_ports == 0);
+
+  struct NodeOut { uint32_t st; int32_t nvictims, nviolating; };
+  std::vector<NodeOut> po((size_t)std::max(N, 1));
+  uint32_t nom_status = 0;
+  // staged path: the potential victims of every node, in reprieve order
+  std::vector<PNode> pn;
+  std::vector<PVictim> pv;
+  std::vector<Victim> all;  // parallel to pv
+  std::vector<uint8_t> vo;
+  // segment path: per-node victim masks (listCandidates), the device's cut and pick
+  std::vector<PSegOut> so;
+  PickOut pick{};
+
+  uint8_t* hp = (uint8_t*)h_pinned;
+  hipStream_t s = c->stream;
+  const MirrorView& m = c->view;
+  BatchView bv{};
+  auto stage_pod = [&]() -> int {  // the preemptor's program + stats, then the cycle's statuses
     if ((rc = ensure_scratch(cp.blob.size(), 1, true, cp.arena_words))) return rc;
-    const size_t pn_b = sizeof(PNode) * (size_t)N, pv_b = sizeof(PVictim) * (size_t)std::max(V, 1);
-    const size_t po_b = sizeof(POut) * (size_t)N, vo_b = (size_t)std::max(V, 1);
-    if ((rc = ensure(d_pre, pn_b + pv_b + po_b + vo_b + 64))) return rc;
-    uint8_t* dp = (uint8_t*)d_pre.p;
-    PNode* d_pn = (PNode*)dp;
-    PVictim* d_pv = (PVictim*)(dp + pn_b);
-    POut* d_po = (POut*)(dp + pn_b + pv_b);
-    uint8_t* d_vo = dp + pn_b + pv_b + po_b;
-    uint8_t* hp = (uint8_t*)h_pinned;
+    hp = (uint8_t*)h_pinned;
     std::memcpy(hp, cp.blob.data(), cp.blob.size());
     uint32_t off0 = 0;
     PodStats* hs = (PodStats*)(hp + ((cp.blob.size() + 15) & ~size_t(15)));
@@ -315,23 +338,170 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       hs->max_raw[q] = enc_i64(INT64_MIN);
       hs->min_raw[q] = enc_i64(INT64_MAX);
     }
-    hipStream_t s = c->stream;
-    const MirrorView& m = c->view;
     PCHK(hipMemcpyAsync(d_descs.p, hp, cp.blob.size(), hipMemcpyHostToDevice, s));
     PCHK(hipMemcpyAsync(d_off.p, &off0, 4, hipMemcpyHostToDevice, s));
     PCHK(hipMemcpyAsync(d_stats.p, hs, sizeof(PodStats), hipMemcpyHostToDevice, s));
-    PCHK(hipMemcpyAsync(d_pn, pn.data(), pn_b, hipMemcpyHostToDevice, s));
-    if (V) PCHK(hipMemcpyAsync(d_pv, pv.data(), pv_b, hipMemcpyHostToDevice, s));
-    const BatchView bv = bview(1);
+    bv = bview(1);
     if (D.flags & DF_AGGREGATE) PCHK(launch_aggregate(m, bv, 0, D, s));
-    const bool lds = cp.blob.size() <= (size_t)kBlobLds;
-    PCHK(launch_filter_score(m, bv, 0, s, nullptr, nullptr, 0, -1, lds));
-    PCHK(launch_preempt(m, bv, 0, d_pn, d_pv, d_vo, d_po, all_nodes ? 1 : 0, s));
+    PCHK(launch_filter_score(m, bv, 0, s, nullptr, nullptr, 0, -1, cp.blob.size() <= (size_t)kBlobLds));
+    return KSG_OK;
+  };
+  auto finish_device = [&]() -> int {
     if (D.arena_words) PCHK(hipMemsetAsync(d_arena.p, 0, (size_t)D.arena_words * 8, s));  // k_select did not run
-    PCHK(hipMemcpyAsync(po.data(), d_po, po_b, hipMemcpyDeviceToHost, s));
-    if (V) PCHK(hipMemcpyAsync(vo.data(), d_vo, vo_b, hipMemcpyDeviceToHost, s));
     if (nom_ix >= 0) PCHK(hipMemcpyAsync(&nom_status, bv.status + nom_ix, 4, hipMemcpyDeviceToHost, s));
     PCHK(hipStreamSynchronize(s));
+    return KSG_OK;
+  };
+
+  if (seg) {
+    // ---- PodDisruptionBudgets as selector programs over the pod table's labels
+    std::vector<int32_t> pool;
+    std::vector<PdbDev> pd(pdbs.size());
+    bool any_dis = false;
+    for (size_t k = 0; k < pdbs.size(); ++k) {
+      int32_t off = 0;
+      const bool ok = pdbs[k].sel_ok && c->compile_lsel(pdbs[k].sel, nullptr, &pool, &off);
+      pd[k] = PdbDev{c->ns_id(pdbs[k].ns), off, pdbs[k].allowed, ok ? 1 : 0};
+      any_dis |= !pdbs[k].disrupted.empty();
+    }
+    std::vector<uint8_t> dis;
+    if (any_dis) {  // DisruptedPods names -> pod-table slots (rare: a budget mid-eviction)
+      dis.assign(c->pt_node.size(), 0);
+      for (auto& kv : c->pods)
+        for (size_t k = 0; k < pdbs.size(); ++k)
+          if (pdbs[k].disrupted.count(kv.second.name)) dis[kv.second.slot] |= (uint8_t)(1u << k);
+    }
+    if ((rc = stage_pod())) return rc;
+    const size_t pd_b = sizeof(PdbDev) * pd.size(), pool_b = 4 * pool.size(), dis_b = dis.size();
+    if ((rc = ensure(d_pdb, pd_b + pool_b + dis_b + 64))) return rc;
+    if ((rc = ensure(d_psout, sizeof(PSegOut) * (size_t)N))) return rc;
+    uint8_t* dp = (uint8_t*)d_pdb.p;
+    if (pd_b) PCHK(hipMemcpyAsync(dp, pd.data(), pd_b, hipMemcpyHostToDevice, s));
+    if (pool_b) PCHK(hipMemcpyAsync(dp + pd_b, pool.data(), pool_b, hipMemcpyHostToDevice, s));
+    if (dis_b) PCHK(hipMemcpyAsync(dp + pd_b + pool_b, dis.data(), dis_b, hipMemcpyHostToDevice, s));
+    PreemptView v{};
+    v.seg = (const PRec*)d_seg.p;
+    v.cnt = (const int32_t*)d_segcnt.p;
+    v.pdb = (const PdbDev*)dp;
+    v.pdb_pool = (const int32_t*)(dp + pd_b);
+    v.disrupted = dis_b ? dp + pd_b + pool_b : nullptr;
+    v.out = (PSegOut*)d_psout.p;
+    v.npdb = (int32_t)pd.size();
+    v.prio = p.priority;
+    v.all_nodes = all_nodes ? 1 : 0;
+    v.pts_check = pts_on ? 1 : 0;
+    v.now = now;
+    PCHK(launch_preempt_seg(m, bv, 0, v, s));
+    if ((rc = ensure(d_pick, sizeof(PickOut) + 4 * (size_t)N + 64))) return rc;
+    PickOut* d_po = (PickOut*)d_pick.p;
+    PCHK(launch_preempt_pick((const PSegOut*)d_psout.p, N, offset_in, pct, absn, (int32_t*)(d_po + 1), d_po, s));
+    PCHK(hipMemcpyAsync(&pick, d_po, sizeof(PickOut), hipMemcpyDeviceToHost, s));
+    if (list) {  // the whole per-node result, for the candidate listing (and a host check of the pick)
+      so.resize((size_t)N);
+      PCHK(hipMemcpyAsync(so.data(), d_psout.p, sizeof(PSegOut) * (size_t)N, hipMemcpyDeviceToHost, s));
+    }
+    if ((rc = finish_device())) return rc;
+    if (pick.unsupported) {
+      c->err = "preemption: a victim changes the pod's PodTopologySpread counts (not supported on the device)";
+      return KSG_ENOTSUP;
+    }
+    for (int32_t i = 0; list && i < N; ++i) po[i] = NodeOut{so[i].st, so[i].nvictims, so[i].nviolating};
+  } else {
+    // ---- host-staged records: the potential victims of every node, in reprieve order
+    pn.assign((size_t)std::max(N, 1), PNode{});
+    const uint32_t* conflict = reinterpret_cast<const uint32_t*>(cp.blob.data() + D.port_conflict_off);
+    auto conflicts = [&](uint32_t pid) {
+      return ports_on && (int32_t)(pid >> 5) < D.n_port_words && ((conflict[pid >> 5] >> (pid & 31u)) & 1u);
+    };
+    const int32_t pns = c->ns_id(p.ns);
+    std::vector<std::string> scal;  // the preemptor's scalar resources in PodDesc order
+    {
+      const ScalarReq* sr = reinterpret_cast<const ScalarReq*>(cp.blob.data() + D.scalar_off);
+      for (int k = 0; k < D.n_scalar; ++k) scal.push_back(c->scalar_ix.strs[sr[k].slot]);
+    }
+    std::vector<Victim> vs;
+    for (int32_t i = 0; i < N; ++i) {
+      NodeRec* r = c->node(order[i]);
+      PNode& nd = pn[i];
+      nd = PNode{(int32_t)pv.size(), 0, 0u, 0};
+      vs.clear();
+      for (const std::string& uid : r->pods) {  // isPreemptionAllowed (:396-399): lower priority
+        const BoundPod& bp = c->pods.at(uid);
+        if (bp.priority < p.priority) vs.push_back(Victim{&uid, &bp, bp.has_start ? bp.start_ns : now, false});
+      }
+      if (vs.empty()) continue;
+      // PodTopologySpread / InterPodAffinity counts a victim could change (their RemovePod/AddPod
+      // extensions) are outside what k_preempt re-evaluates: refuse rather than approximate
+      for (const Victim& v : vs) {
+        if (pts_on && c->pt_ns[v.bp->slot] == pns)
+          for (auto& sp : p.spreads)
+            if (sp.when == "DoNotSchedule" && sp.sel.present && lsel_match_slot(*c, sp.sel, v.bp->slot)) {
+              c->err = "preemption: a victim changes the pod's PodTopologySpread counts (not supported on the device)";
+              return KSG_ENOTSUP;
+            }
+        if (ipa_req || v.bp->req_anti) {
+          c->err = "preemption: InterPodAffinity terms between the pod and a victim (not supported on the device)";
+          return KSG_ENOTSUP;
+        }
+      }
+      std::stable_sort(vs.begin(), vs.end(), more_important);  // sort.Slice (:309-311), see header
+      // filterPodsWithPDBViolation (:406-452) over the sorted list
+      std::vector<int32_t> allowed(pdbs.size());
+      for (size_t k = 0; k < pdbs.size(); ++k) allowed[k] = pdbs[k].allowed;
+      for (Victim& v : vs) {
+        if (c->pt_lbl_cnt[v.bp->slot] == 0) continue;  // a pod with no labels matches no PDB
+        const std::string& vns = c->ns_ix.strs[c->pt_ns[v.bp->slot]];
+        for (size_t k = 0; k < pdbs.size(); ++k) {
+          const Pdb& b = pdbs[k];
+          if (b.ns != vns || !b.sel_ok || !lsel_match_slot(*c, b.sel, v.bp->slot)) continue;
+          if (b.disrupted.count(v.bp->name)) continue;
+          if (--allowed[k] < 0) v.viol = true;
+        }
+      }
+      std::stable_partition(vs.begin(), vs.end(), [](const Victim& v) { return v.viol; });
+      std::set<uint32_t> vports;
+      for (const Victim& v : vs) {
+        PVictim x{};
+        x.cpu = v.bp->res.cpu;
+        x.mem = v.bp->res.mem;
+        x.eph = v.bp->res.eph;
+        for (size_t k = 0; k < scal.size(); ++k)
+          for (auto& sv : v.bp->res.scalar)
+            if (sv.first == scal[k]) x.sc[k] += sv.second;
+        for (uint32_t pid : v.bp->port_ids) {
+          vports.insert(pid);
+          if (conflicts(pid)) x.flags |= PV_PORT;
+        }
+        if (v.viol) x.flags |= PV_VIOL;
+        pv.push_back(x);
+        all.push_back(v);
+      }
+      nd.vcnt = (int32_t)vs.size();
+      // NodeInfo.RemovePod drops a victim's ports from the node's set even if another pod holds them too
+      for (uint32_t pid : r->ports)
+        if (!vports.count(pid) && conflicts(pid)) nd.flags |= PN_BASE_PORT;
+    }
+    const int32_t V = (int32_t)pv.size();
+    std::vector<POut> pout((size_t)std::max(N, 1));
+    vo.assign((size_t)std::max(V, 1), 0);
+    if (N > 0) {
+      if ((rc = stage_pod())) return rc;
+      const size_t pn_b = sizeof(PNode) * (size_t)N, pv_b = sizeof(PVictim) * (size_t)std::max(V, 1);
+      const size_t po_b = sizeof(POut) * (size_t)N, vo_b = (size_t)std::max(V, 1);
+      if ((rc = ensure(d_pre, pn_b + pv_b + po_b + vo_b + 64))) return rc;
+      uint8_t* dp = (uint8_t*)d_pre.p;
+      PNode* d_pn = (PNode*)dp;
+      PVictim* d_pv = (PVictim*)(dp + pn_b);
+      POut* d_po = (POut*)(dp + pn_b + pv_b);
+      uint8_t* d_vo = dp + pn_b + pv_b + po_b;
+      PCHK(hipMemcpyAsync(d_pn, pn.data(), pn_b, hipMemcpyHostToDevice, s));
+      if (V) PCHK(hipMemcpyAsync(d_pv, pv.data(), pv_b, hipMemcpyHostToDevice, s));
+      PCHK(launch_preempt(m, bv, 0, d_pn, d_pv, d_vo, d_po, all_nodes ? 1 : 0, s));
+      PCHK(hipMemcpyAsync(pout.data(), d_po, po_b, hipMemcpyDeviceToHost, s));
+      if (V) PCHK(hipMemcpyAsync(vo.data(), d_vo, vo_b, hipMemcpyDeviceToHost, s));
+      if ((rc = finish_device())) return rc;
+    }
+    for (int32_t i = 0; i < N; ++i) po[i] = NodeOut{pout[i].st, pout[i].nvictims, pout[i].nviolating};
   }
   // ---- 1) PodEligibleToPreemptOthers, the nominated-node half (:369-386)
   if (nom_ix >= 0 && status_code(nom_status) != KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE) {
@@ -347,15 +517,17 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     }
   }
   // ---- 2) findCandidates: potential nodes in snapshot order, offset, numCandidates (:215-238)
+  // (the segment path's k_preempt_pick did this on the device; with listCandidates the host redoes it
+  // over the whole per-node result and checks that both agree)
+  const bool host_cut = !seg || list;
   std::vector<int32_t> pot;
-  for (int32_t i = 0; i < N; ++i)
+  for (int32_t i = 0; host_cut && i < N; ++i)
     if (po[i].st != PS_NOT_CHECKED) pot.push_back(i);
-  const int32_t P = (int32_t)pot.size();
-  res->num_potential = P;
+  int32_t P = (int32_t)pot.size();
   struct Cand { int32_t node; int64_t viol; };
   std::vector<Cand> nv, vl;
   int32_t offset = 0, ncand = 0;
-  if (P > 0) {
+  if (host_cut && P > 0) {
     offset = (int32_t)(((offset_in % P) + P) % P);
     int64_t n = (int64_t)P * pct / 100;
     if (n < absn) n = absn;
@@ -373,27 +545,37 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   }
   std::vector<Cand> cands = nv;
   cands.insert(cands.end(), vl.begin(), vl.end());
-  res->num_candidates = (int32_t)cands.size();
-  // each candidate's victims, importance order (sorted again when both groups contributed, :345-348)
+  int32_t ncandidates = (int32_t)cands.size();
+  // each candidate's victims, importance order (reprieve order, sorted again when both PDB groups
+  // contributed, :345-348)
   auto victims_of = [&](int32_t i) {
-    std::vector<const Victim*> out;
-    const PNode& nd = pn[i];
+    std::vector<Victim> out;
     bool g0 = false, g1 = false;
-    for (int32_t q = 0; q < nd.vcnt; ++q)
-      if (vo[nd.voff + q]) {
-        out.push_back(&all[nd.voff + q]);
-        (all[nd.voff + q].viol ? g0 : g1) = true;
-      }
-    if (g0 && g1)
-      std::stable_sort(out.begin(), out.end(), [](const Victim* a, const Victim* b) { return more_important(*a, *b); });
+    if (seg) {
+      const PSegOut& o = list ? so[i] : pick.best_out;
+      const auto& sp = seg_pods[i];
+      for (int pass = 0; pass < 2; ++pass)
+        for (int q = 0; q < h_segcnt[i]; ++q) {
+          const bool vic = (o.vmask[q >> 6] >> (q & 63)) & 1ull, isv = (o.violmask[q >> 6] >> (q & 63)) & 1ull;
+          if (!vic || isv != (pass == 0)) continue;
+          out.push_back(Victim{&sp[q]->uid, sp[q], sp[q]->has_start ? sp[q]->start_ns : now, isv});
+        }
+    } else {
+      const PNode& nd = pn[i];
+      for (int32_t q = 0; q < nd.vcnt; ++q)
+        if (vo[nd.voff + q]) out.push_back(all[nd.voff + q]);
+    }
+    for (const Victim& v : out) (v.viol ? g0 : g1) = true;
+    if (g0 && g1) std::stable_sort(out.begin(), out.end(), more_important);
     return out;
   };
   // ---- 4) SelectCandidate / pickOneNodeForPreemption (:262-397)
-  int32_t best = -1;
-  if (cands.size() == 1) {
+  int32_t best = -1;  // index into cands
+  if (!host_cut) {
+  } else if (cands.size() == 1) {
     best = 0;
   } else if (!cands.empty()) {
-    std::vector<std::vector<const Victim*>> cv;
+    std::vector<std::vector<Victim>> cv;
     for (auto& cd : cands) cv.push_back(victims_of(cd.node));
     std::vector<int32_t> sel(cands.size());
     for (size_t k = 0; k < cands.size(); ++k) sel[k] = (int32_t)k;
@@ -401,22 +583,22 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       const auto& v = cv[k];
       switch (f) {
         case 0: return -cands[k].viol;                      // minNumPDBViolating
-        case 1: return -(int64_t)v[0]->bp->priority;        // minHighestPriority
+        case 1: return -(int64_t)v[0].bp->priority;         // minHighestPriority
         case 2: {                                           // minSumPriorities
           int64_t sum = 0;
-          for (auto* x : v) sum += (int64_t)x->bp->priority + (int64_t)2147483648LL;
+          for (auto& x : v) sum += (int64_t)x.bp->priority + (int64_t)2147483648LL;
           return -sum;
         }
         case 3: return -(int64_t)v.size();                  // minNumPods
         default: {                                          // latestStartTime: GetEarliestPodStartTime
-          int64_t t = v[0]->start;
-          int32_t mp = v[0]->bp->priority;
-          for (auto* x : v) {
-            if (x->bp->priority == mp) {
-              if (x->start < t) t = x->start;
-            } else if (x->bp->priority > mp) {
-              mp = x->bp->priority;
-              t = x->start;
+          int64_t t = v[0].start;
+          int32_t mp = v[0].bp->priority;
+          for (auto& x : v) {
+            if (x.bp->priority == mp) {
+              if (x.start < t) t = x.start;
+            } else if (x.bp->priority > mp) {
+              mp = x.bp->priority;
+              t = x.start;
             }
           }
           return t;
@@ -438,14 +620,30 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     }
     best = sel[0];
   }
+  int32_t best_node = best >= 0 ? cands[best].node : -1;
+  int64_t best_viol = best >= 0 ? cands[best].viol : 0;
+  if (seg) {
+    if (host_cut && (pick.best != best_node || pick.potential != P || pick.ncandidates != ncandidates)) {
+      c->err = "preemption: the device's candidate pick differs from the host's";
+      return KSG_EDEVICE;
+    }
+    P = pick.potential;
+    offset = pick.offset;
+    ncand = pick.ncand;
+    ncandidates = pick.ncandidates;
+    best_node = pick.best;
+    if (best_node >= 0) best_viol = pick.best_out.nviolating;
+  }
+  res->num_potential = P;
+  res->num_candidates = ncandidates;
   std::string msg;
-  if (best >= 0) {
-    const int32_t i = cands[best].node;
+  if (best_node >= 0) {
+    const int32_t i = best_node;
     res->status = KSG_CODE_SUCCESS;
     res->reason = KSG_PREEMPT_OK;
     res->node_index = i;
-    res->num_victims = po[i].nvictims;
-    res->num_pdb_violations = cands[best].viol;
+    res->num_victims = (seg && !list) ? pick.best_out.nvictims : po[i].nvictims;
+    res->num_pdb_violations = best_viol;
   } else {
     res->reason = KSG_PREEMPT_NO_CANDIDATES;
     msg = "0/" + std::to_string(N) + " nodes are available: preemption is not helpful for scheduling.";
@@ -456,7 +654,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
         ",\"potential\":" + std::to_string(P) + ",\"message\":";
     json_str(o, msg);
     o += ",\"candidates\":[";
-    for (size_t k = 0; k < cands.size(); ++k) {
+    for (size_t k = 0; list && k < cands.size(); ++k) {
       if (k) o += ",";
       o += "{\"node\":";
       json_str(o, order[cands[k].node]);
@@ -464,19 +662,19 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       auto v = victims_of(cands[k].node);
       for (size_t q = 0; q < v.size(); ++q) {
         if (q) o += ",";
-        json_str(o, v[q]->uid);
+        json_str(o, *v[q].uid);
       }
       o += "]}";
     }
     o += "],\"selected\":";
-    if (best >= 0) json_str(o, order[cands[best].node]);
+    if (best_node >= 0) json_str(o, order[best_node]);
     else o += "null";
     o += ",\"victims\":[";
-    if (best >= 0) {
-      auto v = victims_of(cands[best].node);
+    if (best_node >= 0) {
+      auto v = victims_of(best_node);
       for (size_t q = 0; q < v.size(); ++q) {
         if (q) o += ",";
-        json_str(o, v[q]->uid);
+        json_str(o, *v[q].uid);
       }
     }
     o += "]}";

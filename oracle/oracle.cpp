@@ -1965,7 +1965,7 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
   res->node_index = -1;
   int64_t offsetIn = 0, now = 0;
   int64_t pct = 10, absn = 100;
-  bool allNodes = false;
+  bool allNodes = false, list = false;
   std::vector<OPdb> pdbs;
   try {
     mj::Value a = (args_json && args_len) ? mj::parse(args_json, args_len) : mj::Value{};
@@ -1974,6 +1974,7 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
     pct = a.i64("minCandidateNodesPercentage", 10);
     absn = a.i64("minCandidateNodesAbsolute", 100);
     if (const mj::Value* b = a.has("allNodes")) allNodes = b->kind == mj::Value::Bool && b->b;
+    if (const mj::Value* b = a.has("listCandidates")) list = b->kind == mj::Value::Bool && b->b;
     if (const mj::Value* ps = a.has("pdbs"))
       for (auto& v : ps->arr) {
         OPdb b;
@@ -2125,7 +2126,7 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
     }
     return o + "]";
   };
-  for (size_t k = 0; k < cands.size(); ++k) {
+  for (size_t k = 0; list && k < cands.size(); ++k) {
     if (k) dj += ",";
     dj += "{\"node\":";
     ojson_str(dj, cands[k].first->node.name);

@@ -150,7 +150,7 @@ def run_preempt_case(b, case, names):
     errs = []
     e = case["expect"]
     try:
-        r, d = b.preempt(b.compile(case["pod"]), case.get("args") or {})
+        r, d = b.preempt(b.compile(case["pod"]), dict(case.get("args") or {}, listCandidates=True))
     except KsgError as ex:
         if case.get("device") == "ENOTSUP" and getattr(b, "prefix", "") == "ksg_" and f"rc={KSG_ENOTSUP}" in str(ex):
             return []

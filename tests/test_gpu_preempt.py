@@ -96,10 +96,14 @@ def cluster(seed, n_nodes, per_node):
 
 
 def compare(dev, orc, pod, args):
-    r1, d1 = dev.preempt(dev.compile(pod), args)
+    """Both device paths (the device-resident pod segments, and host-staged records via the
+    debugHostStaged diagnostic) against the oracle."""
+    args = dict(args, listCandidates=True)
     r2, d2 = orc.preempt(orc.compile(pod), args)
-    assert r1.as_tuple() == r2.as_tuple(), (r1.as_tuple(), r2.as_tuple(), d1, d2)
-    assert d1 == d2
+    for extra in ({}, {"debugHostStaged": True}):
+        r1, d1 = dev.preempt(dev.compile(pod), dict(args, **extra))
+        assert r1.as_tuple() == r2.as_tuple(), (extra, r1.as_tuple(), r2.as_tuple(), d1, d2)
+        assert d1 == d2, extra
     return r1, d1
 
 
@@ -116,8 +120,15 @@ def test_preempt_matches_oracle_random(native, seed):
                 "minCandidateNodesAbsolute": rng.choice([1, 3, 100])}
         if args["minCandidateNodesPercentage"] == 0 and args["minCandidateNodesAbsolute"] == 0:
             args["minCandidateNodesAbsolute"] = 1
-        r, _ = compare(dev, orc, pod, args)
+        r, d = compare(dev, orc, pod, args)
         found += r.status == 0
+        if r.status == 0 and q % 3 == 0:  # actuate: the victims go, the pod binds; the next query sees it
+            for uid in d["victims"]:
+                dev.remove_pod(uid)
+                orc.remove_pod(uid)
+            p2 = dict(pod, spec=dict(pod["spec"], nodeName=d["selected"]))
+            dev.add_pod(p2)
+            orc.add_pod(p2)
     assert found > 0  # the streams do exercise a nomination
 
 
