@@ -302,7 +302,10 @@ struct PreemptView {
   PSegOut* out;              // [n]
   int32_t npdb, prio, all_nodes, pts_check;
   int64_t now;               // GetPodStartTime for pods without a start time
+  const long long* pts_mm;   // [kPreemptCons][3]: per DoNotSchedule constraint the domain minimum, its
+                             // multiplicity and the next larger count (k_pts_minima)
 };
+constexpr int kPreemptCons = 4;  // DoNotSchedule constraints whose counts the victims may move (more: unsupported)
 
 // Per-pod device result (ScheduleResult + diagnostics), written by the select kernel.
 struct DevResult {

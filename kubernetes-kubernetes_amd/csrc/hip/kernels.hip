@@ -3442,6 +3442,96 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
 }
 
 
+// The cycle's PodTopologySpread counts as the preemption dry run sees them at node i: the preFilterState
+// clone with the victims' RemovePod / AddPod applied (podtopologyspread/filtering.go:157-212).  Every
+// victim is on node i, so only the count of node i's own domain moves; the domain minimum becomes the
+// smaller of that count and the minimum over the other domains -- what criticalPaths.update tracks
+// exactly for a sequence of updates to one domain.  InterPodAffinity counts pass through unchanged.
+struct PreemptTopo {
+  ArenaTopo a;
+  int64_t hb[kPreemptCons];    // constraint c's histogram base, -1 unused
+  int64_t vi[kPreemptCons];    // node i's domain value under constraint c
+  int64_t cnt0[kPreemptCons];  // its cycle count
+  int64_t dlt[kPreemptCons];   // + reprieved - removed victims that constraint c counts
+  int64_t excl[kPreemptCons];  // minimum over the other domains
+  __device__ __forceinline__ int64_t cnt(int32_t hist_base, int32_t lref, int32_t v, int ls) const {
+    int64_t x = a.cnt(hist_base, lref, v, ls);
+#pragma unroll
+    for (int c = 0; c < kPreemptCons; ++c)
+      if (hb[c] == hist_base && vi[c] == v) x += dlt[c];
+    return x;
+  }
+  __device__ __forceinline__ int64_t pmin(int c) const {
+    int64_t r = a.pmin(c);
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k)
+      if (k == c && hb[k] >= 0) {
+        const int64_t own = cnt0[k] + dlt[k];
+        r = own < excl[k] ? own : excl[k];
+      }
+    return r;
+  }
+  __device__ __forceinline__ uint32_t pndom(int c) const { return a.pndom(c); }
+  __device__ __forceinline__ uint32_t any() const { return a.any(); }
+};
+
+// Per DoNotSchedule constraint (one workgroup each): the minimum count over the present domains, how many
+// domains hold it, and the next larger count -- the minimum over "every domain but one holding the
+// minimum", which PreemptTopo needs for the node whose own domain is that one.
+__global__ __launch_bounds__(kBlock) void k_pts_minima(BatchView b, int pod, long long* mm) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  const int c = blockIdx.x;
+  if (c >= d.n_ptsf) return;
+  const PtsCons cs = at<PtsCons>(base, d.ptsf_off)[c];
+  const long long INF = 0x7fffffffffffffffll;
+  long long mn = INF, nx = INF, cnt = 0;
+  for (int v = threadIdx.x; v < cs.nvals; v += kBlock) {
+    if (!b.arena[cs.pres_base + v]) continue;
+    const long long x = (long long)b.arena[cs.hist_base + v];
+    if (x < mn) {
+      nx = mn;
+      mn = x;
+      cnt = 1;
+    } else if (x == mn) {
+      ++cnt;
+    } else if (x < nx) {
+      nx = x;
+    }
+  }
+  __shared__ long long s[3][kBlock];
+  s[0][threadIdx.x] = mn;
+  s[1][threadIdx.x] = cnt;
+  s[2][threadIdx.x] = nx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long m0 = INF, c0 = 0, n0 = INF;
+    for (int t = 0; t < kBlock; ++t) {
+      const long long m1 = s[0][t], c1 = s[1][t], n1 = s[2][t];
+      if (c1 == 0) continue;
+      if (m1 < m0) {
+        n0 = m0 < n1 ? m0 : n1;
+        m0 = m1;
+        c0 = c1;
+      } else if (m1 == m0) {
+        c0 += c1;
+        n0 = n0 < n1 ? n0 : n1;
+      } else {
+        n0 = n0 < m1 ? n0 : m1;
+      }
+    }
+    mm[3 * c] = m0;
+    mm[3 * c + 1] = c0;
+    mm[3 * c + 2] = n0;
+  }
+}
+
+hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* mm, hipStream_t s) {
+  if (ncons <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pts_minima, dim3(ncons), dim3(kBlock), 0, s, b, pod, mm);
+  return hipGetLastError();
+}
+
 // k_preempt_seg: k_preempt over the device-resident pod segments (PreemptView).  The filter re-runs and
 // the reprieve are k_preempt's; what the host staged per call there is derived here: the potential
 // victims (the segment suffix below the preemptor's priority), filterPodsWithPDBViolation
@@ -3478,18 +3568,52 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
     pv.out[i] = o;
     return;
   }
-  if (pv.pts_check) {  // a victim counted by a DoNotSchedule constraint would move the pod's spread counts
-    const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
-    const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
-    for (int q = first; q < cnt; ++q) {
-      const int32_t slot = r[q].slot;
-      if (m.pod_ns[slot] != d.ns_id) continue;
-      const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
-      const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
-      for (int32_t c = 0; c < d.n_ptsf; ++c)
-        if (lsel_match(sp + cs[c].sel, lb, ln)) o.flags |= 1u;
+  // PodTopologySpread counts the victims move (updateWithPod, podtopologyspread/filtering.go:181-212):
+  // constraint c counts a victim in the preemptor's namespace that matches c's selector, at a node that
+  // carries every constraint key and passes c's node-inclusion policies (pts_eligible)
+  PreemptTopo tp;
+  tp.a = ArenaTopo{b.stats + pod, b.arena};
+#pragma unroll
+  for (int c = 0; c < kPreemptCons; ++c) tp.hb[c] = tp.vi[c] = -1, tp.cnt0[c] = tp.dlt[c] = tp.excl[c] = 0;
+  const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+  const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
+  uint32_t elig = 0;
+  if (pv.pts_check) {
+    if (d.n_ptsf > kPreemptCons) {  // more constraints than PreemptTopo tracks: unsupported if any victim counts
+      for (int q = first; q < cnt; ++q) {
+        const int32_t slot = r[q].slot;
+        if (m.pod_ns[slot] != d.ns_id) continue;
+        const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+        const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+        for (int32_t c = 0; c < d.n_ptsf; ++c)
+          if (lsel_match(sp + cs[c].sel, lb, ln)) o.flags |= 1u;
+      }
+    } else {
+      elig = pts_eligible(m, base, d, cs, d.n_ptsf, i);
+#pragma unroll
+      for (int c = 0; c < kPreemptCons; ++c)
+        if (c < d.n_ptsf && ((elig >> c) & 1u)) {
+          const int32_t v = node_label(m, cs[c].slot, i);
+          tp.hb[c] = cs[c].hist_base;
+          tp.vi[c] = v;
+          tp.cnt0[c] = (int64_t)b.arena[cs[c].hist_base + v];
+          const long long* mm = pv.pts_mm + 3 * c;
+          tp.excl[c] = (tp.cnt0[c] == mm[0] && mm[1] == 1) ? mm[2] : mm[0];
+        }
     }
   }
+  auto counts = [&](int q) -> uint32_t {  // the constraints whose count victim q is part of
+    if (!elig) return 0u;
+    const int32_t slot = r[q].slot;
+    if (m.pod_ns[slot] != d.ns_id) return 0u;
+    const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+    const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+    uint32_t bits = 0;
+#pragma unroll
+    for (int c = 0; c < kPreemptCons; ++c)
+      if (((elig >> c) & 1u) && lsel_match(sp + cs[c].sel, lb, ln)) bits |= 1u << c;
+    return bits;
+  };
   // filterPodsWithPDBViolation over the importance-ordered potential victims
   unsigned long long viol0 = 0ull, viol1 = 0ull;  // two words, no dynamically indexed array (scratch)
   if (pv.npdb > 0) {
@@ -3528,15 +3652,20 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
       port |= !held;
     }
   NodeCore nc = load_core(m, i);
+  bool moves = false;  // some victim moves a spread count: the topology filters re-run on every reprieve
   for (int q = first; q < cnt; ++q) {
     nc.rcpu -= r[q].cpu;
     nc.rmem -= r[q].mem;
     nc.reph -= r[q].eph;
+    const uint32_t k = counts(q);
+#pragma unroll
+    for (int c = 0; c < kPreemptCons; ++c) tp.dlt[c] -= (k >> c) & 1u;
+    moves |= k != 0;
   }
   nc.npods -= cnt - first;
   int64_t sreq[kPreemptScalar] = {0, 0, 0, 0};  // the host takes this path only for pods without scalar requests
   uint32_t st = preempt_node_filters(m, nc, sreq, base, d, i, port);
-  if (st == 0) st = topo_filters(m, base, d, i, ArenaTopo{b.stats + pod, b.arena}, 0);
+  if (st == 0) st = topo_filters(m, base, d, i, tp, 0);
   o.st = st;
   unsigned long long vm0 = 0ull, vm1 = 0ull, vv0 = 0ull, vv1 = 0ull;
   if (st == 0) {
@@ -3550,10 +3679,17 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
         t.rmem += x.mem;
         t.reph += x.eph;
         t.npods += 1;
-        const bool tp = port || conf(x.port[0]) || conf(x.port[1]);
-        if (preempt_node_filters(m, t, sreq, base, d, i, tp) == 0) {
+        const bool tpo = port || conf(x.port[0]) || conf(x.port[1]);
+        const uint32_t k = moves ? counts(q) : 0u;
+        PreemptTopo tt = tp;
+#pragma unroll
+        for (int c = 0; c < kPreemptCons; ++c) tt.dlt[c] += (k >> c) & 1u;
+        bool fits = preempt_node_filters(m, t, sreq, base, d, i, tpo) == 0;
+        if (fits && k) fits = topo_filters(m, base, d, i, tt, 0) == 0;
+        if (fits) {
           nc = t;
-          port = tp;
+          port = tpo;
+          tp = tt;
         } else {
           (q < 64 ? vm0 : vm1) |= 1ull << (q & 63);
           o.nvictims += 1;

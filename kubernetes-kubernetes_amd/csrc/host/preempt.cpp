@@ -29,6 +29,7 @@ hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod,
 hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, const PNode* pn, const PVictim* pv,
                           uint8_t* vout, POut* out, int all_nodes, hipStream_t s);
 hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s);
+hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* mm, hipStream_t s);
 hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_t pct, int64_t absn, int32_t* pot,
                                PickOut* res, hipStream_t s);
 
@@ -372,10 +373,14 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
           if (pdbs[k].disrupted.count(kv.second.name)) dis[kv.second.slot] |= (uint8_t)(1u << k);
     }
     if ((rc = stage_pod())) return rc;
+    const size_t mm_b = 8 * 3 * kPreemptCons;
     const size_t pd_b = sizeof(PdbDev) * pd.size(), pool_b = 4 * pool.size(), dis_b = dis.size();
-    if ((rc = ensure(d_pdb, pd_b + pool_b + dis_b + 64))) return rc;
+    if ((rc = ensure(d_pdb, mm_b + pd_b + pool_b + dis_b + 64))) return rc;
+    long long* d_mm = (long long*)d_pdb.p;  // k_pts_minima's output, then the budgets
+    const bool pts_minima = pts_on && D.n_ptsf <= kPreemptCons;
+    if (pts_minima) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
     if ((rc = ensure(d_psout, sizeof(PSegOut) * (size_t)N))) return rc;
-    uint8_t* dp = (uint8_t*)d_pdb.p;
+    uint8_t* dp = (uint8_t*)d_pdb.p + mm_b;
     if (pd_b) PCHK(hipMemcpyAsync(dp, pd.data(), pd_b, hipMemcpyHostToDevice, s));
     if (pool_b) PCHK(hipMemcpyAsync(dp + pd_b, pool.data(), pool_b, hipMemcpyHostToDevice, s));
     if (dis_b) PCHK(hipMemcpyAsync(dp + pd_b + pool_b, dis.data(), dis_b, hipMemcpyHostToDevice, s));
@@ -391,6 +396,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     v.all_nodes = all_nodes ? 1 : 0;
     v.pts_check = pts_on ? 1 : 0;
     v.now = now;
+    v.pts_mm = d_mm;
     PCHK(launch_preempt_seg(m, bv, 0, v, s));
     if ((rc = ensure(d_pick, sizeof(PickOut) + 4 * (size_t)N + 64))) return rc;
     PickOut* d_po = (PickOut*)d_pick.p;

@@ -15,8 +15,8 @@ rand.NewSource(4) (cycle 0 -> 4, 1 -> 1, 2 -> 3) where parallelism is disabled, 
 every node is checked, so the offset cannot change the candidate set).  Expected candidates compare
 as the test compares them: victims sorted by name, candidates sorted by node name.
 
-Cases the device path declines (victims that change PodTopologySpread / InterPodAffinity counts)
-carry "device": "ENOTSUP"; the oracle must still match them.
+The case the device path declines (victims that change InterPodAffinity counts) carries "device":
+"ENOTSUP"; the oracle must still match it.
 Output: tests/golden/preemption.json (data only).
 """
 import json
@@ -135,8 +135,7 @@ def dry_run_cases():
                 [pod("pod-a1", MID, "node-a", labels={"foo": ""}), pod("pod-a2", LOW, "node-a", labels={"foo": ""}),
                  pod("pod-b1", LOW, "node-b", labels={"foo": ""}), pod("pod-x1", HIGH, "node-x", labels={"foo": ""}),
                  pod("pod-x2", HIGH, "node-x", labels={"foo": ""})],
-                {"node-a": cand(["pod-a2"]), "node-b": cand(["pod-b1"])}, plugins=("PodTopologySpread",),
-                device="ENOTSUP"),
+                {"node-a": cand(["pod-a2"]), "node-b": cand(["pod-b1"])}, plugins=("PodTopologySpread",)),
         dry_run(908, "preemption with violation of same pdb", ["node1"], pod("p", HIGH, req=VLARGE),
                 [pod("p1.1", MID, "node1", MEDIUM, labels={"app": "foo"}),
                  pod("p1.2", MID, "node1", MEDIUM, labels={"app": "foo"})],

@@ -180,18 +180,64 @@ def test_preempt_large_cluster(native):
         assert r.status == 0 and r.num_potential == 5000 and r.num_candidates >= 100
 
 
-def test_preempt_declines_topology_victims(native):
-    """Victims that change the pod's PodTopologySpread counts are outside the device contract."""
+def spread_cluster(seed, n_nodes):
+    """Pods labelled app=a/b in one namespace over zoned, hostname-labelled nodes; preemptors spread by
+    zone and hostname (DoNotSchedule), so their victims move the spread counts."""
+    rng = random.Random(seed)
+    nodes = [mk_node(i, rng) for i in range(n_nodes)]
+    existing = []
+    for i, n in enumerate(nodes):
+        for k in range(rng.randrange(6)):
+            p = mk_pod(f"e{i}-{k}", rng, node=n["metadata"]["name"])
+            p["metadata"]["namespace"] = "default"
+            p["metadata"]["labels"] = {"app": rng.choice(["a", "b"])}
+            existing.append(p)
+    return rng, nodes, existing
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_preempt_spread_victims_match_oracle(native, seed):
+    """Victims that move the preemptor's PodTopologySpread counts (PreemptTopo): the device-resident path
+    against the oracle's literal RemovePod / AddPod + criticalPaths; the host-staged path declines."""
+    from ksg.abi import KsgError
+    rng, nodes, existing = spread_cluster(100 + seed, 40 + 30 * seed)
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    found = 0
+    for q in range(10):
+        pod = mk_pod(f"pre{q}", rng, prio=rng.choice([500, 1000]), big=True)
+        pod["metadata"]["namespace"] = "default"
+        pod["metadata"]["labels"] = {"app": rng.choice(["a", "b"])}
+        pod["spec"]["containers"][0]["resources"]["requests"].pop("example.com/gpu", None)
+        keys = rng.sample(["topology.kubernetes.io/zone", "kubernetes.io/hostname"], rng.choice([1, 2]))
+        pod["spec"]["topologySpreadConstraints"] = [
+            {"maxSkew": rng.choice([1, 2]), "topologyKey": k, "whenUnsatisfiable": "DoNotSchedule",
+             "labelSelector": {"matchLabels": {"app": rng.choice(["a", "b"])}}} for k in keys]
+        # a clock past every start time keeps the device-resident segments in use (see DESIGN §4.7)
+        args = {"offset": rng.randrange(1000), "allNodes": rng.random() < 0.3, "listCandidates": True,
+                "now": 1704153600 * 10 ** 9,
+                "minCandidateNodesPercentage": rng.choice([10, 100]), "minCandidateNodesAbsolute": rng.choice([1, 100])}
+        r2, d2 = orc.preempt(orc.compile(pod), args)
+        r1, d1 = dev.preempt(dev.compile(pod), args)
+        assert r1.as_tuple() == r2.as_tuple(), (r1.as_tuple(), r2.as_tuple(), d1, d2)
+        assert d1 == d2
+        found += r1.status == 0
+        try:  # the host-staged path declines victims that move the counts, or agrees
+            r3, d3 = dev.preempt(dev.compile(pod), dict(args, debugHostStaged=True))
+            assert r3.as_tuple() == r2.as_tuple() and d3 == d2
+        except KsgError as e:
+            assert "rc=-5" in str(e)
+    assert found > 0
+
+
+def test_preempt_declines_affinity_victims(native):
+    """Victims with required anti-affinity terms (they move InterPodAffinity's existing-anti counts) are
+    outside the device contract."""
     rng, nodes, existing = cluster(3, 30, 6)
-    for p in existing:
-        p["metadata"]["labels"]["app"] = "a"
-        p["metadata"]["namespace"] = "default"
+    existing[0]["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"app": "zz"}}, "topologyKey": "kubernetes.io/hostname"}]}}
+    existing[0]["spec"]["priority"] = -100
     dev = build(native, nodes, existing)
     pod = mk_pod("pre", rng, prio=1000, big=True)
-    pod["metadata"]["namespace"] = "default"
-    pod["spec"]["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone",
-                                                 "whenUnsatisfiable": "DoNotSchedule",
-                                                 "labelSelector": {"matchLabels": {"app": "a"}}}]
     from ksg.abi import KsgError
     with pytest.raises(KsgError, match="rc=-5"):
         dev.preempt(dev.compile(pod), {})
