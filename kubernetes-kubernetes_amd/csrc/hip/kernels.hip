@@ -3897,4 +3897,24 @@ hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, 
   return hipGetLastError();
 }
 
+
+// Evaluation output of a node-sharded context: each rank scatters the per-node vectors of its own block
+// range into a zeroed full-length buffer, which an all-reduce (MAX) over the ranks then completes on
+// every rank -- statuses and the weighted normalised scores are all non-negative, so 0 is the identity.
+// Layout: [n] status | [kNumPlugins][n] plugin scores | [n] TotalScore.
+__global__ __launch_bounds__(kBlock) void k_eval_pack(BatchView b, int n, int cap, int lo, int hi,
+                                                      unsigned long long* g) {
+  const int i = lo + (int)blockIdx.x * kBlock + (int)threadIdx.x;
+  if (i >= hi || i >= n) return;
+  g[i] = b.status[i];
+#pragma unroll
+  for (int q = 0; q < kNumPlugins; ++q) g[(size_t)(1 + q) * n + i] = (unsigned long long)b.out_scores[(size_t)q * cap + i];
+  g[(size_t)(1 + kNumPlugins) * n + i] = (unsigned long long)b.out_total[i];
+}
+hipError_t launch_eval_pack(const BatchView& b, int n, int cap, int lo, int hi, unsigned long long* g, hipStream_t s) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_eval_pack, dim3((hi - lo + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, n, cap, lo, hi, g);
+  return hipGetLastError();
+}
+
 }  // namespace ksg

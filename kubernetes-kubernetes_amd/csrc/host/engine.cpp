@@ -28,6 +28,7 @@ hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod,
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, bool lds);
 hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s);
 hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, const PodDesc& d, hipStream_t s);
+hipError_t launch_eval_pack(const BatchView& b, int n, int cap, int lo, int hi, unsigned long long* g, hipStream_t s);
 hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0 = 0,
                             int nblk = -1);
 hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
@@ -1020,7 +1021,8 @@ Engine::~Engine() {
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
   if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps})
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps,
+                    &d_evg, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -1147,10 +1149,6 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const int n = (int)pods.size();
   if (n == 0) return KSG_OK;
   if (eval && n != 1) return KSG_EINVAL;
-  if (eval && comm) {
-    c->err = "per-node evaluation output is not gathered across node shards (use an unsharded context)";
-    return KSG_ENOTSUP;
-  }
   c->order();
   if (c->order().empty()) {  // ErrNoNodesAvailable (schedule_one.go:569-571)
     for (int i = 0; i < n; ++i) results[i] = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
@@ -1653,13 +1651,31 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if ((rc = close_chunk(n))) return rc;
   std::vector<uint32_t> st;
   std::vector<int64_t> outs, tot;
+  std::vector<unsigned long long> gath;
+  if (eval && comm) {
+    // node-sharded: gather every rank's range of the per-node vectors (collective: every rank's call
+    // carries the same evaluation request, as it carries the same pods)
+    const size_t words = (size_t)(2 + kNumPlugins) * (size_t)m.n;
+    if ((rc = ensure(d_evg, words * 8 + 8))) return rc;
+    HIPCHK(hipMemsetAsync(d_evg.p, 0, words * 8, s));
+    const int lo = shard_blk0 * kBlock, hi = std::min(m.n, (shard_blk0 + shard_nblk) * kBlock);
+    HIPCHK(launch_eval_pack(bv, m.n, m.cap, lo, hi, (unsigned long long*)d_evg.p, s));
+    if (comm->all_reduce_max((unsigned long long*)d_evg.p, words, s)) {
+      c->err = comm->err;
+      return KSG_EDEVICE;
+    }
+    gath.resize(words);
+    HIPCHK(hipMemcpyAsync(gath.data(), d_evg.p, words * 8, hipMemcpyDeviceToHost, s));
+  }
   if (eval) {
     st.resize(m.n);
     outs.resize((size_t)m.cap * kNumPlugins);
     tot.resize(m.n);
-    HIPCHK(hipMemcpyAsync(st.data(), d_status.p, (size_t)m.n * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(outs.data(), d_out.p, outs.size() * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
+    if (!comm) {
+      HIPCHK(hipMemcpyAsync(st.data(), d_status.p, (size_t)m.n * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(outs.data(), d_out.p, outs.size() * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
+    }
   }
   if (chunks.size() > 1)  // pipelined: settle each chunk as soon as its results have landed
     for (size_t k = (size_t)settled; k < chunks.size(); ++k) {
@@ -1936,6 +1952,14 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                  "topology %.3f (spread %.3f  affinity %.3f  placement+tables %.3f)  masks+assume %.3f\n", cprof_[0] / n,
                  cprof_[1] / n, cprof_[2] / n, cprof_[3] / n, cprof_[5] / n, cprof_[6] / n, cprof_[7] / n, cprof_[4] / n);
     for (double& v : cprof_) v = 0;
+  }
+  if (eval && comm) {  // unpack the gathered vectors
+    const size_t n = (size_t)m.n;
+    for (size_t i = 0; i < n; ++i) {
+      st[i] = (uint32_t)gath[i];
+      for (int q = 0; q < kNumPlugins; ++q) outs[(size_t)q * m.cap + i] = (int64_t)gath[(1 + q) * n + i];
+      tot[i] = (int64_t)gath[(1 + kNumPlugins) * n + i];
+    }
   }
   if (eval) {
     const int32_t N = m.n;

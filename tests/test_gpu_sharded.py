@@ -148,13 +148,37 @@ def test_c3_pod_affinity_sharded():
     _check(ranks, o, pods, chunk=50)
 
 
-def test_eval_output_is_refused_when_sharded():
-    from ksg.abi import KsgError
-    rng, cfg, nodes, existing, names = rand_cluster(5, n_nodes=50, n_existing=5)
-    ranks, _ = _group(2, cfg, nodes, existing)
-    h = ranks[0].compile(rand_pod(rng, 0, names))
-    with pytest.raises(KsgError, match="not gathered"):
-        ranks[0].schedule_one(h, evaluate=True)
+@pytest.mark.parametrize("world,seed", [(2, 7), (3, 8)])
+def test_eval_output_gathered_when_sharded(world, seed):
+    """Per-node evaluation output on a node-sharded context (the plugin-level hook's input): every rank
+    returns the whole snapshot's statuses, per-plugin scores and TotalScores, gathered over the ranks,
+    equal to the oracle's, for a stream of pods with assume."""
+    rng, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=[0, 0, 0, 0, 0, 0, 0, 700, 900][seed],
+                                                    n_existing=60)
+    ranks, o = _group(world, cfg, nodes, existing)
+    pods = [rand_pod(rng, k, names) for k in range(25)]
+    out = [[] for _ in ranks]
+    errs = []
+
+    def work(r):
+        try:
+            for p in pods:
+                res, ev = ranks[r].schedule_one(ranks[r].compile(p), assume=True, evaluate=True)
+                out[r].append((res.as_tuple(), ev))
+        except Exception as e:  # surfaced below
+            errs.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    for k, p in enumerate(pods):
+        res, ev = o.schedule_one(o.compile(p), assume=True, evaluate=True)
+        for r in range(world):
+            assert out[r][k][0] == res.as_tuple(), f"rank {r} pod {k}"
+            assert out[r][k][1] == ev, f"rank {r} pod {k}: evaluation output differs"
 
 
 def test_rccl_transport_single_rank_matches_oracle():
