@@ -238,10 +238,8 @@ int ksg_preempt(ksg_ctx* ctx, int32_t handle, const char* args_json, size_t args
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
-    if (ctx->cluster->cfg.sharded()) {
-      ctx->err = "preemption on a node-sharded context is not supported";
-      return KSG_ENOTSUP;
-    }
+    // node-sharded contexts: every rank holds the whole mirror and pod table, so each rank runs the
+    // PostFilter over every node by itself (no exchange) and returns the identical choice
     std::string d;
     const int rc = ctx->engine->preempt(it->second, args_json, args_len, result, detail ? &d : nullptr);
     if (rc) return with_err(ctx, rc);

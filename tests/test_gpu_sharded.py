@@ -181,6 +181,33 @@ def test_eval_output_gathered_when_sharded(world, seed):
             assert out[r][k][1] == ev, f"rank {r} pod {k}: evaluation output differs"
 
 
+def test_preemption_on_sharded_ranks():
+    """DefaultPreemption on a node-sharded group: each rank holds the whole mirror and runs the PostFilter
+    over every node itself; every rank's choice equals the oracle's."""
+    from test_gpu_preempt import build, cluster, mk_pod
+    rng, nodes, existing = cluster(21, 300, 6)
+    name = f"t-{uuid.uuid4().hex[:8]}"
+    from ksg.native import Scheduler
+    ranks = []
+    for r in range(2):
+        s = Scheduler({"device": 0, "distributed": {"worldSize": 2, "rank": r, "localGroup": name}})
+        for ns in ("default", "team"):
+            s.upsert_namespace({"metadata": {"name": ns}})
+        for n in nodes:
+            s.add_node(n)
+        for p in existing:
+            s.add_pod(p)
+        ranks.append(s)
+    o = build(oracle, nodes, existing)
+    for q in range(8):
+        pod = mk_pod(f"pre{q}", rng, prio=1000, big=True)
+        args = {"offset": q * 31, "now": 1704153600 * 10 ** 9, "listCandidates": True}
+        r0, d0 = o.preempt(o.compile(pod), args)
+        for s in ranks:
+            r1, d1 = s.preempt(s.compile(pod), args)
+            assert r1.as_tuple() == r0.as_tuple() and d1 == d0, f"pod {q}"
+
+
 def test_rccl_transport_single_rank_matches_oracle():
     """The RCCL transport itself (ncclGetUniqueId -> ncclCommInitRank -> in-stream ncclAllReduce
     MAX between the kernels) at worldSize 1 -- the one-GPU box cannot host two RCCL ranks."""
