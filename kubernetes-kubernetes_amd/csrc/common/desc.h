@@ -304,6 +304,9 @@ struct PreemptView {
   int64_t now;               // GetPodStartTime for pods without a start time
   const long long* pts_mm;   // [kPreemptCons][3]: per DoNotSchedule constraint the domain minimum, its
                              // multiplicity and the next larger count (k_pts_minima)
+  const int32_t* ex_contrib; // [slot][kPreemptCons]: the pod's required anti-affinity terms that match the
+                             // preemptor, per existing-anti key (k_preempt_terms); nullptr: none
+  int32_t ipa_check, pad2;
 };
 constexpr int kPreemptCons = 4;  // DoNotSchedule constraints whose counts the victims may move (more: unsupported)
 

@@ -3454,11 +3454,19 @@ struct PreemptTopo {
   int64_t cnt0[kPreemptCons];  // its cycle count
   int64_t dlt[kPreemptCons];   // + reprieved - removed victims that constraint c counts
   int64_t excl[kPreemptCons];  // minimum over the other domains
+  // InterPodAffinity (filtering.go:75-85 updateWithPod): [0, 4) the preemptor's required affinity terms,
+  // [4, 8) its required anti-affinity terms, [8, 12) the existing-anti keys; each moves the count of node
+  // i's own domain (its value of the term's key)
+  int32_t ihb[3 * kPreemptCons], ivi[3 * kPreemptCons];
+  int32_t idl[3 * kPreemptCons];
   __device__ __forceinline__ int64_t cnt(int32_t hist_base, int32_t lref, int32_t v, int ls) const {
     int64_t x = a.cnt(hist_base, lref, v, ls);
 #pragma unroll
     for (int c = 0; c < kPreemptCons; ++c)
       if (hb[c] == hist_base && vi[c] == v) x += dlt[c];
+#pragma unroll
+    for (int k = 0; k < 3 * kPreemptCons; ++k)
+      if (ihb[k] == hist_base && ivi[k] == v) x += idl[k];
     return x;
   }
   __device__ __forceinline__ int64_t pmin(int c) const {
@@ -3532,6 +3540,42 @@ hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* 
   return hipGetLastError();
 }
 
+// The existing pods' required anti-affinity terms that match the preemptor (the term role of k_aggregate,
+// AffinityTerm.Matches, types.go:391-396), counted per owning pod-table slot and existing-anti key: what a
+// victim's RemovePod takes out of existingAntiAffinityCounts at its node (filtering.go:75-85).
+__global__ __launch_bounds__(kBlock) void k_preempt_terms(MirrorView m, BatchView b, int pod, int32_t* contrib,
+                                                          uint32_t* unsup) {
+  const int j = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+  if (j >= m.n_terms) return;
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  const DTerm t = m.terms[j];
+  if (t.kind != T_REQ_ANTI || m.pod_node[t.owner] < 0 || t.key >= d.n_keytab) return;
+  const int32_t* kt = at<int32_t>(base, d.keytab_off) + (size_t)t.key * kKeytabStride;
+  const int32_t hb = (d.ipa_flags & IPA_EXIST_FILTER) ? kt[1] : -1;
+  if (hb < 0) return;
+  const int32_t* tp = m.term_pool;
+  const unsigned long long* il = at<unsigned long long>(base, d.lbl_off);
+  const unsigned long long* nl = at<unsigned long long>(base, d.nslbl_off);
+  const bool match = (id_in(tp + t.ns_off, t.ns_cnt, d.ns_id) || lsel_match(tp + t.nssel, nl, d.n_nslbl)) &&
+                     lsel_match(tp + t.sel, il, d.n_lbl);
+  if (!match) return;
+  const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
+  for (int e = 0; e < d.n_exkeys; ++e)
+    if (ek[e].base == hb) {
+      if (e < kPreemptCons) atomicAdd(&contrib[(size_t)t.owner * kPreemptCons + e], 1);
+      else atomicOr(unsup, 1u);
+      return;
+    }
+}
+hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, uint32_t* unsup,
+                                hipStream_t s) {
+  if (m.n_terms <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_preempt_terms, dim3((m.n_terms + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, b, pod,
+                     contrib, unsup);
+  return hipGetLastError();
+}
+
 // k_preempt_seg: k_preempt over the device-resident pod segments (PreemptView).  The filter re-runs and
 // the reprieve are k_preempt's; what the host staged per call there is derived here: the potential
 // victims (the segment suffix below the preemptor's priority), filterPodsWithPDBViolation
@@ -3602,6 +3646,69 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
         }
     }
   }
+#pragma unroll
+  for (int k = 0; k < 3 * kPreemptCons; ++k) tp.ihb[k] = tp.ivi[k] = -1, tp.idl[k] = 0;
+  const IpaTerm* raff = at<IpaTerm>(base, d.raff_off);
+  const IpaTerm* ranti = at<IpaTerm>(base, d.ranti_off);
+  const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
+  const int nra = pv.ipa_check ? d.n_raff : 0, nrn = pv.ipa_check ? d.n_ranti : 0;
+  const int nex = (pv.ipa_check && pv.ex_contrib) ? d.n_exkeys : 0;
+  if (pv.ipa_check) {
+    if (nra > kPreemptCons || nrn > kPreemptCons || nex > kPreemptCons) o.flags |= 1u;  // beyond PreemptTopo
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k) {
+      if (k < nra) {
+        tp.ihb[k] = raff[k].hist_base;
+        tp.ivi[k] = node_label(m, raff[k].slot, i);
+      }
+      if (k < nrn) {
+        tp.ihb[kPreemptCons + k] = ranti[k].hist_base;
+        tp.ivi[kPreemptCons + k] = node_label(m, ranti[k].slot, i);
+      }
+      if (k < nex) {
+        tp.ihb[2 * kPreemptCons + k] = ek[k].base;
+        tp.ivi[2 * kPreemptCons + k] = node_label(m, ek[k].slot, i);
+      }
+    }
+  }
+  // victim q's InterPodAffinity effect, applied with sign sg: the preemptor's affinity terms count it when
+  // it matches all of them, its anti-affinity terms each when it matches, and its own required
+  // anti-affinity terms that match the preemptor count at their keys; false: no count moves
+  auto ipa_apply = [&](int q, PreemptTopo& x, int sg) -> bool {
+    if (!pv.ipa_check || (nra == 0 && nrn == 0 && nex == 0)) return false;
+    const int32_t slot = r[q].slot;
+    const int32_t ns = m.pod_ns[slot];
+    const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+    const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+    const int32_t* sp2 = at<int32_t>(base, d.sel_pool_off);
+    bool moved = false;
+    bool all = nra > 0;
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k)
+      if (k < nra) all = all && term_matches_pod(sp2, raff[k], ns, lb, ln);
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k) {
+      if (all && k < nra && tp.ivi[k] >= 0) {
+        x.idl[k] += sg;
+        moved = true;
+      }
+      if (k < nrn && tp.ivi[kPreemptCons + k] >= 0 && term_matches_pod(sp2, ranti[k], ns, lb, ln)) {
+        x.idl[kPreemptCons + k] += sg;
+        moved = true;
+      }
+      if (k < nex && tp.ivi[2 * kPreemptCons + k] >= 0) {
+        const int32_t cn = pv.ex_contrib[(size_t)slot * kPreemptCons + k];
+        if (cn) {
+          x.idl[2 * kPreemptCons + k] += sg * cn;
+          moved = true;
+        }
+      }
+    }
+    // affinityCounts emptied by the removal could flip the "no pod matches anywhere" rule
+    // (filtering.go:404-415) for a preemptor matching its own terms: outside PreemptTopo
+    if (all && sg < 0 && (d.ipa_flags & IPA_SELF_ALL)) o.flags |= 1u;
+    return moved;
+  };
   auto counts = [&](int q) -> uint32_t {  // the constraints whose count victim q is part of
     if (!elig) return 0u;
     const int32_t slot = r[q].slot;
@@ -3661,6 +3768,7 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
 #pragma unroll
     for (int c = 0; c < kPreemptCons; ++c) tp.dlt[c] -= (k >> c) & 1u;
     moves |= k != 0;
+    moves |= ipa_apply(q, tp, -1);
   }
   nc.npods -= cnt - first;
   int64_t sreq[kPreemptScalar] = {0, 0, 0, 0};  // the host takes this path only for pods without scalar requests
@@ -3684,8 +3792,9 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
         PreemptTopo tt = tp;
 #pragma unroll
         for (int c = 0; c < kPreemptCons; ++c) tt.dlt[c] += (k >> c) & 1u;
+        const bool im = moves && ipa_apply(q, tt, +1);
         bool fits = preempt_node_filters(m, t, sreq, base, d, i, tpo) == 0;
-        if (fits && k) fits = topo_filters(m, base, d, i, tt, 0) == 0;
+        if (fits && (k || im)) fits = topo_filters(m, base, d, i, tt, 0) == 0;
         if (fits) {
           nc = t;
           port = tpo;
@@ -3805,14 +3914,22 @@ __global__ __launch_bounds__(kPickThreads) void k_preempt_pick(const PSegOut* ou
   if (nc < absn) nc = absn;
   if (nc > P) nc = P;
   const int ncand = (int)nc;
-  // the cut: first rotated position j whose candidate brings (min(NV, nc) >= 1, min(NV, nc) + min(VV, nc) >= nc)
+  // one pass in rotated order: running non-violating / violating counts (block scans), the cut -- the first
+  // position whose candidate brings min(NV, nc) >= 1 and min(NV, nc) + min(VV, nc) >= nc -- and every
+  // thread's best candidate up to it.  Candidate order: the non-violating list, then the violating one,
+  // each in rotated order (the tie-break index needs no list sizes: class in the high bits).
   auto cls = [&](int j) {  // 1: non-violating candidate, 2: violating candidate, 0: neither
     const PSegOut& o = out[pot[(offset + j) % P]];
     if (o.st != 0 || o.nvictims == 0) return 0;
     return o.nviolating == 0 ? 1 : 2;
   };
-  if (t == 0) s_cut = INT32_MAX;
+  __shared__ int s_nvc, s_vvc;
+  if (t == 0) {
+    s_cut = INT32_MAX;
+    s_nvc = s_vvc = 0;
+  }
   __syncthreads();
+  PickKey best{0, 0, 0, 0, 0, 0, -1};
   int NV = 0, VV = 0;
   for (int b0 = 0; b0 < P; b0 += kPickThreads) {
     const int j = b0 + t;
@@ -3820,53 +3937,37 @@ __global__ __launch_bounds__(kPickThreads) void k_preempt_pick(const PSegOut* ou
     int tn, tv;
     const int en = block_excl_scan(c == 1 ? 1 : 0, &tn, s_w);
     const int ev = block_excl_scan(c == 2 ? 1 : 0, &tv, s_w);
-    int64_t nvc = (int64_t)(NV + en + (c == 1 ? 1 : 0)), vvc = (int64_t)(VV + ev + (c == 2 ? 1 : 0));
-    nvc = nvc < nc ? nvc : nc;
-    vvc = vvc < nc ? vvc : nc;
+    const int nvi = NV + en + (c == 1 ? 1 : 0), vvi = VV + ev + (c == 2 ? 1 : 0);  // inclusive counts
+    const int64_t nvc = nvi < nc ? nvi : nc, vvc = vvi < nc ? vvi : nc;
     if (c != 0 && nvc >= 1 && nvc + vvc >= nc) atomicMin(&s_cut, j);
     __syncthreads();
-    NV += tn;
-    VV += tv;
-    if (s_cut != INT32_MAX) break;  // uniform: every lane reads the shared value after the barrier
-  }
-  __syncthreads();
-  const int cut = s_cut == INT32_MAX ? P - 1 : s_cut;
-  // candidates over [0, cut]; the non-violating list's size decides the violating candidates' order
-  NV = 0;
-  VV = 0;
-  int nvtot = 0;
-  for (int b0 = 0; b0 <= cut; b0 += kPickThreads) {
-    const int j = b0 + t;
-    const int c = j <= cut ? cls(j) : 0;
-    int tn, tv;
-    block_excl_scan(c == 1 ? 1 : 0, &tn, s_w);
-    block_excl_scan(c == 2 ? 1 : 0, &tv, s_w);
-    NV += tn;
-    VV += tv;
-  }
-  nvtot = NV < ncand ? NV : ncand;
-  const int vvtot = VV < ncand ? VV : ncand;
-  PickKey best{0, 0, 0, 0, 0, 0, -1};
-  NV = 0;
-  VV = 0;
-  for (int b0 = 0; b0 <= cut; b0 += kPickThreads) {
-    const int j = b0 + t;
-    const int c = j <= cut ? cls(j) : 0;
-    int tn, tv;
-    const int en = block_excl_scan(c == 1 ? 1 : 0, &tn, s_w);
-    const int ev = block_excl_scan(c == 2 ? 1 : 0, &tv, s_w);
-    int idx = -1;
-    if (c == 1 && NV + en < ncand) idx = NV + en;
-    if (c == 2 && VV + ev < ncand) idx = nvtot + VV + ev;
-    if (idx >= 0) {
-      const int node = pot[(offset + j) % P];
-      const PSegOut& o = out[node];
-      PickKey k{-(int64_t)o.nviolating, -(int64_t)o.hiprio, -o.sumprio, -(int64_t)o.nvictims, o.earliest, idx, node};
-      if (pick_better(k, best)) best = k;
+    const int cut = s_cut;
+    if (c != 0 && j <= cut) {
+      int idx = -1;
+      if (c == 1 && nvi - 1 < ncand) idx = nvi - 1;
+      if (c == 2 && vvi - 1 < ncand) idx = (1 << 24) + vvi - 1;
+      if (idx >= 0) {
+        const int node = pot[(offset + j) % P];
+        const PSegOut& o = out[node];
+        PickKey k{-(int64_t)o.nviolating, -(int64_t)o.hiprio, -o.sumprio, -(int64_t)o.nvictims, o.earliest, idx, node};
+        if (pick_better(k, best)) best = k;
+      }
+    }
+    if (j == cut) {
+      s_nvc = (int)nvc;
+      s_vvc = (int)vvc;
     }
     NV += tn;
     VV += tv;
+    if (cut != INT32_MAX) break;  // uniform: every lane read the shared value after the barrier
   }
+  __syncthreads();
+  if (s_cut == INT32_MAX && t == 0) {  // no cut: every potential node was checked
+    s_nvc = NV < ncand ? NV : ncand;
+    s_vvc = VV < ncand ? VV : ncand;
+  }
+  __syncthreads();
+  const int nvtot = s_nvc, vvtot = s_vvc;
   s_k[t] = best;
   __syncthreads();
   for (int w = kPickThreads / 2; w > 0; w >>= 1) {

@@ -477,7 +477,7 @@ class Engine {
   DevBuf d_astamps;          // k_agg_loop diagnostic stamps
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)
-  DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick;
+  DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick, d_contrib_buf;
   std::vector<PRec> h_seg;
   std::vector<int32_t> h_segcnt;
   std::vector<std::vector<const BoundPod*>> seg_pods;

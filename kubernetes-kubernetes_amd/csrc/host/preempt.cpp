@@ -30,6 +30,8 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
                           uint8_t* vout, POut* out, int all_nodes, hipStream_t s);
 hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s);
 hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* mm, hipStream_t s);
+hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, uint32_t* unsup,
+                                hipStream_t s);
 hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_t pct, int64_t absn, int32_t* pot,
                                PickOut* res, hipStream_t s);
 
@@ -44,7 +46,7 @@ hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_
 
 namespace {
 
-enum : int { P_PORTS = KSG_PLUGIN_NODE_PORTS, P_PTS = KSG_PLUGIN_POD_TOPOLOGY_SPREAD };
+enum : int { P_PORTS = KSG_PLUGIN_NODE_PORTS, P_PTS = KSG_PLUGIN_POD_TOPOLOGY_SPREAD, P_IPA = KSG_PLUGIN_INTER_POD_AFFINITY };
 
 struct Pdb {  // policy/v1 PodDisruptionBudget, the fields filterPodsWithPDBViolation reads
   std::string ns;
@@ -304,11 +306,12 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   int32_t nom_ix = p.nominated_node.empty() ? -1 : c->index_of(p.nominated_node);
   if (N > 0 && (rc = c->ensure_mirror())) return rc;
   // The device-resident segments serve every pod whose victims' order the cache already knows (no pod
-  // sorted by the call's clock, see seg_build) and that the device groups itself: no scalar requests,
-  // no required InterPodAffinity terms on either side, at most kMaxPdb budgets.  The rest take the
-  // host-staged records (same kernel core).
-  bool seg = N > 0 && !staged && D.n_scalar == 0 && !ipa_req && c->req_anti_pods == 0 && pdbs.size() <= (size_t)kMaxPdb &&
+  // sorted by the call's clock, see seg_build) and that the device groups itself: no scalar requests, at
+  // most kMaxPdb budgets.  The rest take the host-staged records (same kernel core, which declines
+  // victims that move PodTopologySpread / InterPodAffinity counts).
+  bool seg = N > 0 && !staged && D.n_scalar == 0 && pdbs.size() <= (size_t)kMaxPdb &&
              (c->nostart_pods == 0 || now > c->max_start_ns);
+  const bool ipa_on = (D.filter_mask >> P_IPA) & 1u;
   if (seg && (rc = seg_refresh())) return rc;
   seg = seg && seg_overflow == 0 && (!ports_on || seg_many_ports == 0);
 
@@ -323,6 +326,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   // segment path: per-node victim masks (listCandidates), the device's cut and pick
   std::vector<PSegOut> so;
   PickOut pick{};
+  uint32_t tunsup = 0;
 
   uint8_t* hp = (uint8_t*)h_pinned;
   hipStream_t s = c->stream;
@@ -379,6 +383,19 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     long long* d_mm = (long long*)d_pdb.p;  // k_pts_minima's output, then the budgets
     const bool pts_minima = pts_on && D.n_ptsf <= kPreemptCons;
     if (pts_minima) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
+    // existing pods' required anti-affinity terms matching the preemptor, per slot and key
+    int32_t* d_contrib = nullptr;
+    uint32_t* d_tunsup = nullptr;
+    const bool terms = ipa_on && D.n_exkeys > 0 && m.n_terms > 0;
+    if (terms) {
+      const size_t cb = sizeof(int32_t) * kPreemptCons * (size_t)std::max(m.pods_hw, 1);
+      if ((rc = ensure(d_contrib_buf, cb + 64))) return rc;
+      d_contrib = (int32_t*)d_contrib_buf.p;
+      d_tunsup = (uint32_t*)((uint8_t*)d_contrib_buf.p + cb);
+      PCHK(hipMemsetAsync(d_contrib_buf.p, 0, cb + 4, s));
+      PCHK(launch_preempt_terms(m, bv, 0, d_contrib, d_tunsup, s));
+      PCHK(hipMemcpyAsync(&tunsup, d_tunsup, 4, hipMemcpyDeviceToHost, s));
+    }
     if ((rc = ensure(d_psout, sizeof(PSegOut) * (size_t)N))) return rc;
     uint8_t* dp = (uint8_t*)d_pdb.p + mm_b;
     if (pd_b) PCHK(hipMemcpyAsync(dp, pd.data(), pd_b, hipMemcpyHostToDevice, s));
@@ -397,6 +414,8 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     v.pts_check = pts_on ? 1 : 0;
     v.now = now;
     v.pts_mm = d_mm;
+    v.ex_contrib = d_contrib;
+    v.ipa_check = ipa_on ? 1 : 0;
     PCHK(launch_preempt_seg(m, bv, 0, v, s));
     if ((rc = ensure(d_pick, sizeof(PickOut) + 4 * (size_t)N + 64))) return rc;
     PickOut* d_po = (PickOut*)d_pick.p;
@@ -407,8 +426,9 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       PCHK(hipMemcpyAsync(so.data(), d_psout.p, sizeof(PSegOut) * (size_t)N, hipMemcpyDeviceToHost, s));
     }
     if ((rc = finish_device())) return rc;
-    if (pick.unsupported) {
-      c->err = "preemption: a victim changes the pod's PodTopologySpread counts (not supported on the device)";
+    if (pick.unsupported || tunsup) {
+      c->err = "preemption: a victim's effect on the pod's PodTopologySpread / InterPodAffinity counts is outside "
+               "what the device tracks (more than 4 constraints, terms or keys, or an emptied affinity count)";
       return KSG_ENOTSUP;
     }
     for (int32_t i = 0; list && i < N; ++i) po[i] = NodeOut{so[i].st, so[i].nvictims, so[i].nviolating};

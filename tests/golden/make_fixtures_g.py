@@ -15,8 +15,7 @@ rand.NewSource(4) (cycle 0 -> 4, 1 -> 1, 2 -> 3) where parallelism is disabled, 
 every node is checked, so the offset cannot change the candidate set).  Expected candidates compare
 as the test compares them: victims sorted by name, candidates sorted by node name.
 
-The case the device path declines (victims that change InterPodAffinity counts) carries "device":
-"ENOTSUP"; the oracle must still match it.
+A case the device path declines would carry "device": "ENOTSUP" (none does).
 Output: tests/golden/preemption.json (data only).
 """
 import json
@@ -128,7 +127,7 @@ def dry_run_cases():
         dry_run(822, "pod with anti-affinity is preempted", n2, pod("p", HIGH, req=SMALL, labels={"foo": ""}),
                 [pod("p1.1", LOW, "node1", SMALL, labels={"foo": ""}, anti_exists=("foo", "hostname")),
                  pod("p1.2", MID, "node1", SMALL), pod("p1.3", HIGH, "node1", SMALL), pod("p2", HIGH, "node2", SMALL)],
-                {"node1": cand(["p1.1"])}, plugins=("NodeResourcesFit", "InterPodAffinity"), device="ENOTSUP"),
+                {"node1": cand(["p1.1"])}, plugins=("NodeResourcesFit", "InterPodAffinity")),
         dry_run(854, "preemption to resolve pod topology spread filter failure",
                 ["node-a/zone1", "node-b/zone1", "node-x/zone2"],
                 pod("p", HIGH, labels={"foo": ""}, spreads=[spread(1, "zone"), spread(1, "hostname")]),

@@ -229,15 +229,58 @@ def test_preempt_spread_victims_match_oracle(native, seed):
     assert found > 0
 
 
-def test_preempt_declines_affinity_victims(native):
-    """Victims with required anti-affinity terms (they move InterPodAffinity's existing-anti counts) are
-    outside the device contract."""
-    rng, nodes, existing = cluster(3, 30, 6)
-    existing[0]["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
-        {"labelSelector": {"matchLabels": {"app": "zz"}}, "topologyKey": "kubernetes.io/hostname"}]}}
-    existing[0]["spec"]["priority"] = -100
-    dev = build(native, nodes, existing)
-    pod = mk_pod("pre", rng, prio=1000, big=True)
+def affinity_cluster(seed, n_nodes):
+    """Existing pods with required anti-affinity terms (hostname / zone) against app labels, and
+    preemptors with required pod affinity / anti-affinity terms: victims move InterPodAffinity's
+    existingAntiAffinityCounts, affinityCounts and antiAffinityCounts."""
+    rng = random.Random(seed)
+    nodes = [mk_node(i, rng) for i in range(n_nodes)]
+    existing = []
+    for i, n in enumerate(nodes):
+        for k in range(rng.randrange(6)):
+            p = mk_pod(f"e{i}-{k}", rng, node=n["metadata"]["name"])
+            p["metadata"]["namespace"] = "default"
+            p["metadata"]["labels"] = {"app": rng.choice(["a", "b", "c"])}
+            p["spec"]["containers"][0]["resources"]["requests"].pop("example.com/gpu", None)
+            if rng.random() < 0.15:
+                p["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                    {"labelSelector": {"matchLabels": {"app": rng.choice(["a", "b"])}},
+                     "topologyKey": rng.choice(["kubernetes.io/hostname", "topology.kubernetes.io/zone"])}]}}
+            existing.append(p)
+    return rng, nodes, existing
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_preempt_affinity_victims_match_oracle(native, seed):
+    """Victims that move the preemptor's InterPodAffinity counts: the device-resident path (PreemptTopo's
+    InterPodAffinity deltas, k_preempt_terms) against the oracle's literal RemovePod / AddPod; an
+    unsupported case (a self-matching preemptor whose affinity counts a victim empties) is declined."""
     from ksg.abi import KsgError
-    with pytest.raises(KsgError, match="rc=-5"):
-        dev.preempt(dev.compile(pod), {})
+    rng, nodes, existing = affinity_cluster(200 + seed, 40 + 30 * seed)
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    found = declined = 0
+    for q in range(12):
+        pod = mk_pod(f"pre{q}", rng, prio=rng.choice([500, 1000]), big=True)
+        pod["metadata"]["namespace"] = "default"
+        pod["metadata"]["labels"] = {"app": rng.choice(["a", "b", "c"])}
+        pod["spec"]["containers"][0]["resources"]["requests"].pop("example.com/gpu", None)
+        kind = rng.choice(["none", "affinity", "anti"])
+        if kind != "none":
+            key = "podAffinity" if kind == "affinity" else "podAntiAffinity"
+            pod["spec"]["affinity"] = {key: {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"app": rng.choice(["a", "b", "c"])}},
+                 "topologyKey": rng.choice(["kubernetes.io/hostname", "topology.kubernetes.io/zone"])}]}}
+        args = {"offset": rng.randrange(1000), "allNodes": rng.random() < 0.3, "listCandidates": True,
+                "now": 1704153600 * 10 ** 9,
+                "minCandidateNodesPercentage": rng.choice([10, 100]), "minCandidateNodesAbsolute": rng.choice([1, 100])}
+        r2, d2 = orc.preempt(orc.compile(pod), args)
+        try:
+            r1, d1 = dev.preempt(dev.compile(pod), args)
+        except KsgError as e:
+            assert "rc=-5" in str(e) and kind == "affinity", e
+            declined += 1
+            continue
+        assert r1.as_tuple() == r2.as_tuple(), (kind, r1.as_tuple(), r2.as_tuple(), d1, d2)
+        assert d1 == d2, kind
+        found += r1.status == 0
+    assert found > 0 and declined < 6
