@@ -437,12 +437,12 @@ int Cluster::remove_pod(const std::string& uid) {
     }                                                        \
   } while (0)
 
-int Cluster::ensure_mirror() {
+int Cluster::ensure_mirror(bool pods_needed) {
   order();
   if (!layout_dirty) {
     int rc = flush_node_updates();
     if (!rc) rc = flush_node_dynamic();
-    return rc ? rc : upload_pod_table();
+    return rc ? rc : upload_pod_table(!pods_needed);
   }
   if (!defer_relayout && !mirror_suspect) {  // node adds / removes / zone moves: move the unchanged nodes' columns
     bool done = false;

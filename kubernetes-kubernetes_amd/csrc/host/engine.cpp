@@ -1235,7 +1235,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
   }
   const auto T1 = clk::now();
-  if ((rc = c->ensure_mirror())) return rc;
+  bool pods_needed = eval != nullptr || compiled < n;  // later chunks are compiled after the first launch
+  for (int i = 0; i < compiled && !pods_needed; ++i)
+    pods_needed = (reinterpret_cast<const PodDesc*>(cp[i].blob.data())->flags & DF_AGGREGATE) != 0;
+  if ((rc = c->ensure_mirror(pods_needed))) return rc;
   // ---- staging: [offsets n | program sizes n | PodStats n | DevResult n | give-up flags n | programs]
   // in pinned memory; each chunk's programs, offsets and stats go up in their own H2D copies
   size_t desc_bytes = 0;
@@ -1348,11 +1351,14 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const int max_wg = std::min(256 / W, comm && c->cfg.nccl_id.empty() ? cus / W : cus);
   int G = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
   G = std::min(std::max(G, (NBs + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NBs, 1), max_wg));
-  const bool use_loop = (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
+  // a single-pod call (the per-pod API) runs faster on the launch path: the loop's launch, granule
+  // zeroing and LDS load of every node core cost more than two per-node launches (scripts/single_pod_probe.py)
+  const bool loop_worth = comm || n > 1;
+  const bool use_loop = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
                         (int64_t)G * kLoopMaxBlk >= NBs && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   // k_agg_loop (unsharded): the same geometry; every workgroup's LDS lists must hold its nodes' pods
   // and terms plus everything this batch can add (each pod, and its own terms, at most once)
-  bool use_agg = !comm && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 && G <= cus &&
+  bool use_agg = loop_worth && !comm && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 && G <= cus &&
                  (int64_t)G * kLoopMaxBlk >= NB && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   if (use_agg) {
     bool any = false;

@@ -322,7 +322,9 @@ class Cluster {
   // reserve a slot for `p` (node index -1 until placed); its terms go live with the slot
   int32_t pod_table_put(const PodSpec& p, int32_t node_index);
   void pod_table_drop(int32_t slot);
-  int upload_pod_table();
+  // lazy: skip the upload (keeping pods_dirty) when the device copy has room for every slot -- the
+  // device-side AssumePod only writes pod_node[slot] -- and no pod of the call reads the table
+  int upload_pod_table(bool lazy = false);
   std::vector<double> log_tab;  // go math.Log(k), k < log_n
   int32_t scalar_slot(const std::string& n);  // -1 if too many distinct scalars
   uint32_t port_id(std::string ip, std::string proto, int32_t port);
@@ -339,7 +341,7 @@ class Cluster {
   std::vector<int32_t> static_dirty_;
   std::vector<uint8_t> static_queued_;
   DevBuf upd_dev_;
-  int ensure_mirror();                       // (re)build device arrays if dirty
+  int ensure_mirror(bool pods_needed = true);  // (re)build device arrays if dirty
   // diff the device mirror (dynamic + static node columns, pod table) against the host shadow;
   // sync: run ensure_mirror first (what the next cycle does)
   int compare_mirror(bool sync, int32_t* ndiff, int32_t* first);

@@ -207,7 +207,11 @@ double go_log(double x) {
   return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
 }
 
-int Cluster::upload_pod_table() {
+int Cluster::upload_pod_table(bool lazy) {
+  // a call whose pods never read the pod table (no PodTopologySpread / InterPodAffinity work) only needs
+  // pod_node to have room for the slots its assumes write: the table goes up with the next call that
+  // reads it (every single-pod call of a node-local stream would otherwise re-upload the whole table)
+  if (lazy && pods_dirty && pt_dev_[0].p && pt_dev_[0].bytes >= pt_node.size() * 4 + 4) return KSG_OK;
   // log table covers topoSize + 2 for every topoSize <= N (scoring.go:293-299)
   const int32_t need_log = (int32_t)order_.size() + 4;
   bool log_dirty = false;
