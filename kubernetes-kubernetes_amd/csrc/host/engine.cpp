@@ -1020,7 +1020,7 @@ Engine::~Engine() {
   for (hipEvent_t e : cev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
   if (cstream) (void)hipStreamDestroy(cstream);
-  for (DevBuf* b : {&d_descs, &d_off, &d_stats, &d_results, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
+  for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps,
                     &d_evg, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf})
     if (b->p) (void)hipFree(b->p);
@@ -1045,9 +1045,18 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena
   const size_t nb = cap / kBlock + 1;
   int rc;
   if ((rc = ensure(d_descs, desc_bytes))) return rc;
-  if ((rc = ensure(d_off, (size_t)pods * 8))) return rc;
-  if ((rc = ensure(d_stats, (size_t)pods * sizeof(PodStats)))) return rc;
-  if ((rc = ensure(d_results, (size_t)pods * sizeof(DevResult)))) return rc;
+  // offsets + program sizes, PodStats and DevResult in one allocation laid out like the pinned staging
+  // area (run_batch), so a single-chunk batch sends them up in one copy; d_off / d_stats / d_results are
+  // views into it (re-derived here for every batch size)
+  const size_t meta = ((size_t)pods * 8 + 15) & ~size_t(15);
+  const size_t stats_b = (size_t)pods * sizeof(PodStats), res_b = (size_t)pods * sizeof(DevResult);
+  if ((rc = ensure(d_meta, meta + stats_b + res_b + 16))) return rc;
+  d_off.p = d_meta.p;
+  d_off.bytes = (size_t)pods * 8;
+  d_stats.p = (uint8_t*)d_meta.p + meta;
+  d_stats.bytes = stats_b;
+  d_results.p = (uint8_t*)d_meta.p + meta + stats_b;
+  d_results.bytes = res_b;
   if ((rc = ensure(d_status, cap * 4))) return rc;
   if ((rc = ensure(d_fmask, nb * (kBlock / 64) * 8))) return rc;
   if ((rc = ensure(d_blk, nb * 4))) return rc;
@@ -1311,10 +1320,15 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
     if (b > a) {
       HIPCHK(hipMemcpyAsync((uint8_t*)d_descs.p + o0, hdesc + o0, o - o0, hipMemcpyHostToDevice, st_));
-      HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + a, h_offs + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice, st_));
-      HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + n + a, h_offs + n + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice, st_));
-      HIPCHK(hipMemcpyAsync((PodStats*)d_stats.p + a, hs + a, (size_t)(b - a) * sizeof(PodStats),
-                            hipMemcpyHostToDevice, st_));
+      if (a == 0 && b == n) {  // the whole batch: offsets, sizes and stats are one contiguous range
+        HIPCHK(hipMemcpyAsync(d_meta.p, hp, meta + (size_t)n * sizeof(PodStats), hipMemcpyHostToDevice, st_));
+      } else {
+        HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + a, h_offs + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice, st_));
+        HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + n + a, h_offs + n + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice,
+                              st_));
+        HIPCHK(hipMemcpyAsync((PodStats*)d_stats.p + a, hs + a, (size_t)(b - a) * sizeof(PodStats),
+                              hipMemcpyHostToDevice, st_));
+      }
     }
     if (async) {
       HIPCHK(hipEventRecord(pev[2 * (size_t)staged_chunks], cstream));

@@ -468,7 +468,9 @@ class Engine {
 
  private:
   // per-batch device scratch
-  DevBuf d_descs, d_off, d_stats, d_results, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
+  DevBuf d_descs, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
+  DevBuf d_meta;                         // owns the three views below (ensure_scratch)
+  DevBuf d_off, d_stats, d_results;      // views: program offsets + sizes, PodStats, DevResult
   DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)
   DevBuf d_xa, d_xp, d_xb;  // node-sharded exchange vectors, one set per pod of the batch
   DevBuf d_evg;             // node-sharded evaluation output, gathered over the ranks
