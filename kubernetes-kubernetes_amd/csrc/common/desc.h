@@ -342,6 +342,9 @@ struct PodStats {
   uint32_t rot_out;                   // nextStartNodeIndex after this pod (schedule_one.go:686-687)
   uint32_t processed;                 // nodes processed by findNodesThatPassFilters
   int32_t samp_end;                   // snapshot index of the (K+1)-th feasible node in rotated order, -1: none
+                                      // (node-sharded: -2 on the ranks that do not hold it)
+  int32_t keep[4];                    // node-sharded cut: this rank's kept nodes are the feasible ones in
+                                      // [keep[0], keep[1]) or [keep[2], keep[3]) (k_sample_shard_b)
   uint32_t pad[3];
 };
 
@@ -415,8 +418,13 @@ enum XaWord : int {
   XA_MAX_NA,
   XA_MAX_IPA,
   XA_NMIN_IPA,
+  XA_END,                       // percentageOfNodesToScore cut: 1 + the (K+1)-th feasible node, from its rank
+  XA_PROC,                      // 1 + processedNodes, from the same rank (0: every rank knows it)
   XA_WORDS = 4 * kMaxShards,
 };
+static_assert(XA_PROC < XA_WORDS, "XA layout");
+// The cut's pre-exchange (k_sample_shard_a): per-rank feasible counts before the cut
+enum XsWord : int { XS_CNT = 0, XS_BELOW = kMaxShards, XS_WORDS = 2 * kMaxShards };
 enum XpWord : int { XP_MAX_PTS = 0, XP_NMIN_PTS = 1, XP_WORDS = 4 };
 enum XbWord : int { XB_KEY = 0, XB_NODE = kMaxShards, XB_WORDS = 2 * kMaxShards };
 struct RankPtrs { unsigned long long* p[kMaxShards]; };  // every rank's exchange vector (local transport)
@@ -449,6 +457,7 @@ struct ShardView {
   unsigned long long* xa;     // [pods][XA_WORDS]
   unsigned long long* xp;     // [pods][XP_WORDS]
   unsigned long long* xb;     // [pods][XB_WORDS]
+  unsigned long long* xs;     // [pods][XS_WORDS]
 };
 
 // ---- persistent scheduling loop (k_sched_loop) -------------------------------------

@@ -1173,19 +1173,26 @@ __global__ __launch_bounds__(kBlock) void k_sample_find(MirrorView m, BatchView 
 // the normalising plugins' raw-score max/min, PodTopologySpread PreScore's ignored-node count and
 // domain presence (podtopologyspread/scoring.go:61-115).  Evaluation output: nodes past the cut
 // were never processed, so they carry no status (result[i] == nil, schedule_one.go:845-850).
-__global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView b, int pod) {
+// Node-sharded (shard != 0): the grid covers this rank's blocks from blk0, and the kept feasible
+// nodes are k_sample_shard_b's intervals; the statuses of unprocessed nodes are cleared by
+// k_select_shard once exchange A has carried the cut's end node to every rank.
+__global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView b, int pod, int blk0, int shard) {
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
-  const int blk = (int)blockIdx.x;
+  const int blk = blk0 + (int)blockIdx.x;
   const int i = blk * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t cap = (size_t)m.cap;
   const int end = ps->samp_end, s = (int)ps->rot;
-  const bool inproc = i < m.n && (end < 0 || in_cyclic(i, s, end));
+  bool inproc;
+  if (shard)
+    inproc = i < m.n && ((i >= ps->keep[0] && i < ps->keep[1]) || (i >= ps->keep[2] && i < ps->keep[3]));
+  else
+    inproc = i < m.n && (end < 0 || in_cyclic(i, s, end));
   const unsigned long long word = b.fmask[(size_t)blk * (kBlock / 64) + wave];
   const bool kept = inproc && ((word >> lane) & 1ull);
-  if ((d.flags & DF_EVAL_OUT) && i < m.n && !inproc) b.status[i] = 0u;
+  if (!shard && (d.flags & DF_EVAL_OUT) && i < m.n && !inproc) b.status[i] = 0u;
   const unsigned long long ballot = __ballot(kept);
   if (lane == 0) b.fmask[(size_t)blk * (kBlock / 64) + wave] = ballot;
   const uint32_t sm = d.score_mask;
@@ -1248,6 +1255,137 @@ __global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView
 }
 
 // ---- node-sharded path ----------------------------------------------------------------
+// percentageOfNodesToScore on a node-sharded context.  The cut needs the global rotated prefix of
+// feasible counts, so it costs one more all-reduce: k_sample_shard_a publishes this rank's feasible
+// count and its feasible nodes before the rotation start (XS words); k_sample_shard_b cuts with the
+// global figures.  The kept nodes are the global feasible ranks [below, below + K) mod F, the first
+// K of the rotated order (schedule_one.go:809-824); intersected with this rank's ranks [P, P + c)
+// they are at most two snapshot-index intervals, which k_sample_apply keeps.  The rank holding the
+// (K+1)-th feasible node knows end and processedNodes and publishes them in exchange A (XA_END,
+// XA_PROC); k_commit advances nextStartNodeIndex from them on every rank (:686-687).
+__device__ __forceinline__ uint32_t pod_rot_in(const BatchView& b, const PodDesc& d, const PodStats* ps) {
+  return d.prev_pod < 0 ? ps->rot_in : b.stats[d.prev_pod].rot_out;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sample_shard_a(MirrorView m, BatchView b, ShardView sv, int pod) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  unsigned long long* x = sv.xs + (size_t)pod * XS_WORDS;
+  const uint32_t rot_in = pod_rot_in(b, d, ps);
+  if (d.flags & DF_PREFILTER_REJECT) {  // the cycle ends before findNodesThatPassFilters (:635-648)
+    if (threadIdx.x == 0) {
+      ps->rot = 0;
+      ps->rot_out = rot_in;
+      ps->processed = 0;
+      ps->samp_end = -1;
+    }
+    if (threadIdx.x < XS_WORDS) x[threadIdx.x] = 0ull;
+    return;
+  }
+  const bool sub = (d.flags & DF_SUBSET) != 0;
+  const int32_t* subset = at<int32_t>(base, d.subset_off);
+  const int cnt = sub ? d.subset_cnt : m.n;
+  const int s = cnt == 0 ? 0 : (sub ? subset[rot_in % (uint32_t)cnt] : (int)rot_in);
+  const int k0 = sv.blk0, k1 = sv.blk0 + sv.nblk;
+  __shared__ uint32_t s_red[kBlock / 64];
+  __shared__ uint32_t s_below;
+  uint32_t c = 0;
+  for (int k = k0 + threadIdx.x; k < k1; k += kBlock) c += b.blk_cnt[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  c = 0;
+  for (int w = 0; w < kBlock / 64; ++w) c += s_red[w];
+  const uint32_t below = s > 0 ? count_below(b, k0, k1, s) : 0u;
+  if (threadIdx.x == 0) {
+    s_below = below;
+    ps->rot = (uint32_t)s;
+  }
+  __syncthreads();
+  if (threadIdx.x < XS_WORDS) {
+    const int w = threadIdx.x;
+    unsigned long long v = 0;
+    if (w == XS_CNT + sv.rank) v = c;
+    else if (w == XS_BELOW + sv.rank) v = s_below;
+    x[w] = v;
+  }
+}
+
+// cut = 0 (DF_ROTDEV without DF_SAMPLE): nothing is cut and no XS exchange ran; processedNodes is
+// the whole list.
+__global__ __launch_bounds__(kBlock) void k_sample_shard_b(MirrorView m, BatchView b, ShardView sv, int pod, int cut) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  if (d.flags & DF_PREFILTER_REJECT) return;
+  const unsigned long long* x = sv.xs + (size_t)pod * XS_WORDS;
+  const bool sub = (d.flags & DF_SUBSET) != 0;
+  const int32_t* subset = at<int32_t>(base, d.subset_off);
+  const int cnt = sub ? d.subset_cnt : m.n;
+  const int N = m.n;
+  const int s = (int)ps->rot;
+  const uint32_t K = (uint32_t)d.num_to_find;
+  uint32_t F = 0, below = 0, P = 0, c = 0;
+  if (cut)
+    for (int r = 0; r < sv.world; ++r) {
+      const uint32_t cr = (uint32_t)x[XS_CNT + r];
+      F += cr;
+      below += (uint32_t)x[XS_BELOW + r];
+      if (r < sv.rank) P += cr;
+      if (r == sv.rank) c = cr;
+    }
+  if (!cut || F <= K) {  // every feasible node is kept
+    if (threadIdx.x == 0) {
+      ps->samp_end = -1;
+      ps->processed = (uint32_t)cnt;
+      ps->keep[0] = 0;
+      ps->keep[1] = N;
+      ps->keep[2] = ps->keep[3] = 0;
+    }
+    return;
+  }
+  const int k0 = sv.blk0, k1 = sv.blk0 + sv.nblk;
+  const uint32_t gE = (below + K) % F;  // global feasible rank of the (K+1)-th node in rotated order
+  const bool owner = gE >= P && gE < P + c;
+  int end = -2;
+  uint32_t processed = 0;
+  if (owner) {
+    end = find_rank_node(b, k0, k1, gE - P);
+    __syncthreads();
+    if (sub) {  // rotated position inside the PreFilterResult list
+      __shared__ int s_pos[2];
+      for (int q = threadIdx.x; q < cnt; q += kBlock) {
+        if (subset[q] == s) s_pos[0] = q;
+        if (subset[q] == end) s_pos[1] = q;
+      }
+      __syncthreads();
+      processed = (uint32_t)((s_pos[1] - s_pos[0] + cnt) % cnt);
+    } else {
+      processed = (uint32_t)((end - s + N) % N);
+    }
+  }
+  // kept global ranks: [below, min(below + K, F)) and [0, below + K - F) when it wraps
+  const uint32_t lo[2] = {below, 0u};
+  const uint32_t hi[2] = {below + K < F ? below + K : F, below + K > F ? below + K - F : 0u};
+  int iv[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t a = lo[j] > P ? lo[j] : P, e = hi[j] < P + c ? hi[j] : P + c;
+    if (a < e) {  // uniform over the block
+      __syncthreads();
+      iv[2 * j] = find_rank_node(b, k0, k1, a - P);
+      __syncthreads();
+      iv[2 * j + 1] = find_rank_node(b, k0, k1, e - 1 - P) + 1;
+    }
+  }
+  if (threadIdx.x == 0) {
+    ps->samp_end = end;
+    ps->processed = processed;
+    for (int j = 0; j < 4; ++j) ps->keep[j] = iv[j];
+  }
+}
+
 // k_xpack_a (1 block): this rank's share of the first exchange -- feasible count, feasible nodes
 // before nextStartNodeIndex, PodTopologySpread non-ignored count, normalisation maxima/minima.
 __global__ __launch_bounds__(kBlock) void k_xpack_a(BatchView b, ShardView sv, int pod) {
@@ -1264,7 +1402,9 @@ __global__ __launch_bounds__(kBlock) void k_xpack_a(BatchView b, ShardView sv, i
   __syncthreads();
   c = 0;
   for (int w = 0; w < kBlock / 64; ++w) c += s_red[w];
-  const uint32_t below = d.rot_start > 0 ? count_below(b, k0, k1, d.rot_start) : 0u;
+  const int s = (d.flags & DF_ROTDEV) ? (int)ps->rot : d.rot_start;
+  const uint32_t below = s > 0 ? count_below(b, k0, k1, s) : 0u;
+  const bool cut_owner = (d.flags & DF_ROTDEV) && ps->samp_end >= 0;  // this rank holds the cut's end node
   unsigned long long* x = sv.xa + (size_t)pod * XA_WORDS;
   if (threadIdx.x < XA_WORDS) {
     const int w = threadIdx.x;
@@ -1276,6 +1416,8 @@ __global__ __launch_bounds__(kBlock) void k_xpack_a(BatchView b, ShardView sv, i
     else if (w == XA_MAX_NA) v = ps->max_raw[P_NA];
     else if (w == XA_MAX_IPA) v = ps->max_raw[P_IPA];
     else if (w == XA_NMIN_IPA) v = ~ps->min_raw[P_IPA];
+    else if (w == XA_END) v = cut_owner ? (unsigned long long)ps->samp_end + 1ull : 0ull;
+    else if (w == XA_PROC) v = cut_owner ? (unsigned long long)ps->processed + 1ull : 0ull;
     x[w] = v;
   }
 }
@@ -1330,6 +1472,12 @@ __global__ __launch_bounds__(kBlock) void k_select_shard(MirrorView m, BatchView
   const unsigned long long* xa = sv.xa + (size_t)pod * XA_WORDS;
   const unsigned long long* xp = sv.xp + (size_t)pod * XP_WORDS;
   const int blk = sv.blk0 + blockIdx.x;
+  if ((d.flags & (DF_EVAL_OUT | DF_SAMPLE)) == (DF_EVAL_OUT | DF_SAMPLE) && xa[XA_END] && sv.nblk > 0) {
+    // a cut feasible list: nodes past the cut were never processed (result[i] == nil,
+    // schedule_one.go:845-850)
+    const int i = blk * kBlock + threadIdx.x;
+    if (i < m.n && !in_cyclic(i, (int)ps->rot, (int)(xa[XA_END] - 1ull))) b.status[i] = 0u;
+  }
   if (sv.nblk == 0) {  // an empty shard publishes an empty share and still zeroes its arena
     for (int w = threadIdx.x; w < d.arena_words; w += kBlock) b.arena[w] = 0ull;
     if (threadIdx.x < XB_WORDS) sv.xb[(size_t)pod * XB_WORDS + threadIdx.x] = 0ull;
@@ -1391,6 +1539,10 @@ __global__ void k_commit(MirrorView m, BatchView b, ShardView sv, int pod) {
       best = xb[XB_KEY + r];
       node = (int)xb[XB_NODE + r] - 1;
     }
+  if ((d.flags & DF_ROTDEV) && !(d.flags & DF_PREFILTER_REJECT)) {  // nextStartNodeIndex (:686-687)
+    if (xa[XA_PROC]) ps->processed = (uint32_t)(xa[XA_PROC] - 1ull);
+    ps->rot_out = m.n > 0 ? (uint32_t)(((uint64_t)pod_rot_in(b, d, ps) + ps->processed) % (uint64_t)m.n) : 0u;
+  }
   commit_result(m, b, base, d, ps, pod, F, node, best);
 }
 
@@ -3238,7 +3390,18 @@ hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, int count, hip
 hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s) {
   const int nb = (m.n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_sample_find, dim3(1), dim3(kBlock), 0, s, m, b, pod, nb);
-  if (cut && nb > 0) hipLaunchKernelGGL(k_sample_apply, dim3(nb), dim3(kBlock), 0, s, m, b, pod);
+  if (cut && nb > 0) hipLaunchKernelGGL(k_sample_apply, dim3(nb), dim3(kBlock), 0, s, m, b, pod, 0, 0);
+  return hipGetLastError();
+}
+hipError_t launch_sample_shard_a(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_sample_shard_a, dim3(1), dim3(kBlock), 0, s, m, b, sv, pod);
+  return hipGetLastError();
+}
+hipError_t launch_sample_shard_b(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, bool cut,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(k_sample_shard_b, dim3(1), dim3(kBlock), 0, s, m, b, sv, pod, cut ? 1 : 0);
+  if (cut && sv.nblk > 0)
+    hipLaunchKernelGGL(k_sample_apply, dim3(sv.nblk), dim3(kBlock), 0, s, m, b, pod, sv.blk0, 1);
   return hipGetLastError();
 }
 hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s) {
@@ -3294,7 +3457,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
                       reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
-                      reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_node_update),
+                      reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_sample_shard_a),
+                      reinterpret_cast<const void*>(&k_sample_shard_b),        reinterpret_cast<const void*>(&k_node_update),
                       reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
   for (const void* f : fs) {

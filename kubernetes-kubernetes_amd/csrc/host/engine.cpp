@@ -32,6 +32,9 @@ hipError_t launch_eval_pack(const BatchView& b, int n, int cap, int lo, int hi, 
 hipError_t launch_pts_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, int blk0 = 0,
                             int nblk = -1);
 hipError_t launch_xpack_a(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+hipError_t launch_sample_shard_a(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
+hipError_t launch_sample_shard_b(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, bool cut,
+                                 hipStream_t s);
 hipError_t launch_unpack_pts(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
 hipError_t launch_xpack_p(const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
 hipError_t launch_select_shard(const MirrorView& m, const BatchView& b, const ShardView& sv, int pod, hipStream_t s);
@@ -488,13 +491,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     // percentageOfNodesToScore / a profile without score plugins: nextStartNodeIndex then depends
     // on where the filter pass stopped, so it lives on the device (DF_ROTDEV, k_sample_find)
     if (!any_score) D.flags |= DF_NO_SCORE;
-    if (rotdev()) {
-      if (comm) {
-        c->err = "percentageOfNodesToScore != 100 (or no score plugins) is not supported on a node-sharded context";
-        return KSG_ENOTSUP;
-      }
-      D.flags |= DF_ROTDEV;
-    }
+    if (rotdev()) D.flags |= DF_ROTDEV;
     if (score_err) D.flags |= DF_SCORE_ERROR;
     if (conflict || (!out->prefilter_error && out->ipa_parse_error)) {
       // PreFilter UnschedulableAndUnresolvable (NodeAffinity conflict, InterPodAffinity parse):
@@ -1021,7 +1018,7 @@ Engine::~Engine() {
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
   if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps,
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps,
                     &d_evg, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
@@ -1070,6 +1067,7 @@ int Engine::ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena
     if ((rc = ensure(d_xa, (size_t)pods * XA_WORDS * 8))) return rc;
     if ((rc = ensure(d_xp, (size_t)pods * XP_WORDS * 8))) return rc;
     if ((rc = ensure(d_xb, (size_t)pods * XB_WORDS * 8))) return rc;
+    if ((rc = ensure(d_xs, (size_t)pods * XS_WORDS * 8))) return rc;
     HIPCHK(hipMemsetAsync(d_xp.p, 0, (size_t)pods * XP_WORDS * 8, c->stream));
   }
   if (d_arena.bytes < (size_t)arena_words * 8 + 8) {
@@ -2029,6 +2027,7 @@ int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv,
   sv.xa = (unsigned long long*)d_xa.p;
   sv.xp = (unsigned long long*)d_xp.p;
   sv.xb = (unsigned long long*)d_xb.p;
+  sv.xs = (unsigned long long*)d_xs.p;
   const double frac = m.n > 0 ? std::min(1.0, (double)sv.nblk * kBlock / (double)m.n) : 0.0;
   const int stride = c->cfg.timing_stride;
   int& timed = *timed_out;
@@ -2050,10 +2049,17 @@ int Engine::run_sharded(const std::vector<CompiledPod>& cp, const BatchView& bv,
     } else {
       HIPCHK(launch_filter_score(m, bv, i, s, nullptr, nullptr, sv.blk0, sv.nblk, cp[i].blob.size() <= (size_t)kBlobLds));
     }
+    int rc = KSG_OK;
+    if (hd.flags & DF_ROTDEV) {  // percentageOfNodesToScore: the cut needs every rank's counts first
+      const bool cut = (hd.flags & DF_SAMPLE) != 0;
+      HIPCHK(launch_sample_shard_a(m, bv, sv, i, s));
+      if (cut && (rc = xchg(sv.xs + (size_t)i * XS_WORDS, XS_WORDS))) return rc;
+      HIPCHK(launch_sample_shard_b(m, bv, sv, i, cut, s));
+    }
     HIPCHK(launch_xpack_a(bv, sv, i, s));
     const bool pts = (hd.score_mask & (1u << P_PTS)) != 0;
     if (comm->group_begin()) return KSG_EDEVICE;
-    int rc = xchg(sv.xa + (size_t)i * XA_WORDS, XA_WORDS);
+    rc = xchg(sv.xa + (size_t)i * XA_WORDS, XA_WORDS);
     if (!rc && pts) {  // ScheduleAnyway domain presence (arena words) is OR-ed across shards
       const PtsCons* cs = reinterpret_cast<const PtsCons*>(cp[i].blob.data() + hd.ptss_off);
       for (int32_t k = 0; k < hd.n_ptss && !rc; ++k)

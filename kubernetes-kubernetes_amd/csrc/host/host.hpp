@@ -472,7 +472,7 @@ class Engine {
   DevBuf d_meta;                         // owns the three views below (ensure_scratch)
   DevBuf d_off, d_stats, d_results;      // views: program offsets + sizes, PodStats, DevResult
   DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)
-  DevBuf d_xa, d_xp, d_xb;  // node-sharded exchange vectors, one set per pod of the batch
+  DevBuf d_xa, d_xp, d_xb, d_xs;  // node-sharded exchange vectors, one set per pod of the batch
   DevBuf d_evg;             // node-sharded evaluation output, gathered over the ranks
   DevBuf d_gran, d_fail, d_stamps;  // k_sched_loop: exchange granules (local), give-up flag, stamps
   std::vector<unsigned long long*> gran_all;  // every rank's granule array as mapped here ([rank] = d_gran)

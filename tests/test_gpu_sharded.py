@@ -181,6 +181,71 @@ def test_eval_output_gathered_when_sharded(world, seed):
             assert out[r][k][1] == ev, f"rank {r} pod {k}: evaluation output differs"
 
 
+# ---- percentageOfNodesToScore on node-sharded contexts: the cut takes one more all-reduce of the
+# per-rank feasible counts (k_sample_shard_a/b), the rank holding the (K+1)-th feasible node of the
+# rotated order publishes end and processedNodes, and nextStartNodeIndex advances on every rank
+# from them (schedule_one.go:686-687,778-884).
+SHARD_SAMPLING = [(0, {}), (7, {}), (30, {}), (55, {"nodeResourcesFit": {"scoringStrategy": {"type": "MostAllocated"}}}),
+                  (100, {"disabledPlugins": ["TaintToleration", "NodeAffinity", "NodeResourcesFit", "PodTopologySpread",
+                                             "InterPodAffinity", "NodeResourcesBalancedAllocation", "ImageLocality"]})]
+
+
+@pytest.mark.parametrize("k", range(len(SHARD_SAMPLING)))
+@pytest.mark.parametrize("world", [2, 3])
+def test_sampling_sharded_matches_oracle(world, k):
+    pct, extra = SHARD_SAMPLING[k]
+    rng, cfg, nodes, existing, names = rand_cluster(7100 + 10 * k + world, n_nodes=[0, 0, 900, 1300][world],
+                                                    n_existing=80)
+    ranks, o = _group(world, dict(cfg, **extra, percentageOfNodesToScore=pct), nodes, existing)
+    _check(ranks, o, [rand_pod(rng, q, names) for q in range(120)], chunk=40)
+
+
+def test_sampling_sharded_basic_rotation():
+    """SchedulingBasic with pct 10 on W = 4: every pod's cut ends on some rank and the rotation walks
+    across all four shards."""
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(2300, 200, 300, hetero=True)
+    ranks, o = _group(4, {"percentageOfNodesToScore": 10}, nodes, init)
+    _check(ranks, o, pods, chunk=150)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sampling_sharded_eval_and_subset(world):
+    """Evaluation output of a cut list (unprocessed nodes carry no status) and PreFilterResult subsets
+    that are themselves sampled, gathered over the ranks."""
+    from ksg.objects import PodW
+    rng, cfg, nodes, existing, names = rand_cluster(7300 + world, n_nodes=1000, n_existing=60)
+    ranks, o = _group(world, {"percentageOfNodesToScore": 12}, nodes, existing)
+    pods = []
+    for q in range(14):
+        sub = rng.sample(names, 400)
+        pods.append(PodW(f"s{q}", uid=f"s{q}").req({"cpu": "100m"}).node_affinity_required(
+            [{"matchFields": [{"key": "metadata.name", "operator": "In", "values": sub}]}]).obj())
+        pods.append(rand_pod(rng, q, names))
+    out = [[] for _ in ranks]
+    errs = []
+
+    def work(r):
+        try:
+            for p in pods:
+                res, ev = ranks[r].schedule_one(ranks[r].compile(p), assume=True, evaluate=True)
+                out[r].append((res.as_tuple(), ev))
+        except Exception as e:  # surfaced below
+            errs.append((r, e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    for q, p in enumerate(pods):
+        res, ev = o.schedule_one(o.compile(p), assume=True, evaluate=True)
+        for r in range(world):
+            assert out[r][q][0] == res.as_tuple(), f"rank {r} pod {q}"
+            assert out[r][q][1] == ev, f"rank {r} pod {q}: evaluation output differs"
+
+
 def test_preemption_on_sharded_ranks():
     """DefaultPreemption on a node-sharded group: each rank holds the whole mirror and runs the PostFilter
     over every node itself; every rank's choice equals the oracle's."""

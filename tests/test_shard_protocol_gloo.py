@@ -4,7 +4,8 @@ This is the CPU rehearsal of what k_xpack_a / k_select_shard / k_commit do aroun
 all-reduces: every rank owns a contiguous range of the snapshot order, publishes its feasible
 count (and the count before nextStartNodeIndex) in its own slot of a MAX-reduced vector, derives
 global feasible positions from the reduced slots, packs (TotalScore, heap pre-order key) for its
-nodes, and publishes its best (key, node); the winner is the max key over the ranks.  Checked
+nodes, and publishes its best (key, node); the winner is the max key over the ranks.  Also the
+percentageOfNodesToScore cut (k_sample_shard_a/b, (c) below).  Checked
 against (a) the oracle's container/heap root (ksgo_heap_root) on tie-heavy score lists with
 random rotations, and (b) the oracle's chosen node over a scheduling stream, whose TotalScores
 the oracle computes with the unsharded NormalizeScore maxima.
@@ -80,6 +81,41 @@ def sharded_select(feasible, totals, start, world, rank, blk):
     return xb[MAXS + w] - 1
 
 
+def sharded_cut(feasible, start, K, world, rank, blk):
+    """-> (this rank's kept nodes, processedNodes): k_sample_shard_a/b's protocol.  XS slots carry
+    every rank's feasible count and its count before the rotation start; the kept global feasible
+    ranks [below, below + K) mod F become at most two node intervals of this rank; the rank holding
+    the (K+1)-th feasible node publishes processedNodes + 1 (XA_PROC, MAX-reduced)."""
+    n = len(feasible)
+    lo, hi = shard(n, world, rank, blk)
+    mine = [i for i in range(lo, hi) if feasible[i]]
+    xs = [0] * (2 * MAXS)
+    xs[rank] = len(mine)
+    xs[MAXS + rank] = sum(1 for i in mine if i < start)
+    xs = allreduce_max(xs)
+    F = sum(xs[:world])
+    below = sum(xs[MAXS:MAXS + world])
+    P = sum(xs[:rank])
+    c = len(mine)
+    proc_word = 0
+    if F <= K:
+        kept = set(mine)
+    else:
+        gE = (below + K) % F
+        if P <= gE < P + c:
+            end = mine[gE - P]
+            proc_word = (end - start + n) % n + 1
+        kept = set()
+        for a, e in ((below, min(below + K, F)), (0, max(0, below + K - F))):
+            a, e = max(a, P), min(e, P + c)
+            if a < e:
+                i0, i1 = mine[a - P], mine[e - 1 - P] + 1
+                kept |= {i for i in mine if i0 <= i < i1}
+    proc_word = allreduce_max([proc_word])[0]
+    processed = proc_word - 1 if proc_word else n
+    return kept, processed
+
+
 def _heap_root(lib, scores):
     arr = (C.c_int64 * len(scores))(*scores)
     return lib.ksgo_heap_root(arr, len(scores))
@@ -107,6 +143,27 @@ def _worker(rank, world, port, seed, q):
             order = [i for i in list(range(start, n)) + list(range(start)) if feasible[i]]
             want = order[_heap_root(lib, [totals[i] for i in order])] if order else -1
             assert got == want, (case, got, want)
+        # (c) the percentageOfNodesToScore cut: the first K feasible nodes of the rotated order and
+        # processedNodes = the rotated position of the (K+1)-th (schedule_one.go:809-824,686-687)
+        for case in range(200):
+            n = rng.randint(1, 120)
+            feasible = [rng.random() < rng.choice([0.1, 0.5, 0.9]) for _ in range(n)]
+            start = rng.randrange(n)
+            K = rng.randint(1, n)
+            blk = rng.choice([1, 4, 16])
+            kept, processed = sharded_cut(feasible, start, K, world, rank, blk)
+            order = [i for i in list(range(start, n)) + list(range(start))]
+            want, seen, want_proc = set(), 0, n
+            for pos, i in enumerate(order):
+                if feasible[i]:
+                    if seen == K:
+                        want_proc = pos
+                        break
+                    want.add(i)
+                    seen += 1
+            lo, hi = shard(n, world, rank, blk)
+            assert kept == {i for i in want if lo <= i < hi}, (case, sorted(kept), sorted(want))
+            assert processed == want_proc, (case, processed, want_proc)
         # (b) a scheduling stream: the oracle's TotalScores (unsharded normalisation), sharded argmax
         r2, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=700, n_existing=60)
         o = oracle(cfg)
