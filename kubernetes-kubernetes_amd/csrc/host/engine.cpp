@@ -1206,7 +1206,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   std::vector<int32_t> pre_slot;
   if (pipe && assume) {
     pre_slot.resize(n);
+    const auto Tr = clk::now();
     for (int i = 0; i < n; ++i) pre_slot[i] = c->pod_table_put(*pods[i], -1);
+    reserve_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tr).count();
   }
   std::vector<CompiledPod> cp(n);
   int compiled = 0;
@@ -1395,8 +1397,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                 *std::max_element(nt.begin(), nt.end()) + own <= kAggTerms;
     }
   }
-  struct LoopRun { int first, count; double bytes; bool agg; };
+  struct LoopRun { int first, count; double bytes; bool agg, timed; };
   std::vector<LoopRun> runs;
+  // loopTimingStride k: every k-th loop launch carries HIP events on its dispatch packet (0: none)
+  auto loop_timed = [&](size_t r) { return c->cfg.loop_timing_stride > 0 && r % (size_t)c->cfg.loop_timing_stride == 0; };
   if (use_agg && (rc = ensure(d_agran, (size_t)kLoopMaxPods * 256 * kAGran * 8))) return rc;
   if (use_loop || use_agg) {
     if (use_loop && (rc = gran_setup())) return rc;
@@ -1583,8 +1587,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         c->err = comm->err;
         return KSG_EDEVICE;
       }
-      HIPCHK(launch_sched_loop(m, bv, lv, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
-      runs.push_back({i, j - i, rb, false});
+      const bool tl = loop_timed(runs.size());
+      HIPCHK(launch_sched_loop(m, bv, lv, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr));
+      runs.push_back({i, j - i, rb, false, tl});
       launches += j - i;
       i = j;
       continue;
@@ -1634,8 +1639,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       av.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)i * kAggStamps : nullptr;
       av.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)n * kAggStamps + (size_t)i * G * 4
                                       : nullptr;
-      HIPCHK(launch_agg_loop(m, bv, av, s, lev[2 * runs.size()], lev[2 * runs.size() + 1]));
-      runs.push_back({i, j - i, rb, true});
+      const bool tl = loop_timed(runs.size());
+      HIPCHK(launch_agg_loop(m, bv, av, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr));
+      runs.push_back({i, j - i, rb, true, tl});
       launches += j - i;
       i = j;
       continue;
@@ -1730,19 +1736,22 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   last_kernel = 0;
   if (!runs.empty()) {  // a loop dominates: per-pod time inside k_sched_loop / k_agg_loop and bytes per pod
     double lms[2] = {0, 0}, lb[2] = {0, 0};
-    int lp[2] = {0, 0};
+    int lp[2] = {0, 0}, tp[2] = {0, 0};
     for (size_t r = 0; r < runs.size(); ++r) {
-      float x = 0;
-      HIPCHK(hipEventElapsedTime(&x, lev[2 * r], lev[2 * r + 1]));
       const int k = runs[r].agg ? 1 : 0;
-      lms[k] += x;
+      if (runs[r].timed) {
+        float x = 0;
+        HIPCHK(hipEventElapsedTime(&x, lev[2 * r], lev[2 * r + 1]));
+        lms[k] += x;
+        tp[k] += runs[r].count;
+      }
       lb[k] += runs[r].bytes;
       lp[k] += runs[r].count;
     }
     const int k = lp[1] > lp[0] ? 1 : 0;
     if (lp[k] * 2 >= launches) {
       last_kernel = 1 + k;
-      last_kernel_ms = lms[k] / lp[k];
+      last_kernel_ms = tp[k] ? lms[k] / tp[k] : 0.0;  // per pod over the timed launches
       last_bytes = lb[k] / lp[k];
     }
     if (c->cfg.loop_stamps) {  // mean per-phase time (us) of the looped pods, workgroup 0's view
@@ -1964,8 +1973,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (c->cfg.loop_stamps) {
     const auto T4 = clk::now();
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    std::fprintf(stderr, "[host, us per pod] compile %.3f  stage+launch %.3f  wait %.3f  results+assume %.3f\n",
-                 us(T0, T1) / n, us(T1, T2) / n, us(T2, T3) / n, us(T3, T4) / n);
+    std::fprintf(stderr, "[host, us per pod] compile %.3f  stage+launch %.3f  wait %.3f  results+assume %.3f | "
+                 "batch: chunk-0 compile %.1f us (slot reservation %.1f us), settle after the wait %.1f us\n",
+                 us(T0, T1) / n, us(T1, T2) / n, us(T2, T3) / n, us(T3, T4) / n, us(T0, T1), reserve_us_, us(T3, T4));
+    reserve_us_ = 0;
     std::fprintf(stderr, "[compile sections, us per pod] node-affinity %.3f  taints+ports %.3f  resources+images %.3f  "
                  "topology %.3f (spread %.3f  affinity %.3f  placement+tables %.3f)  masks+assume %.3f\n", cprof_[0] / n,
                  cprof_[1] / n, cprof_[2] / n, cprof_[3] / n, cprof_[5] / n, cprof_[6] / n, cprof_[7] / n, cprof_[4] / n);

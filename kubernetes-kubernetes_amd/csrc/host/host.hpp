@@ -151,6 +151,7 @@ struct Config {
   bool has_added_pref = false;
   std::vector<std::pair<int32_t, NSTerm>> added_pref;
   int device = 0;
+  int loop_timing_stride = 1;  // time every k-th persistent-loop launch with HIP events (0: none)
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
@@ -434,6 +435,7 @@ class Engine {
   int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
               const uint8_t* node_list = nullptr);
   double cprof_[8] = {};  // loopStamps: compile time per section (us), reported with the host line
+  double reserve_us_ = 0;   // loopStamps: the batch's pod-table slot reservation (us)
   int compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* B, PodDesc* D, uint32_t* fmask,
                        uint32_t* smask, CompiledPod* out);
   // run a batch of cycles (device-resident, sequential semantics)

@@ -558,6 +558,7 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     if (const JVal* fg = d.get(r, "featureGates")) c->taint_cmp_ops = d.boolean(*fg, "TaintTolerationComparisonOperators");
     c->device = (int)d.num(r, "device", 0);
     c->timing_stride = (int)d.num(r, "kernelTimingStride", 0);
+    c->loop_timing_stride = (int)d.num(r, "loopTimingStride", 1);
     if (const JVal* pl = d.get(r, "persistentLoop")) c->persistent_loop = pl->type == JVal::BOOL && pl->b;
     c->loop_wg = (int)d.num(r, "loopWorkgroups", 0);
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
