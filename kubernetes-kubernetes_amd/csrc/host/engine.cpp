@@ -1244,9 +1244,19 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
   }
   const auto T1 = clk::now();
-  bool pods_needed = eval != nullptr || compiled < n;  // later chunks are compiled after the first launch
+  bool pods_needed = eval != nullptr;
   for (int i = 0; i < compiled && !pods_needed; ++i)
     pods_needed = (reinterpret_cast<const PodDesc*>(cp[i].blob.data())->flags & DF_AGGREGATE) != 0;
+  // Later chunks are compiled after the first launch, so the table goes up now if any of their pods
+  // may read it: a superset of compile_topology's DF_AGGREGATE test (own spread constraints or
+  // affinity terms, or existing pods' terms that InterPodAffinity filters / scores every pod with;
+  // the batch's own pods' terms are already in the key tables, reserved above).  A node-local stream
+  // then skips re-uploading a pod table that grows with every batch.
+  if (!pods_needed && compiled < n) {
+    const bool existing_terms = !c->exanti_keys.empty() || !c->score_keys_req.empty() || !c->score_keys_pref.empty();
+    for (int i = compiled; i < n && !pods_needed; ++i)
+      pods_needed = existing_terms || !pods[i]->spreads.empty() || pods[i]->has_pod_affinity || pods[i]->has_pod_anti;
+  }
   if ((rc = c->ensure_mirror(pods_needed))) return rc;
   // ---- staging: [offsets n | program sizes n | PodStats n | DevResult n | give-up flags n | programs]
   // in pinned memory; each chunk's programs, offsets and stats go up in their own H2D copies
@@ -1438,7 +1448,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     return KSG_OK;
   };
   // results + host shadow of the device-side assumes for pods [a, b)
+  double settle_us = 0;  // loopStamps: host time spent mirroring results into the cache
   auto settle = [&](int a, int b) -> int {
+    const auto Ts = clk::now();
+    struct Acc {
+      double* t; clk::time_point s;
+      ~Acc() { *t += std::chrono::duration<double, std::micro>(clk::now() - s).count(); }
+    } acc_{&settle_us, Ts};
     for (int i = a; i < b; ++i) {
       ksg_result& r = results[i];
       if (cp[i].error) {
@@ -1529,13 +1545,14 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       need += cp[j].blob.size();
       aw = std::max(aw, cp[j].arena_words);
     }
-    if (c->layout_dirty || c->pods_dirty || o + need > desc_cap || aw > arena_words) {
+    // (a stale pod table matters only to a batch with pods that read it: pods_needed)
+    if (c->layout_dirty || (c->pods_dirty && pods_needed) || o + need > desc_cap || aw > arena_words) {
       // the mirror must be re-laid out or the buffers grown: drain the device and mirror what it
       // assumed first (the same state a batch boundary here would give)
       if ((r2 = drain())) return r2;
       if (c->cfg.loop_stamps)
         std::fprintf(stderr, "[host] pipeline drained before pod %d (%s)\n", i,
-                     c->layout_dirty || c->pods_dirty ? "mirror re-layout" : "staging grown");
+                     c->layout_dirty || (c->pods_dirty && pods_needed) ? "mirror re-layout" : "staging grown");
       if ((r2 = settle_closed())) return r2;
       if ((r2 = c->ensure_mirror())) return r2;
       arena_words = std::max(arena_words, aw);
@@ -1701,11 +1718,20 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       HIPCHK(hipMemcpyAsync(tot.data(), d_total.p, (size_t)m.n * 8, hipMemcpyDeviceToHost, s));
     }
   }
+  std::string chunk_log;  // loopStamps: per chunk, the host's wait for its results and its settle (us)
   if (chunks.size() > 1)  // pipelined: settle each chunk as soon as its results have landed
     for (size_t k = (size_t)settled; k < chunks.size(); ++k) {
+      const auto Tw = clk::now();
+      const double s0 = settle_us;
       HIPCHK(hipEventSynchronize(cev[k]));
+      const double wt = std::chrono::duration<double, std::micro>(clk::now() - Tw).count();
       if ((use_loop || use_agg) && hfail[k]) return loop_fault(chunks[k].a, fault_detail());
       if ((rc = settle(chunks[k].a, chunks[k].b))) return rc;
+      if (c->cfg.loop_stamps) {
+        char buf[96];
+        std::snprintf(buf, sizeof buf, " [%d pods: wait %.1f settle %.1f]", chunks[k].b - chunks[k].a, wt, settle_us - s0);
+        chunk_log += buf;
+      }
     }
   HIPCHK(hipStreamSynchronize(s));
   if (copy_stream) HIPCHK(hipStreamSynchronize(cstream));
@@ -1973,6 +1999,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (c->cfg.loop_stamps) {
     const auto T4 = clk::now();
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    std::fprintf(stderr, "[host chunks]%s  settle total %.1f us\n", chunk_log.c_str(), settle_us);
     std::fprintf(stderr, "[host, us per pod] compile %.3f  stage+launch %.3f  wait %.3f  results+assume %.3f | "
                  "batch: chunk-0 compile %.1f us (slot reservation %.1f us), settle after the wait %.1f us\n",
                  us(T0, T1) / n, us(T1, T2) / n, us(T2, T3) / n, us(T3, T4) / n, us(T0, T1), reserve_us_, us(T3, T4));

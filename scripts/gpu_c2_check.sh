@@ -1,0 +1,14 @@
+#!/bin/bash
+# Full GPU parity suite, then C2 / C3 / C5 bench lines and the C2 host probe.  Each GPU step has its
+# own time limit; a crash/timeout (rc > 1) ends the script.
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || exit $rc
+}
+step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider
+step bench_c2 300 python bench.py --steps 10 --warmup 2 --cpu-seconds 5
+step bench_c3 400 python bench.py --workload c3 --steps 3 --warmup 1 --cpu-seconds 5
+step host_probe 300 python -u scripts/c2_host_probe.py
