@@ -475,7 +475,7 @@ struct LoopView {
   const uint32_t* desc_bytes;  // [batch pods] program sizes (indexed like BatchView::desc_off)
   unsigned long long* wstamps;  // diagnostic: [npods][nwg][8] exchange / owner times (nullptr)
   int32_t give_up_at;        // diagnostic: every workgroup gives up at this pod of the run (-1: never)
-  int32_t pad_;
+  int32_t wave_map;          // which hardware wave plays which role (k_sched_loop kWaveMap; 0: identity)
 };
 // exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
 // A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)

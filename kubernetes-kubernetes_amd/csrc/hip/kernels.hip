@@ -1727,6 +1727,11 @@ __device__ __forceinline__ bool post_ok(const PodDesc& d, const PodDesc& nd) {
 
 constexpr int kLoopThreads = kBlock + 128;  // four evaluation waves, one selection wave, one helper wave
 
+// Role of each hardware wave of a k_sched_loop workgroup (roles: 0-3 evaluation, 4 selection, 5 helper).
+// A workgroup's waves go to the CU's four SIMDs round robin, so waves w and w + 4 share a SIMD:
+// map 0 pairs the selection wave with evaluation wave 0, map 1 with the helper, map 2 runs it alone
+// (two evaluation waves then share a SIMD).
+__constant__ int8_t kWaveMap[3][kLoopThreads / 64] = {{0, 1, 2, 3, 4, 5}, {4, 0, 1, 2, 5, 3}, {0, 1, 4, 3, 5, 2}};
 __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
@@ -1757,12 +1762,14 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   const int gid = lv.rank * G + w, P = lv.world * G;  // my participant index, participants (rank-major)
   const int k0 = lv.blk0 + (int)((int64_t)lv.nblk * w / G), k1 = lv.blk0 + (int)((int64_t)lv.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)kWaveMap[lv.wave_map][threadIdx.x >> 6]);  // my role
+  const int vt = wave * 64 + lane;           // my thread index in role order
   const bool sel = wave == kBlock / 64;      // the selection wave: exchanges + phase 2
   const bool hlp = wave == kBlock / 64 + 1;  // the helper wave: candidate pre-evaluation + staging
-  const int t = (int)threadIdx.x;          // evaluation waves: my slot in each block of my range
+  const int t = vt;                          // evaluation waves: my slot in each block of my range
   auto stamp_s = [&](int q, int k) {       // diagnostic phase stamps: WG 0's selection lane 0
-    if (lv.stamps && w == 0 && threadIdx.x == kBlock) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    if (lv.stamps && w == 0 && vt == kBlock) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
 
   if (t < kBlock) {  // evaluation waves
@@ -1927,7 +1934,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     if (lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
   };
 
-  for (int k = (int)threadIdx.x; k < lv.npods; k += kLoopThreads) {
+  for (int k = vt; k < lv.npods; k += kLoopThreads) {
     s_off[k] = b.desc_off[lv.first_pod + k];
     s_len[k] = lv.desc_bytes[lv.first_pod + k];
   }
@@ -1944,7 +1951,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   __syncthreads();
   if (t < kBlock && lv.npods > 0) phase1(lv.first_pod, 0, 0, nullptr);
   __syncthreads();
-  if (threadIdx.x == kBlock && lv.npods > 0) publish_a(0, 0);
+  if (vt == kBlock && lv.npods > 0) publish_a(0, 0);
 
   for (int q = 0; q < lv.npods; ++q) {
     if (q == lv.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)

@@ -1598,6 +1598,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       lv.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)i * 8 : nullptr;
       lv.desc_bytes = (const uint32_t*)d_off.p + n;
       lv.give_up_at = c->cfg.debug_give_up_at;
+      lv.wave_map = c->cfg.loop_wave_map;
       lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr;
       // in-process ranks: every rank is past its allocations before any rank's first loop starts
       if (runs.empty() && comm && comm->launch_gate()) {

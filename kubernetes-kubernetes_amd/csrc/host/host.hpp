@@ -156,6 +156,7 @@ struct Config {
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int agg_debug = 0;            // AggView::debug (diagnostic)
+  int loop_wave_map = 0;        // k_sched_loop role-to-wave placement (kWaveMap in kernels.hip)
   int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
   // sharded: the loop's per-pod exchange device-to-device (granules over xGMI).  Default on for RCCL

@@ -564,6 +564,8 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
     c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);
     c->debug_give_up_at = (int)d.num(r, "debugLoopGiveUpAt", -1);
+    c->loop_wave_map = (int)d.num(r, "loopWaveMap", 0);
+    if (c->loop_wave_map < 0 || c->loop_wave_map > 2) c->loop_wave_map = 0;
     if (const JVal* dx = d.get(r, "deviceExchange")) c->dev_exchange = dx->type == JVal::BOOL && dx->b ? 1 : 0;
     c->loop_stamps = d.boolean(r, "loopStamps");
     if (const JVal* ds = d.get(r, "distributed")) {  // node-sharded evaluation

@@ -34,6 +34,13 @@ def run(cfg, label):
     s.close()
 
 
+if sys.argv[1:] == ["wavemap"]:
+    for rep in range(2):
+        for wm in (0, 1, 2):
+            run({"loopWaveMap": wm}, f"loopWaveMap {wm}")
+    for wm in (0, 1, 2):
+        run({"loopWaveMap": wm, "loopStamps": True}, f"loopWaveMap {wm} stamps")
+    sys.exit(0)
 if sys.argv[1:] != ["stamps"]:
     run({"loopTimingStride": 1}, "events on every loop launch")
     run({"loopTimingStride": 0}, "no loop events")

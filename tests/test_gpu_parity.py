@@ -233,6 +233,27 @@ def test_persistent_loop_geometries(native, wg):
             assert rs[k].as_tuple() == ro.as_tuple(), f"wg {wg} hetero {hetero} pod {k}"
 
 
+@pytest.mark.parametrize("wave_map", [1, 2])
+def test_persistent_loop_wave_maps(native, wave_map):
+    """k_sched_loop with its roles on other hardware waves (loopWaveMap): the same results as the
+    oracle on heterogeneous and all-tied clusters and on a random mixed stream."""
+    from ksg.synth import scheduling_basic
+    for hetero, n_nodes in ((True, 3000), (False, 1500)):
+        nodes, init, pods = scheduling_basic(n_nodes, 300, 300, hetero=hetero)
+        g, o = _pair(native, {"loopWaveMap": wave_map}, nodes, init)
+        rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+        for k, p in enumerate(pods):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[k].as_tuple() == ro.as_tuple(), f"map {wave_map} hetero {hetero} pod {k}"
+    rng, cfg, nodes, existing, names = rand_cluster(5100 + wave_map, n_nodes=800, n_existing=80)
+    g, o = _pair(native, dict(cfg, loopWaveMap=wave_map), nodes, existing)
+    pods = [rand_pod(rng, k, names) for k in range(120)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"map {wave_map} mixed pod {k}"
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_persistent_loop_mixed_runs(native, seed):
     """Random pods: runs of node-local pods go through k_sched_loop, PTS/IPA pods through the
