@@ -209,6 +209,14 @@ def test_sampling_sharded_basic_rotation():
     _check(ranks, o, pods, chunk=150)
 
 
+def test_sampling_sharded_with_empty_shard():
+    """400 nodes (two 256-node blocks) on W = 3: one rank holds no node; the cut's counts, intervals
+    and processedNodes still agree on every rank."""
+    rng, cfg, nodes, existing, names = rand_cluster(7400, n_nodes=400, n_existing=40)
+    ranks, o = _group(3, dict(cfg, percentageOfNodesToScore=30), nodes, existing)
+    _check(ranks, o, [rand_pod(rng, q, names) for q in range(60)], chunk=20)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sampling_sharded_eval_and_subset(world):
     """Evaluation output of a cut list (unprocessed nodes carry no status) and PreFilterResult subsets
