@@ -427,8 +427,8 @@ class Engine {
   explicit Engine(Cluster* c);
   ~Engine();
   Cluster* c;
-  std::map<int32_t, PodSpec> queue;
-  std::map<int32_t, std::string> assumed;  // handle -> uid
+  std::unordered_map<int32_t, PodSpec> queue;  // handle -> compiled-for-API pod (find / insert / erase only)
+  std::unordered_map<int32_t, std::string> assumed;  // handle -> uid
   int32_t next_handle = 1;
 
   enum Mode { CYCLE, FILTER_ONE, SCORE_ONE };
