@@ -198,6 +198,7 @@ int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* r
 int ksg_schedule_batch(ksg_ctx* ctx, const int32_t* handles, int32_t n, uint32_t flags, ksg_result* results) {
   if (!ctx || n < 0 || (n && (!handles || !results))) return KSG_EINVAL;
   GUARD({
+    ctx->engine->api_t0_ = std::chrono::steady_clock::now();  // loopStamps: the handle lookups' share
     std::vector<const PodSpec*> pods;
     std::vector<int32_t> hs(handles, handles + n);
     pods.reserve((size_t)n);

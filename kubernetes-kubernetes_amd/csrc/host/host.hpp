@@ -16,6 +16,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <chrono>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -436,6 +437,7 @@ class Engine {
   int compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool eval, CompiledPod* out,
               const uint8_t* node_list = nullptr);
   double cprof_[8] = {};  // loopStamps: compile time per section (us), reported with the host line
+  std::chrono::steady_clock::time_point api_t0_{};  // loopStamps: ksg_schedule_batch entry
   double reserve_us_ = 0;   // loopStamps: the batch's pod-table slot reservation (us)
   int compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* B, PodDesc* D, uint32_t* fmask,
                        uint32_t* smask, CompiledPod* out);
