@@ -157,6 +157,7 @@ struct Config {
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int agg_debug = 0;            // AggView::debug (diagnostic)
+  int first_chunk = 32;         // pods in a pipelined batch's first chunk (the host work before the first launch)
   int loop_wave_map = 0;        // k_sched_loop role-to-wave placement (kWaveMap in kernels.hip)
   int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))

@@ -565,6 +565,7 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);
     c->debug_give_up_at = (int)d.num(r, "debugLoopGiveUpAt", -1);
     c->loop_wave_map = (int)d.num(r, "loopWaveMap", 0);
+    c->first_chunk = std::max(8, std::min(256, (int)d.num(r, "pipelineFirstChunk", 32)));
     if (c->loop_wave_map < 0 || c->loop_wave_map > 2) c->loop_wave_map = 0;
     if (const JVal* dx = d.get(r, "deviceExchange")) c->dev_exchange = dx->type == JVal::BOOL && dx->b ? 1 : 0;
     c->loop_stamps = d.boolean(r, "loopStamps");

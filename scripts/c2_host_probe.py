@@ -34,6 +34,11 @@ def run(cfg, label):
     s.close()
 
 
+if sys.argv[1:] == ["chunk"]:
+    for rep in range(2):
+        for fc in (64, 32, 16):
+            run({"pipelineFirstChunk": fc}, f"pipelineFirstChunk {fc}")
+    sys.exit(0)
 if sys.argv[1:] == ["wavemap"]:
     for rep in range(2):
         for wm in (0, 1, 2):
