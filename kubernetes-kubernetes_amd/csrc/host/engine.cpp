@@ -1259,7 +1259,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (int i = compiled; i < n && !pods_needed; ++i)
       pods_needed = existing_terms || !pods[i]->spreads.empty() || pods[i]->has_pod_affinity || pods[i]->has_pod_anti;
   }
+  const auto Tm = clk::now();
   if ((rc = c->ensure_mirror(pods_needed))) return rc;
+  mirror_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tm).count();
   // ---- staging: [offsets n | program sizes n | PodStats n | DevResult n | give-up flags n | programs]
   // in pinned memory; each chunk's programs, offsets and stats go up in their own H2D copies
   size_t desc_bytes = 0;
@@ -2004,10 +2006,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     std::fprintf(stderr, "[host chunks]%s  settle total %.1f us\n", chunk_log.c_str(), settle_us);
     std::fprintf(stderr, "[host, us per pod] compile %.3f  stage+launch %.3f  wait %.3f  results+assume %.3f | "
-                 "batch: API entry -> run %.1f us, chunk-0 compile %.1f us (slot reservation %.1f us), settle after the wait "
-                 "%.1f us\n",
+                 "batch: API entry -> run %.1f us, chunk-0 compile %.1f us (slot reservation %.1f us), mirror + pod "
+                 "table before the first launch %.1f us, settle after the wait %.1f us\n",
                  us(T0, T1) / n, us(T1, T2) / n, us(T2, T3) / n, us(T3, T4) / n,
-                 api_t0_.time_since_epoch().count() ? us(api_t0_, T0) : 0.0, us(T0, T1), reserve_us_, us(T3, T4));
+                 api_t0_.time_since_epoch().count() ? us(api_t0_, T0) : 0.0, us(T0, T1), reserve_us_, mirror_us_,
+                 us(T3, T4));
     reserve_us_ = 0;
     std::fprintf(stderr, "[compile sections, us per pod] node-affinity %.3f  taints+ports %.3f  resources+images %.3f  "
                  "topology %.3f (spread %.3f  affinity %.3f  placement+tables %.3f)  masks+assume %.3f\n", cprof_[0] / n,

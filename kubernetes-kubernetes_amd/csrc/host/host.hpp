@@ -439,7 +439,8 @@ class Engine {
               const uint8_t* node_list = nullptr);
   double cprof_[8] = {};  // loopStamps: compile time per section (us), reported with the host line
   std::chrono::steady_clock::time_point api_t0_{};  // loopStamps: ksg_schedule_batch entry
-  double reserve_us_ = 0;   // loopStamps: the batch's pod-table slot reservation (us)
+  double reserve_us_ = 0;
+  double mirror_us_ = 0;    // loopStamps: ensure_mirror before the batch's first launch (us)   // loopStamps: the batch's pod-table slot reservation (us)
   int compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* B, PodDesc* D, uint32_t* fmask,
                        uint32_t* smask, CompiledPod* out);
   // run a batch of cycles (device-resident, sequential semantics)
