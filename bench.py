@@ -81,6 +81,8 @@ WORKLOADS = {
     "c4-anti": ("PreferredPodAntiAffinity", 15000, 15000, 3),
     "c5": ("Mixed 100k-node cluster (50% default, 10% each node-affinity / pod-affinity / anti-affinity / "
            "preferred anti-affinity / zone spread)", 100000, 10000, 4),
+    "dts": ("DefaultTopologySpreading (pods selected by a Service: PodTopologySpread system default "
+            "constraints)", 5000, 5000, None),
 }
 
 
@@ -107,7 +109,7 @@ def usable_cpus():
     return n
 
 
-def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100):
+def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=()):
     """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
     Filter / Score loops over nodes on a pool of that many threads (the reference's
     Parallelizer.Until with parallelism 16), results identical to the sequential oracle
@@ -118,6 +120,8 @@ def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100):
     if pct != 100:  # the cut filter pass runs sequentially in the oracle (its Score loop stays parallel)
         cfg["percentageOfNodesToScore"] = pct
     o = oracle(cfg)
+    for ob in objects:
+        o.upsert_object(ob)
     for n in nodes:
         o.add_node(n)
     for p in init:
@@ -166,6 +170,7 @@ def main():
     n_init = (a.init_pods if a.init_pods is not None else d_init) * grow
     n_meas = a.steps * a.batch
     n_warm = max(a.warmup, 1 if sharded else 0) * a.batch
+    objects = []
     if a.workload in ("c2", "c2-hetero"):
         nodes, init, pods = synth.scheduling_basic(n_nodes, n_init, n_warm + n_meas, hetero=a.workload == "c2-hetero")
     elif a.workload == "c3":
@@ -174,6 +179,8 @@ def main():
         nodes, init, pods = synth.scheduling_pod_affinity(n_nodes, n_init, n_warm + n_meas)
     elif c5:
         nodes, init, pods = synth.mixed_cluster(n_nodes, n_init, n_warm + n_meas)
+    elif a.workload == "dts":
+        nodes, init, pods, objects = synth.default_topology_spreading(n_nodes, n_init, n_warm + n_meas)
     else:
         nodes, init, pods = synth.topology_spreading(n_nodes, n_init, n_warm + n_meas,
                                                      preferred_anti=a.workload == "c4-anti")
@@ -192,6 +199,8 @@ def main():
             cfg["distributed"] = {"worldSize": world, "rank": rank, "ncclId": obj[0]}
             cfg["deviceExchange"] = dev_exchange
         s = Scheduler(cfg)
+        for ob in objects:
+            s.upsert_object(ob)
         for n in nodes:
             s.add_node(n)
         for p in init:
@@ -274,15 +283,16 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             # the reference's default parallelism (16 goroutines over nodes), then one thread
             v, done, cdt, ores = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads,
-                                              pct=a.pct)
-            v1, done1, cdt1, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct)
+                                              pct=a.pct, objects=objects)
+            v1, done1, cdt1, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct,
+                                              objects=objects)
             # every CPU the process may use (affinity mask and cgroup quota)
             ncpu = usable_cpus()
             if ncpu == a.cpu_threads:
                 va, donea, cdta = v, done, cdt
             else:
                 va, donea, cdta, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=ncpu,
-                                                  pct=a.pct)
+                                                  pct=a.pct, objects=objects)
             cpu = {"value": round(v, 2), "unit": "pods/s", "cores": a.cpu_threads, "kind": "port",
                    "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
@@ -323,7 +333,7 @@ def main():
             "dtype": "int64",
             "data": "synthetic (scheduler_perf node-default / pod-default templates, seeded)",
             "config": {"workload": f"{wname} {n_nodes} nodes / {n_init} init pods / "
-                                   f"{n_meas} measured pods" + ("" if sharded else " per GPU")
+                                   f"{n_meas} measured pods" + ("" if sharded or world == 1 else " per GPU")
                                    + (f" (BASELINE configs[{cfg_ix}])" if cfg_ix is not None else ""),
                        "nodes": n_nodes, "pods_per_step": a.batch, "percentageOfNodesToScore": a.pct,
                        "plugins": "default",

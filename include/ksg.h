@@ -127,6 +127,8 @@ typedef struct ksg_eval_out {
  *    "balancedAllocation": {"resources": [...]},
  *    "interPodAffinity": {"hardPodAffinityWeight": 1, "ignorePreferredTermsOfExistingPods": false},
  *    "nodeAffinity": {"addedAffinity": <v1.NodeAffinity>},
+ *    "podTopologySpread": {"defaultingType": "System" | "List",     (PodTopologySpreadArgs)
+ *                          "defaultConstraints": [<v1.TopologySpreadConstraint without labelSelector>]},
  *    "device": 0, "distributed": {"worldSize": 1, "rank": 0, "ncclId": "<hex>"}}
  * Absent keys take the upstream defaults.  Returns NULL on failure (ksg_create_error()). */
 ksg_ctx *ksg_create(const char *config_json, size_t len);
@@ -138,6 +140,16 @@ const char *ksg_last_error(const ksg_ctx *ctx);
  * (backend/cache/cache.go:515-695, eventhandlers.go:51-412).  Snapshot node order is
  * the nodeTree zone round-robin order (node_tree.go:119-143). */
 int ksg_upsert_namespace(ksg_ctx *ctx, const char *ns_json, size_t len);
+/* The listers PodTopologySpread's default constraints read (podtopologyspread/plugin.go:145-150,
+ * helper.DefaultSelector in plugins/helper/spread.go:37-95): a v1 Service or ReplicationController,
+ * or an apps/v1 ReplicaSet or StatefulSet, as JSON (kind, metadata.namespace/name, spec.selector).
+ * Upsert replaces the object of that kind, namespace and name; remove takes the kind name
+ * ("Service", "ReplicationController", "ReplicaSet", "StatefulSet").  A pod without constraints of
+ * its own then gets the profile's default constraints (System: kubernetes.io/hostname maxSkew 3 and
+ * topology.kubernetes.io/zone maxSkew 5, ScheduleAnyway) with the merged selector of the objects that
+ * select it (common.go:59-75). */
+int ksg_upsert_object(ksg_ctx *ctx, const char *obj_json, size_t len);
+int ksg_remove_object(ksg_ctx *ctx, const char *kind, const char *ns, const char *name);
 int ksg_add_node(ksg_ctx *ctx, const char *node_json, size_t len);
 int ksg_update_node(ksg_ctx *ctx, const char *node_json, size_t len);
 int ksg_remove_node(ksg_ctx *ctx, const char *name);
@@ -147,7 +159,12 @@ int ksg_num_nodes(const ksg_ctx *ctx);
 /* name of the node at snapshot index `index`; returns its length or a KSG_E* code */
 int ksg_node_name(const ksg_ctx *ctx, int32_t index, char *buf, size_t cap);
 
-/* ---- pods to schedule: compiled once, like PodInfo creation (framework/types.go:1183) */
+/* ---- pods to schedule: compiled once, like PodInfo creation (framework/types.go:1183).
+ * KSG_ENOTSUP: the pod needs a plugin outside the device path -- a PersistentVolumeClaim, generic
+ * ephemeral, CSI-migratable in-tree (GCE PD, AWS EBS, Cinder, Azure Disk/File, vSphere, Portworx), RBD
+ * or iSCSI volume (VolumeBinding, VolumeZone, NodeVolumeLimits, VolumeRestrictions) or
+ * spec.resourceClaims (DynamicResources).  The context is unaffected; such pods stay with the
+ * caller's own scheduling path. */
 int ksg_pod_compile(ksg_ctx *ctx, const char *pod_json, size_t len, int32_t *handle);
 int ksg_pod_release(ksg_ctx *ctx, int32_t handle);
 

@@ -21,8 +21,8 @@ namespace ksg {
 
 constexpr int kNumPlugins = 10;  // KSG_NUM_PLUGINS
 constexpr int kBlock = 256;      // threads per block of the per-node kernels (4 waves)
-constexpr int kMaxScalar = 16;   // interned extended/scalar resource columns
-constexpr int kPortSlots = 8;    // used-port slots per node (grown by the host if exceeded)
+constexpr int kMaxScalar = 16;   // minimum extended/scalar resource columns (MirrorView::scalar_cols grows)
+constexpr int kPortSlots = 8;    // minimum used-port slots per node (MirrorView::port_slots grows with the cluster)
 constexpr int kMaxCons = 32;      // PodTopologySpread constraints per kind per pod (eligibility is a 32-bit mask)
 constexpr int kMaxPodTerms = 64;  // InterPodAffinity terms per kind per pod
 constexpr int kAggMaxCons = 8;    // k_agg_loop: constraints / terms per kind of a looped pod (LDS minima, the
@@ -102,7 +102,9 @@ struct PtsCons {
   int32_t nvals;        // domains (label values of the key)
   int32_t lref;         // k_agg_loop: where hist_base's counts live (AggRef)
   int32_t pref;         // k_agg_loop: where pres_base's flags live (AggRef; unused for node-local keys)
-  int32_t pad[3];
+  int32_t absent;       // DF_PTS_ANYTOPO score constraints: the domain of a node without the key (the ""
+                        // value's id, or an extra entry past the values), -1 otherwise
+  int32_t pad[2];
 };
 // an InterPodAffinity term of the incoming pod (interpodaffinity/filtering.go:246-283, scoring.go:81-125)
 struct IpaTerm {
@@ -160,6 +162,9 @@ enum DescFlags : uint32_t {
   DF_LFAST = 1u << 18,             // DF_FAST's shape for the node-local plugins (k_agg_loop: eval_core_fast + the
                                    // PodTopologySpread / InterPodAffinity filters and score after it)
   DF_TERMINATING = 1u << 19,       // the pod has a deletionTimestamp (its pod-table slot's flag)
+  DF_PTS_ANYTOPO = 1u << 20,       // PodTopologySpread scores with system-default constraints: requireAllTopologies
+                                   // is false (podtopologyspread/scoring.go:141-144), no node is ignored and a node
+                                   // without a constraint's key is in its "" domain (PtsCons::absent)
 };
 
 struct PodDesc {
@@ -357,14 +362,14 @@ struct MirrorView {
   const int64_t* alloc_eph;
   const int32_t* alloc_pods;
   const uint32_t* flags;          // bit0 unschedulable
-  const int64_t* scalar_alloc;    // [kMaxScalar][cap]
+  const int64_t* scalar_alloc;    // [scalar_cols][cap]
   int64_t* req_cpu;
   int64_t* req_mem;
   int64_t* req_eph;
   int64_t* nz_cpu;
   int64_t* nz_mem;
   int32_t* num_pods;
-  int64_t* scalar_req;            // [kMaxScalar][cap]
+  int64_t* scalar_req;            // [scalar_cols][cap]
   const uint32_t* taint_off;      // [n+1]
   const uint32_t* taint_ids;
   const uint32_t* img_off;        // [n+1]
@@ -372,7 +377,7 @@ struct MirrorView {
   const int32_t* labels;          // [slots][cap] local value id, -1 absent
   const int64_t* label_num;       // [slots][cap] parsed integer value
   const uint8_t* label_num_ok;    // [slots][cap]
-  uint32_t* ports;                // [cap][kPortSlots] port id, 0xffffffff empty
+  uint32_t* ports;                // [cap][port_slots] port id, 0xffffffff empty
   // pod table (NodeInfo.Pods of every node, flattened; slots indexed by the host)
   int32_t pods_hw;                // slots in use (high-water mark)
   int32_t n_terms;                // term table entries in use
@@ -386,6 +391,8 @@ struct MirrorView {
   const int32_t* term_pool;       // their selector programs / namespace id lists
   const double* log_tab;          // go math.Log(k) for k in [0, log_n)
   int32_t log_n;
+  int32_t port_slots;             // `ports` row stride: >= every node's host ports + what a batch can assume
+  int32_t scalar_cols;            // scalar resource columns (>= the interned extended resources)
   int32_t pad_;
 };
 
@@ -439,16 +446,17 @@ struct NodeUpdate {
   int64_t alloc_cpu, alloc_mem, alloc_eph;
   int32_t alloc_pods;
   uint32_t flags;
-  int64_t scalar[kMaxScalar];
+  uint32_t sc_off, sc_cnt;          // the node's scalar allocatable in the flush's ScalarEntry pool
 };
 struct LabelEntry { int32_t slot, value; int64_t num; int32_t ok, pad; };
+struct ScalarEntry { int32_t slot, pad; int64_t value; };  // one non-zero scalar resource column of a node
 // One node's dynamic columns (NodeInfo.Requested / NonZeroRequested / len(Pods) / UsedPorts)
 // after pod events, flushed in bulk at the next cycle (Cluster::flush_node_dynamic -> k_node_dyn).
 struct NodeDyn {
   int32_t node, num_pods;
   int64_t req_cpu, req_mem, req_eph, nz_cpu, nz_mem;
-  int64_t scalar[kMaxScalar];
-  uint32_t ports[kPortSlots];
+  uint32_t sc_off, sc_cnt;      // the node's scalar requests in the flush's ScalarEntry pool
+  uint32_t port_off, port_cnt;  // the node's UsedPorts ids in the flush's id pool
 };
 
 struct ShardView {

@@ -73,11 +73,11 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
         }
         if (d.n_ptss) {  // processAllNode (scoring.go:155-189) + per-node hostname counts (:207-214)
           const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-          const uint32_t el = pts_eligible(m, base, d, cs, d.n_ptss, n);
+          const uint32_t el = pts_eligible(m, base, d, cs, d.n_ptss, n, (d.flags & DF_PTS_ANYTOPO) == 0);
           for (int32_t c = 0; c < d.n_ptss; ++c) {
             if (lsel_empty(sp + cs[c].sel) || !lsel_match(sp + cs[c].sel, pl, pn)) continue;
             if (cs[c].hostname) add(cs[c].hist_base + n, 1);
-            else if ((el >> c) & 1u) add(cs[c].hist_base + node_label(m, cs[c].slot, n), 1);
+            else if ((el >> c) & 1u) add(cs[c].hist_base + pts_domain(m, cs[c], n), 1);
           }
         }
       }
@@ -224,14 +224,13 @@ __global__ __launch_bounds__(kBlock) void k_pts_score(MirrorView m, BatchView b,
   int64_t raw = 0;
   if (i < m.n && ((b.fmask[(size_t)blk * (kBlock / 64) + wave] >> lane) & 1ull)) {
     const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-    bool ignored = false;
-    for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
-    if (ignored) {
+    if (pts_ignored(m, d, cs, i)) {
       raw = -1;
     } else {
       double score = 0.0;
       for (int32_t c = 0; c < d.n_ptss; ++c) {
         const int32_t v = node_label(m, cs[c].slot, i);
+        if (v < 0) continue;  // only keys the node carries score (scoring.go:213-222)
         long long cnt;
         int32_t sz;
         if (cs[c].hostname) {

@@ -150,10 +150,12 @@ __device__ __forceinline__ bool untolerated_noschedule(const MirrorView& m, cons
 }
 // nodeLabelsMatchSpreadConstraints + matchNodeInclusionPolicies per constraint
 // (podtopologyspread/common.go:43-80): bit c set if node i counts for constraint c
+// need_all = false: requireAllTopologies off (system-default scoring, scoring.go:171-174), every node counts
 __device__ __forceinline__ uint32_t pts_eligible(const MirrorView& m, const uint8_t* base, const PodDesc& d,
-                                                 const PtsCons* cs, int32_t n, int i) {
-  for (int32_t c = 0; c < n; ++c)
-    if (node_label(m, cs[c].slot, i) < 0) return 0u;
+                                                 const PtsCons* cs, int32_t n, int i, bool need_all = true) {
+  if (need_all)
+    for (int32_t c = 0; c < n; ++c)
+      if (node_label(m, cs[c].slot, i) < 0) return 0u;
   int na = -1, tn = -1;
   uint32_t bits = 0;
   for (int32_t c = 0; c < n; ++c) {
@@ -168,6 +170,21 @@ __device__ __forceinline__ uint32_t pts_eligible(const MirrorView& m, const uint
     bits |= 1u << c;
   }
   return bits;
+}
+
+// PodTopologySpread PreScore's domain of node i for ScheduleAnyway constraint c: the key's value, or
+// with DF_PTS_ANYTOPO the "" domain of a node without the key (node.Labels[key] == "", scoring.go:95-106,
+// 175-181); -1 otherwise
+__device__ __forceinline__ int32_t pts_domain(const MirrorView& m, const PtsCons& c, int i) {
+  const int32_t v = node_label(m, c.slot, i);
+  return v >= 0 ? v : c.absent;
+}
+// a feasible node PreScore ignores (IgnoredNodes, scoring.go:82-88): some key missing, requireAllTopologies on
+__device__ __forceinline__ bool pts_ignored(const MirrorView& m, const PodDesc& d, const PtsCons* cs, int i) {
+  if (d.flags & DF_PTS_ANYTOPO) return false;
+  bool ignored = false;
+  for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
+  return ignored;
 }
 
 __device__ __forceinline__ bool term_matches_pod(const int32_t* sp, const IpaTerm& t, int32_t ns,

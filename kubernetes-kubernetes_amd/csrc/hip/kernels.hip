@@ -262,8 +262,8 @@ __device__ uint32_t run_filters(const MirrorView& m, const NodeCore& nc, const u
   }
   // NodePorts (node_ports.go:150-176 -> HostPortInfo.CheckConflict, precompiled per port id)
   if ((fm >> P_PORTS) & 1u) {
-    const uint32_t* slots = m.ports + (size_t)i * kPortSlots;
-    for (int s = 0; s < kPortSlots; ++s) {
+    const uint32_t* slots = m.ports + (size_t)i * m.port_slots;
+    for (int s = 0; s < m.port_slots; ++s) {
       uint32_t pid = slots[s];
       if (pid != 0xffffffffu && bit(base, d.port_conflict_off, pid, d.n_port_words))
         return pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
@@ -487,15 +487,13 @@ __device__ __forceinline__ NodeEval eval_node(const MirrorView& m, const BatchVi
   // counts feed the normalising weights (podtopologyspread/scoring.go:61-115)
   if ((sm >> P_PTS) & 1u) {
     const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-    bool ignored = false;
-    for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
-    if (!ignored) {
+    if (!pts_ignored(m, d, cs, i)) {
       r.pts = true;
       PodStats* ps = b.stats + pod;
       // a cut feasible list (DF_SAMPLE): k_sample_apply marks the kept nodes' domains instead
       for (int32_t c = 0; c < ((d.flags & DF_SAMPLE) ? 0 : d.n_ptss); ++c) {
         if (cs[c].hostname) continue;
-        mark_domains(b.arena + cs[c].pres_base, node_label(m, cs[c].slot, i), true, &ps->pts_distinct[c]);
+        mark_domains(b.arena + cs[c].pres_base, pts_domain(m, cs[c], i), true, &ps->pts_distinct[c]);
       }
     }
   }
@@ -632,8 +630,8 @@ __device__ __forceinline__ NodeEval eval_core_fast(const MirrorView& m, const No
         st = pack_status(C_UU, P_NA, KSG_R_NODE_AFFINITY_POD);
     }
     if (st == 0 && ((fm >> P_PORTS) & 1u)) {  // NodePorts
-      const uint32_t* slots = m.ports + (size_t)i * kPortSlots;
-      for (int k = 0; k < kPortSlots; ++k) {
+      const uint32_t* slots = m.ports + (size_t)i * m.port_slots;
+      for (int k = 0; k < m.port_slots; ++k) {
         const uint32_t pid = slots[k];
         if (pid != 0xffffffffu && bit(base, d.port_conflict_off, pid, d.n_port_words)) {
           st = pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
@@ -1006,12 +1004,12 @@ __device__ __forceinline__ bool commit_result(const MirrorView& m, const BatchVi
     const ScalarReq* sr = at<ScalarReq>(base, d.a_scalar_off);
     for (int k = 0; k < d.n_a_scalar; ++k) m.scalar_req[(size_t)sr[k].slot * cap + j] += sr[k].qty;
     const uint32_t* pp = at<uint32_t>(base, d.pod_ports_off);
-    uint32_t* slots = m.ports + (size_t)j * kPortSlots;
+    uint32_t* slots = m.ports + (size_t)j * m.port_slots;
     if (d.slot >= 0) m.pod_node[d.slot] = j;  // the pod joins NodeInfo.Pods (pod table)
     for (int k = 0; k < d.n_pod_ports; ++k) {  // HostPortInfo.Add: set semantics
       bool present = false;
       int empty = -1;
-      for (int q = 0; q < kPortSlots; ++q) {
+      for (int q = 0; q < m.port_slots; ++q) {  // the host sized the stride for every assume of the batch
         present |= slots[q] == pp[k];
         if (slots[q] == 0xffffffffu && empty < 0) empty = q;
       }
@@ -1205,13 +1203,10 @@ __global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView
   bool pts = false;
   if ((sm >> P_PTS) & 1u) {
     const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-    bool ignored = false;
-    if (kept)
-      for (int32_t c = 0; c < d.n_ptss; ++c) ignored |= node_label(m, cs[c].slot, i) < 0;
-    pts = kept && !ignored;
+    pts = kept && !pts_ignored(m, d, cs, i);
     for (int32_t c = 0; c < d.n_ptss; ++c) {
       if (cs[c].hostname) continue;
-      mark_domains(b.arena + cs[c].pres_base, pts ? node_label(m, cs[c].slot, i) : 0, pts, &ps->pts_distinct[c]);
+      mark_domains(b.arena + cs[c].pres_base, pts ? pts_domain(m, cs[c], i) : 0, pts, &ps->pts_distinct[c]);
     }
   }
   mt = wave_max_u64(mt);
@@ -3295,7 +3290,7 @@ hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipSt
 // ---- incremental mirror ingestion (Cache.UpdateNode, cache.go UpdateNode + UpdateSnapshot's
 // generation diff): one thread per updated node writes its static columns in place.
 __global__ __launch_bounds__(kBlock) void k_node_update(MirrorView m, const NodeUpdate* u, const uint32_t* ids,
-                                                       const LabelEntry* lbl, int count) {
+                                                       const LabelEntry* lbl, const ScalarEntry* sc, int count) {
   const int k = blockIdx.x * kBlock + threadIdx.x;
   if (k >= count) return;
   const NodeUpdate r = u[k];
@@ -3307,7 +3302,9 @@ __global__ __launch_bounds__(kBlock) void k_node_update(MirrorView m, const Node
   const_cast<int64_t*>(m.alloc_eph)[i] = r.alloc_eph;
   const_cast<int32_t*>(m.alloc_pods)[i] = r.alloc_pods;
   const_cast<uint32_t*>(m.flags)[i] = r.flags;
-  for (int q = 0; q < kMaxScalar; ++q) const_cast<int64_t*>(m.scalar_alloc)[(size_t)q * cap + i] = r.scalar[q];
+  for (int q = 0; q < m.scalar_cols; ++q) const_cast<int64_t*>(m.scalar_alloc)[(size_t)q * cap + i] = 0;
+  for (uint32_t q = 0; q < r.sc_cnt; ++q)
+    const_cast<int64_t*>(m.scalar_alloc)[(size_t)sc[r.sc_off + q].slot * cap + i] = sc[r.sc_off + q].value;
   for (int q = 0; q < r.n_taint; ++q) const_cast<uint32_t*>(m.taint_ids)[r.taint_off + q] = ids[r.id_off + q];
   for (int q = 0; q < r.n_img; ++q) const_cast<uint32_t*>(m.img_ids)[r.img_off + q] = ids[r.id_off + r.n_taint + q];
   for (int q = 0; q < r.lbl_cnt; ++q) {
@@ -3319,9 +3316,9 @@ __global__ __launch_bounds__(kBlock) void k_node_update(MirrorView m, const Node
   }
 }
 hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const uint32_t* ids, const LabelEntry* lbl,
-                              int count, hipStream_t s) {
+                              const ScalarEntry* sc, int count, hipStream_t s) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_node_update, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, u, ids, lbl, count);
+  hipLaunchKernelGGL(k_node_update, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, u, ids, lbl, sc, count);
   return hipGetLastError();
 }
 // ---- node add / remove without a full re-layout (Cluster::relayout_gather): every surviving node's
@@ -3342,7 +3339,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(uint8_t* dst, const uint
     reinterpret_cast<uint32_t*>(dst)[ro + i] = reinterpret_cast<const uint32_t*>(src)[ro + s];
   } else if (esz == 1) {
     dst[ro + i] = src[ro + s];
-  } else {  // ports: kPortSlots uint32 per node
+  } else {  // ports: port_slots uint32 per node
     for (int k = 0; k < esz / 4; ++k)
       reinterpret_cast<uint32_t*>(dst)[(ro + i) * (size_t)(esz / 4) + k] =
           reinterpret_cast<const uint32_t*>(src)[(ro + s) * (size_t)(esz / 4) + k];
@@ -3373,7 +3370,8 @@ hipError_t launch_gather_csr(uint32_t* dst, const uint32_t* src, const int32_t* 
 
 // pod events (NodeInfo.update via AddPod / RemovePod / ForgetPod): one thread per queued node
 // writes its dynamic columns in place
-__global__ __launch_bounds__(kBlock) void k_node_dyn(MirrorView m, const NodeDyn* d, int count) {
+__global__ __launch_bounds__(kBlock) void k_node_dyn(MirrorView m, const NodeDyn* d, const uint32_t* port_pool,
+                                                     const ScalarEntry* sc, int count) {
   const int k = blockIdx.x * kBlock + threadIdx.x;
   if (k >= count) return;
   const NodeDyn& r = d[k];
@@ -3386,12 +3384,15 @@ __global__ __launch_bounds__(kBlock) void k_node_dyn(MirrorView m, const NodeDyn
   m.nz_cpu[i] = r.nz_cpu;
   m.nz_mem[i] = r.nz_mem;
   m.num_pods[i] = r.num_pods;
-  for (int q = 0; q < kMaxScalar; ++q) m.scalar_req[(size_t)q * cap + i] = r.scalar[q];
-  for (int q = 0; q < kPortSlots; ++q) m.ports[(size_t)i * kPortSlots + q] = r.ports[q];
+  for (int q = 0; q < m.scalar_cols; ++q) m.scalar_req[(size_t)q * cap + i] = 0;
+  for (uint32_t q = 0; q < r.sc_cnt; ++q) m.scalar_req[(size_t)sc[r.sc_off + q].slot * cap + i] = sc[r.sc_off + q].value;
+  for (int q = 0; q < m.port_slots; ++q)
+    m.ports[(size_t)i * m.port_slots + q] = (uint32_t)q < r.port_cnt ? port_pool[r.port_off + q] : 0xffffffffu;
 }
-hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, int count, hipStream_t s) {
+hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, const uint32_t* port_pool, const ScalarEntry* sc,
+                           int count, hipStream_t s) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_node_dyn, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, d, count);
+  hipLaunchKernelGGL(k_node_dyn, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, d, port_pool, sc, count);
   return hipGetLastError();
 }
 hipError_t launch_sample(const MirrorView& m, const BatchView& b, int pod, bool cut, hipStream_t s) {
@@ -3922,8 +3923,8 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
   };
   bool port = false;  // a conflicting port no potential victim holds (NodeInfo.RemovePod drops shared ones too)
   if (ports_on)
-    for (int s = 0; s < kPortSlots; ++s) {
-      const uint32_t pid = m.ports[(size_t)i * kPortSlots + s];
+    for (int s = 0; s < m.port_slots; ++s) {
+      const uint32_t pid = m.ports[(size_t)i * m.port_slots + s];
       if (!conf(pid)) continue;
       bool held = false;
       for (int q = first; q < cnt; ++q) held |= r[q].port[0] == pid || r[q].port[1] == pid;

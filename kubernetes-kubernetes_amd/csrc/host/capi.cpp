@@ -108,6 +108,30 @@ int ksg_upsert_namespace(ksg_ctx* ctx, const char* ns_json, size_t len) {
   })
 }
 
+int ksg_upsert_object(ksg_ctx* ctx, const char* obj_json, size_t len) {
+  if (!ctx || !obj_json) return KSG_EINVAL;
+  GUARD({
+    SelectorObj o;
+    if (!decode_selector_obj(obj_json, len, &o, &ctx->err)) return KSG_EINVAL;
+    return with_err(ctx, ctx->cluster->upsert_object(std::move(o)));
+  })
+}
+
+int ksg_remove_object(ksg_ctx* ctx, const char* kind, const char* ns, const char* name) {
+  if (!ctx || !kind || !name) return KSG_EINVAL;
+  GUARD({
+    const int k = obj_kind(kind);
+    if (k < 0) {
+      ctx->err = std::string("unsupported kind ") + kind;
+      return KSG_EINVAL;
+    }
+    const std::string n = (ns && *ns) ? ns : "default";
+    const int rc = ctx->cluster->remove_object(k, n, name);
+    if (rc == KSG_ENOTFOUND) ctx->err = std::string(kind) + " " + n + "/" + name + " not found";
+    return with_err(ctx, rc);
+  })
+}
+
 int ksg_add_node(ksg_ctx* ctx, const char* node_json, size_t len) {
   if (!ctx || !node_json) return KSG_EINVAL;
   GUARD({
@@ -172,6 +196,10 @@ int ksg_pod_compile(ksg_ctx* ctx, const char* pod_json, size_t len, int32_t* han
   GUARD({
     PodSpec p;
     if (!decode_pod(pod_json, len, &p, &ctx->err)) return KSG_EINVAL;
+    if (!p.unsupported.empty()) {  // declined, not mis-evaluated: the caller schedules it on the CPU path
+      ctx->err = "pod " + p.ns + "/" + p.name + ": " + p.unsupported;
+      return KSG_ENOTSUP;
+    }
     const int32_t h = ctx->engine->next_handle++;
     ctx->engine->queue[h] = std::move(p);
     *handle = h;

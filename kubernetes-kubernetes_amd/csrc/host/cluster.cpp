@@ -11,9 +11,10 @@
 #include "host.hpp"
 
 namespace ksg {
-hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const uint32_t* ids, const LabelEntry* lbl,
+hipError_t launch_node_update(const MirrorView& m, const NodeUpdate* u, const uint32_t* ids, const LabelEntry* lbl, const ScalarEntry* sc,
                               int count, hipStream_t s);
-hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, int count, hipStream_t s);
+hipError_t launch_node_dyn(const MirrorView& m, const NodeDyn* d, const uint32_t* port_pool, const ScalarEntry* sc,
+                           int count, hipStream_t s);
 
 static const char* zone_key(const NodeSpec& n, std::string* out) {  // node/topology/helpers.go:31-58
   auto get = [&](const char* a, const char* b) -> std::string {
@@ -64,8 +65,7 @@ int32_t Cluster::key_id(const std::string& k) {
 int32_t Cluster::scalar_slot(const std::string& n) {
   int32_t id = scalar_ix.find(n);
   if (id >= 0) return id;
-  if ((int)scalar_ix.strs.size() >= kMaxScalar) return -1;
-  layout_dirty = true;  // a new column must exist on the device
+  layout_dirty = true;  // a new column must exist on the device (the layout widens scalar_cols as needed)
   return scalar_ix.get(n);
 }
 uint32_t Cluster::port_id(std::string ip, std::string proto, int32_t port) {  // HostPortInfo.sanitize
@@ -184,6 +184,85 @@ bool Cluster::key_unique(int32_t key) {
 int Cluster::upsert_namespace(const NamespaceSpec& ns) {
   namespaces[ns.name] = ns;
   return KSG_OK;
+}
+
+// ---- the selecting objects of PodTopologySpread's default constraints ---------------------------
+int Cluster::upsert_object(SelectorObj&& o) {
+  if (o.kind == OBJ_SERVICE) services[o.ns][o.name] = std::move(o.sel);
+  else owners[o.kind - 1][{o.ns, o.name}] = std::move(o.sel);
+  return KSG_OK;
+}
+int Cluster::remove_object(int kind, const std::string& ns, const std::string& name) {
+  if (kind == OBJ_SERVICE) {
+    auto it = services.find(ns);
+    if (it == services.end() || !it->second.erase(name)) return KSG_ENOTFOUND;
+    if (it->second.empty()) services.erase(it);
+    return KSG_OK;
+  }
+  if (kind < OBJ_RC || kind > OBJ_SS) return KSG_EINVAL;
+  return owners[kind - 1].erase({ns, name}) ? KSG_OK : KSG_ENOTFOUND;
+}
+
+// helper.DefaultSelector (plugins/helper/spread.go:37-95).  Services of the pod's namespace whose
+// (non-nil) selector matches the pod's labels merge their selector maps (GetPodServices :98-119); the
+// controller owner then merges an RC's map (:67-71) or appends an RS / StatefulSet selector's
+// requirements (:72-87; a nil or unparsable LabelSelector adds nothing).  Matching is an AND of
+// requirements, so their order (sorted by key upstream) does not matter.
+bool Cluster::default_selector(const PodSpec& p, LabelSel* out) {
+  std::map<std::string, std::string> set;  // labels.Set; labels.Merge lets the later map win
+  auto sit = services.find(p.ns);
+  if (sit != services.end())
+    for (auto& kv : sit->second) {
+      const LabelSel& s = kv.second;
+      if (!s.present) continue;  // nil selector: matches nothing (:109-112)
+      bool m = true;             // labels.Set(selector).AsSelectorPreValidated().Matches(pod labels)
+      for (auto& r : s.match) {
+        auto it = std::lower_bound(p.labels.begin(), p.labels.end(), std::make_pair(r.first, std::string()));
+        m = m && it != p.labels.end() && it->first == r.first && it->second == r.second;
+      }
+      if (m)
+        for (auto& r : s.match) set[r.first] = r.second;
+    }
+  out->present = true;
+  out->exprs.clear();
+  if (p.has_controller) {
+    // schema.ParseGroupVersion (runtime/schema/group_version.go:211-227); an error keeps the services' selector
+    std::string group, version;
+    const std::string& gv = p.owner_api;
+    const size_t slashes = (size_t)std::count(gv.begin(), gv.end(), '/');
+    bool ok = true;
+    if (gv.empty() || gv == "/") {
+    } else if (slashes == 0) {
+      version = gv;
+    } else if (slashes == 1) {
+      group = gv.substr(0, gv.find('/'));
+      version = gv.substr(gv.find('/') + 1);
+    } else {
+      ok = false;
+    }
+    int kind = -1;
+    if (ok && group.empty() && version == "v1" && p.owner_kind == "ReplicationController") kind = OBJ_RC;
+    if (ok && group == "apps" && version == "v1" && p.owner_kind == "ReplicaSet") kind = OBJ_RS;
+    if (ok && group == "apps" && version == "v1" && p.owner_kind == "StatefulSet") kind = OBJ_SS;
+    if (kind >= 0) {
+      auto it = owners[kind - 1].find({p.ns, p.owner_name});  // listers are namespaced by the pod's namespace
+      if (it != owners[kind - 1].end()) {
+        const LabelSel& s = it->second;
+        if (kind == OBJ_RC) {
+          for (auto& r : s.match) set[r.first] = r.second;
+        } else if (s.present) {
+          std::vector<int32_t> scratch;
+          int32_t off;
+          if (compile_lsel(s, nullptr, &scratch, &off)) {  // metav1.LabelSelectorAsSelector without error
+            for (auto& r : s.match) out->exprs.push_back({r.first, "In", {r.second}});
+            for (auto& e : s.exprs) out->exprs.push_back(e);
+          }
+        }
+      }
+    }
+  }
+  out->match.assign(set.begin(), set.end());
+  return !(out->match.empty() && out->exprs.empty());  // selector.Empty() (common.go:65-67)
 }
 
 void Cluster::add_images(const NodeSpec& n) {
@@ -346,6 +425,7 @@ void Cluster::apply_pod(NodeRec& r, const BoundPod& bp, int sign) {  // NodeInfo
   for (uint32_t p : bp.port_ids) {  // HostPortInfo.Add/Remove: set semantics (types.go:555-587)
     if (sign > 0) r.ports.insert(p);
     else r.ports.erase(p);
+    ports_hw_ = std::max(ports_hw_, (int32_t)r.ports.size());
   }
 }
 
@@ -437,8 +517,18 @@ int Cluster::remove_pod(const std::string& uid) {
     }                                                        \
   } while (0)
 
+// HostPortInfo has no size limit (kube-scheduler/framework/types.go:553-642): the device's port row
+// stride follows the largest UsedPorts set, plus what the next batch's AssumePods can add (`extra`
+// ids, Engine::run_batch), and a wider stride is a full re-layout.
+void Cluster::reserve_ports(int32_t extra) {
+  ports_need_ = std::max(ports_need_, ports_hw_ + extra);
+  if (view.ports && ports_need_ > view.port_slots) layout_dirty = true;
+}
+
 int Cluster::ensure_mirror(bool pods_needed) {
   order();
+  ports_need_ = std::max(ports_need_, ports_hw_);  // pod events since the last cycle
+  if (view.ports && ports_need_ > view.port_slots) layout_dirty = true;
   if (!layout_dirty) {
     int rc = flush_node_updates();
     if (!rc) rc = flush_node_dynamic();
@@ -449,11 +539,9 @@ int Cluster::ensure_mirror(bool pods_needed) {
     const int rc = relayout_gather(&done);
     if (rc || done) return rc;
   }
-  for (int32_t i : static_dirty_)  // the re-layout below uploads every node
-    if ((size_t)i < static_queued_.size()) static_queued_[i] = 0;
-  static_dirty_.clear();
-  for (int32_t i : dyn_dirty_)
-    if ((size_t)i < dyn_queued_.size()) dyn_queued_[i] = 0;
+  static_dirty_.clear();  // the re-layout below uploads every node
+  static_queued_.assign(order_.size(), 0);  // every queued flag, listed or not (the re-layout uploads all)
+  dyn_queued_.assign(order_.size(), 0);
   dyn_dirty_.clear();
   HIPCHK(hipStreamSynchronize(stream));
   free_all();
@@ -473,28 +561,34 @@ int Cluster::ensure_mirror(bool pods_needed) {
   view.alloc_eph = a64();
   view.alloc_pods = (int32_t*)dalloc((size_t)cap * 4);
   view.flags = (uint32_t*)dalloc((size_t)cap * 4);
-  view.scalar_alloc = (int64_t*)dalloc((size_t)cap * 8 * kMaxScalar);
+  const int32_t sc = std::max<int32_t>(kMaxScalar, (((int32_t)scalar_ix.strs.size() + 7) / 8) * 8);
+  view.scalar_cols = sc;
+  view.scalar_alloc = (int64_t*)dalloc((size_t)cap * 8 * sc);
   view.req_cpu = a64();
   view.req_mem = a64();
   view.req_eph = a64();
   view.nz_cpu = a64();
   view.nz_mem = a64();
   view.num_pods = (int32_t*)dalloc((size_t)cap * 4);
-  view.scalar_req = (int64_t*)dalloc((size_t)cap * 8 * kMaxScalar);
+  view.scalar_req = (int64_t*)dalloc((size_t)cap * 8 * sc);
   view.taint_off = (uint32_t*)dalloc((size_t)(cap + 1) * 4);
   view.img_off = (uint32_t*)dalloc((size_t)(cap + 1) * 4);
   view.labels = (int32_t*)dalloc((size_t)cap * 4 * slots_cap_);
   view.label_num = (int64_t*)dalloc((size_t)cap * 8 * slots_cap_);
   view.label_num_ok = (uint8_t*)dalloc((size_t)cap * slots_cap_);
-  view.ports = (uint32_t*)dalloc((size_t)cap * 4 * kPortSlots);
+  for (int32_t i = 0; i < n; ++i) ports_hw_ = std::max(ports_hw_, (int32_t)nodes_[order_[(size_t)i]]->ports.size());
+  ports_need_ = std::max(ports_need_, ports_hw_);
+  const int32_t ps = std::max<int32_t>(kPortSlots, ((ports_need_ + ports_need_ / 2 + 7) / 8) * 8);
+  view.port_slots = ps;
+  view.ports = (uint32_t*)dalloc((size_t)cap * 4 * ps);
 
   std::vector<int64_t> acpu(cap, 0), amem(cap, 0), aeph(cap, 0), rcpu(cap, 0), rmem(cap, 0), reph(cap, 0),
       zcpu(cap, 0), zmem(cap, 0);
   std::vector<int32_t> apods(cap, 0), npods(cap, 0);
   std::vector<uint32_t> flags(cap, 0), toff(cap + 1, 0), ioff(cap + 1, 0), tids, iids;
   int64_t taint_max = 0;
-  std::vector<int64_t> salloc((size_t)cap * kMaxScalar, 0), sreq((size_t)cap * kMaxScalar, 0);
-  std::vector<uint32_t> ports((size_t)cap * kPortSlots, 0xffffffffu);
+  std::vector<int64_t> salloc((size_t)cap * sc, 0), sreq((size_t)cap * sc, 0);
+  std::vector<uint32_t> ports((size_t)cap * ps, 0xffffffffu);
   for (int32_t i = 0; i < n; ++i) {
     const NodeRec& r = *nodes_[order_[i]];
     acpu[i] = r.alloc_cpu;
@@ -515,9 +609,8 @@ int Cluster::ensure_mirror(bool pods_needed) {
     taint_max = std::max<int64_t>(taint_max, (int64_t)r.taint_ids.size());
     ioff[i] = (uint32_t)iids.size();
     iids.insert(iids.end(), r.image_ids.begin(), r.image_ids.end());
-    if (r.ports.size() > (size_t)kPortSlots) { err = "node " + r.spec.name + " uses more host ports than supported"; return KSG_ENOTSUP; }
     int q = 0;
-    for (uint32_t p : r.ports) ports[(size_t)i * kPortSlots + q++] = p;
+    for (uint32_t p : r.ports) ports[(size_t)i * ps + q++] = p;
   }
   for (int32_t i = n; i <= cap; ++i) {
     toff[i] = (uint32_t)tids.size();
@@ -593,7 +686,9 @@ int Cluster::relayout_gather(bool* done) {
   *done = false;
   const int32_t n = (int32_t)order_.size();
   const int32_t cap = view.cap;
-  if (!view.req_cpu || laid_epoch_ == 0 || n == 0 || n + 1 > cap || slots_used_ > slots_cap_) return KSG_OK;
+  if (!view.req_cpu || laid_epoch_ == 0 || n == 0 || n + 1 > cap || slots_used_ > slots_cap_ ||
+      (int32_t)scalar_ix.strs.size() > view.scalar_cols)
+    return KSG_OK;
   std::vector<NodeRec*> recs((size_t)n);
   for (int32_t i = 0; i < n; ++i) recs[(size_t)i] = nodes_[order_[(size_t)i]].get();
   std::vector<int32_t> src((size_t)n, -1);
@@ -603,7 +698,7 @@ int Cluster::relayout_gather(bool* done) {
   int32_t fresh = 0;
   for (int32_t i = 0; i < n; ++i) {
     const NodeRec& r = *recs[(size_t)i];
-    if (r.ports.size() > (size_t)kPortSlots) return KSG_OK;  // the full path reports it
+    if ((int32_t)r.ports.size() > view.port_slots) return KSG_OK;  // the full path widens the stride
     src[(size_t)i] = (r.laid_epoch == laid_epoch_ && !r.stale) ? r.laid_ix : -1;
     fresh += src[(size_t)i] < 0;
     toff[(size_t)i] = (uint32_t)nt;
@@ -619,7 +714,7 @@ int Cluster::relayout_gather(bool* done) {
   if (nt > taint_cap_ || ni > img_cap_) return KSG_OK;
   if (fresh * 2 > n) return KSG_OK;  // mostly new columns: the full path is as cheap
   // device scratch: the index map, the new CSR offsets, one column block
-  const size_t blk = (size_t)cap * 8 * (size_t)std::max(kMaxScalar, std::max(slots_used_, 1));
+  const size_t blk = (size_t)cap * 8 * (size_t)std::max(view.scalar_cols, std::max(slots_used_, 1));
   const size_t o_src = 0, o_toff = ((size_t)n * 4 + 255) & ~size_t(255),
                o_ioff = o_toff + (((size_t)(cap + 1) * 4 + 255) & ~size_t(255)),
                o_blk = o_ioff + (((size_t)(cap + 1) * 4 + 255) & ~size_t(255));
@@ -650,8 +745,8 @@ int Cluster::relayout_gather(bool* done) {
     if ((rc = col(p, 1, 8))) return rc;
   for (const void* p : {(const void*)view.alloc_pods, (const void*)view.num_pods, (const void*)view.flags})
     if ((rc = col(p, 1, 4))) return rc;
-  if ((rc = col(view.scalar_alloc, kMaxScalar, 8)) || (rc = col(view.scalar_req, kMaxScalar, 8)) ||
-      (rc = col(view.ports, 1, 4 * kPortSlots)) || (rc = col(view.labels, laid_slots_, 4)) ||
+  if ((rc = col(view.scalar_alloc, view.scalar_cols, 8)) || (rc = col(view.scalar_req, view.scalar_cols, 8)) ||
+      (rc = col(view.ports, 1, 4 * view.port_slots)) || (rc = col(view.labels, laid_slots_, 4)) ||
       (rc = col(view.label_num, laid_slots_, 8)) || (rc = col(view.label_num_ok, laid_slots_, 1)))
     return rc;
   // CSR ids, then the new offsets
@@ -769,6 +864,7 @@ int Cluster::flush_node_updates() {
   std::vector<NodeUpdate> rec(cnt);
   std::vector<uint32_t> ids;
   std::vector<LabelEntry> lbl;
+  std::vector<ScalarEntry> scv;
   std::vector<int64_t> vnum;
   for (size_t q = 0; q < cnt; ++q) {
     const int32_t i = static_dirty_[q];
@@ -782,7 +878,9 @@ int Cluster::flush_node_updates() {
     u.alloc_eph = r.alloc_eph;
     u.alloc_pods = (int32_t)r.alloc_pods;
     u.flags = r.spec.unschedulable ? 1u : 0u;
-    for (auto& kv : r.scalar_alloc) u.scalar[kv.first] = kv.second;
+    u.sc_off = (uint32_t)scv.size();
+    for (auto& kv : r.scalar_alloc) scv.push_back({kv.first, 0, kv.second});
+    u.sc_cnt = (uint32_t)(scv.size() - u.sc_off);
     u.taint_off = node_toff_[i];
     u.img_off = node_ioff_[i];
     u.n_taint = (int32_t)r.taint_ids.size();
@@ -805,8 +903,10 @@ int Cluster::flush_node_updates() {
   }
   static_dirty_.clear();
   const size_t b0 = cnt * sizeof(NodeUpdate), b1 = std::max<size_t>(ids.size(), 1) * 4,
-               b2 = std::max<size_t>(lbl.size(), 1) * sizeof(LabelEntry);
-  const size_t o1 = (b0 + 15) & ~size_t(15), o2 = (o1 + b1 + 15) & ~size_t(15), total = o2 + b2;
+               b2 = std::max<size_t>(lbl.size(), 1) * sizeof(LabelEntry),
+               b3 = std::max<size_t>(scv.size(), 1) * sizeof(ScalarEntry);
+  const size_t o1 = (b0 + 15) & ~size_t(15), o2 = (o1 + b1 + 15) & ~size_t(15), o3 = (o2 + b2 + 15) & ~size_t(15),
+               total = o3 + b3;
   if (upd_dev_.bytes < total) {
     if (upd_dev_.p) (void)hipFree(upd_dev_.p);
     upd_dev_.p = nullptr;
@@ -817,10 +917,11 @@ int Cluster::flush_node_updates() {
   std::memcpy(host.data(), rec.data(), b0);
   if (!ids.empty()) std::memcpy(host.data() + o1, ids.data(), ids.size() * 4);
   if (!lbl.empty()) std::memcpy(host.data() + o2, lbl.data(), lbl.size() * sizeof(LabelEntry));
+  if (!scv.empty()) std::memcpy(host.data() + o3, scv.data(), scv.size() * sizeof(ScalarEntry));
   uint8_t* d = (uint8_t*)upd_dev_.p;
   HIPCHK(hipMemcpyAsync(d, host.data(), total, hipMemcpyHostToDevice, stream));
   HIPCHK(launch_node_update(view, (const NodeUpdate*)d, (const uint32_t*)(d + o1), (const LabelEntry*)(d + o2),
-                            (int)cnt, stream));
+                            (const ScalarEntry*)(d + o3), (int)cnt, stream));
   HIPCHK(hipStreamSynchronize(stream));  // the host staging vector dies here
   return KSG_OK;
 }
@@ -843,16 +944,12 @@ int Cluster::flush_node_dynamic() {
   if (dyn_dirty_.empty()) return KSG_OK;
   const size_t cnt = dyn_dirty_.size();
   std::vector<NodeDyn> rec(cnt);
+  std::vector<uint32_t> pool;  // UsedPorts ids
+  std::vector<ScalarEntry> scv;  // scalar requests
   for (size_t q = 0; q < cnt; ++q) {
     const int32_t i = dyn_dirty_[q];
     dyn_queued_[i] = 0;
     NodeRec& r = *nodes_[order_[i]];
-    if (r.ports.size() > (size_t)kPortSlots) {
-      err = "node " + r.spec.name + " uses more host ports than supported";
-      layout_dirty = true;  // the next cycle re-lays out (and reports the same)
-      dyn_dirty_.clear();
-      return KSG_ENOTSUP;
-    }
     NodeDyn& d = rec[q];
     std::memset(&d, 0, sizeof(d));
     d.node = i;
@@ -862,14 +959,18 @@ int Cluster::flush_node_dynamic() {
     d.req_eph = r.req_eph;
     d.nz_cpu = r.nz_cpu;
     d.nz_mem = r.nz_mem;
-    for (auto& kv : r.scalar_req) d.scalar[kv.first] = kv.second;
-    for (int q2 = 0; q2 < kPortSlots; ++q2) d.ports[q2] = 0xffffffffu;
-    int k = 0;
-    for (uint32_t p : r.ports) d.ports[k++] = p;
+    d.sc_off = (uint32_t)scv.size();
+    for (auto& kv : r.scalar_req)
+      if (kv.second) scv.push_back({kv.first, 0, kv.second});
+    d.sc_cnt = (uint32_t)(scv.size() - d.sc_off);
+    d.port_off = (uint32_t)pool.size();
+    d.port_cnt = (uint32_t)r.ports.size();  // <= view.port_slots: ensure_mirror re-lays out first otherwise
+    pool.insert(pool.end(), r.ports.begin(), r.ports.end());
     r.stale = false;
   }
   dyn_dirty_.clear();
-  const size_t bytes = cnt * sizeof(NodeDyn);
+  const size_t rec_bytes = cnt * sizeof(NodeDyn), o_sc = (rec_bytes + pool.size() * 4 + 15) & ~size_t(15),
+               bytes = o_sc + std::max<size_t>(scv.size(), 1) * sizeof(ScalarEntry);
   if (dyn_dev_.bytes < bytes) {
     if (dyn_dev_.p) (void)hipFree(dyn_dev_.p);
     dyn_dev_.p = nullptr;
@@ -877,8 +978,14 @@ int Cluster::flush_node_dynamic() {
     HIPCHK(hipMalloc(&dyn_dev_.p, bytes * 2));
     dyn_dev_.bytes = bytes * 2;
   }
-  HIPCHK(hipMemcpyAsync(dyn_dev_.p, rec.data(), bytes, hipMemcpyHostToDevice, stream));
-  HIPCHK(launch_node_dyn(view, (const NodeDyn*)dyn_dev_.p, (int)cnt, stream));
+  HIPCHK(hipMemcpyAsync(dyn_dev_.p, rec.data(), rec_bytes, hipMemcpyHostToDevice, stream));
+  if (!pool.empty())
+    HIPCHK(hipMemcpyAsync((uint8_t*)dyn_dev_.p + rec_bytes, pool.data(), pool.size() * 4, hipMemcpyHostToDevice, stream));
+  if (!scv.empty())
+    HIPCHK(hipMemcpyAsync((uint8_t*)dyn_dev_.p + o_sc, scv.data(), scv.size() * sizeof(ScalarEntry), hipMemcpyHostToDevice,
+                          stream));
+  HIPCHK(launch_node_dyn(view, (const NodeDyn*)dyn_dev_.p, (const uint32_t*)((uint8_t*)dyn_dev_.p + rec_bytes),
+                         (const ScalarEntry*)((uint8_t*)dyn_dev_.p + o_sc), (int)cnt, stream));
   HIPCHK(hipStreamSynchronize(stream));  // the host records die here
   return KSG_OK;
 }
@@ -903,7 +1010,8 @@ int Cluster::compare_mirror(bool sync, int32_t* ndiff, int32_t* first) {
   HIPCHK(hipStreamSynchronize(stream));
   std::vector<int64_t> rc_((size_t)n), rm((size_t)n), re((size_t)n), zc((size_t)n), zm((size_t)n), ac((size_t)n), am((size_t)n);
   std::vector<int32_t> np((size_t)n), ap((size_t)n);
-  std::vector<uint32_t> fl((size_t)n), pt((size_t)n * kPortSlots);
+  const int32_t ps = view.port_slots;
+  std::vector<uint32_t> fl((size_t)n), pt((size_t)n * ps);
   auto down = [&](void* dst, const void* src, size_t bytes) -> int {
     if (!bytes) return KSG_OK;
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
@@ -915,7 +1023,7 @@ int Cluster::compare_mirror(bool sync, int32_t* ndiff, int32_t* first) {
       (rc = down(zm.data(), view.nz_mem, (size_t)n * 8)) || (rc = down(ac.data(), view.alloc_cpu, (size_t)n * 8)) ||
       (rc = down(am.data(), view.alloc_mem, (size_t)n * 8)) || (rc = down(np.data(), view.num_pods, (size_t)n * 4)) ||
       (rc = down(ap.data(), view.alloc_pods, (size_t)n * 4)) || (rc = down(fl.data(), view.flags, (size_t)n * 4)) ||
-      (rc = down(pt.data(), view.ports, (size_t)n * kPortSlots * 4)))
+      (rc = down(pt.data(), view.ports, (size_t)n * ps * 4)))
     return rc;
   auto bad = [&](int32_t where) {
     if (*first < 0) *first = where;
@@ -928,8 +1036,8 @@ int Cluster::compare_mirror(bool sync, int32_t* ndiff, int32_t* first) {
       continue;
     }
     std::set<uint32_t> dp;
-    for (int k = 0; k < kPortSlots; ++k)
-      if (pt[(size_t)i * kPortSlots + k] != 0xffffffffu) dp.insert(pt[(size_t)i * kPortSlots + k]);
+    for (int k = 0; k < ps; ++k)
+      if (pt[(size_t)i * ps + k] != 0xffffffffu) dp.insert(pt[(size_t)i * ps + k]);
     if (rc_[i] != r->req_cpu || rm[i] != r->req_mem || re[i] != r->req_eph || zc[i] != r->nz_cpu || zm[i] != r->nz_mem ||
         np[i] != r->num_pods || ac[i] != r->alloc_cpu || am[i] != r->alloc_mem || ap[i] != (int32_t)r->alloc_pods ||
         (fl[i] & 1u) != (r->spec.unschedulable ? 1u : 0u) || dp != r->ports)

@@ -650,16 +650,36 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
   D.slot = -1;
 
   // ---------------- PodTopologySpread (filterTopologySpreadConstraints, common.go:87-128)
+  // A pod without constraints of its own gets the plugin's default constraints (getConstraints,
+  // filtering.go:220-235; buildDefaultConstraints, common.go:59-75), whose selector is
+  // helper.DefaultSelector over the Services / RCs / RSs / StatefulSets selecting the pod; an Empty
+  // selector means no constraint at all.
+  const bool use_defaults = p.spreads.empty() && !cfg.pts_defaults.empty();
+  LabelSel dsel;
+  bool dsel_done = false, dsel_ok = false;
+  // requireAllTopologies = len(pod.Spec.TopologySpreadConstraints) > 0 || !systemDefaulted (scoring.go:141-144):
+  // system-defaulted scoring ignores no node, and a node without the key is in the "" domain
+  const bool anytopo = use_defaults && cfg.pts_system_defaulted;
   auto build_cons = [&](const char* action, std::vector<PtsCons>* cons, bool score) -> bool {
-    for (auto& sp : p.spreads) {
+    const std::vector<Spread>& src = use_defaults ? cfg.pts_defaults : p.spreads;
+    for (auto& sp : src) {
       if (sp.when != action) continue;
-      StrMap ml;
-      for (auto& k : sp.match_label_keys)  // MatchLabelKeysInPodTopologySpread (on by default)
-        for (auto& kv : p.labels)
-          if (kv.first == k) ml.push_back(kv);
-      std::sort(ml.begin(), ml.end());
       PtsCons pc{};
-      if (!c->compile_lsel(sp.sel, sp.sel.present ? &ml : nullptr, &pool, &pc.sel)) return false;
+      if (use_defaults) {
+        if (!dsel_done) {
+          dsel_ok = c->default_selector(p, &dsel);
+          dsel_done = true;
+        }
+        if (!dsel_ok) return true;  // selector.Empty(): no default constraints (common.go:65-67)
+        if (!c->compile_lsel(dsel, nullptr, &pool, &pc.sel, true)) return false;
+      } else {
+        StrMap ml;
+        for (auto& k : sp.match_label_keys)  // MatchLabelKeysInPodTopologySpread (on by default)
+          for (auto& kv : p.labels)
+            if (kv.first == k) ml.push_back(kv);
+        std::sort(ml.begin(), ml.end());
+        if (!c->compile_lsel(sp.sel, sp.sel.present ? &ml : nullptr, &pool, &pc.sel)) return false;
+      }
       const int32_t key = c->key_id(sp.key);
       pc.slot = slot_of(key);
       pc.max_skew = sp.max_skew;
@@ -669,6 +689,13 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       pc.taint_honor = sp.taint_honor ? 1 : 0;
       pc.hostname = (score && sp.key == "kubernetes.io/hostname") ? 1 : 0;
       pc.nvals = pc.hostname ? N : nvals(key);
+      pc.absent = -1;
+      if (score && anytopo && !pc.hostname) {
+        // a node without the key counts in the "" domain: its value id if some node carries key="",
+        // else one extra histogram entry past the interned values
+        const int32_t e = c->keys[key].values.find("");
+        pc.absent = e >= 0 ? e : pc.nvals++;
+      }
       pc.hist_base = alloc(pc.nvals, key, false);
       pc.pres_base = pc.hostname ? -1 : alloc(pc.nvals, key, true);
       cons->push_back(pc);
@@ -690,6 +717,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       ptss.clear();
     }
     if (ptss.empty() || N == 0) *smask &= ~(1u << P_PTS);
+    if (!ptss.empty() && anytopo) D.flags |= DF_PTS_ANYTOPO;
   }
   if (ptsf.size() > (size_t)kMaxCons || ptss.size() > (size_t)kMaxCons) {
     c->err = "more topology spread constraints than the device path supports";
@@ -978,7 +1006,7 @@ double Engine::algo_bytes(const PodDesc& d) const {
   if (fm & (1u << P_NA)) {
     b += 4.0 * (d.na_required.nterm + d.na_selector.nterm + d.na_added.nterm);  // one label column per term (lower bound)
   }
-  if (fm & (1u << P_PORTS)) b += 4.0 * kPortSlots;
+  if (fm & (1u << P_PORTS)) b += 4.0 * c->view.port_slots;
   if (fm & (1u << P_FIT)) {
     b += 4 + 4;                                            // alloc pods, pod count
     if (d.fit_any) {
@@ -1258,6 +1286,17 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     const bool existing_terms = !c->exanti_keys.empty() || !c->score_keys_req.empty() || !c->score_keys_pref.empty();
     for (int i = compiled; i < n && !pods_needed; ++i)
       pods_needed = existing_terms || !pods[i]->spreads.empty() || pods[i]->has_pod_affinity || pods[i]->has_pod_anti;
+  }
+  {  // host ports the batch's assumes can add to one node (the device row must hold them)
+    int32_t extra = 0;
+    for (int i = 0; i < n; ++i) {
+      for (auto& k : pods[i]->containers)
+        for (auto& hp : k.ports) extra += hp.port > 0;
+      for (auto& k : pods[i]->init_containers)
+        if (k.sidecar)
+          for (auto& hp : k.ports) extra += hp.port > 0;
+    }
+    c->reserve_ports(extra);
   }
   const auto Tm = clk::now();
   if ((rc = c->ensure_mirror(pods_needed))) return rc;

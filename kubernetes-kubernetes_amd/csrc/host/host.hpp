@@ -96,6 +96,13 @@ struct PodSpec {
   ResVec overhead, pod_requests;
   std::vector<Spread> spreads;
   std::vector<std::string> image_volumes;
+  // why a pod to schedule is outside the device's plugin set ("" if it is not): volumes or resource
+  // claims whose plugins (VolumeBinding, VolumeRestrictions, NodeVolumeLimits, VolumeZone,
+  // DynamicResources) would not Skip their PreFilter for it
+  std::string unsupported;
+  // metav1.GetControllerOfNoCopy: the ownerReference with controller == true (helper/spread.go:51-55)
+  bool has_controller = false;
+  std::string owner_api, owner_kind, owner_name;
   // DefaultPreemption inputs (corev1helpers.PodPriority, util.GetPodStartTime, preemption/util.go:23-35)
   int32_t priority = 0;          // spec.priority (0 when nil)
   bool has_start = false;        // status.startTime != nil
@@ -114,10 +121,21 @@ struct NodeSpec {
   std::vector<NodeImage> images;
 };
 struct NamespaceSpec { std::string name; StrMap labels; };
+// The objects PodTopologySpread's default constraints derive a pod's selector from
+// (helper.DefaultSelector, plugins/helper/spread.go:37-95): Services and ReplicationControllers carry a
+// map selector (present = non-nil), ReplicaSets and StatefulSets a metav1.LabelSelector.
+enum ObjKind : int { OBJ_SERVICE = 0, OBJ_RC = 1, OBJ_RS = 2, OBJ_SS = 3 };
+struct SelectorObj {
+  int kind = OBJ_SERVICE;
+  std::string ns, name;
+  LabelSel sel;  // map selectors are sel.match (exprs empty); sel.present = selector != nil
+};
 
 bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err);
 bool decode_node(const char* p, size_t n, NodeSpec* out, std::string* err);
 bool decode_namespace(const char* p, size_t n, NamespaceSpec* out, std::string* err);
+bool decode_selector_obj(const char* p, size_t n, SelectorObj* out, std::string* err);
+int obj_kind(const std::string& kind);  // -1: not one of the four
 
 // pod requests (component-helpers/resource/helpers.go:151-291) for the scheduler's uses
 struct PodResources {
@@ -151,6 +169,10 @@ struct Config {
   std::vector<NSTerm> added_required;
   bool has_added_pref = false;
   std::vector<std::pair<int32_t, NSTerm>> added_pref;
+  // PodTopologySpreadArgs (podtopologyspread/plugin.go:104-131): defaultingType System (the v1 default,
+  // defaults.go:225-229) uses systemDefaultConstraints (plugin.go:46-57); List uses defaultConstraints
+  bool pts_system_defaulted = true;
+  std::vector<Spread> pts_defaults;
   int device = 0;
   int loop_timing_stride = 1;  // time every k-th persistent-loop launch with HIP events (0: none)
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
@@ -258,6 +280,14 @@ class Cluster {
 
   // informer-fed cache events
   int upsert_namespace(const NamespaceSpec& ns);
+  // Service / ReplicationController / ReplicaSet / StatefulSet listers (podtopologyspread/plugin.go:145-150)
+  int upsert_object(SelectorObj&& o);
+  int remove_object(int kind, const std::string& ns, const std::string& name);
+  // helper.DefaultSelector (plugins/helper/spread.go:37-95) as a LabelSel: the merged Service / RC
+  // selector maps in `match`, the RS / SS requirements in `exprs`; false when it is Empty()
+  bool default_selector(const PodSpec& p, LabelSel* out);
+  std::map<std::string, std::map<std::string, LabelSel>> services;  // namespace -> name -> selector
+  std::map<std::pair<std::string, std::string>, LabelSel> owners[3];  // OBJ_RC / RS / SS by (ns, name)
   int add_node(NodeSpec&& n);
   int update_node(NodeSpec&& n);
   int remove_node(const std::string& name);
@@ -311,7 +341,9 @@ class Cluster {
   // sorted (key id << 32 | value id) set of a label map; values are interned
   std::vector<unsigned long long> label_set(const StrMap& labels);
   // metav1.LabelSelectorAsSelector into an int32 program appended to *pool; false on a parse error
-  bool compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off);
+  // prevalidated_match: s.match is a labels.Set turned into a selector without validation
+  bool compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off,
+                    bool prevalidated_match = false);
 
   // ---- pod table: every bound/assumed pod as (node, namespace, flags, labels) + its affinity terms
   std::vector<int32_t> pt_node, pt_ns;
@@ -346,6 +378,10 @@ class Cluster {
   std::vector<uint8_t> static_queued_;
   DevBuf upd_dev_;
   int ensure_mirror(bool pods_needed = true);  // (re)build device arrays if dirty
+  // the next batch's AssumePods may add up to `extra` host-port ids to one node (widens the stride)
+  void reserve_ports(int32_t extra);
+  int32_t ports_hw_ = 0;    // largest UsedPorts set of any node so far
+  int32_t ports_need_ = 0;  // port row stride the device layout must have
   // diff the device mirror (dynamic + static node columns, pod table) against the host shadow;
   // sync: run ensure_mirror first (what the next cycle does)
   int compare_mirror(bool sync, int32_t* ndiff, int32_t* first);

@@ -258,6 +258,15 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
     if (out->uid.empty()) out->uid = out->ns + "/" + out->name;
     out->labels = kv_map(d, d.get(*md, "labels"));
     out->terminating = d.present(*md, "deletionTimestamp");
+    // metav1.GetControllerOfNoCopy (apimachinery/pkg/apis/meta/v1/controller_ref.go): the first
+    // ownerReference with controller == true
+    d.each(d.get(*md, "ownerReferences"), [&](const JVal& o) {
+      if (out->has_controller || !d.boolean(o, "controller")) return;
+      out->has_controller = true;
+      out->owner_api = d.str(o, "apiVersion");
+      out->owner_kind = d.str(o, "kind");
+      out->owner_name = d.str(o, "name");
+    });
     if (const JVal* st = d.get(r, "status")) {
       const std::string t = d.str(*st, "startTime");
       if (!t.empty()) {
@@ -349,7 +358,22 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
     });
     d.each(d.get(*sp, "volumes"), [&](const JVal& v) {
       if (const JVal* im = d.get(v, "image")) out->image_volumes.push_back(d.str(*im, "reference"));
+      // the volume plugins' PreFilter Skip rules: VolumeBinding / VolumeZone / NodeVolumeLimits run for
+      // PVC and generic ephemeral volumes (volume_binding.go:350-358, csi.go:239-249) and for in-tree
+      // volumes CSI migration translates (csi-translation-lib translate.go:30-38,197-204);
+      // VolumeRestrictions for GCE PD / AWS EBS / RBD / iSCSI (volume_restrictions.go:168-197)
+      static const char* kPlugged[] = {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore",
+                                       "cinder", "azureDisk", "azureFile", "vsphereVolume", "portworxVolume", "rbd",
+                                       "iscsi"};
+      for (const char* k : kPlugged)
+        if (out->unsupported.empty() && d.present(v, k))
+          out->unsupported = std::string("volume \"") + d.str(v, "name") + "\" (" + k +
+                             ") needs the volume plugins, which run outside the device path";
     });
+    bool claims = false;  // DynamicResources PreFilter runs for pods with resource claims (dynamicresources.go:446-479)
+    d.each(d.get(*sp, "resourceClaims"), [&](const JVal&) { claims = true; });
+    if (claims && out->unsupported.empty())
+      out->unsupported = "spec.resourceClaims needs DynamicResources, which runs outside the device path";
     return true;
   } catch (std::exception& e) {
     *err = e.what();
@@ -391,6 +415,42 @@ bool decode_namespace(const char* p, size_t n, NamespaceSpec* out, std::string* 
     if (!md || d.str(*md, "name").empty()) { *err = "namespace without name"; return false; }
     out->name = d.str(*md, "name");
     out->labels = kv_map(d, d.get(*md, "labels"));
+    return true;
+  } catch (std::exception& e) {
+    *err = e.what();
+    return false;
+  }
+}
+
+int obj_kind(const std::string& k) {
+  if (k == "Service") return OBJ_SERVICE;
+  if (k == "ReplicationController") return OBJ_RC;
+  if (k == "ReplicaSet") return OBJ_RS;
+  if (k == "StatefulSet") return OBJ_SS;
+  return -1;
+}
+
+// v1.Service / v1.ReplicationController (spec.selector: map[string]string) and apps/v1 ReplicaSet /
+// StatefulSet (spec.selector: *metav1.LabelSelector), the four kinds helper.DefaultSelector lists
+bool decode_selector_obj(const char* p, size_t n, SelectorObj* out, std::string* err) {
+  try {
+    JDoc d(p, n);
+    const JVal& r = d.root();
+    out->kind = obj_kind(d.str(r, "kind"));
+    if (out->kind < 0) { *err = "kind must be Service, ReplicationController, ReplicaSet or StatefulSet"; return false; }
+    const JVal* md = d.get(r, "metadata");
+    if (!md || d.str(*md, "name").empty()) { *err = "object without name"; return false; }
+    out->name = d.str(*md, "name");
+    out->ns = d.str(*md, "namespace", "default");
+    if (out->ns.empty()) out->ns = "default";  // apiserver defaulting of metadata.namespace
+    const JVal* sp = d.get(r, "spec");
+    const JVal* sel = sp ? d.get(*sp, "selector") : nullptr;
+    if (out->kind == OBJ_SERVICE || out->kind == OBJ_RC) {
+      out->sel.present = sel != nullptr;
+      out->sel.match = kv_map(d, sel);
+    } else {
+      out->sel = label_sel(d, sel);
+    }
     return true;
   } catch (std::exception& e) {
     *err = e.what();
@@ -518,6 +578,14 @@ Config::Config() {
     enabled[i] = true;
     weight[i] = w[i];
   }
+  Spread h, z;  // systemDefaultConstraints (podtopologyspread/plugin.go:46-57), the System defaulting
+  h.key = "kubernetes.io/hostname";
+  h.when = "ScheduleAnyway";
+  h.max_skew = 3;
+  z.key = "topology.kubernetes.io/zone";
+  z.when = "ScheduleAnyway";
+  z.max_skew = 5;
+  pts_defaults = {h, z};
 }
 
 static int plugin_by_name(const std::string& n) {
@@ -625,6 +693,37 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     if (const JVal* ipa = d.get(r, "interPodAffinity")) {
       if (d.present(*ipa, "hardPodAffinityWeight")) c->hard_weight = (int32_t)d.num(*ipa, "hardPodAffinityWeight");
       c->ignore_pref_existing = d.boolean(*ipa, "ignorePreferredTermsOfExistingPods");
+    }
+    {  // PodTopologySpreadArgs (validation_pluginargs.go:102-174; plugin.go:46-57,120-127)
+      const JVal* pa = d.get(r, "podTopologySpread");
+      const std::string dt = pa ? d.str(*pa, "defaultingType", "System") : "System";  // defaults.go:225-229
+      if (dt != "System" && dt != "List") { *err = "podTopologySpread.defaultingType: Unsupported value"; return false; }
+      bool bad = false;
+      std::vector<Spread> list;
+      if (pa)
+        d.each(d.get(*pa, "defaultConstraints"), [&](const JVal& x) {
+          Spread s;
+          s.max_skew = (int32_t)d.num(x, "maxSkew");
+          s.key = d.str(x, "topologyKey");
+          s.when = d.str(x, "whenUnsatisfiable");
+          if (d.present(x, "minDomains")) s.min_domains = (int32_t)d.num(x, "minDomains");
+          const std::string ap = d.str(x, "nodeAffinityPolicy"), tp = d.str(x, "nodeTaintsPolicy");
+          s.aff_honor = ap.empty() || ap == "Honor";
+          s.taint_honor = tp == "Honor";
+          if (s.max_skew <= 0 || s.key.empty() || !valid_label_key(s.key) ||
+              (s.when != "DoNotSchedule" && s.when != "ScheduleAnyway") || d.present(x, "labelSelector"))
+            bad = true;
+          for (auto& o : list)
+            if (o.key == s.key && o.when == s.when) bad = true;  // validateConstraintNotRepeat
+          list.push_back(std::move(s));
+        });
+      if (bad) { *err = "podTopologySpread.defaultConstraints: invalid constraint"; return false; }
+      if (dt == "System" && !list.empty()) {
+        *err = "podTopologySpread.defaultingType: Invalid value: \"System\": when .defaultConstraints are not empty";
+        return false;
+      }
+      c->pts_system_defaulted = dt == "System";
+      if (!c->pts_system_defaulted) c->pts_defaults = std::move(list);  // System: Config() set them
     }
     if (const JVal* na = d.get(r, "nodeAffinity"))
       if (const JVal* aa = d.get(*na, "addedAffinity")) {

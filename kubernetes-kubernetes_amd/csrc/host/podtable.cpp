@@ -30,7 +30,8 @@ std::vector<unsigned long long> Cluster::label_set(const StrMap& labels) {
 // metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:36-71) with
 // labels.NewRequirement validation (selector.go:185-226).  merge_labels: the matchLabelKeys
 // label set PodTopologySpread prepends (common.go:96-106,130-143).
-bool Cluster::compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off) {
+bool Cluster::compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off,
+                           bool prevalidated_match) {
   *off = (int32_t)pool->size();
   if (!s.present) {  // nil selector: labels.Nothing()
     pool->push_back(1);
@@ -41,7 +42,8 @@ bool Cluster::compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::v
   std::vector<Req> reqs;
   bool ok = true;
   for (auto& kv : s.match) {
-    ok = ok && valid_label_key(kv.first) && valid_label_value(kv.second);
+    // labels.SelectorFromValidatedSet (selector.go:976-987) does not validate: DefaultSelector's merged maps
+    ok = ok && (prevalidated_match || (valid_label_key(kv.first) && valid_label_value(kv.second)));
     reqs.push_back({kv.first, LS_IN, {kv.second}});
   }
   for (auto& e : s.exprs) {

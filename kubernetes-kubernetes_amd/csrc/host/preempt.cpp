@@ -7,7 +7,8 @@
 //   DryRunPreemption (preemption.go:174-196, 404-457) -- k_preempt, one thread per node;
 //   the candidate cut of DryRunPreemption with sequential Parallelizer semantics (parallelism 1, the
 //   reference's own deterministic test mode) and SelectCandidate / pickOneNodeForPreemption
-//   (preemption.go:262-397) on the host, over the per-node results.
+//   (preemption.go:262-397) in k_preempt_pick on the device; with listCandidates the host re-derives
+//   both over the per-node results and fails the call if they disagree.
 // Actuation (deleting victims, patching nominatedNodeName, executor.go) is the caller's: the result
 // names the node and the victims.
 //
@@ -259,8 +260,8 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     pct = (int32_t)d.num(r, "minCandidateNodesPercentage", 10);
     absn = (int32_t)d.num(r, "minCandidateNodesAbsolute", 100);
     all_nodes = d.boolean(r, "allNodes");
-    staged = d.boolean(r, "debugHostStaged");
-    list = d.boolean(r, "listCandidates");  // detail lists every DryRunPreemption candidate  // diagnostic: force the host-staged victim records
+    staged = d.boolean(r, "debugHostStaged");  // diagnostic: force the host-staged victim records
+    list = d.boolean(r, "listCandidates");     // detail lists every DryRunPreemption candidate
     d.each(d.get(r, "pdbs"), [&](const JVal& v) {
       Pdb b;
       if (const JVal* md = d.get(v, "metadata")) b.ns = d.str(*md, "namespace", "default");

@@ -106,6 +106,8 @@ def _sig(lib, prefix):
     d("destroy", None, vp)
     d("last_error", cp, vp)
     d("upsert_namespace", C.c_int, vp, cp, sz)
+    d("upsert_object", C.c_int, vp, cp, sz)
+    d("remove_object", C.c_int, vp, cp, cp, cp)
     d("add_node", C.c_int, vp, cp, sz)
     d("update_node", C.c_int, vp, cp, sz)
     d("remove_node", C.c_int, vp, cp)
@@ -170,6 +172,15 @@ class Backend:
     def upsert_namespace(self, ns):
         b = _js(ns)
         self._chk(self.f["upsert_namespace"](self.ctx, b, len(b)), "upsert_namespace")
+
+    def upsert_object(self, obj):
+        """A Service / ReplicationController / ReplicaSet / StatefulSet (PodTopologySpread defaults)."""
+        b = _js(obj)
+        self._chk(self.f["upsert_object"](self.ctx, b, len(b)), "upsert_object")
+
+    def remove_object(self, kind, namespace, name):
+        self._chk(self.f["remove_object"](self.ctx, kind.encode(), (namespace or "").encode(), name.encode()),
+                  "remove_object")
 
     def add_node(self, node):
         b = _js(node)

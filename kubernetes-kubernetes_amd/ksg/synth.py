@@ -242,3 +242,25 @@ def mixed_cluster(n_nodes, n_init, n_pods, zones=10, seed=0x5EED):
         else:
             pods.append(pod_with_topology_spreading(nm, "sched-1"))
     return nodes, init, pods
+
+
+def pod_with_label(name, ns):
+    """templates/pod-with-label.yaml: label app=scheduler-perf, one pause container without requests."""
+    return PodW(name, ns).labels({"app": "scheduler-perf"}).container(image="registry.k8s.io/pause:3.10.1").obj()
+
+
+def default_topology_spreading(n_nodes, n_init, n_pods, seed=0x5EED):
+    """scheduler_perf DefaultTopologySpreading (topology_spreading/performance-config.yaml:102-147):
+    node-default nodes labelled topology.kubernetes.io/zone moon-1/2/3 round-robin, one Service
+    (templates/service.yaml, selector app=scheduler-perf) in service-ns, init pod-default pods, then
+    measured pod-with-label pods in service-ns -- they have no constraints of their own, so every one
+    is scored by PodTopologySpread's system default constraints (hostname maxSkew 3, zone maxSkew 5)
+    with the Service's selector.  -> (nodes, init pods (bound), measured pods, objects)."""
+    nodes, init, _ = topology_spreading(n_nodes, n_init, 0, seed=seed)
+    for p in init:
+        p["metadata"]["namespace"] = "default"
+    service = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "service-0", "namespace": "service-ns"},
+               "spec": {"selector": {"app": "scheduler-perf"}, "ports": [{"protocol": "TCP", "port": 80,
+                                                                            "targetPort": 8000}]}}
+    pods = [pod_with_label(f"pod-{k}", "service-ns") for k in range(n_pods)]
+    return nodes, init, pods, [service]

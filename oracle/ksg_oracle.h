@@ -22,6 +22,8 @@ const char *ksgo_create_error(void);
 void ksgo_destroy(ksgo_ctx *ctx);
 const char *ksgo_last_error(const ksgo_ctx *ctx);
 int ksgo_upsert_namespace(ksgo_ctx *ctx, const char *json, size_t len);
+int ksgo_upsert_object(ksgo_ctx *ctx, const char *json, size_t len);
+int ksgo_remove_object(ksgo_ctx *ctx, const char *kind, const char *ns, const char *name);
 int ksgo_add_node(ksgo_ctx *ctx, const char *json, size_t len);
 int ksgo_update_node(ksgo_ctx *ctx, const char *json, size_t len);
 int ksgo_remove_node(ksgo_ctx *ctx, const char *name);

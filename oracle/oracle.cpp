@@ -126,10 +126,22 @@ struct Config {
   std::vector<ParsedNodeSelectorTerm> addedRequired;
   bool hasAddedPreferred = false;
   PreferredTerms addedPreferred;
+  // PodTopologySpreadArgs: DefaultingType System (v1 default, defaults.go:225-229) -> the plugin's
+  // systemDefaultConstraints (podtopologyspread/plugin.go:46-57,124-127); List -> DefaultConstraints
+  bool ptsSystemDefaulted = true;
+  std::vector<TopologySpreadConstraint> ptsDefaults;
   Config() {
     // default_plugins.go:35-50
     const int64_t w[KSG_NUM_PLUGINS] = {0, 0, 3, 2, 0, 1, 2, 2, 1, 1};
     for (int i = 0; i < KSG_NUM_PLUGINS; ++i) { enabled[i] = true; weight[i] = w[i]; }
+    TopologySpreadConstraint h, z;
+    h.topologyKey = "kubernetes.io/hostname";
+    h.whenUnsatisfiable = "ScheduleAnyway";
+    h.maxSkew = 3;
+    z.topologyKey = "topology.kubernetes.io/zone";
+    z.whenUnsatisfiable = "ScheduleAnyway";
+    z.maxSkew = 5;
+    ptsDefaults = {h, z};
   }
 };
 
@@ -184,6 +196,31 @@ static bool decode_config(const mj::Value& v, Config* c, std::string* err) {
   if (auto ipa = v.has("interPodAffinity")) {
     if (ipa->has("hardPodAffinityWeight")) c->hardPodAffinityWeight = (int32_t)ipa->i64("hardPodAffinityWeight");
     c->ignorePreferredTermsOfExistingPods = ipa->boolean("ignorePreferredTermsOfExistingPods");
+  }
+  if (auto pa = v.has("podTopologySpread")) {  // validation_pluginargs.go:102-174
+    std::string dt = pa->str("defaultingType", "System");
+    if (dt != "System" && dt != "List") { *err = "defaultingType: Unsupported value"; return false; }
+    std::vector<TopologySpreadConstraint> list;
+    if (auto dc = pa->has("defaultConstraints"))
+      for (auto& x : dc->arr) {
+        TopologySpreadConstraint t = decode_tsc(x);
+        Requirement probe;
+        if (t.maxSkew <= 0 || t.topologyKey.empty() || !new_requirement(t.topologyKey, Op::Exists, {}, &probe) ||
+            (t.whenUnsatisfiable != "DoNotSchedule" && t.whenUnsatisfiable != "ScheduleAnyway") ||
+            t.labelSelector.present) {
+          *err = "invalid default constraint";
+          return false;
+        }
+        for (auto& o : list)
+          if (o.topologyKey == t.topologyKey && o.whenUnsatisfiable == t.whenUnsatisfiable) {
+            *err = "duplicate default constraint";
+            return false;
+          }
+        list.push_back(t);
+      }
+    if (dt == "System" && !list.empty()) { *err = "System defaulting with defaultConstraints"; return false; }
+    c->ptsSystemDefaulted = dt == "System";
+    if (!c->ptsSystemDefaulted) c->ptsDefaults = list;
   }
   if (auto na = v.has("nodeAffinity"))
     if (auto aa = na->has("addedAffinity")) {
@@ -441,6 +478,9 @@ struct ksgo_ctx {
   std::unique_ptr<Pool> pool;  // cfg.threads > 1
   std::string err;
   std::map<std::string, Namespace> namespaces;
+  // Service / ReplicationController / ReplicaSet / StatefulSet listers (podtopologyspread/plugin.go:145-150)
+  std::map<std::string, std::map<std::string, SelectorObject>> services;  // namespace -> name
+  std::map<std::tuple<std::string, std::string, std::string>, SelectorObject> owners;  // (kind, ns, name)
   std::map<std::string, std::unique_ptr<NodeInfoO>> nodes;
   // nodeTree (backend/cache/node_tree.go)
   std::vector<std::string> zones;
@@ -584,10 +624,62 @@ static int64_t count_pods_match(const std::vector<PodInfo*>& pods, const Selecto
   }
   return n;
 }
+// helper.DefaultSelector (plugins/helper/spread.go:37-95)
+static Selector default_selector(const ksgo_ctx* c, const Pod& pod) {
+  Labels labelSet;
+  auto sit = c->services.find(pod.ns);  // GetPodServices (:98-119)
+  if (sit != c->services.end())
+    for (auto& kv : sit->second) {
+      const SelectorObject& svc = kv.second;
+      if (!svc.hasMap) continue;  // nil selector matches nothing
+      bool m = true;              // labels.Set(selector).AsSelectorPreValidated().Matches
+      for (auto& r : svc.map) {
+        auto it = pod.labels.find(r.first);
+        if (it == pod.labels.end() || it->second != r.second) m = false;
+      }
+      if (m)
+        for (auto& r : svc.map) labelSet[r.first] = r.second;  // labels.Merge
+    }
+  auto as_selector = [](const Labels& set) {  // labels.SelectorFromValidatedSet (selector.go:976-987)
+    Selector s;
+    for (auto& kv : set) s.reqs.push_back({kv.first, Op::Equals, {kv.second}});
+    return s;
+  };
+  Selector selector = as_selector(labelSet);
+  if (!pod.hasController) return selector;
+  std::string group, version;  // schema.ParseGroupVersion (runtime/schema/group_version.go:211-227)
+  const std::string& gv = pod.ownerAPIVersion;
+  if (!(gv.empty() || gv == "/")) {
+    size_t n = std::count(gv.begin(), gv.end(), '/');
+    if (n == 0) version = gv;
+    else if (n == 1) { group = gv.substr(0, gv.find('/')); version = gv.substr(gv.find('/') + 1); }
+    else return selector;
+  }
+  auto find = [&](const char* kind) -> const SelectorObject* {
+    auto it = c->owners.find({kind, pod.ns, pod.ownerName});
+    return it == c->owners.end() ? nullptr : &it->second;
+  };
+  if (group.empty() && version == "v1" && pod.ownerKind == "ReplicationController") {
+    if (const SelectorObject* rc = find("ReplicationController")) {
+      for (auto& kv : rc->map) labelSet[kv.first] = kv.second;
+      selector = as_selector(labelSet);
+    }
+  } else if (group == "apps" && version == "v1" && (pod.ownerKind == "ReplicaSet" || pod.ownerKind == "StatefulSet")) {
+    if (const SelectorObject* o = find(pod.ownerKind.c_str())) {
+      Selector other;
+      // LabelSelectorAsSelector; Requirements() of labels.Nothing() is (nil, false)
+      if (label_selector_as_selector(o->sel, &other) && !other.nothing)
+        for (auto& r : other.reqs) selector.reqs.push_back(r);
+    }
+  }
+  return selector;
+}
+
 // filterTopologySpreadConstraints (common.go:87-128)
-static bool filter_tsc(const Pod& pod, const std::string& action, std::vector<Cycle::TSC>* out) {
+static bool filter_tsc(const std::vector<TopologySpreadConstraint>& tsc, const Pod& pod, const std::string& action,
+                       std::vector<Cycle::TSC>* out) {
   out->clear();
-  for (auto& c : pod.tsc) {
+  for (auto& c : tsc) {
     if (c.whenUnsatisfiable != action) continue;
     Selector sel;
     if (!label_selector_as_selector(c.labelSelector, &sel)) return false;
@@ -614,6 +706,19 @@ static bool filter_tsc(const Pod& pod, const std::string& action, std::vector<Cy
     t.taintHonor = c.nodeTaintsPolicy.empty() ? false : c.nodeTaintsPolicy == "Honor";
     out->push_back(t);
   }
+  return true;
+}
+// getConstraints (filtering.go:220-235) / initPreScoreState's choice (scoring.go:66-80): the pod's own
+// constraints, else buildDefaultConstraints (common.go:59-75)
+static bool get_constraints(const ksgo_ctx* c, const Pod& pod, const std::string& action, std::vector<Cycle::TSC>* out) {
+  if (!pod.tsc.empty()) return filter_tsc(pod.tsc, pod, action, out);
+  if (!filter_tsc(c->cfg.ptsDefaults, pod, action, out) || out->empty()) return true;
+  Selector sel = default_selector(c, pod);
+  if (sel.empty()) {
+    out->clear();
+    return true;
+  }
+  for (auto& t : *out) t.sel = sel;
   return true;
 }
 
@@ -690,7 +795,7 @@ static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std
       return Status{};
     }
     case KSG_PLUGIN_POD_TOPOLOGY_SPREAD: {  // filtering.go:139-149, 237-311
-      if (!filter_tsc(pod, "DoNotSchedule", &cy.ptsF)) return mk(KSG_CODE_ERROR, 0);
+      if (!get_constraints(c, pod, "DoNotSchedule", &cy.ptsF)) return mk(KSG_CODE_ERROR, 0);
       if (cy.ptsF.empty()) { *skip = true; return Status{}; }
       size_t nc = cy.ptsF.size();
       cy.tpMatch.assign(nc, {});
@@ -1023,8 +1128,8 @@ static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& n
     }
     case KSG_PLUGIN_POD_TOPOLOGY_SPREAD: {  // scoring.go:118-194
       if (c->list.empty()) { return mk(KSG_CODE_SKIP, 0); }
-      bool requireAll = !pod.tsc.empty();  // systemDefaulted = true
-      if (!filter_tsc(pod, "ScheduleAnyway", &cy.ptsS)) return mk(KSG_CODE_ERROR, 0);
+      bool requireAll = !pod.tsc.empty() || !c->cfg.ptsSystemDefaulted;  // scoring.go:141-144
+      if (!get_constraints(c, pod, "ScheduleAnyway", &cy.ptsS)) return mk(KSG_CODE_ERROR, 0);
       if (cy.ptsS.empty()) { return mk(KSG_CODE_SKIP, 0); }
       size_t nc = cy.ptsS.size();
       cy.ignored.clear();
@@ -1516,6 +1621,30 @@ const char* ksgo_create_error(void) { return g_create_error.c_str(); }
 void ksgo_destroy(ksgo_ctx* c) { delete c; }
 const char* ksgo_last_error(const ksgo_ctx* c) { return c->err.c_str(); }
 
+int ksgo_upsert_object(ksgo_ctx* c, const char* json, size_t len) {
+  SelectorObject o;
+  try {
+    mj::Value v = mj::parse(json, len);
+    if (!decode_selector_object(v, &o, &c->err)) return KSG_EINVAL;
+  } catch (std::exception& e) {
+    c->err = e.what();
+    return KSG_EINVAL;
+  }
+  if (o.kind == "Service") c->services[o.ns][o.name] = o;
+  else c->owners[{o.kind, o.ns, o.name}] = o;
+  return KSG_OK;
+}
+int ksgo_remove_object(ksgo_ctx* c, const char* kind, const char* ns, const char* name) {
+  std::string k = kind, n = (ns && *ns) ? ns : "default", nm = name;
+  if (k == "Service") {
+    auto it = c->services.find(n);
+    if (it == c->services.end() || !it->second.erase(nm)) return KSG_ENOTFOUND;
+    return KSG_OK;
+  }
+  if (k != "ReplicationController" && k != "ReplicaSet" && k != "StatefulSet") return KSG_EINVAL;
+  return c->owners.erase({k, n, nm}) ? KSG_OK : KSG_ENOTFOUND;
+}
+
 int ksgo_upsert_namespace(ksgo_ctx* c, const char* json, size_t len) {
   try {
     Namespace ns;
@@ -1681,8 +1810,21 @@ int ksgo_node_name(const ksgo_ctx* c, int32_t index, char* buf, size_t cap) {
 
 int ksgo_pod_compile(ksgo_ctx* c, const char* json, size_t len, int32_t* handle) {
   try {
+    mj::Value v = mj::parse(json, len);
     auto p = std::make_unique<Pod>();
-    if (!decode_pod(mj::parse(json, len), p.get(), &c->err)) return KSG_EINVAL;
+    if (!decode_pod(v, p.get(), &c->err)) return KSG_EINVAL;
+    // the contract's plugin set: volume plugins / DynamicResources would not Skip their PreFilter for
+    // these pods (volume_binding.go:350-358, nodevolumelimits/csi.go:239-249, volume_restrictions.go:
+    // 168-197, dynamicresources.go:446-479), so the pod is declined as the product declines it
+    if (auto sp = v.has("spec")) {
+      if (auto vols = sp->has("volumes"))
+        for (auto& vol : vols->arr)
+          for (const char* k : {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "cinder",
+                                "azureDisk", "azureFile", "vsphereVolume", "portworxVolume", "rbd", "iscsi"})
+            if (vol.has(k)) { c->err = std::string("volume needs ") + k + " plugins"; return KSG_ENOTSUP; }
+      if (auto rc = sp->has("resourceClaims"))
+        if (rc->is_arr() && !rc->arr.empty()) { c->err = "resourceClaims"; return KSG_ENOTSUP; }
+    }
     int32_t h = c->nextHandle++;
     c->queue[h] = std::move(p);
     *handle = h;

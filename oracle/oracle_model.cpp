@@ -367,6 +367,43 @@ static bool rfc3339_ns(const std::string& t, int64_t* out) {
   return true;
 }
 
+TopologySpreadConstraint decode_tsc(const mj::Value& c) {
+  TopologySpreadConstraint t;
+  t.maxSkew = (int32_t)c.i64("maxSkew");
+  t.topologyKey = c.str("topologyKey");
+  t.whenUnsatisfiable = c.str("whenUnsatisfiable");
+  t.labelSelector = decode_label_selector(c.get("labelSelector"));
+  if (c.has("minDomains")) { t.hasMinDomains = true; t.minDomains = (int32_t)c.i64("minDomains"); }
+  t.nodeAffinityPolicy = c.str("nodeAffinityPolicy");
+  t.nodeTaintsPolicy = c.str("nodeTaintsPolicy");
+  t.matchLabelKeys = decode_strs(c.get("matchLabelKeys"));
+  return t;
+}
+
+bool decode_selector_object(const mj::Value& v, SelectorObject* out, std::string* err) {
+  *out = SelectorObject{};
+  out->kind = v.str("kind");
+  if (out->kind != "Service" && out->kind != "ReplicationController" && out->kind != "ReplicaSet" &&
+      out->kind != "StatefulSet") {
+    *err = "unsupported kind " + out->kind;
+    return false;
+  }
+  const mj::Value* md = v.has("metadata");
+  if (!md || md->str("name").empty()) { *err = "object without name"; return false; }
+  out->name = md->str("name");
+  out->ns = md->str("namespace", "default");
+  if (out->ns.empty()) out->ns = "default";
+  const mj::Value* sp = v.has("spec");
+  const mj::Value* sel = sp ? sp->has("selector") : nullptr;
+  if (out->kind == "Service" || out->kind == "ReplicationController") {
+    out->hasMap = sel != nullptr;
+    out->map = decode_labels(sel);
+  } else {
+    out->sel = decode_label_selector(sel);
+  }
+  return true;
+}
+
 bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
   *out = Pod{};
   const mj::Value* md = v.has("metadata");
@@ -378,6 +415,14 @@ bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
   if (out->uid.empty()) out->uid = out->ns + "/" + out->name;
   out->labels = decode_labels(md->get("labels"));
   out->terminating = md->has("deletionTimestamp") != nullptr;
+  if (auto refs = md->has("ownerReferences"))
+    for (auto& r : refs->arr)
+      if (!out->hasController && r.boolean("controller")) {
+        out->hasController = true;
+        out->ownerAPIVersion = r.str("apiVersion");
+        out->ownerKind = r.str("kind");
+        out->ownerName = r.str("name");
+      }
   if (const mj::Value* st = v.has("status")) {
     std::string t = st->str("startTime");
     if (!t.empty()) {
@@ -452,18 +497,7 @@ bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
   if (auto rs = sp->has("resources"))
     if (!decode_reslist(rs->get("requests"), &out->podRequests, err)) return false;
   if (auto tsc = sp->has("topologySpreadConstraints"))
-    for (auto& c : tsc->arr) {
-      TopologySpreadConstraint t;
-      t.maxSkew = (int32_t)c.i64("maxSkew");
-      t.topologyKey = c.str("topologyKey");
-      t.whenUnsatisfiable = c.str("whenUnsatisfiable");
-      t.labelSelector = decode_label_selector(c.get("labelSelector"));
-      if (c.has("minDomains")) { t.hasMinDomains = true; t.minDomains = (int32_t)c.i64("minDomains"); }
-      t.nodeAffinityPolicy = c.str("nodeAffinityPolicy");
-      t.nodeTaintsPolicy = c.str("nodeTaintsPolicy");
-      t.matchLabelKeys = decode_strs(c.get("matchLabelKeys"));
-      out->tsc.push_back(t);
-    }
+    for (auto& c : tsc->arr) out->tsc.push_back(decode_tsc(c));
   if (auto vols = sp->has("volumes"))
     for (auto& vol : vols->arr)
       if (auto im = vol.has("image")) out->imageVolumes.push_back(im->str("reference"));

@@ -127,9 +127,23 @@ struct Pod {
   std::string preemptionPolicy;   // spec.preemptionPolicy
   std::string nominatedNodeName;  // status.nominatedNodeName
   bool terminatingByPreemption = false;  // preemption.PodTerminatingByPreemption (preemption/util.go:23-35)
+  // metav1.GetControllerOfNoCopy (apimachinery/pkg/apis/meta/v1/controller_ref.go:48-56)
+  bool hasController = false;
+  std::string ownerAPIVersion, ownerKind, ownerName;
 };
 
 struct Namespace { std::string name; Labels labels; };
+
+// v1.Service / v1.ReplicationController (spec.selector map[string]string, nil-able) and apps/v1
+// ReplicaSet / StatefulSet (spec.selector *metav1.LabelSelector): what helper.DefaultSelector lists
+struct SelectorObject {
+  std::string kind, ns, name;
+  bool hasMap = false;  // Service / RC: selector != nil
+  Labels map;
+  LabelSelectorSpec sel;  // RS / StatefulSet
+};
+bool decode_selector_object(const mj::Value& v, SelectorObject* out, std::string* err);
+TopologySpreadConstraint decode_tsc(const mj::Value& c);
 
 bool decode_node(const mj::Value& v, Node* out, std::string* err);
 bool decode_pod(const mj::Value& v, Pod* out, std::string* err);

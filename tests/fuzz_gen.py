@@ -232,3 +232,57 @@ def rand_cluster(seed, n_nodes, n_existing, cfg_index=None, topology=True):
 
 def namespaces():
     return [make_namespace(n, l) for n, l in NAMESPACES]
+
+
+# ---- PodTopologySpread default constraints: the selecting objects (helper.DefaultSelector) ------------
+OWNER_KINDS = [("apps/v1", "ReplicaSet"), ("apps/v1", "StatefulSet"), ("v1", "ReplicationController"),
+               ("extensions/v1beta1", "ReplicaSet"), ("apps/v1/x", "ReplicaSet")]
+
+
+def rand_objects(rng, n=8):
+    """Services / RCs / RSs / StatefulSets over the APPS labels, in the fuzz namespaces."""
+    out = []
+    for k in range(n):
+        kind = rng.choice(["Service", "Service", "ReplicationController", "ReplicaSet", "StatefulSet"])
+        ns = rng.choice([n for n, _ in NAMESPACES])
+        o = {"apiVersion": "apps/v1" if kind in ("ReplicaSet", "StatefulSet") else "v1", "kind": kind,
+             "metadata": {"name": f"{kind.lower()}-{k % 3}", "namespace": ns}, "spec": {}}
+        if kind in ("Service", "ReplicationController"):
+            r = rng.random()
+            if r < 0.1:
+                pass  # nil selector
+            elif r < 0.15:
+                o["spec"]["selector"] = {}
+            else:
+                sel = {"app": rng.choice(APPS)}
+                if rng.random() < 0.3:
+                    sel["tier"] = rng.choice(["fe", "be"])
+                o["spec"]["selector"] = sel
+        else:
+            sel = rand_label_selector(rng)
+            if sel is not None:
+                o["spec"]["selector"] = sel
+        out.append(o)
+    return out
+
+
+def add_owner(rng, p):
+    """A controller ownerReference naming one of rand_objects' names (which may not exist)."""
+    if rng.random() < 0.7:
+        api, kind = rng.choice(OWNER_KINDS)
+        p["metadata"]["ownerReferences"] = [{"apiVersion": api, "kind": kind, "name": f"{kind.lower()}-{rng.randint(0, 2)}",
+                                             "controller": rng.random() < 0.9}]
+    return p
+
+
+PTS_DEFAULT_CONFIGS = [
+    {},  # System defaulting: hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway
+    {"podTopologySpread": {"defaultingType": "List", "defaultConstraints": [
+        {"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule"},
+        {"maxSkew": 2, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "ScheduleAnyway"}]}},
+    {"podTopologySpread": {"defaultingType": "List", "defaultConstraints": [
+        {"maxSkew": 2, "topologyKey": "disk", "whenUnsatisfiable": "ScheduleAnyway", "nodeTaintsPolicy": "Honor"},
+        {"maxSkew": 3, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "DoNotSchedule",
+         "minDomains": 2}]}},
+    {"podTopologySpread": {"defaultingType": "List"}},
+]

@@ -467,6 +467,7 @@ CONSTS = {
     "v1.ResourceEphemeralStorage": "ephemeral-storage",
     "fwk.Success": 0, "fwk.Error": 1, "fwk.Unschedulable": 2, "fwk.UnschedulableAndUnresolvable": 3,
     "fwk.Wait": 4, "fwk.Skip": 5, "fwk.Pending": 6,
+    "config.ListDefaulting": "List", "config.SystemDefaulting": "System",
     "fwk.MaxNodeScore": 100, "framework.MaxNodeScore": 100, "fwk.MinNodeScore": 0,
     "st.PodAffinityWithRequiredReq": "req", "st.PodAffinityWithPreferredReq": "pref",
     "st.PodAffinityWithRequiredPreferredReq": "reqpref", "st.PodAntiAffinityWithRequiredReq": "req",
@@ -520,6 +521,10 @@ class Status(dict):
 
 
 MAP_TYPES = {"v1.ResourceList"}  # named map types: keys are expressions, not field names
+# typed object literals (e.g. &appsv1.ReplicaSet{...} in a test's objs) -> (apiVersion, kind)
+OBJECT_KINDS = {"v1.Service": ("v1", "Service"), "v1.ReplicationController": ("v1", "ReplicationController"),
+                "appsv1.ReplicaSet": ("apps/v1", "ReplicaSet"), "appsv1.StatefulSet": ("apps/v1", "StatefulSet")}
+GROUP_VERSIONS = {"appsv1.SchemeGroupVersion": "apps/v1", "v1.SchemeGroupVersion": "v1"}
 
 
 class Evaluator:
@@ -620,9 +625,14 @@ class Evaluator:
             out[jname] = val
         if kind == "named" and typ[1] in ("fwk.NodeScore", "framework.NodeScore"):
             return {"name": out.get("name"), "score": out.get("score", 0)}
+        if kind == "named" and typ[1] in OBJECT_KINDS:  # runtime.Object literals keep their kind
+            api, k = OBJECT_KINDS[typ[1]]
+            out = dict(out, apiVersion=api, kind=k)
         return out
 
     def call(self, fn, args, env):
+        if fn[0] == "index":  # explicit type arguments (ptr.To[int64](0), sets.New[string](...))
+            return self.call(fn[1], args, env)
         # builder method call?
         if fn[0] == "sel":
             name = None
@@ -638,6 +648,9 @@ class Evaluator:
                 return LSB()
             if name in ("ptr.To", "resource.MustParse", "int64", "int32", "int", "v1.ResourceName", "string"):
                 return self.ev(args[0], env)
+            if name is not None and name.endswith(".WithKind") and name[:-len(".WithKind")] in GROUP_VERSIONS:
+                # schema.GroupVersion.WithKind -> GroupVersionKind
+                return {"apiVersion": GROUP_VERSIONS[name[:-len(".WithKind")]], "kind": self.ev(args[0], env)}
             if name == "fmt.Sprintf":
                 vals = [self.ev(a, env) for a in args]
                 return go_sprintf(*vals)
@@ -810,8 +823,9 @@ class PodB(Builder):
         self.o["spec"]["priority"] = p
         return self
 
-    def m_OwnerReference(self, name, gvk):
-        self.o["metadata"]["ownerReferences"] = [{"name": name}]
+    def m_OwnerReference(self, name, gvk):  # wrappers.go:353-363: a controller reference
+        self.o["metadata"]["ownerReferences"] = [{"apiVersion": gvk["apiVersion"], "kind": gvk["kind"],
+                                                   "name": name, "controller": True}]
         return self
 
     def m_Toleration(self, key):

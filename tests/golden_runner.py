@@ -33,6 +33,8 @@ def build(make_backend, case):
     b = make_backend(case.get("config") or {})
     for ns in case.get("namespaces", []):
         b.upsert_namespace(ns)
+    for o in case.get("objects", []):  # Services / RCs / RSs / StatefulSets (PodTopologySpread defaults)
+        b.upsert_object(o)
     for n in case_nodes(case):
         b.add_node(n)
     for p in case.get("existing", []):
@@ -48,6 +50,12 @@ def run_case(make_backend, case):
         except KsgError:
             return []
         return ["config accepted but the reference rejects it"]
+    if case["kind"] == "config_ok":
+        try:
+            make_backend(case["config"]).close()
+        except KsgError as ex:
+            return [f"config rejected but the reference accepts it: {ex}"]
+        return []
     b = build(make_backend, case)
     if case["kind"] == "events":
         errs = run_events_case(b, case)
