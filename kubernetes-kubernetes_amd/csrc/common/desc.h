@@ -104,7 +104,8 @@ struct PtsCons {
   int32_t pref;         // k_agg_loop: where pres_base's flags live (AggRef; unused for node-local keys)
   int32_t absent;       // DF_PTS_ANYTOPO score constraints: the domain of a node without the key (the ""
                         // value's id, or an extra entry past the values), -1 otherwise
-  int32_t pad[2];
+  int32_t pbit;         // k_agg_loop score constraints: first bit of its domains in the presence vector
+  int32_t pad;
 };
 // an InterPodAffinity term of the incoming pod (interpodaffinity/filtering.go:246-283, scoring.go:81-125)
 struct IpaTerm {
@@ -498,7 +499,7 @@ constexpr int kAggGWords = 1024;   // compact shared-region words per pod (stage
 constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local histograms per pod
 constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
 constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
-constexpr int kAGran = 9;          // granules per participant per pod
+constexpr int kAGran = 12;         // granules per participant per pod
 enum AggGran : int {
   AG_Z0 = 0,   // {InterPodAffinity "any" bits}: every count of the pod is in the shared region
   AG_Z1 = 1,   // node-local DoNotSchedule constraint 0: {min count over my eligible nodes (24) | eligible nodes (20)}
@@ -507,10 +508,16 @@ enum AggGran : int {
   AG_A1 = 4,   // {max raw TaintToleration + 1 | max raw NodeAffinity + 1}
   AG_A2 = 5,   // max raw InterPodAffinity (biased, 0 = none)
   AG_A3 = 6,   // min raw InterPodAffinity (biased and reversed, 0 = none)
-  AG_B = 7,    // packed (TotalScore, pre-order) key
-  AG_BN = 8,   // the snapshot index + 1 of the workgroup's best node (every workgroup folds the
+  AG_P0 = 7,   // PodTopologySpread scoring: presence bits [0, 48) of my feasible, non-ignored nodes' domains
+  AG_P1 = 8,   // {non-ignored feasible nodes (20) | presence bits [48, 76) (28)}
+  AG_B = 9,    // packed (TotalScore, pre-order) key
+  AG_BN = 10,  // the snapshot index + 1 of the workgroup's best node (every workgroup folds the
                // chosen pod into the next pod's counts)
+  AG_PX = 11,  // PodTopologySpread raw-score {max + 1 (24) | 2^24 - 1 - min (24)} over my scored nodes
 };
+constexpr int kAggScoreCons = 2;   // k_agg_loop: ScheduleAnyway constraints of a looped pod (per-node counts in LDS)
+constexpr int kAggPresBits = 76;   // k_agg_loop: presence bits of its non-hostname score constraints' domains
+constexpr int64_t kAggPtsRawMax = ((int64_t)1 << 24) - 2;  // raw PodTopologySpread scores the granules carry
 constexpr int64_t kAggIpaBias = (int64_t)1 << 46;  // |raw InterPodAffinity| < 2^46 (host-checked)
 constexpr int kAggStamps = 16;                     // diagnostic stamps per pod (AggView::stamps)
 struct AggView {

@@ -2338,7 +2338,8 @@ __device__ __forceinline__ void agran_put(const AggView& av, int q, int w, int s
 }
 // One wave: poll granules [slot0, slot0 + NS) of every workgroup for pod q until all tags match.
 template <int NS>
-__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep]) {
+__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep],
+                                           int nact = NS) {  // only granules [slot0, slot0 + nact) are polled
   const int lane = threadIdx.x & 63;
   const int P = av.nwg;
   const unsigned long long* g = av.gran + (size_t)q * P * kAGran + slot0;
@@ -2352,7 +2353,7 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
 #pragma unroll
       for (int k = 0; k < NS; ++k) {
         unsigned long long y = want << 48;
-        if (v < P) y = __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v < P && k < nact) y = __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok &= (y >> 48) == want;
         x[k][r] = y & kPayload;
       }
@@ -2446,7 +2447,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ unsigned long long s_ball[kAggThreads / 64];  // [wave] feasibility ballots
   __shared__ int32_t s_lh[kAggLocal * kAggSlots];          // node-local histograms
   __shared__ unsigned long long s_gh[kAggGWords];          // shared-region partials, then totals
-  __shared__ uint8_t s_elig[kAggSlots];                    // DoNotSchedule eligibility bits per node
+  __shared__ uint16_t s_elig[kAggSlots];                   // eligibility per node: DoNotSchedule c (bit c),
+                                                           // ScheduleAnyway c (bit 8 + c)
+  __shared__ uint32_t s_pc[kAggScoreCons][kAggSlots];      // PodTopologySpread score: count at my node's
+                                                           // domain per constraint (~0u: the node lacks the key)
   __shared__ uint32_t s_pods[kAggPods], s_terms[kAggTerms];  // (slot | term) << 9 | node slot
   __shared__ uint32_t s_np, s_nt;
   __shared__ uint32_t s_off[kLoopMaxPods];
@@ -2456,12 +2460,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ long long s_lmin[kAggLocalCons];
   __shared__ uint32_t s_lcnt[kAggLocalCons];
   __shared__ unsigned long long s_wx[kAggThreads / 64][4];
-  __shared__ uint32_t s_wu[kAggThreads / 64][2];
+  __shared__ uint32_t s_wu[kAggThreads / 64][3];           // feasible, before the start, PTS non-ignored
+  __shared__ unsigned long long s_wp[kAggThreads / 64][2]; // PTS domain presence bits [0, 64), [64, 128)
+  __shared__ uint32_t s_psz[kAggScoreCons];                // PTS topology sizes of the pod being decided
+  __shared__ unsigned long long s_pxm[2];                  // wave 1 -> 0: its half's raw PTS max+1 / reversed min
+  __shared__ int s_px_q, s_pxd_q;                          // wave 1 -> 0: half done; wave 0 -> 1: exchange PX done
+  __shared__ int64_t s_pts_mx, s_pts_mn;                   // PTS NormalizeScore max / min of the pod
   __shared__ int s_gnode, s_pend_ls;  // the chosen node of the pod just decided; my pending list append
   __shared__ unsigned long long s_best;
   // the fold plan of pod q into pod q+1 (built while pod q is decided): what q+1's aggregation would
   // add for pod q at its node, keyed by the label slot it is counted under
-  struct FoldItem { int32_t lref, slot, cons, wt; uint32_t anyb, pad; };
+  struct FoldItem { int32_t lref, slot, cons, wt; uint32_t anyb; int32_t absent; };  // cons >= 8: score constraint
   constexpr int kFoldMax = 80;
   __shared__ FoldItem s_fi[kFoldMax];
   __shared__ int32_t s_fv[kFoldMax];  // the chosen node's value id of each item's slot
@@ -2523,6 +2532,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     gbar();
     // node role: DoNotSchedule eligibility (nodeLabelsMatchSpreadConstraints + inclusion policies,
     // podtopologyspread/common.go:43-80) and the shared domains it makes present (filtering.go:255-311)
+    const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
     for (int ls = tid; ls < kAggSlots; ls += nthr) {
       const int i = nlo + ls;
       uint32_t el = 0;
@@ -2531,7 +2541,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         for (int32_t c = 0; c < d.n_ptsf; ++c)
           if (((el >> c) & 1u) && cf[c].lref >= 0) s_gh[cf[c].pref + node_label(m, cf[c].slot, i)] = 1ull;
       }
-      s_elig[ls] = (uint8_t)el;
+      // processAllNode's node test for the ScheduleAnyway counts (scoring.go:164-181)
+      if (ls < nk * kBlock && i < m.n && d.n_ptss)
+        el |= pts_eligible(m, base, d, cs, d.n_ptss, i, (d.flags & DF_PTS_ANYTOPO) == 0) << 8;
+      s_elig[ls] = (uint16_t)el;
     }
     gbar();
     if (tid == 0) __hip_atomic_store(&s_elig_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2555,6 +2568,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           for (int32_t c = 0; c < d.n_ptsf; ++c)
             if (((el >> c) & 1u) && !lsel_empty(sp + cf[c].sel) && lsel_match(sp + cf[c].sel, pl, pn))
               add(cf[c].lref, node_label(m, cf[c].slot, n), ls, 1);
+        }
+        if (!term && pns == d.ns_id && d.n_ptss) {  // PreScore counts (scoring.go:155-189), hostname per node (:207-214)
+          const uint32_t el = s_elig[ls] >> 8;
+          for (int32_t c = 0; c < d.n_ptss; ++c) {
+            if (lsel_empty(sp + cs[c].sel) || !lsel_match(sp + cs[c].sel, pl, pn)) continue;
+            if (cs[c].hostname) add(cs[c].lref, 0, ls, 1);
+            else if ((el >> c) & 1u) add(cs[c].lref, pts_domain(m, cs[c], n), ls, 1);
+          }
         }
         if (d.n_raff) {  // affinityCounts (filtering.go:256-266)
           const IpaTerm* ts = at<IpaTerm>(base, d.raff_off);
@@ -2784,7 +2805,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     // (s_nfi was reset after the previous fold: a reset here by one lane would race the others' pushes)
     auto push = [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb) __attribute__((always_inline)) {
       const uint32_t k = atomicAdd(&s_nfi, 1u);
-      if (k < (uint32_t)kFoldMax) s_fi[k] = FoldItem{lref, slot, cons, wt, anyb, 0u};
+      if (k < (uint32_t)kFoldMax) s_fi[k] = FoldItem{lref, slot, cons, wt, anyb, -1};
     };
     // lane 0: PodTopologySpread + required affinity; 1..8 ranti; 9..16 paff; 17..24 panti; 32.. own terms
     if (gl == 0) {
@@ -2810,6 +2831,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       const IpaTerm* ts = at<IpaTerm>(base, aff ? d.paff_off : d.panti_off);
       if ((d.ipa_flags & IPA_PREF) && k2 < (aff ? d.n_paff : d.n_panti) && term_matches_pod(sp, ts[k2], pns, pl, pn))
         push(ts[k2].lref, ts[k2].slot, -1, aff ? ts[k2].weight : -ts[k2].weight, 8u);
+    } else if (gl >= 25 && gl < 25 + kAggScoreCons) {  // ScheduleAnyway constraint gl - 25 of pod q+1
+      const int c = gl - 25;
+      const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+      if (c < d.n_ptss && !term && pns == d.ns_id && !lsel_empty(sp + cs[c].sel) && lsel_match(sp + cs[c].sel, pl, pn)) {
+        const uint32_t k = atomicAdd(&s_nfi, 1u);
+        if (k < (uint32_t)kFoldMax)  // hostname: every node counts (no eligibility); else node test bit 8 + c
+          s_fi[k] = FoldItem{cs[c].lref, cs[c].slot, cs[c].hostname ? -1 : 8 + c, 1, 0u, cs[c].hostname ? 0 : cs[c].absent};
+      }
     } else if (gl >= 32 && (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE))) {
       const int32_t* own = at<int32_t>(bp, dp.own_terms_off);
       for (int k2 = gl - 32; k2 < dp.n_own_terms; k2 += 32) {
@@ -2875,6 +2904,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_bn_q = -1;
     s_a_q = -1;
     s_p2_q = -1;
+    s_px_q = -1;
+    s_pxd_q = -1;
     s_elig_q = -1;
   }
   __syncthreads();
@@ -2946,6 +2977,42 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       if (my_node) ne = eval_agg(m, lds_core(s_core, kk, tt), s_core.bwo[kk][tt], pf, base, d, my_iq, tp, t);
       const bool feas = ne.st == 0;
       const unsigned long long ballot = __ballot(feas);
+      // PodTopologySpread score inputs (scoring.go:61-115, 199-226): the count at my node's domain per
+      // constraint (the weights need exchange A's topology sizes), and the domains of my feasible,
+      // non-ignored nodes as presence bits
+      unsigned long long pb0 = 0, pb1 = 0;
+      bool pts_on = false;
+      if ((d.score_mask >> P_PTS) & 1u) {
+        const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+        const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
+        bool ign = false;
+        uint32_t cnt[kAggScoreCons];
+#pragma unroll
+        for (int c = 0; c < kAggScoreCons; ++c) {
+          cnt[c] = ~0u;
+          if (c < d.n_ptss && my_node) {
+            const int32_t v = node_label(m, cs[c].slot, my_iq);
+            if (v >= 0) cnt[c] = (uint32_t)tp.cnt(cs[c].hist_base, cs[c].lref, cs[c].hostname ? 0 : v, t);
+            else ign |= !anytopo;
+          }
+          s_pc[c][t] = cnt[c];
+        }
+        pts_on = feas && !ign;
+        if (pts_on)
+#pragma unroll
+          for (int c = 0; c < kAggScoreCons; ++c)
+            if (c < d.n_ptss && !cs[c].hostname) {
+              const int b = cs[c].pbit + pts_domain(m, cs[c], my_iq);
+              if (b < 64) pb0 |= 1ull << b;
+              else pb1 |= 1ull << (b - 64);
+            }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          pb0 |= __shfl_xor(pb0, o, 64);
+          pb1 |= __shfl_xor(pb1, o, 64);
+        }
+      }
+      const unsigned long long pball = __ballot(pts_on);
       const int lim = d.rot_start - (nlo + wave * 64);
       const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
       s_sv[t] = SlotVal{ne.fixed, (uint32_t)ne.rt, (uint32_t)ne.rna};
@@ -2965,6 +3032,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         s_ball[wave] = ballot;
         s_wu[wave][0] = (uint32_t)__popcll(ballot);
         s_wu[wave][1] = (uint32_t)__popcll(ballot & bm);
+        s_wu[wave][2] = (uint32_t)__popcll(pball);
+        s_wp[wave][0] = pb0;
+        s_wp[wave][1] = pb1;
         s_wx[wave][0] = et;
         s_wx[wave][1] = en;
         s_wx[wave][2] = ei;
@@ -2998,10 +3068,23 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           agran_put(av, q, w, AG_A1, g1);
           agran_put(av, q, w, AG_A2, bi);
           agran_put(av, q, w, AG_A3, bn);
+          if ((d.score_mask >> P_PTS) & 1u) {  // PodTopologySpread: domain presence, non-ignored count
+            uint32_t ni = 0;
+            unsigned long long p0 = 0, p1 = 0;
+            for (int v = 0; v < kAggThreads / 64; ++v) {
+              ni += s_wu[v][2];
+              p0 |= s_wp[v][0];
+              p1 |= s_wp[v][1];
+            }
+            agran_put(av, q, w, AG_P0, p0 & ((1ull << 48) - 1ull));
+            agran_put(av, q, w, AG_P1, (unsigned long long)(ni & 0xfffffu) |
+                                           ((((p0 >> 48) | (p1 << 16)) & ((1ull << 28) - 1ull)) << 20));
+          }
           wstamp(q, 1);
         }
-        unsigned long long xa[4][kMaxSweep];
-        const bool ok = agran_sweep<4>(av, q, AG_A0, xa);
+        const bool pts_q = ((d.score_mask >> P_PTS) & 1u) != 0;
+        unsigned long long xa[6][kMaxSweep];
+        const bool ok = agran_sweep<6>(av, q, AG_A0, xa, pts_q ? 6 : 4);
         uint32_t F = 0, wp = 0, bf = 0;
         unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
 #pragma unroll
@@ -3026,6 +3109,33 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         nmax = wave_max_u64(nmax);
         imax = wave_max_u64(imax);
         inmax = wave_max_u64(inmax);
+        if (pts_q) {  // the topology sizes (initPreScoreState, scoring.go:82-115)
+          uint32_t ni = 0;
+          unsigned long long p0 = 0, p1 = 0;
+#pragma unroll
+          for (int r = 0; r < kMaxSweep; ++r)
+            if (lane + 64 * r < G) {
+              ni += (uint32_t)(xa[5][r] & 0xfffffull);
+              p0 |= xa[4][r];
+              p1 |= xa[5][r] >> 20;
+            }
+          ni = wave_sum_u32(ni);
+          for (int o = 32; o > 0; o >>= 1) {
+            p0 |= __shfl_xor(p0, o, 64);
+            p1 |= __shfl_xor(p1, o, 64);
+          }
+          // bits [0, 48) in p0, [48, 76) in p1
+          if (lane < kAggScoreCons && lane < d.n_ptss) {
+            const PtsCons& pc = at<PtsCons>(base, d.ptss_off)[lane];
+            uint32_t sz = ni;  // hostname: len(filteredNodes) - len(IgnoredNodes)
+            if (!pc.hostname) {
+              sz = 0;
+              for (int bb = pc.pbit; bb < pc.pbit + pc.nvals; ++bb)
+                sz += (uint32_t)((bb < 48 ? (p0 >> bb) : (p1 >> (bb - 48))) & 1ull);
+            }
+            s_psz[lane] = sz;
+          }
+        }
         if (lane == 0) {
           s_F = F;
           s_psb = bf;
@@ -3042,6 +3152,80 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         while (__hip_atomic_load(&s_a_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
           __builtin_amdgcn_s_sleep(1);
       }
+      constexpr int kH = kAggThreads / 128;
+      if (((d.score_mask >> P_PTS) & 1u) && s_ok) {
+        // ---- PodTopologySpread.Score of my half's feasible nodes with the global topology sizes
+        // (scoring.go:199-226; k_pts_score's arithmetic), into s_pc[0]; NormalizeScore's max / min over
+        // every workgroup's scored nodes by exchange PX (scoring.go:229-268)
+        const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+        const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
+        double wt[kAggScoreCons];
+#pragma unroll
+        for (int c = 0; c < kAggScoreCons; ++c) wt[c] = c < d.n_ptss ? m.log_tab[s_psz[c] + 2] : 0.0;
+        unsigned long long hmx = 0, hmn = 0;
+#pragma unroll
+        for (int vv = 0; vv < kH; ++vv) {
+          const int v = wave * kH + vv, ls = v * 64 + lane;
+          const bool f = ((s_ball[v] >> lane) & 1ull) != 0;
+          bool ign = false;
+          double score = 0.0;
+#pragma unroll
+          for (int c = 0; c < kAggScoreCons; ++c) {
+            if (c >= d.n_ptss) continue;
+            const uint32_t cnt = s_pc[c][ls];
+            if (cnt == ~0u) {
+              ign |= !anytopo;
+              continue;
+            }
+            const double prod = (double)cnt * wt[c];
+            const double term = prod + (double)(cs[c].max_skew - 1);
+            score = score + term;
+          }
+          const bool scored = f && !ign;
+          const uint32_t raw = (uint32_t)(int64_t)round(score);  // math.Round: half away from zero
+          s_pc[0][ls] = scored ? raw : ~0u;
+          if (scored) {
+            hmx = (unsigned long long)raw + 1ull > hmx ? (unsigned long long)raw + 1ull : hmx;
+            const unsigned long long r = (1ull << 24) - 1ull - raw;
+            hmn = r > hmn ? r : hmn;
+          }
+        }
+        hmx = wave_max_u64(hmx);
+        hmn = wave_max_u64(hmn);
+        if (wave == 1) {
+          if (lane == 0) {
+            s_pxm[0] = hmx;
+            s_pxm[1] = hmn;
+            __hip_atomic_store(&s_px_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          while (__hip_atomic_load(&s_pxd_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+            __builtin_amdgcn_s_sleep(1);
+        } else {
+          while (__hip_atomic_load(&s_px_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+            __builtin_amdgcn_s_sleep(1);
+          hmx = s_pxm[0] > hmx ? s_pxm[0] : hmx;
+          hmn = s_pxm[1] > hmn ? s_pxm[1] : hmn;
+          if (lane == 0) agran_put(av, q, w, AG_PX, (hmx << 24) | hmn);
+          unsigned long long xp[1][kMaxSweep];
+          const bool okp = agran_sweep<1>(av, q, AG_PX, xp);
+          unsigned long long gx = 0, gn = 0;
+#pragma unroll
+          for (int r = 0; r < kMaxSweep; ++r)
+            if (lane + 64 * r < G) {
+              const unsigned long long a = xp[0][r] >> 24, bb = xp[0][r] & 0xffffffull;
+              gx = a > gx ? a : gx;
+              gn = bb > gn ? bb : gn;
+            }
+          gx = wave_max_u64(gx);
+          gn = wave_max_u64(gn);
+          if (lane == 0) {
+            s_pts_mx = gx ? (int64_t)gx - 1 : 0;  // maxScore starts at 0 (scoring.go:239)
+            s_pts_mn = gn ? (int64_t)(((1ull << 24) - 1ull) - gn) : 0;
+            if (!okp) s_ok = 0u;
+            __hip_atomic_store(&s_pxd_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+      }
       // ---- phase 2 over my half of the slots (wave v: ballots [4v, 4v + 4)): positions in the rotated
       // feasible list, NormalizeScore + weights, the best packed key
       const bool ok = s_ok != 0u;
@@ -3054,17 +3238,19 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       int knode = -1;
       if (ok) {
         // every LDS read of my half issued up front, then the arithmetic
-        constexpr int kH = kAggThreads / 128;
         unsigned long long ballot[kH];
         SlotVal sv[kH];
         int64_t ri[kH];
-        const bool ipa = ((d.score_mask >> P_IPA) & 1u) != 0;
+        uint32_t rp[kH];
+        const bool ipa = ((d.score_mask >> P_IPA) & 1u) != 0, pts = ((d.score_mask >> P_PTS) & 1u) != 0;
+        const int64_t pmx = s_pts_mx, pmn = s_pts_mn;
 #pragma unroll
         for (int vv = 0; vv < kH; ++vv) {
           const int v = wave * kH + vv;
           ballot[vv] = s_ball[v];
           sv[vv] = s_sv[v * 64 + lane];
           ri[vv] = ipa ? s_ri[v * 64 + lane] : 0;
+          rp[vv] = pts ? s_pc[0][v * 64 + lane] : 0u;
         }
         // branch-free: the four chains are independent, so the compiler interleaves them
 #pragma unroll
@@ -3073,7 +3259,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           const bool f = ((ballot[vv] >> lane) & 1ull) != 0;
           const uint32_t g = acc + wave_prefix_count(ballot[vv], lane);
           const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-          const int64_t total = agg_total(d, sv[vv].fixed, sv[vv].rt, sv[vv].rn, ri[vv], mx_t, mx_n, mx_i, mn_i, ipa_any);
+          int64_t total = agg_total(d, sv[vv].fixed, sv[vv].rt, sv[vv].rn, ri[vv], mx_t, mx_n, mx_i, mn_i, ipa_any);
+          if (pts && !(d.flags & DF_NO_SCORE)) {  // PodTopologySpread NormalizeScore (scoring.go:250-266)
+            const int64_t sc = rp[vv] == ~0u ? 0 : pmx == 0 ? 100 : go_div(100 * (pmx + pmn - (int64_t)rp[vv]), pmx);
+            total += sc * d.weight[P_PTS];
+          }
           const unsigned long long kv = f ? pack_best(total, pos) : 0ull;
           knode = kv > key ? nlo + ls : knode;
           key = kv > key ? kv : key;
@@ -3107,7 +3297,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           uint32_t el = 0;
           if (sp1 && wn >= 0) {
             const PodDesc& dn = *reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3]);
-            if (dn.n_ptsf) {
+            if (dn.n_ptsf || dn.n_ptss) {
               while (__hip_atomic_load(&s_elig_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q + 1)
                 __builtin_amdgcn_s_sleep(1);
               el = s_elig[wn - nlo];
@@ -3213,11 +3403,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             uint32_t any = 0;
             for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) {
               const FoldItem it = s_fi[k];
-              const int32_t v = s_fv[k];
+              const int32_t v = s_fv[k] >= 0 ? s_fv[k] : it.absent;  // absent: the "" domain (DF_PTS_ANYTOPO)
               if (v < 0 || (it.cons >= 0 && !((el >> it.cons) & 1u))) continue;
               if (it.lref >= 0) {
                 const unsigned long long old = atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
-                if (it.cons >= 0) {  // a DoNotSchedule domain count went up by one: its minimum moves
+                if (it.cons >= 0 && it.cons < 8) {  // a DoNotSchedule domain count went up by one: its minimum moves
                   const int c = it.cons;  // only if this was the minimum's one domain (one item per constraint)
                   if ((long long)old == s_pmin[c]) {
                     if (s_pmult[c] == 1u) s_pmin[c] = (long long)old + 1;

@@ -850,10 +850,28 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
   }
   for (auto* v : {&raff, &ranti, &paff, &panti})
     for (auto& t : *v) t.lref = aref(t.hist_base);
+  for (auto& pc : ptss) {
+    pc.lref = aref(pc.hist_base);
+    pc.pref = aref(pc.pres_base);
+  }
   D.agg_gwords = gwords;
   D.agg_nlocal = nlocal;
   D.agg_local_cons = local_cons;
-  out->agg_ok = ptss.empty() && nlocal <= kAggLocal && gwords <= kAggGWords && nlc <= kAggLocalCons &&
+  // ScheduleAnyway constraints in k_agg_loop: per-node counts of at most kAggScoreCons constraints in LDS,
+  // their domains as presence bits in exchange A, raw scores < 2^24 in exchange PX
+  bool pts_loop = ptss.size() <= (size_t)kAggScoreCons;
+  {
+    int32_t bits = 0;
+    double raw_bound = 0;
+    const double cnt_bound = (double)c->pt_node.size() + (double)kLoopMaxPods + 1.0;
+    for (auto& pc : ptss) {
+      pc.pbit = pc.hostname ? -1 : bits;
+      bits += pc.hostname ? 0 : pc.nvals;
+      raw_bound += cnt_bound * go_log((double)N + 3.0) + (double)pc.max_skew;
+    }
+    pts_loop = pts_loop && bits <= kAggPresBits && raw_bound < (double)kAggPtsRawMax;
+  }
+  out->agg_ok = pts_loop && nlocal <= kAggLocal && gwords <= kAggGWords && nlc <= kAggLocalCons &&
                 ptsf.size() <= (size_t)kAggMaxCons && raff.size() <= (size_t)kAggMaxTerms &&
                 ranti.size() <= (size_t)kAggMaxTerms && paff.size() <= (size_t)kAggMaxTerms &&
                 panti.size() <= (size_t)kAggMaxTerms;
@@ -960,14 +978,13 @@ bool Engine::loop_ok(const CompiledPod& p) const {
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
   return loop_bounds_ok(p);
 }
-// A pod k_agg_loop takes: any CYCLE pod without PodTopologySpread scoring, evaluation output,
-// PreFilter outcomes or sampling, whose histograms fit the loop's placement (CompiledPod::agg_ok).
+// A pod k_agg_loop takes: any CYCLE pod without evaluation output, PreFilter outcomes or sampling, whose
+// histograms and PodTopologySpread score constraints fit the loop's placement (CompiledPod::agg_ok).
 bool Engine::agg_loop_ok(const CompiledPod& p) const {
   if (p.error || !p.agg_ok) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
   if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET))
     return false;
-  if (d.score_mask & (1u << P_PTS)) return false;
   // the fold plan holds <= 8 items per kind of the next pod's constraints / terms plus one per own
   // term of the pod just placed (kFoldMax = 80 in k_agg_loop)
   if (d.n_own_terms > 4 * kAggMaxTerms) return false;

@@ -263,7 +263,10 @@ def rand_objects(rng, n=8):
             if sel is not None:
                 o["spec"]["selector"] = sel
         out.append(o)
-    return out
+    last = {}  # one object per (kind, namespace, name): a later one replaces it, as an upsert does
+    for o in out:
+        last[(o["kind"], o["metadata"]["namespace"], o["metadata"]["name"])] = o
+    return list(last.values())
 
 
 def add_owner(rng, p):

@@ -85,6 +85,7 @@ def test_default_topology_spreading_workload(native):
     nodes, init, pods, objects = default_topology_spreading(1000, 1000, 500)
     g, o = _pair(native, {}, nodes, init, objects)
     rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    assert g.kernel_stats()[3] == "k_agg_loop"  # the system-default scoring runs in the persistent loop
     for k, p in enumerate(pods):
         ro, _ = o.schedule_one(o.compile(p), assume=True)
         assert rs[k].as_tuple() == ro.as_tuple(), f"pod {k}"
@@ -104,3 +105,41 @@ def test_default_constraints_plugin_entry_points(native, seed):
         assert g.run_score_plugin(hg, "PodTopologySpread") == o.run_score_plugin(ho, "PodTopologySpread"), k
         assert g.run_score_plugin(hg, "PodTopologySpread", listed) == o.run_score_plugin(ho, "PodTopologySpread",
                                                                                          listed), k
+
+
+def _soft_pod(rng, k, names):
+    """A pod whose PodTopologySpread work is scoring only: ScheduleAnyway constraints of its own (on zone,
+    hostname or disk, some with inclusion policies), or none (then the system defaults apply)."""
+    from fuzz_gen import rand_label_selector, TOPO_KEYS
+    p = add_owner(rng, rand_pod(rng, k, names, topology=False))
+    if rng.random() < 0.5:
+        cs = []
+        for key in rng.sample(TOPO_KEYS, rng.randint(1, 2)):
+            c = {"maxSkew": rng.randint(1, 6), "topologyKey": key, "whenUnsatisfiable": "ScheduleAnyway"}
+            sel = rand_label_selector(rng)
+            if sel is not None:
+                c["labelSelector"] = sel
+            if rng.random() < 0.2:
+                c["nodeTaintsPolicy"] = "Honor"
+            cs.append(c)
+        p["spec"]["topologySpreadConstraints"] = cs
+    return p
+
+
+@pytest.mark.parametrize("seed,wg", [(0, 0), (1, 3), (2, 0), (3, 17)])
+def test_agg_loop_pts_scoring_matches_launch_path(native, seed, wg):
+    """PodTopologySpread scoring inside k_agg_loop (counts per node in LDS, topology sizes from exchange
+    A's presence bits, NormalizeScore over exchange PX) against the per-pod launch path and the oracle."""
+    rng, _, nodes, existing, names = rand_cluster(8000 + seed, n_nodes=[300, 700, 1100, 520][seed], n_existing=200)
+    objects = rand_objects(rng, 12)
+    cfg = {"loopWorkgroups": wg} if wg else {}
+    g, o = _pair(native, cfg, nodes, existing, objects)
+    g2, _ = _pair(native, dict(cfg, aggLoop=False), nodes, existing, objects)
+    pods = [_soft_pod(rng, k, names) for k in range(160)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    assert g.kernel_stats()[3] == "k_agg_loop"
+    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple() == rs2[k].as_tuple(), f"seed {seed} pod {k}"
+    assert g.compare_mirror(sync=False) == (0, -1)
