@@ -65,6 +65,8 @@ def parse():
                     help="sharded: the per-pod RCCL all-reduce path for every pod (default: the loop's device exchange)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the multi-core CPU baseline (the reference's default parallelism is 16)")
+    ap.add_argument("--extra-config", default=None,
+                    help="JSON merged into the scheduler config (diagnostics / A-B runs, e.g. '{\"loopUnit\": 256}')")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
@@ -192,6 +194,8 @@ def main():
         """Scheduler with the cluster loaded, warm-up batches run (then forgotten, so the timed run
         starts from the config state); None if the warm-up failed on this rank."""
         cfg = {"device": local, "kernelTimingStride": a.timing_stride, "percentageOfNodesToScore": a.pct}
+        if a.extra_config:
+            cfg.update(json.loads(a.extra_config))
         if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
             obj = [comm_unique_id() if rank == 0 else None]
             if dist is not None:

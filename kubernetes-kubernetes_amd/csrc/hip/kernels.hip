@@ -1656,16 +1656,19 @@ __device__ __forceinline__ int64_t loop_total(const PodDesc& d, int64_t fixed, i
 // The loop's node cores live in LDS (structure of arrays, [block of my range][slot]): the
 // evaluation waves read them every pod, the committing thread applies the AssumePod to them and
 // to the mirror alike, and the selection wave reads its candidate's core for the pre-evaluation.
-struct LoopCores {
-  int64_t acpu[kLoopMaxBlk][kBlock], amem[kLoopMaxBlk][kBlock], aeph[kLoopMaxBlk][kBlock];
-  int64_t rcpu[kLoopMaxBlk][kBlock], rmem[kLoopMaxBlk][kBlock], reph[kLoopMaxBlk][kBlock];
-  int64_t nzcpu[kLoopMaxBlk][kBlock], nzmem[kLoopMaxBlk][kBlock];
-  int64_t bwo[kLoopMaxBlk][kBlock];  // BalancedAllocation without the pod (pod-independent)
-  int32_t apods[kLoopMaxBlk][kBlock], npods[kLoopMaxBlk][kBlock];
-  uint32_t flags[kLoopMaxBlk][kBlock], tlo[kLoopMaxBlk][kBlock], thi[kLoopMaxBlk][kBlock];
-  uint32_t ilo[kLoopMaxBlk][kBlock], ihi[kLoopMaxBlk][kBlock];
+template <int U>
+struct LoopCoresT {
+  int64_t acpu[kLoopMaxBlk][U], amem[kLoopMaxBlk][U], aeph[kLoopMaxBlk][U];
+  int64_t rcpu[kLoopMaxBlk][U], rmem[kLoopMaxBlk][U], reph[kLoopMaxBlk][U];
+  int64_t nzcpu[kLoopMaxBlk][U], nzmem[kLoopMaxBlk][U];
+  int64_t bwo[kLoopMaxBlk][U];  // BalancedAllocation without the pod (pod-independent)
+  int32_t apods[kLoopMaxBlk][U], npods[kLoopMaxBlk][U];
+  uint32_t flags[kLoopMaxBlk][U], tlo[kLoopMaxBlk][U], thi[kLoopMaxBlk][U];
+  uint32_t ilo[kLoopMaxBlk][U], ihi[kLoopMaxBlk][U];
 };
-__device__ __forceinline__ NodeCore lds_core(const LoopCores& L, int kk, int t) {
+using LoopCores = LoopCoresT<kBlock>;  // k_agg_loop's layout (256-node blocks)
+template <int U>
+__device__ __forceinline__ NodeCore lds_core(const LoopCoresT<U>& L, int kk, int t) {
   NodeCore c;
   c.acpu = L.acpu[kk][t];
   c.amem = L.amem[kk][t];
@@ -1684,7 +1687,8 @@ __device__ __forceinline__ NodeCore lds_core(const LoopCores& L, int kk, int t) 
   c.ihi = L.ihi[kk][t];
   return c;
 }
-__device__ __forceinline__ void lds_put_dynamic(LoopCores& L, int kk, int t, const NodeCore& c) {
+template <int U>
+__device__ __forceinline__ void lds_put_dynamic(LoopCoresT<U>& L, int kk, int t, const NodeCore& c) {
   L.rcpu[kk][t] = c.rcpu;
   L.rmem[kk][t] = c.rmem;
   L.reph[kk][t] = c.reph;
@@ -1720,31 +1724,34 @@ __device__ __forceinline__ bool post_ok(const PodDesc& d, const PodDesc& nd) {
   return (d.flags & DF_ASSUME) && (nd.flags & DF_FAST) && !(((nd.filter_mask >> P_PORTS) & 1u) && d.n_pod_ports > 0);
 }
 
-constexpr int kLoopThreads = kBlock + 128;  // four evaluation waves, one selection wave, one helper wave
+constexpr int kLoopThreads = kBlock + 128;  // NW = 4: four evaluation waves, one selection wave, one helper wave
 
 // Role of each hardware wave of a k_sched_loop workgroup (roles: 0-3 evaluation, 4 selection, 5 helper).
 // A workgroup's waves go to the CU's four SIMDs round robin, so waves w and w + 4 share a SIMD:
 // map 0 pairs the selection wave with evaluation wave 0, map 1 with the helper, map 2 runs it alone
 // (two evaluation waves then share a SIMD).
 __constant__ int8_t kWaveMap[3][kLoopThreads / 64] = {{0, 1, 2, 3, 4, 5}, {4, 0, 1, 2, 5, 3}, {0, 1, 4, 3, 5, 2}};
-__global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
+template <int NW>
+__global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
+  constexpr int U = NW * 64;                  // nodes per unit: one per evaluation-wave lane
+  constexpr int kLoopThreads = U + 128;       // NW evaluation waves, one selection wave, one helper wave
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
-  __shared__ LoopCores s_core;
-  __shared__ unsigned long long s_ball[2][kLoopMaxBlk][kBlock / 64];  // [pod parity]
+  __shared__ LoopCoresT<U> s_core;
+  __shared__ unsigned long long s_ball[2][kLoopMaxBlk][NW];  // [pod parity]
   // phase-1 slots: weighted fixed score, raw TaintToleration / NodeAffinity scores (< 2^31, host-checked)
-  __shared__ int64_t s_fx[2][kLoopMaxBlk][kBlock];
-  __shared__ uint32_t s_rt[2][kLoopMaxBlk][kBlock], s_rn[2][kLoopMaxBlk][kBlock];
+  __shared__ int64_t s_fx[2][kLoopMaxBlk][U];
+  __shared__ uint32_t s_rt[2][kLoopMaxBlk][U], s_rn[2][kLoopMaxBlk][U];
   // the same for pod q+1 on each node as if pod q were assumed there (default-plugin pods): the
   // chosen node's next evaluation is ready when the winner is known
-  __shared__ int64_t s_fx2[kLoopMaxBlk][kBlock], s_bwo2[kLoopMaxBlk][kBlock];
-  __shared__ uint32_t s_rt2[kLoopMaxBlk][kBlock], s_rn2[kLoopMaxBlk][kBlock];
-  __shared__ unsigned long long s_ball2[kLoopMaxBlk][kBlock / 64];
-  __shared__ uint32_t s_u[2][2][kBlock / 64];
-  __shared__ unsigned long long s_x[2][2][kBlock / 64];
+  __shared__ int64_t s_fx2[kLoopMaxBlk][U], s_bwo2[kLoopMaxBlk][U];
+  __shared__ uint32_t s_rt2[kLoopMaxBlk][U], s_rn2[kLoopMaxBlk][U];
+  __shared__ unsigned long long s_ball2[kLoopMaxBlk][NW];
+  __shared__ uint32_t s_u[2][2][NW];
+  __shared__ unsigned long long s_x[2][2][NW];
   __shared__ uint32_t s_off[kLoopMaxPods], s_len[kLoopMaxPods];  // the run's program offsets / sizes
   __shared__ uint32_t s_ok, s_F, s_cand_ok;
   __shared__ int s_win, s_cand_q, s_cand_node, s_ipa, s_gnode;
-  __shared__ unsigned long long s_tm[2][kBlock], s_tn[2][kBlock];  // per-slot maxima of phase 1 (encoded)
+  __shared__ unsigned long long s_tm[2][U], s_tn[2][U];  // per-slot maxima of phase 1 (encoded)
   __shared__ uint32_t s_e_done;  // evaluation waves that finished a phase 1 (monotonic)
   // the candidate's state if it wins, prepared by the helper wave: its core columns with the pod
   // added, and its evaluation wave's exchange-A partials for the next pod
@@ -1755,22 +1762,26 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   __shared__ unsigned long long s_best;
   const int w = blockIdx.x, G = lv.nwg;
   const int gid = lv.rank * G + w, P = lv.world * G;  // my participant index, participants (rank-major)
-  const int k0 = lv.blk0 + (int)((int64_t)lv.nblk * w / G), k1 = lv.blk0 + (int)((int64_t)lv.nblk * (w + 1) / G);
+  // my node units [k0, k1) of the rank's range (lv.blk0 / lv.nblk count 256-node blocks)
+  const int ub0 = lv.blk0 * (kBlock / U), unb = lv.nblk * (kBlock / U);
+  const int k0 = ub0 + (int)((int64_t)unb * w / G), k1 = ub0 + (int)((int64_t)unb * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)kWaveMap[lv.wave_map][threadIdx.x >> 6]);  // my role
+  // my role (NW = 2: one wave per SIMD, no placement to choose)
+  const int wave = NW == 4 ? __builtin_amdgcn_readfirstlane((int)kWaveMap[lv.wave_map][threadIdx.x >> 6])
+                           : (int)(threadIdx.x >> 6);
   const int vt = wave * 64 + lane;           // my thread index in role order
-  const bool sel = wave == kBlock / 64;      // the selection wave: exchanges + phase 2
-  const bool hlp = wave == kBlock / 64 + 1;  // the helper wave: candidate pre-evaluation + staging
+  const bool sel = wave == NW;      // the selection wave: exchanges + phase 2
+  const bool hlp = wave == NW + 1;  // the helper wave: candidate pre-evaluation + staging
   const int t = vt;                          // evaluation waves: my slot in each block of my range
   auto stamp_s = [&](int q, int k) {       // diagnostic phase stamps: WG 0's selection lane 0
-    if (lv.stamps && w == 0 && vt == kBlock) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    if (lv.stamps && w == 0 && vt == U) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
 
-  if (t < kBlock) {  // evaluation waves
+  if (t < U) {  // evaluation waves
 #pragma unroll
     for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
-      const int i = (k0 + kk) * kBlock + t;
+      const int i = (k0 + kk) * U + t;
       if (kk < nk && i < m.n) {
         const NodeCore c = load_core(m, i);
         s_core.acpu[kk][t] = c.acpu;
@@ -1801,7 +1812,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   unsigned long long t_mt = 0, t_mn = 0;
   uint32_t w_cnt = 0, w_below = 0;
   auto below_mask = [&](int kk, int srot) __attribute__((always_inline)) -> unsigned long long {
-    const int lim = srot - ((k0 + kk) * kBlock + wave * 64);
+    const int lim = srot - ((k0 + kk) * U + wave * 64);
     return lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
   };
   auto publish_partials = [&](int par) __attribute__((always_inline)) {
@@ -1844,7 +1855,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
 #pragma unroll
     for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
       if (kk < nk) {
-        const int i = (k0 + kk) * kBlock + t;
+        const int i = (k0 + kk) * U + t;
         NodeEval ne{1u, false, 0, 0, 0, 0};
         if (post) {  // both evaluations, independent chains the compiler interleaves
           NodeEval ne2{1u, false, 0, 0, 0, 0};
@@ -1885,10 +1896,10 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
       if (kk < nk) {
         // every LDS read of the block issued up front (unconditional), then the arithmetic
-        unsigned long long ballot[kBlock / 64];
-        int64_t fx[kBlock / 64], rt[kBlock / 64], rn[kBlock / 64];
+        unsigned long long ballot[NW];
+        int64_t fx[NW], rt[NW], rn[NW];
 #pragma unroll
-        for (int v = 0; v < kBlock / 64; ++v) {
+        for (int v = 0; v < NW; ++v) {
           ballot[v] = s_ball[par][kk][v];
           if (v >= vlo && v < vhi) {
             fx[v] = s_fx[par][kk][v * 64 + lane];
@@ -1897,13 +1908,13 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
           }
         }
 #pragma unroll
-        for (int v = 0; v < kBlock / 64; ++v) {  // branch-free: independent chains interleave
+        for (int v = 0; v < NW; ++v) {  // branch-free: independent chains interleave
           if (v >= vlo && v < vhi) {
             const bool f = ((ballot[v] >> lane) & 1ull) != 0;
             const uint32_t g = acc + wave_prefix_count(ballot[v], lane);
             const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
             const unsigned long long kv = f ? pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos) : 0ull;
-            *knode = kv > *key ? (k0 + kk) * kBlock + v * 64 + lane : *knode;
+            *knode = kv > *key ? (k0 + kk) * U + v * 64 + lane : *knode;
             *key = kv > *key ? kv : *key;
           }
           acc += (uint32_t)__popcll(ballot[v]);
@@ -1916,7 +1927,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
   auto publish_a = [&](int pq, int par) __attribute__((always_inline)) {
     uint32_t c = 0, bl = 0;
     unsigned long long a = 0, bb = 0;
-    for (int v = 0; v < kBlock / 64; ++v) {
+    for (int v = 0; v < NW; ++v) {
       c += s_u[par][0][v];
       bl += s_u[par][1][v];
       a = s_x[par][0][v] > a ? s_x[par][0][v] : a;
@@ -1944,9 +1955,9 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     if (lv.npods > 1) stage_prog(lv.first_pod + 1, 1);
   }
   __syncthreads();
-  if (t < kBlock && lv.npods > 0) phase1(lv.first_pod, 0, 0, nullptr);
+  if (t < U && lv.npods > 0) phase1(lv.first_pod, 0, 0, nullptr);
   __syncthreads();
-  if (vt == kBlock && lv.npods > 0) publish_a(0, 0);
+  if (vt == U && lv.npods > 0) publish_a(0, 0);
 
   for (int q = 0; q < lv.npods; ++q) {
     if (q == lv.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
@@ -1993,7 +2004,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
       const int64_t mx_t = tmax ? (int64_t)tmax - 1 : 0, mx_n = nmax ? (int64_t)nmax - 1 : 0;
       unsigned long long key = 0;
       int knode = -1;
-      if (ok) phase2_half(0, kBlock / 64, acc, F, ps_before, mx_t, mx_n, d, par, &key, &knode);
+      if (ok) phase2_half(0, NW, acc, F, ps_before, mx_t, mx_n, d, par, &key, &knode);
       const unsigned long long wkey = wave_max_u64(key);
       const unsigned long long hold = __ballot(key == wkey && key != 0ull);
       const int cand = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
@@ -2072,12 +2083,12 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
         const PodDesc& nd = *reinterpret_cast<const PodDesc*>(nb);
         cand_ok = cand >= 0 && post_ok(d, nd) ? 1u : 0u;
         while (__hip_atomic_load(&s_e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
-               (uint32_t)(kBlock / 64) * (uint32_t)(q + 2))
+               (uint32_t)(NW) * (uint32_t)(q + 2))
           __builtin_amdgcn_s_sleep(1);
         int cw = -1;
         unsigned long long tm = 0, tn = 0;
         if (cand_ok) {  // the candidate's evaluation wave, as its partials will be if it wins
-          const int kw = cand / kBlock - k0, sl = cand % kBlock;
+          const int kw = cand / U - k0, sl = cand % U;
           cw = sl >> 6;
           const bool cf = ((s_ball2[kw][cw] >> (sl & 63)) & 1ull) != 0;
           const int64_t crt = s_rt2[kw][sl], crn = s_rn2[kw][sl];
@@ -2101,7 +2112,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
             const unsigned long long old = s_ball[npar][kw][cw];
             const unsigned long long bit = 1ull << (sl & 63);
             const unsigned long long nbal = cf ? (old | bit) : (old & ~bit);
-            const int lim = nd.rot_start - ((k0 + kw) * kBlock + cw * 64);
+            const int lim = nd.rot_start - ((k0 + kw) * U + cw * 64);
             const unsigned long long bmk = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
             s_cball = nbal;
             s_ccnt = s_u[npar][0][cw] - (uint32_t)__popcll(old) + (uint32_t)__popcll(nbal);
@@ -2113,7 +2124,7 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
         if (lane == 0) {
           uint32_t c = 0, bl = 0, cc = 0, cbl = 0;
           unsigned long long xa = 0, xb = 0, ca = 0, cb = 0;
-          for (int v = 0; v < kBlock / 64; ++v) {
+          for (int v = 0; v < NW; ++v) {
             const uint32_t u0 = s_u[npar][0][v], u1 = s_u[npar][1][v];
             const unsigned long long x0v = s_x[npar][0][v], x1v = s_x[npar][1][v];
             c += u0;
@@ -2150,21 +2161,21 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
     {
       const uint32_t F = s_F;
       const int win = s_win;
-      const int wsl = win >= 0 ? win - k0 * kBlock : -1;  // kk * kBlock + slot
+      const int wsl = win >= 0 ? win - k0 * U : -1;  // kk * U + slot
       const bool owner_wg = F > 0 && wsl >= 0 && (d.flags & DF_ASSUME);
       const int gnode = s_gnode;
       const bool remote = lv.world > 1 && F > 0 && (gnode < lv.blk0 * kBlock || gnode >= (lv.blk0 + lv.nblk) * kBlock);
       if (!owner_wg) {  // exchange A of pod q+1 already published by the selection wave
         if (F == 0) {
           if (w == 0 && t == 0) commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
-        } else if (wsl >= 0 && t == wsl % kBlock) {  // chosen here, not assumed
+        } else if (wsl >= 0 && t == wsl % U) {  // chosen here, not assumed
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, nullptr, s_ipa);
         } else if (remote && w == 0 && t == 0) {  // chosen on another rank: the result and this replica's assume
           commit_result(m, b, base, d, b.stats + pod, pod, F, gnode, s_best, nullptr, s_ipa);
         }
       } else if (s_cand_ok) {  // the helper prepared everything: LDS stores, then publish
-        if (t == wsl % kBlock) {
-          const int kw = wsl / kBlock, cw = t >> 6;
+        if (t == wsl % U) {
+          const int kw = wsl / U, cw = t >> 6;
           if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
           NodeCore c = lds_core(s_core, kw, t);
           assume_core(c, d);
@@ -2186,8 +2197,8 @@ __global__ __launch_bounds__(kLoopThreads) void k_sched_loop(MirrorView m, Batch
           if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);
         }
-      } else if (t < kBlock && wave == ((wsl % kBlock) >> 6)) {  // generic pods: re-evaluate here
-        const int kw = wsl / kBlock, owner = wsl % 64;
+      } else if (t < U && wave == ((wsl % U) >> 6)) {  // generic pods: re-evaluate here
+        const int kw = wsl / U, owner = wsl % 64;
         const uint8_t* nb = s_blob[bn];
         const PodDesc& nd = *reinterpret_cast<const PodDesc*>(nb);
         bool feas = ((s_ball[npar][kw][wave] >> lane) & 1ull) != 0;
@@ -3629,12 +3640,20 @@ hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int n
   hipLaunchKernelGGL(k_max_reduce, dim3(nb < 64 ? (nb > 0 ? nb : 1) : 64), dim3(kBlock), 0, s, dst, src, nsrc, count);
   return hipGetLastError();
 }
+// unit 128: 128-node workgroups (two evaluation waves, every role on a SIMD of its own); 256: four
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
-                             hipEvent_t t0, hipEvent_t t1) {
-  if (t0)
-    hipExtLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kLoopThreads), 0, s, t0, t1, 0, m, b, lv);
-  else
-    hipLaunchKernelGGL(k_sched_loop, dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
+                             hipEvent_t t0, hipEvent_t t1, int unit) {
+  if (unit == 128) {
+    if (t0)
+      hipExtLaunchKernelGGL(k_sched_loop<2>, dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, t0, t1, 0, m, b, lv);
+    else
+      hipLaunchKernelGGL(k_sched_loop<2>, dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
+  } else {
+    if (t0)
+      hipExtLaunchKernelGGL(k_sched_loop<4>, dim3(lv.nwg), dim3(kLoopThreads), 0, s, t0, t1, 0, m, b, lv);
+    else
+      hipLaunchKernelGGL(k_sched_loop<4>, dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
+  }
   return hipGetLastError();
 }
 hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
@@ -3654,7 +3673,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_a),            reinterpret_cast<const void*>(&k_unpack_pts),
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
-                      reinterpret_cast<const void*>(&k_sched_loop),         reinterpret_cast<const void*>(&k_sample_find),
+                      reinterpret_cast<const void*>(&k_sched_loop<4>), reinterpret_cast<const void*>(&k_sched_loop<2>),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_sample_shard_a),
                       reinterpret_cast<const void*>(&k_sample_shard_b),        reinterpret_cast<const void*>(&k_node_update),
                       reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop),

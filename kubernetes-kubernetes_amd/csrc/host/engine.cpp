@@ -43,7 +43,7 @@ hipError_t launch_commit(const MirrorView& m, const BatchView& b, const ShardVie
 hipError_t set_diag(unsigned long long* p);
 #endif
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
-                             hipEvent_t t0, hipEvent_t t1);
+                             hipEvent_t t0, hipEvent_t t1, int unit);
 hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
                            hipEvent_t t1);
 hipError_t warm_kernels();
@@ -1438,8 +1438,22 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // a single-pod call (the per-pod API) runs faster on the launch path: the loop's launch, granule
   // zeroing and LDS load of every node core cost more than two per-node launches (scripts/single_pod_probe.py)
   const bool loop_worth = comm || n > 1;
-  const bool use_loop = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && G >= 1 &&
-                        (int64_t)G * kLoopMaxBlk >= NBs && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
+  // k_sched_loop's unit: 128-node workgroups (two evaluation waves: each role on a SIMD of its own, the
+  // selection wave's phase 2 no longer shares one with phase 1) when they fit -- at most
+  // kLoopMaxBlk units per workgroup, at most 256 participants -- else 256-node workgroups
+  int GS = G, unit = 256;
+  if (c->cfg.loop_unit != 256) {
+    const int NU = 2 * NBs;  // 128-node units of the largest shard
+    int g2 = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
+    g2 = std::min(std::max(g2, (NU + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NU, 1), max_wg));
+    if ((int64_t)g2 * kLoopMaxBlk >= NU && (int64_t)g2 * W <= 256) {
+      GS = g2;
+      unit = 128;
+    }
+  }
+  const bool use_loop = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && GS >= 1 &&
+                        (int64_t)GS * kLoopMaxBlk * unit >= (int64_t)NBs * kBlock &&
+                        (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   // k_agg_loop (unsharded): the same geometry; every workgroup's LDS lists must hold its nodes' pods
   // and terms plus everything this batch can add (each pod, and its own terms, at most once)
   bool use_agg = loop_worth && !comm && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 && G <= cus &&
@@ -1477,7 +1491,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if ((rc = ensure(d_fail, 16))) return rc;
     HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
     if (c->cfg.loop_stamps) {
-      const size_t sb = (size_t)n * 8 * 8 + 64 * 8 + (size_t)n * G * 8 * 8;
+      const size_t sb = (size_t)n * 8 * 8 + 64 * 8 + (size_t)n * std::max(G, GS) * 8 * 8;
       if ((rc = ensure(d_stamps, sb))) return rc;
       HIPCHK(hipMemsetAsync(d_stamps.p, 0, sb, s));
 #ifdef KSG_DIAG
@@ -1647,7 +1661,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       LoopView lv{};
       lv.first_pod = i;
       lv.npods = j - i;
-      lv.nwg = G;
+      lv.nwg = GS;
       lv.blk0 = sblk0;
       lv.nblk = snblk;
       lv.world = W;
@@ -1659,14 +1673,15 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       lv.desc_bytes = (const uint32_t*)d_off.p + n;
       lv.give_up_at = c->cfg.debug_give_up_at;
       lv.wave_map = c->cfg.loop_wave_map;
-      lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * G * 8 : nullptr;
+      lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * GS * 8 : nullptr;
       // in-process ranks: every rank is past its allocations before any rank's first loop starts
       if (runs.empty() && comm && comm->launch_gate()) {
         c->err = comm->err;
         return KSG_EDEVICE;
       }
       const bool tl = loop_timed(runs.size());
-      HIPCHK(launch_sched_loop(m, bv, lv, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr));
+      HIPCHK(launch_sched_loop(m, bv, lv, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr,
+                               unit));
       runs.push_back({i, j - i, rb, false, tl});
       launches += j - i;
       i = j;
@@ -1967,7 +1982,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       }
 #endif
       {  // per-workgroup publish skew: max - min over workgroups of the A and B publish times
-        std::vector<unsigned long long> ws((size_t)n * G * 8);
+        std::vector<unsigned long long> ws((size_t)n * GS * 8);
         HIPCHK(hipMemcpy(ws.data(), (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64, ws.size() * 8,
                          hipMemcpyDeviceToHost));
         double ska = 0, skb = 0, ab = 0;
@@ -1975,9 +1990,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         for (auto& r : sruns)
           for (int q = r.first; q + 1 < r.first + r.count; ++q) {
             unsigned long long amin = ~0ull, amax = 0, bmin = ~0ull, bmax = 0, an = ~0ull;
-            for (int g = 0; g < G; ++g) {
-              const unsigned long long a = ws[((size_t)q * G + g) * 8], bb = ws[((size_t)q * G + g) * 8 + 1];
-              const unsigned long long a2 = ws[((size_t)(q + 1) * G + g) * 8];
+            for (int g = 0; g < GS; ++g) {
+              const unsigned long long a = ws[((size_t)q * GS + g) * 8], bb = ws[((size_t)q * GS + g) * 8 + 1];
+              const unsigned long long a2 = ws[((size_t)(q + 1) * GS + g) * 8];
               amin = std::min(amin, a); amax = std::max(amax, a);
               bmin = std::min(bmin, bb); bmax = std::max(bmax, bb);
               an = std::min(an, a2);
@@ -1990,18 +2005,18 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
           }
         {  // mean lateness of each workgroup's A publish behind the earliest; and of the workgroup
            // that owned the previous pod's chosen node
-          std::vector<double> late(G, 0.0);
+          std::vector<double> late(GS, 0.0);
           double wl = 0;
           int wn = 0, cntq = 0;
           for (auto& r : sruns)
             for (int q = r.first + 1; q < r.first + r.count; ++q) {
               unsigned long long amin = ~0ull;
-              for (int g = 0; g < G; ++g) amin = std::min(amin, ws[((size_t)q * G + g) * 8]);
+              for (int g = 0; g < GS; ++g) amin = std::min(amin, ws[((size_t)q * GS + g) * 8]);
               if (!amin) continue;
               unsigned long long amax = 0;
               int gl = -1;
-              for (int g = 0; g < G; ++g) {
-                const unsigned long long a = ws[((size_t)q * G + g) * 8];
+              for (int g = 0; g < GS; ++g) {
+                const unsigned long long a = ws[((size_t)q * GS + g) * 8];
                 late[g] += (a - amin) / 100.0;
                 if (a > amax) { amax = a; gl = g; }
               }
@@ -2013,14 +2028,14 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
           int on = 0;
           for (auto& r : sruns)
             for (int q = r.first; q + 1 < r.first + r.count; ++q)
-              for (int g = 0; g < G; ++g) {
-                const unsigned long long c0 = ws[((size_t)q * G + g) * 8 + 2], c1 = ws[((size_t)q * G + g) * 8 + 3];
+              for (int g = 0; g < GS; ++g) {
+                const unsigned long long c0 = ws[((size_t)q * GS + g) * 8 + 2], c1 = ws[((size_t)q * GS + g) * 8 + 3];
                 if (!c0 || !c1) continue;
                 unsigned long long amin = ~0ull;
-                for (int h = 0; h < G; ++h) amin = std::min(amin, ws[((size_t)(q + 1) * G + h) * 8]);
-                const unsigned long long an = ws[((size_t)(q + 1) * G + g) * 8];
-                const unsigned long long c4 = ws[((size_t)q * G + g) * 8 + 4], c5 = ws[((size_t)q * G + g) * 8 + 5];
-                const unsigned long long c6r = ws[((size_t)q * G + g) * 8 + 6], c6 = c6r & ((1ull << 60) - 1);
+                for (int h = 0; h < GS; ++h) amin = std::min(amin, ws[((size_t)(q + 1) * GS + h) * 8]);
+                const unsigned long long an = ws[((size_t)(q + 1) * GS + g) * 8];
+                const unsigned long long c4 = ws[((size_t)q * GS + g) * 8 + 4], c5 = ws[((size_t)q * GS + g) * 8 + 5];
+                const unsigned long long c6r = ws[((size_t)q * GS + g) * 8 + 6], c6 = c6r & ((1ull << 60) - 1);
                 if (c4 && c5 && c6) {
                   seg[0] += (c4 - c0) / 100.0; seg[1] += (c5 - c4) / 100.0; seg[2] += (c6 - c5) / 100.0;
                   seg[3] += (c1 - c6) / 100.0; seg[4] += (double)(c6r >> 60); segn++;
@@ -2037,7 +2052,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
             std::fprintf(stderr, "[k_sched_loop owner, us] commit+fixup %.3f  fixup end -> next A publish %.3f  "
                          "owner's next A lateness %.3f (%d pods)\n", own / on, ownx / on, ownlate / on, on);
           std::string o;
-          for (int g = 0; g < G; ++g) o += " " + std::to_string((int)(1000 * late[g] / std::max(cntq, 1)));
+          for (int g = 0; g < GS; ++g) o += " " + std::to_string((int)(1000 * late[g] / std::max(cntq, 1)));
           std::fprintf(stderr, "[k_sched_loop A lateness per workgroup, ns]%s\n", o.c_str());
           (void)wl; (void)wn;
         }

@@ -182,7 +182,8 @@ struct Config {
   int first_chunk = 32;         // pods in a pipelined batch's first chunk (the host work before the first launch)
   int loop_wave_map = 0;        // k_sched_loop role-to-wave placement (kWaveMap in kernels.hip)
   int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
-  int loop_wg = 0;              // k_sched_loop workgroups (0: min(node blocks, CUs, 128))
+  int loop_wg = 0;              // k_sched_loop workgroups (0: min(node units, CUs, 128))
+  int loop_unit = 128;          // k_sched_loop nodes per workgroup unit: 128 (when it fits) or 256 ("loopUnit")
   // sharded: the loop's per-pod exchange device-to-device (granules over xGMI).  Default on for RCCL
   // ranks (one process per GPU); in-process groups (localGroup, one device) only when asked: their
   // loops must share the device's queues, and residency of all of them at once is not guaranteed

@@ -659,3 +659,26 @@ def test_sampling_pipelined_batch(native, pct):
         for q, p in enumerate(part):
             ro, _ = o.schedule_one(o.compile(p), assume=True)
             assert rs[q].as_tuple() == ro.as_tuple(), f"pct {pct} batch {rnd} pod {q}"
+
+
+@pytest.mark.parametrize("unit,n_nodes", [(128, 5000), (256, 5000), (128, 300), (128, 1100)])
+def test_sched_loop_units_match_oracle(native, unit, n_nodes):
+    """k_sched_loop with 128-node workgroups (two evaluation waves) and with 256-node ones: SchedulingBasic
+    (every score tied: the heap pre-order rule across workgroups) and random node-local pods."""
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(n_nodes, n_nodes // 5, 300, hetero=n_nodes != 5000)
+    g, o = _pair(native, {"loopUnit": unit}, nodes, init)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    assert g.kernel_stats()[3] == "k_sched_loop"
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"pod {k}"
+    rng, cfg, nodes, existing, names = rand_cluster(9100 + n_nodes, n_nodes=n_nodes if n_nodes < 5000 else 700,
+                                                    n_existing=100, topology=False)
+    g, o = _pair(native, dict(cfg, loopUnit=unit), nodes, existing)
+    pods = [rand_pod(rng, k, names, topology=False) for k in range(200)]
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    for k, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"random pod {k}"
+    assert g.compare_mirror(sync=False) == (0, -1)
