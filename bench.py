@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c2", choices=list(WORKLOADS),
-                    help="c2 SchedulingBasic (the metric's config); c3 SchedulingPodAffinity + NodeAffinity + "
+                    help="c2 SchedulingBasic (the metric's config); c1 SchedulingBasic 500 nodes (BASELINE's CPU-reference "
+                         "config: run with --steps 1 --batch 1000); c3 SchedulingPodAffinity + NodeAffinity + "
                          "taints; c4 TopologySpreading; c4-anti PreferredPodAntiAffinity; c5 100k-node mixed "
                          "cluster; c2-hetero / c3-pa variants")
     ap.add_argument("--nodes", type=int, default=None, help="cluster nodes at N=1 (default: the config's)")
@@ -74,6 +75,7 @@ def parse():
 
 # workload -> (name, default nodes, default init pods, BASELINE configs index)
 WORKLOADS = {
+    "c1": ("SchedulingBasic", 500, 500, 0),
     "c2": ("SchedulingBasic", 5000, 1000, 1),
     "c2-hetero": ("SchedulingBasic (heterogeneous nodes)", 5000, 1000, None),
     "c3": ("SchedulingPodAffinity + NodeAffinity + taints (1 in 5 nodes foo:NoSchedule; pod-affinity / "
@@ -111,7 +113,7 @@ def usable_cpus():
     return n
 
 
-def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=()):
+def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), extra=None):
     """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
     Filter / Score loops over nodes on a pool of that many threads (the reference's
     Parallelizer.Until with parallelism 16), results identical to the sequential oracle
@@ -119,6 +121,8 @@ def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=()):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_binding import oracle
     cfg = {"cpuThreads": threads} if threads > 1 else {}
+    if threads > 1 and extra:  # pool knobs (oracle.cpp: cpuSpinUs, cpuParallelWeights)
+        cfg.update(extra)
     if pct != 100:  # the cut filter pass runs sequentially in the oracle (its Score loop stays parallel)
         cfg["percentageOfNodesToScore"] = pct
     o = oracle(cfg)
@@ -137,7 +141,17 @@ def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=()):
         results += [r.as_tuple() for r in o.schedule_batch(hs[done:done + chunk], assume=True)]
         done += min(chunk, len(hs) - done)
     dt = time.perf_counter() - t0
+    # where the cycle's time went (oracle.cpp ksgo_debug_profile): the serial share bounds the scaling
+    import ctypes
+    from oracle_binding import load
+    pr = (ctypes.c_double * 10)()
+    load().ksgo_debug_profile(ctypes.c_void_p(o.ctx), pr, 10)
+    cyc = max(pr[8], 1.0)
+    names = ["prefilter", "filter_pass", "prescore", "score_pass_normalize", "weights", "select_host", "cycle",
+             "assume", "cycles", "snapshot_update"]
+    breakdown = {k: round(pr[i] / cyc, 1) for i, k in enumerate(names) if k != "cycles"}
     o.close()
+    cpu_baseline.breakdown = breakdown  # us per pod of the last call, by cycle section
     return done / dt, done, dt, results
 
 
@@ -173,7 +187,7 @@ def main():
     n_meas = a.steps * a.batch
     n_warm = max(a.warmup, 1 if sharded else 0) * a.batch
     objects = []
-    if a.workload in ("c2", "c2-hetero"):
+    if a.workload in ("c1", "c2", "c2-hetero"):
         nodes, init, pods = synth.scheduling_basic(n_nodes, n_init, n_warm + n_meas, hetero=a.workload == "c2-hetero")
     elif a.workload == "c3":
         nodes, init, pods = synth.scheduling_c3(n_nodes, n_init, n_warm + n_meas)
@@ -288,8 +302,10 @@ def main():
             # the reference's default parallelism (16 goroutines over nodes), then one thread
             v, done, cdt, ores = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads,
                                               pct=a.pct, objects=objects)
+            bk = cpu_baseline.breakdown
             v1, done1, cdt1, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct,
                                               objects=objects)
+            bk1 = cpu_baseline.breakdown
             # every CPU the process may use (affinity mask and cgroup quota)
             ncpu = usable_cpus()
             if ncpu == a.cpu_threads:
@@ -304,8 +320,10 @@ def main():
                              f"{a.cpu_threads} threads ({cpu_model()}, {os.cpu_count()} logical CPUs visible)"
                              + ("; percentageOfNodesToScore < 100: the cut Filter pass is sequential, Score "
                                 "on the pool" if a.pct != 100 else ""),
+                   "us_per_pod_by_section": bk,
                    "single_thread": {"value": round(v1, 2), "cores": 1,
-                                     "sample": f"first {done1} pods, {cdt1:.1f} s, 1 thread"},
+                                     "sample": f"first {done1} pods, {cdt1:.1f} s, 1 thread",
+                                     "us_per_pod_by_section": bk1},
                    "all_cores": {"value": round(va, 2), "cores": ncpu,
                                  "sample": f"first {donea} pods, {cdta:.1f} s, {ncpu} threads = the CPUs this "
                                            f"process may use (affinity mask, cgroup quota)"

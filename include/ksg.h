@@ -216,8 +216,14 @@ int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uin
  * Potential nodes are taken in snapshot order (the reference iterates a map there) and checked with
  * Parallelizer parallelism 1 semantics; victims of equal priority and start time keep NodeInfo.Pods
  * order; candidates tied on every criterion resolve to the earliest in candidate-list order.
- * Pods whose victims would change their PodTopologySpread or InterPodAffinity counts return
- * KSG_ENOTSUP.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
+ * The device re-evaluates a victim's removal for NodeResourcesFit, NodePorts and the pod's
+ * PodTopologySpread / InterPodAffinity counts (RemovePod / AddPod extensions) for up to 4 spread
+ * constraints, affinity terms and topology keys.  KSG_ENOTSUP (nothing selected; ctx->err says
+ * which): a preemptor with more than 4 scalar resources; a victim whose effect on those counts is
+ * beyond that (more constraints / terms / keys, an emptied required-affinity count); and, on the
+ * host-staged record path (victims ordered by the call's clock -- pods without status.startTime --
+ * or scalar-grouped pods), any victim that changes the pod's DoNotSchedule spread counts or shares
+ * required affinity terms with it.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
  * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}] (listCandidates),
  * "selected": <node|null>, "victims": [uid...]}; *detail_len gets its length (KSG_ENOMEM if cap is
  * too small; the result is still filled). */

@@ -38,6 +38,8 @@ int ksgo_schedule_one(ksgo_ctx *ctx, int32_t handle, uint32_t flags, ksg_result 
 int ksgo_schedule_batch(ksgo_ctx *ctx, const int32_t *handles, int32_t n, uint32_t flags,
                         ksg_result *results);
 int ksgo_forget(ksgo_ctx *ctx, int32_t handle);
+/* CPU-baseline breakdown: microseconds per cycle section since the last call (see oracle.cpp) */
+int ksgo_debug_profile(ksgo_ctx *ctx, double *out, int n);
 int ksgo_run_filter_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, int32_t *prefilter_code,
                            uint8_t *codes, uint32_t *reasons);
 int ksgo_run_score_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, const uint8_t *nodes,

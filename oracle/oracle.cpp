@@ -17,6 +17,7 @@
 // Parity is pinned by the reference's own unit-test vectors (tests/golden/).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <condition_variable>
 #include <functional>
@@ -24,6 +25,7 @@
 #include <thread>
 #include <cmath>
 #include <cstring>
+#include <cstdio>
 #include <map>
 #include <memory>
 #include <set>
@@ -112,6 +114,8 @@ static int plugin_id(const std::string& n) {
 struct Config {
   int pct = 100;
   int threads = 1;  // CPU-baseline mode: Filter / Score over nodes on this many threads (Parallelizer.Until)
+  int spin_us = 50;  // CPU-baseline mode: how long an idle worker spins before parking
+  bool par_weights = false;  // CPU-baseline mode: NormalizeScore / weights on the pool too (framework.go:1409-1452)
   bool taintCompareOps = false;  // featureGates.TaintTolerationComparisonOperators
   bool enabled[KSG_NUM_PLUGINS];
   int64_t weight[KSG_NUM_PLUGINS];
@@ -160,6 +164,8 @@ static bool decode_config(const mj::Value& v, Config* c, std::string* err) {
   if (!v.is_obj()) return true;
   if (v.has("percentageOfNodesToScore")) c->pct = (int)v.i64("percentageOfNodesToScore");
   if (v.has("cpuThreads")) c->threads = std::max(1, (int)v.i64("cpuThreads"));
+  if (v.has("cpuSpinUs")) c->spin_us = std::max(0, (int)v.i64("cpuSpinUs"));
+  if (v.has("cpuParallelWeights")) c->par_weights = v.boolean("cpuParallelWeights");
   if (auto fg = v.has("featureGates")) c->taintCompareOps = fg->boolean("TaintTolerationComparisonOperators");
   if (auto w = v.has("scoreWeights"))
     for (auto& kv : w->obj) {
@@ -414,67 +420,108 @@ static Status mk(int code, uint32_t r) { Status s; s.code = code; s.reasons = r;
 // ---------------------------------------------------------------------------
 // the oracle context
 // ---------------------------------------------------------------------------
-// Fork-join pool for the CPU-baseline mode: the reference runs the per-node Filter and Score
-// loops through Parallelizer.Until with 16 goroutines (framework/parallelize/parallelism.go:28,
-// schedule_one.go:840, framework.go:1378).  Workers stay parked on a condition variable between
-// pods; run(n, fn) calls fn(k) for k in [0, n) on n threads (the caller is worker 0).
+// Worker pool for the CPU-baseline mode: the reference runs the per-node Filter and Score loops
+// through Parallelizer.Until (framework/parallelize/parallelism.go:28-76): pieces cut into chunks of
+// chunkSizeFor(n, 16) = min(sqrt(n), n/16 + 1) that workqueue.ParallelizeUntil's workers claim one at a
+// time.  Go starts those goroutines on runtime threads that stay alive and spin briefly for work, so
+// the workers here are persistent threads that spin on a generation counter for up to kSpinUs before
+// parking on a condition variable.  until(n, fn) calls fn(chunk, lo, hi) for every chunk; the caller
+// claims chunks too and returns once every chunk is done, so a worker that is still asleep delays
+// nothing (it finds the job's chunks gone: a chunk ticket carries its job's generation).
 class Pool {
  public:
-  explicit Pool(int n) : n_(n) {
-    for (int k = 1; k < n; ++k) th_.emplace_back([this, k] { loop(k); });
+  Pool(int n, int spin_us) : n_(n), spin_us_(spin_us) {
+    for (int k = 1; k < n; ++k) th_.emplace_back([this] { loop(); });
   }
   ~Pool() {
+    stop_.store(true);
     {
       std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-      ++gen_;
+      gen_.fetch_add(1);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
   int size() const { return n_; }
-  void run(const std::function<void(int)>& fn) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      fn_ = &fn;
-      left_ = n_ - 1;
-      ++gen_;
+  static int chunk_size(int n, int par) {  // parallelism.go:36-45
+    int cs = (int)std::sqrt((double)n);
+    const int r = n / par + 1;
+    if (cs > r) cs = r;
+    else if (cs < 1) cs = 1;
+    return cs;
+  }
+  int chunks(int pieces) const { return pieces <= 0 ? 0 : (pieces + chunk_size(pieces, n_) - 1) / chunk_size(pieces, n_); }
+  void until(int pieces, const std::function<void(int, int, int)>& fn) {
+    if (pieces <= 0) return;
+    const int cs = chunk_size(pieces, n_), nc = (pieces + cs - 1) / cs;
+    fn_.store(&fn, std::memory_order_relaxed);
+    pieces_.store(pieces, std::memory_order_relaxed);
+    csize_.store(cs, std::memory_order_relaxed);
+    nchunks_.store(nc, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
+    const uint64_t g = gen_.load() + 1;
+    ticket_.store(g << 32, std::memory_order_release);  // the job's chunks, claimable from here
+    gen_.store(g);  // seq_cst: pairs with a parking worker's sleepers_ increment (no lost wakeup)
+    if (sleepers_.load() > 0) {
+      { std::lock_guard<std::mutex> l(m_); }
+      cv_.notify_all();
     }
-    cv_.notify_all();
-    fn(0);
-    std::unique_lock<std::mutex> g(m_);
-    done_.wait(g, [this] { return left_ == 0; });
+    work(g);
+    while (done_.load(std::memory_order_acquire) < nc) cpu_relax();
   }
 
  private:
-  void loop(int k) {
-    uint64_t seen = 0;
+  static void cpu_relax() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+  // claim and run chunks of job `g` until none is left (or the job is not g any more)
+  void work(uint64_t g) {
+    uint64_t t = ticket_.load(std::memory_order_acquire);
     for (;;) {
-      const std::function<void(int)>* f;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        f = fn_;
-      }
-      (*f)(k);
-      std::lock_guard<std::mutex> g(m_);
-      if (--left_ == 0) done_.notify_one();
+      if ((t >> 32) != (g & 0xffffffffull)) return;
+      const int c = (int)(uint32_t)t;
+      if (c >= nchunks_.load(std::memory_order_relaxed)) return;
+      if (!ticket_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel)) continue;
+      const int cs = csize_.load(std::memory_order_relaxed), lo = c * cs;
+      (*fn_.load(std::memory_order_relaxed))(c, lo, std::min(pieces_.load(std::memory_order_relaxed), lo + cs));
+      done_.fetch_add(1, std::memory_order_release);
+      t = ticket_.load(std::memory_order_acquire);
     }
   }
-  int n_;
+  void loop() {
+    uint64_t seen = 0;  // gen_ at construction: a job posted before this thread runs is not missed
+    for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int spins = 0; gen_.load(std::memory_order_acquire) == seen; ++spins) {
+        cpu_relax();
+        if ((spins & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+          std::unique_lock<std::mutex> l(m_);
+          sleepers_.fetch_add(1);
+          cv_.wait(l, [&] { return gen_.load() != seen; });
+          sleepers_.fetch_sub(1);
+        }
+      }
+      seen = gen_.load();
+      if (stop_.load()) return;
+      work(seen);
+    }
+  }
+  int n_, spin_us_;
   std::vector<std::thread> th_;
   std::mutex m_;
-  std::condition_variable cv_, done_;
-  const std::function<void(int)>* fn_ = nullptr;
-  uint64_t gen_ = 0;
-  int left_ = 0;
-  bool stop_ = false;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0}, ticket_{0};
+  std::atomic<int> sleepers_{0}, done_{0}, pieces_{0}, csize_{1}, nchunks_{0};
+  std::atomic<bool> stop_{false};
+  std::atomic<const std::function<void(int, int, int)>*> fn_{nullptr};
 };
 
+static inline double nowus() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 struct ksgo_ctx {
   Config cfg;
+  double prof[10] = {};  // ksgo_debug_profile: microseconds per cycle section (CPU-baseline breakdown)
   std::unique_ptr<Pool> pool;  // cfg.threads > 1
   std::string err;
   std::map<std::string, Namespace> namespaces;
@@ -1353,7 +1400,9 @@ static void normalize_scores(Cycle& cy, int p, std::vector<int64_t>& sc, const s
 // schedulePod (schedule_one.go:564-618)
 // ===========================================================================
 static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out* ev) {
+  const double R0 = nowus();
   c->rebuild_list();
+  c->prof[9] += nowus() - R0;
   g_taint_compare_ops = c->cfg.taintCompareOps;
   const int N = (int)c->list.size();
   res->status = KSG_CODE_SUCCESS;
@@ -1376,7 +1425,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
   }
   auto idx_of = [](const NodeInfoO* ni) { return ni->pos; };
   if (N == 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }  // ErrNoNodesAvailable
-
+  double T0 = nowus();
   Cycle cy;
   cy.c = c;
   cy.pod = &pod;
@@ -1428,6 +1477,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     return KSG_OK;
   }
 
+  double T1 = nowus(); c->prof[0] += T1 - T0;
   // ---- nodes to evaluate (schedule_one.go:671-682; map order -> snapshot order)
   std::vector<NodeInfoO*> nodes;
   if (resultAll) nodes = c->list;
@@ -1478,17 +1528,17 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     }
   };
   if (c->pool && numToFind >= numAll) {
-    // CPU-baseline mode: contiguous ranges of the rotated order on the pool's threads, then the
-    // per-range feasible lists concatenated in order -- the sequential loop's result exactly
-    // (with every node to be found there is no early stop to race on)
-    const int T = c->pool->size();
+    // CPU-baseline mode: Parallelizer.Until's chunks of the rotated order (schedule_one.go:840), then
+    // the per-chunk feasible lists concatenated in chunk order -- the sequential loop's result
+    // exactly (with every node to be found there is no early stop to race on)
+    const int T = c->pool->chunks(numAll);
     std::vector<std::vector<NodeInfoO*>> part(T);
     std::vector<int> pfail(T, 0);
-    c->pool->run([&](int k) {
-      const int a = (int)((int64_t)numAll * k / T), b = (int)((int64_t)numAll * (k + 1) / T);
+    c->pool->until(numAll, [&](int k, int a, int b) {
       for (int i = a; i < b; ++i) {
         NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
         Status st = filter_node(ni);
+        if (part[k].empty()) part[k].reserve((size_t)(b - a));
         if (st.ok()) part[k].push_back(ni);
         else { ++pfail[k]; record_failed(ni, st); }
       }
@@ -1510,6 +1560,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
       }
     }
   }
+  double T2 = nowus(); c->prof[1] += T2 - T1;
   int processed = (int)feasible.size() + failed;
   int diagLen = failed;  // NodeToStatus.Len(): explicit per-node statuses only
   c->nextStartNodeIndex = (c->nextStartNodeIndex + processed) % N;  // :686-687
@@ -1540,55 +1591,78 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
       if (st.code == KSG_CODE_SKIP) { cy.skipScore[p] = true; continue; }
       if (!st.ok()) { res->status = KSG_CODE_ERROR; return KSG_OK; }
     }
+    c->prof[2] += nowus() - T2; T2 = nowus();
     // RunScorePlugins (framework.go:1351-1458)
     std::vector<int> active;
     for (int p : kScoreOrder)
       if (c->cfg.enabled[p] && !cy.skipScore[p]) active.push_back(p);
     std::vector<std::vector<int64_t>> scores(active.size(), std::vector<int64_t>(F, 0));
-    for (size_t a = 0; a < active.size(); ++a) {
-      int p = active[a];
-      if (c->pool) {  // CPU-baseline mode: framework.go:1378 scores nodes in parallel
-        const int T = c->pool->size();
-        std::atomic<bool> bad{false};
-        c->pool->run([&](int k) {
-          const int lo = (int)((int64_t)F * k / T), hi = (int)((int64_t)F * (k + 1) / T);
-          for (int i = lo; i < hi; ++i) {
+    if (c->pool) {  // CPU-baseline mode: one Parallelizer.Until pass over the nodes, every plugin's
+                    // Score per node (framework.go:1378-1402), then NormalizeScore per plugin
+      std::atomic<bool> bad{false};
+      c->pool->until(F, [&](int, int lo, int hi) {
+        for (int i = lo; i < hi; ++i)
+          for (size_t a = 0; a < active.size(); ++a) {
             int code;
-            scores[a][i] = score_node(cy, p, feasible[i], &code);
+            scores[a][i] = score_node(cy, active[a], feasible[i], &code);
             if (code != KSG_CODE_SUCCESS) bad = true;
           }
-        });
-        if (bad) { res->status = KSG_CODE_ERROR; return KSG_OK; }
-      } else {
+      });
+      if (bad) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+    }
+    for (size_t a = 0; a < active.size(); ++a) {
+      int p = active[a];
+      if (!c->pool) {
         for (int i = 0; i < F; ++i) {
           int code;
           scores[a][i] = score_node(cy, p, feasible[i], &code);
           if (code != KSG_CODE_SUCCESS) { res->status = KSG_CODE_ERROR; return KSG_OK; }
         }
       }
-      normalize_scores(cy, p, scores[a], feasible);
+      if (!c->pool || !c->cfg.par_weights) normalize_scores(cy, p, scores[a], feasible);
     }
-    // weights + totals (framework.go:1428-1452)
+    if (c->pool && c->cfg.par_weights)  // NormalizeScore per plugin in parallel (framework.go:1409-1423)
+      c->pool->until((int)active.size(), [&](int, int lo, int hi) {
+        for (int a = lo; a < hi; ++a) normalize_scores(cy, active[a], scores[a], feasible);
+      });
+    c->prof[3] += nowus() - T2; T2 = nowus();
+    // weights + totals (framework.go:1428-1452; in parallel over the nodes in CPU-baseline mode)
+    const bool pw = c->pool && c->cfg.par_weights;
+    if (pw) {
+      std::atomic<bool> bad{false};
+      c->pool->until(F, [&](int, int lo, int hi) {
+        for (int i = lo; i < hi; ++i)
+          for (size_t a = 0; a < active.size(); ++a) {
+            const int64_t s = scores[a][i];
+            if (s > 100 || s < 0) bad = true;
+            totals[i] += s * c->cfg.weight[active[a]];
+          }
+      });
+      if (bad) { res->status = KSG_CODE_ERROR; return KSG_OK; }
+    }
     for (size_t a = 0; a < active.size(); ++a) {
+      if (pw && !ev) break;  // done above (ev: the per-plugin record below, totals already summed)
       int p = active[a];
       if (ev) ev->score_plugin_mask |= 1u << p;
       for (int i = 0; i < F; ++i) {
         int64_t s = scores[a][i];
         if (s > 100 || s < 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }
         int64_t w = s * c->cfg.weight[p];
-        totals[i] += w;
+        if (!pw) totals[i] += w;
         if (ev && ev->plugin_scores) ev->plugin_scores[(size_t)p * N + idx_of(feasible[i])] = w;
       }
     }
   }
   if (ev && ev->total_scores)
     for (int i = 0; i < F; ++i) ev->total_scores[idx_of(feasible[i])] = totals[i];
+  c->prof[4] += nowus() - T2; T2 = nowus();
   // ---- host selection: heap.Init + heap.Pop (schedule_one.go:605-606,1054-1063)
   std::vector<HeapEnt> h(F);
   for (int i = 0; i < F; ++i) h[i] = {totals[i], 0, i};
   int win = heap_pop_index(h);
   res->node_index = idx_of(feasible[win]);
   res->total_score = totals[win];
+  c->prof[5] += nowus() - T2;
   return KSG_OK;
 }
 
@@ -1614,7 +1688,7 @@ ksgo_ctx* ksgo_create(const char* json, size_t len) {
     delete c;
     return nullptr;
   }
-  if (c->cfg.threads > 1) c->pool.reset(new Pool(c->cfg.threads));
+  if (c->cfg.threads > 1) c->pool.reset(new Pool(c->cfg.threads, c->cfg.spin_us));
   return c;
 }
 const char* ksgo_create_error(void) { return g_create_error.c_str(); }
@@ -1839,7 +1913,9 @@ int ksgo_pod_release(ksgo_ctx* c, int32_t handle) {
 int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* result, ksg_eval_out* ev) {
   auto it = c->queue.find(handle);
   if (it == c->queue.end()) return KSG_ENOTFOUND;
+  double A0 = nowus();
   int rc = run_cycle(c, *it->second, result, ev);
+  double A1 = nowus(); c->prof[6] += A1 - A0; c->prof[8] += 1;
   if (rc != KSG_OK) return rc;
   if ((flags & KSG_FLAG_ASSUME) && result->status == KSG_CODE_SUCCESS && result->node_index >= 0) {
     // Scheduler.assume (schedule_one.go:1102-1137) -> Cache.AssumePod (cache.go:397)
@@ -1852,6 +1928,15 @@ int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* r
     c->assumedUid[handle] = p.uid;
     c->pods[p.uid] = std::move(pi);
   }
+  c->prof[7] += nowus() - A1;
+  return KSG_OK;
+}
+// CPU-baseline breakdown (bench.py): totals since the last call, in microseconds -- [0] PreFilter,
+// [1] Filter pass, [2] PreScore, [3] Score pass + NormalizeScore, [4] weights, [5] selectHost,
+// [6] whole cycle, [7] assume, [8] cycles, [9] snapshot update (inside [6]); then reset
+int ksgo_debug_profile(ksgo_ctx* c, double* out, int n) {
+  for (int k = 0; k < n && k < 10; ++k) out[k] = c->prof[k];
+  for (double& v : c->prof) v = 0;
   return KSG_OK;
 }
 

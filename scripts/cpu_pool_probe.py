@@ -1,0 +1,25 @@
+"""Diagnostic: the oracle CPU baseline's scaling on this host -- pods/s and per-section us per pod for
+1 thread and for 16 threads under each pool setting (spin before parking, NormalizeScore/weights on
+the pool or not), C2 (5000 nodes) and C1 (500 nodes) shapes."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-kubernetes_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import bench  # noqa: E402
+from ksg import synth  # noqa: E402
+
+for n_nodes, n_init in ((5000, 1000), (500, 500)):
+    nodes, init, pods = synth.scheduling_basic(n_nodes, n_init, 3000)
+    v, done, dt, _ = bench.cpu_baseline(nodes, init, pods, 3.0, threads=1)
+    print(json.dumps({"nodes": n_nodes, "threads": 1, "pods_s": round(v), "sections": bench.cpu_baseline.breakdown}),
+          flush=True)
+    for spin in (0, 20, 50, 100, 300):
+        for pw in (False, True):
+            v, done, dt, _ = bench.cpu_baseline(nodes, init, pods, 2.0, threads=16,
+                                                extra={"cpuSpinUs": spin, "cpuParallelWeights": pw})
+            print(json.dumps({"nodes": n_nodes, "threads": 16, "spin_us": spin, "parallel_weights": pw,
+                              "pods_s": round(v), "sections": bench.cpu_baseline.breakdown}), flush=True)

@@ -682,3 +682,30 @@ def test_sched_loop_units_match_oracle(native, unit, n_nodes):
         ro, _ = o.schedule_one(o.compile(p), assume=True)
         assert rs[k].as_tuple() == ro.as_tuple(), f"random pod {k}"
     assert g.compare_mirror(sync=False) == (0, -1)
+
+
+@pytest.mark.parametrize("unit", [128, 256])
+def test_sched_loop_prepared_and_fixup_paths(native, unit):
+    """k_sched_loop installs the chosen node's next evaluation prepared before the winner is known
+    (default-plugin pods) or has the owner re-evaluate it (a host-port pod after a host-port pod, a
+    node-affinity pod): runs that alternate the two, with every score tied and untied, must match the
+    oracle pod by pod."""
+    from ksg.objects import PodW
+    from ksg.synth import scheduling_basic
+    for hetero in (True, False):
+        nodes, init, base = scheduling_basic(1500, 200, 180, hetero=hetero)
+        g, o = _pair(native, {"loopUnit": unit}, nodes, init)
+        pods = []
+        for k, p in enumerate(base):
+            if k % 7 in (3, 4):  # two host-port pods in a row: the second cannot be prepared
+                p = PodW(f"hp{k}", uid=f"hp{k}").container(requests={"cpu": "100m"}).host_port(8000 + k % 5).obj()
+            elif k % 11 == 5:
+                p = PodW(f"na{k}", uid=f"na{k}").container(requests={"cpu": "200m"}).node_affinity_in(
+                    "kubernetes.io/hostname", [nodes[j]["metadata"]["name"] for j in range(k % 9, 1500, 13)]).obj()
+            pods.append(p)
+        rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+        assert g.kernel_stats()[3] == "k_sched_loop"
+        for k, p in enumerate(pods):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[k].as_tuple() == ro.as_tuple(), f"unit {unit} hetero {hetero} pod {k}"
+        assert g.compare_mirror(sync=False) == (0, -1)

@@ -19,11 +19,13 @@ def _build(cfg, nodes, existing):
     return b
 
 
-@pytest.mark.parametrize("seed,threads", [(0, 2), (1, 4), (2, 16), (3, 3), (4, 16), (5, 7)])
-def test_parallel_oracle_matches_sequential(seed, threads):
+@pytest.mark.parametrize("seed,threads,pw", [(0, 2, False), (1, 4, True), (2, 16, False), (3, 3, True), (4, 16, True),
+                                             (5, 7, False)])
+def test_parallel_oracle_matches_sequential(seed, threads, pw):
+    """pw: NormalizeScore and the weights on the pool too (cpuParallelWeights)."""
     rng, cfg, nodes, existing, names = rand_cluster(seed, n_nodes=150 + 37 * seed, n_existing=60)
     seq = _build(cfg, nodes, existing)
-    par = _build(dict(cfg, cpuThreads=threads), nodes, existing)
+    par = _build(dict(cfg, cpuThreads=threads, cpuParallelWeights=pw, cpuSpinUs=0 if seed % 2 else 50), nodes, existing)
     try:
         for k in range(40):
             pod = rand_pod(rng, k, names)
@@ -41,7 +43,7 @@ def test_parallel_oracle_batch_c2_shape():
     from ksg.synth import scheduling_basic
     nodes, init, pods = scheduling_basic(600, 100, 150, hetero=True)
     seq = _build({}, nodes, init)
-    par = _build({"cpuThreads": 16}, nodes, init)
+    par = _build({"cpuThreads": 16, "cpuParallelWeights": True}, nodes, init)
     try:
         a = seq.schedule_batch([seq.compile(p) for p in pods], assume=True)
         b = par.schedule_batch([par.compile(p) for p in pods], assume=True)
