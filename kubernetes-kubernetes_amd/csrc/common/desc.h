@@ -472,6 +472,28 @@ struct ShardView {
 // ---- persistent scheduling loop (k_sched_loop) -------------------------------------
 // One launch evaluates a run of consecutive pods: `nwg` resident workgroups each own a contiguous
 // range of node blocks for the whole run and meet at two device-scope arrival counters per pod.
+// ---- the resident loop's pod ring (single-pod calls) ------------------------------
+// Host-pinned, device-mapped, fine-grained (uncached on the device).  The host posts pod q's program
+// into blob[q % kRingSlots], then one 64-bit store of ctl = {q + 1 | program bytes << 32}; the loop's
+// workgroups poll ctl, copy the program into LDS and schedule the pod; the committing thread writes
+// res[q % kRingSlots] and, last, its seq = q + 1 (system-scope release).  ctl = kRingStop ends the
+// launch; so does kLoopMaxPods pods or ring_idle of s_memrealtime ticks without a pod (the host
+// relaunches first when it has been idle for half that: the loop never outlives its process).
+constexpr int kRingSlots = 2;
+constexpr uint32_t kRingStop = 0xffffffffu;
+struct alignas(16) RingResult {
+  uint32_t seq, pad[3];
+  DevResult r;
+};
+struct alignas(128) PodRing {
+  unsigned long long ctl;  // [host] {pods posted | bytes << 32} or kRingStop
+  uint32_t pad0[30];
+  uint32_t exited;         // [device] 1: the loop left on its own (idle / pod limit)
+  uint32_t pad1[31];
+  RingResult res[kRingSlots];
+  alignas(128) uint8_t blob[kRingSlots][kBlobLds];
+};
+
 struct LoopView {
   int32_t first_pod, npods;  // pods [first_pod, first_pod + npods) of the batch
   int32_t nwg;               // workgroups of this rank (all resident; one per CU at most)
@@ -485,6 +507,8 @@ struct LoopView {
   unsigned long long* wstamps;  // diagnostic: [npods][nwg][8] exchange / owner times (nullptr)
   int32_t give_up_at;        // diagnostic: every workgroup gives up at this pod of the run (-1: never)
   int32_t wave_map;          // which hardware wave plays which role (k_sched_loop kWaveMap; 0: identity)
+  PodRing* ring;             // resident mode (nullptr: a batch run): pods arrive one by one through the ring
+  unsigned long long ring_idle;  // resident mode: s_memrealtime ticks (100 MHz) without a pod before leaving
 };
 // exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
 // A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)

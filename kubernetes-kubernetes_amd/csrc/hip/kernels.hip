@@ -1641,6 +1641,30 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
   }
 }
 
+// Resident mode: wait for pod q in the ring (one thread).  Returns the pod's program size, or -1 when
+// the launch ends (the host's stop, the pod limit, or lv.ring_idle ticks without a pod).
+__device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
+  if (q >= lv.npods) return -1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t spins = 0;; ++spins) {
+    const unsigned long long v = __hip_atomic_load(&lv.ring->ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t posted = (uint32_t)v;
+    if (posted == kRingStop) return -1;
+    if (posted > (uint32_t)q) return (int)(v >> 32);
+    if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > lv.ring_idle) {
+      if (blockIdx.x == 0) __hip_atomic_store(&lv.ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+// Resident mode: pod q's result to the host (the committing thread, after commit_result)
+__device__ __forceinline__ void ring_post(const LoopView& lv, int q, const DevResult& r) {
+  RingResult& o = lv.ring->res[q % kRingSlots];
+  o.r = r;
+  __hip_atomic_store(&o.seq, (uint32_t)(q + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // NormalizeScore + weights for the loop's plugin set (TaintToleration, NodeAffinity normalised;
 // Fit / BalancedAllocation / ImageLocality already in `fixed`) -- framework.go:1409-1452
 __device__ __forceinline__ int64_t loop_total(const PodDesc& d, int64_t fixed, int64_t rt, int64_t rn, int64_t mx_t,
@@ -1731,7 +1755,9 @@ constexpr int kLoopThreads = kBlock + 128;  // NW = 4: four evaluation waves, on
 // map 0 pairs the selection wave with evaluation wave 0, map 1 with the helper, map 2 runs it alone
 // (two evaluation waves then share a SIMD).
 __constant__ int8_t kWaveMap[3][kLoopThreads / 64] = {{0, 1, 2, 3, 4, 5}, {4, 0, 1, 2, 5, 3}, {0, 1, 4, 3, 5, 2}};
-template <int NW>
+// RING: the resident instance (pods through lv.ring, one run per pod); the batch instance has no run
+// loop at all (its one run is the whole launch), so its code is what it was before the ring existed.
+template <int NW, bool RING>
 __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
   constexpr int U = NW * 64;                  // nodes per unit: one per evaluation-wave lane
   constexpr int kLoopThreads = U + 128;       // NW evaluation waves, one selection wave, one helper wave
@@ -1760,6 +1786,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   __shared__ int s_ga_q;                  // the pod whose s_ga is ready
   __shared__ uint32_t s_ccnt, s_cbelow;
   __shared__ unsigned long long s_best;
+  __shared__ int s_ring_bytes;  // resident mode: the posted pod's program size (-1: the launch ends)
   const int w = blockIdx.x, G = lv.nwg;
   const int gid = lv.rank * G + w, P = lv.world * G;  // my participant index, participants (rank-major)
   // my node units [k0, k1) of the rank's range (lv.blk0 / lv.nblk count 256-node blocks)
@@ -1805,6 +1832,12 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     const uint32_t n16 = s_len[pod - lv.first_pod] / 16u;
     uint4* dst = reinterpret_cast<uint4*>(s_blob[slot]);
     for (uint32_t o = (uint32_t)lane; o < n16; o += 64u) dst[o] = src[o];
+  };
+  // resident mode: pod q's program from the ring (host memory: one round trip, every thread's 16 B)
+  auto stage_ring = [&](int q, int bytes) __attribute__((always_inline)) {
+    const uint4* src = reinterpret_cast<const uint4*>(lv.ring->blob[q % kRingSlots]);
+    uint4* dst = reinterpret_cast<uint4*>(s_blob[q % 3]);
+    for (uint32_t o = threadIdx.x; o < (uint32_t)bytes / 16u; o += (uint32_t)kLoopThreads) dst[o] = src[o];
   };
 
   // ---- evaluation-wave state of the pod being prepared: per-thread maxima of the normalising raw
@@ -1940,26 +1973,41 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     if (lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
   };
 
-  for (int k = vt; k < lv.npods; k += kLoopThreads) {
-    s_off[k] = b.desc_off[lv.first_pod + k];
-    s_len[k] = lv.desc_bytes[lv.first_pod + k];
-  }
+  if (!RING)
+    for (int k = vt; k < lv.npods; k += kLoopThreads) {
+      s_off[k] = b.desc_off[lv.first_pod + k];
+      s_len[k] = lv.desc_bytes[lv.first_pod + k];
+    }
   if (threadIdx.x == 0) {
     s_cand_q = -1;
     s_ga_q = -1;
     s_e_done = 0;
   }
   __syncthreads();
-  if (hlp && lv.npods > 0) {
-    stage_prog(lv.first_pod, 0);
-    if (lv.npods > 1) stage_prog(lv.first_pod + 1, 1);
+  // A batch launch is one run of pods [0, npods).  Resident mode (lv.ring): every pod is a run of its
+  // own, started when the host posts it; the pod index q (granules, stamps, results) keeps counting.
+  for (int run0 = 0;;) {
+  int run_end = lv.npods;
+  if constexpr (RING) {
+    if (threadIdx.x == 0) s_ring_bytes = ring_wait(lv, run0);
+    __syncthreads();
+    const int bytes = s_ring_bytes;
+    if (bytes < 0) return;
+    stage_ring(run0, bytes);
+    run_end = run0 + 1;
+  } else {
+    if (run0 >= run_end) return;
+    if (hlp && lv.npods > 0) {
+      stage_prog(lv.first_pod, 0);
+      if (lv.npods > 1) stage_prog(lv.first_pod + 1, 1);
+    }
   }
   __syncthreads();
-  if (t < U && lv.npods > 0) phase1(lv.first_pod, 0, 0, nullptr);
+  if (t < U) phase1(lv.first_pod + run0, run0 % 3, run0 & 1, nullptr);
   __syncthreads();
-  if (vt == U && lv.npods > 0) publish_a(0, 0);
+  if (vt == U) publish_a(run0, run0 & 1);
 
-  for (int q = 0; q < lv.npods; ++q) {
+  for (int q = run0; q < run_end; ++q) {
     if (q == lv.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
       if (threadIdx.x == 0) {
         __hip_atomic_store(lv.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1969,7 +2017,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     }
     const int pod = lv.first_pod + q, par = q & 1, npar = par ^ 1;
     const int bq = q % 3, bn = (q + 1) % 3, bs = (q + 2) % 3;
-    const bool more = q + 1 < lv.npods;
+    const bool more = q + 1 < run_end;
     const uint8_t* base = s_blob[bq];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
 
@@ -2071,7 +2119,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // both ways -- the candidate not chosen (phase 1 as it is), and chosen (its next evaluation
       // with this pod assumed, computed in phase 1 for default-plugin pods) -- so the selection
       // wave publishes the right pair as soon as exchange B resolves.
-      const bool stage = q + 2 < lv.npods;
+      const bool stage = q + 2 < run_end;
       if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
       if (stage) stage_prog(pod + 2, bs);  // s_blob[(q + 2) % 3] held pod q-1, free since the last barrier
       while (__hip_atomic_load(&s_cand_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)  // posted every pod
@@ -2167,9 +2215,13 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       const bool remote = lv.world > 1 && F > 0 && (gnode < lv.blk0 * kBlock || gnode >= (lv.blk0 + lv.nblk) * kBlock);
       if (!owner_wg) {  // exchange A of pod q+1 already published by the selection wave
         if (F == 0) {
-          if (w == 0 && t == 0) commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
+          if (w == 0 && t == 0) {
+            commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
+            if constexpr (RING) ring_post(lv, q, b.results[pod]);
+          }
         } else if (wsl >= 0 && t == wsl % U) {  // chosen here, not assumed
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, nullptr, s_ipa);
+          if constexpr (RING) ring_post(lv, q, b.results[pod]);
         } else if (remote && w == 0 && t == 0) {  // chosen on another rank: the result and this replica's assume
           commit_result(m, b, base, d, b.stats + pod, pod, F, gnode, s_best, nullptr, s_ipa);
         }
@@ -2196,6 +2248,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           s_x[npar][1][cw] = s_cmn;
           if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);
+          if constexpr (RING) ring_post(lv, q, b.results[pod]);
         }
       } else if (t < U && wave == ((wsl % U) >> 6)) {  // generic pods: re-evaluate here
         const int kw = wsl / U, owner = wsl % 64;
@@ -2206,6 +2259,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           NodeCore c = lds_core(s_core, kw, t);
           assume_core(c, d);
           commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);  // before the re-read
+          if constexpr (RING) ring_post(lv, q, b.results[pod]);
           lds_put_dynamic(s_core, kw, t, c);
           if (more) {
             const NodeEval ne = (nd.flags & DF_FAST)
@@ -2241,6 +2295,9 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     DIAG_FLUSH();
     __syncthreads();  // pod q+1's phase-1 state is final; s_blob[q % 3] is free again
     stamp_s(q, 6);
+  }
+  if constexpr (!RING) return;
+  run0 = run_end;
   }
 }
 
@@ -3643,16 +3700,21 @@ hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int n
 // unit 128: 128-node workgroups (two evaluation waves, every role on a SIMD of its own); 256: four
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
                              hipEvent_t t0, hipEvent_t t1, int unit) {
-  if (unit == 128) {
-    if (t0)
-      hipExtLaunchKernelGGL(k_sched_loop<2>, dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, t0, t1, 0, m, b, lv);
+  if (lv.ring) {  // resident (no timing events: the launch spans many calls)
+    if (unit == 128)
+      hipLaunchKernelGGL((k_sched_loop<2, true>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
     else
-      hipLaunchKernelGGL(k_sched_loop<2>, dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
+      hipLaunchKernelGGL((k_sched_loop<4, true>), dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
+  } else if (unit == 128) {
+    if (t0)
+      hipExtLaunchKernelGGL((k_sched_loop<2, false>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, t0, t1, 0, m, b, lv);
+    else
+      hipLaunchKernelGGL((k_sched_loop<2, false>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
   } else {
     if (t0)
-      hipExtLaunchKernelGGL(k_sched_loop<4>, dim3(lv.nwg), dim3(kLoopThreads), 0, s, t0, t1, 0, m, b, lv);
+      hipExtLaunchKernelGGL((k_sched_loop<4, false>), dim3(lv.nwg), dim3(kLoopThreads), 0, s, t0, t1, 0, m, b, lv);
     else
-      hipLaunchKernelGGL(k_sched_loop<4>, dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
+      hipLaunchKernelGGL((k_sched_loop<4, false>), dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
   }
   return hipGetLastError();
 }
@@ -3673,7 +3735,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_a),            reinterpret_cast<const void*>(&k_unpack_pts),
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
-                      reinterpret_cast<const void*>(&k_sched_loop<4>), reinterpret_cast<const void*>(&k_sched_loop<2>),         reinterpret_cast<const void*>(&k_sample_find),
+                      reinterpret_cast<const void*>(&k_sched_loop<4, false>), reinterpret_cast<const void*>(&k_sched_loop<2, false>),
+                      reinterpret_cast<const void*>(&k_sched_loop<4, true>), reinterpret_cast<const void*>(&k_sched_loop<2, true>),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_sample_shard_a),
                       reinterpret_cast<const void*>(&k_sample_shard_b),        reinterpret_cast<const void*>(&k_node_update),
                       reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop),

@@ -32,6 +32,11 @@ static thread_local std::string g_create_error;
     return KSG_EINVAL;                                \
   }
 
+// The resident single-pod loop holds the stream and node cores in LDS: it ends before any other use
+// of the device and before any change to the cache it mirrors (Engine::schedule_resident)
+static int with_err(ksg_ctx* ctx, int rc);
+static int quiesce(ksg_ctx* ctx) { return with_err(ctx, ctx->engine->resident_stop()); }
+
 static int with_err(ksg_ctx* ctx, int rc) {
   if (rc != KSG_OK) {
     if (!ctx->cluster->err.empty()) ctx->err = ctx->cluster->err;
@@ -104,6 +109,7 @@ int ksg_upsert_namespace(ksg_ctx* ctx, const char* ns_json, size_t len) {
   GUARD({
     NamespaceSpec ns;
     if (!decode_namespace(ns_json, len, &ns, &ctx->err)) return KSG_EINVAL;
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->cluster->upsert_namespace(ns));
   })
 }
@@ -113,6 +119,7 @@ int ksg_upsert_object(ksg_ctx* ctx, const char* obj_json, size_t len) {
   GUARD({
     SelectorObj o;
     if (!decode_selector_obj(obj_json, len, &o, &ctx->err)) return KSG_EINVAL;
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->cluster->upsert_object(std::move(o)));
   })
 }
@@ -126,6 +133,7 @@ int ksg_remove_object(ksg_ctx* ctx, const char* kind, const char* ns, const char
       return KSG_EINVAL;
     }
     const std::string n = (ns && *ns) ? ns : "default";
+    if (const int rs = quiesce(ctx)) return rs;
     const int rc = ctx->cluster->remove_object(k, n, name);
     if (rc == KSG_ENOTFOUND) ctx->err = std::string(kind) + " " + n + "/" + name + " not found";
     return with_err(ctx, rc);
@@ -137,6 +145,7 @@ int ksg_add_node(ksg_ctx* ctx, const char* node_json, size_t len) {
   GUARD({
     NodeSpec n;
     if (!decode_node(node_json, len, &n, &ctx->err)) return KSG_EINVAL;
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->cluster->add_node(std::move(n)));
   })
 }
@@ -146,13 +155,17 @@ int ksg_update_node(ksg_ctx* ctx, const char* node_json, size_t len) {
   GUARD({
     NodeSpec n;
     if (!decode_node(node_json, len, &n, &ctx->err)) return KSG_EINVAL;
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->cluster->update_node(std::move(n)));
   })
 }
 
 int ksg_remove_node(ksg_ctx* ctx, const char* name) {
   if (!ctx || !name) return KSG_EINVAL;
-  GUARD({ return with_err(ctx, ctx->cluster->remove_node(name)); })
+  GUARD({
+    if (const int rs = quiesce(ctx)) return rs;
+    return with_err(ctx, ctx->cluster->remove_node(name));
+  })
 }
 
 int ksg_add_pod(ksg_ctx* ctx, const char* pod_json, size_t len) {
@@ -164,13 +177,17 @@ int ksg_add_pod(ksg_ctx* ctx, const char* pod_json, size_t len) {
       ctx->err = "ksg_add_pod: pod is not bound (spec.nodeName empty)";
       return KSG_EINVAL;
     }
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->cluster->add_pod(p));
   })
 }
 
 int ksg_remove_pod(ksg_ctx* ctx, const char* uid) {
   if (!ctx || !uid) return KSG_EINVAL;
-  GUARD({ return with_err(ctx, ctx->cluster->remove_pod(uid)); })
+  GUARD({
+    if (const int rs = quiesce(ctx)) return rs;
+    return with_err(ctx, ctx->cluster->remove_pod(uid));
+  })
 }
 
 int ksg_num_nodes(const ksg_ctx* ctx) {
@@ -200,6 +217,8 @@ int ksg_pod_compile(ksg_ctx* ctx, const char* pod_json, size_t len, int32_t* han
       ctx->err = "pod " + p.ns + "/" + p.name + ": " + p.unsupported;
       return KSG_ENOTSUP;
     }
+    // the pod's pod-table entry (labels, affinity terms) compiled once, as NewPodInfo does at enqueue
+    ctx->cluster->pod_table_precompile(p);
     const int32_t h = ctx->engine->next_handle++;
     ctx->engine->queue[h] = std::move(p);
     *handle = h;
@@ -217,6 +236,12 @@ int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* r
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    if (!eval && (flags & KSG_FLAG_ASSUME)) {  // the resident loop (node-local pods), else the launch path
+      bool handled = false;
+      const int rc = ctx->engine->schedule_resident(it->second, handle, result, &handled);
+      if (handled) return with_err(ctx, rc);
+    }
+    if (const int rs = quiesce(ctx)) return rs;
     std::vector<const PodSpec*> pods{&it->second};
     std::vector<int32_t> hs{handle};
     return with_err(ctx, ctx->engine->run_batch(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, result, eval));
@@ -226,6 +251,7 @@ int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* r
 int ksg_schedule_batch(ksg_ctx* ctx, const int32_t* handles, int32_t n, uint32_t flags, ksg_result* results) {
   if (!ctx || n < 0 || (n && (!handles || !results))) return KSG_EINVAL;
   GUARD({
+    if (const int rs = quiesce(ctx)) return rs;
     ctx->engine->api_t0_ = std::chrono::steady_clock::now();  // loopStamps: the handle lookups' share
     std::vector<const PodSpec*> pods;
     std::vector<int32_t> hs(handles, handles + n);
@@ -244,6 +270,7 @@ int ksg_forget(ksg_ctx* ctx, int32_t handle) {  // Cache.ForgetPod (backend/cach
   GUARD({
     auto it = ctx->engine->assumed.find(handle);
     if (it == ctx->engine->assumed.end()) return KSG_ENOTFOUND;
+    if (const int rs = quiesce(ctx)) return rs;
     std::string uid = it->second;
     ctx->engine->assumed.erase(it);
     return with_err(ctx, ctx->cluster->remove_pod(uid));
@@ -256,6 +283,7 @@ int ksg_run_filter_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t*
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::FILTER_ONE, plugin, nullptr, prefilter_code,
                                                  codes, reasons, nullptr, nullptr));
   })
@@ -269,6 +297,7 @@ int ksg_preempt(ksg_ctx* ctx, int32_t handle, const char* args_json, size_t args
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
     // node-sharded contexts: every rank holds the whole mirror and pod table, so each rank runs the
     // PostFilter over every node by itself (no exchange) and returns the identical choice
+    if (const int rs = quiesce(ctx)) return rs;
     std::string d;
     const int rc = ctx->engine->preempt(it->second, args_json, args_len, result, detail ? &d : nullptr);
     if (rc) return with_err(ctx, rc);
@@ -295,6 +324,7 @@ int ksg_run_score_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, const uin
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    if (const int rs = quiesce(ctx)) return rs;
     return with_err(ctx, ctx->engine->run_plugin(it->second, Engine::SCORE_ONE, plugin, nodes, status_code, nullptr,
                                                  nullptr, raw, normalized));
   })
@@ -340,7 +370,10 @@ int ksg_last_batch_kernel_stats(const ksg_ctx* ctx, double* avg_kernel_ms, doubl
 
 int ksg_debug_compare_mirror(ksg_ctx* ctx, int32_t sync, int32_t* ndiff, int32_t* first) {
   if (!ctx || !ndiff || !first) return KSG_EINVAL;
-  GUARD(return with_err(ctx, ctx->cluster->compare_mirror(sync != 0, ndiff, first));)
+  GUARD({
+    if (const int rs = quiesce(ctx)) return rs;
+    return with_err(ctx, ctx->cluster->compare_mirror(sync != 0, ndiff, first));
+  })
 }
 
 int ksg_debug_relayouts(const ksg_ctx* ctx, uint64_t* full, uint64_t* gather) {

@@ -525,6 +525,17 @@ void Cluster::reserve_ports(int32_t extra) {
   if (view.ports && ports_need_ > view.port_slots) layout_dirty = true;
 }
 
+// The device work ensure_mirror(false) would do (re-layout, queued node updates, a pod-table upload the
+// lazy rule does not skip): the resident loop holds node cores in LDS and the mirror's addresses in its
+// arguments, so it stops before any of it (Engine::schedule_resident).
+bool Cluster::mirror_pending() {
+  order();
+  if (view.ports && std::max(ports_need_, ports_hw_) > view.port_slots) return true;
+  if (layout_dirty || !static_dirty_.empty() || !dyn_dirty_.empty()) return true;
+  if (pods_dirty && pt_dev_[0].p && pt_dev_[0].bytes >= pt_node.size() * 4 + 4) return false;
+  return pods_dirty || (int32_t)log_tab.size() < (int32_t)order_.size() + 4;
+}
+
 int Cluster::ensure_mirror(bool pods_needed) {
   order();
   ports_need_ = std::max(ports_need_, ports_hw_);  // pod events since the last cycle

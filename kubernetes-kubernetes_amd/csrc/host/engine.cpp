@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <cstddef>
 
 #include "comm.hpp"
 #include "host.hpp"
@@ -1057,6 +1058,8 @@ double Engine::agg_bytes(const PodDesc& d) const {
 }
 
 Engine::~Engine() {
+  (void)resident_stop();
+  if (ring_) (void)hipHostFree(ring_);
   for (hipEvent_t e : tev) (void)hipEventDestroy(e);
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
   for (hipEvent_t e : cev) (void)hipEventDestroy(e);
@@ -2287,6 +2290,203 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
       if (raw) raw[i] = (plugin == P_PTS && rv[i] == -1) ? 0 : rv[i];  // ignored node (scoring.go:203-205)
       if (norm) norm[i] = nv[i];
     }
+  }
+  return KSG_OK;
+}
+
+// ===================================================================================================
+// The resident single-pod loop.  kube-scheduler's scheduling goroutine calls
+// SchedulePod once per pod (schedule_one.go:67-192), so ksg_schedule_one is the hot entry point of a
+// real deployment.  A launch per call costs the loop's start (granule setup, LDS load of every node
+// core) and the HIP API's per-copy overheads; instead one k_sched_loop launch stays resident and the
+// host hands it each pod through a pinned ring (desc.h PodRing): the program and a doorbell go down,
+// the DevResult comes back, with no HIP call on the path.  The launch ends on the host's stop (any
+// other device user, or a mirror change it cannot see), after kLoopMaxPods pods (its granule indices),
+// or by itself after kResidentIdleMs without a pod -- the host relaunches once it has been idle for
+// half that, so a loop never outlives its process.
+// ===================================================================================================
+constexpr int kResidentIdleMs = 40;
+
+int Engine::resident_stop() {
+  if (c->cfg.loop_stamps && res_prof_[4] > 0) {  // where a single-pod call's time went (us per call)
+    const double n = res_prof_[4];
+    std::fprintf(stderr, "[resident loop, %d calls, us per call] compile %.2f  post %.2f  device (post -> result seen) %.2f  "
+                 "settle %.2f\n", (int)n, res_prof_[0] / n, res_prof_[1] / n, res_prof_[2] / n, res_prof_[3] / n);
+    for (double& v : res_prof_) v = 0;
+  }
+  if (!res_running_) return KSG_OK;
+  __atomic_store_n(&ring_->ctl, (unsigned long long)kRingStop, __ATOMIC_RELEASE);
+  res_running_ = false;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return KSG_OK;
+}
+
+int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res, bool* handled) {
+  using clk = std::chrono::steady_clock;
+  *handled = false;
+  if (comm || !c->cfg.resident_loop || !c->cfg.persistent_loop) return KSG_OK;
+  const int32_t N = (int32_t)c->order().size();
+  if (N == 0) return KSG_OK;
+  // the loop's geometry (run_batch's, unsharded)
+  const int NB = (N + kBlock - 1) / kBlock;
+  const int cus = cu_count > 0 ? cu_count : 256;
+  int GS = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128, unit = 256;
+  GS = std::min(std::max(GS, (NB + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NB, 1), cus));
+  if (c->cfg.loop_unit != 256) {
+    const int NU = 2 * NB;
+    int g2 = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
+    g2 = std::min(std::max(g2, (NU + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NU, 1), cus));
+    if ((int64_t)g2 * kLoopMaxBlk >= NU && g2 <= 256) {
+      GS = g2;
+      unit = 128;
+    }
+  }
+  if ((int64_t)GS * kLoopMaxBlk * unit < (int64_t)NB * kBlock) return KSG_OK;
+  if ((int64_t)c->taint_max_per_node >= ((int64_t)1 << 24) - 1) return KSG_OK;
+  // PreFilter / PreScore on the host, as run_batch's compile_upto
+  const auto T0 = clk::now();
+  CompiledPod cp;
+  int rc = compile(p, CYCLE, -1, true, false, &cp);
+  if (rc) {
+    *handled = true;
+    return rc;
+  }
+  if (cp.prefilter_error) cp.error = true;
+  if (!cp.error && !cp.prefilter_reject && (!loop_ok(cp) || cp.blob.size() % 16 != 0)) {
+    c->pod_table_drop(cp.slot);  // not a resident-loop pod: the launch path compiles it again
+    return KSG_OK;
+  }
+  *handled = true;
+  if (cp.error || cp.prefilter_reject) {  // decided on the host (run_batch's settle gives the same)
+    c->pod_table_drop(cp.slot);
+    *res = ksg_result{};
+    res->status = cp.error ? KSG_CODE_ERROR : KSG_CODE_UNSCHEDULABLE;
+    res->node_index = -1;
+    return KSG_OK;
+  }
+  const int64_t ns_before = c->next_start;
+  c->next_start = (c->next_start + cp.num_all) % (int64_t)N;  // schedule_one.go:686-687
+  auto fail = [&](int code) {
+    c->pod_table_drop(cp.slot);
+    c->next_start = ns_before;
+    return code;
+  };
+  {  // host ports this pod's assume can add to one node
+    int32_t extra = 0;
+    for (auto& k : p.containers)
+      for (auto& hp : k.ports) extra += hp.port > 0;
+    for (auto& k : p.init_containers)
+      if (k.sidecar)
+        for (auto& hp : k.ports) extra += hp.port > 0;
+    c->reserve_ports(extra);
+  }
+  hipStream_t s = c->stream;
+  // the running launch sees the mirror as it is, or it stops
+  if (res_running_ && (c->mirror_pending() || res_q_ >= kLoopMaxPods || GS != res_gs_ || unit != res_unit_ ||
+                       clk::now() - res_last_ > std::chrono::milliseconds(kResidentIdleMs / 2)))
+    if ((rc = resident_stop())) return fail(rc);
+  if (!res_running_) {
+    if ((rc = c->ensure_mirror(false))) return fail(rc);
+    if (!ring_) {
+      void* hp = nullptr;
+      if (hipHostMalloc(&hp, sizeof(PodRing), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        c->err = "resident loop: hipHostMalloc of the pod ring failed";
+        return fail(KSG_EDEVICE);
+      }
+      ring_ = (PodRing*)hp;
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+        c->err = "resident loop: the pod ring has no device address";
+        return fail(KSG_EDEVICE);
+      }
+      ring_dev_ = (PodRing*)dp;
+    }
+    std::memset((void*)ring_, 0, offsetof(PodRing, blob));
+    if ((rc = gran_setup())) return fail(rc);
+    if ((rc = ensure(d_fail, 16))) return fail(rc);
+    if ((rc = ensure_scratch(256, kLoopMaxPods, false, 0))) return fail(rc);
+    HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
+    HIPCHK(hipMemsetAsync(d_stats.p, 0, d_stats.bytes, s));  // PodStats::ipa_any = 0 for every pod
+    LoopView lv{};
+    lv.first_pod = 0;
+    lv.npods = kLoopMaxPods;
+    lv.nwg = GS;
+    lv.blk0 = 0;
+    lv.nblk = (c->view.n + kBlock - 1) / kBlock;
+    lv.world = 1;
+    lv.rank = 0;
+    if ((rc = next_gran_tag(&lv.tag))) return fail(rc);
+    lv.gran[0] = gran_all[0];
+    lv.fail = (uint32_t*)d_fail.p;
+    lv.give_up_at = -1;
+    lv.wave_map = c->cfg.loop_wave_map;
+    lv.ring = ring_dev_;
+    lv.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;  // s_memrealtime: 100 MHz
+    HIPCHK(launch_sched_loop(c->view, bview(kLoopMaxPods), lv, s, nullptr, nullptr, unit));
+    res_running_ = true;
+    res_q_ = 0;
+    res_gs_ = GS;
+    res_unit_ = unit;
+  }
+  // post the pod, wait for its result
+  const auto T1 = clk::now();
+  const int q = res_q_;
+  const uint32_t bytes = (uint32_t)cp.blob.size();
+  std::memcpy(ring_->blob[q % kRingSlots], cp.blob.data(), bytes);
+  __atomic_store_n(&ring_->ctl, (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)bytes << 32),
+                   __ATOMIC_RELEASE);
+  RingResult& rr = ring_->res[q % kRingSlots];
+  const auto tw = clk::now();
+  const auto T2 = tw;
+  for (uint64_t spins = 1; __atomic_load_n(&rr.seq, __ATOMIC_ACQUIRE) != (uint32_t)(q + 1); ++spins) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+    if ((spins & 0xfffu) == 0 && clk::now() - tw > std::chrono::seconds(5)) {  // never: fail loudly, not hang
+      __atomic_store_n(&ring_->ctl, (unsigned long long)kRingStop, __ATOMIC_RELEASE);
+      c->err = "resident loop: no result for the posted pod after 5 s";
+      return fail(KSG_EDEVICE);
+    }
+    if ((spins & 0xfffu) == 0 && hipStreamQuery(s) != hipErrorNotReady) {  // the launch ended without it
+      res_running_ = false;
+      (void)hipStreamSynchronize(s);
+      uint32_t f[4] = {0, 0, 0, 0};
+      (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
+      c->layout_dirty = true;
+      c->mirror_suspect = true;
+      c->pods_dirty = true;
+      c->err = std::string("resident loop ended without the pod's result") +
+               (f[0] ? " (an exchange granule never arrived)" : "") + "; the device mirror is rebuilt from the cache";
+      return fail(KSG_EDEVICE);
+    }
+  }
+  const DevResult d = rr.r;
+  res_q_ = q + 1;
+  res_last_ = clk::now();
+  const auto T3 = res_last_;
+  // the result and the host shadow of the device-side assume (run_batch's settle)
+  *res = ksg_result{};
+  res->status = d.status;
+  res->node_index = d.node;
+  res->feasible_nodes = d.feasible;
+  res->evaluated_nodes = cp.num_all;
+  res->total_score = d.feasible > 1 ? d.total : 0;
+  if (res->status == KSG_CODE_SUCCESS && res->node_index >= 0) {
+    std::string uid = p.uid + "#r" + std::to_string(++res_seq_);
+    if ((rc = c->add_pod(p, uid, /*device_done=*/true, cp.slot, &c->order()[(size_t)res->node_index], &cp.res)))
+      return rc;
+    assumed[handle] = uid;
+  } else {
+    c->pod_table_drop(cp.slot);
+  }
+  last_kernel = 1;
+  if (c->cfg.loop_stamps) {
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    res_prof_[0] += us(T0, T1);
+    res_prof_[1] += us(T1, T2);
+    res_prof_[2] += us(T2, T3);
+    res_prof_[3] += us(T3, clk::now());
+    res_prof_[4] += 1;
   }
   return KSG_OK;
 }

@@ -77,6 +77,16 @@ struct Spread {
   std::vector<std::string> match_label_keys;
 };
 
+// A pod's pod-table entry compiled once, when the pod is queued (Cluster::pod_table_precompile), as
+// the reference parses a pod's affinity terms once in framework.NewPodInfo (types.go:422-448): its
+// label set and each affinity term's selector programs as interned ids (stable for the context's
+// life), so reserving its slot in a batch is a copy.
+struct PodTablePre {
+  std::vector<unsigned long long> labels;
+  std::vector<int32_t> words;  // every kept term's selector, namespace selector and namespace ids
+  struct Term { int32_t kind, weight, key, sel, nssel, ns_off, ns_cnt; };  // offsets into `words`
+  std::vector<Term> terms;     // in pod_table_put's order; a category with an invalid selector is absent
+};
 struct PodSpec {
   std::string name, ns, uid;
   StrMap labels;
@@ -110,6 +120,7 @@ struct PodSpec {
   bool preempt_never = false;    // spec.preemptionPolicy == Never
   std::string nominated_node;    // status.nominatedNodeName
   bool preempt_terminating = false;  // PodTerminatingByPreemption
+  mutable std::shared_ptr<const PodTablePre> pt_pre;  // Cluster::pod_table_precompile (same context only)
 };
 struct NodeImage { std::vector<std::string> names; int64_t size; };
 struct NodeSpec {
@@ -177,6 +188,8 @@ struct Config {
   int loop_timing_stride = 1;  // time every k-th persistent-loop launch with HIP events (0: none)
   int timing_stride = 0;  // >0: time every k-th k_filter_score launch with HIP events (bench.py)
   bool persistent_loop = true;  // runs of node-local pods go through k_sched_loop (one launch per run)
+  bool resident_loop = true;    // ksg_schedule_one of a node-local pod: a k_sched_loop launch that stays resident
+                                // between calls, fed through a host-pinned pod ring ("residentLoop")
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int agg_debug = 0;            // AggView::debug (diagnostic)
   int first_chunk = 32;         // pods in a pipelined batch's first chunk (the host work before the first launch)
@@ -341,6 +354,7 @@ class Cluster {
   int32_t ns_id(const std::string& ns) { return ns_ix.get(ns); }
   // sorted (key id << 32 | value id) set of a label map; values are interned
   std::vector<unsigned long long> label_set(const StrMap& labels);
+  void pod_table_precompile(const PodSpec& p);  // PodSpec::pt_pre (ksg_pod_compile; else at first use)
   // metav1.LabelSelectorAsSelector into an int32 program appended to *pool; false on a parse error
   // prevalidated_match: s.match is a labels.Set turned into a selector without validation
   bool compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::vector<int32_t>* pool, int32_t* off,
@@ -379,6 +393,7 @@ class Cluster {
   std::vector<uint8_t> static_queued_;
   DevBuf upd_dev_;
   int ensure_mirror(bool pods_needed = true);  // (re)build device arrays if dirty
+  bool mirror_pending();  // would ensure_mirror(false) touch the device (the resident loop must stop first)
   // the next batch's AssumePods may add up to `extra` host-port ids to one node (widens the stride)
   void reserve_ports(int32_t extra);
   int32_t ports_hw_ = 0;    // largest UsedPorts set of any node so far
@@ -487,6 +502,10 @@ class Engine {
                  uint32_t* reasons, int64_t* raw, int64_t* norm);
   // DefaultPreemption's PostFilter for a pod that failed its cycle (preempt.cpp)
   int preempt(const PodSpec& p, const char* args_json, size_t args_len, ksg_preempt_result* res, std::string* detail);
+  // The resident single-pod loop: ksg_schedule_one of a node-local pod through a
+  // k_sched_loop launch that stays resident between calls; *handled false: the caller takes the launch path
+  int schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res, bool* handled);
+  int resident_stop();  // end the resident launch: every other user of the device or the mirror calls it first
 
   // measurement: average k_filter_score duration (sampled with events when cfg.timing_stride > 0,
   // else the batch's kernel time / launches) and its algorithmic bytes per launch
@@ -548,6 +567,13 @@ class Engine {
   int ensure(DevBuf& b, size_t bytes);
   int ensure_scratch(size_t desc_bytes, int pods, bool eval, int32_t arena_words);
   BatchView bview(int pods);
+  PodRing* ring_ = nullptr;       // the resident loop's pod ring (host-pinned, device-mapped)
+  PodRing* ring_dev_ = nullptr;   // its device address
+  bool res_running_ = false;
+  int res_q_ = 0, res_gs_ = 0, res_unit_ = 0;  // pods posted to the running launch; its geometry
+  std::chrono::steady_clock::time_point res_last_{};  // the last result the host took
+  uint64_t res_seq_ = 0;          // assumed-pod uid suffix
+  double res_prof_[5] = {};       // loopStamps: compile / post / device / settle us, calls
 };
 
 }  // namespace ksg

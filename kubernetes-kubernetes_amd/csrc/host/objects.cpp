@@ -629,6 +629,7 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     c->loop_timing_stride = (int)d.num(r, "loopTimingStride", 1);
     if (const JVal* pl = d.get(r, "persistentLoop")) c->persistent_loop = pl->type == JVal::BOOL && pl->b;
     c->loop_wg = (int)d.num(r, "loopWorkgroups", 0);
+    if (const JVal* rl = d.get(r, "residentLoop")) c->resident_loop = rl->type == JVal::BOOL && rl->b;
     c->loop_unit = (int)d.num(r, "loopUnit", 128) == 256 ? 256 : 128;
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
     c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);

@@ -76,7 +76,48 @@ bool Cluster::compile_lsel(const LabelSel& s, const StrMap* merge_labels, std::v
 
 // framework.NewPodInfo + GetPod*AffinityTerms for an existing pod: a category whose terms do
 // not parse is dropped as a whole (the oracle does the same, oracle_model.cpp new_pod_info).
+void Cluster::pod_table_precompile(const PodSpec& p) {
+  auto pre = std::make_shared<PodTablePre>();
+  pre->labels = label_set(p.labels);
+  auto category = [&](const std::vector<PATerm>& in, int32_t kind) {
+    const size_t w0 = pre->words.size(), t0 = pre->terms.size();
+    for (auto& t : in) {
+      PodTablePre::Term d{};
+      d.kind = kind;
+      d.weight = t.weight;
+      d.key = key_id(t.topo);
+      int32_t so, no;
+      if (!compile_lsel(t.sel, nullptr, &pre->words, &so) || !compile_lsel(t.ns_sel, nullptr, &pre->words, &no)) {
+        pre->words.resize(w0);  // the whole category is dropped, as pod_table_put always did
+        pre->terms.resize(t0);
+        return;
+      }
+      d.sel = so;
+      d.nssel = no;
+      d.ns_off = (int32_t)pre->words.size();
+      if (t.namespaces.empty() && !t.ns_sel.present) {  // newAffinityTerm defaulting (types.go:422-448)
+        pre->words.push_back(ns_id(p.ns));
+      } else {
+        for (auto& n : t.namespaces) pre->words.push_back(ns_id(n));
+      }
+      d.ns_cnt = (int32_t)pre->words.size() - d.ns_off;
+      pre->terms.push_back(d);
+    }
+  };
+  if (p.has_pod_affinity) {
+    category(p.aff_req, T_REQ_AFF);
+    category(p.aff_pref, T_PREF_AFF);
+  }
+  if (p.has_pod_anti) {
+    category(p.anti_req, T_REQ_ANTI);
+    category(p.anti_pref, T_PREF_ANTI);
+  }
+  p.pt_pre = std::move(pre);
+}
+
 int32_t Cluster::pod_table_put(const PodSpec& p, int32_t node_index) {
+  if (!p.pt_pre) pod_table_precompile(p);
+  const PodTablePre& pre = *p.pt_pre;
   int32_t s;
   if (!pt_free.empty()) {
     s = pt_free.back();
@@ -93,60 +134,40 @@ int32_t Cluster::pod_table_put(const PodSpec& p, int32_t node_index) {
   pt_node[s] = node_index;
   pt_ns[s] = ns_id(p.ns);
   pt_flags[s] = p.terminating ? 1u : 0u;
-  const auto ls = label_set(p.labels);
   pt_lbl_off[s] = (uint32_t)pt_pool.size();
-  pt_lbl_cnt[s] = (uint32_t)ls.size();
-  pt_pool.insert(pt_pool.end(), ls.begin(), ls.end());
-
-  auto category = [&](const std::vector<PATerm>& in, int32_t kind) {
-    const size_t pool0 = tt_pool.size();
-    std::vector<DTerm> out;
-    for (auto& t : in) {
-      DTerm d{};
-      d.owner = s;
-      d.kind = kind;
-      d.weight = t.weight;
-      d.key = key_id(t.topo);
-      if (!compile_lsel(t.sel, nullptr, &tt_pool, &d.sel) || !compile_lsel(t.ns_sel, nullptr, &tt_pool, &d.nssel)) {
-        tt_pool.resize(pool0);
-        return;
-      }
-      d.ns_off = (int32_t)tt_pool.size();
-      if (t.namespaces.empty() && !t.ns_sel.present) {  // newAffinityTerm defaulting (types.go:422-448)
-        tt_pool.push_back(ns_id(p.ns));
-      } else {
-        for (auto& n : t.namespaces) tt_pool.push_back(ns_id(n));
-      }
-      d.ns_cnt = (int32_t)tt_pool.size() - d.ns_off;
-      out.push_back(d);
+  pt_lbl_cnt[s] = (uint32_t)pre.labels.size();
+  pt_pool.insert(pt_pool.end(), pre.labels.begin(), pre.labels.end());
+  // the terms: their words appended to the term pool, offsets rebased
+  const int32_t base = (int32_t)tt_pool.size();
+  tt_pool.insert(tt_pool.end(), pre.words.begin(), pre.words.end());
+  for (const PodTablePre::Term& t : pre.terms) {
+    DTerm d{};
+    d.owner = s;
+    d.kind = t.kind;
+    d.weight = t.weight;
+    d.key = t.key;
+    d.sel = base + t.sel;
+    d.nssel = base + t.nssel;
+    d.ns_off = base + t.ns_off;
+    d.ns_cnt = t.ns_cnt;
+    ensure_label_slot(d.key);
+    int32_t j;
+    if (!tt_free.empty()) {
+      j = tt_free.back();
+      tt_free.pop_back();
+      tt[j] = d;
+    } else {
+      j = (int32_t)tt.size();
+      tt.push_back(d);
     }
-    for (auto& d : out) {
-      ensure_label_slot(d.key);
-      int32_t j;
-      if (!tt_free.empty()) {
-        j = tt_free.back();
-        tt_free.pop_back();
-        tt[j] = d;
-      } else {
-        j = (int32_t)tt.size();
-        tt.push_back(d);
-      }
-      pt_terms[s].push_back(j);
-      auto& m = kind == T_REQ_ANTI ? exanti_keys : kind == T_REQ_AFF ? score_keys_req : score_keys_pref;
-      m[d.key]++;
-    }
-  };
-  if (p.has_pod_affinity) {
-    category(p.aff_req, T_REQ_AFF);
-    category(p.aff_pref, T_PREF_AFF);
-  }
-  if (p.has_pod_anti) {
-    category(p.anti_req, T_REQ_ANTI);
-    category(p.anti_pref, T_PREF_ANTI);
+    pt_terms[s].push_back(j);
+    auto& m = t.kind == T_REQ_ANTI ? exanti_keys : t.kind == T_REQ_AFF ? score_keys_req : score_keys_pref;
+    m[d.key]++;
   }
   pods_dirty = true;
   return s;
 }
+
 
 void Cluster::pod_table_drop(int32_t s) {
   if (s < 0 || s >= (int32_t)pt_node.size()) return;

@@ -427,7 +427,8 @@ static Status mk(int code, uint32_t r) { Status s; s.code = code; s.reasons = r;
 // the workers here are persistent threads that spin on a generation counter for up to kSpinUs before
 // parking on a condition variable.  until(n, fn) calls fn(chunk, lo, hi) for every chunk; the caller
 // claims chunks too and returns once every chunk is done, so a worker that is still asleep delays
-// nothing (it finds the job's chunks gone: a chunk ticket carries its job's generation).
+// nothing.  A chunk ticket is {job generation | job's chunk count | next chunk} in one word, so a claim
+// (a compare-and-swap of the whole word) succeeds only for a chunk of the job still posted.
 class Pool {
  public:
   Pool(int n, int spin_us) : n_(n), spin_us_(spin_us) {
@@ -453,14 +454,13 @@ class Pool {
   int chunks(int pieces) const { return pieces <= 0 ? 0 : (pieces + chunk_size(pieces, n_) - 1) / chunk_size(pieces, n_); }
   void until(int pieces, const std::function<void(int, int, int)>& fn) {
     if (pieces <= 0) return;
-    const int cs = chunk_size(pieces, n_), nc = (pieces + cs - 1) / cs;
+    const int cs = chunk_size(pieces, n_), nc = (pieces + cs - 1) / cs;  // nc < 2^16 for any int pieces
     fn_.store(&fn, std::memory_order_relaxed);
     pieces_.store(pieces, std::memory_order_relaxed);
     csize_.store(cs, std::memory_order_relaxed);
-    nchunks_.store(nc, std::memory_order_relaxed);
     done_.store(0, std::memory_order_relaxed);
     const uint64_t g = gen_.load() + 1;
-    ticket_.store(g << 32, std::memory_order_release);  // the job's chunks, claimable from here
+    ticket_.store((g << 32) | ((uint64_t)nc << 16), std::memory_order_release);  // claimable from here
     gen_.store(g);  // seq_cst: pairs with a parking worker's sleepers_ increment (no lost wakeup)
     if (sleepers_.load() > 0) {
       { std::lock_guard<std::mutex> l(m_); }
@@ -481,8 +481,8 @@ class Pool {
     uint64_t t = ticket_.load(std::memory_order_acquire);
     for (;;) {
       if ((t >> 32) != (g & 0xffffffffull)) return;
-      const int c = (int)(uint32_t)t;
-      if (c >= nchunks_.load(std::memory_order_relaxed)) return;
+      const int c = (int)(t & 0xffffu), nc = (int)((t >> 16) & 0xffffu);
+      if (c >= nc) return;
       if (!ticket_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel)) continue;
       const int cs = csize_.load(std::memory_order_relaxed), lo = c * cs;
       (*fn_.load(std::memory_order_relaxed))(c, lo, std::min(pieces_.load(std::memory_order_relaxed), lo + cs));
@@ -513,7 +513,7 @@ class Pool {
   std::mutex m_;
   std::condition_variable cv_;
   std::atomic<uint64_t> gen_{0}, ticket_{0};
-  std::atomic<int> sleepers_{0}, done_{0}, pieces_{0}, csize_{1}, nchunks_{0};
+  std::atomic<int> sleepers_{0}, done_{0}, pieces_{0}, csize_{1};
   std::atomic<bool> stop_{false};
   std::atomic<const std::function<void(int, int, int)>*> fn_{nullptr};
 };

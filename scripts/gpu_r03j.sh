@@ -7,4 +7,5 @@ step() {  # name seconds cmd...
   timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || exit $rc
 }
-step cpu_pool 400 python scripts/cpu_pool_probe.py
+step cpu_crash 300 python -X faulthandler scripts/pw_crash_probe.py
+step cpu_pool 400 python -X faulthandler scripts/cpu_pool_probe.py

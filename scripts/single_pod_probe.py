@@ -1,6 +1,6 @@
 """Latency of one ksg_schedule_one call (the per-pod API a kube-scheduler binding calls from its
-scheduling goroutine) on SchedulingBasic at 5000 nodes, persistent loop vs the launch path, against a
-ksg_schedule_batch of the same pods.  Prints one JSON line."""
+scheduling goroutine) on SchedulingBasic at 5000 nodes: the resident loop (default), the launch path,
+against a ksg_schedule_batch of the same pods.  Prints one JSON line."""
 import json
 import os
 import sys
@@ -29,9 +29,15 @@ def run(cfg, n_pods=2000, batch=False):
         for h in hs[200:]:
             s.schedule_one(h, assume=True)
     dt = time.perf_counter() - t0
+    s.close()
     return dt / n_pods * 1e6
 
 
-out = {"single_loop_us": round(run({}), 1), "single_launch_us": round(run({"persistentLoop": False}), 1),
+if sys.argv[1:] == ["stamps"]:  # the resident call's host / device split (printed at the loop's stop)
+    print(json.dumps({"single_resident_us": round(run({"loopStamps": True}), 1)}))
+    sys.exit(0)
+out = {"single_resident_us": round(run({}), 1),
+       "single_launch_us": round(run({"residentLoop": False}), 1),
+       "single_launch_no_loop_us": round(run({"residentLoop": False, "persistentLoop": False}), 1),
        "batch_us_per_pod": round(run({}, batch=True), 2)}
 print(json.dumps(out))

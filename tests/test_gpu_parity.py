@@ -709,3 +709,61 @@ def test_sched_loop_prepared_and_fixup_paths(native, unit):
             ro, _ = o.schedule_one(o.compile(p), assume=True)
             assert rs[k].as_tuple() == ro.as_tuple(), f"unit {unit} hetero {hetero} pod {k}"
         assert g.compare_mirror(sync=False) == (0, -1)
+
+
+def test_resident_single_pod_calls(native):
+    """ksg_schedule_one through the resident loop (node-local pods) against the oracle, pod by pod, with
+    the events that must stop it in between: informer events, a forget, a batch, pods it declines
+    (PodTopologySpread), an idle gap longer than its self-stop, and more calls than one launch holds."""
+    import time
+    rng, cfg, nodes, existing, names = rand_cluster(9300, n_nodes=900, n_existing=90, topology=False)
+    g, o = _pair(native, cfg, nodes, existing)
+    hist = []
+
+    def one(pod, tag):
+        rg, _ = g.schedule_one(g.compile(pod), assume=True)
+        ro, _ = o.schedule_one(o.compile(pod), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"{tag}: {rg.as_tuple()} != {ro.as_tuple()}"
+        hist.append(pod)
+
+    for k in range(60):
+        one(rand_pod(rng, k, names, topology=False), f"pod {k}")
+    # informer events between calls
+    extra = rand_cluster(9301, n_nodes=12, n_existing=0, topology=False)[2]
+    for n in extra:
+        n["metadata"]["name"] += "-late"
+        n["metadata"].setdefault("labels", {})["kubernetes.io/hostname"] = n["metadata"]["name"]
+        for b in (g, o):
+            b.add_node(n)
+    names = g.node_names()
+    for k in range(60, 120):
+        one(rand_pod(rng, k, names, topology=False), f"pod {k} (after node adds)")
+    # forget, then a pod the loop declines, then a batch
+    hg, ho = g.compile(hist[-1]), o.compile(hist[-1])
+    rg, _ = g.schedule_one(hg, assume=True)
+    ro, _ = o.schedule_one(ho, assume=True)
+    assert rg.as_tuple() == ro.as_tuple()
+    g.forget(hg)
+    o.forget(ho)
+    for k in range(120, 160):
+        one(rand_pod(rng, k, names), f"pod {k} (mixed, some declined)")
+    batch = [rand_pod(rng, 1000 + k, names, topology=False) for k in range(30)]
+    rs = g.schedule_batch([g.compile(p) for p in batch], assume=True)
+    for k, p in enumerate(batch):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"batch pod {k}"
+    time.sleep(0.08)  # longer than the loop's idle self-stop
+    for k in range(160, 1300):  # past one launch's kLoopMaxPods
+        one(rand_pod(rng, k, names, topology=False), f"pod {k}")
+    assert g.compare_mirror(sync=True)[0] == 0
+
+
+def test_resident_loop_off_matches(native):
+    """residentLoop false: the same calls take the launch path (results identical)."""
+    rng, cfg, nodes, existing, names = rand_cluster(9310, n_nodes=500, n_existing=50, topology=False)
+    g, o = _pair(native, dict(cfg, residentLoop=False), nodes, existing)
+    for k in range(40):
+        pod = rand_pod(rng, k, names, topology=False)
+        rg, _ = g.schedule_one(g.compile(pod), assume=True)
+        ro, _ = o.schedule_one(o.compile(pod), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"pod {k}"
