@@ -2017,7 +2017,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     }
     const int pod = lv.first_pod + q, par = q & 1, npar = par ^ 1;
     const int bq = q % 3, bn = (q + 1) % 3, bs = (q + 2) % 3;
-    const bool more = q + 1 < run_end;
+    const bool more = !RING && q + 1 < run_end;  // resident mode: every pod is a run of its own
     const uint8_t* base = s_blob[bq];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
 
@@ -2119,7 +2119,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // both ways -- the candidate not chosen (phase 1 as it is), and chosen (its next evaluation
       // with this pod assumed, computed in phase 1 for default-plugin pods) -- so the selection
       // wave publishes the right pair as soon as exchange B resolves.
-      const bool stage = q + 2 < run_end;
+      const bool stage = !RING && q + 2 < run_end;
       if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
       if (stage) stage_prog(pod + 2, bs);  // s_blob[(q + 2) % 3] held pod q-1, free since the last barrier
       while (__hip_atomic_load(&s_cand_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)  // posted every pod
