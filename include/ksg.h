@@ -208,7 +208,8 @@ int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uin
  *   {"offset": <int>,        GetOffsetAndNumCandidates' random offset (rand.Int31n upstream), taken
  *                            modulo the number of potential nodes
  *    "minCandidateNodesPercentage": 10, "minCandidateNodesAbsolute": 100,   (DefaultPreemptionArgs)
- *    "now": <unix ns>,       GetPodStartTime's clock for pods without status.startTime (utils.go:52-58)
+ *    "now": <unix ns>,       GetPodStartTime's clock for pods without status.startTime (utils.go:52-58;
+ *                            absent: the wall clock, time.Now() as upstream)
  *    "allNodes": false,      true: every snapshot node is a potential node (DryRunPreemption over
  *                            the node list, as the reference's unit tests call it)
  *    "listCandidates": false, true: detail lists every candidate (else "candidates" is empty)

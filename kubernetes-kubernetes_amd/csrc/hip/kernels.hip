@@ -1787,6 +1787,9 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   __shared__ uint32_t s_ccnt, s_cbelow;
   __shared__ unsigned long long s_best;
   __shared__ int s_ring_bytes;  // resident mode: the posted pod's program size (-1: the launch ends)
+  // percentageOfNodesToScore (DF_ROTDEV): s_rot[p & 1] = pod p's rotation start (nextStartNodeIndex),
+  // s_proc = the decided pod's processedNodes (schedule_one.go:686-687, 809-824)
+  __shared__ uint32_t s_rot[2], s_proc;
   const int w = blockIdx.x, G = lv.nwg;
   const int gid = lv.rank * G + w, P = lv.world * G;  // my participant index, participants (rank-major)
   // my node units [k0, k1) of the rank's range (lv.blk0 / lv.nblk count 256-node blocks)
@@ -1803,6 +1806,16 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   const int t = vt;                          // evaluation waves: my slot in each block of my range
   auto stamp_s = [&](int q, int k) {       // diagnostic phase stamps: WG 0's selection lane 0
     if (lv.stamps && w == 0 && vt == U) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  // the committing thread: pod `pod`'s PodStats, with its rotation bookkeeping for commit_result (DF_ROTDEV)
+  auto rot_stats = [&](int pod, int par) __attribute__((always_inline)) -> PodStats* {
+    PodStats* ps = b.stats + pod;
+    if (reinterpret_cast<const PodDesc*>(s_blob[(pod - lv.first_pod) % 3])->flags & DF_ROTDEV) {
+      ps->rot = s_rot[par];
+      ps->processed = s_proc;
+      ps->rot_out = s_rot[par ^ 1];
+    }
+    return ps;
   };
 
   if (t < U) {  // evaluation waves
@@ -1844,9 +1857,25 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   // scores over my feasible nodes; per-wave feasible counts (all, and before nextStartNodeIndex)
   unsigned long long t_mt = 0, t_mn = 0;
   uint32_t w_cnt = 0, w_below = 0;
-  auto below_mask = [&](int kk, int srot) __attribute__((always_inline)) -> unsigned long long {
-    const int lim = srot - ((k0 + kk) * U + wave * 64);
+  auto below_mask_v = [&](int kk, int v, int srot) __attribute__((always_inline)) -> unsigned long long {
+    const int lim = srot - ((k0 + kk) * U + v * 64);
     return lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+  };
+  auto below_mask = [&](int kk, int srot) __attribute__((always_inline)) -> unsigned long long {
+    return below_mask_v(kk, wave, srot);
+  };
+  // DF_ROTDEV pods: the rotation start is known only once the previous pod's processedNodes is, after
+  // phase 1, so exchange A's "feasible before nextStartNodeIndex" is counted from the ballots then.
+  // One wave: lane = (block of my range, evaluation wave); (fkw, fcw) takes ballot fball instead.
+  auto below_wave = [&](int par, int srot, int fkw, int fcw, unsigned long long fball) __attribute__((always_inline))
+      -> uint32_t {
+    const int kk = lane / NW, v = lane % NW;
+    uint32_t c = 0;
+    if (kk < nk) {
+      const unsigned long long bl = (kk == fkw && v == fcw) ? fball : s_ball[par][kk][v];
+      c = (uint32_t)__popcll(bl & below_mask_v(kk, v, srot));
+    }
+    return wave_sum_u32(c);
   };
   auto publish_partials = [&](int par) __attribute__((always_inline)) {
     s_tm[par][t] = t_mt;
@@ -1923,8 +1952,11 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   // phase 2 over the slots of evaluation waves [vlo, vhi) of every block of my range (the selection
   // wave takes all four: splitting it with the helper wave slowed phase 1 more than it saved): positions in
   // the rotated feasible list, NormalizeScore + weights, the best packed (TotalScore, pre-order) key
+  // percentageOfNodesToScore: only the first K feasible nodes of the rotated order are the feasible list
+  // (cutK = K, else ~0); endn gets the node at global feasible index gK, the (K+1)-th of the rotated order
   auto phase2_half = [&](int vlo, int vhi, uint32_t acc, uint32_t F, uint32_t ps_before, int64_t mx_t, int64_t mx_n,
-                         const PodDesc& d, int par, unsigned long long* key, int* knode) __attribute__((always_inline)) {
+                         const PodDesc& d, int par, unsigned long long* key, int* knode, uint32_t cutK, uint32_t gK,
+                         int* endn) __attribute__((always_inline)) {
 #pragma unroll
     for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
       if (kk < nk) {
@@ -1946,12 +1978,34 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
             const bool f = ((ballot[v] >> lane) & 1ull) != 0;
             const uint32_t g = acc + wave_prefix_count(ballot[v], lane);
             const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
-            const unsigned long long kv = f ? pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos) : 0ull;
+            const unsigned long long kv =
+                f && pos < cutK ? pack_best(loop_total(d, fx[v], rt[v], rn[v], mx_t, mx_n), pos) : 0ull;
+            *endn = f && g == gK ? (k0 + kk) * U + v * 64 + lane : *endn;
             *knode = kv > *key ? (k0 + kk) * U + v * 64 + lane : *knode;
             *key = kv > *key ? kv : *key;
           }
           acc += (uint32_t)__popcll(ballot[v]);
         }
+      }
+    }
+  };
+  // the normalising plugins' raw maxima over my nodes in the cut feasible list (rotated position < K):
+  // NormalizeScore runs over the kept list only (schedule_one.go:937-1048 scores feasibleNodes)
+  auto kept_max = [&](uint32_t acc, uint32_t F, uint32_t ps_before, uint32_t K, int par, unsigned long long* mt,
+                      unsigned long long* mn) __attribute__((always_inline)) {
+    for (int kk = 0; kk < nk; ++kk) {
+#pragma unroll
+      for (int v = 0; v < NW; ++v) {
+        const unsigned long long ballot = s_ball[par][kk][v];
+        const bool f = ((ballot >> lane) & 1ull) != 0;
+        const uint32_t g = acc + wave_prefix_count(ballot, lane);
+        const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;
+        if (f && pos < K) {
+          const unsigned long long et = enc_i64(s_rt[par][kk][v * 64 + lane]), en = enc_i64(s_rn[par][kk][v * 64 + lane]);
+          *mt = et > *mt ? et : *mt;
+          *mn = en > *mn ? en : *mn;
+        }
+        acc += (uint32_t)__popcll(ballot);
       }
     }
   };
@@ -1965,6 +2019,11 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       bl += s_u[par][1][v];
       a = s_x[par][0][v] > a ? s_x[par][0][v] : a;
       bb = s_x[par][1][v] > bb ? s_x[par][1][v] : bb;
+    }
+    if (reinterpret_cast<const PodDesc*>(s_blob[pq % 3])->flags & DF_ROTDEV) {  // counted from the ballots
+      bl = 0;
+      for (int kk = 0; kk < nk; ++kk)
+        for (int v = 0; v < NW; ++v) bl += (uint32_t)__popcll(s_ball[par][kk][v] & below_mask_v(kk, v, (int)s_rot[pq & 1]));
     }
     unsigned long long g0, g1;
     a_granules(c, bl, a, bb, &g0, &g1);
@@ -2005,7 +2064,13 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   __syncthreads();
   if (t < U) phase1(lv.first_pod + run0, run0 % 3, run0 & 1, nullptr);
   __syncthreads();
-  if (vt == U) publish_a(run0, run0 & 1);
+  if (vt == U) {
+    const PodDesc& d0 = *reinterpret_cast<const PodDesc*>(s_blob[run0 % 3]);
+    if (d0.flags & DF_ROTDEV)  // the previous launched pod's nextStartNodeIndex, or the host's
+      s_rot[run0 & 1] = RING ? (uint32_t)d0.rot_start  // resident: the host's, from the previous call's result
+                             : d0.prev_pod < 0 ? b.stats[lv.first_pod + run0].rot_in : b.stats[d0.prev_pod].rot_out;
+    publish_a(run0, run0 & 1);
+  }
 
   for (int q = run0; q < run_end; ++q) {
     if (q == lv.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
@@ -2048,25 +2113,67 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       nmax = wave_max_u64(nmax);
       stamp_s(q, 1);
 
+      // percentageOfNodesToScore (DF_ROTDEV, unsharded): findNodesThatPassFilters keeps the first K
+      // feasible nodes of the rotated order and stops at the (K+1)-th (schedule_one.go:809-824)
+      const bool rotd = (d.flags & DF_ROTDEV) != 0;
+      const uint32_t K = rotd ? (uint32_t)d.num_to_find : 0xffffffffu;
+      const bool cut = rotd && F > K;
+      const uint32_t gK = cut ? (ps_before + K) % F : 0xffffffffu;  // its global feasible index
+      if (cut && ok && (tmax > 1 || nmax > 1)) {
+        // some raw TaintToleration / NodeAffinity score is > 0: NormalizeScore's maxima are over the kept
+        // nodes only -- one more exchange (M, at pod index q + kLoopMaxPods) of the kept maxima
+        unsigned long long mt = 0, mn = 0, g0, g1;
+        kept_max(acc, F, ps_before, K, par, &mt, &mn);
+        mt = wave_max_u64(mt);
+        mn = wave_max_u64(mn);
+        a_granules(mt != 0ull ? 1u : 0u, 0u, mt, mn, &g0, &g1);
+        if (lane == 0) gran_put(lv, q + kLoopMaxPods, gid, 1, g1);
+        unsigned long long xm[1][kMaxSweep];
+        ok = gran_sweep<1>(lv, q + kLoopMaxPods, 1, xm);
+        tmax = nmax = 0;
+#pragma unroll
+        for (int r = 0; r < kMaxSweep; ++r) {
+          if (lane + 64 * r < P) {
+            const unsigned long long tv = xm[0][r] & 0xffffffull, nv = (xm[0][r] >> 24) & 0xffffffull;
+            tmax = tv > tmax ? tv : tmax;
+            nmax = nv > nmax ? nv : nmax;
+          }
+        }
+        tmax = wave_max_u64(tmax);
+        nmax = wave_max_u64(nmax);
+      }
+
       // ---- phase 2: positions, NormalizeScore + weights, my range's best packed key
       const int64_t mx_t = tmax ? (int64_t)tmax - 1 : 0, mx_n = nmax ? (int64_t)nmax - 1 : 0;
       unsigned long long key = 0;
-      int knode = -1;
-      if (ok) phase2_half(0, NW, acc, F, ps_before, mx_t, mx_n, d, par, &key, &knode);
+      int knode = -1, endn = -1;
+      if (ok) phase2_half(0, NW, acc, F, ps_before, mx_t, mx_n, d, par, &key, &knode, K, gK, &endn);
       const unsigned long long wkey = wave_max_u64(key);
       const unsigned long long hold = __ballot(key == wkey && key != 0ull);
       const int cand = hold ? __builtin_amdgcn_readlane(knode, (int)__builtin_ctzll(hold)) : -1;
       stamp_s(q, 2);
+      // the holder of the (K+1)-th node: processedNodes = its rotated position (K + the failures before it)
+      uint32_t myproc = 0;
+      if (rotd) {
+        const unsigned long long eh = __ballot(endn >= 0);
+        if (eh) {
+          const int en = __builtin_amdgcn_readlane(endn, (int)__builtin_ctzll(eh));
+          myproc = (uint32_t)(((int64_t)en - (int64_t)s_rot[par] + m.n) % m.n) + 1u;
+        }
+      }
       if (lane == 0) {
         gran_put(lv, q, gid, 2, wkey);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
         if (lv.world > 1) gran_put(lv, q, gid, 3, (unsigned long long)(uint32_t)cand);
+        else if (rotd) gran_put(lv, q, gid, 3, (unsigned long long)myproc);
         if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_cand_node, cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&s_cand_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       stamp_s(q, 3);
       unsigned long long xb[2][kMaxSweep];
-      if (lv.world == 1) {  // unsharded: the owner is found locally, only the keys cross workgroups
+      if (lv.world == 1 && rotd) {  // the keys and the (K+1)-th node's processedNodes
+        ok = ok && gran_sweep<2>(lv, q, 2, xb);
+      } else if (lv.world == 1) {  // unsharded: the owner is found locally, only the keys cross workgroups
         unsigned long long k1[1][kMaxSweep];
         ok = ok && gran_sweep<1>(lv, q, 2, k1);
 #pragma unroll
@@ -2077,7 +2184,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       } else {
         ok = ok && gran_sweep<2>(lv, q, 2, xb);
       }
-      unsigned long long bm = 0;
+      unsigned long long bm = 0, pm = 0;
       int bnode = -1;
 #pragma unroll
       for (int r = 0; r < kMaxSweep; ++r) {
@@ -2085,6 +2192,17 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         if (v > bm) {
           bm = v;
           bnode = (int)(uint32_t)xb[1][r];
+        }
+        if (rotd && (lane + 64 * r) < P) pm = xb[1][r] > pm ? xb[1][r] : pm;
+      }
+      uint32_t rot_next = 0;
+      if (rotd) {  // nextStartNodeIndex for the next pod (schedule_one.go:686-687); all processed without a cut
+        pm = wave_max_u64(pm);
+        const uint32_t proc = cut && pm ? (uint32_t)pm - 1u : (uint32_t)m.n;
+        rot_next = m.n > 0 ? (uint32_t)(((uint64_t)s_rot[par] + proc) % (uint64_t)m.n) : 0u;
+        if (lane == 0) {
+          s_proc = proc;
+          s_rot[npar] = rot_next;
         }
       }
       const unsigned long long gbest = wave_max_u64(bm);
@@ -2095,7 +2213,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       if (lane == 0) {
         s_ok = ok ? 1u : 0u;
         s_best = bm;
-        s_F = F;
+        s_F = cut ? K : F;  // the feasible list's length
         s_win = win;
         s_gnode = F > 0 ? gnode : -1;
       }
@@ -2106,8 +2224,15 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         while (__hip_atomic_load(&s_ga_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
           __builtin_amdgcn_s_sleep(1);
         const bool chosen = win >= 0 && (d.flags & DF_ASSUME);
+        unsigned long long ga0 = s_ga[chosen ? 2 : 0];
+        if (rotd && (!chosen || s_cand_ok)) {  // pod q+1's count before its rotation start, now known
+          const int wsl = chosen ? win - k0 * U : -1;
+          const uint32_t bl = below_wave(npar, (int)rot_next, chosen ? wsl / U : -1, chosen ? (wsl % U) >> 6 : -1,
+                                         s_cball);
+          ga0 = ((unsigned long long)bl << 20) | (ga0 & 0xfffffull);
+        }
         if (lane == 0 && (!chosen || s_cand_ok)) {
-          gran_put(lv, q + 1, gid, 0, s_ga[chosen ? 2 : 0]);
+          gran_put(lv, q + 1, gid, 0, ga0);
           gran_put(lv, q + 1, gid, 1, s_ga[chosen ? 3 : 1]);
           if (lv.wstamps) lv.wstamps[((size_t)(q + 1) * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
         }
@@ -2216,14 +2341,14 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       if (!owner_wg) {  // exchange A of pod q+1 already published by the selection wave
         if (F == 0) {
           if (w == 0 && t == 0) {
-            commit_result(m, b, base, d, b.stats + pod, pod, F, -1, s_best, nullptr, s_ipa);
+            commit_result(m, b, base, d, rot_stats(pod, par), pod, F, -1, s_best, nullptr, s_ipa);
             if constexpr (RING) ring_post(lv, q, b.results[pod]);
           }
         } else if (wsl >= 0 && t == wsl % U) {  // chosen here, not assumed
-          commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, nullptr, s_ipa);
+          commit_result(m, b, base, d, rot_stats(pod, par), pod, F, win, s_best, nullptr, s_ipa);
           if constexpr (RING) ring_post(lv, q, b.results[pod]);
         } else if (remote && w == 0 && t == 0) {  // chosen on another rank: the result and this replica's assume
-          commit_result(m, b, base, d, b.stats + pod, pod, F, gnode, s_best, nullptr, s_ipa);
+          commit_result(m, b, base, d, rot_stats(pod, par), pod, F, gnode, s_best, nullptr, s_ipa);
         }
       } else if (s_cand_ok) {  // the helper prepared everything: LDS stores, then publish
         if (t == wsl % U) {
@@ -2247,7 +2372,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           s_x[npar][0][cw] = s_cmt;
           s_x[npar][1][cw] = s_cmn;
           if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
-          commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);
+          commit_result(m, b, base, d, rot_stats(pod, par), pod, F, win, s_best, &c, s_ipa);
           if constexpr (RING) ring_post(lv, q, b.results[pod]);
         }
       } else if (t < U && wave == ((wsl % U) >> 6)) {  // generic pods: re-evaluate here
@@ -2258,7 +2383,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         if (lane == owner) {
           NodeCore c = lds_core(s_core, kw, t);
           assume_core(c, d);
-          commit_result(m, b, base, d, b.stats + pod, pod, F, win, s_best, &c, s_ipa);  // before the re-read
+          commit_result(m, b, base, d, rot_stats(pod, par), pod, F, win, s_best, &c, s_ipa);  // before the re-read
           if constexpr (RING) ring_post(lv, q, b.results[pod]);
           lds_put_dynamic(s_core, kw, t, c);
           if (more) {
@@ -4337,7 +4462,6 @@ __global__ __launch_bounds__(kPickThreads) void k_preempt_pick(const PSegOut* ou
   for (int b0 = 0; b0 < n; b0 += kPickThreads) {
     const int i = b0 + t;
     const int f = (i < n && out[i].st != PS_NOT_CHECKED) ? 1 : 0;
-    if (i < n && (out[i].flags & 1u)) s_unsup = 1;
     int tot;
     const int r = block_excl_scan(f, &tot, s_w);
     if (f) pot[P + r] = i;
@@ -4386,6 +4510,9 @@ __global__ __launch_bounds__(kPickThreads) void k_preempt_pick(const PSegOut* ou
     if (c != 0 && nvc >= 1 && nvc + vvc >= nc) atomicMin(&s_cut, j);
     __syncthreads();
     const int cut = s_cut;
+    // a node whose result the device could not compute (PSegOut flag bit 0) matters only if the dry
+    // run reaches it: a potential node at or before the cut (DryRunPreemption stops there)
+    if (j < P && j <= cut && (out[pot[(offset + j) % P]].flags & 1u)) s_unsup = 1;
     if (c != 0 && j <= cut) {
       int idx = -1;
       if (c == 1 && nvi - 1 < ncand) idx = nvi - 1;

@@ -581,7 +581,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     // no existing anti-affinity) leave their mask bits set but never reject: not a reason to leave
     const bool topo_filter = D.n_ptsf > 0 || D.n_raff > 0 || D.n_ranti > 0 || (D.ipa_flags & IPA_EXIST_FILTER);
     if (mode == CYCLE && shape && D.n_scalar == 0 && !topo_filter && !(smask & topo) &&
-        !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR | DF_ROTDEV)) &&
+        !(D.flags & (DF_PREFILTER_REJECT | DF_SUBSET | DF_ALL_FEASIBLE | DF_AGGREGATE | DF_SCORE_ERROR)) &&
         c->alloc_bound < ((int64_t)1 << 52) / 100)
       D.flags |= DF_FAST;
     if (mode == CYCLE && shape && D.n_scalar == 0 &&
@@ -975,8 +975,11 @@ bool Engine::rotdev() const {
 bool Engine::loop_ok(const CompiledPod& p) const {
   if (p.error) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
-  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV)) return false;
+  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE)) return false;
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
+  // percentageOfNodesToScore / no-score profiles: the loop cuts the list and carries nextStartNodeIndex
+  // itself (k_sched_loop), unsharded, over the whole snapshot (no PreFilterResult)
+  if ((d.flags & DF_ROTDEV) && (comm || (d.flags & (DF_SUBSET | DF_PREFILTER_REJECT)))) return false;
   return loop_bounds_ok(p);
 }
 // A pod k_agg_loop takes: any CYCLE pod without evaluation output, PreFilter outcomes or sampling, whose
@@ -1153,12 +1156,13 @@ BatchView Engine::bview(int pods) {
   return b;
 }
 
-// The loop's exchange granule array: fixed size (kLoopMaxPods pods x 256 participants), zeroed once,
+// The loop's exchange granule array: fixed size (2 kLoopMaxPods pods x 256 participants), zeroed once,
 // never reallocated (a sharded context's peers map it over IPC).  Sharded, it is uncached device
 // memory: the peers' stores arrive over xGMI and the sweeps must not read a stale cached line.
 int Engine::gran_setup() {
   if (!gran_all.empty()) return KSG_OK;
-  const size_t bytes = (size_t)kLoopMaxPods * 256 * kGran * 8;
+  // [2 kLoopMaxPods]: pod q's sampled-maxima exchange (k_sched_loop, DF_ROTDEV) sits at q + kLoopMaxPods
+  const size_t bytes = (size_t)2 * kLoopMaxPods * 256 * kGran * 8;
   void* p = nullptr;
   if (comm) HIPCHK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
   else HIPCHK(hipMalloc(&p, bytes));
@@ -2365,7 +2369,8 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     return KSG_OK;
   }
   const int64_t ns_before = c->next_start;
-  c->next_start = (c->next_start + cp.num_all) % (int64_t)N;  // schedule_one.go:686-687
+  const bool rot_dev = rotdev();  // the program's rot_start is c->next_start; the loop returns the next one
+  if (!rot_dev) c->next_start = (c->next_start + cp.num_all) % (int64_t)N;  // schedule_one.go:686-687
   auto fail = [&](int code) {
     c->pod_table_drop(cp.slot);
     c->next_start = ns_before;
@@ -2470,6 +2475,10 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
   res->node_index = d.node;
   res->feasible_nodes = d.feasible;
   res->evaluated_nodes = cp.num_all;
+  if (rot_dev) {  // processedNodes and nextStartNodeIndex from the loop (schedule_one.go:686-687)
+    res->evaluated_nodes = d.evaluated;
+    c->next_start = d.rot_next;
+  }
   res->total_score = d.feasible > 1 ? d.total : 0;
   if (res->status == KSG_CODE_SUCCESS && res->node_index >= 0) {
     std::string uid = p.uid + "#r" + std::to_string(++res_seq_);

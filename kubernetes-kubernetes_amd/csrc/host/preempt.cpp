@@ -18,6 +18,7 @@
 // stable, up to 12 elements); candidates tie-break in candidate-list order (the reference iterates a
 // Go map there, preemption.go:316-319).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 #include "host.hpp"
@@ -256,12 +257,16 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     JDoc d(args_json && args_len ? args_json : "{}", args_json && args_len ? args_len : 2);
     const JVal& r = d.root();
     offset_in = d.num(r, "offset", 0);
-    now = d.num(r, "now", 0);
+    // GetPodStartTime's clock for pods without status.startTime (utils.go:52-58: time.Now()); absent,
+    // the wall clock, as upstream -- so the device-resident segments serve the call (seg below)
+    now = d.get(r, "now") ? d.num(r, "now", 0)
+                          : (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::system_clock::now().time_since_epoch()).count();
     pct = (int32_t)d.num(r, "minCandidateNodesPercentage", 10);
     absn = (int32_t)d.num(r, "minCandidateNodesAbsolute", 100);
     all_nodes = d.boolean(r, "allNodes");
     staged = d.boolean(r, "debugHostStaged");  // diagnostic: force the host-staged victim records
-    list = d.boolean(r, "listCandidates");     // detail lists every DryRunPreemption candidate
+    list = d.boolean(r, "listCandidates");      // detail lists every DryRunPreemption candidate
     d.each(d.get(r, "pdbs"), [&](const JVal& v) {
       Pdb b;
       if (const JVal* md = d.get(v, "metadata")) b.ns = d.str(*md, "namespace", "default");
@@ -327,7 +332,6 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   // segment path: per-node victim masks (listCandidates), the device's cut and pick
   std::vector<PSegOut> so;
   PickOut pick{};
-  uint32_t tunsup = 0;
 
   uint8_t* hp = (uint8_t*)h_pinned;
   hipStream_t s = c->stream;
@@ -394,8 +398,9 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       d_contrib = (int32_t*)d_contrib_buf.p;
       d_tunsup = (uint32_t*)((uint8_t*)d_contrib_buf.p + cb);
       PCHK(hipMemsetAsync(d_contrib_buf.p, 0, cb + 4, s));
+      // (a term beyond kPreemptCons keys also has n_exkeys > kPreemptCons, so k_preempt_seg flags every
+      // node: the pick counts the flag only where the dry run reaches, at or before its cut)
       PCHK(launch_preempt_terms(m, bv, 0, d_contrib, d_tunsup, s));
-      PCHK(hipMemcpyAsync(&tunsup, d_tunsup, 4, hipMemcpyDeviceToHost, s));
     }
     if ((rc = ensure(d_psout, sizeof(PSegOut) * (size_t)N))) return rc;
     uint8_t* dp = (uint8_t*)d_pdb.p + mm_b;
@@ -427,7 +432,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       PCHK(hipMemcpyAsync(so.data(), d_psout.p, sizeof(PSegOut) * (size_t)N, hipMemcpyDeviceToHost, s));
     }
     if ((rc = finish_device())) return rc;
-    if (pick.unsupported || tunsup) {
+    if (pick.unsupported) {
       c->err = "preemption: a victim's effect on the pod's PodTopologySpread / InterPodAffinity counts is outside "
                "what the device tracks (more than 4 constraints, terms or keys, or an emptied affinity count)";
       return KSG_ENOTSUP;

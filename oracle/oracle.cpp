@@ -523,6 +523,8 @@ struct ksgo_ctx {
   Config cfg;
   double prof[10] = {};  // ksgo_debug_profile: microseconds per cycle section (CPU-baseline breakdown)
   std::unique_ptr<Pool> pool;  // cfg.threads > 1
+  std::vector<NodeInfoO*> filt_buf;  // CPU-baseline filter pass: per-chunk feasible runs, reused per cycle
+  std::vector<int> filt_lo, filt_cnt, filt_fail;
   std::string err;
   std::map<std::string, Namespace> namespaces;
   // Service / ReplicationController / ReplicaSet / StatefulSet listers (podtopologyspread/plugin.go:145-150)
@@ -1531,21 +1533,30 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     // CPU-baseline mode: Parallelizer.Until's chunks of the rotated order (schedule_one.go:840), then
     // the per-chunk feasible lists concatenated in chunk order -- the sequential loop's result
     // exactly (with every node to be found there is no early stop to race on)
+    // (one buffer for every chunk, as the reference's feasibleNodes slice: chunk k writes its feasible
+    // nodes from its own first index on, so no allocation happens inside the parallel pass)
     const int T = c->pool->chunks(numAll);
-    std::vector<std::vector<NodeInfoO*>> part(T);
-    std::vector<int> pfail(T, 0);
+    c->filt_buf.resize((size_t)numAll);
+    c->filt_lo.assign((size_t)T, 0);
+    c->filt_cnt.assign((size_t)T, 0);
+    c->filt_fail.assign((size_t)T, 0);
+    NodeInfoO** buf = c->filt_buf.data();
     c->pool->until(numAll, [&](int k, int a, int b) {
+      int cnt = 0, nf = 0;
       for (int i = a; i < b; ++i) {
         NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
         Status st = filter_node(ni);
-        if (part[k].empty()) part[k].reserve((size_t)(b - a));
-        if (st.ok()) part[k].push_back(ni);
-        else { ++pfail[k]; record_failed(ni, st); }
+        if (st.ok()) buf[a + cnt++] = ni;
+        else { ++nf; record_failed(ni, st); }
       }
+      c->filt_lo[(size_t)k] = a;
+      c->filt_cnt[(size_t)k] = cnt;
+      c->filt_fail[(size_t)k] = nf;
     });
+    feasible.reserve((size_t)numAll);
     for (int k = 0; k < T; ++k) {
-      feasible.insert(feasible.end(), part[k].begin(), part[k].end());
-      failed += pfail[k];
+      feasible.insert(feasible.end(), buf + c->filt_lo[(size_t)k], buf + c->filt_lo[(size_t)k] + c->filt_cnt[(size_t)k]);
+      failed += c->filt_fail[(size_t)k];
     }
   } else {
     for (int i = 0; i < numAll; ++i) {

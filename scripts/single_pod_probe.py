@@ -37,6 +37,7 @@ if sys.argv[1:] == ["stamps"]:  # the resident call's host / device split (print
     print(json.dumps({"single_resident_us": round(run({"loopStamps": True}), 1)}))
     sys.exit(0)
 out = {"single_resident_us": round(run({}), 1),
+       "single_resident_pct0_us": round(run({"percentageOfNodesToScore": 0}), 1),
        "single_launch_us": round(run({"residentLoop": False}), 1),
        "single_launch_no_loop_us": round(run({"residentLoop": False, "persistentLoop": False}), 1),
        "batch_us_per_pod": round(run({}, batch=True), 2)}

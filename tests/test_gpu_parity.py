@@ -649,7 +649,7 @@ def test_cache_churn_matches_oracle(native, seed):
 @pytest.mark.parametrize("pct", [0, 30])
 def test_sampling_pipelined_batch(native, pct):
     """Default-plugin pods in 600-pod batches take the chunked pipeline; the device-resident
-    nextStartNodeIndex crosses the chunks (and the launch path replaces the persistent loop)."""
+    nextStartNodeIndex crosses the chunks (k_sched_loop carries it from pod to pod and launch to launch)."""
     from ksg import synth
     nodes, init, pods = synth.scheduling_basic(700, 100, 1200, hetero=True)
     g, o = _pair(native, {"percentageOfNodesToScore": pct}, nodes, init)
@@ -755,6 +755,64 @@ def test_resident_single_pod_calls(native):
     time.sleep(0.08)  # longer than the loop's idle self-stop
     for k in range(160, 1300):  # past one launch's kLoopMaxPods
         one(rand_pod(rng, k, names, topology=False), f"pod {k}")
+    assert g.compare_mirror(sync=True)[0] == 0
+
+
+@pytest.mark.parametrize("unit", [128, 256])
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 5, 6])
+def test_sched_loop_sampling_matches_oracle(native, unit, k):
+    """percentageOfNodesToScore inside k_sched_loop: the cut to the first K feasible nodes of the rotated
+    order, processedNodes from the (K+1)-th node's workgroup, nextStartNodeIndex carried pod to pod, the
+    kept-list maxima exchange (PreferNoSchedule taints, preferred node affinity), and runs broken by
+    launch-path pods (PodTopologySpread / InterPodAffinity) that read the loop's rotation and back."""
+    pct, extra = SAMPLING[k]
+    for seed, (n_nodes, topo) in enumerate([(700, False), (1900, True), (5000, False)]):
+        rng, cfg, nodes, existing, names = rand_cluster(9400 + 10 * k + seed, n_nodes=n_nodes, n_existing=120,
+                                                        topology=topo)
+        g, o = _pair(native, dict(cfg, **extra, percentageOfNodesToScore=pct, loopUnit=unit), nodes, existing)
+        for rnd in range(2):
+            pods = [rand_pod(rng, 500 * rnd + q, names, topology=topo and q % 5 == 2) for q in range(150)]
+            rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+            if not topo:
+                assert g.kernel_stats()[3] == "k_sched_loop"
+            for q, p in enumerate(pods):
+                ro, _ = o.schedule_one(o.compile(p), assume=True)
+                assert rs[q].as_tuple() == ro.as_tuple(), f"pct {pct} nodes {n_nodes} batch {rnd} pod {q}"
+        assert g.compare_mirror(sync=False) == (0, -1)
+
+
+def test_sched_loop_sampling_scheduling_basic(native):
+    """SchedulingBasic at upstream's adaptive default (percentageOfNodesToScore 0: 10 % of 5000 nodes)
+    through k_sched_loop, every score tied: the heap pre-order over the cut list and the rotation."""
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(5000, 1000, 1200)
+    g, o = _pair(native, {"percentageOfNodesToScore": 0}, nodes, init)
+    for rnd in range(2):
+        part = pods[600 * rnd:600 * (rnd + 1)]
+        rs = g.schedule_batch([g.compile(p) for p in part], assume=True)
+        assert g.kernel_stats()[3] == "k_sched_loop"
+        for q, p in enumerate(part):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[q].as_tuple() == ro.as_tuple(), f"batch {rnd} pod {q}"
+
+
+@pytest.mark.parametrize("pct", [0, 30])
+def test_resident_single_pod_calls_sampling(native, pct):
+    """The resident loop with percentageOfNodesToScore: each call's rotation start is the host's
+    nextStartNodeIndex, which the call's result (processedNodes) advances; batches in between."""
+    rng, cfg, nodes, existing, names = rand_cluster(9320 + pct, n_nodes=1300, n_existing=90, topology=False)
+    g, o = _pair(native, dict(cfg, percentageOfNodesToScore=pct), nodes, existing)
+    for k in range(200):
+        pod = rand_pod(rng, k, names, topology=False)
+        rg, _ = g.schedule_one(g.compile(pod), assume=True)
+        ro, _ = o.schedule_one(o.compile(pod), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"pod {k}: {rg.as_tuple()} != {ro.as_tuple()}"
+        if k % 50 == 49:
+            batch = [rand_pod(rng, 1000 + k * 10 + j, names, topology=False) for j in range(20)]
+            rs = g.schedule_batch([g.compile(p) for p in batch], assume=True)
+            for j, p in enumerate(batch):
+                ro, _ = o.schedule_one(o.compile(p), assume=True)
+                assert rs[j].as_tuple() == ro.as_tuple(), f"batch after pod {k}, pod {j}"
     assert g.compare_mirror(sync=True)[0] == 0
 
 
