@@ -524,6 +524,7 @@ constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local hi
 constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
 constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
 constexpr int kAGran = 12;         // granules per participant per pod
+constexpr int kAggStartRow = 1024; // k_agg_loop (node-sharded): the start barrier's granule row (= kLoopMaxPods)
 enum AggGran : int {
   AG_Z0 = 0,   // {InterPodAffinity "any" bits}: every count of the pod is in the shared region
   AG_Z1 = 1,   // node-local DoNotSchedule constraint 0: {min count over my eligible nodes (24) | eligible nodes (20)}
@@ -552,8 +553,14 @@ struct AggView {
   int32_t gwords;             // region words per pod (max agg_gwords of the run)
   int32_t debug;              // diagnostic: bit 0 never fold (gather every pod after the previous one is
                               // placed), bit 1 never DF_LFAST (config "aggLoopDebug")
-  unsigned long long* gran;   // [npods][nwg][kAGran]
-  unsigned long long* region; // [npods][gwords]: shared-region partial sums (zeroed by the host)
+  unsigned long long* gran;   // [npods][world * nwg][kAGran] (this rank's)
+  unsigned long long* region; // [npods][gwords]: shared-region sums (zeroed by the host; this rank's)
+  // node shards: participants are world * nwg workgroups, rank-major.  Every granule and
+  // every shared-region partial goes into each rank's array (the peers' are IPC-mapped, uncached).
+  // (the peers' pointers live in device memory, not in the kernel arguments: SGPR pressure)
+  int32_t world, rank;
+  unsigned long long* const* grans;    // [world] every rank's granule array
+  unsigned long long* const* regions;  // [world] every rank's regions
   uint32_t* fail;             // set when a spin gives up
   const uint32_t* desc_bytes; // [batch pods] program sizes
   unsigned long long* stamps; // diagnostic: [npods][kAggStamps] (nullptr)

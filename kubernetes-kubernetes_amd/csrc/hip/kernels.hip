@@ -2525,16 +2525,26 @@ __device__ __forceinline__ int64_t agg_total(const PodDesc& d, int64_t fixed, in
   return total;
 }
 
-__device__ __forceinline__ void agran_put(const AggView& av, int q, int w, int slot, unsigned long long payload) {
-  __hip_atomic_store(av.gran + ((size_t)q * av.nwg + w) * kAGran + slot,
-                     ((unsigned long long)av.tag << 48) | (payload & kPayload), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// publish granule `slot` of participant gid (rank-major) for pod q: unsharded, an agent-scope store;
+// node-sharded, a system-scope store into every rank's array (k_sched_loop's gran_put)
+template <bool SHARD>
+__device__ __forceinline__ void agran_put(const AggView& av, int q, int gid, int slot, unsigned long long payload) {
+  const size_t at = ((size_t)q * (SHARD ? av.world : 1) * av.nwg + gid) * kAGran + slot;
+  const unsigned long long v = ((unsigned long long)av.tag << 48) | (payload & kPayload);
+  if constexpr (!SHARD) {
+    __hip_atomic_store(av.gran + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+#pragma unroll
+    for (int r = 0; r < kMaxShards; ++r)
+      if (r < av.world) __hip_atomic_store(av.grans[r] + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
-// One wave: poll granules [slot0, slot0 + NS) of every workgroup for pod q until all tags match.
-template <int NS>
+// One wave: poll granules [slot0, slot0 + NS) of every participant for pod q until all tags match.
+template <bool SHARD, int NS>
 __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep],
                                            int nact = NS) {  // only granules [slot0, slot0 + nact) are polled
   const int lane = threadIdx.x & 63;
-  const int P = av.nwg;
+  const int P = (SHARD ? av.world : 1) * av.nwg;
   const unsigned long long* g = av.gran + (size_t)q * P * kAGran + slot0;
   const unsigned long long want = (unsigned long long)av.tag;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -2546,7 +2556,9 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
 #pragma unroll
       for (int k = 0; k < NS; ++k) {
         unsigned long long y = want << 48;
-        if (v < P && k < nact) y = __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v < P && k < nact)
+          y = SHARD ? __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                    : __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok &= (y >> 48) == want;
         x[k][r] = y & kPayload;
       }
@@ -2567,68 +2579,8 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
   }
 }
 
-// agran_sweep without holding every participant's granules: each pass visits participant groups of
-// 64 one after another (visit(v, x) per lane, after reset()), and is kept only if every tag matched.
-template <int NS, typename Reset, typename Visit>
-__device__ __forceinline__ bool agran_sweep_visit(const AggView& av, int q, int slot0, Reset&& reset, Visit&& visit) {
-  const int lane = threadIdx.x & 63;
-  const int P = av.nwg;
-  const unsigned long long* g = av.gran + (size_t)q * P * kAGran + slot0;
-  const unsigned long long want = (unsigned long long)av.tag;
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  for (uint32_t spins = 0;; ++spins) {
-    bool ok = true;
-    reset();
-#pragma unroll 1
-    for (int r = 0; r < kMaxSweep && 64 * r < P; ++r) {
-      const int v = lane + 64 * r;
-      unsigned long long x[NS];
-#pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        const unsigned long long y =
-            v < P ? __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : want << 48;
-        ok &= (y >> 48) == want;
-        x[k] = y & kPayload;
-      }
-      if (v < P) visit(v, x);
-    }
-    if (__all(ok)) return true;
-    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
-      if (lane == 0) {
-        __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return false;
-    }
-    if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// One lane: poll granule `slot` of participant p for pod q (give-up as agran_sweep).
-__device__ __forceinline__ bool agran_poll1(const AggView& av, int q, int p, int slot, unsigned long long* out) {
-  const unsigned long long* g = av.gran + ((size_t)q * av.nwg + p) * kAGran + slot;
-  const unsigned long long want = (unsigned long long)av.tag;
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  for (uint32_t spins = 0;; ++spins) {
-    const unsigned long long y = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((y >> 48) == want) {
-      *out = y & kPayload;
-      return true;
-    }
-    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
-      __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(av.fail + 2, (uint32_t)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(av.fail + 3, (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
+// SHARD: node-sharded over the device exchange (av.world > 1); the unsharded instance compiles none of it
+template <bool SHARD>
 __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
@@ -2669,6 +2621,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ int32_t s_fv[kFoldMax];  // the chosen node's value id of each item's slot
   __shared__ uint32_t s_nfi;
   __shared__ int s_pw;                // participant whose key won the pod just decided
+  __shared__ int s_rnode;             // node-sharded: that participant's chosen node (global snapshot index)
   __shared__ uint32_t s_el;           // the chosen node's DoNotSchedule eligibility for the next pod
   __shared__ int s_bn_q;              // the pod whose chosen node (s_gnode, s_el) wave 0 has resolved
   __shared__ int s_a_q, s_p2_q;       // wave 0 -> 1: exchange A of pod q swept; wave 1 -> 0: its phase-2 half done
@@ -2678,6 +2631,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ int64_t s_mx[4];
   __shared__ uint32_t s_pmult[kAggMaxCons];  // DoNotSchedule: present domains at the minimum
   const int w = blockIdx.x, G = av.nwg;
+  const int P = SHARD ? av.world * G : G, gid = SHARD ? av.rank * G + w : w;  // participants (rank-major), mine
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int nlo = k0 * kBlock, nhi = k1 * kBlock < m.n ? k1 * kBlock : m.n;
@@ -2847,7 +2801,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     gbar();
     // my partials of the shared region; node-local DoNotSchedule minima over my eligible nodes
     for (int x = tid; x < gw; x += nthr)
-      if (s_gh[x]) atomicAdd(region + x, s_gh[x]);
+      if (s_gh[x]) {
+        if constexpr (!SHARD) {
+          atomicAdd(region + x, s_gh[x]);
+        } else {  // node-sharded: the sums are global in every rank's region
+          for (int r = 0; r < av.world; ++r)
+            __hip_atomic_fetch_add(av.regions[r] + (size_t)q * av.gwords + x, s_gh[x], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
     if (d.agg_local_cons) {
       int li = 0;
       for (int32_t c = 0; c < d.n_ptsf && li < kAggLocalCons; ++c) {
@@ -2868,6 +2830,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my region atomics performed before Z
+    if constexpr (SHARD) __threadfence_system();       // ... at the peers too
     gbar();
     if (tid == 0) {  // every Z granule is published (zero for an absent constraint)
       unsigned long long z[2] = {0, 0};
@@ -2876,20 +2839,20 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         const unsigned long long m24 = mn > 0xffffffll ? 0xffffffull : (unsigned long long)mn;
         z[li] = ((unsigned long long)s_lcnt[li] << 24) | m24;  // no eligible node: min 2^24-1
       }
-      agran_put(av, q, w, AG_Z0, s_gany);
-      agran_put(av, q, w, AG_Z1, z[0]);
-      agran_put(av, q, w, AG_Z2, z[1]);
+      agran_put<SHARD>(av, q, gid, AG_Z0, s_gany);
+      agran_put<SHARD>(av, q, gid, AG_Z1, z[0]);
+      agran_put<SHARD>(av, q, gid, AG_Z2, z[1]);
     }
   };
   // exchange Z of pod q (wave 0): OR of the any bits, node-local minima and domain counts
   auto sweep_z = [&](int q) __attribute__((always_inline)) {
     unsigned long long z[3][kMaxSweep];
-    const bool ok = agran_sweep<3>(av, q, AG_Z0, z);
+    const bool ok = agran_sweep<SHARD, 3>(av, q, AG_Z0, z);
     uint32_t a = 0, c1 = 0, c2 = 0;
     unsigned long long m1 = 0xffffffull, m2 = 0xffffffull;
 #pragma unroll
     for (int r = 0; r < kMaxSweep; ++r)
-      if (lane + 64 * r < G) {
+      if (lane + 64 * r < P) {
         a |= (uint32_t)z[0][r];
         const unsigned long long x1 = z[1][r] & 0xffffffull, x2 = z[2][r] & 0xffffffull;
         c1 += (uint32_t)(z[1][r] >> 24);
@@ -2919,7 +2882,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(s_blob[q % 3]);
     const unsigned long long* region = av.region + (size_t)q * av.gwords;
     for (int x = tid; x < d.agg_gwords; x += nthr)
-      s_gh[x] = __hip_atomic_load(region + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_gh[x] = SHARD ? __hip_atomic_load(region + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                      : __hip_atomic_load(region + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   // DoNotSchedule minima (criticalPaths, filtering.go:64-124): shared constraints over their present
   // domains (one wave each), node-local ones from exchange Z (all threads; then a barrier)
@@ -3124,6 +3088,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     if (t == 0) fail(0xfffffffeu);
     return;
   }
+  if (SHARD && av.npods > 0) {
+    // every rank zeroed its regions before its launch (stream order): no workgroup adds into a peer's
+    // region before every participant has started (one granule row past the pods, kAggStartRow)
+    if (t == 0) agran_put<SHARD>(av, kAggStartRow, gid, 0, 1ull);
+    if (wave == 0) {
+      unsigned long long x0[1][kMaxSweep];
+      if (!agran_sweep<SHARD, 1>(av, kAggStartRow, 0, x0) && lane == 0) s_ok = 0u;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+  }
   if (av.npods > 0) {
     aggregate(0, t, kAggThreads, wg_bar);
     if (wave == 0) sweep_z(0);
@@ -3257,10 +3232,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           // raw InterPodAffinity biased into [1, 2^47): max as is, min reversed (max of 2^47 - x)
           const unsigned long long bi = c ? (unsigned long long)(dec_i64(mi) + kAggIpaBias) + 1ull : 0ull;
           const unsigned long long bn = c ? (1ull << 47) - (unsigned long long)(dec_i64(ni) + kAggIpaBias) : 0ull;
-          agran_put(av, q, w, AG_A0, g0);
-          agran_put(av, q, w, AG_A1, g1);
-          agran_put(av, q, w, AG_A2, bi);
-          agran_put(av, q, w, AG_A3, bn);
+          agran_put<SHARD>(av, q, gid, AG_A0, g0);
+          agran_put<SHARD>(av, q, gid, AG_A1, g1);
+          agran_put<SHARD>(av, q, gid, AG_A2, bi);
+          agran_put<SHARD>(av, q, gid, AG_A3, bn);
           if ((d.score_mask >> P_PTS) & 1u) {  // PodTopologySpread: domain presence, non-ignored count
             uint32_t ni = 0;
             unsigned long long p0 = 0, p1 = 0;
@@ -3269,24 +3244,24 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
               p0 |= s_wp[v][0];
               p1 |= s_wp[v][1];
             }
-            agran_put(av, q, w, AG_P0, p0 & ((1ull << 48) - 1ull));
-            agran_put(av, q, w, AG_P1, (unsigned long long)(ni & 0xfffffu) |
+            agran_put<SHARD>(av, q, gid, AG_P0, p0 & ((1ull << 48) - 1ull));
+            agran_put<SHARD>(av, q, gid, AG_P1, (unsigned long long)(ni & 0xfffffu) |
                                            ((((p0 >> 48) | (p1 << 16)) & ((1ull << 28) - 1ull)) << 20));
           }
           wstamp(q, 1);
         }
         const bool pts_q = ((d.score_mask >> P_PTS) & 1u) != 0;
         unsigned long long xa[6][kMaxSweep];
-        const bool ok = agran_sweep<6>(av, q, AG_A0, xa, pts_q ? 6 : 4);
+        const bool ok = agran_sweep<SHARD, 6>(av, q, AG_A0, xa, pts_q ? 6 : 4);
         uint32_t F = 0, wp = 0, bf = 0;
         unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
 #pragma unroll
         for (int r = 0; r < kMaxSweep; ++r) {
           const int v = lane + 64 * r;
-          if (v < G) {
+          if (v < P) {
             const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
             F += c;
-            if (v < w) wp += c;
+            if (v < gid) wp += c;
             bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
             const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
             tmax = tv > tmax ? tv : tmax;
@@ -3307,7 +3282,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           unsigned long long p0 = 0, p1 = 0;
 #pragma unroll
           for (int r = 0; r < kMaxSweep; ++r)
-            if (lane + 64 * r < G) {
+            if (lane + 64 * r < P) {
               ni += (uint32_t)(xa[5][r] & 0xfffffull);
               p0 |= xa[4][r];
               p1 |= xa[5][r] >> 20;
@@ -3398,13 +3373,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             __builtin_amdgcn_s_sleep(1);
           hmx = s_pxm[0] > hmx ? s_pxm[0] : hmx;
           hmn = s_pxm[1] > hmn ? s_pxm[1] : hmn;
-          if (lane == 0) agran_put(av, q, w, AG_PX, (hmx << 24) | hmn);
+          if (lane == 0) agran_put<SHARD>(av, q, gid, AG_PX, (hmx << 24) | hmn);
           unsigned long long xp[1][kMaxSweep];
-          const bool okp = agran_sweep<1>(av, q, AG_PX, xp);
+          const bool okp = agran_sweep<SHARD, 1>(av, q, AG_PX, xp);
           unsigned long long gx = 0, gn = 0;
 #pragma unroll
           for (int r = 0; r < kMaxSweep; ++r)
-            if (lane + 64 * r < G) {
+            if (lane + 64 * r < P) {
               const unsigned long long a = xp[0][r] >> 24, bb = xp[0][r] & 0xffffffull;
               gx = a > gx ? a : gx;
               gn = bb > gn ? bb : gn;
@@ -3482,7 +3457,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           wn = s_p2n;
         }
         if (lane == 0) {
-          agran_put(av, q, w, AG_B, wk);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
+          agran_put<SHARD>(av, q, gid, AG_B, wk);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
           wstamp(q, 2);
           stamp(q, 12);
           // my candidate and its DoNotSchedule eligibility for pod q+1 (the gathering group's node
@@ -3496,16 +3471,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
               el = s_elig[wn - nlo];
             }
           }
-          agran_put(av, q, w, AG_BN, (unsigned long long)(uint32_t)(wn + 1) | ((unsigned long long)el << 32));
+          agran_put<SHARD>(av, q, gid, AG_BN, (unsigned long long)(uint32_t)(wn + 1) | ((unsigned long long)el << 32));
         }
         stamp(q, 3);
         unsigned long long xb[2][kMaxSweep];
-        const bool okb = ok && agran_sweep<2>(av, q, AG_B, xb);
+        const bool okb = ok && agran_sweep<SHARD, 2>(av, q, AG_B, xb);
         unsigned long long bmx = 0, bnx = 0;
         int bpart = -1;
 #pragma unroll
         for (int r = 0; r < kMaxSweep; ++r) {
-          const unsigned long long v = (lane + 64 * r) < G ? xb[0][r] : 0ull;
+          const unsigned long long v = (lane + 64 * r) < P ? xb[0][r] : 0ull;
           if (v > bmx) {
             bmx = v;
             bnx = xb[1][r];
@@ -3518,13 +3493,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         const int pw = (F > 0 && bh) ? __builtin_amdgcn_readlane(bpart, hl) : -1;
         const uint32_t bnlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bnx, hl);
         const uint32_t bnhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bnx >> 32), hl);
-        const int gnode = (F > 0 && pw == w) ? wn : -1;  // the chosen node, if it is mine
+        const int gnode = (F > 0 && pw == gid) ? wn : -1;  // the chosen node, if it is mine
         // ======== commit (lane 0): the owner of the chosen node applies AssumePod to its LDS core and
         // the mirror; the pod joins my lists before the next pod that counts it ========
         if (lane == 0) {
           if (!okb) s_ok = 0u;
           s_best = gbest;
           s_pw = pw;
+          if (SHARD) s_rnode = (int)bnlo - 1;  // the chosen node (global index), for a replica's commit
           s_pend_ls = -1;
           if (okb) {
             if (F == 0) {
@@ -3580,6 +3556,21 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     }
     __syncthreads();
     if (!s_ok) return;
+    if (SHARD && t == 0 && w == 0 && s_F > 0 && s_pw >= 0 && s_pw / G != av.rank) {
+      // chosen on another rank: the result, and the pod joins this replica's pod table (the k_aggregate
+      // pod role of later launch-path pods reads it).  The node's mirror columns are not mine in this
+      // launch; the host uploads them with the next cycle's node updates (Cluster::add_pod).
+      DevResult r;
+      r.node = s_rnode;
+      r.feasible = (int32_t)s_F;
+      r.evaluated = 0;
+      r.total = (int64_t)(s_best >> kPreBits);
+      r.key = s_best;
+      r.status = (int32_t)C_OK;
+      r.ipa_any = ipa_any;
+      b.results[pod] = r;
+      if ((d.flags & DF_ASSUME) && d.slot >= 0) m.pod_node[d.slot] = s_rnode;
+    }
     stamp(q, 5);
 
     // ======== pod q+1's counts, final ========
@@ -3845,10 +3836,17 @@ hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const Loop
 }
 hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
                            hipEvent_t t1) {
-  if (t0)
-    hipExtLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
-  else
-    hipLaunchKernelGGL(k_agg_loop, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
+  if (av.world > 1) {
+    if (t0)
+      hipExtLaunchKernelGGL(k_agg_loop<true>, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
+    else
+      hipLaunchKernelGGL(k_agg_loop<true>, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
+  } else {
+    if (t0)
+      hipExtLaunchKernelGGL(k_agg_loop<false>, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
+    else
+      hipLaunchKernelGGL(k_agg_loop<false>, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
+  }
   return hipGetLastError();
 }
 // Loads the module's code object onto the current device now (hipFuncGetAttributes), so that no
@@ -3864,7 +3862,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_sched_loop<4, true>), reinterpret_cast<const void*>(&k_sched_loop<2, true>),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_sample_shard_a),
                       reinterpret_cast<const void*>(&k_sample_shard_b),        reinterpret_cast<const void*>(&k_node_update),
-                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop),
+                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop<false>),
+                      reinterpret_cast<const void*>(&k_agg_loop<true>),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);

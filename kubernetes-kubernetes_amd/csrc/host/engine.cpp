@@ -1070,7 +1070,7 @@ Engine::~Engine() {
   if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps,
-                    &d_evg, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf})
+                    &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -1183,13 +1183,53 @@ int Engine::gran_setup() {
   return KSG_OK;
 }
 
-// Each loop launch gets the next tag (every rank issues the same launches, so the tags agree).
-// After 65535 launches the array is zeroed again; sharded, behind an exchange, so that no rank
-// publishes into a peer's array before that peer has cleared it.
+// k_agg_loop's granule array ((kLoopMaxPods + 1) rows: the last is the node-sharded start barrier) and
+// its per-pod shared regions (kAggGWords words per pod), fixed size, zeroed once.  Node-sharded, both
+// are uncached device memory shared over IPC like k_sched_loop's granules: every workgroup stores its
+// granules and adds its shared-key partials into every rank's copy.
+int Engine::agg_setup() {
+  if (!agran_all.empty()) return KSG_OK;
+  const size_t gb = (size_t)(kLoopMaxPods + 1) * 256 * kAGran * 8, rb = (size_t)kLoopMaxPods * kAggGWords * 8;
+  for (DevBuf* b : {&d_agran, &d_region}) {
+    const size_t bytes = b == &d_agran ? gb : rb;
+    if (b->p) (void)hipFree(b->p);
+    void* p = nullptr;
+    if (comm) HIPCHK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
+    else HIPCHK(hipMalloc(&p, bytes));
+    b->p = p;
+    b->bytes = bytes;
+    HIPCHK(hipMemset(p, 0, bytes));
+  }
+  HIPCHK(hipDeviceSynchronize());
+  if (comm) {
+    std::vector<void*> ga, ra;
+    if (comm->share_buffers(d_agran.p, &ga) || comm->share_buffers(d_region.p, &ra)) {
+      c->err = comm->err;
+      return KSG_EDEVICE;
+    }
+    for (void* q : ga) agran_all.push_back((unsigned long long*)q);
+    for (void* q : ra) region_all.push_back((unsigned long long*)q);
+    // the peer tables k_agg_loop reads (AggView::grans / regions): [0, W) granules, [W, 2W) regions
+    std::vector<unsigned long long*> tab(agran_all);
+    tab.insert(tab.end(), region_all.begin(), region_all.end());
+    int rc;
+    if ((rc = ensure(d_aggpeers, tab.size() * sizeof(void*)))) return rc;
+    HIPCHK(hipMemcpy(d_aggpeers.p, tab.data(), tab.size() * sizeof(void*), hipMemcpyHostToDevice));
+  } else {
+    agran_all.push_back((unsigned long long*)d_agran.p);
+    region_all.push_back((unsigned long long*)d_region.p);
+  }
+  return KSG_OK;
+}
+
+// Each loop launch (k_sched_loop or k_agg_loop) gets the next tag (every rank issues the same launches,
+// so the tags agree).  After 65535 launches the arrays are zeroed again; sharded, behind an exchange, so
+// that no rank publishes into a peer's array before that peer has cleared it.
 int Engine::next_gran_tag(uint32_t* tag) {
   if (++gran_tag > 0xFFFFu) {
     gran_tag = 1;
-    HIPCHK(hipMemsetAsync(d_gran.p, 0, d_gran.bytes, c->stream));
+    if (d_gran.p) HIPCHK(hipMemsetAsync(d_gran.p, 0, d_gran.bytes, c->stream));
+    if (d_agran.p) HIPCHK(hipMemsetAsync(d_agran.p, 0, d_agran.bytes, c->stream));
     if (comm) {
       int rc;
       if ((rc = ensure(d_xb, XB_WORDS * 8))) return rc;
@@ -1461,10 +1501,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const bool use_loop = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && GS >= 1 &&
                         (int64_t)GS * kLoopMaxBlk * unit >= (int64_t)NBs * kBlock &&
                         (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
-  // k_agg_loop (unsharded): the same geometry; every workgroup's LDS lists must hold its nodes' pods
-  // and terms plus everything this batch can add (each pod, and its own terms, at most once)
-  bool use_agg = loop_worth && !comm && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 && G <= cus &&
-                 (int64_t)G * kLoopMaxBlk >= NB && (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
+  // k_agg_loop: the same geometry (node-sharded: over the device exchange, world * G participants);
+  // every workgroup's LDS lists must hold its nodes' pods and terms plus everything this batch can add
+  // (each pod, and its own terms, at most once).  Every rank decides alike: the check covers every
+  // rank's workgroups (each rank holds the whole cluster).
+  bool use_agg = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 &&
+                 G * W <= std::min(cus, 256) && (int64_t)G * kLoopMaxBlk >= NBs &&
+                 (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   if (use_agg) {
     bool any = false;
     int64_t own = 0;
@@ -1475,9 +1518,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       for (int i = 0; i < compiled; ++i) own += cp[i].own_terms;
     use_agg = any && c->pt_node.size() < ((size_t)1 << 23) && c->tt.size() < ((size_t)1 << 23);
     if (use_agg) {
-      std::vector<int32_t> wg_of((size_t)NB), np((size_t)G, 0), nt((size_t)G, 0);
-      for (int w = 0; w < G; ++w)
-        for (int64_t k = (int64_t)NB * w / G; k < (int64_t)NB * (w + 1) / G; ++k) wg_of[(size_t)k] = w;
+      // participant p = r * G + w owns blocks [b0_r + nb_r * w / G, b0_r + nb_r * (w + 1) / G) (shard_range)
+      std::vector<int32_t> wg_of((size_t)NB), np((size_t)G * W, 0), nt((size_t)G * W, 0);
+      for (int r = 0; r < W; ++r) {
+        const int64_t b0 = (int64_t)NB * r / W, nb = (int64_t)NB * (r + 1) / W - b0;
+        for (int w = 0; w < G; ++w)
+          for (int64_t k = b0 + nb * w / G; k < b0 + nb * (w + 1) / G; ++k) wg_of[(size_t)k] = r * G + w;
+      }
       for (int32_t nd : c->pt_node)
         if (nd >= 0 && nd < m.n) np[(size_t)wg_of[(size_t)(nd / kBlock)]]++;
       for (const DTerm& tm : c->tt) {
@@ -1490,9 +1537,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   struct LoopRun { int first, count; double bytes; bool agg, timed; };
   std::vector<LoopRun> runs;
+  std::vector<uint8_t> agg_pod((size_t)n, 0);  // scheduled by k_agg_loop (settle: node-sharded replicas)
+  const int shard_lo = sblk0 * kBlock, shard_hi = (sblk0 + snblk) * kBlock;
   // loopTimingStride k: every k-th loop launch carries HIP events on its dispatch packet (0: none)
   auto loop_timed = [&](size_t r) { return c->cfg.loop_timing_stride > 0 && r % (size_t)c->cfg.loop_timing_stride == 0; };
-  if (use_agg && (rc = ensure(d_agran, (size_t)kLoopMaxPods * 256 * kAGran * 8))) return rc;
+  if (use_agg && (rc = agg_setup())) return rc;
   if (use_loop || use_agg) {
     if (use_loop && (rc = gran_setup())) return rc;
     if ((rc = ensure(d_fail, 16))) return rc;
@@ -1557,7 +1606,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
         static uint64_t seq = 0;
         std::string uid = pods[i]->uid + "#a" + std::to_string(++seq);
-        int rc2 = c->add_pod(*pods[i], uid, /*device_done=*/true, cp[i].slot, &c->order()[r.node_index], &cp[i].res);
+        // a node-sharded k_agg_loop applies the AssumePod to the mirror on the node's own rank only (the
+        // other ranks record the result and the pod table entry): theirs go up with the next node updates
+        const bool foreign = agg_pod[(size_t)i] && comm &&
+                             (r.node_index < shard_lo || r.node_index >= shard_hi);
+        int rc2 = c->add_pod(*pods[i], uid, /*device_done=*/!foreign, cp[i].slot, &c->order()[r.node_index], &cp[i].res);
         if (rc2) return rc2;
         assumed[handles.empty() ? -1 : handles[i]] = uid;
       } else {
@@ -1710,20 +1763,21 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         HIPCHK(hipEventCreate(&e));
         lev.push_back(e);
       }
-      const size_t rbytes = (size_t)(j - i) * (size_t)gw * 8;
-      if ((rc = ensure(d_region, rbytes))) return rc;
-      HIPCHK(hipMemsetAsync(d_region.p, 0, rbytes, s));
-      if (++agran_tag > 0xFFFFu) {
-        agran_tag = 1;
-        HIPCHK(hipMemsetAsync(d_agran.p, 0, d_agran.bytes, s));
-      }
+      const size_t rbytes = (size_t)(j - i) * (size_t)gw * 8;  // <= kLoopMaxPods * kAggGWords words
+      HIPCHK(hipMemsetAsync(d_region.p, 0, rbytes, s));  // (sharded: the loop's start barrier orders the peers' adds)
       AggView av{};
       av.first_pod = i;
       av.npods = j - i;
       av.nwg = G;
-      av.blk0 = 0;
-      av.nblk = NB;
-      av.tag = agran_tag;
+      av.blk0 = sblk0;
+      av.nblk = snblk;
+      av.world = W;
+      av.rank = comm ? c->cfg.rank : 0;
+      if (comm) {
+        av.grans = (unsigned long long* const*)d_aggpeers.p;
+        av.regions = (unsigned long long* const*)d_aggpeers.p + W;
+      }
+      if ((rc = next_gran_tag(&av.tag))) return rc;
       av.gwords = gw;
       av.debug = c->cfg.agg_debug;
       av.give_up_at = c->cfg.debug_give_up_at;
@@ -1739,9 +1793,15 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       av.stamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)i * kAggStamps : nullptr;
       av.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)n * kAggStamps + (size_t)i * G * 4
                                       : nullptr;
+      // in-process ranks: every rank is past its allocations before any rank's first loop starts
+      if (runs.empty() && comm && comm->launch_gate()) {
+        c->err = comm->err;
+        return KSG_EDEVICE;
+      }
       const bool tl = loop_timed(runs.size());
       HIPCHK(launch_agg_loop(m, bv, av, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr));
       runs.push_back({i, j - i, rb, true, tl});
+      std::fill(agg_pod.begin() + i, agg_pod.begin() + j, (uint8_t)1);
       launches += j - i;
       i = j;
       continue;

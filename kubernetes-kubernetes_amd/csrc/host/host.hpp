@@ -540,7 +540,9 @@ class Engine {
   DevBuf d_gran, d_fail, d_stamps;  // k_sched_loop: exchange granules (local), give-up flag, stamps
   std::vector<unsigned long long*> gran_all;  // every rank's granule array as mapped here ([rank] = d_gran)
   uint32_t gran_tag = 0;
-  DevBuf d_agran, d_region;  // k_agg_loop: exchange granules (own tag sequence), per-pod shared regions
+  DevBuf d_agran, d_region;  // k_agg_loop: exchange granules, per-pod shared regions (fixed size once set up)
+  std::vector<unsigned long long*> agran_all, region_all;  // every rank's, as mapped here (node-sharded)
+  DevBuf d_aggpeers;  // node-sharded k_agg_loop: the device copy of agran_all + region_all
   DevBuf d_astamps;          // k_agg_loop diagnostic stamps
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)
@@ -553,8 +555,8 @@ class Engine {
   int32_t seg_n = -1, seg_overflow = 0, seg_many_ports = 0;
   void seg_build(int32_t i, NodeRec& r);
   int seg_refresh();
-  uint32_t agran_tag = 0;
   int gran_setup();
+  int agg_setup();
   int next_gran_tag(uint32_t* tag);
   std::vector<hipEvent_t> lev;  // k_sched_loop timing events (pairs)
   std::vector<hipEvent_t> cev;  // run_batch pipeline: one event per chunk (results landed)

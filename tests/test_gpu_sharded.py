@@ -309,3 +309,61 @@ def test_c5_mixed_sharded_20k(world):
     nodes, init, pods = mixed_cluster(20000, 2000, 120)
     ranks, o = _group(world, {}, nodes, init)
     _check(ranks, o, pods, chunk=60)
+
+
+# ---- k_agg_loop across ranks (deviceExchange): PodTopologySpread / InterPodAffinity pods through the
+# persistent loop, granules and shared-key partials stored into every rank's arrays
+
+def _dominant(ranks):
+    return {s.kernel_stats()[3] for s in ranks}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c5_mixed_sharded_agg_loop(world):
+    """configs[4]'s mixed stream (node-local, spread and affinity pods) on 20000 nodes over W in-process
+    ranks with the device exchange: the spread / affinity pods run in the node-sharded k_agg_loop."""
+    from ksg.synth import mixed_cluster
+    nodes, init, pods = mixed_cluster(20000, 2000, 240)
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=120)
+    for s in ranks:
+        assert s.compare_mirror(sync=True)[0] == 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_sharded_agg_loop(world):
+    from ksg.synth import topology_spreading
+    nodes, init, pods = topology_spreading(2000 * world, 2000, 300)
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=300)
+    assert _dominant(ranks) == {"k_agg_loop"}
+
+
+def test_c4_anti_sharded_agg_loop():
+    from ksg.synth import topology_spreading
+    nodes, init, pods = topology_spreading(3000, 3000, 200, preferred_anti=True)
+    ranks, o = _group(3, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=200)
+    assert _dominant(ranks) == {"k_agg_loop"}
+
+
+def test_c3_sharded_agg_loop():
+    from ksg.synth import scheduling_pod_affinity
+    nodes, init, pods = scheduling_pod_affinity(2000, 2000, 300)
+    ranks, o = _group(2, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=300)
+    assert _dominant(ranks) == {"k_agg_loop"}
+    for s in ranks:
+        assert s.compare_mirror(sync=True)[0] == 0
+
+
+@pytest.mark.parametrize("world,seed", [(2, 5), (3, 6)])
+def test_random_streams_sharded_agg_loop(world, seed):
+    """Random PodTopologySpread / InterPodAffinity pods (zone- and hostname-keyed constraints and terms,
+    preferred terms, existing pods' terms) across ranks, mixed with node-local pods in one batch."""
+    rng, cfg, nodes, existing, names = rand_cluster(3100 + seed, n_nodes=1400 if seed == 5 else 1700,
+                                                    n_existing=200)
+    ranks, o = _group(world, dict(cfg, deviceExchange=True), nodes, existing)
+    _check(ranks, o, [rand_pod(rng, k, names) for k in range(200)], chunk=100)
+    for s in ranks:
+        assert s.compare_mirror(sync=True)[0] == 0
