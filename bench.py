@@ -113,6 +113,26 @@ def usable_cpus():
     return n
 
 
+def cpu_topology():
+    """What the CPU baseline's threads run on: affinity CPUs, the distinct physical cores among them (SMT
+    siblings share one), and the cgroup v2 CPU quota (in CPUs) if any."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            cores.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"affinity_cpus": len(cpus), "physical_cores": len(cores), "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), extra=None):
     """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
     Filter / Score loops over nodes on a pool of that many threads (the reference's
@@ -321,6 +341,7 @@ def main():
                              + ("; percentageOfNodesToScore < 100: the cut Filter pass is sequential, Score "
                                 "on the pool" if a.pct != 100 else ""),
                    "us_per_pod_by_section": bk,
+                   "host_cpus": cpu_topology(),
                    "single_thread": {"value": round(v1, 2), "cores": 1,
                                      "sample": f"first {done1} pods, {cdt1:.1f} s, 1 thread",
                                      "us_per_pod_by_section": bk1},

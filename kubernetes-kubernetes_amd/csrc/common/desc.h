@@ -166,6 +166,9 @@ enum DescFlags : uint32_t {
   DF_PTS_ANYTOPO = 1u << 20,       // PodTopologySpread scores with system-default constraints: requireAllTopologies
                                    // is false (podtopologyspread/scoring.go:141-144), no node is ignored and a node
                                    // without a constraint's key is in its "" domain (PtsCons::absent)
+  DF_AGG_SAME = 1u << 21,          // k_agg_loop: this pod's counts are defined exactly as the previous pod's of the
+                                   // batch (same program but for slot / rotation / own terms): its counts are that
+                                   // pod's plus its placement (fold), no gather (set by the host at staging)
 };
 
 struct PodDesc {

@@ -2089,6 +2089,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     if (sel) {
       // ======== selection wave: exchange A, phase 2, exchange B, pre-evaluation, staging ========
       stamp_s(q, 0);  // exchange A of this pod was published at the end of the previous one
+      if (lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
       unsigned long long xa[2][kMaxSweep];
       bool ok = gran_sweep<2>(lv, q, 0, xa);
       uint32_t F = 0, wp = 0, bf = 0;
@@ -2205,6 +2206,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           s_rot[npar] = rot_next;
         }
       }
+      if (lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 4] = __builtin_amdgcn_s_memrealtime();
       const unsigned long long gbest = wave_max_u64(bm);
       const unsigned long long bh = __ballot(bm == gbest && gbest != 0ull);  // keys are unique
       const int gnode = bh ? __builtin_amdgcn_readlane(bnode, (int)__builtin_ctzll(bh)) : -1;
@@ -2258,58 +2260,91 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         while (__hip_atomic_load(&s_e_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
                (uint32_t)(NW) * (uint32_t)(q + 2))
           __builtin_amdgcn_s_sleep(1);
+        // Everything both variants read is loaded at once (independent LDS reads, one round trip), and
+        // the candidate's replacement values are formed in registers: this runs between phase 1 of pod
+        // q+1 and exchange A, where the owner of the previous pod's node is already the latest.
+        uint32_t u0[NW], u1[NW];
+        unsigned long long x0[NW], x1[NW];
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+          u0[v] = s_u[npar][0][v];
+          u1[v] = s_u[npar][1][v];
+          x0[v] = s_x[npar][0][v];
+          x1[v] = s_x[npar][1][v];
+        }
         int cw = -1;
-        unsigned long long tm = 0, tn = 0;
+        unsigned long long tm = 0, tn = 0, nbal = 0;
+        uint32_t ccnt = 0, cbelow = 0;
         if (cand_ok) {  // the candidate's evaluation wave, as its partials will be if it wins
-          const int kw = cand / U - k0, sl = cand % U;
+          const int kw = cand / U - k0, sl = cand % U, cl = sl & 63;
           cw = sl >> 6;
-          const bool cf = ((s_ball2[kw][cw] >> (sl & 63)) & 1ull) != 0;
+          const unsigned long long b2 = s_ball2[kw][cw];
           const int64_t crt = s_rt2[kw][sl], crn = s_rn2[kw][sl];
+          unsigned long long bk[kLoopMaxBlk];
+          int64_t rtk[kLoopMaxBlk], rnk[kLoopMaxBlk];
+#pragma unroll
+          for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+            bk[kk] = kk < nk ? s_ball[npar][kk][cw] : 0ull;
+            rtk[kk] = kk < nk ? (int64_t)s_rt[npar][kk][sl] : 0;
+            rnk[kk] = kk < nk ? (int64_t)s_rn[npar][kk][sl] : 0;
+          }
           tm = s_tm[npar][cw * 64 + lane];
           tn = s_tn[npar][cw * 64 + lane];
-          if (lane == (sl & 63)) {
-            tm = tn = 0;
-            for (int kk = 0; kk < nk; ++kk) {
-              const bool f = kk == kw ? cf : ((s_ball[npar][kk][cw] >> lane) & 1ull) != 0;
-              if (f) {
-                const unsigned long long et = enc_i64(kk == kw ? crt : s_rt[npar][kk][sl]);
-                const unsigned long long en = enc_i64(kk == kw ? crn : s_rn[npar][kk][sl]);
-                tm = et > tm ? et : tm;
-                tn = en > tn ? en : tn;
-              }
+          const bool cf = ((b2 >> cl) & 1ull) != 0;
+          // the candidate lane's maxima over its blocks, block kw with the post-assume values (uniform)
+          unsigned long long am = 0, an = 0, old = 0;
+#pragma unroll
+          for (int kk = 0; kk < kLoopMaxBlk; ++kk) {
+            if (kk < nk) {
+              const bool f = kk == kw ? cf : ((bk[kk] >> cl) & 1ull) != 0;
+              const unsigned long long et = enc_i64(kk == kw ? crt : rtk[kk]);
+              const unsigned long long en = enc_i64(kk == kw ? crn : rnk[kk]);
+              am = f && et > am ? et : am;
+              an = f && en > an ? en : an;
+              old = kk == kw ? bk[kk] : old;
             }
+          }
+          if (lane == cl) {
+            tm = am;
+            tn = an;
           }
           tm = wave_max_u64(tm);
           tn = wave_max_u64(tn);
-          if (lane == 0) {
-            const unsigned long long old = s_ball[npar][kw][cw];
-            const unsigned long long bit = 1ull << (sl & 63);
-            const unsigned long long nbal = cf ? (old | bit) : (old & ~bit);
-            const int lim = nd.rot_start - ((k0 + kw) * U + cw * 64);
-            const unsigned long long bmk = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
-            s_cball = nbal;
-            s_ccnt = s_u[npar][0][cw] - (uint32_t)__popcll(old) + (uint32_t)__popcll(nbal);
-            s_cbelow = s_u[npar][1][cw] - (uint32_t)__popcll(old & bmk) + (uint32_t)__popcll(nbal & bmk);
-            s_cmt = tm;
-            s_cmn = tn;
+          const unsigned long long bit = 1ull << cl;
+          nbal = cf ? (old | bit) : (old & ~bit);
+          const int lim = nd.rot_start - ((k0 + kw) * U + cw * 64);
+          const unsigned long long bmk = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+          uint32_t ucw0 = 0, ucw1 = 0;
+#pragma unroll
+          for (int v = 0; v < NW; ++v) {
+            ucw0 = v == cw ? u0[v] : ucw0;
+            ucw1 = v == cw ? u1[v] : ucw1;
           }
+          ccnt = ucw0 - (uint32_t)__popcll(old) + (uint32_t)__popcll(nbal);
+          cbelow = ucw1 - (uint32_t)__popcll(old & bmk) + (uint32_t)__popcll(nbal & bmk);
         }
         if (lane == 0) {
           uint32_t c = 0, bl = 0, cc = 0, cbl = 0;
           unsigned long long xa = 0, xb = 0, ca = 0, cb = 0;
+#pragma unroll
           for (int v = 0; v < NW; ++v) {
-            const uint32_t u0 = s_u[npar][0][v], u1 = s_u[npar][1][v];
-            const unsigned long long x0v = s_x[npar][0][v], x1v = s_x[npar][1][v];
-            c += u0;
-            bl += u1;
-            xa = x0v > xa ? x0v : xa;
-            xb = x1v > xb ? x1v : xb;
-            const uint32_t w0 = v == cw ? s_ccnt : u0, w1 = v == cw ? s_cbelow : u1;
-            const unsigned long long y0 = v == cw ? tm : x0v, y1 = v == cw ? tn : x1v;
+            c += u0[v];
+            bl += u1[v];
+            xa = x0[v] > xa ? x0[v] : xa;
+            xb = x1[v] > xb ? x1[v] : xb;
+            const uint32_t w0 = v == cw ? ccnt : u0[v], w1 = v == cw ? cbelow : u1[v];
+            const unsigned long long y0 = v == cw ? tm : x0[v], y1 = v == cw ? tn : x1[v];
             cc += w0;
             cbl += w1;
             ca = y0 > ca ? y0 : ca;
             cb = y1 > cb ? y1 : cb;
+          }
+          if (cw >= 0) {  // the owner's commit installs these (after the barrier)
+            s_cball = nbal;
+            s_ccnt = ccnt;
+            s_cbelow = cbelow;
+            s_cmt = tm;
+            s_cmn = tn;
           }
           a_granules(c, bl, xa, xb, &s_ga[0], &s_ga[1]);
           a_granules(cc, cbl, ca, cb, &s_ga[2], &s_ga[3]);
@@ -2317,6 +2352,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       }
       if (lane == 0) {
         s_cand_ok = cand_ok;
+        if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_ga_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else if (more) {
@@ -2324,6 +2360,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // Only the chosen node changes; its owner redoes it below.
       phase1(pod + 1, bn, npar, &d);
       if (lv.stamps && w == 0 && t == 0) lv.stamps[(size_t)q * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+      if (lv.wstamps && t == 0) lv.wstamps[((size_t)q * G + w) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (!s_ok) return;
@@ -3128,6 +3165,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     PodStats* ps = b.stats + pod;
     const bool more = q + 1 < av.npods;
     const bool sp1 = more && spec(*reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3]));
+    // pod q+1's counts are defined as pod q's (host: DF_AGG_SAME): they are q's counts plus q's placement, so
+    // nothing is gathered for it -- the fold below runs on the counts in LDS, then its minima are recomputed
+    const bool same1 = sp1 && (reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3])->flags & DF_AGG_SAME) &&
+                       !(av.debug & 4);
     stamp(q, 0);
     wstamp(q, 0);
 
@@ -3533,7 +3574,18 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       // ======== waves 2..7: pod q+1's counts before pod q is placed (folded in below), its
       // DoNotSchedule minima, then the program of pod q+2 ========
       const int gt = t - 128, gn = kAggThreads - 128;
-      if (sp1) {
+      if (same1) {
+        if (wave == 2) {
+          if (lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          plan_fold(q, lane);
+          // the chosen node's value of every fold item's label (once wave 0 has resolved the node)
+          while (__hip_atomic_load(&s_bn_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+            __builtin_amdgcn_s_sleep(1);
+          const int nq = s_gnode;
+          const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+          for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
+        }
+      } else if (sp1) {
         aggregate(q + 1, gt, gn, grp_bar);
         if (wave == 2) {
           plan_fold(q, lane);
@@ -3605,6 +3657,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             }
             for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
             if (lane == 0) s_any |= any;
+          }
+          if (same1) {  // the minima over the folded counts (no gathered ones to adjust)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            minima_grp(q + 1, 0, 1);
           }
           if (lane == 0) {
             if (lq >= 0) append(q, lq);

@@ -1243,6 +1243,29 @@ int Engine::next_gran_tag(uint32_t* tag) {
   return KSG_OK;
 }
 
+// k_agg_loop: pod b's counts are defined exactly as pod a's (DF_AGG_SAME) -- the same program but for the fields
+// the aggregation does not read: the pod-table slot, the rotation and the pod's own affinity terms (the last
+// part of the program; the fold of a adds a's own terms to b's counts).  Pods stamped from one template, as
+// every scheduler_perf workload's are, qualify; anything else only loses the shortcut.
+static bool agg_same(const CompiledPod& a, const CompiledPod& b) {
+  if (a.error || b.error || a.blob.size() != b.blob.size() || a.blob.size() < sizeof(PodDesc)) return false;
+  PodDesc x, y;
+  std::memcpy(&x, a.blob.data(), sizeof(PodDesc));
+  std::memcpy(&y, b.blob.data(), sizeof(PodDesc));
+  if (!(x.flags & DF_AGGREGATE) || !(y.flags & DF_AGGREGATE) || x.own_terms_off != y.own_terms_off) return false;
+  for (PodDesc* z : {&x, &y}) {
+    z->slot = 0;
+    z->rot_start = 0;
+    z->prev_pod = 0;
+    z->n_own_terms = 0;
+    z->flags &= ~DF_AGG_SAME;
+  }
+  if (std::memcmp(&x, &y, sizeof(PodDesc)) != 0) return false;
+  const size_t end = x.own_terms_off > 0 ? std::min((size_t)x.own_terms_off, a.blob.size()) : a.blob.size();
+  return end <= sizeof(PodDesc) ||
+         std::memcmp(a.blob.data() + sizeof(PodDesc), b.blob.data() + sizeof(PodDesc), end - sizeof(PodDesc)) == 0;
+}
+
 int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                       ksg_result* results, ksg_eval_out* eval) {
   const int n = (int)pods.size();
@@ -1428,6 +1451,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         st.max_raw[q] = enc_i64(INT64_MIN);
         st.min_raw[q] = enc_i64(INT64_MAX);
       }
+      if (i > 0 && agg_same(cp[i - 1], cp[i])) reinterpret_cast<PodDesc*>(hdesc + o)->flags |= DF_AGG_SAME;
       if (rot_dev && !cp[i].error) {
         reinterpret_cast<PodDesc*>(hdesc + o)->prev_pod = last_launched;
         if (last_launched < 0) st.rot_in = (uint32_t)c->next_start;
@@ -2090,7 +2114,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
               (void)gl;
               cntq++;
             }
-          double own = 0, ownlate = 0, ownx = 0, seg[5] = {0};
+          double own = 0, ownlate = 0, ownx = 0, seg[5] = {0}, oth[4] = {0};
           int segn = 0;
           int on = 0;
           for (auto& r : sruns)
@@ -2101,11 +2125,25 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                 unsigned long long amin = ~0ull;
                 for (int h = 0; h < GS; ++h) amin = std::min(amin, ws[((size_t)(q + 1) * GS + h) * 8]);
                 const unsigned long long an = ws[((size_t)(q + 1) * GS + g) * 8];
-                const unsigned long long c4 = ws[((size_t)q * GS + g) * 8 + 4], c5 = ws[((size_t)q * GS + g) * 8 + 5];
-                const unsigned long long c6r = ws[((size_t)q * GS + g) * 8 + 6], c6 = c6r & ((1ull << 60) - 1);
-                if (c4 && c5 && c6) {
-                  seg[0] += (c4 - c0) / 100.0; seg[1] += (c5 - c4) / 100.0; seg[2] += (c6 - c5) / 100.0;
-                  seg[3] += (c1 - c6) / 100.0; seg[4] += (double)(c6r >> 60); segn++;
+                // against the earliest A(q+1) publish: the owner's pod start, its phase 1 (of q+1) end, its
+                // helper's granules ready, its B sweep done -- and the same for the other workgroups
+                const unsigned long long st = ws[((size_t)q * GS + g) * 8 + 7], p1 = ws[((size_t)q * GS + g) * 8 + 6];
+                const unsigned long long hr = ws[((size_t)q * GS + g) * 8 + 5], bs = ws[((size_t)q * GS + g) * 8 + 4];
+                if (st && p1 && hr && bs) {
+                  seg[0] += ((double)st - (double)amin) / 100.0; seg[1] += ((double)p1 - (double)amin) / 100.0;
+                  seg[2] += ((double)hr - (double)amin) / 100.0; seg[3] += ((double)bs - (double)amin) / 100.0;
+                  double o[4] = {0, 0, 0, 0};
+                  int on2 = 0;
+                  for (int h = 0; h < GS; ++h) {
+                    if (h == g) continue;
+                    const unsigned long long* x = &ws[((size_t)q * GS + h) * 8];
+                    if (!x[7] || !x[6] || !x[5] || !x[4]) continue;
+                    o[0] += ((double)x[7] - (double)amin) / 100.0; o[1] += ((double)x[6] - (double)amin) / 100.0;
+                    o[2] += ((double)x[5] - (double)amin) / 100.0; o[3] += ((double)x[4] - (double)amin) / 100.0;
+                    on2++;
+                  }
+                  if (on2) for (int k = 0; k < 4; ++k) oth[k] += o[k] / on2;
+                  segn++;
                 }
                 own += (c1 - c0) / 100.0;
                 ownx += ((double)an - (double)c1) / 100.0;
@@ -2113,8 +2151,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                 on++;
               }
           if (segn)
-            std::fprintf(stderr, "[k_sched_loop owner steps, us] commit %.3f lds %.3f eval/cand %.3f partials %.3f "
-                         "(cand used %.2f)\n", seg[0] / segn, seg[1] / segn, seg[2] / segn, seg[3] / segn, seg[4] / segn);
+            std::fprintf(stderr, "[k_sched_loop vs the earliest next-A publish, us] owner: pod start %.3f  phase-1 end %.3f  "
+                         "helper ready %.3f  B swept %.3f | others: %.3f %.3f %.3f %.3f\n", seg[0] / segn, seg[1] / segn,
+                         seg[2] / segn, seg[3] / segn, oth[0] / segn, oth[1] / segn, oth[2] / segn, oth[3] / segn);
           if (on)
             std::fprintf(stderr, "[k_sched_loop owner, us] commit+fixup %.3f  fixup end -> next A publish %.3f  "
                          "owner's next A lateness %.3f (%d pods)\n", own / on, ownx / on, ownlate / on, on);

@@ -825,3 +825,34 @@ def test_resident_loop_off_matches(native):
         rg, _ = g.schedule_one(g.compile(pod), assume=True)
         ro, _ = o.schedule_one(o.compile(pod), assume=True)
         assert rg.as_tuple() == ro.as_tuple(), f"pod {k}"
+
+
+@pytest.mark.parametrize("wg", [0, 7])
+def test_agg_loop_same_template_runs(native, wg):
+    """Runs of identical pods (one template: DF_AGG_SAME, no gather -- the previous pod's counts plus its
+    placement) broken by pods of other templates, on zoned nodes with bound pods: topology spreading
+    (DoNotSchedule zone minima recomputed after each fold), preferred / required anti-affinity, required
+    affinity, and unplaceable pods (the fold adds nothing).  Against the oracle and the loop with the
+    shortcut off (aggLoopDebug 4)."""
+    from ksg import synth
+    nodes, init, _ = synth.topology_spreading(900, 600, 0)
+    kinds = [synth.pod_with_topology_spreading, synth.pod_with_preferred_pod_anti_affinity,
+             synth.pod_with_required_anti_affinity, synth.pod_with_pod_affinity]
+    pods, k = [], 0
+    for run, kind in enumerate([0, 0, 1, 0, 2, 1, 1, 3, 0, 2, 0, 1]):
+        for _ in range([30, 1, 12, 45, 3, 20][run % 6]):
+            pods.append(kinds[kind](f"t{k}", "sched-1"))
+            k += 1
+    big = synth.pod_with_topology_spreading("huge", "sched-1")
+    big["spec"]["containers"][0]["resources"] = {"requests": {"cpu": "1000"}}
+    pods[40:40] = [big, dict(big, metadata=dict(big["metadata"], name="huge2", uid="huge2"))]
+    base = {"loopWorkgroups": wg} if wg else {}
+    g, o = _pair(native, base, nodes, init)
+    g2, _ = _pair(native, dict(base, aggLoopDebug=4), nodes, init)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
+    assert g.kernel_stats()[3] == "k_agg_loop"
+    for q, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[q].as_tuple() == ro.as_tuple() == rs2[q].as_tuple(), f"pod {q} ({p['metadata']['name']})"
+    assert g.compare_mirror(sync=False) == (0, -1)
