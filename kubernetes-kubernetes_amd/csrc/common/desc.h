@@ -116,6 +116,8 @@ struct IpaTerm {
   int32_t ns_off, ns_cnt;  // namespace ids (pod selector pool, int32 units)
   int32_t all_ns;       // namespaceSelector matches the empty label set
   int32_t lref;         // k_agg_loop: where hist_base's counts live (AggRef)
+  int32_t nvals;        // values of the topology key: the histogram's length
+  int32_t pad_;
 };
 struct KeyHist { int32_t slot; int32_t base; int32_t lref; int32_t pad; };
 // k_agg_loop's placement of one arena histogram ("AggRef"): >= 0, the histogram's first word in the
@@ -315,6 +317,8 @@ struct PreemptView {
                              // multiplicity and the next larger count (k_pts_minima)
   const int32_t* ex_contrib; // [slot][kPreemptCons]: the pod's required anti-affinity terms that match the
                              // preemptor, per existing-anti key (k_preempt_terms); nullptr: none
+  const long long* aff_tot;  // [kPreemptCons]: per required affinity term of a self-matching preemptor the
+                             // cycle's total count over its histogram (k_aff_totals); nullptr: not needed
   int32_t ipa_check, pad2;
 };
 constexpr int kPreemptCons = 4;  // DoNotSchedule constraints whose counts the victims may move (more: unsupported)

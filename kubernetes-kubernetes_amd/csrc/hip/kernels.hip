@@ -2248,7 +2248,9 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // wave publishes the right pair as soon as exchange B resolves.
       const bool stage = !RING && q + 2 < run_end;
       if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
+#ifndef KSG_STAGE_LATE
       if (stage) stage_prog(pod + 2, bs);  // s_blob[(q + 2) % 3] held pod q-1, free since the last barrier
+#endif
       while (__hip_atomic_load(&s_cand_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)  // posted every pod
         __builtin_amdgcn_s_sleep(1);
       const int cand = __hip_atomic_load(&s_cand_node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2355,12 +2357,16 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_ga_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+#ifdef KSG_STAGE_LATE
+      if (stage) stage_prog(pod + 2, bs);
+#endif
     } else if (more) {
       // ======== evaluation waves: phase 1 of pod q+1 against the cores before this pod's assume.
       // Only the chosen node changes; its owner redoes it below.
       phase1(pod + 1, bn, npar, &d);
       if (lv.stamps && w == 0 && t == 0) lv.stamps[(size_t)q * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-      if (lv.wstamps && t == 0) lv.wstamps[((size_t)q * G + w) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+      if (lv.wstamps && lane == 0)  // the last evaluation wave's phase-1 end
+        atomicMax(&lv.wstamps[((size_t)q * G + w) * 8 + 6], __builtin_amdgcn_s_memrealtime());
     }
     __syncthreads();
     if (!s_ok) return;
@@ -4083,6 +4089,11 @@ struct PreemptTopo {
   // i's own domain (its value of the term's key)
   int32_t ihb[3 * kPreemptCons], ivi[3 * kPreemptCons];
   int32_t idl[3 * kPreemptCons];
+  // a preemptor matching its own required affinity terms (filtering.go:404-415): whether affinityCounts is
+  // empty depends on every count, not only node i's -- the cycle's total per term (atot) with the victims'
+  // deltas at node i's domains; nra < 0: not tracked (the cycle's bit)
+  int64_t atot[kPreemptCons];
+  int32_t nra;
   __device__ __forceinline__ int64_t cnt(int32_t hist_base, int32_t lref, int32_t v, int ls) const {
     int64_t x = a.cnt(hist_base, lref, v, ls);
 #pragma unroll
@@ -4104,8 +4115,47 @@ struct PreemptTopo {
     return r;
   }
   __device__ __forceinline__ uint32_t pndom(int c) const { return a.pndom(c); }
-  __device__ __forceinline__ uint32_t any() const { return a.any(); }
+  __device__ __forceinline__ uint32_t any() const {
+    const uint32_t a0 = a.any();
+    if (nra < 0) return a0;
+    bool nonempty = false;  // affinityCounts after the removals / reprieves: some term's total is not 0
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k) {
+      if (k >= nra) continue;
+      int64_t x = atot[k];
+#pragma unroll
+      for (int j = 0; j < kPreemptCons; ++j)
+        if (j < nra && ihb[j] == ihb[k] && ivi[j] >= 0) x += idl[j];
+      nonempty |= x != 0;
+    }
+    return (a0 & ~1u) | (nonempty ? 1u : 0u);
+  }
 };
+
+// Per required affinity term of the preemptor (at most kPreemptCons): the cycle's total count over the term's
+// histogram (k_aggregate's arena) -- whether affinityCounts is empty once victims are removed (PreemptTopo::any).
+__global__ __launch_bounds__(kBlock) void k_aff_totals(BatchView b, int pod, long long* out) {
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  const int k = blockIdx.x;
+  if (k >= d.n_raff) return;
+  const IpaTerm t = at<IpaTerm>(base, d.raff_off)[k];
+  long long x = 0;
+  for (int v = threadIdx.x; v < t.nvals; v += kBlock) x += (long long)b.arena[t.hist_base + v];
+  __shared__ long long s[kBlock];
+  s[threadIdx.x] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long y = 0;
+    for (int q = 0; q < kBlock; ++q) y += s[q];
+    out[k] = y;
+  }
+}
+hipError_t launch_aff_totals(const BatchView& b, int pod, int nterms, long long* out, hipStream_t s) {
+  if (nterms <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_aff_totals, dim3(nterms), dim3(kBlock), 0, s, b, pod, out);
+  return hipGetLastError();
+}
 
 // Per DoNotSchedule constraint (one workgroup each): the minimum count over the present domains, how many
 // domains hold it, and the next larger count -- the minimum over "every domain but one holding the
@@ -4277,6 +4327,12 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
   const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
   const int nra = pv.ipa_check ? d.n_raff : 0, nrn = pv.ipa_check ? d.n_ranti : 0;
   const int nex = (pv.ipa_check && pv.ex_contrib) ? d.n_exkeys : 0;
+  tp.nra = -1;
+  if (pv.ipa_check && pv.aff_tot && (d.ipa_flags & IPA_SELF_ALL) && nra <= kPreemptCons) {
+    tp.nra = nra;
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k) tp.atot[k] = k < nra ? (int64_t)pv.aff_tot[k] : 0;
+  }
   if (pv.ipa_check) {
     if (nra > kPreemptCons || nrn > kPreemptCons || nex > kPreemptCons) o.flags |= 1u;  // beyond PreemptTopo
 #pragma unroll
@@ -4328,9 +4384,8 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
         }
       }
     }
-    // affinityCounts emptied by the removal could flip the "no pod matches anywhere" rule
-    // (filtering.go:404-415) for a preemptor matching its own terms: outside PreemptTopo
-    if (all && sg < 0 && (d.ipa_flags & IPA_SELF_ALL)) o.flags |= 1u;
+    // (a preemptor matching its own terms: affinityCounts emptied by the removal flips the "no pod matches
+    // anywhere" rule, filtering.go:404-415 -- PreemptTopo::any from the totals and these deltas)
     return moved;
   };
   auto counts = [&](int q) -> uint32_t {  // the constraints whose count victim q is part of

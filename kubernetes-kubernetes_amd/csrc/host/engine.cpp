@@ -762,6 +762,7 @@ int Engine::compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N,
       auto b = bases->find(key);
       if (b == bases->end()) b = bases->emplace(key, alloc(nvals(key), key, false)).first;
       it.hist_base = b->second;
+      it.nvals = nvals(key);
       (void)pref;
       o->push_back(it);
     }

@@ -32,6 +32,7 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
                           uint8_t* vout, POut* out, int all_nodes, hipStream_t s);
 hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s);
 hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* mm, hipStream_t s);
+hipError_t launch_aff_totals(const BatchView& b, int pod, int nterms, long long* out, hipStream_t s);
 hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, uint32_t* unsup,
                                 hipStream_t s);
 hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_t pct, int64_t absn, int32_t* pot,
@@ -382,12 +383,15 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
           if (pdbs[k].disrupted.count(kv.second.name)) dis[kv.second.slot] |= (uint8_t)(1u << k);
     }
     if ((rc = stage_pod())) return rc;
-    const size_t mm_b = 8 * 3 * kPreemptCons;
+    const size_t mm_b = 8 * 4 * kPreemptCons;  // k_pts_minima's [3 kPreemptCons], then k_aff_totals' [kPreemptCons]
     const size_t pd_b = sizeof(PdbDev) * pd.size(), pool_b = 4 * pool.size(), dis_b = dis.size();
     if ((rc = ensure(d_pdb, mm_b + pd_b + pool_b + dis_b + 64))) return rc;
     long long* d_mm = (long long*)d_pdb.p;  // k_pts_minima's output, then the budgets
     const bool pts_minima = pts_on && D.n_ptsf <= kPreemptCons;
     if (pts_minima) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
+    // a preemptor matching its own required affinity terms: the cycle's per-term totals (PreemptTopo::any)
+    const bool aff_tot = ipa_on && (D.ipa_flags & IPA_SELF_ALL) && D.n_raff > 0 && D.n_raff <= kPreemptCons;
+    if (aff_tot) PCHK(launch_aff_totals(bv, 0, D.n_raff, d_mm + 3 * kPreemptCons, s));
     // existing pods' required anti-affinity terms matching the preemptor, per slot and key
     int32_t* d_contrib = nullptr;
     uint32_t* d_tunsup = nullptr;
@@ -421,6 +425,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     v.now = now;
     v.pts_mm = d_mm;
     v.ex_contrib = d_contrib;
+    v.aff_tot = aff_tot ? d_mm + 3 * kPreemptCons : nullptr;
     v.ipa_check = ipa_on ? 1 : 0;
     PCHK(launch_preempt_seg(m, bv, 0, v, s));
     if ((rc = ensure(d_pick, sizeof(PickOut) + 4 * (size_t)N + 64))) return rc;

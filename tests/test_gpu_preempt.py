@@ -253,8 +253,8 @@ def affinity_cluster(seed, n_nodes):
 @pytest.mark.parametrize("seed", range(4))
 def test_preempt_affinity_victims_match_oracle(native, seed):
     """Victims that move the preemptor's InterPodAffinity counts: the device-resident path (PreemptTopo's
-    InterPodAffinity deltas, k_preempt_terms) against the oracle's literal RemovePod / AddPod; an
-    unsupported case (a self-matching preemptor whose affinity counts a victim empties) is declined."""
+    InterPodAffinity deltas, k_preempt_terms, the affinity totals of a self-matching preemptor) against the
+    oracle's literal RemovePod / AddPod."""
     from ksg.abi import KsgError
     rng, nodes, existing = affinity_cluster(200 + seed, 40 + 30 * seed)
     dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
@@ -277,10 +277,42 @@ def test_preempt_affinity_victims_match_oracle(native, seed):
         try:
             r1, d1 = dev.preempt(dev.compile(pod), args)
         except KsgError as e:
-            assert "rc=-5" in str(e) and kind == "affinity", e
-            declined += 1
-            continue
+            raise AssertionError(f"declined ({kind}): {e}")
         assert r1.as_tuple() == r2.as_tuple(), (kind, r1.as_tuple(), r2.as_tuple(), d1, d2)
         assert d1 == d2, kind
         found += r1.status == 0
-    assert found > 0 and declined < 6
+    assert found > 0 and declined == 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_preempt_self_affinity_victims_match_oracle(native, seed):
+    """A preemptor that matches its own required affinity terms (filtering.go:404-415): removing victims
+    that are the only pods its terms count empties affinityCounts, and the "first pod of a series" rule
+    then admits the node.  The matching pods sit on few nodes; the device's per-term totals plus the
+    victims' deltas against the oracle's literal RemovePod / AddPod."""
+    rng, nodes, existing = affinity_cluster(300 + seed, 30 + 20 * seed)
+    # "rare": the pods of one or two nodes only -- removing them as victims can empty affinityCounts
+    hosts = rng.sample(sorted({p["spec"]["nodeName"] for p in existing}), 2)
+    for p in existing:
+        if p["spec"]["nodeName"] == hosts[0] or (p["spec"]["nodeName"] == hosts[1] and rng.random() < 0.3):
+            p["metadata"]["labels"] = {"app": "rare"}
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    found = 0
+    for q in range(12):
+        # "solo": no existing pod matches (the map is empty from the start)
+        app = rng.choice(["rare", "rare", "rare", "a", "solo"])
+        pod = mk_pod(f"self{q}", rng, prio=1000, big=True)
+        pod["metadata"]["namespace"] = "default"
+        pod["metadata"]["labels"] = {"app": app}
+        pod["spec"]["containers"][0]["resources"]["requests"].pop("example.com/gpu", None)
+        pod["spec"]["affinity"] = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": {"matchLabels": {"app": app}},
+             "topologyKey": rng.choice(["kubernetes.io/hostname", "topology.kubernetes.io/zone"])}]}}
+        args = {"offset": rng.randrange(1000), "allNodes": rng.random() < 0.5, "listCandidates": True,
+                "now": 1704153600 * 10 ** 9, "minCandidateNodesPercentage": 100, "minCandidateNodesAbsolute": 100}
+        r2, d2 = orc.preempt(orc.compile(pod), args)
+        r1, d1 = dev.preempt(dev.compile(pod), args)
+        assert r1.as_tuple() == r2.as_tuple(), (app, r1.as_tuple(), r2.as_tuple(), d1, d2)
+        assert d1 == d2, app
+        found += r1.status == 0
+    assert found > 0
