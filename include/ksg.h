@@ -218,13 +218,13 @@ int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uin
  * Parallelizer parallelism 1 semantics; victims of equal priority and start time keep NodeInfo.Pods
  * order; candidates tied on every criterion resolve to the earliest in candidate-list order.
  * The device re-evaluates a victim's removal for NodeResourcesFit, NodePorts and the pod's
- * PodTopologySpread / InterPodAffinity counts (RemovePod / AddPod extensions) for up to 4 spread
+ * PodTopologySpread / InterPodAffinity counts (RemovePod / AddPod extensions) for up to 8 spread
  * constraints, affinity terms and topology keys.  KSG_ENOTSUP (nothing selected; ctx->err says
  * which): a preemptor with more than 4 scalar resources; a victim whose effect on those counts is
- * beyond that (more constraints / terms / keys, an emptied required-affinity count); and, on the
- * host-staged record path (victims ordered by the call's clock -- pods without status.startTime --
- * or scalar-grouped pods), any victim that changes the pod's DoNotSchedule spread counts or shares
- * required affinity terms with it.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
+ * beyond that (more constraints / terms / keys); and, on the host-staged record path (a call whose
+ * "now" precedes a bound pod's start time while pods without status.startTime exist, scalar-grouped
+ * preemptors, more than 8 budgets, nodes of more than 128 pods), any victim that changes the pod's
+ * DoNotSchedule spread counts or shares required affinity terms with it.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
  * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}] (listCandidates),
  * "selected": <node|null>, "victims": [uid...]}; *detail_len gets its length (KSG_ENOMEM if cap is
  * too small; the result is still filled). */

@@ -321,7 +321,7 @@ struct PreemptView {
                              // cycle's total count over its histogram (k_aff_totals); nullptr: not needed
   int32_t ipa_check, pad2;
 };
-constexpr int kPreemptCons = 4;  // DoNotSchedule constraints whose counts the victims may move (more: unsupported)
+constexpr int kPreemptCons = 8;  // DoNotSchedule constraints / affinity terms / keys whose counts the victims may move (more: unsupported)
 
 // Per-pod device result (ScheduleResult + diagnostics), written by the select kernel.
 struct DevResult {

@@ -439,7 +439,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     if ((rc = finish_device())) return rc;
     if (pick.unsupported) {
       c->err = "preemption: a victim's effect on the pod's PodTopologySpread / InterPodAffinity counts is outside "
-               "what the device tracks (more than 4 constraints, terms or keys, or an emptied affinity count)";
+               "what the device tracks (more than 8 constraints, terms or keys)";
       return KSG_ENOTSUP;
     }
     for (int32_t i = 0; list && i < N; ++i) po[i] = NodeOut{so[i].st, so[i].nvictims, so[i].nviolating};
