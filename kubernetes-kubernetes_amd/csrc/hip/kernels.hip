@@ -1646,8 +1646,11 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
 __device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
   if (q >= lv.npods) return -1;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  // relaxed polls: the ring is coherent host memory, and a system-scope acquire on every poll would
+  // invalidate the caches under the other workgroups' work; the program is read after the doorbell's value
+  // is known (control dependence), with system-scope loads that bypass the device caches (stage_ring)
   for (uint32_t spins = 0;; ++spins) {
-    const unsigned long long v = __hip_atomic_load(&lv.ring->ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long v = __hip_atomic_load(&lv.ring->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t posted = (uint32_t)v;
     if (posted == kRingStop) return -1;
     if (posted > (uint32_t)q) return (int)(v >> 32);
@@ -1659,10 +1662,19 @@ __device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
   }
 }
 // Resident mode: pod q's result to the host (the committing thread, after commit_result)
+// The record goes to host memory with system-scope (write-through) stores; once they have completed
+// (vmcnt), the sequence word follows in the same PCIe posted-write stream.  (A system-scope release here
+// would write the whole L2 back first.)
 __device__ __forceinline__ void ring_post(const LoopView& lv, int q, const DevResult& r) {
   RingResult& o = lv.ring->res[q % kRingSlots];
-  o.r = r;
-  __hip_atomic_store(&o.seq, (uint32_t)(q + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  static_assert(sizeof(DevResult) % 8 == 0, "DevResult is stored as 8-byte words");
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&r);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(&o.r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(DevResult) / 8); ++k)
+    __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&o.seq, (uint32_t)(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // NormalizeScore + weights for the loop's plugin set (TaintToleration, NodeAffinity normalised;
@@ -1847,10 +1859,13 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     for (uint32_t o = (uint32_t)lane; o < n16; o += 64u) dst[o] = src[o];
   };
   // resident mode: pod q's program from the ring (host memory: one round trip, every thread's 16 B)
+  // (system-scope loads: they bypass the device caches, so a ring slot reused kRingSlots pods later is
+  // never read stale -- the doorbell poll is relaxed, no acquire invalidates the caches)
   auto stage_ring = [&](int q, int bytes) __attribute__((always_inline)) {
-    const uint4* src = reinterpret_cast<const uint4*>(lv.ring->blob[q % kRingSlots]);
-    uint4* dst = reinterpret_cast<uint4*>(s_blob[q % 3]);
-    for (uint32_t o = threadIdx.x; o < (uint32_t)bytes / 16u; o += (uint32_t)kLoopThreads) dst[o] = src[o];
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(lv.ring->blob[q % kRingSlots]);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(s_blob[q % 3]);
+    for (uint32_t o = threadIdx.x; o < (uint32_t)bytes / 8u; o += (uint32_t)kLoopThreads)
+      dst[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   };
 
   // ---- evaluation-wave state of the pod being prepared: per-thread maxima of the normalising raw
