@@ -2263,9 +2263,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // wave publishes the right pair as soon as exchange B resolves.
       const bool stage = !RING && q + 2 < run_end;
       if (lane == 0) s_ipa = (int)b.stats[pod].ipa_any;  // for the result record (off the critical path)
-#ifndef KSG_STAGE_LATE
       if (stage) stage_prog(pod + 2, bs);  // s_blob[(q + 2) % 3] held pod q-1, free since the last barrier
-#endif
       while (__hip_atomic_load(&s_cand_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)  // posted every pod
         __builtin_amdgcn_s_sleep(1);
       const int cand = __hip_atomic_load(&s_cand_node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2372,9 +2370,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_ga_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-#ifdef KSG_STAGE_LATE
-      if (stage) stage_prog(pod + 2, bs);
-#endif
+
     } else if (more) {
       // ======== evaluation waves: phase 1 of pod q+1 against the cores before this pod's assume.
       // Only the chosen node changes; its owner redoes it below.
