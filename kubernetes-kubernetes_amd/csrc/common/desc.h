@@ -573,7 +573,7 @@ struct AggView {
   unsigned long long* stamps; // diagnostic: [npods][kAggStamps] (nullptr)
   unsigned long long* wstamps;  // diagnostic: [npods][nwg][4] phase-1 start, A publish, B publish, commit end
   int32_t give_up_at;         // diagnostic: every workgroup gives up at this pod of the run (-1: never)
-  int32_t pad_;
+  int32_t ptss;               // some pod of the run has PodTopologySpread scoring (the k_agg_loop<., true> instance)
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

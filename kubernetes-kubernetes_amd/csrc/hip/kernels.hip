@@ -2633,8 +2633,10 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
   }
 }
 
-// SHARD: node-sharded over the device exchange (av.world > 1); the unsharded instance compiles none of it
-template <bool SHARD>
+// SHARD: node-sharded over the device exchange (av.world > 1); the unsharded instance compiles none of it.
+// PTSS: some pod of the run has PodTopologySpread scoring (ScheduleAnyway constraints); the instance
+// without it leaves that code out (its registers and issue slots cost the other pods ~1 us).
+template <bool SHARD, bool PTSS>
 __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
@@ -2743,7 +2745,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           if (((el >> c) & 1u) && cf[c].lref >= 0) s_gh[cf[c].pref + node_label(m, cf[c].slot, i)] = 1ull;
       }
       // processAllNode's node test for the ScheduleAnyway counts (scoring.go:164-181)
-      if (ls < nk * kBlock && i < m.n && d.n_ptss)
+      if (PTSS && ls < nk * kBlock && i < m.n && d.n_ptss)
         el |= pts_eligible(m, base, d, cs, d.n_ptss, i, (d.flags & DF_PTS_ANYTOPO) == 0) << 8;
       s_elig[ls] = (uint16_t)el;
     }
@@ -2770,7 +2772,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             if (((el >> c) & 1u) && !lsel_empty(sp + cf[c].sel) && lsel_match(sp + cf[c].sel, pl, pn))
               add(cf[c].lref, node_label(m, cf[c].slot, n), ls, 1);
         }
-        if (!term && pns == d.ns_id && d.n_ptss) {  // PreScore counts (scoring.go:155-189), hostname per node (:207-214)
+        if (PTSS && !term && pns == d.ns_id && d.n_ptss) {  // PreScore counts (scoring.go:155-189), hostname per node (:207-214)
           const uint32_t el = s_elig[ls] >> 8;
           for (int32_t c = 0; c < d.n_ptss; ++c) {
             if (lsel_empty(sp + cs[c].sel) || !lsel_match(sp + cs[c].sel, pl, pn)) continue;
@@ -3042,7 +3044,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       const IpaTerm* ts = at<IpaTerm>(base, aff ? d.paff_off : d.panti_off);
       if ((d.ipa_flags & IPA_PREF) && k2 < (aff ? d.n_paff : d.n_panti) && term_matches_pod(sp, ts[k2], pns, pl, pn))
         push(ts[k2].lref, ts[k2].slot, -1, aff ? ts[k2].weight : -ts[k2].weight, 8u);
-    } else if (gl >= 25 && gl < 25 + kAggScoreCons) {  // ScheduleAnyway constraint gl - 25 of pod q+1
+    } else if (PTSS && gl >= 25 && gl < 25 + kAggScoreCons) {  // ScheduleAnyway constraint gl - 25 of pod q+1
       const int c = gl - 25;
       const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
       if (c < d.n_ptss && !term && pns == d.ns_id && !lsel_empty(sp + cs[c].sel) && lsel_match(sp + cs[c].sel, pl, pn)) {
@@ -3208,7 +3210,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       // non-ignored nodes as presence bits
       unsigned long long pb0 = 0, pb1 = 0;
       bool pts_on = false;
-      if ((d.score_mask >> P_PTS) & 1u) {
+      if (PTSS && ((d.score_mask >> P_PTS) & 1u)) {
         const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
         const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
         bool ign = false;
@@ -3294,7 +3296,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           agran_put<SHARD>(av, q, gid, AG_A1, g1);
           agran_put<SHARD>(av, q, gid, AG_A2, bi);
           agran_put<SHARD>(av, q, gid, AG_A3, bn);
-          if ((d.score_mask >> P_PTS) & 1u) {  // PodTopologySpread: domain presence, non-ignored count
+          if (PTSS && ((d.score_mask >> P_PTS) & 1u)) {  // PodTopologySpread: domain presence, non-ignored count
             uint32_t ni = 0;
             unsigned long long p0 = 0, p1 = 0;
             for (int v = 0; v < kAggThreads / 64; ++v) {
@@ -3308,7 +3310,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           }
           wstamp(q, 1);
         }
-        const bool pts_q = ((d.score_mask >> P_PTS) & 1u) != 0;
+        const bool pts_q = PTSS && ((d.score_mask >> P_PTS) & 1u) != 0;
         unsigned long long xa[6][kMaxSweep];
         const bool ok = agran_sweep<SHARD, 6>(av, q, AG_A0, xa, pts_q ? 6 : 4);
         uint32_t F = 0, wp = 0, bf = 0;
@@ -3379,7 +3381,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           __builtin_amdgcn_s_sleep(1);
       }
       constexpr int kH = kAggThreads / 128;
-      if (((d.score_mask >> P_PTS) & 1u) && s_ok) {
+      if (PTSS && ((d.score_mask >> P_PTS) & 1u) && s_ok) {
         // ---- PodTopologySpread.Score of my half's feasible nodes with the global topology sizes
         // (scoring.go:199-226; k_pts_score's arithmetic), into s_pc[0]; NormalizeScore's max / min over
         // every workgroup's scored nodes by exchange PX (scoring.go:229-268)
@@ -3468,7 +3470,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         SlotVal sv[kH];
         int64_t ri[kH];
         uint32_t rp[kH];
-        const bool ipa = ((d.score_mask >> P_IPA) & 1u) != 0, pts = ((d.score_mask >> P_PTS) & 1u) != 0;
+        const bool ipa = ((d.score_mask >> P_IPA) & 1u) != 0, pts = PTSS && ((d.score_mask >> P_PTS) & 1u) != 0;
         const int64_t pmx = s_pts_mx, pmn = s_pts_mn;
 #pragma unroll
         for (int vv = 0; vv < kH; ++vv) {
@@ -3909,16 +3911,17 @@ hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const Loop
 }
 hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
                            hipEvent_t t1) {
+  auto go = [&](auto kern) {
+    if (t0)
+      hipExtLaunchKernelGGL(kern, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
+    else
+      hipLaunchKernelGGL(kern, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
+  };
   if (av.world > 1) {
-    if (t0)
-      hipExtLaunchKernelGGL(k_agg_loop<true>, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
-    else
-      hipLaunchKernelGGL(k_agg_loop<true>, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
+    go(k_agg_loop<true, true>);  // (the sharded instance without PTSS spills registers: not built)
   } else {
-    if (t0)
-      hipExtLaunchKernelGGL(k_agg_loop<false>, dim3(av.nwg), dim3(kAggThreads), 0, s, t0, t1, 0, m, b, av);
-    else
-      hipLaunchKernelGGL(k_agg_loop<false>, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
+    if (av.ptss) go(k_agg_loop<false, true>);
+    else go(k_agg_loop<false, false>);
   }
   return hipGetLastError();
 }
@@ -3935,8 +3938,9 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_sched_loop<4, true>), reinterpret_cast<const void*>(&k_sched_loop<2, true>),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_sample_shard_a),
                       reinterpret_cast<const void*>(&k_sample_shard_b),        reinterpret_cast<const void*>(&k_node_update),
-                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop<false>),
-                      reinterpret_cast<const void*>(&k_agg_loop<true>),
+                      reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop<false, false>),
+                      reinterpret_cast<const void*>(&k_agg_loop<false, true>),
+                      reinterpret_cast<const void*>(&k_agg_loop<true, true>),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);

@@ -1777,8 +1777,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       double rb = 0;
       int32_t gw = 1;
       const int cut = chunk_end(i);
+      bool ptss = false;
       while (j < n && j < cut && j - i < kLoopMaxPods && agg_loop_ok(cp[j]) && !loop_ok(cp[j])) {
         const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[j].blob.data());
+        ptss = ptss || ((hd.score_mask >> P_PTS) & 1u) || hd.n_ptss > 0;
         rb += algo_bytes(hd) + agg_bytes(hd);
         gw = std::max(gw, hd.agg_gwords);
         ++j;
@@ -1804,6 +1806,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       }
       if ((rc = next_gran_tag(&av.tag))) return rc;
       av.gwords = gw;
+      av.ptss = ptss ? 1 : 0;
       av.debug = c->cfg.agg_debug;
       av.give_up_at = c->cfg.debug_give_up_at;
       av.gran = (unsigned long long*)d_agran.p;

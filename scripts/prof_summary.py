@@ -69,7 +69,7 @@ def main():
         wa = sum(w) / len(w) if w else 0.0
         pl.append(f"{k:60s} dispatches {len(f):6d} FETCH_KiB {fa:10.2f} (x2 {2 * fa:10.2f}) WRITE_KiB {wa:10.2f}")
         for kn, per_unit in (("k_filter_score", 1), ("k_sched_loop", loop_pods), ("k_agg_loop", loop_pods)):
-            if k.endswith(kn):
+            if k.split("<")[0].endswith(kn):  # (templated kernels: k_sched_loop<2, false>)
                 traffic[kn] = {"kernel": kn, "nodes": nodes, "workload": workload, "fetch_kib_raw": fa / per_unit,
                                "write_kib": wa / per_unit,
                                "bytes_per_launch": round((fa + wa) * 1024.0 / per_unit, 1),
