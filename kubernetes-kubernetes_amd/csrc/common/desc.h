@@ -171,6 +171,9 @@ enum DescFlags : uint32_t {
   DF_AGG_SAME = 1u << 21,          // k_agg_loop: this pod's counts are defined exactly as the previous pod's of the
                                    // batch (same program but for slot / rotation / own terms): its counts are that
                                    // pod's plus its placement (fold), no gather (set by the host at staging)
+  DF_RAW0 = 1u << 22,              // every node's raw TaintToleration and NodeAffinity scores are 0 (no intolerable
+                                   // PreferNoSchedule taint exists, no preferred terms): k_sched_loop's helper forms
+                                   // the chosen variant's maxima from the counts alone
 };
 
 struct PodDesc {
@@ -530,6 +533,7 @@ constexpr int kAggGWords = 1024;   // compact shared-region words per pod (stage
 constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local histograms per pod
 constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
 constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
+constexpr int kAggSpillMax = 1 << 20;  // pod / term list entries past those per workgroup (HBM spill rows)
 constexpr int kAGran = 12;         // granules per participant per pod
 constexpr int kAggStartRow = 1024; // k_agg_loop (node-sharded): the start barrier's granule row (= kLoopMaxPods)
 enum AggGran : int {
@@ -574,6 +578,10 @@ struct AggView {
   unsigned long long* wstamps;  // diagnostic: [npods][nwg][4] phase-1 start, A publish, B publish, commit end
   int32_t give_up_at;         // diagnostic: every workgroup gives up at this pod of the run (-1: never)
   int32_t ptss;               // some pod of the run has PodTopologySpread scoring (the k_agg_loop<., true> instance)
+  // a workgroup's pod / term lists past kAggPods / kAggTerms entries (nodes that gathered many pods):
+  // [nwg][spill_pods + spill_terms] in HBM, this rank's workgroups
+  uint32_t* spill;
+  int32_t spill_pods, spill_terms;
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -2290,7 +2290,31 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         int cw = -1;
         unsigned long long tm = 0, tn = 0, nbal = 0;
         uint32_t ccnt = 0, cbelow = 0;
-        if (cand_ok) {  // the candidate's evaluation wave, as its partials will be if it wins
+        if (cand_ok && (nd.flags & DF_RAW0)) {
+          // every raw TaintToleration / NodeAffinity score is 0: a wave's maxima are enc(0) when it has a
+          // feasible node, else 0 -- the chosen variant needs only the candidate's feasibility bit
+          const int kw = cand / U - k0, sl = cand % U, cl = sl & 63;
+          cw = sl >> 6;
+          const unsigned long long b2 = s_ball2[kw][cw];
+          unsigned long long old = 0;
+#pragma unroll
+          for (int kk = 0; kk < kLoopMaxBlk; ++kk)
+            if (kk < nk && kk == kw) old = s_ball[npar][kk][cw];
+          const bool cf = ((b2 >> cl) & 1ull) != 0;
+          const unsigned long long bit = 1ull << cl;
+          nbal = cf ? (old | bit) : (old & ~bit);
+          const int lim = nd.rot_start - ((k0 + kw) * U + cw * 64);
+          const unsigned long long bmk = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+          uint32_t ucw0 = 0, ucw1 = 0;
+#pragma unroll
+          for (int v = 0; v < NW; ++v) {
+            ucw0 = v == cw ? u0[v] : ucw0;
+            ucw1 = v == cw ? u1[v] : ucw1;
+          }
+          ccnt = ucw0 - (uint32_t)__popcll(old) + (uint32_t)__popcll(nbal);
+          cbelow = ucw1 - (uint32_t)__popcll(old & bmk) + (uint32_t)__popcll(nbal & bmk);
+          tm = tn = ccnt > 0 ? enc_i64(0) : 0ull;
+        } else if (cand_ok) {  // the candidate's evaluation wave, as its partials will be if it wins
           const int kw = cand / U - k0, sl = cand % U, cl = sl & 63;
           cw = sl >> 6;
           const unsigned long long b2 = s_ball2[kw][cw];
@@ -2691,6 +2715,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int nlo = k0 * kBlock, nhi = k1 * kBlock < m.n ? k1 * kBlock : m.n;
+  // my pod / term lists: the first kAggPods / kAggTerms entries in LDS, the rest in my HBM spill rows
+  uint32_t* const spl = av.spill + (size_t)w * (size_t)(av.spill_pods + av.spill_terms);
+  const uint32_t pcap = (uint32_t)kAggPods + (uint32_t)av.spill_pods, tcap = (uint32_t)kAggTerms + (uint32_t)av.spill_terms;
+  auto put_pod = [&](uint32_t k, uint32_t e) __attribute__((always_inline)) {
+    if (k < (uint32_t)kAggPods) s_pods[k] = e;
+    else spl[k - (uint32_t)kAggPods] = e;
+  };
+  auto put_term = [&](uint32_t k, uint32_t e) __attribute__((always_inline)) {
+    if (k < (uint32_t)kAggTerms) s_terms[k] = e;
+    else spl[(uint32_t)av.spill_pods + k - (uint32_t)kAggTerms] = e;
+  };
   const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
   const int kk = t / kBlock, tt = t % kBlock;  // my node slot t = kk * kBlock + tt
   const int my_i = (k0 + kk) * kBlock + tt;
@@ -2760,7 +2795,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     for (uint32_t k = (uint32_t)tid; k < nitems; k += (uint32_t)nthr) {
       if (k < np) {
         // pod role: the pod's selectors against one pod on my nodes (k_aggregate's pod role)
-        const uint32_t e = s_pods[k];
+        const uint32_t e = k < (uint32_t)kAggPods ? s_pods[k] : spl[k - (uint32_t)kAggPods];
         const int s = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
         const int32_t pns = m.pod_ns[s];
         const bool term = (m.pod_flags[s] & 1u) != 0;
@@ -2826,7 +2861,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         }
       } else {
         // term role: one existing affinity term of a pod on my nodes against the incoming pod
-        const uint32_t e = s_terms[k - np];
+        const uint32_t kt2 = k - np;
+        const uint32_t e = kt2 < (uint32_t)kAggTerms ? s_terms[kt2] : spl[(uint32_t)av.spill_pods + kt2 - (uint32_t)kAggTerms];
         const int j = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
         const DTerm tm = m.terms[j];
         if (tm.key >= d.n_keytab) continue;
@@ -3081,14 +3117,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     const uint8_t* bp = s_blob[q % 3];
     const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
     const uint32_t np = s_np, nt = s_nt;
-    if (np < (uint32_t)kAggPods) s_pods[np] = ((uint32_t)dp.slot << 9) | (uint32_t)lq;
+    put_pod(np, ((uint32_t)dp.slot << 9) | (uint32_t)lq);
     const int32_t* own = at<int32_t>(bp, dp.own_terms_off);
     uint32_t k2 = 0;
-    for (; k2 < (uint32_t)dp.n_own_terms && nt + k2 < (uint32_t)kAggTerms; ++k2)
-      s_terms[nt + k2] = ((uint32_t)own[k2] << 9) | (uint32_t)lq;
+    for (; k2 < (uint32_t)dp.n_own_terms && nt + k2 < tcap; ++k2) put_term(nt + k2, ((uint32_t)own[k2] << 9) | (uint32_t)lq);
     s_np = np + 1;
     s_nt = nt + k2;
-    if (np >= (uint32_t)kAggPods || k2 < (uint32_t)dp.n_own_terms) fail(0xfffffffdu);  // host-checked
+    if (np >= pcap || k2 < (uint32_t)dp.n_own_terms) fail(0xfffffffdu);  // host-checked
   };
   auto wg_bar = [&]() __attribute__((always_inline)) { __syncthreads(); };
 
@@ -3126,7 +3161,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     const int n = m.pod_node[s];
     if (n >= nlo && n < nhi) {
       const uint32_t k = atomicAdd(&s_np, 1u);
-      if (k < (uint32_t)kAggPods) s_pods[k] = ((uint32_t)s << 9) | (uint32_t)(n - nlo);
+      if (k < pcap) put_pod(k, ((uint32_t)s << 9) | (uint32_t)(n - nlo));
     }
   }
   for (int j = t; j < m.n_terms; j += kAggThreads) {
@@ -3134,13 +3169,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     const int n = tm.kind >= 0 ? m.pod_node[tm.owner] : -1;
     if (n >= nlo && n < nhi) {
       const uint32_t k = atomicAdd(&s_nt, 1u);
-      if (k < (uint32_t)kAggTerms) s_terms[k] = ((uint32_t)j << 9) | (uint32_t)(n - nlo);
+      if (k < tcap) put_term(k, ((uint32_t)j << 9) | (uint32_t)(n - nlo));
     }
   }
   if (av.npods > 0) stage_prog(0, t, kAggThreads);
   if (av.npods > 1) stage_prog(1, t, kAggThreads);
   __syncthreads();
-  if (s_np > (uint32_t)kAggPods || s_nt > (uint32_t)kAggTerms) {  // host-checked; never taken
+  if (s_np > pcap || s_nt > tcap) {  // host-checked; never taken
     if (t == 0) fail(0xfffffffeu);
     return;
   }

@@ -299,6 +299,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   }
 
   // TaintToleration: per distinct taint, "not tolerated" bits (taint_toleration.go:102-196)
+  bool any_intol = false;  // some PreferNoSchedule taint of the cluster is not tolerated (raw scores can be > 0)
   {
     const size_t T = c->taints.size();
     const int32_t words = (int32_t)((T + 31) / 32);
@@ -321,6 +322,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     D.n_taint_words = words;
     D.untol_ns_off = B.put(untol);
     D.intol_pns_off = B.put(intol);
+    for (uint32_t x : intol) any_intol = any_intol || x != 0;
     for (auto& t : p.tolerations)  // NodeUnschedulable (node_unschedulable.go:133-138)
       if (tolerates(t, "node.kubernetes.io/unschedulable", "", "NoSchedule", cfg.taint_cmp_ops)) D.flags |= DF_TOLERATES_UNSCHED;
   }
@@ -560,6 +562,10 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   D.filter_mask = fmask;
   D.score_mask = smask;
   out->score_mask = smask;
+  // raw TaintToleration / NodeAffinity scores are 0 on every node: nothing intolerable to count, no terms to weigh
+  if ((!((smask >> P_TAINT) & 1u) || !any_intol) &&
+      (!((smask >> P_NA) & 1u) || (D.na_preferred.nterm == 0 && D.na_added_pref.nterm == 0)))
+    D.flags |= DF_RAW0;
   if (assume) {
     D.flags |= DF_ASSUME;
     // live once k_select's assume writes its node index; a pipelined batch reserved it up front
@@ -1070,7 +1076,7 @@ Engine::~Engine() {
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
   if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps,
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill,
                     &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
@@ -1533,6 +1539,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   bool use_agg = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 &&
                  G * W <= std::min(cus, 256) && (int64_t)G * kLoopMaxBlk >= NBs &&
                  (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
+  int64_t spill_p = 0, spill_t = 0;  // k_agg_loop: HBM list entries per workgroup (AggView::spill)
   if (use_agg) {
     bool any = false;
     int64_t own = 0;
@@ -1556,8 +1563,12 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         const int32_t nd = tm.kind >= 0 && tm.owner >= 0 ? c->pt_node[(size_t)tm.owner] : -1;
         if (nd >= 0 && nd < m.n) nt[(size_t)wg_of[(size_t)(nd / kBlock)]]++;
       }
-      use_agg = *std::max_element(np.begin(), np.end()) + (int64_t)n <= kAggPods &&
-                *std::max_element(nt.begin(), nt.end()) + own <= kAggTerms;
+      // entries past the LDS lists go to the workgroup's HBM spill rows (nodes that gathered many pods,
+      // e.g. required pod affinity piling pods onto the nodes of the pods they follow)
+      auto up64 = [](int64_t v) { return v <= 0 ? (int64_t)0 : (v + 63) / 64 * 64; };
+      spill_p = up64(*std::max_element(np.begin(), np.end()) + (int64_t)n - kAggPods);
+      spill_t = up64(*std::max_element(nt.begin(), nt.end()) + own - kAggTerms);
+      use_agg = spill_p <= kAggSpillMax && spill_t <= kAggSpillMax;
     }
   }
   struct LoopRun { int first, count; double bytes; bool agg, timed; };
@@ -1567,6 +1578,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // loopTimingStride k: every k-th loop launch carries HIP events on its dispatch packet (0: none)
   auto loop_timed = [&](size_t r) { return c->cfg.loop_timing_stride > 0 && r % (size_t)c->cfg.loop_timing_stride == 0; };
   if (use_agg && (rc = agg_setup())) return rc;
+  if (use_agg && (rc = ensure(d_aspill, (size_t)G * (size_t)(spill_p + spill_t) * 4 + 4))) return rc;
   if (use_loop || use_agg) {
     if (use_loop && (rc = gran_setup())) return rc;
     if ((rc = ensure(d_fail, 16))) return rc;
@@ -1807,6 +1819,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       if ((rc = next_gran_tag(&av.tag))) return rc;
       av.gwords = gw;
       av.ptss = ptss ? 1 : 0;
+      av.spill = (uint32_t*)d_aspill.p;
+      av.spill_pods = (int32_t)spill_p;
+      av.spill_terms = (int32_t)spill_t;
       av.debug = c->cfg.agg_debug;
       av.give_up_at = c->cfg.debug_give_up_at;
       av.gran = (unsigned long long*)d_agran.p;

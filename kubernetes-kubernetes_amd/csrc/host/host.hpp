@@ -544,6 +544,7 @@ class Engine {
   std::vector<unsigned long long*> agran_all, region_all;  // every rank's, as mapped here (node-sharded)
   DevBuf d_aggpeers;  // node-sharded k_agg_loop: the device copy of agran_all + region_all
   DevBuf d_astamps;          // k_agg_loop diagnostic stamps
+  DevBuf d_aspill;           // k_agg_loop: workgroup pod / term lists past the LDS ones (AggView::spill)
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)
   DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick, d_contrib_buf;

@@ -1,5 +1,7 @@
-"""Diagnostic: the node-sharded scheduler as W in-process ranks on one GPU (localGroup), SchedulingBasic
-with 5000 nodes per rank; pods/s and the loop's per-pod time for each exchange mode."""
+"""Diagnostic: the node-sharded scheduler as W in-process ranks on one GPU (localGroup); pods/s and the loop's
+per-pod time for each exchange mode.  python scripts/shard_probe.py 1,2d,2r,3d [c2|c4|c5]: SchedulingBasic with
+5000 nodes per rank (c2), TopologySpreading with 5000 nodes and pods per rank (c4), the mixed cluster with
+10000 nodes per rank (c5) -- weak scaling, one GPU's queues shared by every rank."""
 import os
 import sys
 import threading
@@ -11,8 +13,15 @@ sys.path.insert(0, os.path.join(ROOT, "kubernetes-kubernetes_amd"))
 from ksg.native import Scheduler  # noqa: E402
 from ksg import synth  # noqa: E402
 
-for world, dx in [(int(w[:-1]), w[-1] == "d") for w in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["2d", "2r"])]:
-    nodes, init, pods = synth.scheduling_basic(5000 * world, 1000 * world, 3000)
+WL = sys.argv[2] if len(sys.argv) > 2 else "c2"
+PER = {"c2": 5000, "c4": 5000, "c5": 10000}[WL]
+for world, dx in [(int(w.rstrip("dr")), w.endswith("d")) for w in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["2d", "2r"])]:
+    if WL == "c4":
+        nodes, init, pods = synth.topology_spreading(PER * world, PER * world, 3000)
+    elif WL == "c5":
+        nodes, init, pods = synth.mixed_cluster(PER * world, 1000 * world, 3000)
+    else:
+        nodes, init, pods = synth.scheduling_basic(PER * world, 1000 * world, 3000)
     name = f"p-{uuid.uuid4().hex[:6]}"
     ranks = []
     for r in range(world):
@@ -42,7 +51,7 @@ for world, dx in [(int(w[:-1]), w[-1] == "d") for w in (sys.argv[1].split(",") i
     for t in ts:
         t.join()
     dt = max(dts)
-    print(f"world {world} {'device' if dx else 'all-reduce'} exchange, {5000 * world} nodes: {2000 / dt:.0f} pods/s, "
+    print(f"{WL} world {world} {'device' if dx else 'all-reduce'} exchange, {PER * world} nodes: {2000 / dt:.0f} pods/s, "
           f"rank 0 stats {ranks[0].kernel_stats()}", flush=True)
     for s in ranks:
         s.close()
