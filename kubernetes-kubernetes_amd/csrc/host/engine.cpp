@@ -1573,6 +1573,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   struct LoopRun { int first, count; double bytes; bool agg, timed; };
   std::vector<LoopRun> runs;
+  // in-process ranks share one device: after a mid-batch drain (buffers regrown) the next loop launch
+  // waits at the gate again, so no rank's allocation is pending while a peer's loop spins on it
+  bool regate = false;
   std::vector<uint8_t> agg_pod((size_t)n, 0);  // scheduled by k_agg_loop (settle: node-sharded replicas)
   const int shard_lo = sblk0 * kBlock, shard_hi = (sblk0 + snblk) * kBlock;
   // loopTimingStride k: every k-th loop launch carries HIP events on its dispatch packet (0: none)
@@ -1725,6 +1728,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         std::fprintf(stderr, "[host] pipeline drained before pod %d (%s)\n", i,
                      c->layout_dirty || (c->pods_dirty && pods_needed) ? "mirror re-layout" : "staging grown");
       if ((r2 = settle_closed())) return r2;
+      if (comm && comm->launch_gate()) {  // every rank drained before any rank allocates
+        c->err = comm->err;
+        return KSG_EDEVICE;
+      }
+      regate = true;
       if ((r2 = c->ensure_mirror())) return r2;
       arena_words = std::max(arena_words, aw);
       o = 0;
@@ -1772,10 +1780,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       lv.wave_map = c->cfg.loop_wave_map;
       lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * GS * 8 : nullptr;
       // in-process ranks: every rank is past its allocations before any rank's first loop starts
-      if (runs.empty() && comm && comm->launch_gate()) {
+      if ((runs.empty() || regate) && comm && comm->launch_gate()) {
         c->err = comm->err;
         return KSG_EDEVICE;
       }
+      regate = false;
       const bool tl = loop_timed(runs.size());
       HIPCHK(launch_sched_loop(m, bv, lv, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr,
                                unit));
@@ -1837,10 +1846,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       av.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_astamps.p + (size_t)n * kAggStamps + (size_t)i * G * 4
                                       : nullptr;
       // in-process ranks: every rank is past its allocations before any rank's first loop starts
-      if (runs.empty() && comm && comm->launch_gate()) {
+      if ((runs.empty() || regate) && comm && comm->launch_gate()) {
         c->err = comm->err;
         return KSG_EDEVICE;
       }
+      regate = false;
       const bool tl = loop_timed(runs.size());
       HIPCHK(launch_agg_loop(m, bv, av, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr));
       runs.push_back({i, j - i, rb, true, tl});
