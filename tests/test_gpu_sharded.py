@@ -367,3 +367,34 @@ def test_random_streams_sharded_agg_loop(world, seed):
     _check(ranks, o, [rand_pod(rng, k, names) for k in range(200)], chunk=100)
     for s in ranks:
         assert s.compare_mirror(sync=True)[0] == 0
+
+
+def test_spilled_lists_sharded_agg_loop():
+    """Node-sharded k_agg_loop whose workgroups hold more pods / terms than their LDS lists (the HBM spill
+    rows): 1000 zoned nodes over 2 ranks, one workgroup each, 9000 bound pods of which
+    4500 carry a preferred anti-affinity term, then a mixed PTS / IPA stream."""
+    from ksg import synth
+    nodes, init, pods = synth.mixed_cluster(1000, 4500, 160)
+    names = [n["metadata"]["name"] for n in nodes]
+    for k in range(4500):
+        p = synth.pod_with_preferred_pod_anti_affinity(f"pa-{k}", "sched-1")
+        p["spec"]["nodeName"] = names[(k * 7) % len(names)]
+        init.append(p)
+    ranks, o = _group(2, {"deviceExchange": True, "loopWorkgroups": 1}, nodes, init)
+    _check(ranks, o, pods, chunk=160)
+    assert _dominant(ranks) == {"k_agg_loop"}
+    for s in ranks:
+        assert s.compare_mirror(sync=True)[0] == 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c5_pipelined_batches_sharded_agg_loop(world):
+    """600-pod batches of the mixed stream over W in-process ranks with the device exchange: the batch runs
+    as pipelined chunks (later chunks compiled while the loop runs, drains when staging grows), every
+    rank passing the host gate before each loop launch that follows a drain."""
+    from ksg.synth import mixed_cluster
+    nodes, init, pods = mixed_cluster(6000, 1200, 1200)
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=600)
+    for s in ranks:
+        assert s.compare_mirror(sync=True)[0] == 0
