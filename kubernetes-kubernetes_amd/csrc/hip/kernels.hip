@@ -2644,11 +2644,12 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
     if (__all(ok)) return true;
     if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
       const unsigned long long miss = __ballot(!ok);
-      if (lane == 0) {
+      uint32_t first = 0u;  // the first failure's record is kept (a later give-up is its consequence)
+      if (lane == 0 && __hip_atomic_compare_exchange_strong(av.fail, &first, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)) {
         __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(av.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
     }
@@ -2737,8 +2738,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     if (av.wstamps && t == 0) av.wstamps[((size_t)q * G + w) * 4 + k] = __builtin_amdgcn_s_memrealtime();
   };
   auto fail = [&](uint32_t code) {
-    __hip_atomic_store(av.fail + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(av.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t first = 0u;
+    if (__hip_atomic_compare_exchange_strong(av.fail, &first, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_store(av.fail + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(av.fail + 2, (uint32_t)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   };
   auto stage_prog = [&](int q, int tid, int nthr) __attribute__((always_inline)) {
     const uint4* src = reinterpret_cast<const uint4*>(b.descs + s_off[q]);

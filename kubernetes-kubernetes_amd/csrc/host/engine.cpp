@@ -1681,6 +1681,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   auto fault_detail = [&]() -> std::string {
     uint32_t f[4] = {0, 0, 0, 0};
     (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
+    if (f[1] >= 0xfffffff0u)  // k_agg_loop's own checks (list capacity): the first failure is kept
+      return "persistent loop stopped: workgroup " + std::to_string(f[2]) + " failed check " + std::to_string(0xffffffffu - f[1]) +
+             " (1: its pod / term lists exceed their capacity at launch, 2: an append overflowed)";
     return "persistent loop gave up (an exchange granule never arrived): pod " + std::to_string(f[1]) +
            " of its run, granule " + std::to_string(f[2]) + ", participant " + std::to_string(f[3]);
   };
