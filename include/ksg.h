@@ -285,6 +285,20 @@ int ksg_debug_relayouts(const ksg_ctx *ctx, uint64_t *full, uint64_t *gather);
  * scoring.go:287-299: log(size + 2)).  Returns n. */
 int ksg_debug_log_table(double *out, int32_t n);
 
+/* Parity diagnostics of the node-sharded exchange (no device needed), so host-side protocol tests drive the
+ * layout the kernels use rather than a copy of it.  ksg_debug_exchange_layout fills out[0..20] with
+ * kMaxShards, the all-reduce word indices XA_CNT, XA_BELOW, XA_NONIGN, XA_MAX_TAINT, XA_MAX_NA, XA_MAX_IPA,
+ * XA_NMIN_IPA, XA_END, XA_PROC, XA_WORDS, XB_KEY, XB_NODE, XB_WORDS, XP_MAX_PTS, XP_NMIN_PTS, XP_WORDS,
+ * XS_CNT, XS_BELOW, XS_WORDS and kPreBits (returns 21, KSG_EINVAL if cap is smaller).  ksg_debug_pack_best is
+ * the (TotalScore, heap pre-order) key every exchange B carries (selectHost, schedule_one.go:1005-1085).
+ * ksg_debug_gran_a packs a persistent loop's exchange-A granule payload (which 0: {below | count}, which 1:
+ * {max raw NodeAffinity + 1 | max raw TaintToleration + 1}, 0 when count is 0); _decode inverts both. */
+int ksg_debug_exchange_layout(int32_t *out, int32_t cap);
+uint64_t ksg_debug_pack_best(int64_t total, uint32_t pos);
+uint64_t ksg_debug_gran_a(int32_t which, uint32_t count, uint32_t below, int64_t max_taint, int64_t max_na);
+int ksg_debug_gran_a_decode(uint64_t g0, uint64_t g1, uint32_t *count, uint32_t *below, int64_t *taint_p1,
+                            int64_t *na_p1);
+
 #ifdef __cplusplus
 }
 #endif

@@ -655,4 +655,25 @@ KSG_HD inline bool id_in(const int32_t* ids, int32_t n, int32_t x) {
 KSG_HD inline unsigned long long enc_i64(int64_t v) { return (unsigned long long)v ^ 0x8000000000000000ull; }
 KSG_HD inline int64_t dec_i64(unsigned long long u) { return (int64_t)(u ^ 0x8000000000000000ull); }
 
+// ---- persistent-loop exchange granules: 8 bytes, {launch tag (16) | payload (48)} ----
+constexpr unsigned long long kGranPayload = (1ull << 48) - 1ull;
+KSG_HD inline unsigned long long gran_word(uint32_t tag, unsigned long long payload) {
+  return ((unsigned long long)tag << 48) | (payload & kGranPayload);
+}
+// k_sched_loop exchange A, granule 0: {feasible nodes before nextStartNodeIndex (20) | feasible nodes (20)}
+KSG_HD inline unsigned long long gran_a_counts(uint32_t cnt, uint32_t below) {
+  return ((unsigned long long)below << 20) | cnt;  // counts < 2^20 (host-checked)
+}
+// granule 1: {max raw NodeAffinity + 1 (24) | max raw TaintToleration + 1 (24)} over the feasible nodes (0: none);
+// the maxima arrive order-encoded (enc_i64), raw scores are < 2^24 - 1 (host-checked)
+KSG_HD inline unsigned long long gran_a_maxima(uint32_t cnt, unsigned long long enc_t, unsigned long long enc_n) {
+  const unsigned long long tp1 = cnt ? (unsigned long long)dec_i64(enc_t) + 1ull : 0ull;
+  const unsigned long long np1 = cnt ? (unsigned long long)dec_i64(enc_n) + 1ull : 0ull;
+  return (np1 << 24) | tp1;
+}
+KSG_HD inline uint32_t gran_a_count(unsigned long long g) { return (uint32_t)(g & 0xfffffull); }
+KSG_HD inline uint32_t gran_a_below(unsigned long long g) { return (uint32_t)((g >> 20) & 0xfffffull); }
+KSG_HD inline unsigned long long gran_a_tp1(unsigned long long g) { return g & 0xffffffull; }
+KSG_HD inline unsigned long long gran_a_np1(unsigned long long g) { return (g >> 24) & 0xffffffull; }
+
 }  // namespace ksg

@@ -1576,7 +1576,7 @@ __global__ __launch_bounds__(kBlock) void k_max_reduce(unsigned long long* dst, 
 // A granule is {tag(16) | payload(48)}: the tag is the batch's (host counter, never 0), so an array
 // needs no zeroing between batches and a stale granule never matches.  Every granule is written
 // exactly once per batch, into every rank's array (the local one, and the peers' over xGMI).
-constexpr unsigned long long kPayload = (1ull << 48) - 1ull;
+constexpr unsigned long long kPayload = kGranPayload;
 
 // diagnostic phase stamps (config "loopStamps"): workgroup 0's lane 0, 100 MHz constant clock
 __device__ __forceinline__ void stamp(const LoopView& lv, int q, int k) {
@@ -1587,7 +1587,7 @@ __device__ __forceinline__ void stamp(const LoopView& lv, int q, int k) {
 // scope into each rank's array (the peers' are IPC-mapped, uncached device memory).
 __device__ __forceinline__ void gran_put(const LoopView& lv, int q, int gid, int slot, unsigned long long payload) {
   const int P = lv.world * lv.nwg;
-  const unsigned long long v = ((unsigned long long)lv.tag << 48) | (payload & kPayload);
+  const unsigned long long v = gran_word(lv.tag, payload);
   const size_t at = ((size_t)q * P + gid) * kGran + slot;
   if (lv.world == 1) {
     __hip_atomic_store(lv.gran[0] + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1748,10 +1748,8 @@ __device__ __forceinline__ void assume_core(NodeCore& c, const PodDesc& d) {
 // host-checked: +1 so that 0 means "no feasible node")
 __device__ __forceinline__ void a_granules(uint32_t c, uint32_t bl, unsigned long long a, unsigned long long bb,
                                            unsigned long long* g0, unsigned long long* g1) {
-  const unsigned long long tp1 = c ? (unsigned long long)dec_i64(a) + 1ull : 0ull;   // < 2^24 (host-checked)
-  const unsigned long long np1 = c ? (unsigned long long)dec_i64(bb) + 1ull : 0ull;  // < 2^24
-  *g0 = ((unsigned long long)bl << 20) | c;                                          // counts < 2^20
-  *g1 = (np1 << 24) | tp1;
+  *g0 = gran_a_counts(c, bl);  // desc.h: the layout the host-side protocol test drives too
+  *g1 = gran_a_maxima(c, a, bb);
 }
 
 // Can pod `nd`'s evaluation of a node be computed, before pod `d` is assumed, as it will be after?
@@ -2113,11 +2111,11 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       for (int r = 0; r < kMaxSweep; ++r) {
         const int v = lane + 64 * r;
         if (v < P) {
-          const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
+          const uint32_t c = gran_a_count(xa[0][r]);
           F += c;
           if (v < gid) wp += c;
-          bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
-          const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
+          bf += gran_a_below(xa[0][r]);
+          const unsigned long long tv = gran_a_tp1(xa[1][r]), nv = gran_a_np1(xa[1][r]);
           tmax = tv > tmax ? tv : tmax;
           nmax = nv > nmax ? nv : nmax;
         }
@@ -2246,7 +2244,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           const int wsl = chosen ? win - k0 * U : -1;
           const uint32_t bl = below_wave(npar, (int)rot_next, chosen ? wsl / U : -1, chosen ? (wsl % U) >> 6 : -1,
                                          s_cball);
-          ga0 = ((unsigned long long)bl << 20) | (ga0 & 0xfffffull);
+          ga0 = gran_a_counts(gran_a_count(ga0), bl);
         }
         if (lane == 0 && (!chosen || s_cand_ok)) {
           gran_put(lv, q + 1, gid, 0, ga0);
@@ -2608,7 +2606,7 @@ __device__ __forceinline__ int64_t agg_total(const PodDesc& d, int64_t fixed, in
 template <bool SHARD>
 __device__ __forceinline__ void agran_put(const AggView& av, int q, int gid, int slot, unsigned long long payload) {
   const size_t at = ((size_t)q * (SHARD ? av.world : 1) * av.nwg + gid) * kAGran + slot;
-  const unsigned long long v = ((unsigned long long)av.tag << 48) | (payload & kPayload);
+  const unsigned long long v = gran_word(av.tag, payload);
   if constexpr (!SHARD) {
     __hip_atomic_store(av.gran + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
@@ -3359,11 +3357,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         for (int r = 0; r < kMaxSweep; ++r) {
           const int v = lane + 64 * r;
           if (v < P) {
-            const uint32_t c = (uint32_t)(xa[0][r] & 0xfffffull);
+            const uint32_t c = gran_a_count(xa[0][r]);
             F += c;
             if (v < gid) wp += c;
-            bf += (uint32_t)((xa[0][r] >> 20) & 0xfffffull);
-            const unsigned long long tv = xa[1][r] & 0xffffffull, nv = (xa[1][r] >> 24) & 0xffffffull;
+            bf += gran_a_below(xa[0][r]);
+            const unsigned long long tv = gran_a_tp1(xa[1][r]), nv = gran_a_np1(xa[1][r]);
             tmax = tv > tmax ? tv : tmax;
             nmax = nv > nmax ? nv : nmax;
             imax = xa[2][r] > imax ? xa[2][r] : imax;

@@ -389,4 +389,32 @@ int ksg_debug_log_table(double* out, int32_t n) {
   return n;
 }
 
+int ksg_debug_exchange_layout(int32_t* out, int32_t cap) {
+  using namespace ksg;
+  const int32_t v[] = {kMaxShards, XA_CNT,   XA_BELOW, XA_NONIGN,  XA_MAX_TAINT, XA_MAX_NA,   XA_MAX_IPA,
+                       XA_NMIN_IPA, XA_END,  XA_PROC,  XA_WORDS,   XB_KEY,       XB_NODE,     XB_WORDS,
+                       XP_MAX_PTS, XP_NMIN_PTS, XP_WORDS, XS_CNT,   XS_BELOW,     XS_WORDS,    kPreBits};
+  const int32_t n = (int32_t)(sizeof v / sizeof v[0]);
+  if (!out || cap < n) return KSG_EINVAL;
+  for (int32_t k = 0; k < n; ++k) out[k] = v[k];
+  return n;
+}
+
+uint64_t ksg_debug_pack_best(int64_t total, uint32_t pos) { return ksg::pack_best(total, pos); }
+
+uint64_t ksg_debug_gran_a(int32_t which, uint32_t count, uint32_t below, int64_t max_taint, int64_t max_na) {
+  return which == 0 ? ksg::gran_a_counts(count, below)
+                    : ksg::gran_a_maxima(count, ksg::enc_i64(max_taint), ksg::enc_i64(max_na));
+}
+
+int ksg_debug_gran_a_decode(uint64_t g0, uint64_t g1, uint32_t* count, uint32_t* below, int64_t* taint_p1,
+                            int64_t* na_p1) {
+  if (!count || !below || !taint_p1 || !na_p1) return KSG_EINVAL;
+  *count = ksg::gran_a_count(g0);
+  *below = ksg::gran_a_below(g0);
+  *taint_p1 = (int64_t)ksg::gran_a_tp1(g1);
+  *na_p1 = (int64_t)ksg::gran_a_np1(g1);
+  return KSG_OK;
+}
+
 }  // extern "C"
