@@ -1,6 +1,6 @@
 """Diagnostic: C5 (mixed 100k-node cluster) batch by batch -- wall ms, the batch's kernel stats (avg ms per
 pod, pods in a loop, kernel) and mirror re-layouts -- to show what changes as assumed pods accumulate.
-python scripts/c5_growth_probe.py [batches] [nodes]"""
+python scripts/c5_growth_probe.py [batches] [nodes] [c5|c2]  (c2: SchedulingBasic, 1000 init pods)"""
 import os
 import sys
 import time
@@ -12,7 +12,11 @@ from ksg import synth  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 100000
-nodes, init, pods = synth.mixed_cluster(N, N // 10, B * 1000)
+WL = sys.argv[3] if len(sys.argv) > 3 else "c5"
+if WL == "c2":
+    nodes, init, pods = synth.scheduling_basic(N, 1000, B * 1000)
+else:
+    nodes, init, pods = synth.mixed_cluster(N, N // 10, B * 1000)
 s = Scheduler({"device": 0, "kernelTimingStride": 1})
 for n in nodes:
     s.add_node(n)
