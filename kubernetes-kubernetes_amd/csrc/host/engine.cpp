@@ -960,7 +960,7 @@ Engine::Engine(Cluster* cl) : c(cl) {
 // A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
 // PodTopologySpread / InterPodAffinity scores, no per-node evaluation output).
 // No extended-resource requests anywhere in the pod (the batch pipeline's compile-cannot-fail test).
-static bool calc_scalar_free(const PodSpec& p) {
+bool pod_scalar_free(const PodSpec& p) {
   auto ok = [](const ResVec& v) {
     for (auto& r : v)
       if (r.name != "cpu" && r.name != "memory" && r.name != "ephemeral-storage") return false;
@@ -971,6 +971,9 @@ static bool calc_scalar_free(const PodSpec& p) {
   for (auto& k : p.init_containers)
     if (!ok(k.req)) return false;
   return ok(p.pod_requests) && ok(p.overhead);
+}
+static bool calc_scalar_free(const PodSpec& p) {  // decided once per pod at decode (ksg_pod_compile)
+  return p.scalar_free >= 0 ? p.scalar_free != 0 : pod_scalar_free(p);
 }
 
 bool Engine::rotdev() const {
@@ -1327,6 +1330,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // before the first launch.
   bool pipe = bnd.size() > 1;
   for (int i = 0; i < n && pipe; ++i) pipe = calc_scalar_free(*pods[i]);
+  const auto Tp = clk::now();
   std::vector<int32_t> pre_slot;
   if (pipe && assume) {
     pre_slot.resize(n);
@@ -1334,6 +1338,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (int i = 0; i < n; ++i) pre_slot[i] = c->pod_table_put(*pods[i], -1);
     reserve_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tr).count();
   }
+  const auto Tv0 = clk::now();
   std::vector<CompiledPod> cp(n);
   int compiled = 0;
   // compile pods [compiled, b) against the cache (PreFilter / PreScore on the host)
@@ -1356,6 +1361,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     return KSG_OK;
   };
   int rc;
+  const auto Tv1 = clk::now();
   {
     const int64_t start = c->next_start;
     if ((rc = compile_upto(pipe ? bnd[0] : n))) {  // nothing launched: the batch fails as a whole
@@ -1368,6 +1374,12 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     }
   }
   const auto T1 = clk::now();
+  {
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    c0_us_[0] = us(T0, Tp);
+    c0_us_[1] = us(Tv0, Tv1);
+    c0_us_[2] = us(Tv1, T1);
+  }
   bool pods_needed = eval != nullptr;
   for (int i = 0; i < compiled && !pods_needed; ++i)
     pods_needed = (reinterpret_cast<const PodDesc*>(cp[i].blob.data())->flags & DF_AGGREGATE) != 0;
@@ -2221,6 +2233,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
                  api_t0_.time_since_epoch().count() ? us(api_t0_, T0) : 0.0, us(T0, T1), reserve_us_, mirror_us_,
                  us(T3, T4));
     reserve_us_ = 0;
+    std::fprintf(stderr, "[chunk 0, us] plan + scalar check %.1f  program vectors %.1f  compile %.1f\n", c0_us_[0],
+                 c0_us_[1], c0_us_[2]);
     std::fprintf(stderr, "[compile sections, us per pod] node-affinity %.3f  taints+ports %.3f  resources+images %.3f  "
                  "topology %.3f (spread %.3f  affinity %.3f  placement+tables %.3f)  masks+assume %.3f\n", cprof_[0] / n,
                  cprof_[1] / n, cprof_[2] / n, cprof_[3] / n, cprof_[5] / n, cprof_[6] / n, cprof_[7] / n, cprof_[4] / n);

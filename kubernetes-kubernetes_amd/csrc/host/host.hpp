@@ -121,7 +121,11 @@ struct PodSpec {
   std::string nominated_node;    // status.nominatedNodeName
   bool preempt_terminating = false;  // PodTerminatingByPreemption
   mutable std::shared_ptr<const PodTablePre> pt_pre;  // Cluster::pod_table_precompile (same context only)
+  // every request / overhead names cpu, memory or ephemeral-storage only (1), or not (0); -1: not yet
+  // known.  Set by decode_pod, so a batch's pipeline check does not re-compare resource names.
+  int8_t scalar_free = -1;
 };
+bool pod_scalar_free(const PodSpec& p);  // the check behind PodSpec::scalar_free
 struct NodeImage { std::vector<std::string> names; int64_t size; };
 struct NodeSpec {
   std::string name;
@@ -492,7 +496,8 @@ class Engine {
   double cprof_[8] = {};  // loopStamps: compile time per section (us), reported with the host line
   std::chrono::steady_clock::time_point api_t0_{};  // loopStamps: ksg_schedule_batch entry
   double reserve_us_ = 0;
-  double mirror_us_ = 0;    // loopStamps: ensure_mirror before the batch's first launch (us)   // loopStamps: the batch's pod-table slot reservation (us)
+  double mirror_us_ = 0;    // loopStamps: ensure_mirror before the batch's first launch (us)
+  double c0_us_[3] = {};    // loopStamps: chunk 0's plan + scalar check, program vectors, compile (us)
   int compile_topology(const PodSpec& p, Mode mode, int plugin, int32_t N, Blob* B, PodDesc* D, uint32_t* fmask,
                        uint32_t* smask, CompiledPod* out);
   // run a batch of cycles (device-resident, sequential semantics)

@@ -374,6 +374,7 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
     d.each(d.get(*sp, "resourceClaims"), [&](const JVal&) { claims = true; });
     if (claims && out->unsupported.empty())
       out->unsupported = "spec.resourceClaims needs DynamicResources, which runs outside the device path";
+    out->scalar_free = pod_scalar_free(*out) ? 1 : 0;
     return true;
   } catch (std::exception& e) {
     *err = e.what();
