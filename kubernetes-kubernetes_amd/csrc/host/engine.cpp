@@ -1332,11 +1332,28 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   for (int i = 0; i < n && pipe; ++i) pipe = calc_scalar_free(*pods[i]);
   const auto Tp = clk::now();
   std::vector<int32_t> pre_slot;
+  struct HeadroomReset {
+    Cluster* c;
+    ~HeadroomReset() { c->pt_headroom = 0; }
+  } headroom_reset{c};
   if (pipe && assume) {
-    pre_slot.resize(n);
-    const auto Tr = clk::now();
-    for (int i = 0; i < n; ++i) pre_slot[i] = c->pod_table_put(*pods[i], -1);
-    reserve_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tr).count();
+    // A batch none of whose pods can read the pod table (the superset test pods_needed uses below: no
+    // existing pod's terms, no own spread constraints or affinity terms) leaves each slot to its pod's
+    // compile, which overlaps the device; the device's pod_node column only keeps room for them.
+    // (and no PodTopologySpread system default can apply: no selecting object in the cache)
+    bool local = c->exanti_keys.empty() && c->score_keys_req.empty() && c->score_keys_pref.empty() &&
+                 (c->cfg.pts_defaults.empty() ||
+                  (c->services.empty() && c->owners[0].empty() && c->owners[1].empty() && c->owners[2].empty()));
+    for (int i = 0; i < n && local; ++i)
+      local = pods[i]->spreads.empty() && !pods[i]->has_pod_affinity && !pods[i]->has_pod_anti;
+    if (local) {
+      c->pt_headroom = n;
+    } else {
+      pre_slot.resize(n);
+      const auto Tr = clk::now();
+      for (int i = 0; i < n; ++i) pre_slot[i] = c->pod_table_put(*pods[i], -1);
+      reserve_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tr).count();
+    }
   }
   const auto Tv0 = clk::now();
   std::vector<CompiledPod> cp(n);

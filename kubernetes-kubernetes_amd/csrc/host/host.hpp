@@ -380,6 +380,9 @@ class Cluster {
   // lazy: skip the upload (keeping pods_dirty) when the device copy has room for every slot -- the
   // device-side AssumePod only writes pod_node[slot] -- and no pod of the call reads the table
   int upload_pod_table(bool lazy = false);
+  // pod-table slots a pipelined batch may still take after its first launch (Engine::run_batch): the
+  // device's pod_node column keeps room for them, since the loops' assumes write pod_node[slot]
+  int32_t pt_headroom = 0;
   std::vector<double> log_tab;  // go math.Log(k), k < log_n
   int32_t scalar_slot(const std::string& n);  // -1 if too many distinct scalars
   uint32_t port_id(std::string ip, std::string proto, int32_t port);

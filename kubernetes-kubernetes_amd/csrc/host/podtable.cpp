@@ -234,7 +234,8 @@ int Cluster::upload_pod_table(bool lazy) {
   // a call whose pods never read the pod table (no PodTopologySpread / InterPodAffinity work) only needs
   // pod_node to have room for the slots its assumes write: the table goes up with the next call that
   // reads it (every single-pod call of a node-local stream would otherwise re-upload the whole table)
-  if (lazy && pods_dirty && pt_dev_[0].p && pt_dev_[0].bytes >= pt_node.size() * 4 + 4) return KSG_OK;
+  const bool room = pt_dev_[0].p && pt_dev_[0].bytes >= (pt_node.size() + (size_t)pt_headroom) * 4 + 4;
+  if (lazy && pods_dirty && room) return KSG_OK;
   // log table covers topoSize + 2 for every topoSize <= N (scoring.go:293-299)
   const int32_t need_log = (int32_t)order_.size() + 4;
   bool log_dirty = false;
@@ -244,7 +245,7 @@ int Cluster::upload_pod_table(bool lazy) {
     for (size_t k = old; k < log_tab.size(); ++k) log_tab[k] = go_log((double)k);
     log_dirty = true;
   }
-  if (!pods_dirty && !log_dirty) return KSG_OK;
+  if (!pods_dirty && !log_dirty && room) return KSG_OK;  // (a batch's headroom may need a larger pod_node)
   // compact the label pool when most of it is garbage
   size_t live = 0;
   for (size_t s = 0; s < pt_node.size(); ++s) live += pt_lbl_cnt[s];
@@ -260,7 +261,7 @@ int Cluster::upload_pod_table(bool lazy) {
   }
   int rc;
   const size_t P = pt_node.size(), T = tt.size();
-  if ((rc = grow(pt_dev_[0], P * 4 + 4))) return rc;
+  if ((rc = grow(pt_dev_[0], (P + (size_t)pt_headroom) * 4 + 4))) return rc;
   if ((rc = grow(pt_dev_[1], P * 4 + 4))) return rc;
   if ((rc = grow(pt_dev_[2], P * 4 + 4))) return rc;
   if ((rc = grow(pt_dev_[3], P * 4 + 4))) return rc;
