@@ -523,6 +523,12 @@ struct LoopView {
 // exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
 // A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)
 constexpr int kGran = 4;
+// A persistent loop's give-up record (LoopView::fail / AggView::fail): [0] flag, [1] pod of the run
+// (the granule row; or a k_agg_loop check code), [2] granule (or workgroup), [3] first missing sweep
+// lane, [4] loop (1 k_sched_loop, 2 k_agg_loop), [5] its granule tag, [6, 7] the sweep's missing-lane
+// ballot at the give-up (lane l: some participant l + 64 k had not published)
+constexpr int kFailWords = 8;
+constexpr int kFailBytes = kFailWords * 4;
 
 // ---- persistent loop for pods with pod-table aggregation (k_agg_loop) ---------------
 // Same workgroup geometry as k_sched_loop (unsharded).  Each workgroup also owns the pod-table slots

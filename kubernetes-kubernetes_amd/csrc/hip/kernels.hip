@@ -1632,6 +1632,10 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
         __hip_atomic_store(lv.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(lv.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(lv.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_sched_loop
+        __hip_atomic_store(lv.fail + 5, (uint32_t)lv.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail + 6, (uint32_t)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lv.fail + 7, (uint32_t)(miss >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(lv.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
@@ -2648,6 +2652,10 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
         __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(av.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail + 4, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_agg_loop
+        __hip_atomic_store(av.fail + 5, (uint32_t)av.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail + 6, (uint32_t)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(av.fail + 7, (uint32_t)(miss >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
     }
@@ -3962,6 +3970,21 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
     else go(k_agg_loop<false, false>);
   }
   return hipGetLastError();
+}
+// Workgroups of each persistent loop one CU holds at once (the loops' grids must be resident as a whole:
+// every workgroup spins on the others' granules): [0] k_sched_loop 128-node unit, [1] 256-node unit,
+// [2] k_agg_loop, [3] its node-sharded instance.  0 means the kernel cannot be resident at all.
+hipError_t loop_occupancy(int (&occ)[4]) {
+  struct K { const void* f; int threads; } ks[4] = {
+      {reinterpret_cast<const void*>(&k_sched_loop<2, false>), 2 * 64 + 128},
+      {reinterpret_cast<const void*>(&k_sched_loop<4, false>), kLoopThreads},
+      {reinterpret_cast<const void*>(&k_agg_loop<false, true>), kAggThreads},
+      {reinterpret_cast<const void*>(&k_agg_loop<true, true>), kAggThreads}};
+  for (int i = 0; i < 4; ++i) {
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[i], ks[i].f, ks[i].threads, 0);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 // Loads the module's code object onto the current device now (hipFuncGetAttributes), so that no
 // first launch inside a batch does it while an in-process peer's persistent loop is running.

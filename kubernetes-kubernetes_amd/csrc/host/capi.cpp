@@ -79,7 +79,7 @@ ksg_ctx* ksg_create(const char* config_json, size_t len) {
     }
     if (cfg.sharded()) {  // node-sharded: join the exchange group (collective across the ranks)
       std::string err;
-      ctx->engine->comm = make_comm(cfg, &err);
+      ctx->engine->comm = make_comm(cfg, ctx->cluster->own_queue, &err);
       if (!ctx->engine->comm) {
         g_create_error = err;
         delete ctx;

@@ -5,6 +5,7 @@
 // (framework/types.go:445-468), the nodeTree zone round-robin order (node_tree.go:52-143) and
 // UpdateSnapshot's list rule (cache.go:190-296, 318-358).  Node add/remove re-lays the mirror
 // out; node updates are rewritten in place; pod events touch one node.
+#include <atomic>
 #include <algorithm>
 #include <cstring>
 
@@ -31,10 +32,23 @@ static const char* zone_key(const NodeSpec& n, std::string* out) {  // node/topo
   return out->c_str();
 }
 
+int hw_queues() {
+  static const int q = [] {
+    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+    return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
+  }();
+  return q;
+}
+static std::atomic<int> g_streams{0};
+bool stream_created() { return g_streams.fetch_add(1) + 1 + 1 <= hw_queues(); }  // + the null stream
+void stream_destroyed() { g_streams.fetch_sub(1); }
+
 Cluster::Cluster(const Config& c) : cfg(c) {
   std::memset(&view, 0, sizeof(view));
   if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
     err = "cannot open HIP device " + std::to_string(cfg.device);
+  else
+    own_queue = stream_created();
 }
 
 Cluster::~Cluster() {
@@ -43,7 +57,10 @@ Cluster::~Cluster() {
     if (b.p) (void)hipFree(b.p);
   if (upd_dev_.p) (void)hipFree(upd_dev_.p);
   if (dyn_dev_.p) (void)hipFree(dyn_dev_.p);
-  if (stream) (void)hipStreamDestroy(stream);
+  if (stream) {
+    (void)hipStreamDestroy(stream);
+    stream_destroyed();
+  }
 }
 
 void* Cluster::dalloc(size_t bytes) {

@@ -52,6 +52,7 @@ class RcclComm : public Comm {
       err = "share_buffers: allocation failed";
       return KSG_EDEVICE;
     }
+    (void)stream_created();
     int rc = KSG_OK;
     if (hipMemcpy(d + (size_t)rank * hb, &h, hb, hipMemcpyHostToDevice) != hipSuccess ||
         ncclAllGather(d + (size_t)rank * hb, d, hb, ncclChar, comm, s) != ncclSuccess ||
@@ -62,6 +63,7 @@ class RcclComm : public Comm {
     }
     (void)hipFree(d);
     (void)hipStreamDestroy(s);
+    stream_destroyed();
     if (rc) return rc;
     all->assign(world, nullptr);
     for (int r = 0; r < world; ++r) {
@@ -123,6 +125,7 @@ struct LocalGroup {
   std::mutex mu;
   std::condition_variable cv;
   int world = 0, arrived = 0, members = 0;
+  bool own_queues = true;  // every member's stream has a hardware queue of its own
   uint64_t gen = 0;
   std::vector<unsigned long long*> bufs;
   std::vector<hipEvent_t> evs;
@@ -213,6 +216,11 @@ class LocalComm : public Comm {
     return KSG_OK;
   }
 
+  bool own_queues() const override {
+    std::lock_guard<std::mutex> lk(g->mu);
+    return g->members == g->world && g->own_queues;
+  }
+
   int launch_gate() override {
     int sl = 0;
     if (!rendezvous(nullptr, nullptr, 0, &sl)) {
@@ -232,7 +240,7 @@ class LocalComm : public Comm {
   }
 };
 
-std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err) {
+std::unique_ptr<Comm> make_comm(const Config& cfg, bool own_queue, std::string* err) {
   if (!cfg.sharded()) return nullptr;
   if (!cfg.nccl_id.empty()) {
     ncclUniqueId id;
@@ -275,6 +283,7 @@ std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err) {
       return nullptr;
     }
     ++g->members;
+    g->own_queues = g->own_queues && own_queue;
     c->g = g;
   }
   return c;

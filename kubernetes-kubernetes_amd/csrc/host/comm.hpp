@@ -41,11 +41,15 @@ class Comm {
   // collective: every rank passes its device buffer; all[r] becomes rank r's buffer as mapped in
   // this process (in-process: the pointer itself; RCCL ranks: an IPC mapping of the peer's memory)
   virtual int share_buffers(void* mine, std::vector<void*>* all) = 0;
+  // every rank's stream has a hardware queue of its own (in-process groups: all ranks joined and
+  // each Cluster::own_queue; RCCL ranks each own a device)
+  virtual bool own_queues() const { return true; }
   std::string err;
 };
 
 // nullptr + *err on failure; cfg.world == 1 never creates one
-std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err);
+// own_queue: this rank's stream has a hardware queue of its own (Cluster::own_queue)
+std::unique_ptr<Comm> make_comm(const Config& cfg, bool own_queue, std::string* err);
 // ncclGetUniqueId as 256 hex characters (rank 0 creates it and hands it to every rank)
 int comm_unique_id(std::string* hex, std::string* err);
 

@@ -49,6 +49,7 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
                            hipEvent_t t1);
 hipError_t warm_kernels();
 hipError_t warm_aggregate();
+hipError_t loop_occupancy(int (&occ)[4]);
 
 #define HIPCHK(x)                                               \
   do {                                                          \
@@ -955,6 +956,8 @@ Engine::Engine(Cluster* cl) : c(cl) {
   // every kernel's code object loaded before the first batch (see warm_kernels)
   if (c->err.empty() && (warm_kernels() != hipSuccess || warm_aggregate() != hipSuccess))
     c->err = "cannot load the kernels' code object on HIP device " + std::to_string(c->cfg.device);
+  if (c->err.empty() && loop_occupancy(loop_occ) != hipSuccess)
+    c->err = "cannot query the persistent loops' occupancy on HIP device " + std::to_string(c->cfg.device);
 }
 
 // A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
@@ -1077,7 +1080,10 @@ Engine::~Engine() {
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
   for (hipEvent_t e : cev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
-  if (cstream) (void)hipStreamDestroy(cstream);
+  if (cstream) {
+    (void)hipStreamDestroy(cstream);
+    stream_destroyed();
+  }
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill,
                     &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf})
@@ -1257,6 +1263,43 @@ int Engine::next_gran_tag(uint32_t* tag) {
 // the aggregation does not read: the pod-table slot, the rotation and the pod's own affinity terms (the last
 // part of the program; the fold of a adds a's own terms to b's counts).  Pods stamped from one template, as
 // every scheduler_perf workload's are, qualify; anything else only loses the shortcut.
+// The participants (p = rank * g + workgroup) a set names, per rank: "rank 0 wg {0,3-7}; rank 2 wg {0-7}"
+static std::string participants_by_rank(const std::vector<uint8_t>& in, int world, int g) {
+  std::string out;
+  for (int r = 0; r < world; ++r) {
+    std::string ws;
+    int cnt = 0;
+    for (int w = 0; w < g; ++w) {
+      if (!in[(size_t)(r * g + w)]) continue;
+      int e = w;  // a run of consecutive workgroups as a-b
+      while (e + 1 < g && in[(size_t)(r * g + e + 1)]) ++e;
+      ws += (cnt ? "," : "") + std::to_string(w) + (e > w ? "-" + std::to_string(e) : "");
+      cnt += e - w + 1;
+      w = e;
+    }
+    if (cnt) out += (out.empty() ? "rank " : "; rank ") + std::to_string(r) + " wg {" + ws + "} of " + std::to_string(g);
+  }
+  return out.empty() ? "none" : out;
+}
+
+// Which participants a loop give-up (record f, kFailWords) waited for: at the give-up (the sweep's
+// missing-lane ballot; exact up to 64 participants) and still after the drain (the granule row `row`
+// of this rank's array, read back).  Absent at the give-up but present after the drain: that loop was
+// late -- not resident yet (a queue or CU it waited for); absent in both: it stopped or never ran.
+static std::string give_up_detail(const uint32_t* f, const std::vector<unsigned long long>& row, int ng, int world, int g) {
+  const int P = world * g;
+  const unsigned long long ball = (unsigned long long)f[6] | ((unsigned long long)f[7] << 32);
+  std::vector<uint8_t> at(P, 0), now(P, 0);
+  for (int p = 0; p < P; ++p) {
+    now[(size_t)p] = row.size() >= (size_t)P * ng && (row[(size_t)p * ng + f[2]] >> 48) != (unsigned long long)f[5];
+    at[(size_t)p] = ((ball >> (p & 63)) & 1ull) && (P <= 64 || now[(size_t)p]);
+  }
+  return std::string(f[4] == 2 ? "k_agg_loop" : "k_sched_loop") + " granule row " + std::to_string(f[1]) + " slot " +
+         std::to_string(f[2]) + ": missing at the give-up " + participants_by_rank(at, world, g) +
+         (P > 64 ? " (sweep lanes fold 64 participants: intersected with the drain)" : "") + "; still missing after the drain " +
+         participants_by_rank(now, world, g);
+}
+
 static bool agg_same(const CompiledPod& a, const CompiledPod& b) {
   if (a.error || b.error || a.blob.size() != b.blob.size() || a.blob.size() < sizeof(PodDesc)) return false;
   PodDesc x, y;
@@ -1290,15 +1333,12 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const auto T0 = clk::now();
   // ---- the chunk plan (needs the exchange mode of a sharded context)
   const int W = comm ? c->cfg.world : 1;
-  // In-process ranks (localGroup, one device) need every rank's loop resident at once: each rank has
-  // its own stream, and streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES, default 4)
-  // share queues and serialise.  Such groups keep the all-reduce path.
-  static const int hwq = [] {
-    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
-    return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
-  }();
+  // In-process ranks (localGroup, one device) need every rank's loop resident at once, so every
+  // rank's stream must have a hardware queue of its own: on a shared queue a rank's loop waits behind
+  // a peer's loop that spins on it (Cluster::own_queue).  The group decides as one (Comm::own_queues):
+  // otherwise it keeps the all-reduce path.
   const bool rccl = !c->cfg.nccl_id.empty();
-  const bool dx = comm && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) && (rccl || W < hwq);
+  const bool dx = comm && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) && (rccl || comm->own_queues());
   // Host/device pipeline: the batch runs as chunks.  While the device schedules chunk k the host
   // compiles and stages chunk k+1, then mirrors the finished chunks' assumes into the cache.  Only
   // chunk 0's compile and the last chunk's bookkeeping are exposed, so chunk 0 is short (32 pods,
@@ -1466,7 +1506,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // (not for in-process rank groups: their streams already outnumber the hardware queues, and a
   // copy stream's event wait sharing a queue with a peer's loop launch would hold that loop back)
   const bool copy_stream = pipe && (!comm || rccl);
-  if (copy_stream && !cstream) HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+  if (copy_stream && !cstream) {
+    HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    (void)stream_created();
+  }
   while (pev.size() < 2 * bnd.size()) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1558,8 +1601,13 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       unit = 128;
     }
   }
+  // residency: a loop's workgroups spin on each other, so its whole grid -- every in-process rank's
+  // grid, as those share this device -- must fit in what the CUs hold at once (loop_occ); a grid that
+  // does not is never launched, instead of spinning until the give-up
+  const int64_t dev_ranks = comm && !rccl ? W : 1;
   const bool use_loop = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && NB > 0 && GS >= 1 &&
                         (int64_t)GS * kLoopMaxBlk * unit >= (int64_t)NBs * kBlock &&
+                        (int64_t)GS * dev_ranks <= (int64_t)cus * loop_occ[unit == 128 ? 0 : 1] &&
                         (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   // k_agg_loop: the same geometry (node-sharded: over the device exchange, world * G participants);
   // every workgroup's LDS lists must hold its nodes' pods and terms plus everything this batch can add
@@ -1567,6 +1615,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // rank's workgroups (each rank holds the whole cluster).
   bool use_agg = loop_worth && (!comm || dx) && !eval && c->cfg.persistent_loop && c->cfg.agg_loop && NB > 0 && G >= 1 &&
                  G * W <= std::min(cus, 256) && (int64_t)G * kLoopMaxBlk >= NBs &&
+                 (int64_t)G * dev_ranks <= (int64_t)cus * loop_occ[W > 1 ? 3 : 2] &&
                  (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
   int64_t spill_p = 0, spill_t = 0;  // k_agg_loop: HBM list entries per workgroup (AggView::spill)
   if (use_agg) {
@@ -1613,8 +1662,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   if (use_agg && (rc = ensure(d_aspill, (size_t)G * (size_t)(spill_p + spill_t) * 4 + 4))) return rc;
   if (use_loop || use_agg) {
     if (use_loop && (rc = gran_setup())) return rc;
-    if ((rc = ensure(d_fail, 16))) return rc;
-    HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
+    if ((rc = ensure(d_fail, kFailBytes))) return rc;
+    HIPCHK(hipMemsetAsync(d_fail.p, 0, kFailBytes, s));
     if (c->cfg.loop_stamps) {
       const size_t sb = (size_t)n * 8 * 8 + 64 * 8 + (size_t)n * std::max(G, GS) * 8 * 8;
       if ((rc = ensure(d_stamps, sb))) return rc;
@@ -1708,13 +1757,22 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     return KSG_EDEVICE;
   };
   auto fault_detail = [&]() -> std::string {
-    uint32_t f[4] = {0, 0, 0, 0};
-    (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
+    uint32_t f[kFailWords] = {};
+    (void)hipMemcpyAsync(f, d_fail.p, kFailBytes, hipMemcpyDeviceToHost, s);  // not the null stream (§6)
+    (void)hipStreamSynchronize(s);
     if (f[1] >= 0xfffffff0u)  // k_agg_loop's own checks (list capacity): the first failure is kept
       return "persistent loop stopped: workgroup " + std::to_string(f[2]) + " failed check " + std::to_string(0xffffffffu - f[1]) +
              " (1: its pod / term lists exceed their capacity at launch, 2: an append overflowed)";
-    return "persistent loop gave up (an exchange granule never arrived): pod " + std::to_string(f[1]) +
-           " of its run, granule " + std::to_string(f[2]) + ", participant " + std::to_string(f[3]);
+    const bool agg = f[4] == 2;
+    const int g = agg ? G : GS, ng = agg ? kAGran : kGran;
+    std::vector<unsigned long long> row((size_t)W * g * ng);
+    const DevBuf& gb = agg ? d_agran : d_gran;
+    if (gb.p && ((size_t)f[1] + 1) * row.size() * 8 <= gb.bytes)
+      (void)hipMemcpyAsync(row.data(), (const unsigned long long*)gb.p + (size_t)f[1] * row.size(), row.size() * 8,
+                           hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    return "persistent loop gave up (an exchange granule never arrived) on rank " + std::to_string(comm ? c->cfg.rank : 0) +
+           ": " + give_up_detail(f, row, ng, W, g);
   };
   int settled = 0;  // chunks whose results are mirrored into the cache
   auto settle_closed = [&]() -> int {  // after a stream sync: every closed chunk
@@ -1970,7 +2028,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   if (!runs.empty()) {
     uint32_t fail = 0;
-    HIPCHK(hipMemcpy(&fail, d_fail.p, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(&fail, d_fail.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     if (fail) return loop_fault(n, fault_detail());
   }
   float ms = 0;
@@ -2508,6 +2567,7 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     }
   }
   if ((int64_t)GS * kLoopMaxBlk * unit < (int64_t)NB * kBlock) return KSG_OK;
+  if ((int64_t)GS > (int64_t)cus * loop_occ[unit == 128 ? 0 : 1]) return KSG_OK;  // residency (run_batch)
   if ((int64_t)c->taint_max_per_node >= ((int64_t)1 << 24) - 1) return KSG_OK;
   // PreFilter / PreScore on the host, as run_batch's compile_upto
   const auto T0 = clk::now();
@@ -2570,9 +2630,9 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     }
     std::memset((void*)ring_, 0, offsetof(PodRing, blob));
     if ((rc = gran_setup())) return fail(rc);
-    if ((rc = ensure(d_fail, 16))) return fail(rc);
+    if ((rc = ensure(d_fail, kFailBytes))) return fail(rc);
     if ((rc = ensure_scratch(256, kLoopMaxPods, false, 0))) return fail(rc);
-    HIPCHK(hipMemsetAsync(d_fail.p, 0, 16, s));
+    HIPCHK(hipMemsetAsync(d_fail.p, 0, kFailBytes, s));
     HIPCHK(hipMemsetAsync(d_stats.p, 0, d_stats.bytes, s));  // PodStats::ipa_any = 0 for every pod
     LoopView lv{};
     lv.first_pod = 0;
@@ -2617,13 +2677,20 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     if ((spins & 0xfffu) == 0 && hipStreamQuery(s) != hipErrorNotReady) {  // the launch ended without it
       res_running_ = false;
       (void)hipStreamSynchronize(s);
-      uint32_t f[4] = {0, 0, 0, 0};
-      (void)hipMemcpy(f, d_fail.p, 16, hipMemcpyDeviceToHost);
+      uint32_t f[kFailWords] = {};
+      (void)hipMemcpyAsync(f, d_fail.p, kFailBytes, hipMemcpyDeviceToHost, s);
+      std::vector<unsigned long long> row((size_t)res_gs_ * kGran);
+      if (f[0] && ((size_t)f[1] + 1) * row.size() * 8 <= d_gran.bytes)
+        (void)hipMemcpyAsync(row.data(), (const unsigned long long*)d_gran.p + (size_t)f[1] * row.size(), row.size() * 8,
+                             hipMemcpyDeviceToHost, s);
+      (void)hipStreamSynchronize(s);
       c->layout_dirty = true;
       c->mirror_suspect = true;
       c->pods_dirty = true;
       c->err = std::string("resident loop ended without the pod's result") +
-               (f[0] ? " (an exchange granule never arrived)" : "") + "; the device mirror is rebuilt from the cache";
+               (f[0] ? " (an exchange granule never arrived: " + give_up_detail(f, row, kGran, 1, res_gs_) + ")"
+                     : std::string()) +
+               "; the device mirror is rebuilt from the cache";
       return fail(KSG_EDEVICE);
     }
   }

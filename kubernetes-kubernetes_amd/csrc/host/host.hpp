@@ -27,6 +27,14 @@
 
 namespace ksg {
 
+// HIP streams this library holds in the process (every context's stream, copy streams, transient
+// ones).  The HIP runtime gives a new stream its own hardware queue while the process holds fewer
+// than GPU_MAX_HW_QUEUES (default 4) and shares the least-used one after that; the null stream takes
+// one too.  stream_created() returns whether the new stream's queue is its own.
+int hw_queues();
+bool stream_created();
+void stream_destroyed();
+
 // ===================================================================================
 // objects
 // ===================================================================================
@@ -390,6 +398,11 @@ class Cluster {
   // ---- HBM mirror
   MirrorView view;
   hipStream_t stream = nullptr;
+  // the stream got a hardware queue of its own: when it was created, every stream of this library in
+  // the process plus the null stream fitted in GPU_MAX_HW_QUEUES (stream_created below).  In-process
+  // rank groups need it for the device exchange (a rank's loop queued behind a peer's spinning loop
+  // on a shared queue never starts).
+  bool own_queue = true;
   bool layout_dirty = true;
   bool defer_relayout = false;  // ensure_label_slot only marks layout_dirty (pods in flight)
   bool mirror_suspect = false;  // device columns may hold assumes the cache lacks: rebuild all of them
@@ -523,6 +536,10 @@ class Engine {
   int32_t last_launches = 0;
   int32_t last_kernel = 0;  // 0: k_filter_score figures; 1: k_sched_loop (per-pod time in the loop)
   int cu_count = 0;
+  // workgroups of each persistent loop a CU holds at once (loop_occupancy: [0] k_sched_loop 128-node
+  // unit, [1] 256-node unit, [2] k_agg_loop, [3] node-sharded k_agg_loop); a loop's whole grid -- all
+  // ranks' grids for in-process groups, which share the device -- must fit in cu_count * that
+  int loop_occ[4] = {0, 0, 0, 0};
   bool loop_ok(const CompiledPod& p) const;
   bool loop_bounds_ok(const CompiledPod& p) const;  // the loops' granule payload bounds
   bool agg_loop_ok(const CompiledPod& p) const;

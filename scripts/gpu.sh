@@ -1,0 +1,52 @@
+#!/bin/bash
+# The one GPU-box runner (replaces the per-round scripts/gpu_*.sh one-offs).
+#
+#   gpurun -- bash scripts/gpu.sh STEP [STEP ...]
+#
+# Steps (each GPU step has its own time limit; a crash, abort or timeout (rc > 1) ends the script
+# before any further GPU work; every step writes gpurun_out/<name>.log):
+#   suite               pytest -m gpu, whole suite
+#   tests=<file[::k]>   pytest on one file / node id (-m gpu)
+#   smoke               __graft_entry__.smoke()
+#   bench=<wl>[:steps]  bench.py --workload <wl> (c1 c2 c2pct0 c3 c4 c4-anti c5 dts), 3 steps by default
+#   prof=<wl>           rocprofv3 --kernel-trace --stats of a short bench run of <wl>
+#   pmc=<wl>            FETCH_SIZE and WRITE_SIZE passes (separate rocprofv3 runs) of <wl>
+#   py=<script>[:args]  python3 -u scripts/<script> args (probes); ',' in args becomes ' '
+export TMPDIR=/tmp
+mkdir -p gpurun_out/prof
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc"; tail -n 3 "gpurun_out/$name.log"; [ $rc -le 1 ] || exit $rc
+}
+bench_args() {  # workload -> bench.py arguments
+  case $1 in
+    c2pct0) echo "--workload c2 --pct 0" ;;
+    *) echo "--workload $1" ;;
+  esac
+}
+PYT="python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider"
+for s in "$@"; do
+  case $s in
+    suite) step suite 900 $PYT tests -m gpu ;;
+    tests=*) f=${s#tests=}; step "tests_$(basename "${f%%::*}" .py)" 600 $PYT "$f" -m gpu -v ;;
+    smoke) step smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench=*)
+      a=${s#bench=}; wl=${a%%:*}; n=3; [ "$a" != "$wl" ] && n=${a#*:}
+      step "bench_$wl" 400 python -u bench.py $(bench_args "$wl") --steps "$n" --warmup 1 --cpu-seconds 5 ;;
+    prof=*)
+      wl=${s#prof=}
+      step "prof_$wl" 400 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof/trace_$wl" -o run -- \
+        python3 bench.py $(bench_args "$wl") --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc=*)
+      wl=${s#pmc=}
+      step "pmcf_$wl" 300 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/prof/pmc_fetch_$wl" -o run -- \
+        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline
+      step "pmcw_$wl" 300 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/prof/pmc_write_$wl" -o run -- \
+        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline ;;
+    py=*)
+      a=${s#py=}; sc=${a%%:*}; args=""; [ "$a" != "$sc" ] && args=${a#*:}
+      step "py_${sc%.py}" 400 python3 -u "scripts/$sc" ${args//,/ } ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -8,6 +8,7 @@ loop-eligible pods exchange through the persistent loop's granules stored into e
 oracle's ScheduleResult for every pod of the stream (sequential assume semantics), including
 empty shards (clusters smaller than W * 256 nodes) and PodTopologySpread/InterPodAffinity pods.
 """
+import os
 import threading
 import uuid
 
@@ -387,7 +388,7 @@ def test_spilled_lists_sharded_agg_loop():
         assert s.compare_mirror(sync=True)[0] == 0
 
 
-@pytest.mark.parametrize("world", [2])  # W = 3: one start-barrier give-up in a full-suite run
+@pytest.mark.parametrize("world", [2, 3])
 def test_c5_pipelined_batches_sharded_agg_loop(world):
     """600-pod batches of the mixed stream over W in-process ranks with the device exchange: the batch runs
     as pipelined chunks (later chunks compiled while the loop runs, drains when staging grows), every
@@ -398,3 +399,25 @@ def test_c5_pipelined_batches_sharded_agg_loop(world):
     _check(ranks, o, pods, chunk=600)
     for s in ranks:
         assert s.compare_mirror(sync=True)[0] == 0
+
+
+@pytest.mark.skipif(os.environ.get("GPU_MAX_HW_QUEUES", "4") != "4", reason="counts HIP's default 4 hardware queues")
+def test_device_exchange_needs_own_queues():
+    """In-process ranks take the device exchange only when every rank's stream has a hardware queue of its
+    own: with another context's stream alive, a W = 3 group's three streams plus the null
+    stream exceed GPU_MAX_HW_QUEUES = 4, so HIP would put two of them on one queue, where a rank's loop
+    waits behind a peer's loop that spins on it.  That group must keep the all-reduce path (and still
+    match the oracle); once the other context is gone, a new W = 3 group runs the loop."""
+    from ksg.native import Scheduler
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(1877, 300, 600, hetero=True)
+    other = Scheduler({"device": 0})
+    ranks, o = _group(3, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=300)
+    assert _dominant(ranks) == {"k_filter_score"}
+    for s in ranks:
+        s.close()
+    other.close()
+    ranks, o = _group(3, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=300)
+    assert _dominant(ranks) == {"k_sched_loop"}
