@@ -285,6 +285,13 @@ int ksg_debug_relayouts(const ksg_ctx *ctx, uint64_t *full, uint64_t *gather);
  * scoring.go:287-299: log(size + 2)).  Returns n. */
 int ksg_debug_log_table(double *out, int32_t n);
 
+/* The requests the library derives from one v1.Pod (no context, no device): out[0..4] are
+ * CalculateResource's Requested MilliCPU / Memory / EphemeralStorage and Non0CPU / Non0Mem
+ * (pkg/scheduler/framework/types.go:1035-1076, with the in-place resize status resources of
+ * component-helpers/resource/helpers.go:193-260,299-304), out[5..7] Fit's PreFilter request
+ * (noderesources/fit.go:317-325, spec only).  Returns 8, or KSG_EINVAL. */
+int ksg_debug_pod_resources(const char *pod_json, size_t len, int64_t *out, int32_t cap);
+
 /* Parity diagnostics of the node-sharded exchange (no device needed), so host-side protocol tests drive the
  * layout the kernels use rather than a copy of it.  ksg_debug_exchange_layout fills out[0..20] with
  * kMaxShards, the all-reduce word indices XA_CNT, XA_BELOW, XA_NONIGN, XA_MAX_TAINT, XA_MAX_NA, XA_MAX_IPA,

@@ -389,6 +389,18 @@ int ksg_debug_log_table(double* out, int32_t n) {
   return n;
 }
 
+int ksg_debug_pod_resources(const char* pod_json, size_t len, int64_t* out, int32_t cap) {
+  using namespace ksg;
+  if (!pod_json || !out || cap < 8) return KSG_EINVAL;
+  PodSpec p;
+  std::string err;
+  if (!decode_pod(pod_json, len, &p, &err)) return KSG_EINVAL;
+  const PodResources r = calc_resources(p), f = calc_fit_request(p);
+  const int64_t v[8] = {r.cpu, r.mem, r.eph, r.nz_cpu, r.nz_mem, f.cpu, f.mem, f.eph};
+  for (int k = 0; k < 8; ++k) out[k] = v[k];
+  return 8;
+}
+
 int ksg_debug_exchange_layout(int32_t* out, int32_t cap) {
   using namespace ksg;
   const int32_t v[] = {kMaxShards, XA_CNT,   XA_BELOW, XA_NONIGN,  XA_MAX_TAINT, XA_MAX_NA,   XA_MAX_IPA,

@@ -363,18 +363,25 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   }
 
   mark(1);
-  // NodeResourcesFit PreFilter + assume payload (fit.go:317-335; framework/types.go:1035-1076)
+  // NodeResourcesFit PreFilter (fit.go:317-335: the spec's requests) and the assume payload
+  // (CalculateResource, framework/types.go:1035-1076: a resized pod's status resources count too; the
+  // two differ only for a pod that carries status resources)
   const PodResources res = calc_resources(p);
+  const PodResources fit = p.has_status_res ? calc_fit_request(p) : res;
   out->res = res;
   out->port_ids = own;
-  D.req_cpu = res.cpu;
-  D.req_mem = res.mem;
-  D.req_eph = res.eph;
+  D.req_cpu = fit.cpu;
+  D.req_mem = fit.mem;
+  D.req_eph = fit.eph;
   std::vector<ScalarReq> fsr, asr;
   for (auto& s : res.scalar) {
     int32_t slot = c->scalar_slot(s.first);
     if (slot < 0) { c->err = "too many extended resources"; return KSG_ENOTSUP; }
     asr.push_back({slot, 0, s.second});
+  }
+  for (auto& s : fit.scalar) {
+    int32_t slot = c->scalar_slot(s.first);
+    if (slot < 0) { c->err = "too many extended resources"; return KSG_ENOTSUP; }
     if (s.second == 0) continue;
     const bool extended = s.first.find('/') != std::string::npos && s.first.find("kubernetes.io/") == std::string::npos;
     if (extended) {
@@ -383,7 +390,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     }
     fsr.push_back({slot, 0, s.second});
   }
-  D.fit_any = (res.cpu > 0 || res.mem > 0 || res.eph > 0 || !res.scalar.empty()) ? 1 : 0;
+  D.fit_any = (fit.cpu > 0 || fit.mem > 0 || fit.eph > 0 || !fit.scalar.empty()) ? 1 : 0;
   D.n_scalar = (int32_t)fsr.size();
   D.scalar_off = B.put(fsr);
   D.a_cpu = res.cpu;
@@ -400,7 +407,7 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
     std::vector<ScoreRes> v;
     ResVec nm;
     if (!useRequested) nm = {{"cpu", 100}, {"memory", 200LL * 1024 * 1024 * 1000}};
-    const ResVec reqs = pod_requests(p, useRequested ? nullptr : &nm);
+    const ResVec reqs = pod_requests(p, useRequested ? nullptr : &nm, true);  // resource_allocation.go:236-259
     *best_effort = true;
     for (auto& sp : specs) {
       ScoreRes r{};
@@ -970,10 +977,10 @@ bool pod_scalar_free(const PodSpec& p) {
     return true;
   };
   for (auto& k : p.containers)
-    if (!ok(k.req)) return false;
+    if (!ok(k.req) || !ok(k.st_req) || !ok(k.st_alloc)) return false;
   for (auto& k : p.init_containers)
-    if (!ok(k.req)) return false;
-  return ok(p.pod_requests) && ok(p.overhead);
+    if (!ok(k.req) || !ok(k.st_req) || !ok(k.st_alloc)) return false;
+  return ok(p.pod_requests) && ok(p.overhead) && ok(p.pod_st_req) && ok(p.pod_st_alloc);
 }
 static bool calc_scalar_free(const PodSpec& p) {  // decided once per pod at decode (ksg_pod_compile)
   return p.scalar_free >= 0 ? p.scalar_free != 0 : pod_scalar_free(p);

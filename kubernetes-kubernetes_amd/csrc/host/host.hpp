@@ -71,10 +71,15 @@ struct PATerm {
 struct Tol { std::string key, op, value, effect; };
 struct HostPort { std::string ip, proto; int32_t port; };
 struct Container {
-  std::string image;
+  std::string name, image;
   ResVec req;
   std::vector<HostPort> ports;
   bool sidecar = false;
+  // InPlacePodVerticalScaling (GA, kube_features.go:1479-1483): the container status of the same name
+  // (status.containerStatuses, then initContainerStatuses) with resources != nil -- its actuated
+  // requests (resources.requests) and allocatedResources (component-helpers resource/helpers.go:199-215)
+  bool has_status = false;
+  ResVec st_req, st_alloc;
 };
 struct Spread {
   int32_t max_skew = 0;
@@ -112,6 +117,13 @@ struct PodSpec {
   std::vector<Container> containers, init_containers;
   bool has_overhead = false;
   ResVec overhead, pod_requests;
+  // in-place resize state (helpers.go:160-170, 299-320; InPlacePodLevelResourcesVerticalScaling is on
+  // by default, kube_features.go:1474-1477): status.resources != nil with its requests and
+  // status.allocatedResources, and the first PodResizePending condition's reason == Infeasible
+  bool has_pod_status_res = false;
+  ResVec pod_st_req, pod_st_alloc;
+  bool resize_infeasible = false;
+  bool has_status_res = false;  // some container, or the pod, carries status resources
   std::vector<Spread> spreads;
   std::vector<std::string> image_volumes;
   // why a pod to schedule is outside the device's plugin set ("" if it is not): volumes or resource
@@ -167,8 +179,13 @@ struct PodResources {
   int64_t nz_cpu = 0, nz_mem = 0;
   // Fit filter max-request vector (SetMaxResource) -- identical values in practice
 };
-ResVec pod_requests(const PodSpec& p, const ResVec* non_missing);
+// resource.PodRequests; use_status: PodResourcesOptions.UseStatusResources (CalculateResource and the
+// score plugins' calculatePodResourceRequest set it, Fit's PreFilter does not: fit.go:317-325)
+ResVec pod_requests(const PodSpec& p, const ResVec* non_missing, bool use_status);
 PodResources calc_resources(const PodSpec& p);
+// Fit's PreFilter request (computePodResourceRequest, fit.go:317-325: no status resources), in
+// calc_resources' units (non-zero fields unused)
+PodResources calc_fit_request(const PodSpec& p);
 double go_log(double x);  // Go's math.Log (podtable.cpp)
 bool tolerates(const Tol& t, const std::string& key, const std::string& value, const std::string& effect,
                bool cmp_ops);

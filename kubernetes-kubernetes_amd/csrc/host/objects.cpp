@@ -185,6 +185,7 @@ static PATerm pa_term(const JDoc& d, const JVal& t, int32_t weight) {
   return p;
 }
 static bool container(const JDoc& d, const JVal& c, Container* out, std::string* err) {
+  out->name = d.str(c, "name");
   out->image = d.str(c, "image");
   if (const JVal* r = d.get(c, "resources"))
     if (!res_list(d, d.get(*r, "requests"), &out->req, err)) return false;
@@ -267,7 +268,35 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
       out->owner_kind = d.str(o, "kind");
       out->owner_name = d.str(o, "name");
     });
+    // container statuses by name (AggregateContainerRequests' map: containerStatuses, then
+    // initContainerStatuses over them), kept while their resources are non-nil
+    struct CStat { std::string name; bool res; ResVec req, alloc; };
+    std::vector<CStat> cstats;
     if (const JVal* st = d.get(r, "status")) {
+      bool ok = true;
+      for (const char* key : {"containerStatuses", "initContainerStatuses"})
+        d.each(d.get(*st, key), [&](const JVal& cs) {
+          CStat x{d.str(cs, "name"), false, {}, {}};
+          if (const JVal* rs = d.get(cs, "resources")) {
+            x.res = true;
+            ok = ok && res_list(d, d.get(*rs, "requests"), &x.req, err);
+          }
+          ok = ok && res_list(d, d.get(cs, "allocatedResources"), &x.alloc, err);
+          cstats.push_back(std::move(x));
+        });
+      if (const JVal* rs = d.get(*st, "resources")) {
+        out->has_pod_status_res = true;
+        ok = ok && res_list(d, d.get(*rs, "requests"), &out->pod_st_req, err);
+        ok = ok && res_list(d, d.get(*st, "allocatedResources"), &out->pod_st_alloc, err);
+      }
+      // IsPodResizeInfeasible (helpers.go:311-320): the first PodResizePending condition decides
+      bool seen_resize = false;
+      d.each(d.get(*st, "conditions"), [&](const JVal& c) {
+        if (seen_resize || d.str(c, "type") != "PodResizePending") return;
+        seen_resize = true;
+        out->resize_infeasible = d.str(c, "reason") == "Infeasible";
+      });
+      if (!ok) return false;
       const std::string t = d.str(*st, "startTime");
       if (!t.empty()) {
         if (!parse_rfc3339(t, &out->start_ns)) { *err = "bad status.startTime " + t; return false; }
@@ -337,6 +366,20 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
       out->init_containers.push_back(std::move(k));
     });
     if (!ok) return false;
+    auto attach = [&](Container& k) {
+      const CStat* found = nullptr;
+      for (const CStat& x : cstats)
+        if (x.name == k.name) found = &x;  // the last of the name wins (the map's overwrite)
+      if (!found || !found->res) return;
+      k.has_status = true;
+      k.st_req = found->req;
+      k.st_alloc = found->alloc;
+      out->has_status_res = true;
+    };
+    for (auto& k : out->containers) attach(k);
+    for (auto& k : out->init_containers)
+      if (k.sidecar) attach(k);  // only restartable init containers read their status (helpers.go:236-246)
+    out->has_status_res = out->has_status_res || out->has_pod_status_res;
     if (const JVal* oh = d.get(*sp, "overhead")) {
       out->has_overhead = true;
       if (!res_list(d, oh, &out->overhead, err)) return false;
@@ -488,12 +531,28 @@ static bool pod_level_supported(const std::string& n) {
   return n == "cpu" || n == "memory" || n.rfind("hugepages-", 0) == 0;
 }
 
-ResVec pod_requests(const PodSpec& p, const ResVec* non_missing) {
-  ResVec reqs;
-  for (const auto& c : p.containers) add_res(reqs, with_non_missing(c.req, non_missing));
+// determineEffectiveRequests (helpers.go:299-304) with max (:494-507): a resize the kubelet reported
+// Infeasible counts its actuated and allocated requests only, any other the per-resource maximum of the
+// spec, actuated and allocated requests
+static ResVec effective_requests(bool infeasible, const ResVec& spec, const ResVec& actuated, const ResVec& alloc) {
+  ResVec out = infeasible ? actuated : spec;
+  if (!infeasible) max_res(out, actuated);
+  max_res(out, alloc);
+  return out;
+}
+static const ResVec& container_requests(const PodSpec& p, const Container& c, bool use_status, ResVec* tmp) {
+  if (!use_status || !c.has_status) return c.req;
+  *tmp = effective_requests(p.resize_infeasible, c.req, c.st_req, c.st_alloc);
+  return *tmp;
+}
+
+ResVec pod_requests(const PodSpec& p, const ResVec* non_missing, bool use_status) {
+  use_status = use_status && p.has_status_res;
+  ResVec reqs, tmp;
+  for (const auto& c : p.containers) add_res(reqs, with_non_missing(container_requests(p, c, use_status, &tmp), non_missing));
   ResVec restartable, init;
   for (const auto& c : p.init_containers) {
-    ResVec cr = with_non_missing(c.req, non_missing);
+    ResVec cr = with_non_missing(container_requests(p, c, use_status, &tmp), non_missing);
     if (c.sidecar) {
       add_res(reqs, cr);
       add_res(restartable, cr);
@@ -509,26 +568,36 @@ ResVec pod_requests(const PodSpec& p, const ResVec* non_missing) {
   max_res(reqs, init);
   bool pod_level = false;
   for (const auto& r : p.pod_requests) pod_level |= pod_level_supported(r.name);
-  if (pod_level)
+  if (pod_level) {
+    // InPlacePodLevelResourcesVerticalScaling with status.resources set: each pod-level request is the
+    // effective one, 0 where that list lacks it (helpers.go:160-179)
+    const bool eff = use_status && p.has_pod_status_res;
+    const ResVec effr = eff ? effective_requests(p.resize_infeasible, p.pod_requests, p.pod_st_req, p.pod_st_alloc) : ResVec{};
     for (const auto& r : p.pod_requests)
       if (pod_level_supported(r.name)) {
+        int64_t v = r.milli;
+        if (eff) {
+          auto e = std::find_if(effr.begin(), effr.end(), [&](const ResAmount& x) { return x.name == r.name; });
+          v = e == effr.end() ? 0 : e->milli;
+        }
         auto it = std::find_if(reqs.begin(), reqs.end(), [&](const ResAmount& x) { return x.name == r.name; });
-        if (it == reqs.end()) reqs.push_back(r);
-        else it->milli = r.milli;
+        if (it == reqs.end()) reqs.push_back({r.name, v});
+        else it->milli = v;
       }
+  }
   if (p.has_overhead) add_res(reqs, p.overhead);
   return reqs;
 }
 
 PodResources calc_resources(const PodSpec& p) {  // framework/types.go:1035-1076
-  const ResVec requests = pod_requests(p, nullptr);
+  const ResVec requests = pod_requests(p, nullptr, true);
   bool pod_level = false;
   for (const auto& r : p.pod_requests) pod_level |= pod_level_supported(r.name);
   ResVec nm;  // getNonMissingContainerRequests (types.go:1387-1415)
   const int64_t cpu_def = 100, mem_def = 200LL * 1024 * 1024 * 1000;
   if (!pod_level || !has_res(requests, "cpu")) nm.push_back({"cpu", cpu_def});
   if (!pod_level || !has_res(requests, "memory")) nm.push_back({"memory", mem_def});
-  const ResVec non0 = nm.empty() ? requests : pod_requests(p, &nm);
+  const ResVec non0 = nm.empty() ? requests : pod_requests(p, &nm, true);
   PodResources out;
   for (const auto& r : requests) {
     if (r.name == "cpu") out.cpu += r.milli;
@@ -539,6 +608,17 @@ PodResources calc_resources(const PodSpec& p) {  // framework/types.go:1035-1076
   for (const auto& r : non0) {
     if (r.name == "cpu") out.nz_cpu = r.milli;
     else if (r.name == "memory") out.nz_mem = milli_ceil(r.milli);
+  }
+  return out;
+}
+
+PodResources calc_fit_request(const PodSpec& p) {  // fit.go:317-325 (SetMaxResource over PodRequests)
+  PodResources out;
+  for (const auto& r : pod_requests(p, nullptr, false)) {
+    if (r.name == "cpu") out.cpu += r.milli;
+    else if (r.name == "memory") out.mem += milli_ceil(r.milli);
+    else if (r.name == "ephemeral-storage") out.eph += milli_ceil(r.milli);
+    else if (r.name != "pods" && scalar_resource(r.name)) out.scalar.push_back({r.name, milli_ceil(r.milli)});
   }
   return out;
 }

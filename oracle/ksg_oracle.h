@@ -51,6 +51,7 @@ int ksgo_preempt(ksgo_ctx *ctx, int32_t handle, const char *args_json, size_t ar
 
 /* Go math.Log restatement (exposed so tests can compare it with libm). */
 double ksgo_go_log(double x);
+int ksgo_debug_pod_resources(const char *json, size_t len, int64_t *out, int32_t cap);
 /* container/heap Init over (score) with nodeScoreHeap.Less, returns index of the root. */
 int32_t ksgo_heap_root(const int64_t *scores, int32_t n);
 

@@ -832,7 +832,7 @@ static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std
       if (cy.wantPorts.empty()) *skip = true;
       return Status{};
     case KSG_PLUGIN_NODE_RESOURCES_FIT: {  // fit.go:317-335 computePodResourceRequest
-      ResList reqs = pod_requests(pod, nullptr);
+      ResList reqs = pod_requests(pod, nullptr, false);  // "pod hasn't scheduled yet": no status resources
       Resource r;  // SetMaxResource (types.go:1325-1344)
       for (auto& kv : reqs) {
         if (kv.first == "memory") r.memory = std::max(r.memory, milli_to_value(kv.second));
@@ -1032,7 +1032,7 @@ static Status run_filter(Cycle& cy, int p, NodeInfoO* ni) {
 static int64_t pod_resource_request(const Pod& pod, const std::string& name, bool useRequested) {
   ResList nonMissing;
   if (!useRequested) { nonMissing["cpu"] = 100; nonMissing["memory"] = 200LL * 1024 * 1024 * 1000; }
-  ResList reqs = pod_requests(pod, useRequested ? nullptr : &nonMissing);
+  ResList reqs = pod_requests(pod, useRequested ? nullptr : &nonMissing, true);  // UseStatusResources
   auto it = reqs.find(name);
   int64_t m = it == reqs.end() ? 0 : it->second;
   return name == "cpu" ? m : milli_to_value(m);
@@ -2378,6 +2378,29 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
 }
 
 double ksgo_go_log(double x) { return go_log(x); }
+
+// CalculateResource (framework/types.go:1035-1076) and Fit's computePodResourceRequest (fit.go:317-325)
+// of one pod: out[0..4] MilliCPU, Memory, EphemeralStorage, Non0CPU, Non0Mem; out[5..7] the Fit request
+int ksgo_debug_pod_resources(const char* json, size_t len, int64_t* out, int32_t cap) {
+  if (!json || !out || cap < 8) return KSG_EINVAL;
+  std::string err;
+  Pod p;
+  try {
+    if (!decode_pod(mj::parse(json, len), &p, &err)) return KSG_EINVAL;
+  } catch (const std::exception&) {
+    return KSG_EINVAL;
+  }
+  const PodResource r = calculate_resource(p);
+  int64_t fit[3] = {0, 0, 0};
+  for (auto& kv : pod_requests(p, nullptr, false)) {
+    if (kv.first == "cpu") fit[0] = kv.second;
+    else if (kv.first == "memory") fit[1] = milli_to_value(kv.second);
+    else if (kv.first == "ephemeral-storage") fit[2] = milli_to_value(kv.second);
+  }
+  const int64_t o[8] = {r.res.milliCPU, r.res.memory, r.res.ephemeral, r.non0CPU, r.non0Mem, fit[0], fit[1], fit[2]};
+  for (int k = 0; k < 8; ++k) out[k] = o[k];
+  return 8;
+}
 
 int32_t ksgo_heap_root(const int64_t* scores, int32_t n) {
   if (n <= 0) return -1;

@@ -437,6 +437,30 @@ bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
               out->terminating && c.str("status") == "True" && c.str("reason") == "PreemptionByScheduler";
           break;
         }
+    if (const mj::Value* cs = st->has("conditions"))
+      for (auto& c : cs->arr) out->conditions.push_back({c.str("type"), c.str("reason")});
+    auto statuses = [&](const char* key, std::vector<Pod::ContainerStatus>* o) {
+      if (const mj::Value* l = st->has(key))
+        for (auto& c : l->arr) {
+          Pod::ContainerStatus x;
+          x.name = c.str("name");
+          if (const mj::Value* r = c.has("resources")) {
+            x.hasResources = true;
+            if (!decode_reslist(r->get("requests"), &x.requests, err)) return false;
+          }
+          if (!decode_reslist(c.get("allocatedResources"), &x.allocated, err)) return false;
+          o->push_back(x);
+        }
+      return true;
+    };
+    if (!statuses("containerStatuses", &out->containerStatuses) ||
+        !statuses("initContainerStatuses", &out->initContainerStatuses))
+      return false;
+    if (const mj::Value* r = st->has("resources")) {
+      out->hasStatusResources = true;
+      if (!decode_reslist(r->get("requests"), &out->statusRequests, err)) return false;
+      if (!decode_reslist(st->get("allocatedResources"), &out->statusAllocated, err)) return false;
+    }
   }
   const mj::Value* sp = v.has("spec");
   if (!sp) return true;
@@ -588,16 +612,49 @@ bool pod_level_requests_set(const Pod& p) {
   return false;
 }
 
-ResList pod_requests(const Pod& p, const ResList* nonMissing, bool skipPodLevel) {  // helpers.go:151-291
+static bool is_pod_resize_infeasible(const Pod& p) {  // helpers.go:311-320
+  for (auto& c : p.conditions)
+    if (c.first == "PodResizePending") return c.second == "Infeasible";
+  return false;
+}
+static ResList max_of(const ResList& a, const ResList& b) {  // max(a, b), helpers.go:494-507
+  ResList r = a;
+  max_list(r, b);
+  return r;
+}
+// determineEffectiveRequests (helpers.go:299-304)
+static ResList determine_effective_requests(const Pod& p, const ResList& spec, const ResList& actuated,
+                                            const ResList& allocated) {
+  if (is_pod_resize_infeasible(p)) return max_of(actuated, allocated);
+  return max_of(max_of(spec, actuated), allocated);
+}
+
+ResList pod_requests(const Pod& p, const ResList* nonMissing, bool useStatus, bool skipPodLevel) {  // helpers.go:151-291
+  // AggregateContainerRequests (:193-291)
+  std::map<std::string, const Pod::ContainerStatus*> containerStatuses;
+  if (useStatus) {
+    for (auto& cs : p.containerStatuses) containerStatuses[cs.name] = &cs;
+    for (auto& cs : p.initContainerStatuses) containerStatuses[cs.name] = &cs;
+  }
   ResList reqs;
   for (auto& c : p.containers) {
     ResList cr = c.requests;
+    if (useStatus) {
+      auto it = containerStatuses.find(c.name);
+      if (it != containerStatuses.end() && it->second->hasResources)
+        cr = determine_effective_requests(p, c.requests, it->second->requests, it->second->allocated);
+    }
     if (nonMissing && !nonMissing->empty()) cr = apply_non_missing(cr, *nonMissing);
     add_list(reqs, cr);
   }
   ResList restartable, initReqs;
   for (auto& c : p.initContainers) {
     ResList cr = c.requests;
+    if (useStatus && c.restartAlways) {
+      auto it = containerStatuses.find(c.name);
+      if (it != containerStatuses.end() && it->second->hasResources)
+        cr = determine_effective_requests(p, c.requests, it->second->requests, it->second->allocated);
+    }
     if (nonMissing && !nonMissing->empty()) cr = apply_non_missing(cr, *nonMissing);
     if (c.restartAlways) {
       add_list(reqs, cr);
@@ -612,15 +669,28 @@ ResList pod_requests(const Pod& p, const ResList* nonMissing, bool skipPodLevel)
     max_list(initReqs, cr);
   }
   max_list(reqs, initReqs);
-  if (!skipPodLevel && pod_level_requests_set(p))  // :157-179 (PodLevelResources on by default)
+  if (!skipPodLevel && pod_level_requests_set(p)) {  // :157-179 (PodLevelResources on by default)
+    bool haveEffective = false;
+    ResList effectiveReqs;
+    if (useStatus && p.hasStatusResources) {  // InPlacePodLevelResourcesVerticalScaling (on by default)
+      effectiveReqs = determine_effective_requests(p, p.podRequests, p.statusRequests, p.statusAllocated);
+      haveEffective = true;
+    }
     for (auto& kv : p.podRequests)
-      if (supported_pod_level(kv.first)) reqs[kv.first] = kv.second;
+      if (supported_pod_level(kv.first)) {
+        reqs[kv.first] = kv.second;
+        if (haveEffective) {  // effectiveReqs[name]: the zero Quantity when absent
+          auto it = effectiveReqs.find(kv.first);
+          reqs[kv.first] = it == effectiveReqs.end() ? 0 : it->second;
+        }
+      }
+  }
   if (p.hasOverhead) add_list(reqs, p.overhead);  // :182-184
   return reqs;
 }
 
-PodResource calculate_resource(const Pod& p) {  // framework/types.go:1035-1076
-  ResList requests = pod_requests(p, nullptr);
+PodResource calculate_resource(const Pod& p) {  // framework/types.go:1035-1076 (UseStatusResources: GA gate)
+  ResList requests = pod_requests(p, nullptr, true);
   bool podLevelSet = pod_level_requests_set(p);
   ResList nonMissing;  // getNonMissingContainerRequests :1387-1415
   if (!podLevelSet) {
@@ -631,7 +701,7 @@ PodResource calculate_resource(const Pod& p) {  // framework/types.go:1035-1076
     if (!requests.count("memory")) nonMissing["memory"] = 200LL * 1024 * 1024 * 1000;
   }
   ResList non0 = requests;
-  if (!nonMissing.empty()) non0 = pod_requests(p, &nonMissing);
+  if (!nonMissing.empty()) non0 = pod_requests(p, &nonMissing, true);
   PodResource r;
   // Resource.Add (types.go:1270-1291): cpu -> MilliValue, others -> Value
   for (auto& kv : requests) {

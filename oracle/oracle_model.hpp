@@ -118,6 +118,14 @@ struct Pod {
   bool hasOverhead = false;
   ResList overhead;
   ResList podRequests;  // spec.resources.requests (pod-level resources)
+  // status (InPlacePodVerticalScaling): v1.ContainerStatus name / resources (nil?) .requests /
+  // allocatedResources, in list order; status.resources (nil?) .requests; status.allocatedResources;
+  // status.conditions' (type, reason) in order
+  struct ContainerStatus { std::string name; bool hasResources = false; ResList requests, allocated; };
+  std::vector<ContainerStatus> containerStatuses, initContainerStatuses;
+  bool hasStatusResources = false;
+  ResList statusRequests, statusAllocated;
+  std::vector<std::pair<std::string, std::string>> conditions;
   std::vector<TopologySpreadConstraint> tsc;
   std::vector<std::string> imageVolumes;  // volumes[].image.reference
   // DefaultPreemption
@@ -183,7 +191,9 @@ bool new_pod_info(const Pod& p, PodInfo* out);
 bool is_scalar_resource_name(const std::string& n);  // scheduler/util/utils.go:200-203
 // resource.PodRequests (component-helpers/resource/helpers.go:151-291), as used by
 // the scheduler: nonMissing != nullptr applies NonMissingContainerRequests.
-ResList pod_requests(const Pod& p, const ResList* nonMissing, bool skipPodLevel = false);
+// resource.PodRequests (helpers.go:151-291); useStatus: PodResourcesOptions.UseStatusResources (with
+// InPlacePodLevelResourcesVerticalScalingEnabled, both on by default)
+ResList pod_requests(const Pod& p, const ResList* nonMissing, bool useStatus, bool skipPodLevel = false);
 bool pod_level_requests_set(const Pod& p);  // helpers.go:108-124
 PodResource calculate_resource(const Pod& p);  // framework/types.go:1035-1076
 

@@ -230,6 +230,47 @@ def rand_cluster(seed, n_nodes, n_existing, cfg_index=None, topology=True):
     return rng, cfg, nodes, existing, names
 
 
+def add_resize_status(rng, pod):
+    """In-place resize state on a bound pod (InPlacePodVerticalScaling, GA): container statuses whose
+    resources / allocatedResources differ from the spec, sometimes for an init or sidecar container of
+    the same name, a pod-level request with status.resources, and a PodResizePending (Deferred /
+    Infeasible) or PodResizeInProgress condition (component-helpers resource/helpers.go:193-320)."""
+    spec, st = pod["spec"], pod.setdefault("status", {})
+
+    def some():
+        r = {}
+        if rng.random() < 0.8:
+            r["cpu"] = rng.choice(["50m", "200m", "750m", "2", "4"])
+        if rng.random() < 0.7:
+            r["memory"] = rng.choice(["64Mi", "300Mi", "2Gi", "6Gi"])
+        if rng.random() < 0.1:
+            r["ephemeral-storage"] = rng.choice(["512Mi", "2Gi"])
+        return r
+
+    for key, skey in (("containers", "containerStatuses"), ("initContainers", "initContainerStatuses")):
+        for c in spec.get(key, []):
+            if rng.random() < 0.6:
+                cs = {"name": c["name"]}
+                if rng.random() < 0.85:
+                    cs["resources"] = {"requests": some()} if rng.random() < 0.9 else {}
+                if rng.random() < 0.5:
+                    cs["allocatedResources"] = some()
+                st.setdefault(skey, []).append(cs)
+    if rng.random() < 0.15:
+        spec["resources"] = {"requests": some()}
+        if rng.random() < 0.7:
+            st["resources"] = {"requests": some()}
+            if rng.random() < 0.5:
+                st["allocatedResources"] = some()
+    r = rng.random()
+    if r < 0.25:
+        st.setdefault("conditions", []).append({"type": "PodResizePending", "status": "True",
+                                                "reason": rng.choice(["Deferred", "Infeasible"])})
+    elif r < 0.35:
+        st.setdefault("conditions", []).append({"type": "PodResizeInProgress", "status": "True"})
+    return pod
+
+
 def namespaces():
     return [make_namespace(n, l) for n, l in NAMESPACES]
 

@@ -504,6 +504,29 @@ class Unknown(Exception):
     pass
 
 
+_QSUFFIX = {"n": (10, -9), "u": (10, -6), "m": (10, -3), "": (10, 0), "k": (10, 3), "M": (10, 6), "G": (10, 9),
+            "T": (10, 12), "P": (10, 15), "E": (10, 18), "Ki": (2, 10), "Mi": (2, 20), "Gi": (2, 30), "Ti": (2, 40),
+            "Pi": (2, 50), "Ei": (2, 60)}
+
+
+def quantity_value(q, milli=False):
+    """resource.Quantity's Value() / MilliValue() of a canonical quantity string: the exact amount,
+    rounded up (apimachinery/pkg/api/resource/quantity.go ScaledValue rounds toward +infinity)."""
+    from fractions import Fraction
+    m = re.fullmatch(r"([+-]?[0-9.]+)(?:[eE]([+-]?\d+)|(Ki|Mi|Gi|Ti|Pi|Ei|[numkMGTPE])?)", q.strip())
+    if not m:
+        raise Unknown(f"quantity {q!r}")
+    v = Fraction(m.group(1))
+    if m.group(2) is not None:
+        v *= Fraction(10) ** int(m.group(2))
+    else:
+        base, exp = _QSUFFIX[m.group(3) or ""]
+        v *= Fraction(base) ** exp
+    if milli:
+        v *= 1000
+    return -((-v.numerator) // v.denominator)
+
+
 def lower_camel(name):
     if name.isupper():
         return name.lower()
@@ -667,6 +690,10 @@ class Evaluator:
                 return Status(code=vals[0], reasons=vals[1:])
             if name in ("fwk.AsStatus",):
                 return Status(code=1, reasons=[])
+            if fn[2] in ("MilliValue", "Value") and not args:  # resource.Quantity methods on a parsed quantity
+                q = self.ev(fn[1], env)
+                if isinstance(q, (str, int)):
+                    return quantity_value(str(q), milli=fn[2] == "MilliValue")
             recv = self.ev(fn[1], env) if name is None or not name.split(".")[0] in ("st", "ptr", "fwk") else None
             if recv is None and name is not None and name.split(".")[0] in self.consts_pkgs():
                 raise Unknown(name)

@@ -1,4 +1,5 @@
 """Runs the golden fixtures (tests/golden/*.json) against any ksg.h backend."""
+import ctypes as C
 import glob
 import json
 import os
@@ -56,6 +57,8 @@ def run_case(make_backend, case):
         except KsgError as ex:
             return [f"config rejected but the reference accepts it: {ex}"]
         return []
+    if case["kind"] == "pod_resources":
+        return run_pod_resources_case(make_backend, case)
     b = build(make_backend, case)
     if case["kind"] == "events":
         errs = run_events_case(b, case)
@@ -223,4 +226,84 @@ def run_events_case(b, case):
         except KsgError as e:
             if not op.get("error"):
                 errs.append(f"op {i}: {kind} failed: {e}")
+    return errs
+
+
+RES_KEYS = ("cpu", "memory", "ephemeral-storage")
+
+
+def debug_pod_resources(lib, prefix, pod):
+    """<prefix>debug_pod_resources: CalculateResource [cpu, memory, eph, non0 cpu, non0 mem] + Fit's request."""
+    f = getattr(lib, prefix + "debug_pod_resources")
+    f.restype = C.c_int
+    f.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_int64), C.c_int32]
+    b = json.dumps(pod).encode()
+    out = (C.c_int64 * 8)()
+    rc = f(b, len(b), out, 8)
+    if rc != 8:
+        raise KsgError(f"{prefix}debug_pod_resources: rc={rc}")
+    return list(out)
+
+
+def pod_resources_mismatches(v, case):
+    """The decoded requests of a pod_resources case against its want (see make_fixtures_i.py's views)."""
+    w = case["want"]
+    if case["view"] in ("calc", "status"):
+        got = dict(zip(RES_KEYS + ("non0_cpu", "non0_mem"), v[:5]))
+    else:
+        got = dict(zip(RES_KEYS, v[5:8]))
+    return [f"{k} {got[k]} != {w[k]}" for k in w if got[k] != w[k]]
+
+
+def _qty(key, v):
+    return f"{v}m" if key == "cpu" else str(v)
+
+
+def run_pod_resources_case(make_backend, case):
+    """The requests a pod amounts to, decoded and then as the evaluation sees them:
+    calc / status -- the pod bound to a node: a probe pod asking for allocatable - want of one resource
+    fits (NodeResourcesFit), one asking for one unit more does not, so the node's Requested column (the
+    device mirror, for the device backend) is exactly want; spec -- the pod itself to schedule: it fits
+    a node whose allocatable is want and not one with one unit less (Fit's PreFilter request)."""
+    b = make_backend({})
+    errs = pod_resources_mismatches(debug_pod_resources(b.lib, b.prefix, case["pod"]), case)
+    w = case["want"]
+    big = {"cpu": 10 ** 9, "memory": 2 ** 50, "ephemeral-storage": 2 ** 50}
+
+    def node(name, alloc):
+        return {"metadata": {"name": name, "labels": {"kubernetes.io/hostname": name}},
+                "status": {"allocatable": dict({k: _qty(k, alloc[k]) for k in RES_KEYS}, pods="110")}}
+
+    def probe(key, amount):
+        return {"metadata": {"name": f"probe-{key}-{amount}", "namespace": "default", "uid": f"probe-{key}-{amount}"},
+                "spec": {"containers": [{"name": "p", "resources": {"requests": {key: _qty(key, amount)}}}]}}
+
+    if case["view"] in ("calc", "status"):
+        alloc = {k: w[k] + {"cpu": 1000, "memory": 2 ** 30, "ephemeral-storage": 2 ** 30}[k] for k in RES_KEYS}
+        b.add_node(node("n0", alloc))
+        bound = json.loads(json.dumps(case["pod"]))
+        bound["spec"]["nodeName"] = "n0"
+        b.add_pod(bound)
+        for k in RES_KEYS:
+            for extra, want_code in ((0, 0), (1, 2)):
+                h = b.compile(probe(k, alloc[k] - w[k] + extra))
+                _, codes, _ = b.run_filter_plugin(h, "NodeResourcesFit")
+                b.release(h)
+                if (codes[0] == 0) != (want_code == 0):  # a failure is 2, or 3 past the allocatable itself
+                    errs.append(f"bound: probe {k} +{extra} code {codes[0]} (Requested {k} != {w[k]})")
+    else:
+        nodes = [("fit", {k: w[k] for k in RES_KEYS})]
+        nodes += [(f"short-{k}", dict(big, **{k: w[k] - 1})) for k in RES_KEYS if w[k] > 0]
+        for name, alloc in nodes:
+            b.add_node(node(name, {k: (alloc[k] if k in alloc else big[k]) for k in RES_KEYS}))
+        names = b.node_names()
+        h = b.compile(case["pod"])
+        _, codes, _ = b.run_filter_plugin(h, "NodeResourcesFit")
+        b.release(h)
+        by = dict(zip(names, codes))
+        for name, _ in nodes:
+            want_code = 0 if name == "fit" else 2
+            if (by[name] == 0) != (want_code == 0):
+                errs.append(f"Fit request: node {name} code {by[name]} != {want_code}")
+    b.close()
     return errs

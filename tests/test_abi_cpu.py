@@ -84,6 +84,26 @@ def test_no_kernel_uses_scratch(tmp_path):
     assert not used, used
 
 
+def test_pod_resources_decode_matches_reference_vectors():
+    """The library's host decode of a pod's requests (ksg_debug_pod_resources: CalculateResource with the
+    in-place resize status resources, and Fit's spec-only request) against the reference's own vectors
+    (tests/golden/pod_resources.json, make_fixtures_i.py) -- no device needed; the device check of the
+    same vectors (the mirror's Requested column) is test_golden_vectors_on_device."""
+    import json
+
+    from golden_runner import debug_pod_resources, pod_resources_mismatches
+    lib = C.CDLL(_ensure_built())
+    here = os.path.dirname(os.path.abspath(__file__))
+    cases = json.load(open(os.path.join(here, "golden", "pod_resources.json")))["cases"]
+    assert len(cases) >= 30
+    bad = {}
+    for c in cases:
+        errs = pod_resources_mismatches(debug_pod_resources(lib, "ksg_", c["pod"]), c)
+        if errs:
+            bad[c["name"]] = errs
+    assert not bad, bad
+
+
 def test_log_table_matches_oracle_go_log_bit_for_bit():
     """The table PodTopologySpread scores read on the device (Cluster::log_tab) against the
     oracle's math.Log restatement, for every log(size + 2) a 100k-node cluster can need

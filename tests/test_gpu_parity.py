@@ -8,7 +8,7 @@ import random
 
 import pytest
 
-from fuzz_gen import namespaces, rand_cluster, rand_pod
+from fuzz_gen import add_resize_status, namespaces, rand_cluster, rand_pod
 from golden_runner import load_cases, run_case
 from oracle_binding import oracle
 
@@ -76,6 +76,49 @@ def test_batch_matches_sequential_oracle(native, seed):
     for k, p in enumerate(pods):
         ro, _ = o.schedule_one(o.compile(p), assume=True)
         assert rs[k].as_tuple() == ro.as_tuple(), f"seed {seed} pod {k}"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_resized_bound_pods_match_oracle(native, seed):
+    """Bound pods mid-resize (InPlacePodVerticalScaling, GA: container / pod-level status resources,
+    allocatedResources, Deferred / Infeasible / InProgress conditions) count as CalculateResource counts
+    them (framework/types.go:1035-1076 with helpers.go:193-320) in the device mirror: a stream scheduled
+    on small nodes, where Fit and the allocation scores depend on those requests, matches the oracle pod by
+    pod, through batches (the persistent loop) and single calls; resized pods are also removed and re-added
+    between batches; the mirror equals the cache."""
+    rng, cfg, nodes, existing, names = rand_cluster(4200 + seed, n_nodes=[64, 300, 700, 1100][seed], n_existing=0,
+                                                    cfg_index=[0, 1, 3, 2][seed])
+    for n in nodes:  # small nodes: the resized pods' requests decide Fit
+        n["status"]["allocatable"]["cpu"] = rng.choice(["4", "6", "8"])
+        n["status"]["allocatable"]["memory"] = rng.choice(["8Gi", "12Gi", "16Gi"])
+    existing = []
+    for k in range(len(nodes) * 2):
+        p = add_resize_status(rng, rand_pod(rng, 300000 + k, names, topology=False))
+        p["spec"].get("affinity", {}).pop("nodeAffinity", None)
+        p["spec"]["nodeName"] = rng.choice(names)
+        existing.append(p)
+    g, o = _pair(native, cfg, nodes, existing)
+    assert g.compare_mirror(sync=True) == (0, -1)
+    k = 0
+    for rnd in range(4):
+        pods = [rand_pod(rng, 10 * k + j, names, topology=False) for j in range(60)]
+        if rnd % 2:  # a few incoming pods carry status too (Fit ignores it, the scores read it)
+            pods = [add_resize_status(rng, p) if rng.random() < 0.3 else p for p in pods]
+        rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+        for j, p in enumerate(pods):
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rs[j].as_tuple() == ro.as_tuple(), f"seed {seed} round {rnd} pod {j}"
+        for j in range(8):  # single calls
+            p = rand_pod(rng, 10 * k + 100 + j, names, topology=False)
+            rg, _ = g.schedule_one(g.compile(p), assume=True)
+            ro, _ = o.schedule_one(o.compile(p), assume=True)
+            assert rg.as_tuple() == ro.as_tuple(), f"seed {seed} round {rnd} single {j}"
+        for p in rng.sample(existing, 5):  # a resized pod's delete and re-add
+            for b in (g, o):
+                b.remove_pod(p["metadata"]["uid"])
+                b.add_pod(p)
+        k += 1
+        assert g.compare_mirror(sync=True) == (0, -1)
 
 
 def test_ties_follow_heap_preorder(native):
