@@ -495,13 +495,32 @@ struct alignas(16) RingResult {
   uint32_t seq, pad[3];
   DevResult r;
 };
+// k_agg_loop's resident instance also takes the pod's pod-table entry through the ring (entry[q %
+// kRingSlots], its size in ctl bits [48, 64)): the owner of the chosen node writes it into the device
+// pod table when it commits the pod, so the pods after it count it.  The host laid the
+// entry out in its shadow (Cluster::pod_table_put) and checked that the device arrays hold it.
+struct RingEntry {
+  int32_t slot;                // pod-table slot (-1: none; nothing is written)
+  int32_t ns;
+  uint32_t flags, lbl_off, lbl_cnt;
+  int32_t tpool_off, tpool_cnt;  // term-pool words [tpool_off, tpool_off + tpool_cnt)
+  int32_t nterms;
+  // followed by unsigned long long labels[lbl_cnt], int32_t tpool[tpool_cnt] (padded to 8 bytes),
+  // RingTerm terms[nterms]
+};
+struct RingTerm {
+  int32_t j, pad;  // term-table index
+  DTerm d;
+};
+constexpr int kRingEntryBytes = 8192;
 struct alignas(128) PodRing {
-  unsigned long long ctl;  // [host] {pods posted | bytes << 32} or kRingStop
+  unsigned long long ctl;  // [host] {pods posted | program bytes << 32 | entry bytes << 48} or kRingStop
   uint32_t pad0[30];
   uint32_t exited;         // [device] 1: the loop left on its own (idle / pod limit)
   uint32_t pad1[31];
   RingResult res[kRingSlots];
   alignas(128) uint8_t blob[kRingSlots][kBlobLds];
+  alignas(128) uint8_t entry[kRingSlots][kRingEntryBytes];
 };
 
 struct LoopView {
@@ -588,6 +607,9 @@ struct AggView {
   // [nwg][spill_pods + spill_terms] in HBM, this rank's workgroups
   uint32_t* spill;
   int32_t spill_pods, spill_terms;
+  // resident instance (k_agg_loop<false, true, true>): pods through the ring, one run per pod
+  PodRing* ring;
+  unsigned long long ring_idle;  // s_memrealtime ticks without a pod before the launch ends by itself
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -1647,30 +1647,35 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
 
 // Resident mode: wait for pod q in the ring (one thread).  Returns the pod's program size, or -1 when
 // the launch ends (the host's stop, the pod limit, or lv.ring_idle ticks without a pod).
-__device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
-  if (q >= lv.npods) return -1;
+// (ring_wait_p: the ctl word's bits [32, 64), i.e. the program bytes and, for k_agg_loop, the entry bytes << 16)
+__device__ __forceinline__ int ring_wait_p(PodRing* ring, int q, int npods, unsigned long long idle) {
+  if (q >= npods) return -1;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   // relaxed polls: the ring is coherent host memory, and a system-scope acquire on every poll would
   // invalidate the caches under the other workgroups' work; the program is read after the doorbell's value
   // is known (control dependence), with system-scope loads that bypass the device caches (stage_ring)
   for (uint32_t spins = 0;; ++spins) {
-    const unsigned long long v = __hip_atomic_load(&lv.ring->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long v = __hip_atomic_load(&ring->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t posted = (uint32_t)v;
     if (posted == kRingStop) return -1;
     if (posted > (uint32_t)q) return (int)(v >> 32);
-    if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > lv.ring_idle) {
-      if (blockIdx.x == 0) __hip_atomic_store(&lv.ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > idle) {
+      if (blockIdx.x == 0) __hip_atomic_store(&ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return -1;
     }
     __builtin_amdgcn_s_sleep(2);
   }
 }
+__device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
+  const int v = ring_wait_p(lv.ring, q, lv.npods, lv.ring_idle);
+  return v < 0 ? v : (v & 0xffff);
+}
 // Resident mode: pod q's result to the host (the committing thread, after commit_result)
 // The record goes to host memory with system-scope (write-through) stores; once they have completed
 // (vmcnt), the sequence word follows in the same PCIe posted-write stream.  (A system-scope release here
 // would write the whole L2 back first.)
-__device__ __forceinline__ void ring_post(const LoopView& lv, int q, const DevResult& r) {
-  RingResult& o = lv.ring->res[q % kRingSlots];
+__device__ __forceinline__ void ring_post_p(PodRing* ring, int q, const DevResult& r) {
+  RingResult& o = ring->res[q % kRingSlots];
   static_assert(sizeof(DevResult) % 8 == 0, "DevResult is stored as 8-byte words");
   const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&r);
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(&o.r);
@@ -1680,6 +1685,7 @@ __device__ __forceinline__ void ring_post(const LoopView& lv, int q, const DevRe
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&o.seq, (uint32_t)(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void ring_post(const LoopView& lv, int q, const DevResult& r) { ring_post_p(lv.ring, q, r); }
 
 // NormalizeScore + weights for the loop's plugin set (TaintToleration, NodeAffinity normalised;
 // Fit / BalancedAllocation / ImageLocality already in `fixed`) -- framework.go:1409-1452
@@ -2664,10 +2670,34 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
   }
 }
 
+// k_agg_loop's resident mode: the committed pod's pod-table entry (RingEntry, staged in LDS) into the
+// device pod table -- what Cluster::upload_pod_table would write for it -- so that the pods after it
+// count it (the owner of its node appends it to its lists).  One thread; pod_node is commit_result's.
+__device__ __forceinline__ void apply_entry(const MirrorView& m, const uint8_t* e) {
+  const RingEntry& h = *reinterpret_cast<const RingEntry*>(e);
+  if (h.slot < 0) return;
+  const size_t s = (size_t)h.slot;
+  const_cast<int32_t*>(m.pod_ns)[s] = h.ns;
+  const_cast<uint32_t*>(m.pod_flags)[s] = h.flags;
+  const_cast<uint32_t*>(m.pod_lbl_off)[s] = h.lbl_off;
+  const_cast<uint32_t*>(m.pod_lbl_cnt)[s] = h.lbl_cnt;
+  const unsigned long long* lb = reinterpret_cast<const unsigned long long*>(e + sizeof(RingEntry));
+  unsigned long long* pool = const_cast<unsigned long long*>(m.lbl_pool) + h.lbl_off;
+  for (uint32_t k = 0; k < h.lbl_cnt; ++k) pool[k] = lb[k];
+  const int32_t* tw = reinterpret_cast<const int32_t*>(lb + h.lbl_cnt);
+  int32_t* tp = const_cast<int32_t*>(m.term_pool) + h.tpool_off;
+  for (int32_t k = 0; k < h.tpool_cnt; ++k) tp[k] = tw[k];
+  const RingTerm* rt = reinterpret_cast<const RingTerm*>(tw + ((h.tpool_cnt + 1) & ~1));
+  DTerm* terms = const_cast<DTerm*>(m.terms);
+  for (int32_t k = 0; k < h.nterms; ++k) terms[rt[k].j] = rt[k].d;
+}
+
 // SHARD: node-sharded over the device exchange (av.world > 1); the unsharded instance compiles none of it.
 // PTSS: some pod of the run has PodTopologySpread scoring (ScheduleAnyway constraints); the instance
 // without it leaves that code out (its registers and issue slots cost the other pods ~1 us).
-template <bool SHARD, bool PTSS>
+// RING: the resident instance (ksg_schedule_one of PodTopologySpread / InterPodAffinity pods):
+// pods through av.ring, each a run of its own -- gathered when it arrives, no fold, no staging ahead.
+template <bool SHARD, bool PTSS, bool RING = false>
 __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
@@ -2717,6 +2747,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ int s_p2n;
   __shared__ int64_t s_mx[4];
   __shared__ uint32_t s_pmult[kAggMaxCons];  // DoNotSchedule: present domains at the minimum
+  __shared__ int s_ring_bytes;                // resident mode: {program bytes | entry bytes << 16}, -1: the end
   const int w = blockIdx.x, G = av.nwg;
   const int P = SHARD ? av.world * G : G, gid = SHARD ? av.rank * G + w : w;  // participants (rank-major), mine
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
@@ -3152,7 +3183,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_core.ihi[kk][tt] = c.ihi;
     lds_put_dynamic(s_core, kk, tt, c);
   }
-  for (int k = t; k < av.npods; k += kAggThreads) s_off[k] = b.desc_off[av.first_pod + k];
+  if (!RING)
+    for (int k = t; k < av.npods; k += kAggThreads) s_off[k] = b.desc_off[av.first_pod + k];
   if (t == 0) {
     s_np = 0;
     s_nt = 0;
@@ -3183,8 +3215,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       if (k < tcap) put_term(k, ((uint32_t)j << 9) | (uint32_t)(n - nlo));
     }
   }
-  if (av.npods > 0) stage_prog(0, t, kAggThreads);
-  if (av.npods > 1) stage_prog(1, t, kAggThreads);
+  if (!RING && av.npods > 0) stage_prog(0, t, kAggThreads);
+  if (!RING && av.npods > 1) stage_prog(1, t, kAggThreads);
   __syncthreads();
   if (s_np > pcap || s_nt > tcap) {  // host-checked; never taken
     if (t == 0) fail(0xfffffffeu);
@@ -3201,7 +3233,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     __syncthreads();
     if (!s_ok) return;
   }
-  if (av.npods > 0) {
+  if (!RING && av.npods > 0) {
     aggregate(0, t, kAggThreads, wg_bar);
     if (wave == 0) sweep_z(0);
     __syncthreads();
@@ -3220,6 +3252,35 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   };
 
   for (int q = 0; q < av.npods; ++q) {
+    if constexpr (RING) {
+      // ======== resident mode: pod q from the ring (host memory, bypassing the device caches): its program
+      // into s_blob[q % 3], its pod-table entry into s_blob[(q + 1) % 3]; then its counts ========
+      if (t == 0) s_ring_bytes = ring_wait_p(av.ring, q, av.npods, av.ring_idle);
+      __syncthreads();
+      const int rb = s_ring_bytes;
+      if (rb < 0) return;
+      {
+        const int pw8 = (rb & 0xffff) / 8, ew8 = (rb >> 16) / 8;
+        const unsigned long long* ps_ = reinterpret_cast<const unsigned long long*>(av.ring->blob[q % kRingSlots]);
+        const unsigned long long* es_ = reinterpret_cast<const unsigned long long*>(av.ring->entry[q % kRingSlots]);
+        unsigned long long* pd = reinterpret_cast<unsigned long long*>(s_blob[q % 3]);
+        unsigned long long* ed = reinterpret_cast<unsigned long long*>(s_blob[(q + 1) % 3]);
+        for (int k = t; k < pw8 + ew8; k += kAggThreads) {
+          if (k < pw8) pd[k] = __hip_atomic_load(ps_ + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          else ed[k - pw8] = __hip_atomic_load(es_ + (k - pw8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (t == 0 && ew8 == 0) reinterpret_cast<RingEntry*>(ed)->slot = -1;
+      }
+      __syncthreads();
+      aggregate(q, t, kAggThreads, wg_bar);
+      if (wave == 0) sweep_z(q);
+      __syncthreads();
+      if (!s_ok) return;
+      load_totals(q, t, kAggThreads);
+      __syncthreads();
+      minima(q);
+      __syncthreads();
+    }
     if (q == av.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
       if (t == 0) fail((uint32_t)q);
       return;
@@ -3228,7 +3289,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     const uint8_t* base = s_blob[q % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
     PodStats* ps = b.stats + pod;
-    const bool more = q + 1 < av.npods;
+    const bool more = !RING && q + 1 < av.npods;
     const bool sp1 = more && spec(*reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3]));
     // pod q+1's counts are defined as pod q's (host: DF_AGG_SAME): they are q's counts plus q's placement, so
     // nothing is gathered for it -- the fold below runs on the counts in LDS, then its minima are recomputed
@@ -3610,7 +3671,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           s_pend_ls = -1;
           if (okb) {
             if (F == 0) {
-              if (w == 0) commit_result(m, b, base, d, ps, pod, 0, -1, gbest, nullptr, (int)ipa_any);
+              if (w == 0) {
+                commit_result(m, b, base, d, ps, pod, 0, -1, gbest, nullptr, (int)ipa_any);
+                if constexpr (RING) ring_post_p(av.ring, q, b.results[pod]);
+              }
             } else if (gnode >= nlo && gnode < nhi) {
               const int ls = gnode - nlo;
               if (d.flags & DF_ASSUME) {
@@ -3619,9 +3683,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
                 commit_result(m, b, base, d, ps, pod, F, gnode, gbest, &c, (int)ipa_any);
                 lds_put_dynamic(s_core, ls / kBlock, ls % kBlock, c);
                 if (d.slot >= 0) s_pend_ls = ls;
+                if constexpr (RING) apply_entry(m, s_blob[(q + 1) % 3]);
               } else {
                 commit_result(m, b, base, d, ps, pod, F, gnode, gbest, nullptr, (int)ipa_any);
               }
+              if constexpr (RING) ring_post_p(av.ring, q, b.results[pod]);
             }
           }
           // the chosen node and its eligibility for the fold, to the gathering group
@@ -3669,7 +3735,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
         }
       }
-      if (q + 2 < av.npods) stage_prog(q + 2, gt, gn);  // s_blob[(q+2)%3] held pod q-1
+      if (!RING && q + 2 < av.npods) stage_prog(q + 2, gt, gn);  // s_blob[(q+2)%3] held pod q-1
     }
     __syncthreads();
     if (!s_ok) return;
@@ -3745,6 +3811,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         minima(q + 1);
         __syncthreads();
       }
+    } else if (RING) {
+      // the next pod arrives through the ring: pod q joins its node owner's lists now, and its entry
+      // (written by the owner's committing thread) is read from L2 by the pods after it
+      if (t == 0 && s_pend_ls >= 0) append(q, s_pend_ls);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     stamp(q, 8);
   }
@@ -3963,7 +4036,9 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
     else
       hipLaunchKernelGGL(kern, dim3(av.nwg), dim3(kAggThreads), 0, s, m, b, av);
   };
-  if (av.world > 1) {
+  if (av.ring) {
+    go(k_agg_loop<false, true, true>);  // the resident instance (unsharded)
+  } else if (av.world > 1) {
     go(k_agg_loop<true, true>);  // (the sharded instance without PTSS spills registers: not built)
   } else {
     if (av.ptss) go(k_agg_loop<false, true>);
@@ -4002,6 +4077,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop<false, false>),
                       reinterpret_cast<const void*>(&k_agg_loop<false, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<true, true>),
+                      reinterpret_cast<const void*>(&k_agg_loop<false, true, true>),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);

@@ -236,7 +236,7 @@ int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* r
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
-    if (!eval && (flags & KSG_FLAG_ASSUME)) {  // the resident loop (node-local pods), else the launch path
+    if (!eval && (flags & KSG_FLAG_ASSUME)) {  // a resident loop (k_sched_loop / k_agg_loop), else the launch path
       bool handled = false;
       const int rc = ctx->engine->schedule_resident(it->second, handle, result, &handled);
       if (handled) return with_err(ctx, rc);

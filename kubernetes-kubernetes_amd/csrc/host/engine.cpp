@@ -2538,6 +2538,8 @@ int Engine::run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* n
 // half that, so a loop never outlives its process.
 // ===================================================================================================
 constexpr int kResidentIdleMs = 40;
+// k_agg_loop's resident launch: own affinity terms its pods may append to the lists (spill-row budget)
+constexpr int kRingTermBudget = 4096;
 
 int Engine::resident_stop() {
   if (c->cfg.loop_stamps && res_prof_[4] > 0) {  // where a single-pod call's time went (us per call)
@@ -2559,7 +2561,8 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
   if (comm || !c->cfg.resident_loop || !c->cfg.persistent_loop) return KSG_OK;
   const int32_t N = (int32_t)c->order().size();
   if (N == 0) return KSG_OK;
-  // the loop's geometry (run_batch's, unsharded)
+  // the loops' geometry (run_batch's, unsharded): k_sched_loop's GS workgroups of `unit` nodes, and
+  // k_agg_loop's G workgroups of 256-node blocks
   const int NB = (N + kBlock - 1) / kBlock;
   const int cus = cu_count > 0 ? cu_count : 256;
   int GS = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128, unit = 256;
@@ -2573,9 +2576,15 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       unit = 128;
     }
   }
-  if ((int64_t)GS * kLoopMaxBlk * unit < (int64_t)NB * kBlock) return KSG_OK;
-  if ((int64_t)GS > (int64_t)cus * loop_occ[unit == 128 ? 0 : 1]) return KSG_OK;  // residency (run_batch)
-  if ((int64_t)c->taint_max_per_node >= ((int64_t)1 << 24) - 1) return KSG_OK;
+  const bool taint_ok = (int64_t)c->taint_max_per_node < ((int64_t)1 << 24) - 1;
+  const bool sched_geo = taint_ok && (int64_t)GS * kLoopMaxBlk * unit >= (int64_t)NB * kBlock &&
+                         (int64_t)GS <= (int64_t)cus * loop_occ[unit == 128 ? 0 : 1];  // residency (run_batch)
+  int G = c->cfg.loop_wg > 0 ? c->cfg.loop_wg : 128;
+  G = std::min(std::max(G, (NB + kLoopMaxBlk - 1) / kLoopMaxBlk), std::min(std::max(NB, 1), std::min(cus, 256)));
+  const bool agg_geo = taint_ok && c->cfg.agg_loop && (int64_t)G * kLoopMaxBlk >= NB &&
+                       (int64_t)G <= (int64_t)cus * loop_occ[2] && c->pt_node.size() < ((size_t)1 << 23) &&
+                       c->tt.size() < ((size_t)1 << 23);
+  if (!sched_geo && !agg_geo) return KSG_OK;
   // PreFilter / PreScore on the host, as run_batch's compile_upto
   const auto T0 = clk::now();
   CompiledPod cp;
@@ -2585,7 +2594,18 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     return rc;
   }
   if (cp.prefilter_error) cp.error = true;
-  if (!cp.error && !cp.prefilter_reject && (!loop_ok(cp) || cp.blob.size() % 16 != 0)) {
+  // which resident loop takes the pod: node-local pods k_sched_loop (or a running k_agg_loop, which takes
+  // them too), PodTopologySpread / InterPodAffinity pods k_agg_loop with their pod-table entry
+  alignas(16) static thread_local uint8_t entry[kRingEntryBytes];
+  size_t entry_bytes = 0;
+  int kind = 0;
+  if (!cp.error && !cp.prefilter_reject && cp.blob.size() % 16 == 0) {
+    const bool sched_ok = sched_geo && loop_ok(cp);
+    const bool agg_ok = agg_geo && agg_loop_ok(cp) && cp.own_terms <= 4 * kAggMaxTerms;
+    if (agg_ok && (!sched_ok || (res_running_ && res_kind_ == 2))) kind = 2;
+    else if (sched_ok) kind = 1;
+  }
+  if (!cp.error && !cp.prefilter_reject && kind == 0) {
     c->pod_table_drop(cp.slot);  // not a resident-loop pod: the launch path compiles it again
     return KSG_OK;
   }
@@ -2615,12 +2635,38 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     c->reserve_ports(extra);
   }
   hipStream_t s = c->stream;
-  // the running launch sees the mirror as it is, or it stops
-  if (res_running_ && (c->mirror_pending() || res_q_ >= kLoopMaxPods || GS != res_gs_ || unit != res_unit_ ||
+  if (kind == 2) {
+    // the pod's pod-table entry, which the loop writes into the device table when it commits the pod:
+    // it must fit the ring and the device arrays as the last upload sized them, else the table goes up
+    // again before a new launch
+    entry_bytes = cp.slot >= 0 ? c->ring_entry(cp.slot, entry, kRingEntryBytes) : 0;
+    if (cp.slot >= 0 && entry_bytes == 0) {
+      if ((rc = resident_stop())) return fail(rc);
+      if ((rc = c->ensure_mirror(true))) return fail(rc);
+      entry_bytes = c->ring_entry(cp.slot, entry, kRingEntryBytes);
+      if (entry_bytes == 0) {  // larger than the ring's entry area: the launch path takes it
+        c->pod_table_drop(cp.slot);
+        c->next_start = ns_before;
+        *handled = false;
+        return KSG_OK;
+      }
+    }
+  }
+  // the running launch sees the mirror as it is, or it stops (so does a launch of the other kind)
+  if (res_running_ && (c->mirror_pending() || res_q_ >= kLoopMaxPods || res_kind_ != kind ||
+                       (kind == 1 && (GS != res_gs_ || unit != res_unit_)) || (kind == 2 && G != res_gs_) ||
+                       (kind == 2 && res_terms_ + cp.own_terms > kRingTermBudget) ||
                        clk::now() - res_last_ > std::chrono::milliseconds(kResidentIdleMs / 2)))
     if ((rc = resident_stop())) return fail(rc);
   if (!res_running_) {
-    if ((rc = c->ensure_mirror(false))) return fail(rc);
+    if ((rc = c->ensure_mirror(kind == 2))) return fail(rc);
+    if (kind == 2 && cp.slot >= 0) {  // (the upload may have moved the label pool: the entry again)
+      entry_bytes = c->ring_entry(cp.slot, entry, kRingEntryBytes);
+      if (entry_bytes == 0) {
+        c->err = "resident loop: the pod-table entry does not fit after the upload";
+        return fail(KSG_EDEVICE);
+      }
+    }
     if (!ring_) {
       void* hp = nullptr;
       if (hipHostMalloc(&hp, sizeof(PodRing), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
@@ -2636,38 +2682,98 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       ring_dev_ = (PodRing*)dp;
     }
     std::memset((void*)ring_, 0, offsetof(PodRing, blob));
-    if ((rc = gran_setup())) return fail(rc);
     if ((rc = ensure(d_fail, kFailBytes))) return fail(rc);
     if ((rc = ensure_scratch(256, kLoopMaxPods, false, 0))) return fail(rc);
     HIPCHK(hipMemsetAsync(d_fail.p, 0, kFailBytes, s));
     HIPCHK(hipMemsetAsync(d_stats.p, 0, d_stats.bytes, s));  // PodStats::ipa_any = 0 for every pod
-    LoopView lv{};
-    lv.first_pod = 0;
-    lv.npods = kLoopMaxPods;
-    lv.nwg = GS;
-    lv.blk0 = 0;
-    lv.nblk = (c->view.n + kBlock - 1) / kBlock;
-    lv.world = 1;
-    lv.rank = 0;
-    if ((rc = next_gran_tag(&lv.tag))) return fail(rc);
-    lv.gran[0] = gran_all[0];
-    lv.fail = (uint32_t*)d_fail.p;
-    lv.give_up_at = -1;
-    lv.wave_map = c->cfg.loop_wave_map;
-    lv.ring = ring_dev_;
-    lv.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;  // s_memrealtime: 100 MHz
-    HIPCHK(launch_sched_loop(c->view, bview(kLoopMaxPods), lv, s, nullptr, nullptr, unit));
+    if (kind == 1) {
+      if ((rc = gran_setup())) return fail(rc);
+      LoopView lv{};
+      lv.first_pod = 0;
+      lv.npods = kLoopMaxPods;
+      lv.nwg = GS;
+      lv.blk0 = 0;
+      lv.nblk = NB;
+      lv.world = 1;
+      lv.rank = 0;
+      if ((rc = next_gran_tag(&lv.tag))) return fail(rc);
+      lv.gran[0] = gran_all[0];
+      lv.fail = (uint32_t*)d_fail.p;
+      lv.give_up_at = -1;
+      lv.wave_map = c->cfg.loop_wave_map;
+      lv.ring = ring_dev_;
+      lv.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;  // s_memrealtime: 100 MHz
+      HIPCHK(launch_sched_loop(c->view, bview(kLoopMaxPods), lv, s, nullptr, nullptr, unit));
+      res_gs_ = GS;
+      res_unit_ = unit;
+    } else {
+      if ((rc = agg_setup())) return fail(rc);
+      // every workgroup's pod / term lists: its nodes' pods and terms now, plus what the launch can append
+      // (kLoopMaxPods pods and kRingTermBudget terms), past kAggPods / kAggTerms in its HBM spill rows
+      std::vector<int32_t> np((size_t)G, 0), nt((size_t)G, 0);
+      auto wg_of = [&](int32_t nd) { return (int)((int64_t)(nd / kBlock) * G / NB); };
+      auto owner = [&](int32_t nd) {  // the workgroup whose block range [NB w / G, NB (w + 1) / G) holds nd
+        int w = wg_of(nd);
+        while (w > 0 && (int64_t)NB * w / G > nd / kBlock) --w;
+        while (w + 1 < G && (int64_t)NB * (w + 1) / G <= nd / kBlock) ++w;
+        return w;
+      };
+      for (int32_t nd : c->pt_node)
+        if (nd >= 0 && nd < c->view.n) np[(size_t)owner(nd)]++;
+      for (const DTerm& tm : c->tt) {
+        const int32_t nd = tm.kind >= 0 && tm.owner >= 0 ? c->pt_node[(size_t)tm.owner] : -1;
+        if (nd >= 0 && nd < c->view.n) nt[(size_t)owner(nd)]++;
+      }
+      auto up64 = [](int64_t v) { return v <= 0 ? (int64_t)0 : (v + 63) / 64 * 64; };
+      const int64_t spill_p = up64(*std::max_element(np.begin(), np.end()) + (int64_t)kLoopMaxPods - kAggPods);
+      const int64_t spill_t = up64(*std::max_element(nt.begin(), nt.end()) + (int64_t)kRingTermBudget - kAggTerms);
+      if (spill_p > kAggSpillMax || spill_t > kAggSpillMax) {  // no resident launch: the launch path
+        c->pod_table_drop(cp.slot);
+        c->next_start = ns_before;
+        *handled = false;
+        return KSG_OK;
+      }
+      if ((rc = ensure(d_aspill, (size_t)G * (size_t)(spill_p + spill_t) * 4 + 4))) return fail(rc);
+      HIPCHK(hipMemsetAsync(d_region.p, 0, (size_t)kLoopMaxPods * kAggGWords * 8, s));
+      AggView av{};
+      av.first_pod = 0;
+      av.npods = kLoopMaxPods;
+      av.nwg = G;
+      av.blk0 = 0;
+      av.nblk = NB;
+      av.world = 1;
+      av.rank = 0;
+      if ((rc = next_gran_tag(&av.tag))) return fail(rc);
+      av.gwords = kAggGWords;
+      av.ptss = 1;
+      av.spill = (uint32_t*)d_aspill.p;
+      av.spill_pods = (int32_t)spill_p;
+      av.spill_terms = (int32_t)spill_t;
+      av.debug = c->cfg.agg_debug;
+      av.give_up_at = -1;
+      av.gran = (unsigned long long*)d_agran.p;
+      av.region = (unsigned long long*)d_region.p;
+      av.fail = (uint32_t*)d_fail.p;
+      av.ring = ring_dev_;
+      av.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;
+      HIPCHK(launch_agg_loop(c->view, bview(kLoopMaxPods), av, s, nullptr, nullptr));
+      res_gs_ = G;
+      res_terms_ = 0;
+    }
     res_running_ = true;
+    res_kind_ = kind;
     res_q_ = 0;
-    res_gs_ = GS;
-    res_unit_ = unit;
   }
-  // post the pod, wait for its result
+  // post the pod (and its pod-table entry), wait for its result
   const auto T1 = clk::now();
   const int q = res_q_;
   const uint32_t bytes = (uint32_t)cp.blob.size();
   std::memcpy(ring_->blob[q % kRingSlots], cp.blob.data(), bytes);
-  __atomic_store_n(&ring_->ctl, (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)bytes << 32),
+  if (entry_bytes) std::memcpy(ring_->entry[q % kRingSlots], entry, entry_bytes);
+  if (kind == 2) res_terms_ += cp.own_terms;
+  __atomic_store_n(&ring_->ctl,
+                   (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)bytes << 32) |
+                       ((unsigned long long)entry_bytes << 48),
                    __ATOMIC_RELEASE);
   RingResult& rr = ring_->res[q % kRingSlots];
   const auto tw = clk::now();
@@ -2686,16 +2792,19 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       (void)hipStreamSynchronize(s);
       uint32_t f[kFailWords] = {};
       (void)hipMemcpyAsync(f, d_fail.p, kFailBytes, hipMemcpyDeviceToHost, s);
-      std::vector<unsigned long long> row((size_t)res_gs_ * kGran);
-      if (f[0] && ((size_t)f[1] + 1) * row.size() * 8 <= d_gran.bytes)
-        (void)hipMemcpyAsync(row.data(), (const unsigned long long*)d_gran.p + (size_t)f[1] * row.size(), row.size() * 8,
+      const int ng = res_kind_ == 2 ? kAGran : kGran;
+      const DevBuf& gb = res_kind_ == 2 ? d_agran : d_gran;
+      std::vector<unsigned long long> row((size_t)res_gs_ * ng);
+      if (f[0] && ((size_t)f[1] + 1) * row.size() * 8 <= gb.bytes)
+        (void)hipMemcpyAsync(row.data(), (const unsigned long long*)gb.p + (size_t)f[1] * row.size(), row.size() * 8,
                              hipMemcpyDeviceToHost, s);
       (void)hipStreamSynchronize(s);
       c->layout_dirty = true;
       c->mirror_suspect = true;
       c->pods_dirty = true;
       c->err = std::string("resident loop ended without the pod's result") +
-               (f[0] ? " (an exchange granule never arrived: " + give_up_detail(f, row, kGran, 1, res_gs_) + ")"
+               (f[0] ? " (" + (f[1] >= 0xfffffff0u ? "a list check failed" : "an exchange granule never arrived: " +
+                                                                                 give_up_detail(f, row, ng, 1, res_gs_)) + ")"
                      : std::string()) +
                "; the device mirror is rebuilt from the cache";
       return fail(KSG_EDEVICE);
@@ -2724,7 +2833,7 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
   } else {
     c->pod_table_drop(cp.slot);
   }
-  last_kernel = 1;
+  last_kernel = kind == 2 ? 2 : 1;
   if (c->cfg.loop_stamps) {
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     res_prof_[0] += us(T0, T1);

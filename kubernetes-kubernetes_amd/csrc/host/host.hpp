@@ -402,6 +402,11 @@ class Cluster {
   // reserve a slot for `p` (node index -1 until placed); its terms go live with the slot
   int32_t pod_table_put(const PodSpec& p, int32_t node_index);
   void pod_table_drop(int32_t slot);
+  // the term-pool words the last pod_table_put appended (the resident k_agg_loop's RingEntry)
+  int32_t last_tpool_off = 0, last_tpool_cnt = 0;
+  // slot s's pod-table entry as a RingEntry (+ labels, term-pool words, terms) into out; its size, or 0
+  // when it does not fit in cap bytes or in the device arrays as they are (the table must go up again)
+  size_t ring_entry(int32_t s, uint8_t* out, size_t cap) const;
   // lazy: skip the upload (keeping pods_dirty) when the device copy has room for every slot -- the
   // device-side AssumePod only writes pod_node[slot] -- and no pod of the call reads the table
   int upload_pod_table(bool lazy = false);
@@ -616,6 +621,8 @@ class Engine {
   PodRing* ring_dev_ = nullptr;   // its device address
   bool res_running_ = false;
   int res_q_ = 0, res_gs_ = 0, res_unit_ = 0;  // pods posted to the running launch; its geometry
+  int res_kind_ = 0;              // the running launch: 1 k_sched_loop, 2 k_agg_loop (pod-table pods)
+  int64_t res_terms_ = 0;         // k_agg_loop: own affinity terms of the pods posted (its spill rows' budget)
   std::chrono::steady_clock::time_point res_last_{};  // the last result the host took
   uint64_t res_seq_ = 0;          // assumed-pod uid suffix
   double res_prof_[5] = {};       // loopStamps: compile / post / device / settle us, calls

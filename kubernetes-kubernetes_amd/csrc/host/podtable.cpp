@@ -140,6 +140,8 @@ int32_t Cluster::pod_table_put(const PodSpec& p, int32_t node_index) {
   // the terms: their words appended to the term pool, offsets rebased
   const int32_t base = (int32_t)tt_pool.size();
   tt_pool.insert(tt_pool.end(), pre.words.begin(), pre.words.end());
+  last_tpool_off = base;
+  last_tpool_cnt = (int32_t)pre.words.size();
   for (const PodTablePre::Term& t : pre.terms) {
     DTerm d{};
     d.owner = s;
@@ -168,6 +170,49 @@ int32_t Cluster::pod_table_put(const PodSpec& p, int32_t node_index) {
   return s;
 }
 
+
+size_t Cluster::ring_entry(int32_t s, uint8_t* out, size_t cap) const {
+  if (s < 0 || s >= (int32_t)pt_node.size()) return 0;
+  const uint32_t lo = pt_lbl_off[(size_t)s], lc = pt_lbl_cnt[(size_t)s];
+  const std::vector<int32_t>& js = pt_terms[(size_t)s];
+  const size_t tw = ((size_t)last_tpool_cnt + 1) & ~(size_t)1;
+  const size_t bytes = sizeof(RingEntry) + (size_t)lc * 8 + tw * 4 + js.size() * sizeof(RingTerm);
+  if (bytes > cap || bytes % 8 != 0) return 0;
+  // the device arrays must already hold every index the entry writes (as upload_pod_table sized them)
+  int32_t jmax = -1;
+  for (int32_t j : js) jmax = std::max(jmax, j);
+  const size_t ps = ((size_t)s + 1) * 4;
+  if (!pt_dev_[0].p || pt_dev_[0].bytes < ps || pt_dev_[1].bytes < ps || pt_dev_[2].bytes < ps || pt_dev_[3].bytes < ps ||
+      pt_dev_[4].bytes < ps || pt_dev_[5].bytes < ((size_t)lo + lc) * 8 ||
+      pt_dev_[6].bytes < (size_t)(jmax + 1) * sizeof(DTerm) ||
+      pt_dev_[7].bytes < ((size_t)last_tpool_off + (size_t)last_tpool_cnt) * 4)
+    return 0;
+  RingEntry h{};
+  h.slot = s;
+  h.ns = pt_ns[(size_t)s];
+  h.flags = pt_flags[(size_t)s];
+  h.lbl_off = lo;
+  h.lbl_cnt = lc;
+  h.tpool_off = last_tpool_off;
+  h.tpool_cnt = last_tpool_cnt;
+  h.nterms = (int32_t)js.size();
+  uint8_t* o = out;
+  std::memcpy(o, &h, sizeof h);
+  o += sizeof h;
+  std::memcpy(o, pt_pool.data() + lo, (size_t)lc * 8);
+  o += (size_t)lc * 8;
+  std::memset(o, 0, tw * 4);
+  std::memcpy(o, tt_pool.data() + last_tpool_off, (size_t)last_tpool_cnt * 4);
+  o += tw * 4;
+  for (int32_t j : js) {
+    RingTerm r{};
+    r.j = j;
+    r.d = tt[(size_t)j];
+    std::memcpy(o, &r, sizeof r);
+    o += sizeof r;
+  }
+  return bytes;
+}
 
 void Cluster::pod_table_drop(int32_t s) {
   if (s < 0 || s >= (int32_t)pt_node.size()) return;

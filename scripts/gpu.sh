@@ -29,7 +29,7 @@ PYT="python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cache
 for s in "$@"; do
   case $s in
     suite) step suite 900 $PYT tests -m gpu ;;
-    tests=*) f=${s#tests=}; step "tests_$(basename "${f%%::*}" .py)" 600 $PYT "$f" -m gpu -v ;;
+    tests=*) f=${s#tests=}; n=$(basename "$f"); n=${n//[^A-Za-z0-9]/_}; step "tests_${n:0:80}" 600 $PYT "$f" -m gpu -v ;;
     smoke) step smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench=*)
       a=${s#bench=}; wl=${a%%:*}; n=3; [ "$a" != "$wl" ] && n=${a#*:}

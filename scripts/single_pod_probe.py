@@ -1,6 +1,15 @@
 """Latency of one ksg_schedule_one call (the per-pod API a kube-scheduler binding calls from its
-scheduling goroutine) on SchedulingBasic at 5000 nodes: the resident loop (default), the launch path,
-against a ksg_schedule_batch of the same pods.  Prints one JSON line."""
+scheduling goroutine, schedule_one.go:67-192): the resident loops (default: k_sched_loop for node-local
+pods, k_agg_loop for PodTopologySpread / InterPodAffinity pods), the launch path, and a
+ksg_schedule_batch of the same pods.  Prints one JSON line per workload.
+
+  python scripts/single_pod_probe.py [workload ...]     c2 (SchedulingBasic 5000 nodes, default), c2pct0,
+                                                        dts (DefaultTopologySpreading), c4 (TopologySpreading
+                                                        15000 nodes), c3, c4-anti
+  python scripts/single_pod_probe.py stamps [workload]  the resident call's host / device split
+Every resident call's result is checked against the oracle (after timing), so a fast wrong answer
+does not count.
+"""
 import json
 import os
 import sys
@@ -8,37 +17,76 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-kubernetes_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from ksg import synth  # noqa: E402
 from ksg.native import Scheduler  # noqa: E402
-from ksg.synth import scheduling_basic  # noqa: E402
 
 
-def run(cfg, n_pods=2000, batch=False):
-    nodes, init, pods = scheduling_basic(5000, 1000, n_pods + 200)
+def cluster(wl, n_pods):
+    objects = []
+    if wl in ("c2", "c2pct0"):
+        nodes, init, pods = synth.scheduling_basic(5000, 1000, n_pods)
+    elif wl == "dts":
+        nodes, init, pods, objects = synth.default_topology_spreading(5000, 5000, n_pods)
+    elif wl == "c3":
+        nodes, init, pods = synth.scheduling_c3(5000, 5000, n_pods)
+    else:
+        nodes, init, pods = synth.topology_spreading(15000, 15000, n_pods, preferred_anti=wl == "c4-anti")
+    return nodes, init, pods, objects
+
+
+def run(wl, cfg, n_pods=2000, batch=False, check=False):
+    nodes, init, pods, objects = cluster(wl, n_pods + 200)
+    if wl == "c2pct0":
+        cfg = dict(cfg, percentageOfNodesToScore=0)
     s = Scheduler(cfg)
+    for ob in objects:
+        s.upsert_object(ob)
     for n in nodes:
         s.add_node(n)
     for p in init:
         s.add_pod(p)
     hs = [s.compile(p) for p in pods]
-    for h in hs[:200]:  # warm-up
-        s.schedule_one(h, assume=True)
+    got = [s.schedule_one(h, assume=True)[0].as_tuple() for h in hs[:200]]  # warm-up
     t0 = time.perf_counter()
     if batch:
-        s.schedule_batch(hs[200:], assume=True)
+        got += [r.as_tuple() for r in s.schedule_batch(hs[200:], assume=True)]
     else:
         for h in hs[200:]:
-            s.schedule_one(h, assume=True)
+            got.append(s.schedule_one(h, assume=True)[0].as_tuple())
     dt = time.perf_counter() - t0
+    kern = s.kernel_stats()[3]
     s.close()
-    return dt / n_pods * 1e6
+    mism = None
+    if check:
+        from oracle_binding import oracle
+        o = oracle(dict(percentageOfNodesToScore=0) if wl == "c2pct0" else {})
+        for ob in objects:
+            o.upsert_object(ob)
+        for n in nodes:
+            o.add_node(n)
+        for p in init:
+            o.add_pod(p)
+        mism = 0
+        for k, p in enumerate(pods):
+            if o.schedule_one(o.compile(p), assume=True)[0].as_tuple() != got[k]:
+                mism += 1
+    return dt / n_pods * 1e6, kern, mism
 
 
-if sys.argv[1:] == ["stamps"]:  # the resident call's host / device split (printed at the loop's stop)
-    print(json.dumps({"single_resident_us": round(run({"loopStamps": True}), 1)}))
-    sys.exit(0)
-out = {"single_resident_us": round(run({}), 1),
-       "single_resident_pct0_us": round(run({"percentageOfNodesToScore": 0}), 1),
-       "single_launch_us": round(run({"residentLoop": False}), 1),
-       "single_launch_no_loop_us": round(run({"residentLoop": False, "persistentLoop": False}), 1),
-       "batch_us_per_pod": round(run({}, batch=True), 2)}
-print(json.dumps(out))
+def main():
+    args = sys.argv[1:]
+    if args[:1] == ["stamps"]:  # printed at the loop's stop
+        wl = args[1] if len(args) > 1 else "c2"
+        print(json.dumps({"workload": wl, "single_resident_us": round(run(wl, {"loopStamps": True})[0], 1)}))
+        return
+    for wl in args or ["c2"]:
+        us, kern, mism = run(wl, {}, check=True)
+        out = {"workload": wl, "single_resident_us": round(us, 1), "resident_kernel": kern, "oracle_mismatches": mism,
+               "single_launch_us": round(run(wl, {"residentLoop": False})[0], 1),
+               "batch_us_per_pod": round(run(wl, {}, batch=True)[0], 2)}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -801,6 +801,62 @@ def test_resident_single_pod_calls(native):
     assert g.compare_mirror(sync=True)[0] == 0
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_resident_agg_single_pod_calls(native, seed):
+    """ksg_schedule_one of PodTopologySpread / InterPodAffinity pods through the resident k_agg_loop (the
+    pod's program and its pod-table entry through the ring; the owner of the chosen node writes the entry
+    and appends the pod, so the next calls count it), mixed with node-local pods and Service-selected pods
+    (system default spreading), with informer events, a forget, batches and an idle gap in between, and
+    more calls than one launch holds -- pod by pod against the oracle, the mirror against the cache."""
+    import time
+    from fuzz_gen import rand_objects
+    rng, cfg, nodes, existing, names = rand_cluster(9500 + seed, n_nodes=[700, 1500][seed], n_existing=150)
+    g, o = _pair(native, cfg, nodes, existing)
+    for ob in rand_objects(rng):
+        for b in (g, o):
+            b.upsert_object(ob)
+    agg = 0
+
+    def one(pod, tag):
+        nonlocal agg
+        rg, _ = g.schedule_one(g.compile(pod), assume=True)
+        ro, _ = o.schedule_one(o.compile(pod), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"{tag}: {rg.as_tuple()} != {ro.as_tuple()}"
+        agg += g.kernel_stats()[3] == "k_agg_loop"
+        return pod
+
+    hist = [one(rand_pod(rng, k, names), f"pod {k}") for k in range(200)]
+    extra = rand_cluster(9510 + seed, n_nodes=10, n_existing=0)[2]
+    for n in extra:  # informer events between calls: node adds, a bound pod, a pod deleted
+        n["metadata"]["name"] += "-late"
+        n["metadata"].setdefault("labels", {})["kubernetes.io/hostname"] = n["metadata"]["name"]
+        for b in (g, o):
+            b.add_node(n)
+    names = g.node_names()
+    bound = rand_pod(rng, 5000, names)
+    bound["spec"]["nodeName"] = names[7]
+    for b in (g, o):
+        b.add_pod(bound)
+        b.remove_pod(existing[3]["metadata"]["uid"])
+    hist += [one(rand_pod(rng, k, names), f"pod {k} (after events)") for k in range(200, 400)]
+    hg, ho = g.compile(hist[-1]), o.compile(hist[-1])  # a forget
+    rg, _ = g.schedule_one(hg, assume=True)
+    ro, _ = o.schedule_one(ho, assume=True)
+    assert rg.as_tuple() == ro.as_tuple()
+    g.forget(hg)
+    o.forget(ho)
+    batch = [rand_pod(rng, 2000 + k, names) for k in range(40)]
+    rs = g.schedule_batch([g.compile(p) for p in batch], assume=True)
+    for k, p in enumerate(batch):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"batch pod {k}"
+    time.sleep(0.08)  # longer than the loop's idle self-stop
+    for k in range(400, 1300):  # past one launch's kLoopMaxPods
+        one(rand_pod(rng, k, names, topology=k % 3 != 0), f"pod {k}")
+    assert agg > 600, f"only {agg} calls ran in the resident k_agg_loop"
+    assert g.compare_mirror(sync=True)[0] == 0
+
+
 @pytest.mark.parametrize("unit", [128, 256])
 @pytest.mark.parametrize("k", [0, 1, 2, 3, 5, 6])
 def test_sched_loop_sampling_matches_oracle(native, unit, k):
