@@ -68,6 +68,10 @@ def parse():
                     help="threads of the multi-core CPU baseline (the reference's default parallelism is 16)")
     ap.add_argument("--extra-config", default=None,
                     help="JSON merged into the scheduler config (diagnostics / A-B runs, e.g. '{\"loopUnit\": 256}')")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="no sub-records: the default N=1 SchedulingBasic line also carries the 100k-node C5 "
+                         "record (BASELINE configs[4], the metric's second size) measured by a child bench.py")
+    ap.add_argument("--sub-steps", type=int, default=5, help="steps (of --batch pods) of the C5 sub-record")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
@@ -173,6 +177,25 @@ def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), ex
     o.close()
     cpu_baseline.breakdown = breakdown  # us per pod of the last call, by cycle section
     return done / dt, done, dt, results
+
+
+def sub_record(a):
+    """The metric's 100k-node size (BASELINE configs[4], C5: the mixed 100k-node cluster on one GPU) measured
+    by a child bench.py after this one's scheduler is gone: its pods/s, roofline, CPU baseline and parity."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c5", "--steps", str(a.sub_steps),
+           "--warmup", "1", "--batch", str(a.batch), "--cpu-seconds", str(min(a.cpu_seconds, 6.0)), "--no-sub"]
+    if a.no_cpu_baseline:
+        cmd.append("--no-cpu-baseline")
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, timeout=900, text=True)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        sub = json.loads(line)
+    except Exception as e:  # reported, never a silent omission
+        return {"error": f"C5 sub-record failed: {e!r}"}
+    keep = ("metric", "value", "unit", "node_evals_per_s", "steps", "warmup", "ms_per_step", "config", "placed",
+            "roofline", "cpu_baseline", "parity")
+    return {k: sub.get(k) for k in keep}
 
 
 def main():
@@ -387,13 +410,23 @@ def main():
             "placed": placed,
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "avg_kernel_us": round(kms * 1e3, 3),
-                         "algo_bytes_per_launch": round(kbytes, 1)},
+                         "traffic": traffic,
+                         "traffic_unit": ("HBM bytes per pod (one pod of a persistent-loop dispatch: PMC FETCH_SIZE "
+                                          "+ WRITE_SIZE, separate passes, profiles/traffic_*.json)"
+                                          if kname in ("k_sched_loop", "k_agg_loop") else
+                                          "HBM bytes per k_filter_score launch (PMC FETCH_SIZE + WRITE_SIZE)"),
+                         "avg_kernel_us": round(kms * 1e3, 3),
+                         "avg_kernel_us_unit": "per pod" if kname in ("k_sched_loop", "k_agg_loop") else "per launch",
+                         "algo_bytes_per_launch": round(kbytes, 1),
+                         "algo_bytes_unit": "per pod" if kname in ("k_sched_loop", "k_agg_loop") else "per launch"},
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        print(json.dumps(out), flush=True)
     s.close()
+    if rank == 0:
+        if world == 1 and a.workload == "c2" and not a.no_sub and not sharded:
+            out["c5_100k"] = sub_record(a)
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -664,6 +664,26 @@ static bool match_inclusion(const Cycle& cy, const Cycle::TSC& c, const Node& n)
   if (c.taintHonor && find_untolerated_noschedule(n.taints, cy.pod->tolerations)) return false;
   return true;
 }
+// CPU-baseline mode: a PreFilter / PreScore aggregation over every node of the snapshot runs through
+// Parallelizer.Until as the reference's does (podtopologyspread/filtering.go:292, scoring.go:190,
+// interpodaffinity/filtering.go:231,275, scoring.go:209): body(node, chunk-local state) per node on the
+// pool's chunks, then merge(chunk state) in chunk order.  Every merge here is a sum of counts, so the result
+// is the sequential loop's.  Without a pool, the sequential loop over one local state.
+template <class M, class Body, class Merge>
+static void over_all_nodes(ksgo_ctx* c, Body&& body, Merge&& merge) {
+  const int n = (int)c->list.size();
+  if (!c->pool || n < 2) {
+    M acc{};
+    for (auto* ni : c->list) body(ni, acc);
+    merge(acc);
+    return;
+  }
+  std::vector<M> part((size_t)c->pool->chunks(n));
+  c->pool->until(n, [&](int k, int lo, int hi) {
+    for (int i = lo; i < hi; ++i) body(c->list[(size_t)i], part[(size_t)k]);
+  });
+  for (const M& m : part) merge(m);
+}
 static int64_t count_pods_match(const std::vector<PodInfo*>& pods, const Selector& sel, const std::string& ns) {  // :145-160
   if (sel.empty()) return 0;
   int64_t n = 0;
@@ -848,16 +868,21 @@ static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std
       if (cy.ptsF.empty()) { *skip = true; return Status{}; }
       size_t nc = cy.ptsF.size();
       cy.tpMatch.assign(nc, {});
-      for (auto* ni : c->list) {
+      using TpMatch = std::vector<std::map<std::string, int64_t>>;
+      over_all_nodes<TpMatch>(c, [&](NodeInfoO* ni, TpMatch& tm) {  // processNode (filtering.go:255-300)
         const Node& n = ni->node;
-        if (!node_labels_match_spread(n.labels, cy.ptsF)) continue;
+        if (!node_labels_match_spread(n.labels, cy.ptsF)) return;
+        tm.resize(nc);
         for (size_t i = 0; i < nc; ++i) {
           auto& con = cy.ptsF[i];
           if (!match_inclusion(cy, con, n)) continue;
           const std::string& v = n.labels.at(con.key);
-          cy.tpMatch[i][v] += count_pods_match(ni->pods, con.sel, pod.ns);
+          tm[i][v] += count_pods_match(ni->pods, con.sel, pod.ns);
         }
-      }
+      }, [&](const TpMatch& tm) {
+        for (size_t i = 0; i < tm.size(); ++i)
+          for (auto& kv : tm[i]) cy.tpMatch[i][kv.first] += kv.second;
+      });
       cy.critMin.assign(nc, INT32_MAX);
       for (size_t i = 0; i < nc; ++i)
         for (auto& kv : cy.tpMatch[i]) cy.critMin[i] = std::min(cy.critMin[i], kv.second);
@@ -871,31 +896,39 @@ static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std
       for (auto& t : cy.ipaReqAff) merge_ns(c, t);
       for (auto& t : cy.ipaReqAnti) merge_ns(c, t);
       cy.nsLabels = c->ns_labels(pod.ns);
+      using TopoCounts = std::map<std::pair<std::string, std::string>, int64_t>;
       cy.existingAnti.clear();
-      for (auto* ni : c->list) {  // getExistingAntiAffinityCounts :216-240
+      over_all_nodes<TopoCounts>(c, [&](NodeInfoO* ni, TopoCounts& ea) {  // getExistingAntiAffinityCounts :216-240
         for (auto* ep : ni->podsWithRequiredAntiAffinity)
           for (auto& t : ep->reqAnti)
             if (t.matches(pod, cy.nsLabels)) {
               auto it = ni->node.labels.find(t.topologyKey);
-              if (it != ni->node.labels.end()) cy.existingAnti[{t.topologyKey, it->second}] += 1;
+              if (it != ni->node.labels.end()) ea[{t.topologyKey, it->second}] += 1;
             }
-      }
+      }, [&](const TopoCounts& ea) {
+        for (auto& kv : ea) cy.existingAnti[kv.first] += kv.second;
+      });
       cy.affCounts.clear();
       cy.antiCounts.clear();
       if (!cy.ipaReqAff.empty() || !cy.ipaReqAnti.empty()) {  // :246-283
-        for (auto* ni : c->list)
+        using Two = std::pair<TopoCounts, TopoCounts>;
+        over_all_nodes<Two>(c, [&](NodeInfoO* ni, Two& ac) {
           for (auto* ep : ni->pods) {
             if (pod_matches_all_terms(cy.ipaReqAff, ep->pod))
               for (auto& t : cy.ipaReqAff) {
                 auto it = ni->node.labels.find(t.topologyKey);
-                if (it != ni->node.labels.end()) cy.affCounts[{t.topologyKey, it->second}] += 1;
+                if (it != ni->node.labels.end()) ac.first[{t.topologyKey, it->second}] += 1;
               }
             for (auto& t : cy.ipaReqAnti)
               if (t.matches(ep->pod, nullptr)) {
                 auto it = ni->node.labels.find(t.topologyKey);
-                if (it != ni->node.labels.end()) cy.antiCounts[{t.topologyKey, it->second}] += 1;
+                if (it != ni->node.labels.end()) ac.second[{t.topologyKey, it->second}] += 1;
               }
           }
+        }, [&](const Two& ac) {
+          for (auto& kv : ac.first) cy.affCounts[kv.first] += kv.second;
+          for (auto& kv : ac.second) cy.antiCounts[kv.first] += kv.second;
+        });
       }
       if (cy.existingAnti.empty() && cy.ipaReqAff.empty() && cy.ipaReqAnti.empty()) *skip = true;
       return Status{};
@@ -1203,18 +1236,22 @@ static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& n
         cy.tpWeight[i] = go_log((double)(sz + 2));
       }
       cy.reqNA = get_required_node_affinity(pod);
-      for (auto* ni : c->list) {  // processAllNode :155-189
-        if (requireAll && !node_labels_match_spread(ni->node.labels, cy.ptsS)) continue;
+      using TpCounts = std::vector<std::map<std::string, int64_t>>;
+      over_all_nodes<TpCounts>(c, [&](NodeInfoO* ni, TpCounts& tc) {  // processAllNode :155-189
+        if (requireAll && !node_labels_match_spread(ni->node.labels, cy.ptsS)) return;
+        tc.resize(nc);
         for (size_t i = 0; i < nc; ++i) {
           auto& con = cy.ptsS[i];
           if (!match_inclusion(cy, con, ni->node)) continue;
           auto it = ni->node.labels.find(con.key);
           std::string v = it == ni->node.labels.end() ? "" : it->second;
-          auto ct = cy.tpCounts[i].find(v);
-          if (ct == cy.tpCounts[i].end()) continue;
-          ct->second += count_pods_match(ni->pods, con.sel, pod.ns);
+          if (!cy.tpCounts[i].count(v)) continue;  // (the entries initPreScoreState made; read-only here)
+          tc[i][v] += count_pods_match(ni->pods, con.sel, pod.ns);
         }
-      }
+      }, [&](const TpCounts& tc) {
+        for (size_t i = 0; i < tc.size(); ++i)
+          for (auto& kv : tc[i]) cy.tpCounts[i][kv.first] += kv.second;
+      });
       break;
     }
     case KSG_PLUGIN_INTER_POD_AFFINITY: {  // interpodaffinity/scoring.go:128-221
@@ -1238,8 +1275,9 @@ static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& n
           if (it != node.labels.end()) m[t.topologyKey][it->second] += (int64_t)(weight * mult);
         }
       };
-      for (auto* ni : c->list) {
-        if (!hasConstraints && ni->podsWithAffinity.empty()) continue;
+      using TopoScore = std::pair<bool, std::map<std::string, std::map<std::string, int64_t>>>;
+      over_all_nodes<TopoScore>(c, [&](NodeInfoO* ni, TopoScore& acc) {  // processNode (scoring.go:166-199)
+        if (!hasConstraints && ni->podsWithAffinity.empty()) return;
         const auto& podsToProcess = hasConstraints ? ni->pods : ni->podsWithAffinity;
         std::map<std::string, std::map<std::string, int64_t>> ts;
         for (auto* ep : podsToProcess) {  // processExistingPod :81-125
@@ -1253,11 +1291,15 @@ static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& n
           for (auto& t : ep->prefAnti) processTerm(ts, t.term, t.weight, pod, nsl, node, -1);
         }
         if (!ts.empty()) {
-          any = true;
+          acc.first = true;
           for (auto& kv : ts)
-            for (auto& vv : kv.second) cy.topoScore[kv.first][vv.first] += vv.second;
+            for (auto& vv : kv.second) acc.second[kv.first][vv.first] += vv.second;
         }
-      }
+      }, [&](const TopoScore& acc) {
+        any = any || acc.first;
+        for (auto& kv : acc.second)
+          for (auto& vv : kv.second) cy.topoScore[kv.first][vv.first] += vv.second;
+      });
       if (!any) return mk(KSG_CODE_SKIP, 0);
       break;
     }

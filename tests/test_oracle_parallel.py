@@ -51,3 +51,30 @@ def test_parallel_oracle_batch_c2_shape():
     finally:
         seq.close()
         par.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_parallel_aggregations_match_sequential(seed):
+    """The PodTopologySpread / InterPodAffinity PreFilter and PreScore aggregations on the pool (chunk-local
+    counts summed, as the reference's Parallelizer passes at podtopologyspread/filtering.go:292,
+    scoring.go:190, interpodaffinity/filtering.go:231,275, scoring.go:209), with Service-selected pods
+    (system default spreading) and many existing pods: the sequential oracle's results and evaluations."""
+    from fuzz_gen import rand_objects
+    rng, cfg, nodes, existing, names = rand_cluster(40 + seed, n_nodes=400 + 100 * seed, n_existing=400, cfg_index=0)
+    objs = rand_objects(rng)
+    seq = _build(cfg, nodes, existing)
+    par = _build(dict(cfg, cpuThreads=16), nodes, existing)
+    for ob in objs:
+        seq.upsert_object(ob)
+        par.upsert_object(ob)
+    try:
+        for k in range(60):
+            pod = rand_pod(rng, k, names)
+            rs, es = seq.schedule_one(seq.compile(pod), assume=True, evaluate=True)
+            rp, ep = par.schedule_one(par.compile(pod), assume=True, evaluate=True)
+            assert rs.as_tuple() == rp.as_tuple(), f"pod {k}"
+            for key in es:
+                assert es[key] == ep[key], f"pod {k}: eval[{key}]"
+    finally:
+        seq.close()
+        par.close()
