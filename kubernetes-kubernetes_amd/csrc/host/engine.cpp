@@ -1806,7 +1806,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       if (drain()) return KSG_EDEVICE;
       const int r3 = settle_closed();
       if (r3) return r3;
-      for (int j = i; j < (int)pre_slot.size(); ++j) c->pod_table_drop(pre_slot[j]);
+      // pods [i, compiled) took their slots in compile (node-local batches: pre_slot empty) or up front;
+      // pods past them only up front
+      for (int j = i; j < compiled; ++j) c->pod_table_drop(pre_slot.empty() ? cp[j].slot : pre_slot[j]);
+      for (int j = compiled; j < (int)pre_slot.size(); ++j) c->pod_table_drop(pre_slot[j]);
       if (!rot_dev) c->next_start = ns_before[(size_t)i];  // pods [i, b) were compiled, never launched
       return r2;
     }

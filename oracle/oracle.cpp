@@ -2250,7 +2250,11 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
   try {
     mj::Value a = (args_json && args_len) ? mj::parse(args_json, args_len) : mj::Value{};
     offsetIn = a.i64("offset", 0);
-    now = a.i64("now", 0);
+    // GetPodStartTime's time.Now() for pods without status.startTime (preemption/util.go): the call's
+    // "now", or the wall clock read once per call (the product's default too)
+    now = a.has("now") ? a.i64("now", 0)
+                       : (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                             std::chrono::system_clock::now().time_since_epoch()).count();
     pct = a.i64("minCandidateNodesPercentage", 10);
     absn = a.i64("minCandidateNodesAbsolute", 100);
     if (const mj::Value* b = a.has("allNodes")) allNodes = b->kind == mj::Value::Bool && b->b;

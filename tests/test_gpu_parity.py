@@ -121,6 +121,39 @@ def test_resized_bound_pods_match_oracle(native, seed):
         assert g.compare_mirror(sync=True) == (0, -1)
 
 
+def test_deferred_slots_then_pod_table_batch(native):
+    """A node-local pipelined batch takes its pod-table slots in each pod's compile (after the first launch;
+    the device pod_node column keeps room for them), here reusing slots freed by pod deletions; the next
+    batch's pods read the pod table (PodTopologySpread / InterPodAffinity): it must see every placement of
+    the first batch, and the mirror must equal the cache."""
+    from ksg.synth import scheduling_basic, topology_spreading
+    nodes, init, _ = topology_spreading(800, 600, 0)
+    g, o = _pair(native, {}, nodes, init)
+    for p in init[::3]:  # free pod-table slots for the next batch's compiles to reuse
+        for b in (g, o):
+            b.remove_pod(p["metadata"]["uid"])
+    _, _, local = scheduling_basic(800, 0, 700)
+    for k, p in enumerate(local):
+        p["metadata"]["uid"] = f"local-{k}"
+        p["metadata"]["name"] = f"local-{k}"
+        p["metadata"]["namespace"] = "sched-1"  # the spread pods' namespace: their selector counts these
+        p["metadata"].setdefault("labels", {})["color"] = "blue" if k % 2 else "green"
+    rs = g.schedule_batch([g.compile(p) for p in local], assume=True)
+    for k, p in enumerate(local):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"node-local pod {k}"
+    _, _, spread = topology_spreading(800, 0, 300)
+    for k, p in enumerate(spread):
+        p["metadata"]["uid"] = f"spread-{k}"
+        p["metadata"]["name"] = f"spread-{k}"
+        p["spec"]["topologySpreadConstraints"][0]["labelSelector"] = {"matchLabels": {"color": "blue"}}
+    rs = g.schedule_batch([g.compile(p) for p in spread], assume=True)
+    for k, p in enumerate(spread):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[k].as_tuple() == ro.as_tuple(), f"spread pod {k}"
+    assert g.compare_mirror(sync=True) == (0, -1)
+
+
 def test_ties_follow_heap_preorder(native):
     """All nodes identical: every TotalScore ties, so placement is the heap pre-order rule."""
     from ksg.synth import scheduling_basic

@@ -132,6 +132,23 @@ def test_preempt_matches_oracle_random(native, seed):
     assert found > 0  # the streams do exercise a nomination
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_preempt_without_now(native, seed):
+    """Calls that omit "now": product and oracle each read the wall clock once per call (GetPodStartTime's
+    time.Now()).  Every pod here has status.startTime, so the clock is never decisive and the outcomes
+    (candidates, victims, their order by start time) must agree exactly."""
+    rng, nodes, existing = cluster(70 + seed, 120, 6)
+    for k, p in enumerate(existing):
+        p["status"]["startTime"] = f"2024-01-01T{k % 24:02d}:{rng.randrange(60):02d}:{rng.randrange(60):02d}Z"
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    found = 0
+    for q in range(10):
+        pod = mk_pod(f"pre{q}", rng, prio=rng.choice([100, 500, 1000]), big=True)
+        r, _ = compare(dev, orc, pod, {"offset": rng.randrange(1000), "pdbs": pdbs(rng)})
+        found += r.status == 0
+    assert found > 0
+
+
 def test_preempt_policy_never_and_terminating_victims(native):
     rng, nodes, existing = cluster(11, 40, 5)
     # a victim on the nominated node terminating by preemption blocks a new preemption
