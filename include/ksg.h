@@ -285,6 +285,14 @@ int ksg_debug_relayouts(const ksg_ctx *ctx, uint64_t *full, uint64_t *gather);
  * scoring.go:287-299: log(size + 2)).  Returns n. */
 int ksg_debug_log_table(double *out, int32_t n);
 
+/* The plugin-level shim's consistency check: *events counts the cache mutations the
+ * context has applied (node add / update / remove, pod add / remove, and the assumes and forgets of its
+ * scheduling calls), *list_gen the rebuilds of the snapshot's node list (UpdateSnapshot's
+ * updateNodeInfoSnapshotList, backend/cache/cache.go:223-290: the index order may have changed).  A
+ * binding that counts the events it forwarded detects a mirror that missed one; list_gen tells it when
+ * to re-resolve node names to snapshot indices (ksg_node_name). */
+int ksg_generation(const ksg_ctx *ctx, uint64_t *list_gen, uint64_t *events);
+
 /* The requests the library derives from one v1.Pod (no context, no device): out[0..4] are
  * CalculateResource's Requested MilliCPU / Memory / EphemeralStorage and Non0CPU / Non0Mem
  * (pkg/scheduler/framework/types.go:1035-1076, with the in-place resize status resources of

@@ -389,6 +389,14 @@ int ksg_debug_log_table(double* out, int32_t n) {
   return n;
 }
 
+int ksg_generation(const ksg_ctx* ctx, uint64_t* list_gen, uint64_t* events) {
+  if (!ctx) return KSG_EINVAL;
+  ctx->cluster->order();  // a pending node-list rebuild counts now
+  if (list_gen) *list_gen = ctx->cluster->list_gen;
+  if (events) *events = ctx->cluster->events;
+  return KSG_OK;
+}
+
 int ksg_debug_pod_resources(const char* pod_json, size_t len, int64_t* out, int32_t cap) {
   using namespace ksg;
   if (!pod_json || !out || cap < 8) return KSG_EINVAL;

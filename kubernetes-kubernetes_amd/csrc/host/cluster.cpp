@@ -155,6 +155,7 @@ const std::vector<std::string>& Cluster::order() {
   }
   if (rebuild) {  // updateNodeInfoSnapshotList(updateAll=true) over nodeTree.list (node_tree.go:119-143)
     ++node_gen_;
+    ++list_gen;
     order_.clear();
     size_t longest = 0;
     for (auto& z : zones_) longest = std::max(longest, tree_[z].size());
@@ -362,6 +363,7 @@ int Cluster::add_node(NodeSpec&& n) {
   ++node_gen_;
   auto it = nodes_.find(n.name);
   if (it != nodes_.end() && it->second->real) return update_node(std::move(n));
+  ++events;
   NodeRec* r;
   if (it == nodes_.end()) {
     auto rec = std::make_unique<NodeRec>();
@@ -387,6 +389,7 @@ int Cluster::update_node(NodeSpec&& n) {
   ++node_gen_;
   auto it = nodes_.find(n.name);
   if (it == nodes_.end() || !it->second->real) return add_node(std::move(n));
+  ++events;
   NodeRec& r = *it->second;
   remove_images(r.spec);
   std::string z0, z1;
@@ -411,6 +414,7 @@ int Cluster::remove_node(const std::string& name) {
   ++node_gen_;
   auto it = nodes_.find(name);
   if (it == nodes_.end() || !it->second->real) { err = "node " + name + " is not found"; return KSG_ENOTFOUND; }
+  ++events;
   NodeRec& r = *it->second;
   remove_images(r.spec);
   tree_remove(r.spec);
@@ -454,6 +458,7 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
   const std::string& node_name = node_override ? *node_override : p.node_name;
   if (node_name.empty()) { err = "pod is not bound"; return KSG_EINVAL; }
   if (pods.count(uid)) { err = "pod " + uid + " exists"; return KSG_EEXIST; }
+  ++events;
   NodeRec* r = node(node_name);
   if (!r) {
     auto rec = std::make_unique<NodeRec>();
@@ -501,6 +506,7 @@ int Cluster::add_pod(const PodSpec& p, const std::string& uid_override, bool dev
 int Cluster::remove_pod(const std::string& uid) {
   auto it = pods.find(uid);
   if (it == pods.end()) { err = "unknown pod " + uid; return KSG_ENOTFOUND; }
+  ++events;
   NodeRec* r = node(it->second.node);
   pods_with_affinity -= it->second.with_affinity ? 1 : 0;
   req_anti_pods -= it->second.req_anti ? 1 : 0;

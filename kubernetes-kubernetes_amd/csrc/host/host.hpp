@@ -450,6 +450,9 @@ class Cluster {
   std::vector<uint8_t> dyn_queued_;
   DevBuf dyn_dev_;
   int64_t next_start = 0;                    // Scheduler.nextStartNodeIndex
+  // ksg_generation: cache mutations applied (node add / update / remove, pod add / remove -- assumes and
+  // forgets included) and rebuilds of the snapshot's node list (its order may have changed)
+  uint64_t events = 0, list_gen = 0;
   double taint_ids_per_node = 0, img_ids_per_node = 0;  // CSR densities (algorithmic-bytes model)
   int64_t taint_max_per_node = 0;                        // bounds k_sched_loop's raw-score granules
   int64_t alloc_bound = 0;                               // max cpu/memory allocatable seen (INT64_MAX: a negative one)

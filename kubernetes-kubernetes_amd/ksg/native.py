@@ -33,6 +33,8 @@ def load():
         lib.ksg_shard_range.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         lib.ksg_debug_relayouts.restype = C.c_int
         lib.ksg_debug_relayouts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        lib.ksg_generation.restype = C.c_int
+        lib.ksg_generation.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib.ksg_debug_compare_mirror.restype = C.c_int
         lib.ksg_debug_compare_mirror.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         _lib = lib
@@ -60,6 +62,12 @@ class Scheduler(Backend):
         self._chk(self.lib.ksg_debug_compare_mirror(self.ctx, 1 if sync else 0, C.byref(nd), C.byref(first)),
                   "compare_mirror")
         return nd.value, first.value
+
+    def generation(self):
+        """(node-list rebuilds, cache mutations applied) -- ksg_generation, the plugin shim's consistency check."""
+        lg, ev = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.ksg_generation(self.ctx, C.byref(lg), C.byref(ev)), "generation")
+        return lg.value, ev.value
 
     def relayouts(self):
         """(full mirror rebuilds, gather re-layouts) so far (ksg_debug_relayouts)."""

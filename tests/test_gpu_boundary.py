@@ -159,3 +159,41 @@ def test_resource_claim_pods_are_declined(native):
         with pytest.raises(KsgError):
             b.compile(p)
     _cycle(g, o, PodW("e", uid="e").container(requests={"cpu": "1"}).obj(), "after")
+
+
+def test_generation_counts_cache_events(native):
+    """ksg_generation (the plugin-level shim's check): every applied cache mutation -- node
+    add / update / remove, bound pod add / remove, each assume of a scheduling call, a forget -- counts one
+    event; rejected calls count none; the node-list generation moves when the snapshot list is rebuilt
+    (a node added or removed), not for an in-place node update or pod events."""
+    from ksg.synth import scheduling_basic
+    nodes, init, pods = scheduling_basic(300, 20, 40)
+    s = native({})
+    lg0, ev0 = s.generation()
+    for n in nodes:
+        s.add_node(n)
+    for p in init:
+        s.add_pod(p)
+    lg1, ev1 = s.generation()
+    assert ev1 - ev0 == len(nodes) + len(init)
+    assert lg1 > lg0
+    rs = s.schedule_batch([s.compile(p) for p in pods[:30]], assume=True)
+    placed = sum(r.status == 0 for r in rs)
+    h = s.compile(pods[30])
+    r, _ = s.schedule_one(h, assume=True)
+    placed += r.status == 0
+    lg2, ev2 = s.generation()
+    assert ev2 - ev1 == placed and lg2 == lg1
+    s.forget(h)
+    upd = dict(nodes[5])
+    upd["metadata"] = dict(upd["metadata"], labels=dict(upd["metadata"].get("labels", {}), extra="x"))
+    s.update_node(upd)
+    s.remove_pod(init[0]["metadata"]["uid"])
+    with pytest.raises(Exception):
+        s.remove_pod("no-such-pod")
+    lg3, ev3 = s.generation()
+    assert ev3 - ev2 == 3 and lg3 == lg2
+    s.remove_node(nodes[7]["metadata"]["name"])
+    lg4, ev4 = s.generation()
+    assert ev4 - ev3 == 1 and lg4 > lg3
+    s.close()
