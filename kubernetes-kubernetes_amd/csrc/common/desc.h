@@ -244,18 +244,16 @@ struct PodDesc {
 // The host lays out, per snapshot node, the pods isPreemptionAllowed admits (lower priority than the
 // preemptor) in reprieve order: sorted by MoreImportantPod, the PDB-violating group first
 // (default_preemption.go:280-343).  k_preempt removes them all, re-runs the filters the removal can
-// change (NodePorts, NodeResourcesFit, then PodTopologySpread / InterPodAffinity on the cycle's
-// counts, which the host guarantees no victim changes), and reprieves them one by one.
-constexpr int kPreemptScalar = 4;  // scalar resources of the preemptor whose victim deltas are tracked
+// change (NodePorts, NodeResourcesFit, then PodTopologySpread / InterPodAffinity with the victims'
+// effect on the cycle's counts, PreemptIn), and reprieves them one by one.
 enum PVFlags : uint32_t {
   PV_PORT = 1u,  // the victim holds a host port the preemptor's ports conflict with
   PV_VIOL = 2u,  // the victim is in the PDB-violating group (filterPodsWithPDBViolation)
 };
 struct PVictim {
   int64_t cpu, mem, eph;          // Resource it adds to NodeInfo.Requested (PodInfo.CalculateResource)
-  int64_t sc[kPreemptScalar];     // its request of the preemptor's scalar resources, PodDesc scalar order
   uint32_t flags;                 // PVFlags
-  uint32_t pad;
+  int32_t slot;                   // pod-table slot (namespace, labels, terms; PreemptIn::vsc row)
 };
 enum PNFlags : uint32_t {
   PN_BASE_PORT = 1u,  // a conflicting host port stays on the node with every victim removed
@@ -270,7 +268,7 @@ struct POut {
   uint32_t st;         // packed Filter status with the victims removed (0: fits), or a PStat
   int32_t nvictims;    // victims that stay removed (flag 1 in the per-victim output)
   int32_t nviolating;  // of them, from the PDB-violating group (numViolatingVictim)
-  int32_t pad;
+  uint32_t flags;      // as PSegOut::flags
 };
 
 // The device-resident form (k_preempt_seg): every node's pods as an importance-ordered segment of
@@ -307,6 +305,21 @@ struct PickOut {
   int32_t offset, unsupported, pad[2];          // unsupported: some node's PSegOut flag bit 0
   PSegOut best_out;                             // the chosen node's result (victim masks)
 };
+constexpr int kPreemptCons = 8;  // DoNotSchedule constraints / affinity terms / keys whose counts the victims may move (more: unsupported)
+// What both dry-run kernels (k_preempt_seg, k_preempt) read about the victims' effects beyond Requested:
+// their scalar resources and the PodTopologySpread / InterPodAffinity counts they move.
+struct PreemptIn {
+  int32_t pts_check, ipa_check;
+  const long long* pts_mm;   // [kPreemptCons][3]: per DoNotSchedule constraint the domain minimum, its
+                             // multiplicity and the next larger count (k_pts_minima)
+  const int32_t* ex_contrib; // [slot][kPreemptCons]: the pod's required anti-affinity terms that match the
+                             // preemptor, per existing-anti key (k_preempt_terms); nullptr: none
+  const long long* aff_tot;  // [kPreemptCons]: per required affinity term of a self-matching preemptor the
+                             // cycle's total count over its histogram (k_aff_totals); nullptr: not needed
+  // the preemptor's extended resources (PodDesc scalar order, n_scalar of them, any number):
+  const int64_t* vsc;        // [slot][n_scalar]: each pod's request of them (CalculateResource), 0 rows elsewhere
+  int64_t* sreq;             // [n][n_scalar]: per node, the dry run's Requested of them (the kernel's scratch)
+};
 struct PreemptView {
   const PRec* seg;           // [n][kSegCap]
   const int32_t* cnt;        // [n] records in use
@@ -314,17 +327,10 @@ struct PreemptView {
   const int32_t* pdb_pool;   // their selector programs
   const uint8_t* disrupted;  // [slot] bit k: the pod is in PDB k's DisruptedPods (nullptr: none)
   PSegOut* out;              // [n]
-  int32_t npdb, prio, all_nodes, pts_check;
+  int32_t npdb, prio, all_nodes, pad;
   int64_t now;               // GetPodStartTime for pods without a start time
-  const long long* pts_mm;   // [kPreemptCons][3]: per DoNotSchedule constraint the domain minimum, its
-                             // multiplicity and the next larger count (k_pts_minima)
-  const int32_t* ex_contrib; // [slot][kPreemptCons]: the pod's required anti-affinity terms that match the
-                             // preemptor, per existing-anti key (k_preempt_terms); nullptr: none
-  const long long* aff_tot;  // [kPreemptCons]: per required affinity term of a self-matching preemptor the
-                             // cycle's total count over its histogram (k_aff_totals); nullptr: not needed
-  int32_t ipa_check, pad2;
+  PreemptIn in;
 };
-constexpr int kPreemptCons = 8;  // DoNotSchedule constraints / affinity terms / keys whose counts the victims may move (more: unsupported)
 
 // Per-pod device result (ScheduleResult + diagnostics), written by the select kernel.
 struct DevResult {

@@ -4090,140 +4090,15 @@ hipError_t set_diag(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL
 #endif
 
 // =====================================================================================================
-// k_preempt: DefaultPreemption.SelectVictimsOnNode (default_preemption.go:252-354) for every node the
-// dry run may check (findCandidates' NodesForStatusCode(Unschedulable), preemption.go:174-196, or every
-// node), one thread per node, the preemptor's cycle status in b.status (k_filter_score, evaluation
-// output).  The node's state is the mirror minus the victims: the filters a removal can change run on
-// it -- NodePorts, NodeResourcesFit (the static filters before them passed or fail unchanged), then
-// PodTopologySpread / InterPodAffinity against the cycle's counts, which no victim of this call changes
-// (the host checked) -- and the victims are added back one at a time in reprieve order, each kept
-// removed only when the preemptor no longer fits with it (reprievePod, :316-330).
+// k_preempt / k_preempt_seg: DefaultPreemption.SelectVictimsOnNode (default_preemption.go:252-354) for every
+// node the dry run may check (findCandidates' NodesForStatusCode(Unschedulable), preemption.go:174-196, or
+// every node), one thread per node, the preemptor's cycle status in b.status (k_filter_score, evaluation
+// output).  The node's state is the mirror minus the victims: the filters a removal can change run on it --
+// NodePorts, NodeResourcesFit (the static filters before them passed or fail unchanged), then
+// PodTopologySpread / InterPodAffinity with the victims' RemovePod / AddPod effect on the cycle's counts
+// (PreemptTopo) -- and the victims are added back one at a time in reprieve order, each kept removed only
+// when the preemptor no longer fits with it (reprievePod, :316-343).
 // =====================================================================================================
-__device__ __forceinline__ uint32_t preempt_node_filters(const MirrorView& m, const NodeCore& nc, const int64_t* sreq,
-                                                         const uint8_t* base, const PodDesc& d, int i, bool port) {
-  const uint32_t fm = d.filter_mask;
-  if (((fm >> P_PORTS) & 1u) && port) return pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
-  if ((fm >> P_FIT) & 1u) {  // fit.go:593-734, as run_filters with the node's Requested less the victims
-    uint32_t reasons = 0;
-    bool unresolvable = false;
-    if ((int64_t)nc.npods + 1 > (int64_t)nc.apods) reasons |= KSG_R_TOO_MANY_PODS;
-    if (d.fit_any) {
-      if (d.req_cpu > 0 && d.req_cpu > nc.acpu - nc.rcpu) {
-        reasons |= KSG_R_INSUFFICIENT_CPU;
-        unresolvable |= d.req_cpu > nc.acpu;
-      }
-      if (d.req_mem > 0 && d.req_mem > nc.amem - nc.rmem) {
-        reasons |= KSG_R_INSUFFICIENT_MEMORY;
-        unresolvable |= d.req_mem > nc.amem;
-      }
-      if (d.req_eph > 0 && d.req_eph > nc.aeph - nc.reph) {
-        reasons |= KSG_R_INSUFFICIENT_EPHEMERAL;
-        unresolvable |= d.req_eph > nc.aeph;
-      }
-      const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
-#pragma unroll
-      for (int k = 0; k < kPreemptScalar; ++k) {  // unrolled: sreq stays in registers (no scratch)
-        if (k >= d.n_scalar) break;
-        const int64_t a = m.scalar_alloc[(size_t)sr[k].slot * (size_t)m.cap + (size_t)i];
-        if (sr[k].qty > a - sreq[k]) {
-          reasons |= KSG_R_INSUFFICIENT_SCALAR;
-          unresolvable |= sr[k].qty > a;
-        }
-      }
-    }
-    if (reasons) return pack_status(unresolvable ? C_UU : C_UNSCHED, P_FIT, reasons);
-  }
-  return 0u;
-}
-
-__global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, int pod, const PNode* pn,
-                                                    const PVictim* pv, uint8_t* vout, POut* out, int all_nodes) {
-  const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
-  if (i >= m.n) return;
-  const uint8_t* base = b.descs + b.desc_off[pod];
-  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
-  POut o{PS_NOT_CHECKED, 0, 0, 0};
-  const uint32_t st0 = b.status[i];
-  const PNode nd = pn[i];
-  if (!all_nodes && status_code(st0) != C_UNSCHED) {
-    out[i] = o;
-    return;
-  }
-  if (nd.vcnt == 0) {  // "No preemption victims found for incoming pod" (:291-294)
-    o.st = PS_NO_VICTIMS;
-    out[i] = o;
-    return;
-  }
-  // a status from a filter that reads no pod (or a PreFilter rejection) holds with the victims removed too
-  const uint32_t p0 = status_plugin(st0);
-  if (st0 != 0 && (p0 == P_UNSCHED || p0 == P_NODENAME || p0 == P_TAINT || p0 == P_NA || p0 == 15u)) {
-    o.st = st0;
-    out[i] = o;
-    return;
-  }
-  NodeCore nc = load_core(m, i);
-  int64_t sreq[kPreemptScalar];
-  const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
-  const int ns = d.n_scalar < kPreemptScalar ? d.n_scalar : kPreemptScalar;  // host-checked: n_scalar <= 4
-#pragma unroll
-  for (int k = 0; k < kPreemptScalar; ++k)
-    sreq[k] = k < ns ? m.scalar_req[(size_t)sr[k].slot * (size_t)m.cap + (size_t)i] : 0;
-  const PVictim* v = pv + nd.voff;
-  for (int q = 0; q < nd.vcnt; ++q) {  // removePod of every potential victim (:285-289)
-    nc.rcpu -= v[q].cpu;
-    nc.rmem -= v[q].mem;
-    nc.reph -= v[q].eph;
-#pragma unroll
-    for (int k = 0; k < kPreemptScalar; ++k) sreq[k] -= v[q].sc[k];
-  }
-  nc.npods -= nd.vcnt;
-  bool port = (nd.flags & PN_BASE_PORT) != 0;
-  uint32_t st = preempt_node_filters(m, nc, sreq, base, d, i, port);
-  if (st == 0) {
-    int64_t raw_taint = 0;
-    (void)raw_taint;
-    st = topo_filters(m, base, d, i, ArenaTopo{b.stats + pod, b.arena}, 0);
-  }
-  o.st = st;
-  if (st == 0) {
-    // reprieve in order (:331-343); PodTopologySpread / InterPodAffinity cannot change (host-checked)
-    for (int q = 0; q < nd.vcnt; ++q) {
-      const PVictim x = v[q];
-      NodeCore t = nc;
-      t.rcpu += x.cpu;
-      t.rmem += x.mem;
-      t.reph += x.eph;
-      t.npods += 1;
-      int64_t ts[kPreemptScalar];
-#pragma unroll
-      for (int k = 0; k < kPreemptScalar; ++k) ts[k] = sreq[k] + x.sc[k];
-      const bool tp = port || (x.flags & PV_PORT) != 0;
-      const bool fits = preempt_node_filters(m, t, ts, base, d, i, tp) == 0;
-      if (fits) {
-        nc = t;
-#pragma unroll
-        for (int k = 0; k < kPreemptScalar; ++k) sreq[k] = ts[k];
-        port = tp;
-        vout[nd.voff + q] = 0;
-      } else {
-        vout[nd.voff + q] = 1;
-        o.nvictims += 1;
-        o.nviolating += (x.flags & PV_VIOL) ? 1 : 0;
-      }
-    }
-  }
-  out[i] = o;
-}
-
-hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, const PNode* pn, const PVictim* pv,
-                          uint8_t* vout, POut* out, int all_nodes, hipStream_t s) {
-  const int nb = (m.n + kBlock - 1) / kBlock;
-  if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_preempt, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pn, pv, vout, out, all_nodes);
-  return hipGetLastError();
-}
-
-
 // The cycle's PodTopologySpread counts as the preemption dry run sees them at node i: the preFilterState
 // clone with the victims' RemovePod / AddPod applied (podtopologyspread/filtering.go:157-212).  Every
 // victim is on node i, so only the count of node i's own domain moves; the domain minimum becomes the
@@ -4402,6 +4277,274 @@ hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod
   return hipGetLastError();
 }
 
+
+// Fit with the victims removed (fit.go:593-734, as run_filters): nc holds the node's Requested less the
+// removed victims; sreq (nullptr: no extended resources) the same for each of the preemptor's scalar
+// resources, add (nullptr: none) a victim's request of them being tried back (reprieve)
+__device__ __forceinline__ uint32_t preempt_node_filters(const MirrorView& m, const NodeCore& nc, const int64_t* sreq,
+                                                         const int64_t* add, const uint8_t* base, const PodDesc& d,
+                                                         int i, bool port) {
+  const uint32_t fm = d.filter_mask;
+  if (((fm >> P_PORTS) & 1u) && port) return pack_status(C_UNSCHED, P_PORTS, KSG_R_NODE_PORTS);
+  if ((fm >> P_FIT) & 1u) {
+    uint32_t reasons = 0;
+    bool unresolvable = false;
+    if ((int64_t)nc.npods + 1 > (int64_t)nc.apods) reasons |= KSG_R_TOO_MANY_PODS;
+    if (d.fit_any) {
+      if (d.req_cpu > 0 && d.req_cpu > nc.acpu - nc.rcpu) {
+        reasons |= KSG_R_INSUFFICIENT_CPU;
+        unresolvable |= d.req_cpu > nc.acpu;
+      }
+      if (d.req_mem > 0 && d.req_mem > nc.amem - nc.rmem) {
+        reasons |= KSG_R_INSUFFICIENT_MEMORY;
+        unresolvable |= d.req_mem > nc.amem;
+      }
+      if (d.req_eph > 0 && d.req_eph > nc.aeph - nc.reph) {
+        reasons |= KSG_R_INSUFFICIENT_EPHEMERAL;
+        unresolvable |= d.req_eph > nc.aeph;
+      }
+      const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
+      for (int k = 0; sreq && k < d.n_scalar; ++k) {
+        const int64_t a = m.scalar_alloc[(size_t)sr[k].slot * (size_t)m.cap + (size_t)i];
+        const int64_t used = sreq[k] + (add ? add[k] : 0);
+        if (sr[k].qty > a - used) {
+          reasons |= KSG_R_INSUFFICIENT_SCALAR;
+          unresolvable |= sr[k].qty > a;
+        }
+      }
+    }
+    if (reasons) return pack_status(unresolvable ? C_UU : C_UNSCHED, P_FIT, reasons);
+  }
+  return 0u;
+}
+
+// The victims' topology effects at node i, as both dry-run kernels track them
+struct TopoTrack {
+  PreemptTopo tp;
+  uint32_t elig;        // DoNotSchedule constraints node i is eligible for (pts_eligible)
+  int nra, nrn, nex;    // the preemptor's required affinity / anti-affinity terms, existing-anti keys tracked
+  bool pts_over;        // more DoNotSchedule constraints than PreemptTopo tracks
+};
+__device__ __forceinline__ void topo_track_init(const MirrorView& m, const BatchView& b, int pod, const uint8_t* base,
+                                                const PodDesc& d, int i, const PreemptIn& in, TopoTrack& T,
+                                                uint32_t* flags) {
+  PreemptTopo& tp = T.tp;
+  tp.a = ArenaTopo{b.stats + pod, b.arena};
+#pragma unroll
+  for (int c = 0; c < kPreemptCons; ++c) tp.hb[c] = tp.vi[c] = -1, tp.cnt0[c] = tp.dlt[c] = tp.excl[c] = 0;
+  const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
+  T.elig = 0;
+  T.pts_over = in.pts_check && d.n_ptsf > kPreemptCons;
+  if (in.pts_check && !T.pts_over) {
+    T.elig = pts_eligible(m, base, d, cs, d.n_ptsf, i);
+#pragma unroll
+    for (int c = 0; c < kPreemptCons; ++c)
+      if (c < d.n_ptsf && ((T.elig >> c) & 1u)) {
+        const int32_t v = node_label(m, cs[c].slot, i);
+        tp.hb[c] = cs[c].hist_base;
+        tp.vi[c] = v;
+        tp.cnt0[c] = (int64_t)b.arena[cs[c].hist_base + v];
+        const long long* mm = in.pts_mm + 3 * c;
+        tp.excl[c] = (tp.cnt0[c] == mm[0] && mm[1] == 1) ? mm[2] : mm[0];
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < 3 * kPreemptCons; ++k) tp.ihb[k] = tp.ivi[k] = -1, tp.idl[k] = 0;
+  const IpaTerm* raff = at<IpaTerm>(base, d.raff_off);
+  const IpaTerm* ranti = at<IpaTerm>(base, d.ranti_off);
+  const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
+  T.nra = in.ipa_check ? d.n_raff : 0;
+  T.nrn = in.ipa_check ? d.n_ranti : 0;
+  T.nex = (in.ipa_check && in.ex_contrib) ? d.n_exkeys : 0;
+  tp.nra = -1;
+  if (in.ipa_check && in.aff_tot && (d.ipa_flags & IPA_SELF_ALL) && T.nra <= kPreemptCons) {
+    tp.nra = T.nra;
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k) tp.atot[k] = k < T.nra ? (int64_t)in.aff_tot[k] : 0;
+  }
+  if (in.ipa_check) {
+    if (T.nra > kPreemptCons || T.nrn > kPreemptCons || T.nex > kPreemptCons) *flags |= 1u;  // beyond PreemptTopo
+#pragma unroll
+    for (int k = 0; k < kPreemptCons; ++k) {
+      if (k < T.nra) {
+        tp.ihb[k] = raff[k].hist_base;
+        tp.ivi[k] = node_label(m, raff[k].slot, i);
+      }
+      if (k < T.nrn) {
+        tp.ihb[kPreemptCons + k] = ranti[k].hist_base;
+        tp.ivi[kPreemptCons + k] = node_label(m, ranti[k].slot, i);
+      }
+      if (k < T.nex) {
+        tp.ihb[2 * kPreemptCons + k] = ek[k].base;
+        tp.ivi[2 * kPreemptCons + k] = node_label(m, ek[k].slot, i);
+      }
+    }
+  }
+}
+// The DoNotSchedule constraints whose count the victim in pod-table slot `slot` is part of (updateWithPod,
+// podtopologyspread/filtering.go:181-212): a victim in the preemptor's namespace that matches the constraint's
+// selector, at a node eligible for it.  Beyond kPreemptCons constraints a counted victim is unsupported.
+__device__ __forceinline__ uint32_t topo_counts(const MirrorView& m, const uint8_t* base, const PodDesc& d,
+                                                const TopoTrack& T, int32_t slot, uint32_t* flags) {
+  if (!T.elig && !T.pts_over) return 0u;
+  if (m.pod_ns[slot] != d.ns_id) return 0u;
+  const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+  const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
+  const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+  const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+  if (T.pts_over) {
+    for (int32_t c = 0; c < d.n_ptsf; ++c)
+      if (lsel_match(sp + cs[c].sel, lb, ln)) *flags |= 1u;
+    return 0u;
+  }
+  uint32_t bits = 0;
+#pragma unroll
+  for (int c = 0; c < kPreemptCons; ++c)
+    if (((T.elig >> c) & 1u) && lsel_match(sp + cs[c].sel, lb, ln)) bits |= 1u << c;
+  return bits;
+}
+// The victim's InterPodAffinity effect (filtering.go:75-85), applied to x with sign sg: the preemptor's
+// affinity terms count it when it matches all of them, its anti-affinity terms each when it matches, and
+// its own required anti-affinity terms that match the preemptor count at their keys; false: no count moves
+__device__ __forceinline__ bool topo_ipa(const MirrorView& m, const uint8_t* base, const PodDesc& d, const TopoTrack& T,
+                                         const PreemptIn& in, int32_t slot, PreemptTopo& x, int sg) {
+  if (!in.ipa_check || (T.nra == 0 && T.nrn == 0 && T.nex == 0)) return false;
+  const int32_t ns = m.pod_ns[slot];
+  const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
+  const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
+  const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+  const IpaTerm* raff = at<IpaTerm>(base, d.raff_off);
+  const IpaTerm* ranti = at<IpaTerm>(base, d.ranti_off);
+  bool moved = false;
+  bool all = T.nra > 0;
+#pragma unroll
+  for (int k = 0; k < kPreemptCons; ++k)
+    if (k < T.nra) all = all && term_matches_pod(sp, raff[k], ns, lb, ln);
+#pragma unroll
+  for (int k = 0; k < kPreemptCons; ++k) {
+    if (all && k < T.nra && T.tp.ivi[k] >= 0) {
+      x.idl[k] += sg;
+      moved = true;
+    }
+    if (k < T.nrn && T.tp.ivi[kPreemptCons + k] >= 0 && term_matches_pod(sp, ranti[k], ns, lb, ln)) {
+      x.idl[kPreemptCons + k] += sg;
+      moved = true;
+    }
+    if (k < T.nex && T.tp.ivi[2 * kPreemptCons + k] >= 0) {
+      const int32_t cn = in.ex_contrib[(size_t)slot * kPreemptCons + k];
+      if (cn) {
+        x.idl[2 * kPreemptCons + k] += sg * cn;
+        moved = true;
+      }
+    }
+  }
+  // (a preemptor matching its own terms: affinityCounts emptied by the removal flips the "no pod matches
+  // anywhere" rule, filtering.go:404-415 -- PreemptTopo::any from the totals and these deltas)
+  return moved;
+}
+// the node's Requested of the preemptor's extended resources, in its scratch row (nullptr: none)
+__device__ __forceinline__ int64_t* preempt_sreq(const MirrorView& m, const uint8_t* base, const PodDesc& d,
+                                                 const PreemptIn& in, int i) {
+  if (!in.sreq || d.n_scalar == 0) return nullptr;
+  int64_t* row = in.sreq + (size_t)i * (size_t)d.n_scalar;
+  const ScalarReq* sr = at<ScalarReq>(base, d.scalar_off);
+  for (int k = 0; k < d.n_scalar; ++k) row[k] = m.scalar_req[(size_t)sr[k].slot * (size_t)m.cap + (size_t)i];
+  return row;
+}
+
+// Host-staged victims (PNode / PVictim: the host sorted them and grouped them by PDB violation)
+__global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, int pod, const PNode* pn,
+                                                    const PVictim* pv, uint8_t* vout, POut* out, int all_nodes,
+                                                    PreemptIn in) {
+  const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+  if (i >= m.n) return;
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  POut o{PS_NOT_CHECKED, 0, 0, 0};
+  const uint32_t st0 = b.status[i];
+  const PNode nd = pn[i];
+  if (!all_nodes && status_code(st0) != C_UNSCHED) {
+    out[i] = o;
+    return;
+  }
+  if (nd.vcnt == 0) {  // "No preemption victims found for incoming pod" (:291-294)
+    o.st = PS_NO_VICTIMS;
+    out[i] = o;
+    return;
+  }
+  // a status from a filter that reads no pod (or a PreFilter rejection) holds with the victims removed too
+  const uint32_t p0 = status_plugin(st0);
+  if (st0 != 0 && (p0 == P_UNSCHED || p0 == P_NODENAME || p0 == P_TAINT || p0 == P_NA || p0 == 15u)) {
+    o.st = st0;
+    out[i] = o;
+    return;
+  }
+  NodeCore nc = load_core(m, i);
+  int64_t* sreq = preempt_sreq(m, base, d, in, i);
+  const int ns = d.n_scalar;
+  TopoTrack T;
+  topo_track_init(m, b, pod, base, d, i, in, T, &o.flags);
+  const PVictim* v = pv + nd.voff;
+  bool moves = false;  // some victim moves a topology count: the topology filters re-run on every reprieve
+  for (int q = 0; q < nd.vcnt; ++q) {  // removePod of every potential victim (:285-289)
+    nc.rcpu -= v[q].cpu;
+    nc.rmem -= v[q].mem;
+    nc.reph -= v[q].eph;
+    if (sreq)
+      for (int k = 0; k < ns; ++k) sreq[k] -= in.vsc[(size_t)v[q].slot * ns + k];
+    const uint32_t kb = topo_counts(m, base, d, T, v[q].slot, &o.flags);
+#pragma unroll
+    for (int c = 0; c < kPreemptCons; ++c) T.tp.dlt[c] -= (kb >> c) & 1u;
+    moves |= kb != 0;
+    moves |= topo_ipa(m, base, d, T, in, v[q].slot, T.tp, -1);
+  }
+  nc.npods -= nd.vcnt;
+  bool port = (nd.flags & PN_BASE_PORT) != 0;
+  uint32_t st = preempt_node_filters(m, nc, sreq, nullptr, base, d, i, port);
+  if (st == 0) st = topo_filters(m, base, d, i, T.tp, 0);
+  o.st = st;
+  if (st == 0) {
+    for (int q = 0; q < nd.vcnt; ++q) {  // reprieve in the host's order (:331-343)
+      const PVictim x = v[q];
+      NodeCore t = nc;
+      t.rcpu += x.cpu;
+      t.rmem += x.mem;
+      t.reph += x.eph;
+      t.npods += 1;
+      const int64_t* add = sreq ? in.vsc + (size_t)x.slot * ns : nullptr;
+      const bool tpo = port || (x.flags & PV_PORT) != 0;
+      const uint32_t kb = moves ? topo_counts(m, base, d, T, x.slot, &o.flags) : 0u;
+      PreemptTopo tt = T.tp;
+#pragma unroll
+      for (int c = 0; c < kPreemptCons; ++c) tt.dlt[c] += (kb >> c) & 1u;
+      const bool im = moves && topo_ipa(m, base, d, T, in, x.slot, tt, +1);
+      bool fits = preempt_node_filters(m, t, sreq, add, base, d, i, tpo) == 0;
+      if (fits && (kb || im)) fits = topo_filters(m, base, d, i, tt, 0) == 0;
+      if (fits) {
+        nc = t;
+        if (sreq)
+          for (int k = 0; k < ns; ++k) sreq[k] += add[k];
+        port = tpo;
+        T.tp = tt;
+        vout[nd.voff + q] = 0;
+      } else {
+        vout[nd.voff + q] = 1;
+        o.nvictims += 1;
+        o.nviolating += (x.flags & PV_VIOL) ? 1 : 0;
+      }
+    }
+  }
+  out[i] = o;
+}
+
+hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, const PNode* pn, const PVictim* pv,
+                          uint8_t* vout, POut* out, int all_nodes, const PreemptIn& in, hipStream_t s) {
+  const int nb = (m.n + kBlock - 1) / kBlock;
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_preempt, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pn, pv, vout, out, all_nodes, in);
+  return hipGetLastError();
+}
+
 // k_preempt_seg: k_preempt over the device-resident pod segments (PreemptView).  The filter re-runs and
 // the reprieve are k_preempt's; what the host staged per call there is derived here: the potential
 // victims (the segment suffix below the preemptor's priority), filterPodsWithPDBViolation
@@ -4438,120 +4581,10 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
     pv.out[i] = o;
     return;
   }
-  // PodTopologySpread counts the victims move (updateWithPod, podtopologyspread/filtering.go:181-212):
-  // constraint c counts a victim in the preemptor's namespace that matches c's selector, at a node that
-  // carries every constraint key and passes c's node-inclusion policies (pts_eligible)
-  PreemptTopo tp;
-  tp.a = ArenaTopo{b.stats + pod, b.arena};
-#pragma unroll
-  for (int c = 0; c < kPreemptCons; ++c) tp.hb[c] = tp.vi[c] = -1, tp.cnt0[c] = tp.dlt[c] = tp.excl[c] = 0;
-  const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
-  const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
-  uint32_t elig = 0;
-  if (pv.pts_check) {
-    if (d.n_ptsf > kPreemptCons) {  // more constraints than PreemptTopo tracks: unsupported if any victim counts
-      for (int q = first; q < cnt; ++q) {
-        const int32_t slot = r[q].slot;
-        if (m.pod_ns[slot] != d.ns_id) continue;
-        const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
-        const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
-        for (int32_t c = 0; c < d.n_ptsf; ++c)
-          if (lsel_match(sp + cs[c].sel, lb, ln)) o.flags |= 1u;
-      }
-    } else {
-      elig = pts_eligible(m, base, d, cs, d.n_ptsf, i);
-#pragma unroll
-      for (int c = 0; c < kPreemptCons; ++c)
-        if (c < d.n_ptsf && ((elig >> c) & 1u)) {
-          const int32_t v = node_label(m, cs[c].slot, i);
-          tp.hb[c] = cs[c].hist_base;
-          tp.vi[c] = v;
-          tp.cnt0[c] = (int64_t)b.arena[cs[c].hist_base + v];
-          const long long* mm = pv.pts_mm + 3 * c;
-          tp.excl[c] = (tp.cnt0[c] == mm[0] && mm[1] == 1) ? mm[2] : mm[0];
-        }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 3 * kPreemptCons; ++k) tp.ihb[k] = tp.ivi[k] = -1, tp.idl[k] = 0;
-  const IpaTerm* raff = at<IpaTerm>(base, d.raff_off);
-  const IpaTerm* ranti = at<IpaTerm>(base, d.ranti_off);
-  const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
-  const int nra = pv.ipa_check ? d.n_raff : 0, nrn = pv.ipa_check ? d.n_ranti : 0;
-  const int nex = (pv.ipa_check && pv.ex_contrib) ? d.n_exkeys : 0;
-  tp.nra = -1;
-  if (pv.ipa_check && pv.aff_tot && (d.ipa_flags & IPA_SELF_ALL) && nra <= kPreemptCons) {
-    tp.nra = nra;
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k) tp.atot[k] = k < nra ? (int64_t)pv.aff_tot[k] : 0;
-  }
-  if (pv.ipa_check) {
-    if (nra > kPreemptCons || nrn > kPreemptCons || nex > kPreemptCons) o.flags |= 1u;  // beyond PreemptTopo
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k) {
-      if (k < nra) {
-        tp.ihb[k] = raff[k].hist_base;
-        tp.ivi[k] = node_label(m, raff[k].slot, i);
-      }
-      if (k < nrn) {
-        tp.ihb[kPreemptCons + k] = ranti[k].hist_base;
-        tp.ivi[kPreemptCons + k] = node_label(m, ranti[k].slot, i);
-      }
-      if (k < nex) {
-        tp.ihb[2 * kPreemptCons + k] = ek[k].base;
-        tp.ivi[2 * kPreemptCons + k] = node_label(m, ek[k].slot, i);
-      }
-    }
-  }
-  // victim q's InterPodAffinity effect, applied with sign sg: the preemptor's affinity terms count it when
-  // it matches all of them, its anti-affinity terms each when it matches, and its own required
-  // anti-affinity terms that match the preemptor count at their keys; false: no count moves
-  auto ipa_apply = [&](int q, PreemptTopo& x, int sg) -> bool {
-    if (!pv.ipa_check || (nra == 0 && nrn == 0 && nex == 0)) return false;
-    const int32_t slot = r[q].slot;
-    const int32_t ns = m.pod_ns[slot];
-    const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
-    const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
-    const int32_t* sp2 = at<int32_t>(base, d.sel_pool_off);
-    bool moved = false;
-    bool all = nra > 0;
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k)
-      if (k < nra) all = all && term_matches_pod(sp2, raff[k], ns, lb, ln);
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k) {
-      if (all && k < nra && tp.ivi[k] >= 0) {
-        x.idl[k] += sg;
-        moved = true;
-      }
-      if (k < nrn && tp.ivi[kPreemptCons + k] >= 0 && term_matches_pod(sp2, ranti[k], ns, lb, ln)) {
-        x.idl[kPreemptCons + k] += sg;
-        moved = true;
-      }
-      if (k < nex && tp.ivi[2 * kPreemptCons + k] >= 0) {
-        const int32_t cn = pv.ex_contrib[(size_t)slot * kPreemptCons + k];
-        if (cn) {
-          x.idl[2 * kPreemptCons + k] += sg * cn;
-          moved = true;
-        }
-      }
-    }
-    // (a preemptor matching its own terms: affinityCounts emptied by the removal flips the "no pod matches
-    // anywhere" rule, filtering.go:404-415 -- PreemptTopo::any from the totals and these deltas)
-    return moved;
-  };
-  auto counts = [&](int q) -> uint32_t {  // the constraints whose count victim q is part of
-    if (!elig) return 0u;
-    const int32_t slot = r[q].slot;
-    if (m.pod_ns[slot] != d.ns_id) return 0u;
-    const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
-    const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
-    uint32_t bits = 0;
-#pragma unroll
-    for (int c = 0; c < kPreemptCons; ++c)
-      if (((elig >> c) & 1u) && lsel_match(sp + cs[c].sel, lb, ln)) bits |= 1u << c;
-    return bits;
-  };
+  const PreemptIn& in = pv.in;
+  TopoTrack T;
+  topo_track_init(m, b, pod, base, d, i, in, T, &o.flags);
+  const int ns = d.n_scalar;
   // filterPodsWithPDBViolation over the importance-ordered potential victims
   unsigned long long viol0 = 0ull, viol1 = 0ull;  // two words, no dynamically indexed array (scratch)
   if (pv.npdb > 0) {
@@ -4563,14 +4596,14 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
       const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
       if (ln == 0) continue;  // a pod with no labels matches no PDB
       const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
-      const int32_t ns = m.pod_ns[slot];
+      const int32_t pns = m.pod_ns[slot];
       const uint32_t dis = pv.disrupted ? pv.disrupted[slot] : 0u;
       bool v = false;
 #pragma unroll
       for (int k = 0; k < kMaxPdb; ++k) {
         if (k >= pv.npdb) break;
         const PdbDev pb = pv.pdb[k];
-        if (!pb.ok || pb.ns != ns || !lsel_match(pv.pdb_pool + pb.sel, lb, ln) || ((dis >> k) & 1u)) continue;
+        if (!pb.ok || pb.ns != pns || !lsel_match(pv.pdb_pool + pb.sel, lb, ln) || ((dis >> k) & 1u)) continue;
         if (--allowed[k] < 0) v = true;
       }
       if (v) (q < 64 ? viol0 : viol1) |= 1ull << (q & 63);
@@ -4590,21 +4623,26 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
       port |= !held;
     }
   NodeCore nc = load_core(m, i);
-  bool moves = false;  // some victim moves a spread count: the topology filters re-run on every reprieve
+  int64_t* sreq = preempt_sreq(m, base, d, in, i);
+  auto vsc = [&](const PRec& x) -> const int64_t* {  // the victim's request of the preemptor's scalars
+    return sreq && (x.flags & PR_SCALAR) ? in.vsc + (size_t)x.slot * ns : nullptr;
+  };
+  bool moves = false;  // some victim moves a topology count: the topology filters re-run on every reprieve
   for (int q = first; q < cnt; ++q) {
     nc.rcpu -= r[q].cpu;
     nc.rmem -= r[q].mem;
     nc.reph -= r[q].eph;
-    const uint32_t k = counts(q);
+    if (const int64_t* a = vsc(r[q]))
+      for (int k = 0; k < ns; ++k) sreq[k] -= a[k];
+    const uint32_t k = topo_counts(m, base, d, T, r[q].slot, &o.flags);
 #pragma unroll
-    for (int c = 0; c < kPreemptCons; ++c) tp.dlt[c] -= (k >> c) & 1u;
+    for (int c = 0; c < kPreemptCons; ++c) T.tp.dlt[c] -= (k >> c) & 1u;
     moves |= k != 0;
-    moves |= ipa_apply(q, tp, -1);
+    moves |= topo_ipa(m, base, d, T, in, r[q].slot, T.tp, -1);
   }
   nc.npods -= cnt - first;
-  int64_t sreq[kPreemptScalar] = {0, 0, 0, 0};  // the host takes this path only for pods without scalar requests
-  uint32_t st = preempt_node_filters(m, nc, sreq, base, d, i, port);
-  if (st == 0) st = topo_filters(m, base, d, i, tp, 0);
+  uint32_t st = preempt_node_filters(m, nc, sreq, nullptr, base, d, i, port);
+  if (st == 0) st = topo_filters(m, base, d, i, T.tp, 0);
   o.st = st;
   unsigned long long vm0 = 0ull, vm1 = 0ull, vv0 = 0ull, vv1 = 0ull;
   if (st == 0) {
@@ -4618,18 +4656,21 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
         t.rmem += x.mem;
         t.reph += x.eph;
         t.npods += 1;
+        const int64_t* add = vsc(x);
         const bool tpo = port || conf(x.port[0]) || conf(x.port[1]);
-        const uint32_t k = moves ? counts(q) : 0u;
-        PreemptTopo tt = tp;
+        const uint32_t k = moves ? topo_counts(m, base, d, T, x.slot, &o.flags) : 0u;
+        PreemptTopo tt = T.tp;
 #pragma unroll
         for (int c = 0; c < kPreemptCons; ++c) tt.dlt[c] += (k >> c) & 1u;
-        const bool im = moves && ipa_apply(q, tt, +1);
-        bool fits = preempt_node_filters(m, t, sreq, base, d, i, tpo) == 0;
+        const bool im = moves && topo_ipa(m, base, d, T, in, x.slot, tt, +1);
+        bool fits = preempt_node_filters(m, t, sreq, add, base, d, i, tpo) == 0;
         if (fits && (k || im)) fits = topo_filters(m, base, d, i, tt, 0) == 0;
         if (fits) {
           nc = t;
+          if (add)
+            for (int kk = 0; kk < ns; ++kk) sreq[kk] += add[kk];
           port = tpo;
-          tp = tt;
+          T.tp = tt;
         } else {
           (q < 64 ? vm0 : vm1) |= 1ull << (q & 63);
           o.nvictims += 1;

@@ -598,6 +598,7 @@ class Engine {
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)
   DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick, d_contrib_buf;
+  DevBuf d_vsc;  // preemption: the pods' requests of the preemptor's extended resources + the per-node scratch
   std::vector<PRec> h_seg;
   std::vector<int32_t> h_segcnt;
   std::vector<std::vector<const BoundPod*>> seg_pods;

@@ -29,7 +29,7 @@ hipError_t launch_aggregate(const MirrorView& m, const BatchView& b, int pod, co
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
                                hipEvent_t t1, int blk0, int nblk, bool lds);
 hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, const PNode* pn, const PVictim* pv,
-                          uint8_t* vout, POut* out, int all_nodes, hipStream_t s);
+                          uint8_t* vout, POut* out, int all_nodes, const PreemptIn& in, hipStream_t s);
 hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s);
 hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* mm, hipStream_t s);
 hipError_t launch_aff_totals(const BatchView& b, int pod, int nterms, long long* out, hipStream_t s);
@@ -302,27 +302,20 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   int rc = compile(p, CYCLE, -1, false, true, &cp);
   if (rc) return rc;
   const PodDesc& D = *reinterpret_cast<const PodDesc*>(cp.blob.data());
-  if (D.n_scalar > kPreemptScalar) {
-    c->err = "preemption: the pod requests more than 4 scalar resources";
-    return KSG_ENOTSUP;
-  }
 
   const bool pts_on = (D.filter_mask >> P_PTS & 1u) && D.n_ptsf > 0;
-  const bool ipa_req = !p.aff_req.empty() || !p.anti_req.empty();
   const bool ports_on = (D.filter_mask >> P_PORTS) & 1u;
   int32_t nom_ix = p.nominated_node.empty() ? -1 : c->index_of(p.nominated_node);
   if (N > 0 && (rc = c->ensure_mirror())) return rc;
   // The device-resident segments serve every pod whose victims' order the cache already knows (no pod
-  // sorted by the call's clock, see seg_build) and that the device groups itself: no scalar requests, at
-  // most kMaxPdb budgets.  The rest take the host-staged records (same kernel core, which declines
-  // victims that move PodTopologySpread / InterPodAffinity counts).
-  bool seg = N > 0 && !staged && D.n_scalar == 0 && pdbs.size() <= (size_t)kMaxPdb &&
-             (c->nostart_pods == 0 || now > c->max_start_ns);
+  // sorted by the call's clock, see seg_build) and that the device groups itself: at most kMaxPdb budgets.
+  // The rest take the host-staged records (the same per-node core, k_preempt).
+  bool seg = N > 0 && !staged && pdbs.size() <= (size_t)kMaxPdb && (c->nostart_pods == 0 || now > c->max_start_ns);
   const bool ipa_on = (D.filter_mask >> P_IPA) & 1u;
   if (seg && (rc = seg_refresh())) return rc;
   seg = seg && seg_overflow == 0 && (!ports_on || seg_many_ports == 0);
 
-  struct NodeOut { uint32_t st; int32_t nvictims, nviolating; };
+  struct NodeOut { uint32_t st; int32_t nvictims, nviolating; uint32_t flags; };
   std::vector<NodeOut> po((size_t)std::max(N, 1));
   uint32_t nom_status = 0;
   // staged path: the potential victims of every node, in reprieve order
@@ -357,6 +350,56 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     PCHK(launch_filter_score(m, bv, 0, s, nullptr, nullptr, 0, -1, cp.blob.size() <= (size_t)kBlobLds));
     return KSG_OK;
   };
+  // what both kernels read about the victims beyond Requested (PreemptIn): the cycle's DoNotSchedule minima,
+  // the self-matching affinity totals, the existing anti-affinity terms per victim slot, and the victims'
+  // requests of the preemptor's extended resources; d_pdb's head holds the minima and totals
+  PreemptIn pin{};
+  auto topo_prelude = [&]() -> int {
+    const size_t mm_b = 8 * 4 * kPreemptCons;  // k_pts_minima's [3 kPreemptCons], then k_aff_totals' [kPreemptCons]
+    if ((rc = ensure(d_pdb, mm_b + 64))) return rc;
+    long long* d_mm = (long long*)d_pdb.p;
+    const bool pts_minima = pts_on && D.n_ptsf <= kPreemptCons;
+    if (pts_minima) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
+    // a preemptor matching its own required affinity terms: the cycle's per-term totals (PreemptTopo::any)
+    const bool aff_tot = ipa_on && (D.ipa_flags & IPA_SELF_ALL) && D.n_raff > 0 && D.n_raff <= kPreemptCons;
+    if (aff_tot) PCHK(launch_aff_totals(bv, 0, D.n_raff, d_mm + 3 * kPreemptCons, s));
+    // existing pods' required anti-affinity terms matching the preemptor, per slot and key
+    const bool terms = ipa_on && D.n_exkeys > 0 && m.n_terms > 0;
+    if (terms) {
+      const size_t cb = sizeof(int32_t) * kPreemptCons * (size_t)std::max(m.pods_hw, 1);
+      if ((rc = ensure(d_contrib_buf, cb + 64))) return rc;
+      PCHK(hipMemsetAsync(d_contrib_buf.p, 0, cb + 4, s));
+      // (a term beyond kPreemptCons keys also has n_exkeys > kPreemptCons, so the dry run flags every node:
+      // it counts only where the dry run reaches, at or before its cut)
+      PCHK(launch_preempt_terms(m, bv, 0, (int32_t*)d_contrib_buf.p, (uint32_t*)((uint8_t*)d_contrib_buf.p + cb), s));
+    }
+    pin.pts_check = pts_on ? 1 : 0;
+    pin.ipa_check = ipa_on ? 1 : 0;
+    pin.pts_mm = d_mm;
+    pin.aff_tot = aff_tot ? d_mm + 3 * kPreemptCons : nullptr;
+    pin.ex_contrib = terms ? (const int32_t*)d_contrib_buf.p : nullptr;
+    if (D.n_scalar > 0 && N > 0) {
+      // each pod's request of the preemptor's extended resources, by pod-table slot (only pods that request
+      // extended resources have non-zero rows), and the kernels' per-node scratch of the node's Requested
+      const int ns = D.n_scalar;
+      const ScalarReq* sr = reinterpret_cast<const ScalarReq*>(cp.blob.data() + D.scalar_off);
+      std::vector<int64_t> vsc((size_t)std::max(m.pods_hw, 1) * ns, 0);
+      for (auto& kv : c->pods) {
+        const BoundPod& bp = kv.second;
+        if (bp.res.scalar.empty() || bp.slot < 0 || bp.slot >= m.pods_hw) continue;
+        for (int k = 0; k < ns; ++k)
+          for (auto& sv : bp.res.scalar)
+            if (sv.first == c->scalar_ix.strs[sr[k].slot]) vsc[(size_t)bp.slot * ns + k] += sv.second;
+      }
+      const size_t vb = vsc.size() * 8, sb = (size_t)N * ns * 8;
+      if ((rc = ensure(d_vsc, vb + sb + 64))) return rc;
+      PCHK(hipMemcpyAsync(d_vsc.p, vsc.data(), vb, hipMemcpyHostToDevice, s));
+      PCHK(hipStreamSynchronize(s));  // pageable source
+      pin.vsc = (const int64_t*)d_vsc.p;
+      pin.sreq = (int64_t*)((uint8_t*)d_vsc.p + ((vb + 63) & ~(size_t)63));
+    }
+    return KSG_OK;
+  };
   auto finish_device = [&]() -> int {
     if (D.arena_words) PCHK(hipMemsetAsync(d_arena.p, 0, (size_t)D.arena_words * 8, s));  // k_select did not run
     if (nom_ix >= 0) PCHK(hipMemcpyAsync(&nom_status, bv.status + nom_ix, 4, hipMemcpyDeviceToHost, s));
@@ -383,29 +426,10 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
           if (pdbs[k].disrupted.count(kv.second.name)) dis[kv.second.slot] |= (uint8_t)(1u << k);
     }
     if ((rc = stage_pod())) return rc;
-    const size_t mm_b = 8 * 4 * kPreemptCons;  // k_pts_minima's [3 kPreemptCons], then k_aff_totals' [kPreemptCons]
+    const size_t mm_b = 8 * 4 * kPreemptCons;  // the prelude's minima and totals, then the budgets
     const size_t pd_b = sizeof(PdbDev) * pd.size(), pool_b = 4 * pool.size(), dis_b = dis.size();
     if ((rc = ensure(d_pdb, mm_b + pd_b + pool_b + dis_b + 64))) return rc;
-    long long* d_mm = (long long*)d_pdb.p;  // k_pts_minima's output, then the budgets
-    const bool pts_minima = pts_on && D.n_ptsf <= kPreemptCons;
-    if (pts_minima) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
-    // a preemptor matching its own required affinity terms: the cycle's per-term totals (PreemptTopo::any)
-    const bool aff_tot = ipa_on && (D.ipa_flags & IPA_SELF_ALL) && D.n_raff > 0 && D.n_raff <= kPreemptCons;
-    if (aff_tot) PCHK(launch_aff_totals(bv, 0, D.n_raff, d_mm + 3 * kPreemptCons, s));
-    // existing pods' required anti-affinity terms matching the preemptor, per slot and key
-    int32_t* d_contrib = nullptr;
-    uint32_t* d_tunsup = nullptr;
-    const bool terms = ipa_on && D.n_exkeys > 0 && m.n_terms > 0;
-    if (terms) {
-      const size_t cb = sizeof(int32_t) * kPreemptCons * (size_t)std::max(m.pods_hw, 1);
-      if ((rc = ensure(d_contrib_buf, cb + 64))) return rc;
-      d_contrib = (int32_t*)d_contrib_buf.p;
-      d_tunsup = (uint32_t*)((uint8_t*)d_contrib_buf.p + cb);
-      PCHK(hipMemsetAsync(d_contrib_buf.p, 0, cb + 4, s));
-      // (a term beyond kPreemptCons keys also has n_exkeys > kPreemptCons, so k_preempt_seg flags every
-      // node: the pick counts the flag only where the dry run reaches, at or before its cut)
-      PCHK(launch_preempt_terms(m, bv, 0, d_contrib, d_tunsup, s));
-    }
+    if ((rc = topo_prelude())) return rc;
     if ((rc = ensure(d_psout, sizeof(PSegOut) * (size_t)N))) return rc;
     uint8_t* dp = (uint8_t*)d_pdb.p + mm_b;
     if (pd_b) PCHK(hipMemcpyAsync(dp, pd.data(), pd_b, hipMemcpyHostToDevice, s));
@@ -421,12 +445,8 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     v.npdb = (int32_t)pd.size();
     v.prio = p.priority;
     v.all_nodes = all_nodes ? 1 : 0;
-    v.pts_check = pts_on ? 1 : 0;
     v.now = now;
-    v.pts_mm = d_mm;
-    v.ex_contrib = d_contrib;
-    v.aff_tot = aff_tot ? d_mm + 3 * kPreemptCons : nullptr;
-    v.ipa_check = ipa_on ? 1 : 0;
+    v.in = pin;
     PCHK(launch_preempt_seg(m, bv, 0, v, s));
     if ((rc = ensure(d_pick, sizeof(PickOut) + 4 * (size_t)N + 64))) return rc;
     PickOut* d_po = (PickOut*)d_pick.p;
@@ -442,7 +462,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
                "what the device tracks (more than 8 constraints, terms or keys)";
       return KSG_ENOTSUP;
     }
-    for (int32_t i = 0; list && i < N; ++i) po[i] = NodeOut{so[i].st, so[i].nvictims, so[i].nviolating};
+    for (int32_t i = 0; list && i < N; ++i) po[i] = NodeOut{so[i].st, so[i].nvictims, so[i].nviolating, so[i].flags};
   } else {
     // ---- host-staged records: the potential victims of every node, in reprieve order
     pn.assign((size_t)std::max(N, 1), PNode{});
@@ -450,12 +470,6 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     auto conflicts = [&](uint32_t pid) {
       return ports_on && (int32_t)(pid >> 5) < D.n_port_words && ((conflict[pid >> 5] >> (pid & 31u)) & 1u);
     };
-    const int32_t pns = c->ns_id(p.ns);
-    std::vector<std::string> scal;  // the preemptor's scalar resources in PodDesc order
-    {
-      const ScalarReq* sr = reinterpret_cast<const ScalarReq*>(cp.blob.data() + D.scalar_off);
-      for (int k = 0; k < D.n_scalar; ++k) scal.push_back(c->scalar_ix.strs[sr[k].slot]);
-    }
     std::vector<Victim> vs;
     for (int32_t i = 0; i < N; ++i) {
       NodeRec* r = c->node(order[i]);
@@ -467,20 +481,6 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
         if (bp.priority < p.priority) vs.push_back(Victim{&uid, &bp, bp.has_start ? bp.start_ns : now, false});
       }
       if (vs.empty()) continue;
-      // PodTopologySpread / InterPodAffinity counts a victim could change (their RemovePod/AddPod
-      // extensions) are outside what k_preempt re-evaluates: refuse rather than approximate
-      for (const Victim& v : vs) {
-        if (pts_on && c->pt_ns[v.bp->slot] == pns)
-          for (auto& sp : p.spreads)
-            if (sp.when == "DoNotSchedule" && sp.sel.present && lsel_match_slot(*c, sp.sel, v.bp->slot)) {
-              c->err = "preemption: a victim changes the pod's PodTopologySpread counts (not supported on the device)";
-              return KSG_ENOTSUP;
-            }
-        if (ipa_req || v.bp->req_anti) {
-          c->err = "preemption: InterPodAffinity terms between the pod and a victim (not supported on the device)";
-          return KSG_ENOTSUP;
-        }
-      }
       std::stable_sort(vs.begin(), vs.end(), more_important);  // sort.Slice (:309-311), see header
       // filterPodsWithPDBViolation (:406-452) over the sorted list
       std::vector<int32_t> allowed(pdbs.size());
@@ -502,9 +502,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
         x.cpu = v.bp->res.cpu;
         x.mem = v.bp->res.mem;
         x.eph = v.bp->res.eph;
-        for (size_t k = 0; k < scal.size(); ++k)
-          for (auto& sv : v.bp->res.scalar)
-            if (sv.first == scal[k]) x.sc[k] += sv.second;
+        x.slot = v.bp->slot;
         for (uint32_t pid : v.bp->port_ids) {
           vports.insert(pid);
           if (conflicts(pid)) x.flags |= PV_PORT;
@@ -523,6 +521,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     vo.assign((size_t)std::max(V, 1), 0);
     if (N > 0) {
       if ((rc = stage_pod())) return rc;
+      if ((rc = topo_prelude())) return rc;
       const size_t pn_b = sizeof(PNode) * (size_t)N, pv_b = sizeof(PVictim) * (size_t)std::max(V, 1);
       const size_t po_b = sizeof(POut) * (size_t)N, vo_b = (size_t)std::max(V, 1);
       if ((rc = ensure(d_pre, pn_b + pv_b + po_b + vo_b + 64))) return rc;
@@ -533,12 +532,12 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       uint8_t* d_vo = dp + pn_b + pv_b + po_b;
       PCHK(hipMemcpyAsync(d_pn, pn.data(), pn_b, hipMemcpyHostToDevice, s));
       if (V) PCHK(hipMemcpyAsync(d_pv, pv.data(), pv_b, hipMemcpyHostToDevice, s));
-      PCHK(launch_preempt(m, bv, 0, d_pn, d_pv, d_vo, d_po, all_nodes ? 1 : 0, s));
+      PCHK(launch_preempt(m, bv, 0, d_pn, d_pv, d_vo, d_po, all_nodes ? 1 : 0, pin, s));
       PCHK(hipMemcpyAsync(pout.data(), d_po, po_b, hipMemcpyDeviceToHost, s));
       if (V) PCHK(hipMemcpyAsync(vo.data(), d_vo, vo_b, hipMemcpyDeviceToHost, s));
       if ((rc = finish_device())) return rc;
     }
-    for (int32_t i = 0; i < N; ++i) po[i] = NodeOut{pout[i].st, pout[i].nvictims, pout[i].nviolating};
+    for (int32_t i = 0; i < N; ++i) po[i] = NodeOut{pout[i].st, pout[i].nvictims, pout[i].nviolating, pout[i].flags};
   }
   // ---- 1) PodEligibleToPreemptOthers, the nominated-node half (:369-386)
   if (nom_ix >= 0 && status_code(nom_status) != KSG_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE) {
@@ -572,12 +571,19 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     ncand = (int32_t)n;
     // DryRunPreemption (:404-457) with sequential semantics: stop once a non-violating candidate is
     // held and both lists (each capped at numCandidates) reach numCandidates together
+    bool unsup = false;  // a node the dry run reaches whose result the device could not compute (flag bit 0)
     for (int32_t j = 0; j < P; ++j) {
       const int32_t i = pot[(offset + j) % P];
+      unsup |= (po[i].flags & 1u) != 0;
       if (po[i].st != 0 || po[i].nvictims == 0) continue;
       std::vector<Cand>& l = po[i].nviolating == 0 ? nv : vl;
       if ((int32_t)l.size() < ncand) l.push_back(Cand{i, po[i].nviolating});
       if (!nv.empty() && (int32_t)(nv.size() + vl.size()) >= ncand) break;
+    }
+    if (unsup && !seg) {
+      c->err = "preemption: a victim's effect on the pod's PodTopologySpread / InterPodAffinity counts is outside "
+               "what the device tracks (more than 8 constraints, terms or keys)";
+      return KSG_ENOTSUP;
     }
   }
   std::vector<Cand> cands = nv;
