@@ -11,7 +11,9 @@
 #   bench=<wl>[:steps]  bench.py --workload <wl> (c1 c2 c2pct0 c3 c4 c4-anti c5 dts), 3 steps by default
 #   prof=<wl>           rocprofv3 --kernel-trace --stats of a short bench run of <wl>
 #   pmc=<wl>            FETCH_SIZE and WRITE_SIZE passes (separate rocprofv3 runs) of <wl>
+#   sq=<wl>             one shader-counter pass (instruction mix, wave cycles, clock) of <wl>
 #   py=<script>[:args]  python3 -u scripts/<script> args (probes); ',' in args becomes ' '
+#   repeat=<n>:<script>[:args]  the probe in n fresh processes (e.g. the in-process device-exchange start)
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
 step() {  # name seconds cmd...
@@ -44,6 +46,14 @@ for s in "$@"; do
         python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline
       step "pmcw_$wl" 300 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/prof/pmc_write_$wl" -o run -- \
         python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline ;;
+    sq=*)
+      wl=${s#sq=}
+      step "sq_$wl" 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        GRBM_GUI_ACTIVE GRBM_COUNT -d "gpurun_out/prof/pmc_sq_$wl" -o run -- \
+        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline ;;
+    repeat=*)
+      a=${s#repeat=}; n=${a%%:*}; rest=${a#*:}; sc=${rest%%:*}; args=""; [ "$rest" != "$sc" ] && args=${rest#*:}
+      for k in $(seq 1 "$n"); do step "repeat_${sc%.py}_$k" 200 python3 -u "scripts/$sc" ${args//,/ }; done ;;
     py=*)
       a=${s#py=}; sc=${a%%:*}; args=""; [ "$a" != "$sc" ] && args=${a#*:}
       step "py_${sc%.py}" 400 python3 -u "scripts/$sc" ${args//,/ } ;;

@@ -83,7 +83,7 @@ def main():
         fn = f"traffic_{kn}_{workload}.json" if kn == "k_agg_loop" else f"traffic_{kn}.json"
         json.dump(t, open(os.path.join(out, fn), "w"), indent=1)
 
-    # shader-counter pass (scripts/gpu_prof_sq.sh): instruction mix per wave and per pod, clock
+    # shader-counter pass (scripts/gpu.sh sq=<workload>): instruction mix per wave and per pod, clock
     p = os.path.join(PROF, "pmc_sq", "run_results.db")
     if os.path.exists(p):
         cc = sqlite3.connect(p)
