@@ -293,6 +293,13 @@ int ksg_debug_log_table(double *out, int32_t n);
  * to re-resolve node names to snapshot indices (ksg_node_name). */
 int ksg_generation(const ksg_ctx *ctx, uint64_t *list_gen, uint64_t *events);
 
+/* Measurement helper: ksg_schedule_one(ctx, handles[k], flags, &results[k], NULL) for k = 0..n-1, one call
+ * after the other from native code, as a binding's scheduling goroutine issues them; *us_per_call is the
+ * mean wall time of one call (the per-pod API's latency without an interpreter's call overhead).  Stops at
+ * the first call that fails and returns its code. */
+int ksg_debug_schedule_calls(ksg_ctx *ctx, const int32_t *handles, int32_t n, uint32_t flags, ksg_result *results,
+                             double *us_per_call);
+
 /* The requests the library derives from one v1.Pod (no context, no device): out[0..4] are
  * CalculateResource's Requested MilliCPU / Memory / EphemeralStorage and Non0CPU / Non0Mem
  * (pkg/scheduler/framework/types.go:1035-1076, with the in-place resize status resources of

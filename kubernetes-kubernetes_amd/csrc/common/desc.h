@@ -519,9 +519,18 @@ struct RingTerm {
   DTerm d;
 };
 constexpr int kRingEntryBytes = 8192;
+// k_agg_loop's doorbell is four self-tagged words instead of ctl (ll[k] = {tag = q + 1 | data << 32}, each
+// 8-byte store atomic on its own, so the loop takes them in one poll without a second read over PCIe):
+//   ll[0] data: RING_SAME (pod q is pod q-1's program and entry but for the fields below: nothing is staged,
+//               the loop copies q-1's from LDS and patches them) | RING_AGG_SAME (the program's DF_AGG_SAME);
+//   ll[1..3]:   RING_SAME: {slot, rot_start, entry lbl_off}; else {program bytes, entry bytes, 0}.
+// A stop is ll[0]'s tag kRingStop.
+enum : uint32_t { RING_SAME = 1u, RING_AGG_SAME = 2u };
+constexpr int kRingLL = 4;
 struct alignas(128) PodRing {
   unsigned long long ctl;  // [host] {pods posted | program bytes << 32 | entry bytes << 48} or kRingStop
-  uint32_t pad0[30];
+  unsigned long long ll[kRingLL];  // [host] k_agg_loop's doorbell (above)
+  uint32_t pad0[22];
   uint32_t exited;         // [device] 1: the loop left on its own (idle / pod limit)
   uint32_t pad1[31];
   RingResult res[kRingSlots];

@@ -1666,6 +1666,29 @@ __device__ __forceinline__ int ring_wait_p(PodRing* ring, int q, int npods, unsi
     __builtin_amdgcn_s_sleep(2);
   }
 }
+// k_agg_loop's doorbell (desc.h PodRing::ll), polled by one wave: lanes 0..3 load the four tagged words in
+// one instruction until every tag reads q + 1; lane k's data word into *data.  -1: stop, idle or no pod left.
+__device__ __forceinline__ int ring_wait_ll(PodRing* ring, int q, int npods, unsigned long long idle, int lane,
+                                            uint32_t* data) {
+  if (q >= npods) return -1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t spins = 0;; ++spins) {
+    const unsigned long long v =
+        lane < kRingLL ? __hip_atomic_load(&ring->ll[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    const uint32_t tag = (uint32_t)v;
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)tag) == kRingStop) return -1;
+    const unsigned long long ok = __ballot(lane < kRingLL && tag == (uint32_t)(q + 1));
+    if (ok == (1ull << kRingLL) - 1ull) {
+      *data = (uint32_t)(v >> 32);
+      return 0;
+    }
+    if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > idle) {
+      if (blockIdx.x == 0 && lane == 0) __hip_atomic_store(&ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 __device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
   const int v = ring_wait_p(lv.ring, q, lv.npods, lv.ring_idle);
   return v < 0 ? v : (v & 0xffff);
@@ -2747,7 +2770,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ int s_p2n;
   __shared__ int64_t s_mx[4];
   __shared__ uint32_t s_pmult[kAggMaxCons];  // DoNotSchedule: present domains at the minimum
-  __shared__ int s_ring_bytes;                // resident mode: {program bytes | entry bytes << 16}, -1: the end
+  __shared__ uint32_t s_ll[kRingLL];          // resident mode: the doorbell's data words (desc.h PodRing::ll)
+  __shared__ int s_ring_end;                  // resident mode: -1: the launch ends
+  __shared__ int s_pb, s_eb;                  // resident mode: the last staged program's / entry's bytes
+  __shared__ int s_spec_q;                    // resident mode: the counts hold pod s_spec_q's plus its placement
   const int w = blockIdx.x, G = av.nwg;
   const int P = SHARD ? av.world * G : G, gid = SHARD ? av.rank * G + w : w;  // participants (rank-major), mine
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
@@ -3083,11 +3109,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   // The fold plan of pod q into pod q + 1 (one wave, lanes gl): pod q as an existing pod of q+1 --
   // its labels against q+1's selectors, its own terms against q+1 -- exactly what q+1's aggregation
   // would count for it, less the chosen node's label values (looked up once the node is known).
-  auto plan_fold = [&](int q, int gl) __attribute__((always_inline)) {
+  // (plan_fold_b: the placed pod's program bp, the next pod's base)
+  auto plan_fold_b = [&](const uint8_t* bp, const uint8_t* base, int gl) __attribute__((always_inline)) {
     asm volatile("" : "+v"(gl));  // lane-dependent item selection stays in the loop (register pressure)
-    const uint8_t* bp = s_blob[q % 3];
     const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
-    const uint8_t* base = s_blob[(q + 1) % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
     const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
     const unsigned long long* pl = at<unsigned long long>(bp, dp.lbl_off);
@@ -3154,6 +3179,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     }
   };
+  auto plan_fold = [&](int q, int gl) __attribute__((always_inline)) { plan_fold_b(s_blob[q % 3], s_blob[(q + 1) % 3], gl); };
   // the owner of pod q's node adds it (and its own terms) to my lists: one thread
   auto append = [&](int q, int lq) __attribute__((always_inline)) {
     const uint8_t* bp = s_blob[q % 3];
@@ -3166,6 +3192,34 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_np = np + 1;
     s_nt = nt + k2;
     if (np >= pcap || k2 < (uint32_t)dp.n_own_terms) fail(0xfffffffdu);  // host-checked
+  };
+  // fold the placed pod (the plan in s_fi, the chosen node's label values in s_fv, its eligibility s_el) into
+  // the next pod's counts: shared ones everywhere, node-local ones at the owner (local slot lq); one wave
+  auto fold_pod = [&](int lq) __attribute__((always_inline)) {
+    if (s_gnode < 0) return;
+    const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+    const uint32_t el = s_el;
+    uint32_t any = 0;
+    for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) {
+      const FoldItem it = s_fi[k];
+      const int32_t v = s_fv[k] >= 0 ? s_fv[k] : it.absent;  // absent: the "" domain (DF_PTS_ANYTOPO)
+      if (v < 0 || (it.cons >= 0 && !((el >> it.cons) & 1u))) continue;
+      if (it.lref >= 0) {
+        const unsigned long long old = atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
+        if (it.cons >= 0 && it.cons < 8) {  // a DoNotSchedule domain count went up by one: its minimum moves
+          const int c = it.cons;  // only if this was the minimum's one domain (one item per constraint)
+          if ((long long)old == s_pmin[c]) {
+            if (s_pmult[c] == 1u) s_pmin[c] = (long long)old + 1;
+            else s_pmult[c] -= 1u;
+          }
+        }
+      } else if (lq >= 0) {
+        atomicAdd(&s_lh[(-1 - it.lref) * kAggSlots + lq], it.wt);
+      }
+      any |= it.anyb;
+    }
+    for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
+    if (lane == 0) s_any |= any;
   };
   auto wg_bar = [&]() __attribute__((always_inline)) { __syncthreads(); };
 
@@ -3198,6 +3252,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_px_q = -1;
     s_pxd_q = -1;
     s_elig_q = -1;
+    s_spec_q = -1;
+    s_pb = 0;
+    s_eb = 0;
   }
   __syncthreads();
   for (int s = t; s < m.pods_hw; s += kAggThreads) {
@@ -3255,12 +3312,39 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     if constexpr (RING) {
       // ======== resident mode: pod q from the ring (host memory, bypassing the device caches): its program
       // into s_blob[q % 3], its pod-table entry into s_blob[(q + 1) % 3]; then its counts ========
-      if (t == 0) s_ring_bytes = ring_wait_p(av.ring, q, av.npods, av.ring_idle);
+      if (wave == 0) {
+        uint32_t v = 0;
+        const int r = ring_wait_ll(av.ring, q, av.npods, av.ring_idle, lane, &v);
+        if (lane < kRingLL) s_ll[lane] = v;
+        if (lane == 0) s_ring_end = r;
+      }
+      stamp(q, 9);
       __syncthreads();
-      const int rb = s_ring_bytes;
-      if (rb < 0) return;
-      {
-        const int pw8 = (rb & 0xffff) / 8, ew8 = (rb >> 16) / 8;
+      if (s_ring_end < 0) return;
+      const uint32_t rmode = s_ll[0];
+      if (rmode & RING_SAME) {
+        // pod q-1's program and entry but for the slot, the rotation and the label-pool offset (the host
+        // compared the rest byte for byte): copied in LDS -- the entry first, its buffer takes the program
+        const int pw8 = s_pb / 8, ew8 = s_eb / 8;
+        unsigned long long* ed = reinterpret_cast<unsigned long long*>(s_blob[(q + 1) % 3]);
+        const unsigned long long* es_ = reinterpret_cast<const unsigned long long*>(s_blob[q % 3]);
+        for (int k = t; k < ew8; k += kAggThreads) ed[k] = es_[k];
+        __syncthreads();
+        unsigned long long* pd = reinterpret_cast<unsigned long long*>(s_blob[q % 3]);
+        const unsigned long long* ps_ = reinterpret_cast<const unsigned long long*>(s_blob[(q + 2) % 3]);
+        for (int k = t; k < pw8; k += kAggThreads) pd[k] = ps_[k];
+        __syncthreads();
+        if (t == 0) {
+          PodDesc& dn = *reinterpret_cast<PodDesc*>(s_blob[q % 3]);
+          dn.slot = (int32_t)s_ll[1];
+          dn.rot_start = (int32_t)s_ll[2];
+          dn.flags = (dn.flags & ~DF_AGG_SAME) | ((rmode & RING_AGG_SAME) ? DF_AGG_SAME : 0u);
+          RingEntry& en = *reinterpret_cast<RingEntry*>(ed);
+          en.slot = ew8 ? (int32_t)s_ll[1] : -1;
+          en.lbl_off = s_ll[3];
+        }
+      } else {
+        const int pw8 = (int)s_ll[1] / 8, ew8 = (int)s_ll[2] / 8;
         const unsigned long long* ps_ = reinterpret_cast<const unsigned long long*>(av.ring->blob[q % kRingSlots]);
         const unsigned long long* es_ = reinterpret_cast<const unsigned long long*>(av.ring->entry[q % kRingSlots]);
         unsigned long long* pd = reinterpret_cast<unsigned long long*>(s_blob[q % 3]);
@@ -3269,17 +3353,29 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           if (k < pw8) pd[k] = __hip_atomic_load(ps_ + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           else ed[k - pw8] = __hip_atomic_load(es_ + (k - pw8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        if (t == 0 && ew8 == 0) reinterpret_cast<RingEntry*>(ed)->slot = -1;
+        if (t == 0) {
+          if (ew8 == 0) reinterpret_cast<RingEntry*>(ed)->slot = -1;
+          s_pb = pw8 * 8;
+          s_eb = ew8 * 8;
+        }
       }
       __syncthreads();
-      aggregate(q, t, kAggThreads, wg_bar);
-      if (wave == 0) sweep_z(q);
-      __syncthreads();
-      if (!s_ok) return;
-      load_totals(q, t, kAggThreads);
-      __syncthreads();
-      minima(q);
-      __syncthreads();
+      stamp(q, 13);
+      // the same template as pod q-1 (host: DF_AGG_SAME): pod q's counts are q-1's plus q-1's placement,
+      // folded into the counts in LDS at the end of pod q-1 already (s_spec_q)
+      const PodDesc& dq = *reinterpret_cast<const PodDesc*>(s_blob[q % 3]);
+      if (!((dq.flags & DF_AGG_SAME) && s_spec_q == q - 1 && q > 0)) {
+        aggregate(q, t, kAggThreads, wg_bar);
+        if (wave == 0) sweep_z(q);
+        __syncthreads();
+        if (!s_ok) return;
+        stamp(q, 14);
+        load_totals(q, t, kAggThreads);
+        __syncthreads();
+        stamp(q, 15);
+        minima(q);
+        __syncthreads();
+      }
     }
     if (q == av.give_up_at) {  // diagnostic: as if a workgroup never arrived (host recovery test)
       if (t == 0) fail((uint32_t)q);
@@ -3637,6 +3733,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
                 __builtin_amdgcn_s_sleep(1);
               el = s_elig[wn - nlo];
             }
+          } else if (RING && wn >= 0 && (d.n_ptsf || d.n_ptss)) {
+            el = s_elig[wn - nlo];  // resident: a fold into the next pod is of this pod's template
           }
           agran_put<SHARD>(av, q, gid, AG_BN, (unsigned long long)(uint32_t)(wn + 1) | ((unsigned long long)el << 32));
         }
@@ -3691,7 +3789,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             }
           }
           // the chosen node and its eligibility for the fold, to the gathering group
-          if (sp1) {
+          if (sp1 || RING) {
             const bool placed = okb && F > 0 && pw >= 0 && (d.flags & DF_ASSUME) && d.slot >= 0;
             s_gnode = placed ? (int)bnlo - 1 : -1;
             s_el = placed ? bnhi : 0u;
@@ -3763,32 +3861,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         stamp(q, 6);
         stamp(q, 7);
         if (wave == 0) {
-          const int nq = s_gnode;
-          if (nq >= 0) {  // fold pod q into q+1's counts: shared ones everywhere, node-local ones at the owner
-            const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
-            const uint32_t el = s_el;
-            uint32_t any = 0;
-            for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) {
-              const FoldItem it = s_fi[k];
-              const int32_t v = s_fv[k] >= 0 ? s_fv[k] : it.absent;  // absent: the "" domain (DF_PTS_ANYTOPO)
-              if (v < 0 || (it.cons >= 0 && !((el >> it.cons) & 1u))) continue;
-              if (it.lref >= 0) {
-                const unsigned long long old = atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
-                if (it.cons >= 0 && it.cons < 8) {  // a DoNotSchedule domain count went up by one: its minimum moves
-                  const int c = it.cons;  // only if this was the minimum's one domain (one item per constraint)
-                  if ((long long)old == s_pmin[c]) {
-                    if (s_pmult[c] == 1u) s_pmin[c] = (long long)old + 1;
-                    else s_pmult[c] -= 1u;
-                  }
-                }
-              } else if (lq >= 0) {
-                atomicAdd(&s_lh[(-1 - it.lref) * kAggSlots + lq], it.wt);
-              }
-              any |= it.anyb;
-            }
-            for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
-            if (lane == 0) s_any |= any;
-          }
+          fold_pod(lq);
           if (same1) {  // the minima over the folded counts (no gathered ones to adjust)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             minima_grp(q + 1, 0, 1);
@@ -3813,8 +3886,29 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     } else if (RING) {
       // the next pod arrives through the ring: pod q joins its node owner's lists now, and its entry
-      // (written by the owner's committing thread) is read from L2 by the pods after it
-      if (t == 0 && s_pend_ls >= 0) append(q, s_pend_ls);
+      // (written by the owner's committing thread) is read from L2 by the pods after it.  While the host
+      // turns around, pod q is folded into the counts in LDS as a next pod of its own template would count
+      // it (the plan against q's own program): a next pod marked DF_AGG_SAME starts from them, any other
+      // gathers afresh.  (q's own terms would be read from the table the owner wrote: not for pods with them.)
+      if (wave == 0) {
+        const bool sp = (d.flags & DF_AGGREGATE) && spec(d) && d.n_own_terms == 0 && !(av.debug & 4);
+        if (sp) {
+          plan_fold_b(s_blob[q % 3], s_blob[q % 3], lane);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const int nq = s_gnode;
+          const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+          for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          fold_pod(s_pend_ls);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          minima_grp(q, 0, 1);
+        }
+        if (lane == 0) {
+          if (s_pend_ls >= 0) append(q, s_pend_ls);
+          s_nfi = 0;
+          s_spec_q = sp ? q : -1;
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

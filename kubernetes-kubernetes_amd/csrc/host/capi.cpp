@@ -397,6 +397,16 @@ int ksg_generation(const ksg_ctx* ctx, uint64_t* list_gen, uint64_t* events) {
   return KSG_OK;
 }
 
+int ksg_debug_schedule_calls(ksg_ctx* ctx, const int32_t* handles, int32_t n, uint32_t flags, ksg_result* results,
+                             double* us_per_call) {
+  if (!ctx || n < 0 || (n && (!handles || !results)) || !us_per_call) return KSG_EINVAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int32_t k = 0; k < n; ++k)
+    if (const int rc = ksg_schedule_one(ctx, handles[k], flags, results + k, nullptr)) return rc;
+  *us_per_call = n ? std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / n : 0.0;
+  return KSG_OK;
+}
+
 int ksg_debug_pod_resources(const char* pod_json, size_t len, int64_t* out, int32_t cap) {
   using namespace ksg;
   if (!pod_json || !out || cap < 8) return KSG_EINVAL;

@@ -1266,10 +1266,6 @@ int Engine::next_gran_tag(uint32_t* tag) {
   return KSG_OK;
 }
 
-// k_agg_loop: pod b's counts are defined exactly as pod a's (DF_AGG_SAME) -- the same program but for the fields
-// the aggregation does not read: the pod-table slot, the rotation and the pod's own affinity terms (the last
-// part of the program; the fold of a adds a's own terms to b's counts).  Pods stamped from one template, as
-// every scheduler_perf workload's are, qualify; anything else only loses the shortcut.
 // The participants (p = rank * g + workgroup) a set names, per rank: "rank 0 wg {0,3-7}; rank 2 wg {0-7}"
 static std::string participants_by_rank(const std::vector<uint8_t>& in, int world, int g) {
   std::string out;
@@ -1307,11 +1303,16 @@ static std::string give_up_detail(const uint32_t* f, const std::vector<unsigned 
          participants_by_rank(now, world, g);
 }
 
-static bool agg_same(const CompiledPod& a, const CompiledPod& b) {
-  if (a.error || b.error || a.blob.size() != b.blob.size() || a.blob.size() < sizeof(PodDesc)) return false;
+// k_agg_loop: pod b's counts are defined exactly as pod a's (DF_AGG_SAME) -- the same program but for the fields
+// the aggregation does not read: the pod-table slot, the rotation and the pod's own affinity terms (the last
+// part of the program; the fold of a adds a's own terms to b's counts).  Pods stamped from one template, as
+// every scheduler_perf workload's are, qualify; anything else only loses the shortcut.
+// (also the resident k_agg_loop's ring pods: a against the pod posted before b to the same launch)
+static bool agg_same(const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
+  if (a.size() != b.size() || a.size() < sizeof(PodDesc)) return false;
   PodDesc x, y;
-  std::memcpy(&x, a.blob.data(), sizeof(PodDesc));
-  std::memcpy(&y, b.blob.data(), sizeof(PodDesc));
+  std::memcpy(&x, a.data(), sizeof(PodDesc));
+  std::memcpy(&y, b.data(), sizeof(PodDesc));
   if (!(x.flags & DF_AGGREGATE) || !(y.flags & DF_AGGREGATE) || x.own_terms_off != y.own_terms_off) return false;
   for (PodDesc* z : {&x, &y}) {
     z->slot = 0;
@@ -1321,10 +1322,12 @@ static bool agg_same(const CompiledPod& a, const CompiledPod& b) {
     z->flags &= ~DF_AGG_SAME;
   }
   if (std::memcmp(&x, &y, sizeof(PodDesc)) != 0) return false;
-  const size_t end = x.own_terms_off > 0 ? std::min((size_t)x.own_terms_off, a.blob.size()) : a.blob.size();
+  const size_t end = x.own_terms_off > 0 ? std::min((size_t)x.own_terms_off, a.size()) : a.size();
   return end <= sizeof(PodDesc) ||
-         std::memcmp(a.blob.data() + sizeof(PodDesc), b.blob.data() + sizeof(PodDesc), end - sizeof(PodDesc)) == 0;
+         std::memcmp(a.data() + sizeof(PodDesc), b.data() + sizeof(PodDesc), end - sizeof(PodDesc)) == 0;
 }
+
+static bool agg_same(const CompiledPod& a, const CompiledPod& b) { return !a.error && !b.error && agg_same(a.blob, b.blob); }
 
 int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                       ksg_result* results, ksg_eval_out* eval) {
@@ -2553,8 +2556,41 @@ int Engine::resident_stop() {
   }
   if (!res_running_) return KSG_OK;
   __atomic_store_n(&ring_->ctl, (unsigned long long)kRingStop, __ATOMIC_RELEASE);
+  __atomic_store_n(&ring_->ll[0], (unsigned long long)kRingStop, __ATOMIC_RELEASE);
   res_running_ = false;
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->cfg.loop_stamps && res_kind_ == 2 && res_q_ > 0 && d_astamps.p) {
+    // k_agg_loop ring pods, workgroup 0's view (us): ring wait -> staged -> counts gathered (+ Z) -> totals ->
+    // minima | phase 1 | A | phase 2 | B publish | B sweep + commit | end of pod
+    std::vector<unsigned long long> st((size_t)res_q_ * kAggStamps);
+    HIPCHK(hipMemcpy(st.data(), d_astamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+    // gathered pods: 9 13 14 15 0 ...; folded pods (DF_AGG_SAME): 9 13 0 ...
+    static const int sg[] = {9, 13, 14, 15, 0, 1, 2, 10, 12, 4, 8}, sf[] = {9, 13, 0, 1, 2, 10, 12, 4, 8};
+    double ag[10] = {0}, af[8] = {0};
+    int cg = 0, cf = 0;
+    for (int q = 0; q < res_q_; ++q) {
+      const unsigned long long* t = &st[(size_t)q * kAggStamps];
+      bool okg = true, okf = !t[14];
+      for (int k : sg) okg = okg && t[k] != 0;
+      for (int k : sf) okf = okf && t[k] != 0;
+      if (okg) {
+        for (int k = 0; k < 10; ++k) ag[k] += (double)(t[sg[k + 1]] - t[sg[k]]) / 100.0;
+        cg++;
+      } else if (okf) {
+        for (int k = 0; k < 8; ++k) af[k] += (double)(t[sf[k + 1]] - t[sf[k]]) / 100.0;
+        cf++;
+      }
+    }
+    if (cg)
+      std::fprintf(stderr, "[k_agg_loop ring stamps, %d gathered pods, us] staging %.2f  gather+Z %.2f  totals %.2f  "
+                   "minima %.2f | phase1 %.2f  A %.2f  phase2 %.2f  publishB %.2f  B+commit %.2f  end %.2f\n", cg,
+                   ag[0] / cg, ag[1] / cg, ag[2] / cg, ag[3] / cg, ag[4] / cg, ag[5] / cg, ag[6] / cg, ag[7] / cg,
+                   ag[8] / cg, ag[9] / cg);
+    if (cf)
+      std::fprintf(stderr, "[k_agg_loop ring stamps, %d folded pods, us] staging %.2f  fold+minima %.2f | phase1 %.2f  "
+                   "A %.2f  phase2 %.2f  publishB %.2f  B+commit %.2f  end %.2f\n", cf, af[0] / cf, af[1] / cf,
+                   af[2] / cf, af[3] / cf, af[4] / cf, af[5] / cf, af[6] / cf, af[7] / cf);
+  }
   return KSG_OK;
 }
 
@@ -2759,6 +2795,12 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       av.fail = (uint32_t*)d_fail.p;
       av.ring = ring_dev_;
       av.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;
+      if (c->cfg.loop_stamps) {  // workgroup 0's phase stamps per ring pod (resident_stop prints them)
+        const size_t sb = (size_t)kLoopMaxPods * kAggStamps * 8;
+        if ((rc = ensure(d_astamps, sb))) return fail(rc);
+        HIPCHK(hipMemsetAsync(d_astamps.p, 0, sb, s));
+        av.stamps = (unsigned long long*)d_astamps.p;
+      }
       HIPCHK(launch_agg_loop(c->view, bview(kLoopMaxPods), av, s, nullptr, nullptr));
       res_gs_ = G;
       res_terms_ = 0;
@@ -2771,13 +2813,61 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
   const auto T1 = clk::now();
   const int q = res_q_;
   const uint32_t bytes = (uint32_t)cp.blob.size();
-  std::memcpy(ring_->blob[q % kRingSlots], cp.blob.data(), bytes);
-  if (entry_bytes) std::memcpy(ring_->entry[q % kRingSlots], entry, entry_bytes);
-  if (kind == 2) res_terms_ += cp.own_terms;
-  __atomic_store_n(&ring_->ctl,
-                   (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)bytes << 32) |
-                       ((unsigned long long)entry_bytes << 48),
-                   __ATOMIC_RELEASE);
+  if (kind == 1) {
+    std::memcpy(ring_->blob[q % kRingSlots], cp.blob.data(), bytes);
+    __atomic_store_n(&ring_->ctl, (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)bytes << 32), __ATOMIC_RELEASE);
+  } else {
+    res_terms_ += cp.own_terms;
+    // the same template as the pod before it in this launch: the loop folds that pod's placement into
+    // the counts it holds instead of gathering them again (k_agg_loop's batch shortcut, DF_AGG_SAME)
+    const bool aggsame = q > 0 && agg_same(res_prev_blob_, cp.blob);
+    PodDesc& hd = *reinterpret_cast<PodDesc*>(cp.blob.data());
+    if (aggsame) hd.flags |= DF_AGG_SAME;
+    // the previous pod's program and entry but for the slot, the rotation and the label-pool offset: the
+    // loop copies them in LDS (PodRing::ll, RING_SAME) instead of reading both over PCIe
+    bool same = q > 0 && res_prev_blob_.size() == cp.blob.size() && res_prev_entry_.size() == entry_bytes;
+    uint32_t lbl_off = 0;
+    if (same) {
+      PodDesc& pd = *reinterpret_cast<PodDesc*>(res_prev_blob_.data());
+      const PodDesc keep = pd;
+      pd.slot = hd.slot;
+      pd.rot_start = hd.rot_start;
+      pd.flags = hd.flags;
+      same = std::memcmp(res_prev_blob_.data(), cp.blob.data(), bytes) == 0;
+      pd = keep;
+    }
+    if (same && entry_bytes) {
+      RingEntry& pe = *reinterpret_cast<RingEntry*>(res_prev_entry_.data());
+      const RingEntry& ne = *reinterpret_cast<const RingEntry*>(entry);
+      const RingEntry keep = pe;
+      lbl_off = ne.lbl_off;
+      pe.slot = ne.slot;
+      pe.lbl_off = ne.lbl_off;
+      if (pe.tpool_cnt == 0 && ne.tpool_cnt == 0) pe.tpool_off = ne.tpool_off;  // unread without terms
+      same = std::memcmp(res_prev_entry_.data(), entry, entry_bytes) == 0;
+      pe = keep;
+    }
+    if (c->cfg.agg_debug & 8) same = false;  // diagnostic: every pod staged over PCIe
+    uint32_t dw[kRingLL];
+    if (same) {
+      dw[0] = RING_SAME | (aggsame ? RING_AGG_SAME : 0u);
+      dw[1] = (uint32_t)hd.slot;
+      dw[2] = (uint32_t)hd.rot_start;
+      dw[3] = lbl_off;
+    } else {
+      std::memcpy(ring_->blob[q % kRingSlots], cp.blob.data(), bytes);
+      if (entry_bytes) std::memcpy(ring_->entry[q % kRingSlots], entry, entry_bytes);
+      dw[0] = aggsame ? RING_AGG_SAME : 0u;
+      dw[1] = bytes;
+      dw[2] = (uint32_t)entry_bytes;
+      dw[3] = 0;
+    }
+    for (int k = kRingLL - 1; k >= 0; --k)
+      __atomic_store_n(&ring_->ll[k], (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)dw[k] << 32),
+                       __ATOMIC_RELEASE);
+    res_prev_blob_ = cp.blob;
+    res_prev_entry_.assign(entry, entry + entry_bytes);
+  }
   RingResult& rr = ring_->res[q % kRingSlots];
   const auto tw = clk::now();
   const auto T2 = tw;
@@ -2787,6 +2877,7 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
 #endif
     if ((spins & 0xfffu) == 0 && clk::now() - tw > std::chrono::seconds(5)) {  // never: fail loudly, not hang
       __atomic_store_n(&ring_->ctl, (unsigned long long)kRingStop, __ATOMIC_RELEASE);
+      __atomic_store_n(&ring_->ll[0], (unsigned long long)kRingStop, __ATOMIC_RELEASE);
       c->err = "resident loop: no result for the posted pod after 5 s";
       return fail(KSG_EDEVICE);
     }

@@ -625,6 +625,7 @@ class Engine {
   PodRing* ring_dev_ = nullptr;   // its device address
   bool res_running_ = false;
   int res_q_ = 0, res_gs_ = 0, res_unit_ = 0;  // pods posted to the running launch; its geometry
+  std::vector<uint8_t> res_prev_blob_, res_prev_entry_;  // k_agg_loop ring: the program / entry posted last
   int res_kind_ = 0;              // the running launch: 1 k_sched_loop, 2 k_agg_loop (pod-table pods)
   int64_t res_terms_ = 0;         // k_agg_loop: own affinity terms of the pods posted (its spill rows' budget)
   std::chrono::steady_clock::time_point res_last_{};  // the last result the host took

@@ -37,6 +37,10 @@ def load():
         lib.ksg_generation.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib.ksg_debug_compare_mirror.restype = C.c_int
         lib.ksg_debug_compare_mirror.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        from .abi import Result
+        lib.ksg_debug_schedule_calls.restype = C.c_int
+        lib.ksg_debug_schedule_calls.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_uint32,
+                                                 C.POINTER(Result), C.POINTER(C.c_double)]
         _lib = lib
     return _lib
 
@@ -74,6 +78,18 @@ class Scheduler(Backend):
         f, g = C.c_uint64(), C.c_uint64()
         self._chk(self.lib.ksg_debug_relayouts(self.ctx, C.byref(f), C.byref(g)), "relayouts")
         return f.value, g.value
+
+    def schedule_calls(self, handles, assume=True):
+        """ksg_schedule_one for each handle, back to back from native code (ksg_debug_schedule_calls):
+        (results, mean wall µs per call)."""
+        from .abi import FLAG_ASSUME, Result
+        n = len(handles)
+        hs = (C.c_int32 * n)(*handles)
+        rs = (Result * n)()
+        us = C.c_double()
+        self._chk(self.lib.ksg_debug_schedule_calls(self.ctx, hs, n, FLAG_ASSUME if assume else 0, rs, C.byref(us)),
+                  "schedule_calls")
+        return [rs[i] for i in range(n)], us.value
 
     def shard_range(self):
         """(first snapshot index, node count) this rank evaluates (node-sharded contexts)."""

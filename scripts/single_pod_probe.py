@@ -7,6 +7,8 @@ ksg_schedule_batch of the same pods.  Prints one JSON line per workload.
                                                         dts (DefaultTopologySpreading), c4 (TopologySpreading
                                                         15000 nodes), c3, c4-anti
   python scripts/single_pod_probe.py stamps [workload]  the resident call's host / device split
+single_resident_us times the calls from Python (ctypes), single_resident_native_us from native code
+(ksg_debug_schedule_calls), as a binding's goroutine issues them.
 Every resident call's result is checked against the oracle (after timing), so a fast wrong answer
 does not count.
 """
@@ -35,7 +37,7 @@ def cluster(wl, n_pods):
     return nodes, init, pods, objects
 
 
-def run(wl, cfg, n_pods=2000, batch=False, check=False):
+def run(wl, cfg, n_pods=2000, batch=False, check=False, native=False):
     nodes, init, pods, objects = cluster(wl, n_pods + 200)
     if wl == "c2pct0":
         cfg = dict(cfg, percentageOfNodesToScore=0)
@@ -51,10 +53,13 @@ def run(wl, cfg, n_pods=2000, batch=False, check=False):
     t0 = time.perf_counter()
     if batch:
         got += [r.as_tuple() for r in s.schedule_batch(hs[200:], assume=True)]
+    elif native:  # the calls from native code: no interpreter overhead per call
+        rs, us = s.schedule_calls(hs[200:], assume=True)
+        got += [r.as_tuple() for r in rs]
     else:
         for h in hs[200:]:
             got.append(s.schedule_one(h, assume=True)[0].as_tuple())
-    dt = time.perf_counter() - t0
+    dt = us * n_pods * 1e-6 if native else time.perf_counter() - t0
     kern = s.kernel_stats()[3]
     s.close()
     mism = None
@@ -78,11 +83,14 @@ def main():
     args = sys.argv[1:]
     if args[:1] == ["stamps"]:  # printed at the loop's stop
         wl = args[1] if len(args) > 1 else "c2"
-        print(json.dumps({"workload": wl, "single_resident_us": round(run(wl, {"loopStamps": True})[0], 1)}))
+        print(json.dumps({"workload": wl, "single_resident_us": round(run(wl, {"loopStamps": True})[0], 1),
+                          "single_resident_native_us": round(run(wl, {"loopStamps": True}, native=True)[0], 1)}))
         return
     for wl in args or ["c2"]:
         us, kern, mism = run(wl, {}, check=True)
-        out = {"workload": wl, "single_resident_us": round(us, 1), "resident_kernel": kern, "oracle_mismatches": mism,
+        nus, _, nmism = run(wl, {}, check=True, native=True)
+        out = {"workload": wl, "single_resident_us": round(us, 1), "single_resident_native_us": round(nus, 1),
+               "resident_kernel": kern, "oracle_mismatches": mism, "native_oracle_mismatches": nmism,
                "single_launch_us": round(run(wl, {"residentLoop": False})[0], 1),
                "batch_us_per_pod": round(run(wl, {}, batch=True)[0], 2)}
         print(json.dumps(out), flush=True)

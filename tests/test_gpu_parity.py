@@ -993,6 +993,43 @@ def test_agg_loop_same_template_runs(native, wg):
     assert g.compare_mirror(sync=False) == (0, -1)
 
 
+@pytest.mark.parametrize("debug", [0, 8, 12])
+def test_resident_agg_same_template_calls(native, debug):
+    """ksg_schedule_one of runs of identical pods through the resident k_agg_loop: a pod posted right after
+    one of its template is not staged over PCIe (RING_SAME: the loop copies the previous program and
+    entry in LDS and patches slot, rotation and label offset) and starts from the counts the loop folded
+    at the end of the previous pod (DF_AGG_SAME).  Spread pods (zone DoNotSchedule), pods with own
+    affinity terms (no fold, entries differ), unplaceable pods (nothing to fold), Service-selected pods
+    under system default spreading; against the oracle pod by pod, with the shortcuts off (aggLoopDebug
+    8: every pod staged; 12: staged and gathered), and the mirror against the cache."""
+    from ksg import synth
+    nodes, init, _ = synth.topology_spreading(900, 600, 0)
+    dnodes, dinit, dpods, objects = synth.default_topology_spreading(0, 0, 40)
+    kinds = [synth.pod_with_topology_spreading, synth.pod_with_preferred_pod_anti_affinity,
+             synth.pod_with_required_anti_affinity, synth.pod_with_pod_affinity]
+    pods, k = [], 0
+    for run, kind in enumerate([0, 0, 1, 0, 2, 1, 1, 3, 0, 2, 0, 1]):
+        for _ in range([30, 1, 12, 45, 3, 20][run % 6]):
+            pods.append(kinds[kind](f"t{k}", "sched-1"))
+            k += 1
+    big = synth.pod_with_topology_spreading("huge", "sched-1")
+    big["spec"]["containers"][0]["resources"] = {"requests": {"cpu": "1000"}}
+    pods[40:40] = [big, dict(big, metadata=dict(big["metadata"], name="huge2", uid="huge2"))]
+    pods[100:100] = dpods
+    g, o = _pair(native, {"aggLoopDebug": debug} if debug else {}, nodes, init)
+    for ob in objects:
+        for b in (g, o):
+            b.upsert_object(ob)
+    agg = 0
+    for q, p in enumerate(pods):
+        rg, _ = g.schedule_one(g.compile(p), assume=True)
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"pod {q} ({p['metadata']['name']})"
+        agg += g.kernel_stats()[3] == "k_agg_loop"
+    assert agg > len(pods) * 3 // 4, f"only {agg} of {len(pods)} calls ran in the resident k_agg_loop"
+    assert g.compare_mirror(sync=True)[0] == 0
+
+
 @pytest.mark.parametrize("wg", [1, 0])
 def test_agg_loop_spilled_lists(native, wg):
     """k_agg_loop workgroups whose nodes hold more pods / affinity terms than their LDS lists (2048 each):
