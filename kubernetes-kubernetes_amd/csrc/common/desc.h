@@ -488,13 +488,13 @@ struct ShardView {
 // ---- persistent scheduling loop (k_sched_loop) -------------------------------------
 // One launch evaluates a run of consecutive pods: `nwg` resident workgroups each own a contiguous
 // range of node blocks for the whole run and meet at two device-scope arrival counters per pod.
-// ---- the resident loop's pod ring (single-pod calls) ------------------------------
+// ---- the resident loops' pod ring (single-pod calls) -----------------------------------
 // Host-pinned, device-mapped, fine-grained (uncached on the device).  The host posts pod q's program
-// into blob[q % kRingSlots], then one 64-bit store of ctl = {q + 1 | program bytes << 32}; the loop's
-// workgroups poll ctl, copy the program into LDS and schedule the pod; the committing thread writes
-// res[q % kRingSlots] and, last, its seq = q + 1 (system-scope release).  ctl = kRingStop ends the
-// launch; so does kLoopMaxPods pods or ring_idle of s_memrealtime ticks without a pod (the host
-// relaunches first when it has been idle for half that: the loop never outlives its process).
+// into blob[q % kRingSlots] (unless RING_SAME, below), then the doorbell ll; the loop's workgroups poll
+// it, take the program into LDS and schedule the pod; the committing thread writes res[q % kRingSlots]
+// and, last, its seq = q + 1.  A stop (ll[0]'s tag kRingStop) ends the launch; so does kLoopMaxPods pods
+// or ring_idle of s_memrealtime ticks without a pod (the host relaunches first when it has been idle for
+// half that: the loop never outlives its process).
 constexpr int kRingSlots = 2;
 constexpr uint32_t kRingStop = 0xffffffffu;
 struct alignas(16) RingResult {
@@ -502,7 +502,7 @@ struct alignas(16) RingResult {
   DevResult r;
 };
 // k_agg_loop's resident instance also takes the pod's pod-table entry through the ring (entry[q %
-// kRingSlots], its size in ctl bits [48, 64)): the owner of the chosen node writes it into the device
+// kRingSlots], its size in ll[2]): the owner of the chosen node writes it into the device
 // pod table when it commits the pod, so the pods after it count it.  The host laid the
 // entry out in its shadow (Cluster::pod_table_put) and checked that the device arrays hold it.
 struct RingEntry {
@@ -519,16 +519,21 @@ struct RingTerm {
   DTerm d;
 };
 constexpr int kRingEntryBytes = 8192;
-// k_agg_loop's doorbell is four self-tagged words instead of ctl (ll[k] = {tag = q + 1 | data << 32}, each
-// 8-byte store atomic on its own, so the loop takes them in one poll without a second read over PCIe):
-//   ll[0] data: RING_SAME (pod q is pod q-1's program and entry but for the fields below: nothing is staged,
-//               the loop copies q-1's from LDS and patches them) | RING_AGG_SAME (the program's DF_AGG_SAME);
+// The doorbell is four self-tagged words (ll[k] = {tag = q + 1 | data << 32}, each 8-byte store atomic on
+// its own, so the loop takes them in one poll without a second read over PCIe):
+//   ll[0] data: RING_SAME (pod q is pod q-1's program -- and, k_agg_loop, its entry -- but for the fields
+//               below: nothing is staged, the loop copies q-1's in LDS and patches them) | RING_AGG_SAME
+//               (k_agg_loop: the program's DF_AGG_SAME);
 //   ll[1..3]:   RING_SAME: {slot, rot_start, entry lbl_off}; else {program bytes, entry bytes, 0}.
 // A stop is ll[0]'s tag kRingStop.
 enum : uint32_t { RING_SAME = 1u, RING_AGG_SAME = 2u };
 constexpr int kRingLL = 4;
+// k_sched_loop polls one word instead (its registers leave no room for four): ctl = {q + 1 (bits 0-10) |
+// RING_SAME << 11 | RING_SAME ? slot + 1 << 12 (23 bits), rot_start << 35 (25 bits) : program bytes << 12};
+// q + 1 = kCtlStop ends the launch.
+constexpr unsigned long long kCtlStop = 0x7ffull;
 struct alignas(128) PodRing {
-  unsigned long long ctl;  // [host] {pods posted | program bytes << 32 | entry bytes << 48} or kRingStop
+  unsigned long long ctl;          // [host] k_sched_loop's doorbell
   unsigned long long ll[kRingLL];  // [host] k_agg_loop's doorbell (above)
   uint32_t pad0[22];
   uint32_t exited;         // [device] 1: the loop left on its own (idle / pod limit)
@@ -574,7 +579,7 @@ constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local hi
 constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
 constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
 constexpr int kAggSpillMax = 1 << 20;  // pod / term list entries past those per workgroup (HBM spill rows)
-constexpr int kAGran = 12;         // granules per participant per pod
+constexpr int kAGran = 13;         // granules per participant per pod
 constexpr int kAggStartRow = 1024; // k_agg_loop (node-sharded): the start barrier's granule row (= kLoopMaxPods)
 enum AggGran : int {
   AG_Z0 = 0,   // {InterPodAffinity "any" bits}: every count of the pod is in the shared region
@@ -586,10 +591,12 @@ enum AggGran : int {
   AG_A3 = 6,   // min raw InterPodAffinity (biased and reversed, 0 = none)
   AG_P0 = 7,   // PodTopologySpread scoring: presence bits [0, 48) of my feasible, non-ignored nodes' domains
   AG_P1 = 8,   // {non-ignored feasible nodes (20) | presence bits [48, 76) (28)}
-  AG_B = 9,    // packed (TotalScore, pre-order) key
-  AG_BN = 10,  // the snapshot index + 1 of the workgroup's best node (every workgroup folds the
+  AG_PXA = 9,  // AG_PX of the raw scores phase 1 computed with the previous pod's topology sizes: exact,
+               // and exchange PX skipped, when this pod's sizes (from P0 / P1) equal them
+  AG_B = 10,   // packed (TotalScore, pre-order) key
+  AG_BN = 11,  // the snapshot index + 1 of the workgroup's best node (every workgroup folds the
                // chosen pod into the next pod's counts)
-  AG_PX = 11,  // PodTopologySpread raw-score {max + 1 (24) | 2^24 - 1 - min (24)} over my scored nodes
+  AG_PX = 12,  // PodTopologySpread raw-score {max + 1 (24) | 2^24 - 1 - min (24)} over my scored nodes
 };
 constexpr int kAggScoreCons = 2;   // k_agg_loop: ScheduleAnyway constraints of a looped pod (per-node counts in LDS)
 constexpr int kAggPresBits = 76;   // k_agg_loop: presence bits of its non-hostname score constraints' domains

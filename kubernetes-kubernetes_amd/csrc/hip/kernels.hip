@@ -1645,29 +1645,27 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
   }
 }
 
-// Resident mode: wait for pod q in the ring (one thread).  Returns the pod's program size, or -1 when
-// the launch ends (the host's stop, the pod limit, or lv.ring_idle ticks without a pod).
-// (ring_wait_p: the ctl word's bits [32, 64), i.e. the program bytes and, for k_agg_loop, the entry bytes << 16)
-__device__ __forceinline__ int ring_wait_p(PodRing* ring, int q, int npods, unsigned long long idle) {
-  if (q >= npods) return -1;
+// k_sched_loop's doorbell (desc.h PodRing::ctl), polled by one thread: the posted word, or kCtlStop (the
+// host's stop, the pod limit, or `idle` ticks without a pod).
+__device__ __forceinline__ unsigned long long ring_wait_ctl(PodRing* ring, int q, int npods, unsigned long long idle) {
+  if (q >= npods) return kCtlStop;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  // relaxed polls: the ring is coherent host memory, and a system-scope acquire on every poll would
-  // invalidate the caches under the other workgroups' work; the program is read after the doorbell's value
-  // is known (control dependence), with system-scope loads that bypass the device caches (stage_ring)
   for (uint32_t spins = 0;; ++spins) {
     const unsigned long long v = __hip_atomic_load(&ring->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t posted = (uint32_t)v;
-    if (posted == kRingStop) return -1;
-    if (posted > (uint32_t)q) return (int)(v >> 32);
+    const unsigned long long posted = v & kCtlStop;
+    if (posted == kCtlStop) return kCtlStop;
+    if (posted > (unsigned long long)q) return v;
     if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > idle) {
       if (blockIdx.x == 0) __hip_atomic_store(&ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return -1;
+      return kCtlStop;
     }
     __builtin_amdgcn_s_sleep(2);
   }
 }
 // k_agg_loop's doorbell (desc.h PodRing::ll), polled by one wave: lanes 0..3 load the four tagged words in
-// one instruction until every tag reads q + 1; lane k's data word into *data.  -1: stop, idle or no pod left.
+// one instruction (one 32-byte read over PCIe per poll and workgroup; four single-word reads per poll
+// crowd the link: C4's 59 workgroups took twice as long per call) until every tag reads q + 1; lane k's
+// data word into *data.  -1: stop, idle or no pod left.
 __device__ __forceinline__ int ring_wait_ll(PodRing* ring, int q, int npods, unsigned long long idle, int lane,
                                             uint32_t* data) {
   if (q >= npods) return -1;
@@ -1688,10 +1686,6 @@ __device__ __forceinline__ int ring_wait_ll(PodRing* ring, int q, int npods, uns
     }
     __builtin_amdgcn_s_sleep(2);
   }
-}
-__device__ __forceinline__ int ring_wait(const LoopView& lv, int q) {
-  const int v = ring_wait_p(lv.ring, q, lv.npods, lv.ring_idle);
-  return v < 0 ? v : (v & 0xffff);
 }
 // Resident mode: pod q's result to the host (the committing thread, after commit_result)
 // The record goes to host memory with system-scope (write-through) stores; once they have completed
@@ -1829,7 +1823,8 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   __shared__ int s_ga_q;                  // the pod whose s_ga is ready
   __shared__ uint32_t s_ccnt, s_cbelow;
   __shared__ unsigned long long s_best;
-  __shared__ int s_ring_bytes;  // resident mode: the posted pod's program size (-1: the launch ends)
+  __shared__ unsigned long long s_ring_ctl;  // resident mode: the doorbell word (desc.h PodRing::ctl)
+  __shared__ int s_pb;                       // resident mode: the last staged program's bytes
   // percentageOfNodesToScore (DF_ROTDEV): s_rot[p & 1] = pod p's rotation start (nextStartNodeIndex),
   // s_proc = the decided pod's processedNodes (schedule_one.go:686-687, 809-824)
   __shared__ uint32_t s_rot[2], s_proc;
@@ -2094,11 +2089,31 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   for (int run0 = 0;;) {
   int run_end = lv.npods;
   if constexpr (RING) {
-    if (threadIdx.x == 0) s_ring_bytes = ring_wait(lv, run0);
+    // the tagged doorbell (PodRing::ll); RING_SAME: the previous call's program but for the slot and the
+    // rotation (the host compared the bytes), copied in LDS instead of read over PCIe
+    if (threadIdx.x == 0) s_ring_ctl = ring_wait_ctl(lv.ring, run0, lv.npods, lv.ring_idle);
     __syncthreads();
-    const int bytes = s_ring_bytes;
-    if (bytes < 0) return;
-    stage_ring(run0, bytes);
+    const unsigned long long ctl = s_ring_ctl;
+    if (ctl == kCtlStop) return;
+    if ((ctl >> 11) & 1ull) {
+      if (threadIdx.x < 64) {  // one wave (kBlobLds / 8 words at most)
+        int o = (int)threadIdx.x;
+        asm volatile("" : "+v"(o));
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(s_blob[(run0 + 2) % 3]);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(s_blob[run0 % 3]);
+        for (; o < s_pb / 8; o += 64) dst[o] = src[o];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        PodDesc& dn = *reinterpret_cast<PodDesc*>(s_blob[run0 % 3]);
+        dn.slot = (int32_t)((ctl >> 12) & 0x7fffffull) - 1;
+        dn.rot_start = (int32_t)(ctl >> 35);
+      }
+    } else {
+      const int bytes = (int)((ctl >> 12) & 0xffffull);
+      stage_ring(run0, bytes);
+      if (threadIdx.x == 0) s_pb = bytes;
+    }
     run_end = run0 + 1;
   } else {
     if (run0 >= run_end) return;
@@ -2748,6 +2763,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ uint32_t s_wu[kAggThreads / 64][3];           // feasible, before the start, PTS non-ignored
   __shared__ unsigned long long s_wp[kAggThreads / 64][2]; // PTS domain presence bits [0, 64), [64, 128)
   __shared__ uint32_t s_psz[kAggScoreCons];                // PTS topology sizes of the pod being decided
+  __shared__ uint32_t s_psz_used[kAggScoreCons];           // ... of the previous PTS-scored pod (~0: none),
+  __shared__ double s_pwt[kAggScoreCons];                  //   their weights log(size + 2),
+  __shared__ uint32_t s_praw[PTSS && RING ? kAggThreads : 1];  // phase 1's raw scores with them (~0: not scored)
+  __shared__ unsigned long long s_wq[kAggThreads / 64][2]; //   and their per-wave {max + 1, 2^24 - 1 - min}
   __shared__ unsigned long long s_pxm[2];                  // wave 1 -> 0: its half's raw PTS max+1 / reversed min
   __shared__ int s_px_q, s_pxd_q;                          // wave 1 -> 0: half done; wave 0 -> 1: exchange PX done
   __shared__ int64_t s_pts_mx, s_pts_mn;                   // PTS NormalizeScore max / min of the pod
@@ -3255,6 +3274,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_spec_q = -1;
     s_pb = 0;
     s_eb = 0;
+    for (int c = 0; c < kAggScoreCons; ++c) s_psz_used[c] = ~0u;
   }
   __syncthreads();
   for (int s = t; s < m.pods_hw; s += kAggThreads) {
@@ -3473,6 +3493,43 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     }
     __syncthreads();
+    if (PTSS && RING && ((d.score_mask >> P_PTS) & 1u) && s_psz_used[0] != ~0u) {
+      // each slot's raw PodTopologySpread score with the previous scored pod's topology sizes (the
+      // arithmetic of the score pass after exchange A, below); exchange A checks the sizes and carries
+      // the max / min (AG_PXA)
+      const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+      const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
+      int tq = t;  // opaque per pod: the slot addresses are not hoisted out of the pod loop (registers)
+      asm volatile("" : "+v"(tq));
+      bool ign = false, have = true;
+      double score = 0.0;
+#pragma unroll
+      for (int c = 0; c < kAggScoreCons; ++c) {
+        if (c >= d.n_ptss) continue;
+        have = have && s_psz_used[c] != ~0u;
+        const uint32_t cnt = s_pc[c][tq];
+        if (cnt == ~0u) {
+          ign |= !anytopo;
+          continue;
+        }
+        if (!have) continue;
+        const double prod = (double)cnt * s_pwt[c];
+        const double term = prod + (double)(cs[c].max_skew - 1);
+        score = score + term;
+      }
+      const bool scored = have && ((s_ball[tq >> 6] >> (tq & 63)) & 1ull) && !ign;
+      const uint32_t raw = scored ? (uint32_t)(int64_t)round(score) : 0u;
+      s_praw[tq] = scored ? raw : ~0u;
+      unsigned long long hx = scored ? (unsigned long long)raw + 1ull : 0ull;
+      unsigned long long hn = scored ? (1ull << 24) - 1ull - raw : 0ull;
+      hx = wave_max_u64(hx);
+      hn = wave_max_u64(hn);
+      if (lane == 0) {
+        s_wq[wave][0] = hx;
+        s_wq[wave][1] = hn;
+      }
+      __syncthreads();
+    }
     stamp(q, 1);
     const uint32_t ipa_any = s_any;
 
@@ -3510,6 +3567,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             agran_put<SHARD>(av, q, gid, AG_P0, p0 & ((1ull << 48) - 1ull));
             agran_put<SHARD>(av, q, gid, AG_P1, (unsigned long long)(ni & 0xfffffu) |
                                            ((((p0 >> 48) | (p1 << 16)) & ((1ull << 28) - 1ull)) << 20));
+            unsigned long long hx = 0, hn = 0;
+            for (int v = 0; v < kAggThreads / 64 && s_psz_used[0] != ~0u; ++v) {
+              hx = s_wq[v][0] > hx ? s_wq[v][0] : hx;
+              hn = s_wq[v][1] > hn ? s_wq[v][1] : hn;
+            }
+            if (RING) agran_put<SHARD>(av, q, gid, AG_PXA, (hx << 24) | hn);
           }
           wstamp(q, 1);
         }
@@ -3584,10 +3647,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           __builtin_amdgcn_s_sleep(1);
       }
       constexpr int kH = kAggThreads / 128;
+      bool spec = false;
       if (PTSS && ((d.score_mask >> P_PTS) & 1u) && s_ok) {
         // ---- PodTopologySpread.Score of my half's feasible nodes with the global topology sizes
         // (scoring.go:199-226; k_pts_score's arithmetic), into s_pc[0]; NormalizeScore's max / min over
-        // every workgroup's scored nodes by exchange PX (scoring.go:229-268)
+        // every workgroup's scored nodes by exchange PX (scoring.go:229-268).  When the sizes are the ones
+        // phase 1 guessed (s_psz_used), its raw scores stand and exchange A carried the max / min (AG_PXA).
+        spec = RING && __ballot(lane < d.n_ptss && lane < kAggScoreCons && s_psz[lane] != s_psz_used[lane]) == 0ull &&
+               !(av.debug & 16);
         const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
         const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
         double wt[kAggScoreCons];
@@ -3595,7 +3662,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         for (int c = 0; c < kAggScoreCons; ++c) wt[c] = c < d.n_ptss ? m.log_tab[s_psz[c] + 2] : 0.0;
         unsigned long long hmx = 0, hmn = 0;
 #pragma unroll
-        for (int vv = 0; vv < kH; ++vv) {
+        for (int vv = 0; vv < kH && !spec; ++vv) {
           const int v = wave * kH + vv, ls = v * 64 + lane;
           const bool f = ((s_ball[v] >> lane) & 1ull) != 0;
           bool ign = false;
@@ -3624,7 +3691,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         hmx = wave_max_u64(hmx);
         hmn = wave_max_u64(hmn);
         if (wave == 1) {
-          if (lane == 0) {
+          if (lane == 0 && !spec) {
             s_pxm[0] = hmx;
             s_pxm[1] = hmn;
             __hip_atomic_store(&s_px_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3632,13 +3699,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           while (__hip_atomic_load(&s_pxd_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
             __builtin_amdgcn_s_sleep(1);
         } else {
-          while (__hip_atomic_load(&s_px_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
-            __builtin_amdgcn_s_sleep(1);
-          hmx = s_pxm[0] > hmx ? s_pxm[0] : hmx;
-          hmn = s_pxm[1] > hmn ? s_pxm[1] : hmn;
-          if (lane == 0) agran_put<SHARD>(av, q, gid, AG_PX, (hmx << 24) | hmn);
+          if (!spec) {
+            while (__hip_atomic_load(&s_px_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+              __builtin_amdgcn_s_sleep(1);
+            hmx = s_pxm[0] > hmx ? s_pxm[0] : hmx;
+            hmn = s_pxm[1] > hmn ? s_pxm[1] : hmn;
+            if (lane == 0) agran_put<SHARD>(av, q, gid, AG_PX, (hmx << 24) | hmn);
+          }
           unsigned long long xp[1][kMaxSweep];
-          const bool okp = agran_sweep<SHARD, 1>(av, q, AG_PX, xp);
+          const bool okp = agran_sweep<SHARD, 1>(av, q, spec ? AG_PXA : AG_PX, xp);
           unsigned long long gx = 0, gn = 0;
 #pragma unroll
           for (int r = 0; r < kMaxSweep; ++r)
@@ -3649,6 +3718,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             }
           gx = wave_max_u64(gx);
           gn = wave_max_u64(gn);
+          // the next pod's guess (wave 1 decided spec before this: on a mismatch it published PX first, and on a
+          // match the update writes the values it compared)
+          if (RING && lane < d.n_ptss && lane < kAggScoreCons) {
+            s_psz_used[lane] = s_psz[lane];
+            s_pwt[lane] = m.log_tab[s_psz[lane] + 2];
+          }
           if (lane == 0) {
             s_pts_mx = gx ? (int64_t)gx - 1 : 0;  // maxScore starts at 0 (scoring.go:239)
             s_pts_mn = gn ? (int64_t)(((1ull << 24) - 1ull) - gn) : 0;
@@ -3681,7 +3756,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           ballot[vv] = s_ball[v];
           sv[vv] = s_sv[v * 64 + lane];
           ri[vv] = ipa ? s_ri[v * 64 + lane] : 0;
-          rp[vv] = pts ? s_pc[0][v * 64 + lane] : 0u;
+          rp[vv] = pts ? (spec ? s_praw[v * 64 + lane] : s_pc[0][v * 64 + lane]) : 0u;
         }
         // branch-free: the four chains are independent, so the compiler interleaves them
 #pragma unroll

@@ -993,15 +993,17 @@ def test_agg_loop_same_template_runs(native, wg):
     assert g.compare_mirror(sync=False) == (0, -1)
 
 
-@pytest.mark.parametrize("debug", [0, 8, 12])
+@pytest.mark.parametrize("debug", [0, 8, 28])
 def test_resident_agg_same_template_calls(native, debug):
     """ksg_schedule_one of runs of identical pods through the resident k_agg_loop: a pod posted right after
     one of its template is not staged over PCIe (RING_SAME: the loop copies the previous program and
     entry in LDS and patches slot, rotation and label offset) and starts from the counts the loop folded
     at the end of the previous pod (DF_AGG_SAME).  Spread pods (zone DoNotSchedule), pods with own
     affinity terms (no fold, entries differ), unplaceable pods (nothing to fold), Service-selected pods
-    under system default spreading; against the oracle pod by pod, with the shortcuts off (aggLoopDebug
-    8: every pod staged; 12: staged and gathered), and the mirror against the cache."""
+    under system default spreading (their PodTopologySpread raw scores computed in phase 1 with the
+    previous pod's topology sizes, exchange PX skipped when the sizes hold); against the oracle pod by pod,
+    with the shortcuts off (aggLoopDebug 8: every pod staged; 28: staged, gathered, PX always), and the
+    mirror against the cache."""
     from ksg import synth
     nodes, init, _ = synth.topology_spreading(900, 600, 0)
     dnodes, dinit, dpods, objects = synth.default_topology_spreading(0, 0, 40)
