@@ -114,7 +114,10 @@ static int plugin_id(const std::string& n) {
 struct Config {
   int pct = 100;
   int threads = 1;  // CPU-baseline mode: Filter / Score over nodes on this many threads (Parallelizer.Until)
-  int spin_us = 50;  // CPU-baseline mode: how long an idle worker spins before parking
+  // CPU-baseline mode: how long an idle worker spins before parking.  A cycle's parallel passes are separated
+  // by sequential sections of up to a few hundred µs (PreFilter, PreScore, weights, selectHost); a worker that
+  // parks in between pays a futex wake-up per pass (C4 at 8 threads: 227 pods/s with 50 µs, 328 with 1 ms)
+  int spin_us = 1000;
   bool par_weights = false;  // CPU-baseline mode: NormalizeScore / weights on the pool too (framework.go:1409-1452)
   bool taintCompareOps = false;  // featureGates.TaintTolerationComparisonOperators
   bool enabled[KSG_NUM_PLUGINS];

@@ -8,6 +8,7 @@
 #   suite               pytest -m gpu, whole suite
 #   tests=<file[::k]>   pytest on one file / node id (-m gpu)
 #   smoke               __graft_entry__.smoke()
+#   benchdefault        bench.py with no arguments, as the driver runs it (C2 + the C5 100k sub-record)
 #   bench=<wl>[:steps]  bench.py --workload <wl> (c1 c2 c2pct0 c3 c4 c4-anti c5 dts), 3 steps by default
 #   prof=<wl>           rocprofv3 --kernel-trace --stats of a short bench run of <wl>
 #   pmc=<wl>            FETCH_SIZE and WRITE_SIZE passes (separate rocprofv3 runs) of <wl>
@@ -33,6 +34,7 @@ for s in "$@"; do
     suite) step suite 900 $PYT tests -m gpu ;;
     tests=*) f=${s#tests=}; n=$(basename "$f"); n=${n//[^A-Za-z0-9]/_}; step "tests_${n:0:80}" 600 $PYT "$f" -m gpu -v ;;
     smoke) step smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    benchdefault) step bench_default 600 python -u bench.py ;;
     bench=*)
       a=${s#bench=}; wl=${a%%:*}; n=3; [ "$a" != "$wl" ] && n=${a#*:}
       step "bench_$wl" 400 python -u bench.py $(bench_args "$wl") --steps "$n" --warmup 1 --cpu-seconds 5 ;;

@@ -24,7 +24,7 @@ def main():
     nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
     workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
     # pods per k_sched_loop dispatch, on average: a 1000-pod batch runs as 7 chunks (engine.cpp
-    # run_batch: 64, 320, 370, 148, 59, 24, 15), each one loop dispatch
+    # run_batch: 32, 160, 485, 194, 78, 31, 20), each one loop dispatch
     loop_pods = float(sys.argv[4]) if len(sys.argv) > 4 else 1000.0 / 7.0
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
