@@ -518,7 +518,7 @@ struct RingTerm {
   int32_t j, pad;  // term-table index
   DTerm d;
 };
-constexpr int kRingEntryBytes = 8192;
+constexpr int kRingEntryBytes = 8192;  // (staged into one of the resident k_agg_loop's program slots)
 // The doorbell is four self-tagged words (ll[k] = {tag = q + 1 | data << 32}, each 8-byte store atomic on
 // its own, so the loop takes them in one poll without a second read over PCIe):
 //   ll[0] data: RING_SAME (pod q is pod q-1's program -- and, k_agg_loop, its entry -- but for the fields
@@ -576,8 +576,15 @@ constexpr int kAggThreads = 512;   // one node slot per thread (8 waves)
 constexpr int kAggLocal = 4;       // node-local histograms per pod
 constexpr int kAggGWords = 1024;   // compact shared-region words per pod (staged in LDS)
 constexpr int kAggLocalCons = 2;   // DoNotSchedule constraints on node-local histograms per pod
-constexpr int kAggPods = 2048;     // pod-table slots per workgroup (its nodes' pods)
-constexpr int kAggTerms = 2048;    // existing affinity terms per workgroup
+constexpr int kAggPods = 5120;     // batch k_agg_loop: pod-table slots per workgroup in LDS (its nodes' pods; the
+                                   // rest spill to HBM)
+constexpr int kAggTerms = 5120;    // batch k_agg_loop: existing affinity terms per workgroup in LDS (likewise)
+constexpr int kAggBlobLds = 8192;  // batch k_agg_loop's three program slots: its pods' programs up to this size
+                                   // (larger pods take the launch path); the 24 KB this frees over kBlobLds hold
+                                   // 6144 more list entries, so C5's fill-front workgroup stays in LDS
+constexpr int kAggRingPods = 2048;   // the resident instance keeps kBlobLds program slots (its registers leave no
+constexpr int kAggRingTerms = 2048;  // room for the longer LDS offsets) and the shorter lists
+static_assert(kRingEntryBytes <= kBlobLds, "a ring entry is staged into a k_agg_loop program slot");
 constexpr int kAggSpillMax = 1 << 20;  // pod / term list entries past those per workgroup (HBM spill rows)
 constexpr int kAGran = 13;         // granules per participant per pod
 constexpr int kAggStartRow = 1024; // k_agg_loop (node-sharded): the start barrier's granule row (= kLoopMaxPods)

@@ -2734,10 +2734,14 @@ __device__ __forceinline__ void apply_entry(const MirrorView& m, const uint8_t* 
 // PTSS: some pod of the run has PodTopologySpread scoring (ScheduleAnyway constraints); the instance
 // without it leaves that code out (its registers and issue slots cost the other pods ~1 us).
 // RING: the resident instance (ksg_schedule_one of PodTopologySpread / InterPodAffinity pods):
-// pods through av.ring, each a run of its own -- gathered when it arrives, no fold, no staging ahead.
+// pods through av.ring, each a run of its own -- gathered when it arrives (or, same template, folded at the
+// end of the pod before it), no staging ahead.
 template <bool SHARD, bool PTSS, bool RING = false>
 __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
-  __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
+  constexpr int kBlob = RING ? kBlobLds : kAggBlobLds;       // program slot bytes (desc.h)
+  constexpr uint32_t kLp = RING ? kAggRingPods : kAggPods;     // LDS list entries (the rest spill to HBM)
+  constexpr uint32_t kLt = RING ? kAggRingTerms : kAggTerms;
+  __shared__ __align__(16) uint8_t s_blob[3][kBlob];  // pod p's program in s_blob[p % 3]
   __shared__ LoopCores s_core;
   // phase-1 slots: {weighted fixed score, raw TaintToleration, raw NodeAffinity} in one 16-byte
   // record (one LDS read in phase 2), raw InterPodAffinity apart (read only when it scores)
@@ -2751,7 +2755,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
                                                            // ScheduleAnyway c (bit 8 + c)
   __shared__ uint32_t s_pc[kAggScoreCons][kAggSlots];      // PodTopologySpread score: count at my node's
                                                            // domain per constraint (~0u: the node lacks the key)
-  __shared__ uint32_t s_pods[kAggPods], s_terms[kAggTerms];  // (slot | term) << 9 | node slot
+  __shared__ uint32_t s_pods[kLp], s_terms[kLt];  // (slot | term) << 9 | node slot
   __shared__ uint32_t s_np, s_nt;
   __shared__ uint32_t s_off[kLoopMaxPods];
   __shared__ long long s_pmin[kAggMaxCons];
@@ -2798,16 +2802,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
   const int nlo = k0 * kBlock, nhi = k1 * kBlock < m.n ? k1 * kBlock : m.n;
-  // my pod / term lists: the first kAggPods / kAggTerms entries in LDS, the rest in my HBM spill rows
+  // my pod / term lists: the first kLp / kLt entries in LDS, the rest in my HBM spill rows
   uint32_t* const spl = av.spill + (size_t)w * (size_t)(av.spill_pods + av.spill_terms);
-  const uint32_t pcap = (uint32_t)kAggPods + (uint32_t)av.spill_pods, tcap = (uint32_t)kAggTerms + (uint32_t)av.spill_terms;
+  const uint32_t pcap = kLp + (uint32_t)av.spill_pods, tcap = kLt + (uint32_t)av.spill_terms;
   auto put_pod = [&](uint32_t k, uint32_t e) __attribute__((always_inline)) {
-    if (k < (uint32_t)kAggPods) s_pods[k] = e;
-    else spl[k - (uint32_t)kAggPods] = e;
+    if (k < kLp) s_pods[k] = e;
+    else spl[k - kLp] = e;
   };
   auto put_term = [&](uint32_t k, uint32_t e) __attribute__((always_inline)) {
-    if (k < (uint32_t)kAggTerms) s_terms[k] = e;
-    else spl[(uint32_t)av.spill_pods + k - (uint32_t)kAggTerms] = e;
+    if (k < kLt) s_terms[k] = e;
+    else spl[(uint32_t)av.spill_pods + k - kLt] = e;
   };
   const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
   const int kk = t / kBlock, tt = t % kBlock;  // my node slot t = kk * kBlock + tt
@@ -2882,7 +2886,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     for (uint32_t k = (uint32_t)tid; k < nitems; k += (uint32_t)nthr) {
       if (k < np) {
         // pod role: the pod's selectors against one pod on my nodes (k_aggregate's pod role)
-        const uint32_t e = k < (uint32_t)kAggPods ? s_pods[k] : spl[k - (uint32_t)kAggPods];
+        const uint32_t e = k < kLp ? s_pods[k] : spl[k - kLp];
         const int s = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
         const int32_t pns = m.pod_ns[s];
         const bool term = (m.pod_flags[s] & 1u) != 0;
@@ -2949,7 +2953,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       } else {
         // term role: one existing affinity term of a pod on my nodes against the incoming pod
         const uint32_t kt2 = k - np;
-        const uint32_t e = kt2 < (uint32_t)kAggTerms ? s_terms[kt2] : spl[(uint32_t)av.spill_pods + kt2 - (uint32_t)kAggTerms];
+        const uint32_t e = kt2 < kLt ? s_terms[kt2] : spl[(uint32_t)av.spill_pods + kt2 - kLt];
         const int j = (int)(e >> 9), ls = (int)(e & 511u), n = nlo + ls;
         const DTerm tm = m.terms[j];
         if (tm.key >= d.n_keytab) continue;

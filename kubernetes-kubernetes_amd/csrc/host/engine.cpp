@@ -1005,7 +1005,7 @@ bool Engine::loop_ok(const CompiledPod& p) const {
 // A pod k_agg_loop takes: any CYCLE pod without evaluation output, PreFilter outcomes or sampling, whose
 // histograms and PodTopologySpread score constraints fit the loop's placement (CompiledPod::agg_ok).
 bool Engine::agg_loop_ok(const CompiledPod& p) const {
-  if (p.error || !p.agg_ok) return false;
+  if (p.error || !p.agg_ok || p.blob.size() > (size_t)kAggBlobLds) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
   if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET))
     return false;
@@ -2748,7 +2748,7 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     } else {
       if ((rc = agg_setup())) return fail(rc);
       // every workgroup's pod / term lists: its nodes' pods and terms now, plus what the launch can append
-      // (kLoopMaxPods pods and kRingTermBudget terms), past kAggPods / kAggTerms in its HBM spill rows
+      // (kLoopMaxPods pods and kRingTermBudget terms), past kAggRingPods / kAggRingTerms in its HBM spill rows
       std::vector<int32_t> np((size_t)G, 0), nt((size_t)G, 0);
       auto wg_of = [&](int32_t nd) { return (int)((int64_t)(nd / kBlock) * G / NB); };
       auto owner = [&](int32_t nd) {  // the workgroup whose block range [NB w / G, NB (w + 1) / G) holds nd
@@ -2764,8 +2764,8 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
         if (nd >= 0 && nd < c->view.n) nt[(size_t)owner(nd)]++;
       }
       auto up64 = [](int64_t v) { return v <= 0 ? (int64_t)0 : (v + 63) / 64 * 64; };
-      const int64_t spill_p = up64(*std::max_element(np.begin(), np.end()) + (int64_t)kLoopMaxPods - kAggPods);
-      const int64_t spill_t = up64(*std::max_element(nt.begin(), nt.end()) + (int64_t)kRingTermBudget - kAggTerms);
+      const int64_t spill_p = up64(*std::max_element(np.begin(), np.end()) + (int64_t)kLoopMaxPods - kAggRingPods);
+      const int64_t spill_t = up64(*std::max_element(nt.begin(), nt.end()) + (int64_t)kRingTermBudget - kAggRingTerms);
       if (spill_p > kAggSpillMax || spill_t > kAggSpillMax) {  // no resident launch: the launch path
         c->pod_table_drop(cp.slot);
         c->next_start = ns_before;

@@ -1,6 +1,7 @@
 """Diagnostic: C5 (mixed 100k-node cluster) batch by batch -- wall ms, the batch's kernel stats (avg ms per
 pod, pods in a loop, kernel) and mirror re-layouts -- to show what changes as assumed pods accumulate.
-python scripts/c5_growth_probe.py [batches] [nodes] [c5|c2]  (c2: SchedulingBasic, 1000 init pods)"""
+python scripts/c5_growth_probe.py [batches] [nodes] [c5|c2] [stamps]  (c2: SchedulingBasic, 1000 init pods;
+stamps: loopStamps, the loops' per-phase breakdown of every batch on stderr)"""
 import os
 import sys
 import time
@@ -17,7 +18,7 @@ if WL == "c2":
     nodes, init, pods = synth.scheduling_basic(N, 1000, B * 1000)
 else:
     nodes, init, pods = synth.mixed_cluster(N, N // 10, B * 1000)
-s = Scheduler({"device": 0, "kernelTimingStride": 1})
+s = Scheduler({"device": 0, "kernelTimingStride": 1, "loopStamps": "stamps" in sys.argv[4:]})
 for n in nodes:
     s.add_node(n)
 for p in init:

@@ -1034,24 +1034,34 @@ def test_resident_agg_same_template_calls(native, debug):
 
 @pytest.mark.parametrize("wg", [1, 0])
 def test_agg_loop_spilled_lists(native, wg):
-    """k_agg_loop workgroups whose nodes hold more pods / affinity terms than their LDS lists (2048 each):
-    the rest go to HBM spill rows (AggView::spill).  500 zoned nodes with 4600 bound pods, half carrying a
-    preferred anti-affinity term, then a mixed PTS / IPA batch -- one workgroup (wg 1) or the default
-    geometry -- against the oracle and the per-pod launch path."""
+    """k_agg_loop workgroups whose nodes hold more pods / affinity terms than their LDS lists (5120 each in
+    the batch loop, 2048 in the resident one): the rest go to HBM spill rows (AggView::spill).  500 zoned
+    nodes with 8500 bound pods, 5500 of them carrying a preferred anti-affinity term, then a mixed PTS / IPA
+    batch -- one workgroup (wg 1) or the default geometry -- against the oracle and the per-pod launch path,
+    then single-pod calls through the resident loop against the oracle."""
     from ksg import synth
-    nodes, init, pods = synth.mixed_cluster(500, 2300, 200)
+    nodes, init, pods = synth.mixed_cluster(500, 3000, 260)
     names = [n["metadata"]["name"] for n in nodes]
-    for k in range(2300):
+    for k in range(5500):
         p = synth.pod_with_preferred_pod_anti_affinity(f"pa-{k}", "sched-1")
         p["spec"]["nodeName"] = names[(k * 7) % len(names)]
         init.append(p)
     base = {"loopWorkgroups": wg} if wg else {}
     g, o = _pair(native, base, nodes, init)
     g2, _ = _pair(native, dict(base, aggLoop=False), nodes, init)
-    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    batch, single = pods[:200], pods[200:]
+    rs = g.schedule_batch([g.compile(p) for p in batch], assume=True)
     assert g.kernel_stats()[3] == "k_agg_loop"
-    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
-    for q, p in enumerate(pods):
+    rs2 = g2.schedule_batch([g2.compile(p) for p in batch], assume=True)
+    for q, p in enumerate(batch):
         ro, _ = o.schedule_one(o.compile(p), assume=True)
         assert rs[q].as_tuple() == ro.as_tuple() == rs2[q].as_tuple(), f"pod {q} ({p['metadata']['name']})"
     assert g.compare_mirror(sync=False) == (0, -1)
+    agg = 0
+    for q, p in enumerate(single):
+        rg, _ = g.schedule_one(g.compile(p), assume=True)
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"single pod {q} ({p['metadata']['name']})"
+        agg += g.kernel_stats()[3] == "k_agg_loop"
+    assert agg > len(single) // 2
+    assert g.compare_mirror(sync=True)[0] == 0
