@@ -616,8 +616,10 @@ struct AggView {
   int32_t blk0, nblk;         // node blocks [blk0, blk0 + nblk)
   uint32_t tag;               // granule tag (1..65535)
   int32_t gwords;             // region words per pod (max agg_gwords of the run)
-  int32_t debug;              // diagnostic: bit 0 never fold (gather every pod after the previous one is
-                              // placed), bit 1 never DF_LFAST (config "aggLoopDebug")
+  int32_t debug;              // diagnostic (config "aggLoopDebug"): bit 0 never fold (gather every pod after
+                              // the previous one is placed), bit 1 never DF_LFAST, bit 2 no same-template
+                              // shortcut (DF_AGG_SAME), bit 3 (host) no RING_SAME -- the resident loops stage
+                              // every pod over PCIe, bit 4 the resident loop always runs exchange PX
   unsigned long long* gran;   // [npods][world * nwg][kAGran] (this rank's)
   unsigned long long* region; // [npods][gwords]: shared-region sums (zeroed by the host; this rank's)
   // node shards: participants are world * nwg workgroups, rank-major.  Every granule and
