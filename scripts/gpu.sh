@@ -25,6 +25,8 @@ step() {  # name seconds cmd...
 bench_args() {  # workload -> bench.py arguments
   case $1 in
     c2pct0) echo "--workload c2 --pct 0" ;;
+    c1solo) echo "--workload c1 --extra-config {\"loopWorkgroups\":1,\"loopUnit\":256}" ;;
+    c1g2) echo "--workload c1 --extra-config {\"loopWorkgroups\":2,\"loopUnit\":256}" ;;
     *) echo "--workload $1" ;;
   esac
 }
