@@ -528,6 +528,7 @@ constexpr int kRingEntryBytes = 8192;  // (staged into one of the resident k_agg
 // A stop is ll[0]'s tag kRingStop.
 enum : uint32_t { RING_SAME = 1u, RING_AGG_SAME = 2u };
 constexpr int kRingLL = 4;
+constexpr int kRelayWords = kRingLL + kBlobLds / 8 + kRingEntryBytes / 8;  // AggView::relay
 // k_sched_loop polls one word instead (its registers leave no room for four): ctl = {q + 1 (bits 0-10) |
 // RING_SAME << 11 | RING_SAME ? slot + 1 << 12 (23 bits), rot_start << 35 (25 bits) : program bytes << 12};
 // q + 1 = kCtlStop ends the launch.
@@ -641,6 +642,10 @@ struct AggView {
   // resident instance (k_agg_loop<false, true, true>): pods through the ring, one run per pod
   PodRing* ring;
   unsigned long long ring_idle;  // s_memrealtime ticks without a pod before the launch ends by itself
+  // resident mode with many workgroups: workgroup 0 alone polls the host doorbell and relays it -- and a
+  // staged program and entry -- through device memory (kRelayWords: the doorbell's four tagged words, then the
+  // program, then the entry); the others poll that (nullptr: every workgroup polls the host)
+  unsigned long long* relay;
 };
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

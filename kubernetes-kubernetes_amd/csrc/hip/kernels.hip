@@ -1662,17 +1662,17 @@ __device__ __forceinline__ unsigned long long ring_wait_ctl(PodRing* ring, int q
     __builtin_amdgcn_s_sleep(2);
   }
 }
-// k_agg_loop's doorbell (desc.h PodRing::ll), polled by one wave: lanes 0..3 load the four tagged words in
-// one instruction (one 32-byte read over PCIe per poll and workgroup; four single-word reads per poll
-// crowd the link: C4's 59 workgroups took twice as long per call) until every tag reads q + 1; lane k's
-// data word into *data.  -1: stop, idle or no pod left.
-__device__ __forceinline__ int ring_wait_ll(PodRing* ring, int q, int npods, unsigned long long idle, int lane,
-                                            uint32_t* data) {
+// k_agg_loop's doorbell (desc.h PodRing::ll, or the copy workgroup 0 relays in device memory, AggView::relay),
+// polled by one wave: lanes 0..3 load the four tagged words in one instruction (one 32-byte read over PCIe
+// per poll and workgroup; four single-word reads per poll crowd the link: C4's 59 workgroups took twice as
+// long per call) until every tag reads q + 1; lane k's data word into *data.  -1: stop, idle or no pod left
+// (`exited`, when given, records an idle exit for the host).
+__device__ __forceinline__ int ring_wait_ll(const unsigned long long* ll, uint32_t* exited, int q, int npods,
+                                            unsigned long long idle, int lane, uint32_t* data) {
   if (q >= npods) return -1;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t spins = 0;; ++spins) {
-    const unsigned long long v =
-        lane < kRingLL ? __hip_atomic_load(&ring->ll[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    const unsigned long long v = lane < kRingLL ? __hip_atomic_load(ll + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     const uint32_t tag = (uint32_t)v;
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)tag) == kRingStop) return -1;
     const unsigned long long ok = __ballot(lane < kRingLL && tag == (uint32_t)(q + 1));
@@ -1681,7 +1681,7 @@ __device__ __forceinline__ int ring_wait_ll(PodRing* ring, int q, int npods, uns
       return 0;
     }
     if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > idle) {
-      if (blockIdx.x == 0 && lane == 0) __hip_atomic_store(&ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (exited && blockIdx.x == 0 && lane == 0) __hip_atomic_store(exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return -1;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -2818,6 +2818,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   const int my_i = (k0 + kk) * kBlock + tt;
   const bool my_node = kk < nk && my_i < m.n;
   auto stamp = [&](int q, int k) {
+#ifndef KSG_DIAG
+    if constexpr (RING) return;  // the resident instance's stamps: the diagnostic build (registers)
+#endif
     if (av.stamps && w == 0 && t == 0) av.stamps[(size_t)q * kAggStamps + k] = __builtin_amdgcn_s_memrealtime();
   };
   auto wstamp = [&](int q, int k) {  // thread 0 of every workgroup
@@ -3336,17 +3339,31 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     if constexpr (RING) {
       // ======== resident mode: pod q from the ring (host memory, bypassing the device caches): its program
       // into s_blob[q % 3], its pod-table entry into s_blob[(q + 1) % 3]; then its counts ========
+      // (relay: workgroup 0 polls the host and relays the doorbell -- with the program and entry when they are
+      // staged -- through device memory, where the other workgroups poll: one PCIe reader instead of G)
+      const bool relay = av.relay != nullptr, hostp = !relay || w == 0;
       if (wave == 0) {
         uint32_t v = 0;
-        const int r = ring_wait_ll(av.ring, q, av.npods, av.ring_idle, lane, &v);
+        const int r = ring_wait_ll(hostp ? av.ring->ll : av.relay, hostp ? &av.ring->exited : nullptr, q, av.npods,
+                                   av.ring_idle, lane, &v);
         if (lane < kRingLL) s_ll[lane] = v;
         if (lane == 0) s_ring_end = r;
       }
       stamp(q, 9);
       __syncthreads();
-      if (s_ring_end < 0) return;
+      if (s_ring_end < 0) {
+        if (relay && w == 0 && t == 0)  // the others leave too
+          __hip_atomic_store(av.relay, (unsigned long long)kRingStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
       const uint32_t rmode = s_ll[0];
+      auto relay_doorbell = [&]() __attribute__((always_inline)) {  // workgroup 0, after any relayed bytes landed
+        if (relay && w == 0 && t < kRingLL)
+          __hip_atomic_store(av.relay + t, (unsigned long long)(uint32_t)(q + 1) | ((unsigned long long)s_ll[t] << 32),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      };
       if (rmode & RING_SAME) {
+        relay_doorbell();
         // pod q-1's program and entry but for the slot, the rotation and the label-pool offset (the host
         // compared the rest byte for byte): copied in LDS -- the entry first, its buffer takes the program
         const int pw8 = s_pb / 8, ew8 = s_eb / 8;
@@ -3373,9 +3390,20 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         const unsigned long long* es_ = reinterpret_cast<const unsigned long long*>(av.ring->entry[q % kRingSlots]);
         unsigned long long* pd = reinterpret_cast<unsigned long long*>(s_blob[q % 3]);
         unsigned long long* ed = reinterpret_cast<unsigned long long*>(s_blob[(q + 1) % 3]);
+        // (workgroup 0 of a relay reads the host's copy and writes the device's; the others read the device's)
+        const unsigned long long* sp_ = hostp ? ps_ : av.relay + kRingLL;
+        const unsigned long long* se_ = hostp ? es_ - pw8 : av.relay + kRingLL;
+        const bool put = relay && hostp;
         for (int k = t; k < pw8 + ew8; k += kAggThreads) {
-          if (k < pw8) pd[k] = __hip_atomic_load(ps_ + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          else ed[k - pw8] = __hip_atomic_load(es_ + (k - pw8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const unsigned long long x = __hip_atomic_load((k < pw8 ? sp_ : se_) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (k < pw8) pd[k] = x;
+          else ed[k - pw8] = x;
+          if (put) __hip_atomic_store(av.relay + kRingLL + k, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (put) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the relayed bytes landed before the doorbell
+          __syncthreads();
+          relay_doorbell();
         }
         if (t == 0) {
           if (ew8 == 0) reinterpret_cast<RingEntry*>(ed)->slot = -1;
@@ -3965,7 +3993,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     } else if (RING) {
       // the next pod arrives through the ring: pod q joins its node owner's lists now, and its entry
-      // (written by the owner's committing thread) is read from L2 by the pods after it.  While the host
+      // (written by the owner's committing thread) is read by the owner's gathers of the pods after it.  While the host
       // turns around, pod q is folded into the counts in LDS as a next pod of its own template would count
       // it (the plan against q's own program): a next pod marked DF_AGG_SAME starts from them, any other
       // gathers afresh.  (q's own terms would be read from the table the owner wrote: not for pods with them.)
@@ -3988,9 +4016,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           s_spec_q = sp ? q : -1;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // (no agent-scope fence: the entry the owner wrote is read back only by the owner's own gathers -- its
+      // lists -- within this launch; an agent-scope release / acquire here wrote back and invalidated the L2 of
+      // every workgroup's XCD each pod: 11 µs per call at 100 000 nodes)
       __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     stamp(q, 8);
   }

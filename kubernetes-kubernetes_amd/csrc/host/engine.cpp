@@ -1092,7 +1092,7 @@ Engine::~Engine() {
     stream_destroyed();
   }
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill,
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill, &d_relay,
                     &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf, &d_vsc})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
@@ -2795,6 +2795,11 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       av.fail = (uint32_t*)d_fail.p;
       av.ring = ring_dev_;
       av.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;
+      if (c->cfg.ring_relay_min > 0 && G >= c->cfg.ring_relay_min) {  // stale tags would pass for new ones: zeroed
+        if ((rc = ensure(d_relay, (size_t)kRelayWords * 8))) return fail(rc);
+        HIPCHK(hipMemsetAsync(d_relay.p, 0, (size_t)kRelayWords * 8, s));
+        av.relay = (unsigned long long*)d_relay.p;
+      }
       if (c->cfg.loop_stamps) {  // workgroup 0's phase stamps per ring pod (resident_stop prints them)
         const size_t sb = (size_t)kLoopMaxPods * kAggStamps * 8;
         if ((rc = ensure(d_astamps, sb))) return fail(rc);

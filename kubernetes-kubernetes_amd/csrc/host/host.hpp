@@ -221,6 +221,8 @@ struct Config {
                                 // between calls, fed through a host-pinned pod ring ("residentLoop")
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int agg_debug = 0;            // AggView::debug (diagnostic)
+  int ring_relay_min = 48;      // resident k_agg_loop: relay the doorbell through device memory from this many
+                                // workgroups on (one PCIe poller instead of G)
   int first_chunk = 32;         // pods in a pipelined batch's first chunk (the host work before the first launch)
   int loop_wave_map = 0;        // k_sched_loop role-to-wave placement (kWaveMap in kernels.hip)
   int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
@@ -594,6 +596,7 @@ class Engine {
   std::vector<unsigned long long*> agran_all, region_all;  // every rank's, as mapped here (node-sharded)
   DevBuf d_aggpeers;  // node-sharded k_agg_loop: the device copy of agran_all + region_all
   DevBuf d_astamps;          // k_agg_loop diagnostic stamps
+  DevBuf d_relay;            // the resident k_agg_loop's relayed doorbell and staging (AggView::relay)
   DevBuf d_aspill;           // k_agg_loop: workgroup pod / term lists past the LDS ones (AggView::spill)
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)

@@ -714,6 +714,7 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     c->loop_unit = (int)d.num(r, "loopUnit", 128) == 256 ? 256 : 128;
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
     c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);
+    c->ring_relay_min = (int)d.num(r, "ringRelayMinWorkgroups", 48);
     c->debug_give_up_at = (int)d.num(r, "debugLoopGiveUpAt", -1);
     c->loop_wave_map = (int)d.num(r, "loopWaveMap", 0);
     c->first_chunk = std::max(8, std::min(256, (int)d.num(r, "pipelineFirstChunk", 32)));

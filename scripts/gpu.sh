@@ -15,6 +15,7 @@
 #   sq=<wl>             one shader-counter pass (instruction mix, wave cycles, clock) of <wl>
 #   py=<script>[:args]  python3 -u scripts/<script> args (probes); ',' in args becomes ' '
 #   repeat=<n>:<script>[:args]  the probe in n fresh processes (e.g. the in-process device-exchange start)
+#   pydiag=<script>[:args]  as py=, on the diagnostic library (make -C kubernetes-kubernetes_amd diag; KSG_LIB)
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
 step() {  # name seconds cmd...
@@ -58,6 +59,9 @@ for s in "$@"; do
     repeat=*)
       a=${s#repeat=}; n=${a%%:*}; rest=${a#*:}; sc=${rest%%:*}; args=""; [ "$rest" != "$sc" ] && args=${rest#*:}
       for k in $(seq 1 "$n"); do step "repeat_${sc%.py}_$k" 200 python3 -u "scripts/$sc" ${args//,/ }; done ;;
+    pydiag=*)
+      a=${s#pydiag=}; sc=${a%%:*}; args=""; [ "$a" != "$sc" ] && args=${a#*:}
+      step "pydiag_${sc%.py}" 400 env KSG_LIB="$PWD/kubernetes-kubernetes_amd/lib/libksg_diag.so" python3 -u "scripts/$sc" ${args//,/ } ;;
     py=*)
       a=${s#py=}; sc=${a%%:*}; args=""; [ "$a" != "$sc" ] && args=${a#*:}
       step "py_${sc%.py}" 400 python3 -u "scripts/$sc" ${args//,/ } ;;

@@ -5,7 +5,7 @@ ksg_schedule_batch of the same pods.  Prints one JSON line per workload.
 
   python scripts/single_pod_probe.py [workload ...]     c2 (SchedulingBasic 5000 nodes, default), c2pct0,
                                                         dts (DefaultTopologySpreading), c4 (TopologySpreading
-                                                        15000 nodes), c3, c4-anti
+                                                        15000 nodes), c3, c4-anti, c5 (100 000 nodes)
   python scripts/single_pod_probe.py stamps [workload]  the resident call's host / device split
 single_resident_us times the calls from Python (ctypes), single_resident_native_us from native code
 (ksg_debug_schedule_calls), as a binding's goroutine issues them.
@@ -32,6 +32,8 @@ def cluster(wl, n_pods):
         nodes, init, pods, objects = synth.default_topology_spreading(5000, 5000, n_pods)
     elif wl == "c3":
         nodes, init, pods = synth.scheduling_c3(5000, 5000, n_pods)
+    elif wl == "c5":
+        nodes, init, pods = synth.mixed_cluster(100000, 10000, n_pods)
     else:
         nodes, init, pods = synth.topology_spreading(15000, 15000, n_pods, preferred_anti=wl == "c4-anti")
     return nodes, init, pods, objects
@@ -65,7 +67,7 @@ def run(wl, cfg, n_pods=2000, batch=False, check=False, native=False):
     mism = None
     if check:
         from oracle_binding import oracle
-        o = oracle(dict(percentageOfNodesToScore=0) if wl == "c2pct0" else {})
+        o = oracle(dict(percentageOfNodesToScore=0) if wl == "c2pct0" else {"cpuThreads": 16} if wl == "c5" else {})
         for ob in objects:
             o.upsert_object(ob)
         for n in nodes:
