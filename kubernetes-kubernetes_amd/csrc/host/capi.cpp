@@ -244,7 +244,7 @@ int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* r
     if (const int rs = quiesce(ctx)) return rs;
     std::vector<const PodSpec*> pods{&it->second};
     std::vector<int32_t> hs{handle};
-    return with_err(ctx, ctx->engine->run_batch(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, result, eval));
+    return with_err(ctx, ctx->engine->run_batch_api(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, result, eval));
   })
 }
 
@@ -261,7 +261,7 @@ int ksg_schedule_batch(ksg_ctx* ctx, const int32_t* handles, int32_t n, uint32_t
       if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
       pods.push_back(&it->second);
     }
-    return with_err(ctx, ctx->engine->run_batch(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, results, nullptr));
+    return with_err(ctx, ctx->engine->run_batch_api(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, results, nullptr));
   })
 }
 

@@ -1329,6 +1329,28 @@ static bool agg_same(const std::vector<uint8_t>& a, const std::vector<uint8_t>& 
 
 static bool agg_same(const CompiledPod& a, const CompiledPod& b) { return !a.error && !b.error && agg_same(a.blob, b.blob); }
 
+int Engine::run_batch_api(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
+                          ksg_result* results, ksg_eval_out* eval) {
+  fault_first_ = -1;
+  const int rc = run_batch(pods, handles, assume, results, eval);
+  const int f = fault_first_;
+  if (rc != KSG_EDEVICE || f < 0 || f >= (int)pods.size() || !comm || !c->cfg.nccl_id.empty() || eval) return rc;
+  // every rank of the group lands here for the same chunk (each rank's loop gives up on the same missing
+  // participants; a late rank's loop gives up once it runs alone) and re-runs the same pods, in step
+  const std::string why = c->err;
+  const std::vector<const PodSpec*> rest(pods.begin() + f, pods.end());
+  const std::vector<int32_t> rh(handles.begin() + f, handles.end());
+  force_allreduce_ = true;
+  fault_first_ = -1;
+  const int r2 = run_batch(rest, rh, assume, results + f, nullptr);
+  force_allreduce_ = false;
+  if (r2 == KSG_OK) {
+    ++loop_retries_;
+    c->err = "recovered: " + why + "; re-run over the all-reduce path";
+  }
+  return r2;
+}
+
 int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                       ksg_result* results, ksg_eval_out* eval) {
   const int n = (int)pods.size();
@@ -1348,7 +1370,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // a peer's loop that spins on it (Cluster::own_queue).  The group decides as one (Comm::own_queues):
   // otherwise it keeps the all-reduce path.
   const bool rccl = !c->cfg.nccl_id.empty();
-  const bool dx = comm && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) && (rccl || comm->own_queues());
+  const bool dx = comm && !force_allreduce_ && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) &&
+                  (rccl || comm->own_queues());
   // Host/device pipeline: the batch runs as chunks.  While the device schedules chunk k the host
   // compiles and stages chunk k+1, then mirrors the finished chunks' assumes into the cache.  Only
   // chunk 0's compile and the last chunk's bookkeeping are exposed, so chunk 0 is short (32 pods,
@@ -1764,6 +1787,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     c->pods_dirty = true;
     c->err = why + ": pods " + std::to_string(first) + ".." + std::to_string(n - 1) +
              " of the batch were not scheduled (status Error); the device mirror is rebuilt from the cache";
+    fault_first_ = first;
     return KSG_EDEVICE;
   };
   auto fault_detail = [&]() -> std::string {

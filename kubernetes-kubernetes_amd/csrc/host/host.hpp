@@ -546,6 +546,14 @@ class Engine {
   // run a batch of cycles (device-resident, sequential semantics)
   int run_batch(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                 ksg_result* results, ksg_eval_out* eval);
+  // run_batch, and for an in-process rank group whose persistent loop gave up (its ranks' loops could not all
+  // be resident at once: HIP gives no control over which hardware queue a stream lands on), the pods from the
+  // failed chunk on once more over the all-reduce path
+  int run_batch_api(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
+                    ksg_result* results, ksg_eval_out* eval);
+  int fault_first_ = -1;        // the first pod loop_fault left unscheduled (-1: none), for run_batch_api
+  bool force_allreduce_ = false;  // run_batch_api's retry: no device exchange
+  uint64_t loop_retries_ = 0;   // batches run_batch_api re-ran over the all-reduce path
   int run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* nodes, int32_t* code, uint8_t* codes,
                  uint32_t* reasons, int64_t* raw, int64_t* norm);
   // DefaultPreemption's PostFilter for a pod that failed its cycle (preempt.cpp)

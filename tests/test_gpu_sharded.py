@@ -402,6 +402,19 @@ def test_c5_pipelined_batches_sharded_agg_loop(world):
         assert s.compare_mirror(sync=True)[0] == 0
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_loop_give_up_retried_over_allreduce(world):
+    """An in-process group whose persistent loops give up (forced: debugLoopGiveUpAt makes every workgroup of
+    every rank stop at the same pod) re-runs the pods from the failed chunk over the all-reduce path
+    (Engine::run_batch_api), every rank in step: results equal to the oracle's, mirrors equal to the caches."""
+    from ksg.synth import mixed_cluster
+    nodes, init, pods = mixed_cluster(3000, 600, 400)
+    ranks, o = _group(world, {"deviceExchange": True, "debugLoopGiveUpAt": 40}, nodes, init)
+    _check(ranks, o, pods, chunk=400)
+    for s in ranks:
+        assert s.compare_mirror(sync=True)[0] == 0
+
+
 @pytest.mark.skipif(os.environ.get("GPU_MAX_HW_QUEUES", "4") != "4", reason="counts HIP's default 4 hardware queues")
 def test_device_exchange_needs_own_queues():
     """In-process ranks take the device exchange only when every rank's stream has a hardware queue of its
