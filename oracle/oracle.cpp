@@ -606,6 +606,18 @@ static thread_local std::string g_create_error;
 // ===========================================================================
 // per-cycle evaluation
 // ===========================================================================
+// Go's maps are hash maps: the PreFilter / PreScore aggregation counts (merged sequentially after the parallel
+// passes, as the reference merges its per-node maps) are hash maps here too.  No result depends on their
+// iteration order (lookups, integer sums); tpMatch keeps its order (the preemption restatement seeds
+// criticalPaths in map order).
+struct PairHash {
+  size_t operator()(const std::pair<std::string, std::string>& p) const {
+    return std::hash<std::string>()(p.first) * 1000003u ^ std::hash<std::string>()(p.second);
+  }
+};
+using PairCounts = std::unordered_map<std::pair<std::string, std::string>, int64_t, PairHash>;
+using StrCounts = std::unordered_map<std::string, int64_t>;
+
 struct Cycle {
   ksgo_ctx* c;
   const Pod* pod;
@@ -632,11 +644,11 @@ struct Cycle {
   std::vector<int64_t> critMin;
   std::vector<TSC> ptsS;
   std::set<std::string> ignored;
-  std::vector<std::map<std::string, int64_t>> tpCounts;  // TopologyValueToPodCounts (entries exist)
+  std::vector<StrCounts> tpCounts;  // TopologyValueToPodCounts (entries exist)
   std::vector<double> tpWeight;
   // IPA
-  std::map<std::pair<std::string, std::string>, int64_t> existingAnti, affCounts, antiCounts;
-  std::map<std::string, std::map<std::string, int64_t>> topoScore;
+  PairCounts existingAnti, affCounts, antiCounts;
+  std::map<std::string, StrCounts> topoScore;
   std::vector<AffinityTerm> ipaReqAff, ipaReqAnti;
   std::vector<WeightedAffinityTerm> ipaPrefAff, ipaPrefAnti;
   const Labels* nsLabels = nullptr;
@@ -795,7 +807,6 @@ static bool get_constraints(const ksgo_ctx* c, const Pod& pod, const std::string
 }
 
 // ---- IPA helpers --------------------------------------------------------------------
-using PairCounts = std::map<std::pair<std::string, std::string>, int64_t>;
 static bool pod_matches_all_terms(const std::vector<AffinityTerm>& terms, const Pod& p) {  // filtering.go:188-200
   if (terms.empty()) return false;
   for (auto& t : terms)
@@ -899,7 +910,7 @@ static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std
       for (auto& t : cy.ipaReqAff) merge_ns(c, t);
       for (auto& t : cy.ipaReqAnti) merge_ns(c, t);
       cy.nsLabels = c->ns_labels(pod.ns);
-      using TopoCounts = std::map<std::pair<std::string, std::string>, int64_t>;
+      using TopoCounts = PairCounts;
       cy.existingAnti.clear();
       over_all_nodes<TopoCounts>(c, [&](NodeInfoO* ni, TopoCounts& ea) {  // getExistingAntiAffinityCounts :216-240
         for (auto* ep : ni->podsWithRequiredAntiAffinity)
@@ -1239,7 +1250,7 @@ static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& n
         cy.tpWeight[i] = go_log((double)(sz + 2));
       }
       cy.reqNA = get_required_node_affinity(pod);
-      using TpCounts = std::vector<std::map<std::string, int64_t>>;
+      using TpCounts = std::vector<StrCounts>;
       over_all_nodes<TpCounts>(c, [&](NodeInfoO* ni, TpCounts& tc) {  // processAllNode :155-189
         if (requireAll && !node_labels_match_spread(ni->node.labels, cy.ptsS)) return;
         tc.resize(nc);
@@ -1271,34 +1282,32 @@ static Status prescore_plugin(Cycle& cy, int p, const std::vector<NodeInfoO*>& n
       const Labels* nsl = c->ns_labels(pod.ns);
       cy.topoScore.clear();
       bool any = false;
-      auto processTerm = [&](std::map<std::string, std::map<std::string, int64_t>>& m, const AffinityTerm& t,
-                             int32_t weight, const Pod& target, const Labels* nl, const Node& node, int32_t mult) {
+      using TopoScoreAcc = std::pair<bool, std::map<std::string, StrCounts>>;  // {some node scored, sums}
+      auto processTerm = [&](TopoScoreAcc& m, const AffinityTerm& t, int32_t weight, const Pod& target,
+                             const Labels* nl, const Node& node, int32_t mult) {
         if (t.matches(target, nl)) {
           auto it = node.labels.find(t.topologyKey);
-          if (it != node.labels.end()) m[t.topologyKey][it->second] += (int64_t)(weight * mult);
+          if (it != node.labels.end()) {
+            m.second[t.topologyKey][it->second] += (int64_t)(weight * mult);
+            m.first = true;  // the node's topoScore is non-empty (scoring.go:192-195)
+          }
         }
       };
-      using TopoScore = std::pair<bool, std::map<std::string, std::map<std::string, int64_t>>>;
-      over_all_nodes<TopoScore>(c, [&](NodeInfoO* ni, TopoScore& acc) {  // processNode (scoring.go:166-199)
+      // (each chunk adds its nodes' scores straight into its accumulator: a per-node map, merged, sums the same)
+      over_all_nodes<TopoScoreAcc>(c, [&](NodeInfoO* ni, TopoScoreAcc& acc) {  // processNode (scoring.go:166-199)
         if (!hasConstraints && ni->podsWithAffinity.empty()) return;
         const auto& podsToProcess = hasConstraints ? ni->pods : ni->podsWithAffinity;
-        std::map<std::string, std::map<std::string, int64_t>> ts;
         for (auto* ep : podsToProcess) {  // processExistingPod :81-125
           const Node& node = ni->node;
           if (node.labels.empty()) continue;
-          for (auto& t : cy.ipaPrefAff) processTerm(ts, t.term, t.weight, ep->pod, nullptr, node, 1);
-          for (auto& t : cy.ipaPrefAnti) processTerm(ts, t.term, t.weight, ep->pod, nullptr, node, -1);
+          for (auto& t : cy.ipaPrefAff) processTerm(acc, t.term, t.weight, ep->pod, nullptr, node, 1);
+          for (auto& t : cy.ipaPrefAnti) processTerm(acc, t.term, t.weight, ep->pod, nullptr, node, -1);
           if (c->cfg.hardPodAffinityWeight > 0)
-            for (auto& t : ep->reqAff) processTerm(ts, t, c->cfg.hardPodAffinityWeight, pod, nsl, node, 1);
-          for (auto& t : ep->prefAff) processTerm(ts, t.term, t.weight, pod, nsl, node, 1);
-          for (auto& t : ep->prefAnti) processTerm(ts, t.term, t.weight, pod, nsl, node, -1);
+            for (auto& t : ep->reqAff) processTerm(acc, t, c->cfg.hardPodAffinityWeight, pod, nsl, node, 1);
+          for (auto& t : ep->prefAff) processTerm(acc, t.term, t.weight, pod, nsl, node, 1);
+          for (auto& t : ep->prefAnti) processTerm(acc, t.term, t.weight, pod, nsl, node, -1);
         }
-        if (!ts.empty()) {
-          acc.first = true;
-          for (auto& kv : ts)
-            for (auto& vv : kv.second) acc.second[kv.first][vv.first] += vv.second;
-        }
-      }, [&](const TopoScore& acc) {
+      }, [&](const TopoScoreAcc& acc) {
         any = any || acc.first;
         for (auto& kv : acc.second)
           for (auto& vv : kv.second) cy.topoScore[kv.first][vv.first] += vv.second;
