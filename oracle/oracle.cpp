@@ -114,10 +114,11 @@ static int plugin_id(const std::string& n) {
 struct Config {
   int pct = 100;
   int threads = 1;  // CPU-baseline mode: Filter / Score over nodes on this many threads (Parallelizer.Until)
-  // CPU-baseline mode: how long an idle worker spins before parking.  A cycle's parallel passes are separated
-  // by sequential sections of up to a few hundred µs (PreFilter, PreScore, weights, selectHost); a worker that
-  // parks in between pays a futex wake-up per pass (C4 at 8 threads: 227 pods/s with 50 µs, 328 with 1 ms)
-  int spin_us = 1000;
+  // CPU-baseline mode: how long an idle worker spins before parking.  Longer spins avoid futex wake-ups
+  // between a cycle's parallel passes on an idle machine (C4, 8 threads, this container: 227 -> 328 pods/s at
+  // 1 ms), but on the GPU box's 16-CPU cgroup quota the spinning workers are throttled instead (C3, 16
+  // threads: 1595 pods/s at 50 µs, 1202 at 1 ms; profiles/r04k_cpu_pool_c3.txt)
+  int spin_us = 50;
   bool par_weights = false;  // CPU-baseline mode: NormalizeScore / weights on the pool too (framework.go:1409-1452)
   bool taintCompareOps = false;  // featureGates.TaintTolerationComparisonOperators
   bool enabled[KSG_NUM_PLUGINS];
@@ -608,8 +609,8 @@ static thread_local std::string g_create_error;
 // ===========================================================================
 // Go's maps are hash maps: the PreFilter / PreScore aggregation counts (merged sequentially after the parallel
 // passes, as the reference merges its per-node maps) are hash maps here too.  No result depends on their
-// iteration order (lookups, integer sums); tpMatch keeps its order (the preemption restatement seeds
-// criticalPaths in map order).
+// iteration order (lookups, integer sums, minima); the preemption restatement seeds criticalPaths from
+// tpMatch in key order, over a sorted copy.
 struct PairHash {
   size_t operator()(const std::pair<std::string, std::string>& p) const {
     return std::hash<std::string>()(p.first) * 1000003u ^ std::hash<std::string>()(p.second);
@@ -640,7 +641,7 @@ struct Cycle {
   // PTS
   struct TSC { int32_t maxSkew; std::string key; Selector sel; int32_t minDomains; bool affHonor, taintHonor; };
   std::vector<TSC> ptsF;
-  std::vector<std::map<std::string, int64_t>> tpMatch;  // TpValueToMatchNum
+  std::vector<StrCounts> tpMatch;  // TpValueToMatchNum
   std::vector<int64_t> critMin;
   std::vector<TSC> ptsS;
   std::set<std::string> ignored;
@@ -882,7 +883,9 @@ static Status run_prefilter_plugin(Cycle& cy, int p, bool* skip, std::vector<std
       if (cy.ptsF.empty()) { *skip = true; return Status{}; }
       size_t nc = cy.ptsF.size();
       cy.tpMatch.assign(nc, {});
-      using TpMatch = std::vector<std::map<std::string, int64_t>>;
+      for (size_t i = 0; i < nc; ++i)  // make(map, sizeHeuristic(len(allNodes), c)) (filtering.go:252-254,361-366)
+        if (cy.ptsF[i].key == "kubernetes.io/hostname") cy.tpMatch[i].reserve(c->list.size());
+      using TpMatch = std::vector<StrCounts>;
       over_all_nodes<TpMatch>(c, [&](NodeInfoO* ni, TpMatch& tm) {  // processNode (filtering.go:255-300)
         const Node& n = ni->node;
         if (!node_labels_match_spread(n.labels, cy.ptsF)) return;
@@ -2339,9 +2342,10 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
   std::vector<std::pair<NodeInfoO*, OVictims>> nv, vl;
   int64_t offset = 0, ncand = 0;
   if (P > 0 && preempt_prefilter(c, cy)) {
-    for (auto& m : cy.tpMatch) {  // initial criticalPaths over the domains (map order)
+    for (auto& m : cy.tpMatch) {  // initial criticalPaths over the domains (in key order)
       CritPaths p;
-      for (auto& kv : m) crit_update(p, kv.first, kv.second);
+      const std::map<std::string, int64_t> sorted(m.begin(), m.end());
+      for (auto& kv : sorted) crit_update(p, kv.first, kv.second);
       crit.push_back(p);
     }
     offset = ((offsetIn % P) + P) % P;
