@@ -1647,16 +1647,18 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
 
 // k_sched_loop's doorbell (desc.h PodRing::ctl), polled by one thread: the posted word, or kCtlStop (the
 // host's stop, the pod limit, or `idle` ticks without a pod).
-__device__ __forceinline__ unsigned long long ring_wait_ctl(PodRing* ring, int q, int npods, unsigned long long idle) {
+// (ctl: the host's word, or workgroup 0's relayed copy in device memory; exited, when given, records an idle exit)
+__device__ __forceinline__ unsigned long long ring_wait_ctl(const unsigned long long* ctl, uint32_t* exited, int q,
+                                                            int npods, unsigned long long idle) {
   if (q >= npods) return kCtlStop;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t spins = 0;; ++spins) {
-    const unsigned long long v = __hip_atomic_load(&ring->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long v = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned long long posted = v & kCtlStop;
     if (posted == kCtlStop) return kCtlStop;
     if (posted > (unsigned long long)q) return v;
     if ((spins & 63u) == 63u && __builtin_amdgcn_s_memrealtime() - t0 > idle) {
-      if (blockIdx.x == 0) __hip_atomic_store(&ring->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (exited && blockIdx.x == 0) __hip_atomic_store(exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return kCtlStop;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -1842,8 +1844,14 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   const bool sel = wave == NW;      // the selection wave: exchanges + phase 2
   const bool hlp = wave == NW + 1;  // the helper wave: candidate pre-evaluation + staging
   const int t = vt;                          // evaluation waves: my slot in each block of my range
+  // diagnostic stamps (loopStamps): the resident instance has them in the diagnostic library only (registers)
+#ifdef KSG_DIAG
+  constexpr bool kSt = true;
+#else
+  constexpr bool kSt = !RING;
+#endif
   auto stamp_s = [&](int q, int k) {       // diagnostic phase stamps: WG 0's selection lane 0
-    if (lv.stamps && w == 0 && vt == U) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    if (kSt && lv.stamps && w == 0 && vt == U) lv.stamps[(size_t)q * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
   // the committing thread: pod `pod`'s PodStats, with its rotation bookkeeping for commit_result (DF_ROTDEV)
   auto rot_stats = [&](int pod, int par) __attribute__((always_inline)) -> PodStats* {
@@ -1887,12 +1895,6 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   // resident mode: pod q's program from the ring (host memory: one round trip, every thread's 16 B)
   // (system-scope loads: they bypass the device caches, so a ring slot reused kRingSlots pods later is
   // never read stale -- the doorbell poll is relaxed, no acquire invalidates the caches)
-  auto stage_ring = [&](int q, int bytes) __attribute__((always_inline)) {
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(lv.ring->blob[q % kRingSlots]);
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(s_blob[q % 3]);
-    for (uint32_t o = threadIdx.x; o < (uint32_t)bytes / 8u; o += (uint32_t)kLoopThreads)
-      dst[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  };
 
   // ---- evaluation-wave state of the pod being prepared: per-thread maxima of the normalising raw
   // scores over my feasible nodes; per-wave feasible counts (all, and before nextStartNodeIndex)
@@ -2070,7 +2072,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     a_granules(c, bl, a, bb, &g0, &g1);
     gran_put(lv, pq, gid, 0, g0);
     gran_put(lv, pq, gid, 1, g1);
-    if (lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
+    if (kSt && lv.wstamps) lv.wstamps[((size_t)pq * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
   };
 
   if (!RING)
@@ -2091,7 +2093,15 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   if constexpr (RING) {
     // the tagged doorbell (PodRing::ll); RING_SAME: the previous call's program but for the slot and the
     // rotation (the host compared the bytes), copied in LDS instead of read over PCIe
-    if (threadIdx.x == 0) s_ring_ctl = ring_wait_ctl(lv.ring, run0, lv.npods, lv.ring_idle);
+    // (relay: workgroup 0 polls the host and relays the word through device memory, where the other workgroups
+    // poll: one PCIe poller instead of G; a staged program is still read from the host's ring by all)
+    if (threadIdx.x == 0) {
+      const bool hostp = lv.relay == nullptr || blockIdx.x == 0;
+      const unsigned long long v = ring_wait_ctl(hostp ? &lv.ring->ctl : lv.relay, hostp ? &lv.ring->exited : nullptr,
+                                                 run0, lv.npods, lv.ring_idle);
+      if (lv.relay && hostp) __hip_atomic_store(lv.relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // stops too
+      s_ring_ctl = v;
+    }
     __syncthreads();
     const unsigned long long ctl = s_ring_ctl;
     if (ctl == kCtlStop) return;
@@ -2111,7 +2121,10 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       }
     } else {
       const int bytes = (int)((ctl >> 12) & 0xffffull);
-      stage_ring(run0, bytes);
+      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(lv.ring->blob[run0 % kRingSlots]);
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(s_blob[run0 % 3]);
+      for (uint32_t o = threadIdx.x; o < (uint32_t)bytes / 8u; o += (uint32_t)kLoopThreads)
+        dst[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (threadIdx.x == 0) s_pb = bytes;
     }
     run_end = run0 + 1;
@@ -2150,7 +2163,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     if (sel) {
       // ======== selection wave: exchange A, phase 2, exchange B, pre-evaluation, staging ========
       stamp_s(q, 0);  // exchange A of this pod was published at the end of the previous one
-      if (lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+      if (kSt && lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
       unsigned long long xa[2][kMaxSweep];
       bool ok = gran_sweep<2>(lv, q, 0, xa);
       uint32_t F = 0, wp = 0, bf = 0;
@@ -2227,7 +2240,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         gran_put(lv, q, gid, 2, wkey);  // < 2^48: TotalScore < 2^19 (host-checked) << 29 | pre-order key
         if (lv.world > 1) gran_put(lv, q, gid, 3, (unsigned long long)(uint32_t)cand);
         else if (rotd) gran_put(lv, q, gid, 3, (unsigned long long)myproc);
-        if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        if (kSt && lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_cand_node, cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&s_cand_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -2267,7 +2280,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           s_rot[npar] = rot_next;
         }
       }
-      if (lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+      if (kSt && lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 4] = __builtin_amdgcn_s_memrealtime();
       const unsigned long long gbest = wave_max_u64(bm);
       const unsigned long long bh = __ballot(bm == gbest && gbest != 0ull);  // keys are unique
       const int gnode = bh ? __builtin_amdgcn_readlane(bnode, (int)__builtin_ctzll(bh)) : -1;
@@ -2297,7 +2310,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         if (lane == 0 && (!chosen || s_cand_ok)) {
           gran_put(lv, q + 1, gid, 0, ga0);
           gran_put(lv, q + 1, gid, 1, s_ga[chosen ? 3 : 1]);
-          if (lv.wstamps) lv.wstamps[((size_t)(q + 1) * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
+          if (kSt && lv.wstamps) lv.wstamps[((size_t)(q + 1) * G + w) * 8] = __builtin_amdgcn_s_memrealtime();
         }
       }
       stamp_s(q, 4);
@@ -2437,7 +2450,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       }
       if (lane == 0) {
         s_cand_ok = cand_ok;
-        if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+        if (kSt && lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 5] = __builtin_amdgcn_s_memrealtime();
         __hip_atomic_store(&s_ga_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
 
@@ -2445,8 +2458,8 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // ======== evaluation waves: phase 1 of pod q+1 against the cores before this pod's assume.
       // Only the chosen node changes; its owner redoes it below.
       phase1(pod + 1, bn, npar, &d);
-      if (lv.stamps && w == 0 && t == 0) lv.stamps[(size_t)q * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-      if (lv.wstamps && lane == 0)  // the last evaluation wave's phase-1 end
+      if (kSt && lv.stamps && w == 0 && t == 0) lv.stamps[(size_t)q * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+      if (kSt && lv.wstamps && lane == 0)  // the last evaluation wave's phase-1 end
         atomicMax(&lv.wstamps[((size_t)q * G + w) * 8 + 6], __builtin_amdgcn_s_memrealtime());
     }
     __syncthreads();
@@ -2477,7 +2490,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       } else if (s_cand_ok) {  // the helper prepared everything: LDS stores, then publish
         if (t == wsl % U) {
           const int kw = wsl / U, cw = t >> 6;
-          if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+          if (kSt && lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
           NodeCore c = lds_core(s_core, kw, t);
           assume_core(c, d);
           s_core.rcpu[kw][t] = c.rcpu;
@@ -2495,7 +2508,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
           s_u[npar][1][cw] = s_cbelow;
           s_x[npar][0][cw] = s_cmt;
           s_x[npar][1][cw] = s_cmn;
-          if (lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+          if (kSt && lv.wstamps) lv.wstamps[((size_t)q * G + w) * 8 + 3] = __builtin_amdgcn_s_memrealtime();
           commit_result(m, b, base, d, rot_stats(pod, par), pod, F, win, s_best, &c, s_ipa);
           if constexpr (RING) ring_post(lv, q, b.results[pod]);
         }

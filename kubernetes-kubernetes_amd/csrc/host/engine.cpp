@@ -2766,6 +2766,11 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       lv.wave_map = c->cfg.loop_wave_map;
       lv.ring = ring_dev_;
       lv.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;  // s_memrealtime: 100 MHz
+      if (c->cfg.ring_relay_min > 0 && GS >= c->cfg.ring_relay_min) {  // as k_agg_loop's below (one buffer)
+        if ((rc = ensure(d_relay, (size_t)kRelayWords * 8))) return fail(rc);
+        HIPCHK(hipMemsetAsync(d_relay.p, 0, (size_t)kRelayWords * 8, s));
+        lv.relay = (unsigned long long*)d_relay.p;
+      }
       HIPCHK(launch_sched_loop(c->view, bview(kLoopMaxPods), lv, s, nullptr, nullptr, unit));
       res_gs_ = GS;
       res_unit_ = unit;

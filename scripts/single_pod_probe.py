@@ -5,7 +5,7 @@ ksg_schedule_batch of the same pods.  Prints one JSON line per workload.
 
   python scripts/single_pod_probe.py [workload ...]     c2 (SchedulingBasic 5000 nodes, default), c2pct0,
                                                         dts (DefaultTopologySpreading), c4 (TopologySpreading
-                                                        15000 nodes), c3, c4-anti, c5 (100 000 nodes)
+                                                        15000 nodes), c3, c4-anti, c5 (100 000 nodes), c2big (SchedulingBasic at 100 000 nodes)
   python scripts/single_pod_probe.py stamps [workload]  the resident call's host / device split
 single_resident_us times the calls from Python (ctypes), single_resident_native_us from native code
 (ksg_debug_schedule_calls), as a binding's goroutine issues them.
@@ -28,6 +28,8 @@ def cluster(wl, n_pods):
     objects = []
     if wl in ("c2", "c2pct0"):
         nodes, init, pods = synth.scheduling_basic(5000, 1000, n_pods)
+    elif wl == "c2big":  # SchedulingBasic pods on 100 000 nodes
+        nodes, init, pods = synth.scheduling_basic(100000, 1000, n_pods)
     elif wl == "dts":
         nodes, init, pods, objects = synth.default_topology_spreading(5000, 5000, n_pods)
     elif wl == "c3":
@@ -67,7 +69,7 @@ def run(wl, cfg, n_pods=2000, batch=False, check=False, native=False):
     mism = None
     if check:
         from oracle_binding import oracle
-        o = oracle(dict(percentageOfNodesToScore=0) if wl == "c2pct0" else {"cpuThreads": 16} if wl == "c5" else {})
+        o = oracle(dict(percentageOfNodesToScore=0) if wl == "c2pct0" else {"cpuThreads": 16} if wl in ("c5", "c2big") else {})
         for ob in objects:
             o.upsert_object(ob)
         for n in nodes:

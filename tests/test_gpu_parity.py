@@ -787,13 +787,16 @@ def test_sched_loop_prepared_and_fixup_paths(native, unit):
         assert g.compare_mirror(sync=False) == (0, -1)
 
 
-def test_resident_single_pod_calls(native):
+@pytest.mark.parametrize("relay", [False, True])
+def test_resident_single_pod_calls(native, relay):
     """ksg_schedule_one through the resident loop (node-local pods) against the oracle, pod by pod, with
     the events that must stop it in between: informer events, a forget, a batch, pods it declines
-    (PodTopologySpread), an idle gap longer than its self-stop, and more calls than one launch holds."""
+    (PodTopologySpread), an idle gap longer than its self-stop, and more calls than one launch holds;
+    relay: workgroup 0 relays the doorbell through device memory (ringRelayMinWorkgroups 1, the path of
+    clusters with many workgroups)."""
     import time
     rng, cfg, nodes, existing, names = rand_cluster(9300, n_nodes=900, n_existing=90, topology=False)
-    g, o = _pair(native, cfg, nodes, existing)
+    g, o = _pair(native, dict(cfg, ringRelayMinWorkgroups=1) if relay else cfg, nodes, existing)
     hist = []
 
     def one(pod, tag):
@@ -993,7 +996,7 @@ def test_agg_loop_same_template_runs(native, wg):
     assert g.compare_mirror(sync=False) == (0, -1)
 
 
-@pytest.mark.parametrize("debug", [0, 8, 28])
+@pytest.mark.parametrize("debug", [0, 8, 28, -1])
 def test_resident_agg_same_template_calls(native, debug):
     """ksg_schedule_one of runs of identical pods through the resident k_agg_loop: a pod posted right after
     one of its template is not staged over PCIe (RING_SAME: the loop copies the previous program and
@@ -1018,7 +1021,9 @@ def test_resident_agg_same_template_calls(native, debug):
     big["spec"]["containers"][0]["resources"] = {"requests": {"cpu": "1000"}}
     pods[40:40] = [big, dict(big, metadata=dict(big["metadata"], name="huge2", uid="huge2"))]
     pods[100:100] = dpods
-    g, o = _pair(native, {"aggLoopDebug": debug} if debug else {}, nodes, init)
+    # (debug -1: the doorbell and the staged program relayed through device memory, ringRelayMinWorkgroups 1)
+    g, o = _pair(native, {"ringRelayMinWorkgroups": 1} if debug < 0 else {"aggLoopDebug": debug} if debug else {},
+                 nodes, init)
     for ob in objects:
         for b in (g, o):
             b.upsert_object(ob)
