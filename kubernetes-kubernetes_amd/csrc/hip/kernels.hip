@@ -2677,8 +2677,8 @@ __device__ __forceinline__ void agran_put(const AggView& av, int q, int gid, int
   }
 }
 // One wave: poll granules [slot0, slot0 + NS) of every participant for pod q until all tags match.
-template <bool SHARD, int NS>
-__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep],
+template <bool SHARD, int NS, int MS>
+__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][MS],
                                            int nact = NS) {  // only granules [slot0, slot0 + nact) are polled
   const int lane = threadIdx.x & 63;
   const int P = (SHARD ? av.world : 1) * av.nwg;
@@ -2688,7 +2688,7 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
   for (uint32_t spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
-    for (int r = 0; r < kMaxSweep; ++r) {
+    for (int r = 0; r < MS; ++r) {
       const int v = lane + 64 * r;
 #pragma unroll
       for (int k = 0; k < NS; ++k) {
@@ -2749,8 +2749,11 @@ __device__ __forceinline__ void apply_entry(const MirrorView& m, const uint8_t* 
 // RING: the resident instance (ksg_schedule_one of PodTopologySpread / InterPodAffinity pods):
 // pods through av.ring, each a run of its own -- gathered when it arrives (or, same template, folded at the
 // end of the pod before it), no staging ahead.
-template <bool SHARD, bool PTSS, bool RING = false>
+// MS: sweep rounds of 64 participants (kMaxSweep = 4: up to 256; the 1-round instance for grids of at most 64
+// workgroups holds a quarter of the exchange registers, which pays for the PodTopologySpread PX skip, as in RING)
+template <bool SHARD, bool PTSS, bool RING = false, int MS = kMaxSweep>
 __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
+  constexpr bool kPxa = RING || MS < kMaxSweep;  // phase 1 guesses the PTS raw scores (AG_PXA)
   constexpr int kBlob = RING ? kBlobLds : kAggBlobLds;       // program slot bytes (desc.h)
   constexpr uint32_t kLp = RING ? kAggRingPods : kAggPods;     // LDS list entries (the rest spill to HBM)
   constexpr uint32_t kLt = RING ? kAggRingTerms : kAggTerms;
@@ -2782,7 +2785,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ uint32_t s_psz[kAggScoreCons];                // PTS topology sizes of the pod being decided
   __shared__ uint32_t s_psz_used[kAggScoreCons];           // ... of the previous PTS-scored pod (~0: none),
   __shared__ double s_pwt[kAggScoreCons];                  //   their weights log(size + 2),
-  __shared__ uint32_t s_praw[PTSS && RING ? kAggThreads : 1];  // phase 1's raw scores with them (~0: not scored)
+  __shared__ uint32_t s_praw[PTSS && kPxa ? kAggThreads : 1];  // phase 1's raw scores with them (~0: not scored)
   __shared__ unsigned long long s_wq[kAggThreads / 64][2]; //   and their per-wave {max + 1, 2^24 - 1 - min}
   __shared__ unsigned long long s_pxm[2];                  // wave 1 -> 0: its half's raw PTS max+1 / reversed min
   __shared__ int s_px_q, s_pxd_q;                          // wave 1 -> 0: half done; wave 0 -> 1: exchange PX done
@@ -2832,11 +2835,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   const bool my_node = kk < nk && my_i < m.n;
   auto stamp = [&](int q, int k) {
 #ifndef KSG_DIAG
-    if constexpr (RING) return;  // the resident instance's stamps: the diagnostic build (registers)
+    if constexpr (kPxa) return;  // the resident / 1-round instances' stamps: the diagnostic build (registers)
 #endif
     if (av.stamps && w == 0 && t == 0) av.stamps[(size_t)q * kAggStamps + k] = __builtin_amdgcn_s_memrealtime();
   };
   auto wstamp = [&](int q, int k) {  // thread 0 of every workgroup
+#ifndef KSG_DIAG
+    if constexpr (kPxa) return;
+#endif
     if (av.wstamps && t == 0) av.wstamps[((size_t)q * G + w) * 4 + k] = __builtin_amdgcn_s_memrealtime();
   };
   auto fail = [&](uint32_t code) {
@@ -3045,12 +3051,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   };
   // exchange Z of pod q (wave 0): OR of the any bits, node-local minima and domain counts
   auto sweep_z = [&](int q) __attribute__((always_inline)) {
-    unsigned long long z[3][kMaxSweep];
+    unsigned long long z[3][MS];
     const bool ok = agran_sweep<SHARD, 3>(av, q, AG_Z0, z);
     uint32_t a = 0, c1 = 0, c2 = 0;
     unsigned long long m1 = 0xffffffull, m2 = 0xffffffull;
 #pragma unroll
-    for (int r = 0; r < kMaxSweep; ++r)
+    for (int r = 0; r < MS; ++r)
       if (lane + 64 * r < P) {
         a |= (uint32_t)z[0][r];
         const unsigned long long x1 = z[1][r] & 0xffffffull, x2 = z[2][r] & 0xffffffull;
@@ -3324,7 +3330,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     // region before every participant has started (one granule row past the pods, kAggStartRow)
     if (t == 0) agran_put<SHARD>(av, kAggStartRow, gid, 0, 1ull);
     if (wave == 0) {
-      unsigned long long x0[1][kMaxSweep];
+      unsigned long long x0[1][MS];
       if (!agran_sweep<SHARD, 1>(av, kAggStartRow, 0, x0) && lane == 0) s_ok = 0u;
     }
     __syncthreads();
@@ -3538,7 +3544,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     }
     __syncthreads();
-    if (PTSS && RING && ((d.score_mask >> P_PTS) & 1u) && s_psz_used[0] != ~0u) {
+    if (PTSS && kPxa && ((d.score_mask >> P_PTS) & 1u) && s_psz_used[0] != ~0u) {
       // each slot's raw PodTopologySpread score with the previous scored pod's topology sizes (the
       // arithmetic of the score pass after exchange A, below); exchange A checks the sizes and carries
       // the max / min (AG_PXA)
@@ -3617,17 +3623,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
               hx = s_wq[v][0] > hx ? s_wq[v][0] : hx;
               hn = s_wq[v][1] > hn ? s_wq[v][1] : hn;
             }
-            if (RING) agran_put<SHARD>(av, q, gid, AG_PXA, (hx << 24) | hn);
+            if (kPxa) agran_put<SHARD>(av, q, gid, AG_PXA, (hx << 24) | hn);
           }
           wstamp(q, 1);
         }
         const bool pts_q = PTSS && ((d.score_mask >> P_PTS) & 1u) != 0;
-        unsigned long long xa[6][kMaxSweep];
+        unsigned long long xa[6][MS];
         const bool ok = agran_sweep<SHARD, 6>(av, q, AG_A0, xa, pts_q ? 6 : 4);
         uint32_t F = 0, wp = 0, bf = 0;
         unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
 #pragma unroll
-        for (int r = 0; r < kMaxSweep; ++r) {
+        for (int r = 0; r < MS; ++r) {
           const int v = lane + 64 * r;
           if (v < P) {
             const uint32_t c = gran_a_count(xa[0][r]);
@@ -3652,7 +3658,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           uint32_t ni = 0;
           unsigned long long p0 = 0, p1 = 0;
 #pragma unroll
-          for (int r = 0; r < kMaxSweep; ++r)
+          for (int r = 0; r < MS; ++r)
             if (lane + 64 * r < P) {
               ni += (uint32_t)(xa[5][r] & 0xfffffull);
               p0 |= xa[4][r];
@@ -3698,7 +3704,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         // (scoring.go:199-226; k_pts_score's arithmetic), into s_pc[0]; NormalizeScore's max / min over
         // every workgroup's scored nodes by exchange PX (scoring.go:229-268).  When the sizes are the ones
         // phase 1 guessed (s_psz_used), its raw scores stand and exchange A carried the max / min (AG_PXA).
-        spec = RING && __ballot(lane < d.n_ptss && lane < kAggScoreCons && s_psz[lane] != s_psz_used[lane]) == 0ull &&
+        spec = kPxa && __ballot(lane < d.n_ptss && lane < kAggScoreCons && s_psz[lane] != s_psz_used[lane]) == 0ull &&
                !(av.debug & 16);
         const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
         const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
@@ -3751,11 +3757,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             hmn = s_pxm[1] > hmn ? s_pxm[1] : hmn;
             if (lane == 0) agran_put<SHARD>(av, q, gid, AG_PX, (hmx << 24) | hmn);
           }
-          unsigned long long xp[1][kMaxSweep];
+          unsigned long long xp[1][MS];
           const bool okp = agran_sweep<SHARD, 1>(av, q, spec ? AG_PXA : AG_PX, xp);
           unsigned long long gx = 0, gn = 0;
 #pragma unroll
-          for (int r = 0; r < kMaxSweep; ++r)
+          for (int r = 0; r < MS; ++r)
             if (lane + 64 * r < P) {
               const unsigned long long a = xp[0][r] >> 24, bb = xp[0][r] & 0xffffffull;
               gx = a > gx ? a : gx;
@@ -3765,7 +3771,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           gn = wave_max_u64(gn);
           // the next pod's guess (wave 1 decided spec before this: on a mismatch it published PX first, and on a
           // match the update writes the values it compared)
-          if (RING && lane < d.n_ptss && lane < kAggScoreCons) {
+          if (kPxa && lane < d.n_ptss && lane < kAggScoreCons) {
             s_psz_used[lane] = s_psz[lane];
             s_pwt[lane] = m.log_tab[s_psz[lane] + 2];
           }
@@ -3859,12 +3865,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           agran_put<SHARD>(av, q, gid, AG_BN, (unsigned long long)(uint32_t)(wn + 1) | ((unsigned long long)el << 32));
         }
         stamp(q, 3);
-        unsigned long long xb[2][kMaxSweep];
+        unsigned long long xb[2][MS];
         const bool okb = ok && agran_sweep<SHARD, 2>(av, q, AG_B, xb);
         unsigned long long bmx = 0, bnx = 0;
         int bpart = -1;
 #pragma unroll
-        for (int r = 0; r < kMaxSweep; ++r) {
+        for (int r = 0; r < MS; ++r) {
           const unsigned long long v = (lane + 64 * r) < P ? xb[0][r] : 0ull;
           if (v > bmx) {
             bmx = v;
@@ -4256,7 +4262,8 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
   } else if (av.world > 1) {
     go(k_agg_loop<true, true>);  // (the sharded instance without PTSS spills registers: not built)
   } else {
-    if (av.ptss) go(k_agg_loop<false, true>);
+    if (av.ptss && av.nwg <= 64) go(k_agg_loop<false, true, false, 1>);
+    else if (av.ptss) go(k_agg_loop<false, true>);
     else go(k_agg_loop<false, false>);
   }
   return hipGetLastError();
@@ -4293,6 +4300,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_agg_loop<false, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<true, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<false, true, true>),
+                      reinterpret_cast<const void*>(&k_agg_loop<false, true, false, 1>),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
