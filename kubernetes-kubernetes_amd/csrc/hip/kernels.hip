@@ -2905,7 +2905,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       else atomicAdd(&s_lh[(-1 - lref) * kAggSlots + ls], (int32_t)wt);
     };
     const uint32_t np = s_np, nitems = s_np + ((d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE)) ? s_nt : 0u);
-    for (uint32_t k = (uint32_t)tid; k < nitems; k += (uint32_t)nthr) {
+    // a pod with no selector of its own (only existing pods' terms to test, e.g. a plain pod beside
+    // anti-affinity pods) has nothing to do in the pod role: its scan starts at the term role
+    const bool pod_role = d.n_ptsf || (PTSS && d.n_ptss) || d.n_raff || d.n_ranti || (d.ipa_flags & IPA_PREF);
+    for (uint32_t k = (pod_role ? 0u : np) + (uint32_t)tid; k < nitems; k += (uint32_t)nthr) {
       if (k < np) {
         // pod role: the pod's selectors against one pod on my nodes (k_aggregate's pod role)
         const uint32_t e = k < kLp ? s_pods[k] : spl[k - kLp];
