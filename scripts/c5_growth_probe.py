@@ -1,6 +1,7 @@
 """Diagnostic: C5 (mixed 100k-node cluster) batch by batch -- wall ms, the batch's kernel stats (avg ms per
 pod, pods in a loop, kernel) and mirror re-layouts -- to show what changes as assumed pods accumulate.
-python scripts/c5_growth_probe.py [batches] [nodes] [c5|c2] [stamps]  (c2: SchedulingBasic, 1000 init pods;
+python scripts/c5_growth_probe.py [batches] [nodes] [c5|c2|c3|dts|c4|c4-anti] [stamps]  (c2: SchedulingBasic, 1000 init
+pods; c3 / dts / c4 / c4-anti: as many init pods as nodes;
 stamps: loopStamps, the loops' per-phase breakdown of every batch on stderr)"""
 import os
 import sys
@@ -16,6 +17,12 @@ N = int(sys.argv[2]) if len(sys.argv) > 2 else 100000
 WL = sys.argv[3] if len(sys.argv) > 3 else "c5"
 if WL == "c2":
     nodes, init, pods = synth.scheduling_basic(N, 1000, B * 1000)
+elif WL == "c3":
+    nodes, init, pods = synth.scheduling_c3(N, N, B * 1000)
+elif WL == "dts":
+    nodes, init, pods = synth.default_topology_spreading(N, N, B * 1000)
+elif WL in ("c4", "c4-anti"):
+    nodes, init, pods = synth.topology_spreading(N, N, B * 1000, preferred_anti=WL == "c4-anti")
 else:
     nodes, init, pods = synth.mixed_cluster(N, N // 10, B * 1000)
 s = Scheduler({"device": 0, "kernelTimingStride": 1, "loopStamps": "stamps" in sys.argv[4:]})
