@@ -71,7 +71,8 @@ def parse():
     ap.add_argument("--no-sub", action="store_true",
                     help="no sub-records: the default N=1 SchedulingBasic line also carries the 100k-node C5 "
                          "record (BASELINE configs[4], the metric's second size) measured by a child bench.py")
-    ap.add_argument("--sub-steps", type=int, default=5, help="steps (of --batch pods) of the C5 sub-record")
+    ap.add_argument("--sub-steps", type=int, default=50,
+                    help="steps (of --batch pods) of the C5 sub-record: 50 x 1000 = BASELINE configs[4]'s 50000 pods")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per k_filter_score launch (from a separate rocprofv3 --pmc run)")
     return ap.parse_args()
@@ -194,7 +195,7 @@ def sub_record(a):
     except Exception as e:  # reported, never a silent omission
         return {"error": f"C5 sub-record failed: {e!r}"}
     keep = ("metric", "value", "unit", "node_evals_per_s", "steps", "warmup", "ms_per_step", "config", "placed",
-            "roofline", "cpu_baseline", "parity")
+            "roofline", "kernel_us_per_step", "cpu_baseline", "parity")
     return {k: sub.get(k) for k in keep}
 
 
@@ -419,6 +420,11 @@ def main():
                          "avg_kernel_us_unit": "per pod" if kname in ("k_sched_loop", "k_agg_loop") else "per launch",
                          "algo_bytes_per_launch": round(kbytes, 1),
                          "algo_bytes_unit": "per pod" if kname in ("k_sched_loop", "k_agg_loop") else "per launch"},
+            # the dominant kernel's per-pod (loops) or per-launch time in each timed step: a drift over the
+            # steps (C5's fill-front workgroup) shows as max vs min / first vs last
+            "kernel_us_per_step": {"kernel": kname, "min": round(min(k[0] for k in kstats) * 1e3, 3),
+                                   "max": round(max(k[0] for k in kstats) * 1e3, 3),
+                                   "first": round(kstats[0][0] * 1e3, 3), "last": round(kstats[-1][0] * 1e3, 3)},
             "cpu_baseline": cpu,
             "parity": parity,
         }

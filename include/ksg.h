@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 1
+#define KSG_ABI_VERSION 2 /* 2: ksg_eval_out.normalized_scores */
 
 /* ---- return codes of the ABI functions ------------------------------------------ */
 #define KSG_OK 0
@@ -99,10 +99,15 @@ typedef struct ksg_result {
   int64_t total_score;     /* TotalScore of the chosen node (0 if F <= 1) */
 } ksg_result;
 
-/* Full per-node view of one cycle, used by parity tests and diagnosis rebuilding
+/* Full per-node view of one cycle, used by parity tests, diagnosis rebuilding
  * (Diagnosis.NodeToStatus, framework/types.go:1082-1180; NodePluginScores,
- * interface.go:284-295).  All arrays are caller-owned, sized for ksg_num_nodes()
- * (and KSG_NUM_PLUGINS x num_nodes for plugin_scores), indexed by snapshot index. */
+ * interface.go:284-295) and the plugin-level shim.  All arrays are
+ * caller-owned, sized for ksg_num_nodes() (and KSG_NUM_PLUGINS x num_nodes for
+ * plugin_scores / normalized_scores), indexed by snapshot index; any may be NULL.
+ * normalized_scores is what a ScorePlugin's Score + NormalizeScore hand RunScorePlugins
+ * (framework.go:1351-1423): in [0, 100] for every plugin in score_plugin_mask;
+ * plugin_scores is that value times the profile weight (framework.go:1434-1446), and
+ * total_scores their sum -- NodePluginScores.TotalScore. */
 typedef struct ksg_eval_out {
   int32_t prefilter_code;    /* non-success PreFilter status code (0 if PreFilter passed) */
   int32_t prefilter_plugin;  /* plugin that produced it, KSG_PLUGIN_NONE otherwise */
@@ -112,6 +117,7 @@ typedef struct ksg_eval_out {
   uint32_t score_plugin_mask;/* out: bit p set if score plugin p ran (not skipped) */
   int64_t *plugin_scores;    /* [KSG_NUM_PLUGINS][N] weighted normalised score (feasible nodes) */
   int64_t *total_scores;     /* [N] TotalScore (feasible nodes; 0 elsewhere) */
+  int64_t *normalized_scores;/* [KSG_NUM_PLUGINS][N] normalised score before the weight (ABI 2) */
 } ksg_eval_out;
 
 /* ---- context ------------------------------------------------------------------------
@@ -217,14 +223,14 @@ int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uin
  * Potential nodes are taken in snapshot order (the reference iterates a map there) and checked with
  * Parallelizer parallelism 1 semantics; victims of equal priority and start time keep NodeInfo.Pods
  * order; candidates tied on every criterion resolve to the earliest in candidate-list order.
- * The device re-evaluates a victim's removal for NodeResourcesFit, NodePorts and the pod's
- * PodTopologySpread / InterPodAffinity counts (RemovePod / AddPod extensions) for up to 8 spread
- * constraints, affinity terms and topology keys.  KSG_ENOTSUP (nothing selected; ctx->err says
- * which): a preemptor with more than 4 scalar resources; a victim whose effect on those counts is
- * beyond that (more constraints / terms / keys); and, on the host-staged record path (a call whose
- * "now" precedes a bound pod's start time while pods without status.startTime exist, scalar-grouped
- * preemptors, more than 8 budgets, nodes of more than 128 pods), any victim that changes the pod's
- * DoNotSchedule spread counts or shares required affinity terms with it.  detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
+ * The device re-evaluates a victim's removal for NodeResourcesFit (every requested resource, extended
+ * ones included), NodePorts and the pod's PodTopologySpread / InterPodAffinity counts (RemovePod /
+ * AddPod extensions, filtering.go:157-212 / interpodaffinity/filtering.go:75-85), on both device paths
+ * (the resident pod segments, and host-staged records for nodes of more than 128 pods, more than two
+ * host ports per pod, more than 8 budgets, or a "now" earlier than a bound pod's start time).
+ * KSG_ENOTSUP (nothing selected; ctx->err says which): a victim that moves the pod's counts under more
+ * than 8 spread constraints, required affinity terms or existing-anti-affinity topology keys.
+ * detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
  * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}] (listCandidates),
  * "selected": <node|null>, "victims": [uid...]}; *detail_len gets its length (KSG_ENOMEM if cap is
  * too small; the result is still filled). */
@@ -279,6 +285,12 @@ int ksg_debug_compare_mirror(ksg_ctx *ctx, int32_t sync, int32_t *ndiff, int32_t
  * how many node adds / removes / zone moves were applied by moving the unchanged nodes' columns on
  * the device instead (*gather; UpdateSnapshot's list rebuild, cache.go:273-283). */
 int ksg_debug_relayouts(const ksg_ctx *ctx, uint64_t *full, uint64_t *gather);
+
+/* Persistent-loop health: *give_ups counts the batches whose persistent loop gave up (an exchange granule
+ * never arrived within 10 s, or a forced debugLoopGiveUpAt), *retries the batches an in-process node-sharded
+ * group then re-ran over the all-reduce path (every rank having given up at the same pod).
+ * Both stay 0 in a healthy run; the tests assert it. */
+int ksg_debug_loop_stats(const ksg_ctx *ctx, uint64_t *give_ups, uint64_t *retries);
 
 /* Parity diagnostic (no device needed): fills out[k] = math.Log(float64(k)) for 0 <= k < n with
  * the table PodTopologySpread's score kernel reads (topologyNormalizingWeight, podtopologyspread/

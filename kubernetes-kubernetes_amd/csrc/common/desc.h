@@ -424,7 +424,7 @@ struct BatchView {
   uint32_t* blk_cnt;      // [blocks] feasible nodes per block
   int64_t* fixed;         // [cap] weighted sum of the non-normalised plugin scores
   int64_t* raw;           // [kNumPlugins][cap] raw scores of normalising plugins (+ eval mode: all)
-  int64_t* out_scores;    // eval mode: [kNumPlugins][cap] weighted normalised scores
+  int64_t* out_scores;    // eval mode: [kNumPlugins][cap] normalised scores, unweighted
   int64_t* out_total;     // eval mode: [cap]
   unsigned long long* arena;  // PTS/IPA histograms (zero between pods)
 };

@@ -788,21 +788,21 @@ __device__ int64_t node_total(const BatchView& b, const PodDesc& d, const NormSt
     const int64_t r = b.raw[P_TAINT * cap + i];
     const int64_t v = mx == 0 ? 100 : 100 - go_div(100 * r, mx);
     total += v * d.weight[P_TAINT];
-    if (eval) b.out_scores[P_TAINT * cap + i] = v * d.weight[P_TAINT];
+    if (eval) b.out_scores[P_TAINT * cap + i] = v;
   }
   if ((sm >> P_NA) & 1u) {  // DefaultNormalizeScore(100, reverse=false)
     const int64_t mx = ns.mx_na;
     const int64_t r = b.raw[P_NA * cap + i];
     const int64_t v = mx == 0 ? 0 : go_div(100 * r, mx);
     total += v * d.weight[P_NA];
-    if (eval) b.out_scores[P_NA * cap + i] = v * d.weight[P_NA];
+    if (eval) b.out_scores[P_NA * cap + i] = v;
   }
   if ((sm >> P_PTS) & 1u) {  // PodTopologySpread.NormalizeScore (podtopologyspread/scoring.go:229-268)
     const int64_t mx = ns.mx_pts, mn = ns.mn_pts;
     const int64_t r = b.raw[P_PTS * cap + i];
     const int64_t v = r == -1 ? 0 : (mx == 0 ? 100 : go_div(100 * (mx + mn - r), mx));
     total += v * d.weight[P_PTS];
-    if (eval) b.out_scores[P_PTS * cap + i] = v * d.weight[P_PTS];
+    if (eval) b.out_scores[P_PTS * cap + i] = v;
   }
   if ((sm >> P_IPA) & 1u) {  // InterPodAffinity.NormalizeScore (interpodaffinity/scoring.go:258-290)
     const int64_t r = b.raw[P_IPA * cap + i];
@@ -815,12 +815,12 @@ __device__ int64_t node_total(const BatchView& b, const PodDesc& d, const NormSt
       v = (int64_t)f;
     }
     total += v * d.weight[P_IPA];
-    if (eval) b.out_scores[P_IPA * cap + i] = v * d.weight[P_IPA];
+    if (eval) b.out_scores[P_IPA * cap + i] = v;
   }
-  if (eval) {
-    if ((sm >> P_FIT) & 1u) b.out_scores[P_FIT * cap + i] = b.raw[P_FIT * cap + i] * d.weight[P_FIT];
-    if ((sm >> P_BAL) & 1u) b.out_scores[P_BAL * cap + i] = b.raw[P_BAL * cap + i] * d.weight[P_BAL];
-    if ((sm >> P_IMG) & 1u) b.out_scores[P_IMG * cap + i] = b.raw[P_IMG * cap + i] * d.weight[P_IMG];
+  if (eval) {  // evaluation output: each plugin's normalised, unweighted score (the host applies the weights)
+    if ((sm >> P_FIT) & 1u) b.out_scores[P_FIT * cap + i] = b.raw[P_FIT * cap + i];
+    if ((sm >> P_BAL) & 1u) b.out_scores[P_BAL * cap + i] = b.raw[P_BAL * cap + i];
+    if ((sm >> P_IMG) & 1u) b.out_scores[P_IMG * cap + i] = b.raw[P_IMG * cap + i];
   }
   return total;
 }

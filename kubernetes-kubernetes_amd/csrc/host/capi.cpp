@@ -383,6 +383,13 @@ int ksg_debug_relayouts(const ksg_ctx* ctx, uint64_t* full, uint64_t* gather) {
   return KSG_OK;
 }
 
+int ksg_debug_loop_stats(const ksg_ctx* ctx, uint64_t* give_ups, uint64_t* retries) {
+  if (!ctx || !give_ups || !retries) return KSG_EINVAL;
+  *give_ups = ctx->engine->loop_give_ups_;
+  *retries = ctx->engine->loop_retries_;
+  return KSG_OK;
+}
+
 int ksg_debug_log_table(double* out, int32_t n) {
   if (!out || n < 0) return KSG_EINVAL;
   for (int32_t k = 0; k < n; ++k) out[k] = ksg::go_log((double)k);  // as Cluster::upload_pod_table builds it

@@ -221,6 +221,22 @@ class LocalComm : public Comm {
     return g->members == g->world && g->own_queues;
   }
 
+  int agree(int64_t mine, std::vector<int64_t>* all) override {
+    int64_t v = mine;
+    int sl = 0;
+    if (!rendezvous(reinterpret_cast<unsigned long long*>(&v), nullptr, 0, &sl)) {
+      err = "local exchange: outcome rendezvous timed out";
+      return KSG_EDEVICE;
+    }
+    all->assign(world, 0);
+    for (int r = 0; r < world; ++r) (*all)[r] = *reinterpret_cast<const int64_t*>(g->snap_bufs[sl][r]);
+    if (!rendezvous(nullptr, nullptr, 0, &sl)) {  // every rank has read the others' values (on their stacks)
+      err = "local exchange: outcome rendezvous timed out";
+      return KSG_EDEVICE;
+    }
+    return KSG_OK;
+  }
+
   int launch_gate() override {
     int sl = 0;
     if (!rendezvous(nullptr, nullptr, 0, &sl)) {

@@ -44,6 +44,12 @@ class Comm {
   // every rank's stream has a hardware queue of its own (in-process groups: all ranks joined and
   // each Cluster::own_queue; RCCL ranks each own a device)
   virtual bool own_queues() const { return true; }
+  // host-side: all[r] = rank r's `mine` (in-process groups; the RCCL transport has no host channel and
+  // returns only its own value)
+  virtual int agree(int64_t mine, std::vector<int64_t>* all) {
+    all->assign(1, mine);
+    return 0;
+  }
   std::string err;
 };
 

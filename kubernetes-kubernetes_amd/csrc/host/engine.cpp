@@ -1333,10 +1333,32 @@ int Engine::run_batch_api(const std::vector<const PodSpec*>& pods, const std::ve
                           ksg_result* results, ksg_eval_out* eval) {
   fault_first_ = -1;
   const int rc = run_batch(pods, handles, assume, results, eval);
-  const int f = fault_first_;
-  if (rc != KSG_EDEVICE || f < 0 || f >= (int)pods.size() || !comm || !c->cfg.nccl_id.empty() || eval) return rc;
-  // every rank of the group lands here for the same chunk (each rank's loop gives up on the same missing
-  // participants; a late rank's loop gives up once it runs alone) and re-runs the same pods, in step
+  if (fault_first_ >= 0) ++loop_give_ups_;
+  if (!comm || !c->cfg.nccl_id.empty() || eval) return rc;
+  // In-process groups (one device): every rank learns every rank's outcome before anyone retries.  A loop
+  // give-up re-runs the chunk over the all-reduce path only when every rank gave up at the same pod (each
+  // rank's loop gives up on the same missing participants; a late rank's once it runs alone); a rank that
+  // finished the chunk while another gave up would otherwise pair different pods' exchanges.
+  const int64_t mine = rc == KSG_OK ? -1 : (rc == KSG_EDEVICE && fault_first_ >= 0 ? fault_first_ : -2);
+  std::vector<int64_t> all;
+  if (comm->agree(mine, &all) != KSG_OK) {
+    c->err = comm->err;
+    return KSG_EDEVICE;
+  }
+  bool same = true;
+  for (int64_t v : all) same = same && v == all[0];
+  if (same && all[0] == -1) return rc;  // every rank scheduled the batch
+  const int f = (int)all[0];
+  if (!same || f < 0 || f >= (int)pods.size()) {
+    std::string o;
+    for (size_t r = 0; r < all.size(); ++r)
+      o += (r ? ", rank " : "rank ") + std::to_string(r) + ": " +
+           (all[r] == -1 ? std::string("scheduled") : all[r] == -2 ? std::string("error") : "gave up at pod " + std::to_string(all[r]));
+    if (rc == KSG_OK) c->err.clear();
+    c->err = (c->err.empty() ? std::string() : c->err + "; ") + "in-process group out of step (" + o +
+             "): no retry; rebuild the group";
+    return rc == KSG_OK ? KSG_EDEVICE : rc;
+  }
   const std::string why = c->err;
   const std::vector<const PodSpec*> rest(pods.begin() + f, pods.end());
   const std::vector<int32_t> rh(handles.begin() + f, handles.end());
@@ -2376,9 +2398,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       if (eval->node_reasons) eval->node_reasons[i] = status_reasons(w);
       const bool scored = hr[0].feasible > 1 && status_code(w) == 0;
       if (eval->total_scores) eval->total_scores[i] = scored ? tot[i] : 0;
-      if (eval->plugin_scores)
-        for (int q = 0; q < kNumPlugins; ++q)
-          eval->plugin_scores[(size_t)q * N + i] = scored ? outs[(size_t)q * m.cap + i] : 0;
+      for (int q = 0; q < kNumPlugins; ++q) {  // the device wrote NormalizeScore's output; the weights are
+        const int64_t v = scored ? outs[(size_t)q * m.cap + i] : 0;  // applied here (framework.go:1434-1446)
+        if (eval->normalized_scores) eval->normalized_scores[(size_t)q * N + i] = v;
+        if (eval->plugin_scores) eval->plugin_scores[(size_t)q * N + i] = v * c->cfg.weight[q];
+      }
     }
   }
   return KSG_OK;
@@ -2715,6 +2739,8 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       }
     }
   }
+  bool reposted = false;
+relaunch:
   // the running launch sees the mirror as it is, or it stops (so does a launch of the other kind)
   if (res_running_ && (c->mirror_pending() || res_q_ >= kLoopMaxPods || res_kind_ != kind ||
                        (kind == 1 && (GS != res_gs_ || unit != res_unit_)) || (kind == 2 && G != res_gs_) ||
@@ -2875,7 +2901,7 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     // the counts it holds instead of gathering them again (k_agg_loop's batch shortcut, DF_AGG_SAME)
     const bool aggsame = q > 0 && agg_same(res_prev_blob_, cp.blob);
     PodDesc& hd = *reinterpret_cast<PodDesc*>(cp.blob.data());
-    if (aggsame) hd.flags |= DF_AGG_SAME;
+    hd.flags = aggsame ? (hd.flags | DF_AGG_SAME) : (hd.flags & ~DF_AGG_SAME);  // (a repost after a relaunch: q 0)
     // the previous pod's program and entry but for the slot, the rotation and the label-pool offset: the
     // loop copies them in LDS (PodRing::ll, RING_SAME) instead of reading both over PCIe
     bool same = q > 0 && res_prev_blob_.size() == cp.blob.size() && res_prev_entry_.size() == entry_bytes;
@@ -2885,7 +2911,7 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
       const PodDesc keep = pd;
       pd.slot = hd.slot;
       pd.rot_start = hd.rot_start;
-      pd.flags = hd.flags;
+      pd.flags = (pd.flags & ~DF_AGG_SAME) | (hd.flags & DF_AGG_SAME);  // the one flag the loop patches
       same = std::memcmp(res_prev_blob_.data(), cp.blob.data(), bytes) == 0;
       pd = keep;
     }
@@ -2931,14 +2957,31 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     if ((spins & 0xfffu) == 0 && clk::now() - tw > std::chrono::seconds(5)) {  // never: fail loudly, not hang
       __atomic_store_n(&ring_->ctl, kCtlStop, __ATOMIC_RELEASE);
       __atomic_store_n(&ring_->ll[0], (unsigned long long)kRingStop, __ATOMIC_RELEASE);
-      c->err = "resident loop: no result for the posted pod after 5 s";
+      // the loop leaves at its next poll (or at its exchanges' own give-up): drained before anything else
+      // uses the stream; it may still have committed the pod into the device mirror, which is therefore
+      // rebuilt from the cache, where the pod never arrives
+      (void)hipStreamSynchronize(s);
+      res_running_ = false;
+      c->layout_dirty = true;
+      c->mirror_suspect = true;
+      c->pods_dirty = true;
+      c->err = "resident loop: no result for the posted pod after 5 s; the device mirror is rebuilt from the cache";
       return fail(KSG_EDEVICE);
     }
     if ((spins & 0xfffu) == 0 && hipStreamQuery(s) != hipErrorNotReady) {  // the launch ended without it
       res_running_ = false;
       (void)hipStreamSynchronize(s);
+      if (__atomic_load_n(&rr.seq, __ATOMIC_ACQUIRE) == (uint32_t)(q + 1)) break;  // it landed after all
       uint32_t f[kFailWords] = {};
       (void)hipMemcpyAsync(f, d_fail.p, kFailBytes, hipMemcpyDeviceToHost, s);
+      (void)hipStreamSynchronize(s);
+      if (!f[0] && __atomic_load_n(&ring_->exited, __ATOMIC_ACQUIRE) == 1u && !reposted) {
+        // the loop left on its idle timer before this pod was posted (a host thread held up past the
+        // window, e.g. by the cgroup quota): no workgroup took the pod -- one that had would have waited
+        // for the others' exchanges and given up (f[0]) -- so a new launch takes it
+        reposted = true;
+        goto relaunch;
+      }
       const int ng = res_kind_ == 2 ? kAGran : kGran;
       const DevBuf& gb = res_kind_ == 2 ? d_agran : d_gran;
       std::vector<unsigned long long> row((size_t)res_gs_ * ng);

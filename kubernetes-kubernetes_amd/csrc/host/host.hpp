@@ -554,6 +554,7 @@ class Engine {
   int fault_first_ = -1;        // the first pod loop_fault left unscheduled (-1: none), for run_batch_api
   bool force_allreduce_ = false;  // run_batch_api's retry: no device exchange
   uint64_t loop_retries_ = 0;   // batches run_batch_api re-ran over the all-reduce path
+  uint64_t loop_give_ups_ = 0;  // batches whose persistent loop gave up (forced ones included)
   int run_plugin(const PodSpec& p, Mode mode, int plugin, const uint8_t* nodes, int32_t* code, uint8_t* codes,
                  uint32_t* reasons, int64_t* raw, int64_t* norm);
   // DefaultPreemption's PostFilter for a pod that failed its cycle (preempt.cpp)

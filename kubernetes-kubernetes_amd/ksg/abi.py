@@ -88,6 +88,7 @@ class EvalOut(C.Structure):
         ("score_plugin_mask", C.c_uint32),
         ("plugin_scores", C.POINTER(C.c_int64)),
         ("total_scores", C.POINTER(C.c_int64)),
+        ("normalized_scores", C.POINTER(C.c_int64)),
     ]
 
 
@@ -238,7 +239,8 @@ class Backend:
             reas = (C.c_uint32 * n)()
             ps = (C.c_int64 * (n * NUM_PLUGINS))()
             tot = (C.c_int64 * n)()
-            ev = EvalOut(0, 0, code, plug, reas, 0, ps, tot)
+            nrm = (C.c_int64 * (n * NUM_PLUGINS))()
+            ev = EvalOut(0, 0, code, plug, reas, 0, ps, tot, nrm)
             evp = C.byref(ev)
         self._chk(self.f["schedule_one"](self.ctx, handle, FLAG_ASSUME if assume else 0, C.byref(r), evp), "schedule_one")
         if not evaluate:
@@ -253,6 +255,7 @@ class Backend:
             "score_plugin_mask": ev.score_plugin_mask,
             "plugin_scores": [[ev.plugin_scores[p * n + i] for i in range(n)] for p in range(NUM_PLUGINS)],
             "total_scores": [ev.total_scores[i] for i in range(n)],
+            "normalized_scores": [[ev.normalized_scores[p * n + i] for i in range(n)] for p in range(NUM_PLUGINS)],
         }
         return r, out
 

@@ -37,6 +37,8 @@ def load():
         lib.ksg_generation.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib.ksg_debug_compare_mirror.restype = C.c_int
         lib.ksg_debug_compare_mirror.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.ksg_debug_loop_stats.restype = C.c_int
+        lib.ksg_debug_loop_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         from .abi import Result
         lib.ksg_debug_schedule_calls.restype = C.c_int
         lib.ksg_debug_schedule_calls.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_uint32,
@@ -72,6 +74,13 @@ class Scheduler(Backend):
         lg, ev = C.c_uint64(), C.c_uint64()
         self._chk(self.lib.ksg_generation(self.ctx, C.byref(lg), C.byref(ev)), "generation")
         return lg.value, ev.value
+
+    def loop_stats(self):
+        """(batches whose persistent loop gave up, batches an in-process group re-ran over the all-reduce
+        path) so far (ksg_debug_loop_stats)."""
+        g, r = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.ksg_debug_loop_stats(self.ctx, C.byref(g), C.byref(r)), "loop_stats")
+        return g.value, r.value
 
     def relayouts(self):
         """(full mirror rebuilds, gather re-layouts) so far (ksg_debug_relayouts)."""

@@ -1481,6 +1481,8 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     }
     if (ev->plugin_scores)
       for (int i = 0; i < N * KSG_NUM_PLUGINS; ++i) ev->plugin_scores[i] = 0;
+    if (ev->normalized_scores)
+      for (int i = 0; i < N * KSG_NUM_PLUGINS; ++i) ev->normalized_scores[i] = 0;
   }
   auto idx_of = [](const NodeInfoO* ni) { return ni->pos; };
   if (N == 0) { res->status = KSG_CODE_ERROR; return KSG_OK; }  // ErrNoNodesAvailable
@@ -1718,6 +1720,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
         int64_t w = s * c->cfg.weight[p];
         if (!pw) totals[i] += w;
         if (ev && ev->plugin_scores) ev->plugin_scores[(size_t)p * N + idx_of(feasible[i])] = w;
+        if (ev && ev->normalized_scores) ev->normalized_scores[(size_t)p * N + idx_of(feasible[i])] = s;
       }
     }
   }

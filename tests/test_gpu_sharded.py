@@ -68,12 +68,18 @@ def _run_ranks(ranks, pods, chunk):
     return out
 
 
-def _check(ranks, o, pods, chunk=64):
+def _check(ranks, o, pods, chunk=64, forced_give_up=False):
     got = _run_ranks(ranks, pods, chunk)
     for k, p in enumerate(pods):
         want = o.schedule_one(o.compile(p), assume=True)[0].as_tuple()
         for r in range(len(ranks)):
             assert got[r][k] == want, f"rank {r} pod {k}: {got[r][k]} != oracle {want}"
+    # (give-ups, all-reduce re-runs) per rank: a recovered give-up must not pass as a clean run
+    stats = [s.loop_stats() for s in ranks]
+    if forced_give_up:
+        assert all(g >= 1 and r >= 1 for g, r in stats), stats
+    else:
+        assert all(st == (0, 0) for st in stats), f"persistent-loop give-ups / re-runs per rank: {stats}"
 
 
 def test_shard_ranges_partition_the_snapshot():
@@ -410,7 +416,7 @@ def test_loop_give_up_retried_over_allreduce(world):
     from ksg.synth import mixed_cluster
     nodes, init, pods = mixed_cluster(3000, 600, 400)
     ranks, o = _group(world, {"deviceExchange": True, "debugLoopGiveUpAt": 40}, nodes, init)
-    _check(ranks, o, pods, chunk=400)
+    _check(ranks, o, pods, chunk=400, forced_give_up=True)
     for s in ranks:
         assert s.compare_mirror(sync=True)[0] == 0
 
