@@ -169,8 +169,9 @@ int ksg_node_name(const ksg_ctx *ctx, int32_t index, char *buf, size_t cap);
  * KSG_ENOTSUP: the pod needs a plugin outside the device path -- a PersistentVolumeClaim, generic
  * ephemeral, CSI-migratable in-tree (GCE PD, AWS EBS, Cinder, Azure Disk/File, vSphere, Portworx), RBD
  * or iSCSI volume (VolumeBinding, VolumeZone, NodeVolumeLimits, VolumeRestrictions) or
- * spec.resourceClaims (DynamicResources).  The context is unaffected; such pods stay with the
- * caller's own scheduling path. */
+ * spec.resourceClaims (DynamicResources), or a declared node feature (NodeDeclaredFeatures: a container
+ * restartPolicyRules action RestartAllContainers, or hostNetwork with hostUsers false).  The context is
+ * unaffected; such pods stay with the caller's own scheduling path. */
 int ksg_pod_compile(ksg_ctx *ctx, const char *pod_json, size_t len, int32_t *handle);
 int ksg_pod_release(ksg_ctx *ctx, int32_t handle);
 
@@ -186,6 +187,21 @@ int ksg_schedule_batch(ksg_ctx *ctx, const int32_t *handles, int32_t n, uint32_t
                        ksg_result *results);
 /* Cache.ForgetPod (cache.go:412) of an assumed pod -- unreserveAndForget (schedule_one.go:358) */
 int ksg_forget(ksg_ctx *ctx, int32_t handle);
+
+/* ---- OpportunisticBatching (framework/runtime/batch.go:31-242) ----------------------
+ * With featureGates.OpportunisticBatching on (the default) and a profile whose PodTopologySpread has no
+ * default constraints (disabled, or {"defaultingType": "List", "defaultConstraints": []}), pods get a
+ * SignPod signature (framework.go:884-924); a signed pod whose previous cycle in this context was a pod of
+ * the same signature that left a sorted node list less than 500 ms ago (maxBatchAge) is placed on that
+ * list's next node when the last chosen node rejects it and the hinted node passes every filter
+ * (GetNodeHint, evaluateNominatedNode: schedule_one.go:650-668,718-752) -- ksg_result.evaluated_nodes 1,
+ * feasible_nodes 1, no scores; else it runs the full cycle and stores its own list (StoreScheduleResults).
+ * Every pod of a ksg_schedule_one / ksg_schedule_batch call is one scheduling cycle (SchedulingCycle()),
+ * and the call reads the clock once: ksg_set_clock(ctx, now_ns) makes it now_ns (a caller's time.Now(),
+ * nanoseconds), 0 the wall clock (CLOCK_MONOTONIC).  A node-sharded context refuses such a profile at
+ * ksg_create.  ksg_debug_batching: pods placed by a hint so far, and the cycles counted. */
+int ksg_set_clock(ksg_ctx *ctx, int64_t now_ns);
+int ksg_debug_batching(const ksg_ctx *ctx, uint64_t *hinted, uint64_t *cycles);
 
 /* ---- plugin-granular entry points ---------------------------------------------------
  * The FilterPlugin contract of one plugin over every snapshot node: its PreFilter

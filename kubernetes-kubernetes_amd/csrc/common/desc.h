@@ -174,6 +174,9 @@ enum DescFlags : uint32_t {
   DF_RAW0 = 1u << 22,              // every node's raw TaintToleration and NodeAffinity scores are 0 (no intolerable
                                    // PreferNoSchedule taint exists, no preferred terms): k_sched_loop's helper forms
                                    // the chosen variant's maxima from the counts alone
+  DF_OB = 1u << 23,                // OpportunisticBatching: a signed pod (SignPod non-nil, framework.go:884-924) --
+                                   // k_ob_hint may place it on the stored heap's next node, k_ob_store keeps its
+                                   // cycle's sorted nodes for the next pod (framework/runtime/batch.go:65-229)
 };
 
 struct PodDesc {
@@ -237,7 +240,11 @@ struct PodDesc {
   int32_t agg_gwords;                  // words of the compact shared region (AggRef >= 0)
   int32_t agg_nlocal;                  // node-local histograms (AggRef < 0)
   int32_t agg_local_cons;              // bit c: DoNotSchedule constraint c counts on a node-local histogram
-  int32_t pad2;
+  // ---- OpportunisticBatching (DF_OB; zero otherwise, so programs of unsigned pods compare as before)
+  int32_t ob_hint;                     // 1: the previous cycle of this context was a pod of the same signature
+                                       // without a nominated node -- GetNodeHint may find the state usable
+  int64_t ob_cycle;                    // SchedulingQueue.SchedulingCycle() of this pod's cycle
+  int64_t ob_now;                      // time.Now() of this cycle, ns (maxBatchAge, batch.go:57,208)
 };
 
 // ---- DefaultPreemption: SelectVictimsOnNode per node, one thread each ----------
@@ -342,7 +349,8 @@ struct DevResult {
   uint64_t key;       // winning packed key (debug)
   uint32_t ipa_any;   // PodStats::ipa_any (PreFilter / PreScore Skip decisions taken on the device)
   uint32_t rot_next;  // DF_ROTDEV: nextStartNodeIndex after this pod
-  uint32_t pad[2];
+  uint32_t hinted;    // DF_OB: 1 when the pod took the OpportunisticBatching hint (no full evaluation)
+  uint32_t pad;
 };
 
 // Per-pod scratch (zeroed by the host before each batch).
@@ -367,7 +375,27 @@ struct PodStats {
                                       // (node-sharded: -2 on the ranks that do not hold it)
   int32_t keep[4];                    // node-sharded cut: this rank's kept nodes are the feasible ones in
                                       // [keep[0], keep[1]) or [keep[2], keep[3]) (k_sample_shard_b)
-  uint32_t pad[3];
+  uint32_t ob_done;                   // DF_OB: k_ob_hint placed the pod; the full-evaluation kernels return at once
+  uint32_t pad[2];
+};
+
+// OpportunisticBatching's state on the device (framework/runtime/batch.go:31-58): the sorted nodes a signed
+// pod's cycle left (sortedNodeScores after heap.Init and the winner's Pop: a Go container/heap of
+// (TotalScore, node) entries in heap order, ObEnt[len]), its creation time and the last cycle.  Written by
+// k_ob_store / k_ob_hint only; node indices are snapshot indices (the host remaps them when the node list is
+// rebuilt, -1: a node no longer in the snapshot).
+struct ObEnt {
+  int64_t total;
+  int32_t node;
+  int32_t pad;
+};
+struct ObState {
+  int64_t creation;    // batchState.creationTime (ns, the cycle's clock)
+  int64_t last_cycle;  // lastCycle.cycleCount of the last StoreScheduleResults
+  int32_t last_node;   // lastCycle.chosenNode (-1: none / gone)
+  int32_t len;         // sortedNodes.Len(); 0: stateEmpty (nil state, nil or empty list)
+  uint32_t check;      // k_ob_store: 1 + the first cycle whose heap pop disagreed with k_select's winner
+  uint32_t pad;
 };
 
 // Node mirror view passed to kernels by value.
@@ -427,6 +455,8 @@ struct BatchView {
   int64_t* out_scores;    // eval mode: [kNumPlugins][cap] normalised scores, unweighted
   int64_t* out_total;     // eval mode: [cap]
   unsigned long long* arena;  // PTS/IPA histograms (zero between pods)
+  ObState* ob;            // OpportunisticBatching state (DF_OB pods)
+  ObEnt* ob_heap;         // [cap] its sorted nodes (heap order)
 };
 
 // ---- node-sharded evaluation ----------------------------------------------------

@@ -213,6 +213,10 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
 // PodTopologySpread.Score for every feasible node (podtopologyspread/scoring.go:199-226): raw = round(
 // sum_c cnt_c * log(topoSize_c + 2) + (maxSkew_c - 1)), -1 for ignored nodes; min/max for NormalizeScore.
 __global__ __launch_bounds__(kBlock) void k_pts_score(MirrorView m, BatchView b, int pod, int blk0) {
+  {  // OpportunisticBatching: placed by k_ob_hint, no scores (kernels.hip ob_skip)
+    const PodDesc* pd = reinterpret_cast<const PodDesc*>(b.descs + b.desc_off[pod]);
+    if ((pd->flags & DF_OB) && b.stats[pod].ob_done) return;
+  }
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;

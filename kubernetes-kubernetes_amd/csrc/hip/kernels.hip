@@ -693,12 +693,20 @@ __device__ NodeEval eval_node_fast(const MirrorView& m, const PodFast& pf, const
   return eval_core_fast(m, nc, bal2(nc.rcpu, nc.acpu, nc.rmem, nc.amem), pf, base, d, i);
 }
 
+// OpportunisticBatching: a pod k_ob_hint placed on the stored heap's next node skips the full evaluation
+// (every launch of its per-pod path returns at once; k_select still clears its histograms)
+__device__ __forceinline__ bool ob_skip(const BatchView& b, int pod) {
+  const PodDesc* d = reinterpret_cast<const PodDesc*>(b.descs + b.desc_off[pod]);
+  return (d->flags & DF_OB) && b.stats[pod].ob_done;
+}
+
 // =====================================================================================================
 // k_filter_score
 // =====================================================================================================
 template <bool kLds>
 __global__ __launch_bounds__(kBlock) void k_filter_score(MirrorView m, BatchView b, int pod, int blk0) {
   __shared__ __align__(16) uint8_t s_blob[kLds ? kBlobLds : 16];
+  if (ob_skip(b, pod)) return;
   const uint8_t* base = b.descs + b.desc_off[pod];
   if constexpr (kLds) {
     stage_blob(base, reinterpret_cast<const PodDesc*>(base)->blob_bytes, s_blob);
@@ -930,6 +938,7 @@ __device__ bool select_block(const MirrorView& m, const BatchView& b, const PodD
     const uint32_t pos = g >= ps_before ? g - ps_before : g + F - ps_before;  // rank in evaluation order
     const int64_t total = node_total(b, d, ns, cap, i, eval);
     if (eval) b.out_total[i] = total;
+    if (d.flags & DF_OB) b.ob_heap[pos] = ObEnt{total, i, 0};  // the NodePluginScores list, feasible order
     key = pack_best(total, pos);
   }
   // the PTS/IPA histograms of this pod are dead now: zero them for the next pod on the stream
@@ -974,6 +983,8 @@ __device__ __forceinline__ bool commit_result(const MirrorView& m, const BatchVi
   r.key = best;
   r.status = F > 0 ? (int32_t)C_OK : (int32_t)C_UNSCHED;
   r.ipa_any = ipa_any >= 0 ? (uint32_t)ipa_any : ps->ipa_any;
+  r.hinted = 0;
+  r.pad = 0;
   if (d.flags & DF_ROTDEV) {  // k_sample_find's rotation bookkeeping
     r.evaluated = (int32_t)ps->processed;
     r.rot_next = ps->rot_out;
@@ -1040,6 +1051,10 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((d.flags & DF_OB) && ps->ob_done) {  // placed by k_ob_hint: only the histograms to clear
+    for (int w = blockIdx.x * kBlock + threadIdx.x; w < d.arena_words; w += nblocks * kBlock) b.arena[w] = 0ull;
+    return;
+  }
 
   // ---- global feasible count F, this block's exclusive prefix, and P(s) = feasible nodes
   // before the rotation start (nextStartNodeIndex, schedule_one.go:808) -- one strided pass
@@ -1097,6 +1112,113 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
   if (threadIdx.x == 0) commit_result(m, b, base, d, ps, pod, F, node, best);
 }
 
+// ---- OpportunisticBatching (framework/runtime/batch.go:65-229, schedule_one.go:586-611,650-668) ----------------
+// Go's container/heap down() over the stored NodePluginScores, nodeScoreHeap.Less = TotalScore > (Randomizer 0)
+__device__ __forceinline__ void ob_down(ObEnt* h, int i, int n) {
+  while (true) {
+    const int j1 = 2 * i + 1;
+    if (j1 >= n) break;
+    int j = j1;
+    if (j1 + 1 < n && h[j1 + 1].total > h[j1].total) j = j1 + 1;
+    if (!(h[j].total > h[i].total)) break;
+    const ObEnt t = h[i];
+    h[i] = h[j];
+    h[j] = t;
+    i = j;
+  }
+}
+
+constexpr int64_t kObMaxAgeNs = 500LL * 1000 * 1000;  // maxBatchAge (batch.go:57)
+
+// k_ob_hint (one thread, after PreFilter and the pod's histograms): GetNodeHint (batch.go:65-95) --
+// batchStateCompatible (:167-226: the host checked the signature, the cycle sequence and the nominated
+// node; here the stored state, its age and whether the last chosen node now rejects the pod), the Pop --
+// then evaluateNominatedNode with the hint (schedule_one.go:718-752): the hinted node's filters alone.
+// Feasible: the pod is placed there (schedulePod's one-feasible-node path, :586-598) and
+// StoreScheduleResults(hinted == chosen) keeps the rest of the heap (:110-118).
+__global__ void k_ob_hint(MirrorView m, BatchView b, int pod) {
+  if (threadIdx.x != 0) return;
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  if (!(d.flags & DF_OB) || (d.flags & DF_PREFILTER_REJECT) || !d.ob_hint) return;
+  ObState& st = *b.ob;
+  if (st.len <= 0 || st.last_cycle != d.ob_cycle - 1 || d.ob_now > st.creation + kObMaxAgeNs || st.last_node < 0) return;
+  int64_t rt = 0;
+  const ArenaTopo at{ps, b.arena};
+  if (run_filters(m, load_core(m, st.last_node), base, d, st.last_node, &rt, at, 0) == 0) return;  // not full
+  ObEnt* h = b.ob_heap;
+  const int n = st.len - 1;  // heap.Pop: swap(0, n), down(0, n), take the last
+  const ObEnt top = h[0];
+  h[0] = h[n];
+  h[n] = top;
+  ob_down(h, 0, n);
+  st.len = n;
+  const int hint = top.node;
+  if (hint < 0 || hint >= m.n) return;  // no longer in the snapshot: an error, then the full pass
+  if (run_filters(m, load_core(m, hint), base, d, hint, &rt, at, 0) != 0) return;  // the full pass decides
+  if (d.flags & DF_ROTDEV) {  // the hint path leaves nextStartNodeIndex alone
+    ps->rot_out = d.prev_pod < 0 ? ps->rot_in : b.stats[d.prev_pod].rot_out;
+    ps->processed = 1;
+  }
+  commit_result(m, b, base, d, ps, pod, 1u, hint, 0ull);
+  b.results[pod].hinted = 1u;
+  b.results[pod].evaluated = 1;  // EvaluatedNodes = 1 + diagnosis.NodeToStatus.Len() (no failure)
+  ps->ob_done = 1u;
+  st.last_cycle = d.ob_cycle;
+  st.last_node = hint;
+}
+
+// k_ob_store (one workgroup, after k_select): StoreScheduleResults (batch.go:98-158) for a signed pod whose
+// full evaluation placed it.  One feasible node: the state is dropped (nil list).  Otherwise the feasible
+// list's (TotalScore, node) entries k_select wrote in feasible order become newSortedNodeScores' heap
+// (heap.Init, one level at a time: a level's subtrees are disjoint and every deeper level is done first,
+// which is the order Init's sequential loop visits them in) and the winner is popped.
+__global__ __launch_bounds__(1024) void k_ob_store(BatchView b, int pod) {
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(b.descs + b.desc_off[pod]);
+  PodStats* ps = b.stats + pod;
+  if (!(d.flags & DF_OB) || ps->ob_done) return;
+  const DevResult r = b.results[pod];
+  if (r.status != (int32_t)C_OK || r.node < 0) return;  // FitError / Error: nothing stored (schedulePod returns first)
+  ObState& st = *b.ob;
+  const int n = (int)ps->feasible;
+  ObEnt* h = b.ob_heap;
+  if (n >= 2) {
+    const int last = n / 2 - 1;
+    const int top_level = 31 - __clz(last + 1);
+    for (int L = top_level; L >= 0; --L) {
+      const int lo = (1 << L) - 1, hi = min((1 << (L + 1)) - 2, last);
+      for (int i = lo + (int)threadIdx.x; i <= hi; i += (int)blockDim.x) ob_down(h, i, n);
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x != 0) return;
+  if (n >= 2) {
+    const ObEnt top = h[0];
+    h[0] = h[n - 1];
+    h[n - 1] = top;
+    ob_down(h, 0, n - 1);
+    if (top.node != r.node && st.check == 0) st.check = (uint32_t)(1 + d.ob_cycle);  // never: k_select's pre-order rule
+  }
+  st.len = n >= 2 ? n - 1 : 0;
+  st.creation = d.ob_now;
+  st.last_cycle = d.ob_cycle;
+  st.last_node = r.node;
+}
+
+// the host's remap after the snapshot's node list was rebuilt: old snapshot index -> new (-1: gone)
+__global__ __launch_bounds__(kBlock) void k_ob_remap(ObState* st, ObEnt* h, const int32_t* map, int nold) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < st->len) {
+    const int o = h[i].node;
+    h[i].node = (o >= 0 && o < nold) ? map[o] : -1;
+  }
+  if (i == 0) {
+    const int o = st->last_node;
+    st->last_node = (o >= 0 && o < nold) ? map[o] : -1;
+  }
+}
+
 // ---- percentageOfNodesToScore: the cut feasible list (schedule_one.go:778-884) ---------------------
 // findNodesThatPassFilters checks nodes[(nextStartNodeIndex + i) % numAll] in order and stops at
 // the (K+1)-th feasible node, K = numFeasibleNodesToFind (schedule_one.go:809-824, sequential
@@ -1111,6 +1233,7 @@ __device__ __forceinline__ bool in_cyclic(int i, int lo, int hi) {  // lo != hi
 // k_sample_find (1 block): this pod's rotation start from the device-resident nextStartNodeIndex,
 // the (K+1)-th feasible node of the rotated order, processedNodes and the next rotation.
 __global__ __launch_bounds__(kBlock) void k_sample_find(MirrorView m, BatchView b, int pod, int nblocks) {
+  if (ob_skip(b, pod)) return;  // k_ob_hint kept nextStartNodeIndex (rot_out)
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
@@ -1175,6 +1298,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_find(MirrorView m, BatchView 
 // nodes are k_sample_shard_b's intervals; the statuses of unprocessed nodes are cleared by
 // k_select_shard once exchange A has carried the cut's end node to every rank.
 __global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView b, int pod, int blk0, int shard) {
+  if (ob_skip(b, pod)) return;
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
@@ -4079,6 +4203,19 @@ hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipSt
     hipLaunchKernelGGL(k_select<false>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, nb);
   return hipGetLastError();
 }
+hipError_t launch_ob_hint(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_ob_hint, dim3(1), dim3(64), 0, s, m, b, pod);
+  return hipGetLastError();
+}
+hipError_t launch_ob_store(const BatchView& b, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_ob_store, dim3(1), dim3(1024), 0, s, b, pod);
+  return hipGetLastError();
+}
+hipError_t launch_ob_remap(ObState* st, ObEnt* h, const int32_t* map, int nold, int maxlen, hipStream_t s) {
+  hipLaunchKernelGGL(k_ob_remap, dim3((maxlen + kBlock - 1) / kBlock > 0 ? (maxlen + kBlock - 1) / kBlock : 1),
+                     dim3(kBlock), 0, s, st, h, map, nold);
+  return hipGetLastError();
+}
 // ---- incremental mirror ingestion (Cache.UpdateNode, cache.go UpdateNode + UpdateSnapshot's
 // generation diff): one thread per updated node writes its static columns in place.
 __global__ __launch_bounds__(kBlock) void k_node_update(MirrorView m, const NodeUpdate* u, const uint32_t* ids,
@@ -4304,7 +4441,9 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_agg_loop<true, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<false, true, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<false, true, false, 1>),
-                      reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr)};
+                      reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr),
+                      reinterpret_cast<const void*>(&k_ob_hint),            reinterpret_cast<const void*>(&k_ob_store),
+                      reinterpret_cast<const void*>(&k_ob_remap)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);
     if (e != hipSuccess) return e;

@@ -78,6 +78,12 @@ ksg_ctx* ksg_create(const char* config_json, size_t len) {
       return nullptr;
     }
     if (cfg.sharded()) {  // node-sharded: join the exchange group (collective across the ranks)
+      if (ctx->engine->ob_acting()) {  // before the collective: every rank has the same profile, so all fail here
+        g_create_error = "OpportunisticBatching acts in this profile (PodTopologySpread without default constraints) "
+                         "and the node-sharded scheduler does not run it: set featureGates.OpportunisticBatching false";
+        delete ctx;
+        return nullptr;
+      }
       std::string err;
       ctx->engine->comm = make_comm(cfg, ctx->cluster->own_queue, &err);
       if (!ctx->engine->comm) {
@@ -215,6 +221,11 @@ int ksg_pod_compile(ksg_ctx* ctx, const char* pod_json, size_t len, int32_t* han
     if (!decode_pod(pod_json, len, &p, &ctx->err)) return KSG_EINVAL;
     if (!p.unsupported.empty()) {  // declined, not mis-evaluated: the caller schedules it on the CPU path
       ctx->err = "pod " + p.ns + "/" + p.name + ": " + p.unsupported;
+      return KSG_ENOTSUP;
+    }
+    if (p.needs_features) {  // NodeDeclaredFeatures' PreFilter would not Skip (nodedeclaredfeatures.go:86-104)
+      ctx->err = "pod " + p.ns + "/" + p.name + ": needs a declared node feature (NodeDeclaredFeatures), which runs "
+                 "outside the device path";
       return KSG_ENOTSUP;
     }
     // the pod's pod-table entry (labels, affinity terms) compiled once, as NewPodInfo does at enqueue
@@ -380,6 +391,19 @@ int ksg_debug_relayouts(const ksg_ctx* ctx, uint64_t* full, uint64_t* gather) {
   if (!ctx || !full || !gather) return KSG_EINVAL;
   *full = ctx->cluster->relayouts_full;
   *gather = ctx->cluster->relayouts_gather;
+  return KSG_OK;
+}
+
+int ksg_set_clock(ksg_ctx* ctx, int64_t now_ns) {
+  if (!ctx) return KSG_EINVAL;
+  ctx->engine->ob_clock_ = now_ns;
+  return KSG_OK;
+}
+
+int ksg_debug_batching(const ksg_ctx* ctx, uint64_t* hinted, uint64_t* cycles) {
+  if (!ctx || !hinted || !cycles) return KSG_EINVAL;
+  *hinted = ctx->engine->ob_hinted_;
+  *cycles = (uint64_t)ctx->engine->ob_cycle_;
   return KSG_OK;
 }
 

@@ -49,6 +49,9 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
                            hipEvent_t t1);
 hipError_t warm_kernels();
 hipError_t warm_aggregate();
+hipError_t launch_ob_hint(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_ob_store(const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_ob_remap(ObState* st, ObEnt* h, const int32_t* map, int nold, int maxlen, hipStream_t s);
 hipError_t loop_occupancy(int (&occ)[4]);
 
 #define HIPCHK(x)                                               \
@@ -369,6 +372,10 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   const PodResources res = calc_resources(p);
   const PodResources fit = p.has_status_res ? calc_fit_request(p) : res;
   out->res = res;
+  if (mode == CYCLE && ob_acting()) {  // SignPod: the pod takes part in OpportunisticBatching
+    out->sig = sign(p, fit);
+    if (out->sig >= 0) D.flags |= DF_OB;
+  }
   out->port_ids = own;
   D.req_cpu = fit.cpu;
   D.req_mem = fit.mem;
@@ -989,13 +996,127 @@ static bool calc_scalar_free(const PodSpec& p) {  // decided once per pod at dec
 bool Engine::rotdev() const {
   bool any_score = false;
   for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) any_score |= c->cfg.enabled[q];
-  return c->cfg.pct != 100 || !any_score;
+  // (OpportunisticBatching: a hinted pod leaves nextStartNodeIndex alone, which only the device knows)
+  return c->cfg.pct != 100 || !any_score || ob_acting();
+}
+
+// ---- OpportunisticBatching (framework/runtime/batch.go:31-242) --------------------------
+// Signatures exist only when PodTopologySpread refuses none on profile grounds: disabled, or List
+// defaulting without default constraints (podtopologyspread/plugin.go:92-102); every in-tree plugin of
+// the profile implements SignPlugin and there are no extenders (framework.go:832-876).
+bool Engine::ob_acting() const {
+  const Config& k = c->cfg;
+  return k.ob_gate && (!k.enabled[P_PTS] || (!k.pts_system_defaulted && k.pts_defaults.empty()));
+}
+
+// frameworkImpl.SignPod (framework.go:884-924): the fragments of the profile's plugins keyed by signer
+// name, nil (-1) when a plugin refuses; equal texts <=> equal json.Marshal bytes.  Interned per context.
+int32_t Engine::sign(const PodSpec& p, const PodResources& fit) {
+  const Config& k = c->cfg;
+  const PodSpec::Sign& f = p.sign;
+  std::string o = "sched=" + f.sched;
+  if (k.enabled[P_FIT] || k.enabled[P_BAL]) {  // Fit / BalancedAllocation: computePodResourceRequest
+    o += "|res=" + std::to_string(fit.cpu) + "," + std::to_string(fit.mem) + "," + std::to_string(fit.eph) + ",0";
+    if (fit.scalar.empty()) {
+      o += ",null";
+    } else {
+      std::vector<std::pair<std::string, int64_t>> sc(fit.scalar.begin(), fit.scalar.end());
+      std::sort(sc.begin(), sc.end());
+      o += ",{";
+      for (auto& x : sc) o += x.first + "=" + std::to_string(x.second) + ";";
+      o += "}";
+    }
+  }
+  if (k.enabled[P_TAINT] || k.enabled[P_UNSCHED]) o += "|tol=" + f.tols;
+  if (k.enabled[P_IPA]) {  // interpodaffinity/plugin.go:62-78
+    if (p.has_pod_affinity || p.has_pod_anti) return -1;
+    if (!k.ignore_pref_existing) o += "|lbl=" + f.labels;
+  }
+  if (k.enabled[P_PORTS]) o += "|ports=" + f.ports;
+  if (k.enabled[P_PTS] && (!p.spreads.empty() || k.pts_system_defaulted || !k.pts_defaults.empty())) return -1;
+  if (k.enabled[P_NA]) o += "|na=" + f.na + "|nsel=" + f.nsel;
+  if (k.enabled[P_NODENAME]) o += "|nn=" + p.node_name;
+  if (k.enabled[P_IMG]) o += "|img=" + f.images;
+  o += "|vol=" + f.vols;  // the four volume plugins
+  if (f.claims) return -1;  // DynamicResources
+  o += "|feat=";            // NodeDeclaredFeatures: nothing required (else the pod is refused at compile)
+  auto it = ob_sigs_.find(o);
+  if (it != ob_sigs_.end()) return it->second;
+  const int32_t id = (int32_t)ob_sigs_.size();
+  ob_sigs_.emplace(std::move(o), id);
+  return id;
+}
+
+int64_t Engine::ob_now() const {
+  if (ob_clock_) return ob_clock_;
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One scheduling cycle of this context (every pod of a call, in queue order): its SchedulingCycle count, its
+// clock and whether GetNodeHint may find the state usable -- the previous cycle was a pod of the same
+// signature without a nominated node (batch.go:183-200); the device checks the rest (k_ob_hint).
+int Engine::ob_sequence(CompiledPod& cp, const PodSpec& p, int64_t now) {
+  const int64_t cycle = ++ob_cycle_;
+  if (cp.blob.size() < sizeof(PodDesc) || cp.error) {
+    ob_prev_sig_ = -1;
+    return KSG_OK;
+  }
+  PodDesc& D = *reinterpret_cast<PodDesc*>(cp.blob.data());
+  if (D.flags & DF_OB) {
+    D.ob_cycle = cycle;
+    D.ob_now = now;
+    D.ob_hint = (ob_prev_sig_ == cp.sig && p.nominated_node.empty()) ? 1 : 0;
+  }
+  ob_prev_sig_ = (D.flags & DF_OB) ? cp.sig : -1;
+  return KSG_OK;
+}
+
+void Engine::ob_invalidate() {
+  ob_prev_sig_ = -1;
+  if (d_ob.p) (void)hipMemsetAsync(d_ob.p, 0, sizeof(ObState), c->stream);  // len 0: stateEmpty
+}
+
+// The device state exists (zeroed once), its heap holds cap entries, and its node indices follow the
+// snapshot's node list: after UpdateSnapshot rebuilt the list (cache.go:273-283) every stored index is mapped
+// to the node's new one (-1: removed -- GetNodeInPlacement fails for it and the full pass runs).
+int Engine::ob_sync(hipStream_t s) {
+  int rc_ob_ = KSG_OK;
+  const size_t cap = (size_t)std::max(c->view.cap, 1);
+  if (!d_ob.p) {
+    if ((rc_ob_ = ensure(d_ob, sizeof(ObState)))) return rc_ob_;
+    HIPCHK(hipMemsetAsync(d_ob.p, 0, sizeof(ObState), s));
+  }
+  if (d_ob_heap.bytes < cap * sizeof(ObEnt)) {  // grown: keep the stored heap
+    DevBuf old = d_ob_heap;
+    d_ob_heap = DevBuf{};
+    if ((rc_ob_ = ensure(d_ob_heap, cap * sizeof(ObEnt)))) return rc_ob_;
+    if (old.p) {
+      HIPCHK(hipMemcpyAsync(d_ob_heap.p, old.p, old.bytes, hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+      (void)hipFree(old.p);
+    }
+  }
+  const std::vector<std::string>& order = c->order();
+  if (ob_list_gen_ != c->list_gen || ob_order_.size() != order.size()) {
+    if (!ob_order_.empty()) {
+      std::vector<int32_t> map(ob_order_.size());
+      for (size_t i = 0; i < ob_order_.size(); ++i) map[i] = c->index_of(ob_order_[i]);
+      if ((rc_ob_ = ensure(d_ob_map, map.size() * 4))) return rc_ob_;
+      HIPCHK(hipMemcpyAsync(d_ob_map.p, map.data(), map.size() * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(launch_ob_remap((ObState*)d_ob.p, (ObEnt*)d_ob_heap.p, (const int32_t*)d_ob_map.p, (int)map.size(),
+                             (int)map.size(), s));
+      HIPCHK(hipStreamSynchronize(s));  // the host map buffer goes out of scope
+    }
+    ob_order_ = order;
+    ob_list_gen_ = c->list_gen;
+  }
+  return KSG_OK;
 }
 
 bool Engine::loop_ok(const CompiledPod& p) const {
   if (p.error) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
-  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE)) return false;
+  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_OB)) return false;
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
   // percentageOfNodesToScore / no-score profiles: the loop cuts the list and carries nextStartNodeIndex
   // itself (k_sched_loop), unsharded, over the whole snapshot (no PreFilterResult)
@@ -1007,7 +1128,7 @@ bool Engine::loop_ok(const CompiledPod& p) const {
 bool Engine::agg_loop_ok(const CompiledPod& p) const {
   if (p.error || !p.agg_ok || p.blob.size() > (size_t)kAggBlobLds) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
-  if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET))
+  if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET | DF_OB))
     return false;
   // the fold plan holds <= 8 items per kind of the next pod's constraints / terms plus one per own
   // term of the pod just placed (kFoldMax = 80 in k_agg_loop)
@@ -1093,7 +1214,8 @@ Engine::~Engine() {
   }
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill, &d_relay,
-                    &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf, &d_vsc})
+                    &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf, &d_vsc,
+                    &d_ob, &d_ob_heap, &d_ob_map})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
   if (ev0) (void)hipEventDestroy(ev0);
@@ -1176,6 +1298,8 @@ BatchView Engine::bview(int pods) {
   b.out_scores = (int64_t*)d_out.p;
   b.out_total = (int64_t*)d_total.p;
   b.arena = (unsigned long long*)d_arena.p;
+  b.ob = (ObState*)d_ob.p;
+  b.ob_heap = (ObEnt*)d_ob_heap.p;
   return b;
 }
 
@@ -1453,6 +1577,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const auto Tv0 = clk::now();
   std::vector<CompiledPod> cp(n);
   int compiled = 0;
+  // OpportunisticBatching: every pod of the call is one scheduling cycle; the call reads the clock once
+  const bool ob_on = ob_acting();
+  const int64_t ob_clock = ob_on ? ob_now() : 0;
+  const int64_t ob_cycle0 = ob_cycle_;
+  const int32_t ob_prev0 = ob_prev_sig_;
   // compile pods [compiled, b) against the cache (PreFilter / PreScore on the host)
   std::vector<int64_t> ns_before((size_t)n, 0);  // Scheduler.nextStartNodeIndex before each pod's compile
   auto compile_upto = [&](int b) -> int {
@@ -1463,6 +1592,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       next_slot_ = -1;
       if (rc) return rc;
       if (cp[i].prefilter_error) cp[i].error = true;  // PreFilter Error: status Error, no launch
+      if (ob_on) ob_sequence(cp[i], *pods[i], ob_clock);
       if (!cp[i].prefilter_reject && !cp[i].prefilter_error && !rotdev()) {
         // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
         const int64_t N = (int64_t)c->order().size();
@@ -1478,6 +1608,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     const int64_t start = c->next_start;
     if ((rc = compile_upto(pipe ? bnd[0] : n))) {  // nothing launched: the batch fails as a whole
       c->next_start = start;
+      ob_cycle_ = ob_cycle0;
+      ob_prev_sig_ = ob_prev0;
       if (!pre_slot.empty())
         for (int32_t sl : pre_slot) c->pod_table_drop(sl);
       else
@@ -1518,6 +1650,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   const auto Tm = clk::now();
   if ((rc = c->ensure_mirror(pods_needed))) return rc;
+  if (ob_acting() && (rc = ob_sync(c->stream))) return rc;
   mirror_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tm).count();
   // ---- staging: [offsets n | program sizes n | PodStats n | DevResult n | give-up flags n | programs]
   // in pinned memory; each chunk's programs, offsets and stats go up in their own H2D copies
@@ -1775,6 +1908,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         if (!cp[i].error) c->next_start = d.rot_next;  // the last launched pod's wins
       }
       r.total_score = d.feasible > 1 ? d.total : 0;
+      if (d.hinted) {  // OpportunisticBatching: the hinted node alone was evaluated (k_ob_hint)
+        r.evaluated_nodes = 1;
+        ++ob_hinted_;
+      }
       if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
       if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
         static uint64_t seq = 0;
@@ -1807,6 +1944,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     c->layout_dirty = true;
     c->mirror_suspect = true;  // not a gather re-layout: unchanged nodes' device columns are suspect too
     c->pods_dirty = true;
+    ob_invalidate();
     c->err = why + ": pods " + std::to_string(first) + ".." + std::to_string(n - 1) +
              " of the batch were not scheduled (status Error); the device mirror is rebuilt from the cache";
     fault_first_ = first;
@@ -2016,6 +2154,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
     const bool lds = cp[i].blob.size() <= (size_t)kBlobLds;
     if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));
+    if (hd.flags & DF_OB) HIPCHK(launch_ob_hint(m, bv, i, s));  // GetNodeHint (its counts are ready)
     const bool t = stride > 0 && i % stride == 0;
     if (t) {
       HIPCHK(launch_filter_score(m, bv, i, s, tev[2 * (size_t)timed], tev[2 * (size_t)timed + 1], 0, -1, lds));
@@ -2026,6 +2165,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (hd.flags & DF_ROTDEV) HIPCHK(launch_sample(m, bv, i, (hd.flags & DF_SAMPLE) != 0, s));
     if (hd.score_mask & (1u << P_PTS)) HIPCHK(launch_pts_score(m, bv, i, s));
     HIPCHK(launch_select(m, bv, i, s, lds));
+    if (hd.flags & DF_OB) HIPCHK(launch_ob_store(bv, i, s));  // StoreScheduleResults
     bytes += algo_bytes(hd);
     launches++;
     ++i;
@@ -2383,13 +2523,18 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       tot[i] = (int64_t)gath[(1 + kNumPlugins) * n + i];
     }
   }
+  if (eval && hr[0].hinted) {  // placed by the OpportunisticBatching hint: no status, no score (k_ob_hint)
+    std::fill(st.begin(), st.end(), 0u);
+    std::fill(outs.begin(), outs.end(), 0);
+    std::fill(tot.begin(), tot.end(), 0);
+  }
   if (eval) {
     const int32_t N = m.n;
     eval->prefilter_code = cp[0].prefilter_reject ? cp[0].prefilter_code : 0;
     eval->prefilter_plugin = cp[0].prefilter_reject ? cp[0].prefilter_plugin : 255;
     uint32_t smask = cp[0].score_mask;
     if (!(hr[0].ipa_any & 8u)) smask &= ~(1u << P_IPA);  // InterPodAffinity PreScore Skip (scoring.go:207-209)
-    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject) ? smask : 0;
+    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject && !hr[0].hinted) ? smask : 0;
     for (int32_t i = 0; i < N; ++i) {
       const uint32_t w = st[i];
       if (eval->node_code) eval->node_code[i] = (uint8_t)status_code(w);
@@ -2697,6 +2842,10 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     return KSG_OK;
   }
   *handled = true;
+  if (ob_acting()) {  // a scheduling cycle of an unsigned pod (signed ones take run_batch's path)
+    ++ob_cycle_;
+    ob_prev_sig_ = -1;
+  }
   if (cp.error || cp.prefilter_reject) {  // decided on the host (run_batch's settle gives the same)
     c->pod_table_drop(cp.slot);
     *res = ksg_result{};

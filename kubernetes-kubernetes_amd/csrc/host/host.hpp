@@ -144,6 +144,16 @@ struct PodSpec {
   // every request / overhead names cpu, memory or ephemeral-storage only (1), or not (0); -1: not yet
   // known.  Set by decode_pod, so a batch's pipeline check does not re-compare resource names.
   int8_t scalar_free = -1;
+  // OpportunisticBatching: the pod's SignPod fragments (staging/src/k8s.io/kube-scheduler/framework/signers.go
+  // and the plugins' SignPod), each a canonical text that is equal for two pods iff json.Marshal of the
+  // reference's value is; Engine::sign combines them with the profile (framework.go:884-924)
+  struct Sign {
+    std::string sched, tols, labels, ports, na, nsel, images, vols;
+    bool claims = false;
+  } sign;
+  // NodeDeclaredFeatures' PreFilter would not Skip: the pod needs a declared node feature
+  // (component-helpers/nodedeclaredfeatures: RestartAllContainers rules, hostNetwork with hostUsers false)
+  bool needs_features = false;
 };
 bool pod_scalar_free(const PodSpec& p);  // the check behind PodSpec::scalar_free
 struct NodeImage { std::vector<std::string> names; int64_t size; };
@@ -205,6 +215,7 @@ struct Config {
   int32_t hard_weight = 1;
   bool ignore_pref_existing = false;
   bool taint_cmp_ops = false;
+  bool ob_gate = true;  // featureGates.OpportunisticBatching (framework/runtime/batch.go)
   bool has_added_required = false;
   std::vector<NSTerm> added_required;
   bool has_added_pref = false;
@@ -519,6 +530,7 @@ struct CompiledPod {
   int32_t arena_words = 0;
   bool agg_ok = false;        // fits k_agg_loop's histogram placement
   int32_t own_terms = 0;      // the pod's own affinity terms (k_agg_loop's term-list bound)
+  int32_t sig = -1;           // OpportunisticBatching: the interned SignPod signature (-1: nil)
 };
 struct Blob;
 class Comm;
@@ -587,12 +599,28 @@ class Engine {
   // nextStartNodeIndex advances by a data-dependent count (percentageOfNodesToScore < 100, or
   // numNodesToFind = 1 without score plugins): it is kept on the device across a batch
   bool rotdev() const;
+  // OpportunisticBatching (framework/runtime/batch.go:31-242): the profile signs pods
+  // (the gate is on and PodTopologySpread has no default constraints, plugin.go:92-102)
+  bool ob_acting() const;
+  int32_t sign(const PodSpec& p, const PodResources& fit);  // SignPod, interned; -1: nil
+  int ob_sequence(CompiledPod& cp, const PodSpec& p, int64_t now);  // the cycle's count, clock, hint permission
+  int ob_sync(hipStream_t s);      // device state allocated; node indices remapped after a list rebuild
+  void ob_invalidate();            // after a device fault: no hint from a state the fault may have torn
+  int64_t ob_now() const;          // time.Now() for a scheduling call (ksg_set_clock, else the wall clock)
+  int64_t ob_clock_ = 0;
+  int64_t ob_cycle_ = 0;           // SchedulingCycle(): one per scheduling cycle of this context
+  int32_t ob_prev_sig_ = -1;       // the previous cycle's signature (-1: nil, or no previous cycle)
+  uint64_t ob_list_gen_ = 0;       // the node-list generation the device state's indices refer to
+  std::vector<std::string> ob_order_;  // the snapshot order of that generation (for the remap)
+  std::unordered_map<std::string, int32_t> ob_sigs_;
+  uint64_t ob_hinted_ = 0;         // pods placed by a hint (diagnostic)
   int32_t shard_blk0 = 0, shard_nblk = -1;
   void shard_range(int32_t n, int32_t* blk0, int32_t* nblk) const;
 
  private:
   // per-batch device scratch
   DevBuf d_descs, d_status, d_fmask, d_blk, d_fixed, d_raw, d_out, d_total;
+  DevBuf d_ob, d_ob_heap, d_ob_map;      // OpportunisticBatching: ObState, ObEnt[cap], the remap
   DevBuf d_meta;                         // owns the three views below (ensure_scratch)
   DevBuf d_off, d_stats, d_results;      // views: program offsets + sizes, PodStats, DevResult
   DevBuf d_arena;  // PTS/IPA histograms; kept all-zero between pods (k_select re-zeroes what it used)

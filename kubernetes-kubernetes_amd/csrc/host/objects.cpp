@@ -246,6 +246,8 @@ bool parse_rfc3339(const std::string& s, int64_t* unix_ns) {
   return true;
 }
 
+static void pod_sign_fragments(const JDoc& d, const JVal& root, PodSpec* out);  // below
+
 bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
   try {
     JDoc d(p, n);
@@ -418,11 +420,172 @@ bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {
     if (claims && out->unsupported.empty())
       out->unsupported = "spec.resourceClaims needs DynamicResources, which runs outside the device path";
     out->scalar_free = pod_scalar_free(*out) ? 1 : 0;
+    pod_sign_fragments(d, r, out);
     return true;
   } catch (std::exception& e) {
     *err = e.what();
     return false;
   }
+}
+
+// ---- SignPod fragments (kube-scheduler/framework/signers.go; the plugins' SignPod methods) ------------------
+// canonical text of a JSON value: object members sorted by name, members that json.Marshal's omitempty would
+// leave out of the typed object (null, "", false, empty list / object) dropped
+static void canon_json(const JDoc& d, const JVal& v, std::string& o) {
+  switch (v.type) {
+    case JVal::NUL: o += "null"; return;
+    case JVal::BOOL: o += v.b ? "true" : "false"; return;
+    case JVal::NUM: o += v.s; return;
+    case JVal::STR: o += '"'; o += v.s; o += '"'; return;
+    case JVal::ARR: {
+      o += '[';
+      bool first = true;
+      d.each(&v, [&](const JVal& x) {
+        if (!first) o += ',';
+        first = false;
+        canon_json(d, x, o);
+      });
+      o += ']';
+      return;
+    }
+    case JVal::OBJ: {
+      std::vector<const JVal*> kv;
+      d.each(&v, [&](const JVal& x) {
+        if (x.type == JVal::NUL || (x.type == JVal::STR && x.s.empty()) || (x.type == JVal::BOOL && !x.b) ||
+            ((x.type == JVal::ARR || x.type == JVal::OBJ) && x.count == 0))
+          return;
+        kv.push_back(&x);
+      });
+      std::sort(kv.begin(), kv.end(), [](const JVal* a, const JVal* b) { return a->key < b->key; });
+      o += '{';
+      for (size_t i = 0; i < kv.size(); ++i) {
+        if (i) o += ',';
+        o += '"';
+        o += kv[i]->key;
+        o += "\":";
+        canon_json(d, *kv[i], o);
+      }
+      o += '}';
+      return;
+    }
+  }
+}
+static std::string sorted_list(std::vector<std::string> v) {
+  std::sort(v.begin(), v.end());
+  std::string o = "[";
+  for (auto& x : v) o += x + ",";
+  return o + "]";
+}
+static std::string map_text(const JDoc& d, const JVal* m) {  // map[string]string: null when nil
+  if (!m) return "null";
+  std::vector<std::string> kv;
+  d.each(m, [&](const JVal& x) { kv.push_back(x.key + "=" + (x.type == JVal::STR ? x.s : std::string())); });
+  std::sort(kv.begin(), kv.end());
+  std::string o = "{";
+  for (auto& x : kv) o += x + ";";
+  return o + "}";
+}
+// NodeSelectorTermSigner over NodeSelectorRequirementsSigner (signers.go:67-101)
+static std::string ns_term_text(const JDoc& d, const JVal* t) {
+  auto reqs = [&](const JVal* a) {
+    std::vector<std::string> out;
+    d.each(a, [&](const JVal& r) {
+      std::vector<std::string> vals;
+      d.each(d.get(r, "values"), [&](const JVal& x) { vals.push_back(x.s); });
+      std::sort(vals.begin(), vals.end());
+      std::string t2 = "{key=" + d.str(r, "key") + ";op=" + d.str(r, "operator") + ";values=[";
+      for (auto& x : vals) t2 += x + ",";
+      out.push_back(t2 + "]}");
+    });
+    return sorted_list(out);
+  };
+  return "{exp=" + reqs(t ? d.get(*t, "matchExpressions") : nullptr) + ";fld=" +
+         reqs(t ? d.get(*t, "matchFields") : nullptr) + "}";
+}
+static std::string image_norm(const std::string& n) {  // normalizedImageName (image_locality.go:154-159)
+  const size_t c = n.rfind(':'), s = n.rfind('/');
+  const long lc = c == std::string::npos ? -1 : (long)c, ls = s == std::string::npos ? -1 : (long)s;
+  return lc <= ls ? n + ":latest" : n;
+}
+static void pod_sign_fragments(const JDoc& d, const JVal& root, PodSpec* out) {
+  PodSpec::Sign& f = out->sign;
+  const JVal* md = d.get(root, "metadata");
+  const JVal* sp = d.get(root, "spec");
+  f.labels = map_text(d, md ? d.get(*md, "labels") : nullptr);
+  f.sched = sp ? d.str(*sp, "schedulerName") : "";
+  f.nsel = map_text(d, sp ? d.get(*sp, "nodeSelector") : nullptr);
+  f.na = "null";
+  f.tols = f.ports = f.images = f.vols = "[]";
+  if (!sp) return;
+  {  // TolerationsSigner (:180-189): by (key, value), stable for equal keys
+    std::vector<std::pair<std::pair<std::string, std::string>, std::string>> ts;
+    d.each(d.get(*sp, "tolerations"), [&](const JVal& t) {
+      std::string c;
+      canon_json(d, t, c);
+      ts.push_back({{d.str(t, "key"), d.str(t, "value")}, c});
+    });
+    std::stable_sort(ts.begin(), ts.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    f.tols = "[";
+    for (auto& t : ts) f.tols += t.second + ",";
+    f.tols += "]";
+  }
+  std::vector<int64_t> ports;
+  std::vector<std::string> imgs;
+  for (const char* key : {"containers", "initContainers"})
+    d.each(d.get(*sp, key), [&](const JVal& c) {
+      imgs.push_back(image_norm(d.str(c, "image")));
+      d.each(d.get(c, "ports"), [&](const JVal& pt) {
+        if (d.num(pt, "hostPort") != 0) ports.push_back(d.num(pt, "hostPort"));
+      });
+      d.each(d.get(c, "restartPolicyRules"), [&](const JVal& r) {  // restartallcontainers.InferForScheduling
+        if (d.str(r, "action") == "RestartAllContainers") out->needs_features = true;
+      });
+    });
+  const JVal* hu = d.get(*sp, "hostUsers");  // usernamespaceshostnetwork.InferForScheduling
+  if (d.boolean(*sp, "hostNetwork") && hu && hu->type == JVal::BOOL && !hu->b) out->needs_features = true;
+  std::sort(ports.begin(), ports.end());  // HostPortsSigner (:50-65)
+  ports.erase(std::unique(ports.begin(), ports.end()), ports.end());
+  f.ports = "[";
+  for (int64_t x : ports) f.ports += std::to_string(x) + ",";
+  f.ports += "]";
+  std::sort(imgs.begin(), imgs.end());  // ImageLocality.SignPod (image_locality.go:55-67): a sorted set
+  imgs.erase(std::unique(imgs.begin(), imgs.end()), imgs.end());
+  f.images = "[";
+  for (auto& x : imgs) f.images += x + ",";
+  f.images += "]";
+  std::vector<std::string> vols;  // VolumesSigner (:192-208)
+  d.each(d.get(*sp, "volumes"), [&](const JVal& v) {
+    if (d.present(v, "configMap") || d.present(v, "secret")) return;
+    std::vector<const JVal*> kv;
+    d.each(&v, [&](const JVal& x) {
+      if (x.key != "name") kv.push_back(&x);
+    });
+    std::sort(kv.begin(), kv.end(), [](const JVal* a, const JVal* b) { return a->key < b->key; });
+    std::string c = "{";
+    for (const JVal* x : kv) {  // the VolumeSource: every member but the name (as canon_json, one level up)
+      if (x->type == JVal::NUL || (x->type == JVal::STR && x->s.empty()) || (x->type == JVal::BOOL && !x->b) ||
+          ((x->type == JVal::ARR || x->type == JVal::OBJ) && x->count == 0))
+        continue;
+      c += "\"" + x->key + "\":";
+      canon_json(d, *x, c);
+      c += ",";
+    }
+    vols.push_back(c + "}");
+  });
+  f.vols = sorted_list(vols);
+  if (const JVal* af = d.get(*sp, "affinity"))  // NodeAffinitySigner (:150-178)
+    if (const JVal* na = d.get(*af, "nodeAffinity")) {
+      std::vector<std::string> pref, req;
+      d.each(d.get(*na, "preferredDuringSchedulingIgnoredDuringExecution"), [&](const JVal& t) {
+        pref.push_back("{w=" + std::to_string(d.num(t, "weight")) + ";p=" + ns_term_text(d, d.get(t, "preference")) + "}");
+      });
+      if (const JVal* rq = d.get(*na, "requiredDuringSchedulingIgnoredDuringExecution"))
+        d.each(d.get(*rq, "nodeSelectorTerms"), [&](const JVal& t) { req.push_back(ns_term_text(d, &t)); });
+      f.na = "{req=" + sorted_list(req) + ";pref=" + sorted_list(pref) + "}";
+    }
+  int claims = 0;
+  d.each(d.get(*sp, "resourceClaims"), [&](const JVal&) { ++claims; });
+  f.claims = claims > 0;
 }
 
 bool decode_node(const char* p, size_t n, NodeSpec* out, std::string* err) {
@@ -704,7 +867,11 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     JDoc d(p, n);
     const JVal& r = d.root();
     if (d.present(r, "percentageOfNodesToScore")) c->pct = (int)d.num(r, "percentageOfNodesToScore");
-    if (const JVal* fg = d.get(r, "featureGates")) c->taint_cmp_ops = d.boolean(*fg, "TaintTolerationComparisonOperators");
+    if (const JVal* fg = d.get(r, "featureGates")) {
+      c->taint_cmp_ops = d.boolean(*fg, "TaintTolerationComparisonOperators");
+      const JVal* ob = d.get(*fg, "OpportunisticBatching");  // Beta, on by default (kube_features.go:1674-1676)
+      if (ob && ob->type == JVal::BOOL) c->ob_gate = ob->b;
+    }
     c->device = (int)d.num(r, "device", 0);
     c->timing_stride = (int)d.num(r, "kernelTimingStride", 0);
     c->loop_timing_stride = (int)d.num(r, "loopTimingStride", 1);

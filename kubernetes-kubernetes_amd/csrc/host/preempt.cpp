@@ -301,6 +301,8 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   CompiledPod cp;
   int rc = compile(p, CYCLE, -1, false, true, &cp);
   if (rc) return rc;
+  // the failed cycle's statuses again, not a new cycle: OpportunisticBatching's state stays as it is
+  reinterpret_cast<PodDesc*>(cp.blob.data())->flags &= ~DF_OB;
   const PodDesc& D = *reinterpret_cast<const PodDesc*>(cp.blob.data());
 
   const bool pts_on = (D.filter_mask >> P_PTS & 1u) && D.n_ptsf > 0;

@@ -125,6 +125,7 @@ def _sig(lib, prefix):
     d("run_score_plugin", C.c_int, vp, i32, i32, C.POINTER(C.c_uint8), C.POINTER(i32), C.POINTER(C.c_int64),
       C.POINTER(C.c_int64))
     d("preempt", C.c_int, vp, i32, cp, sz, C.POINTER(PreemptResult), C.c_char_p, sz, C.POINTER(sz))
+    d("set_clock", C.c_int, vp, C.c_int64)
     return f
 
 
@@ -306,6 +307,10 @@ class Backend:
                 mask[i] = 1
         self._chk(self.f["run_score_plugin"](self.ctx, handle, pid, mask, C.byref(st), raw, nrm), "run_score_plugin")
         return st.value, list(raw[:n]), list(nrm[:n])
+
+    def set_clock(self, now_ns):
+        """time.Now() of the next scheduling calls, ns (OpportunisticBatching's maxBatchAge); 0: the wall clock."""
+        self._chk(self.f["set_clock"](self.ctx, int(now_ns)), "set_clock")
 
     def preempt(self, handle, args=None, detail_cap=1 << 20):
         """DefaultPreemption PostFilter for a compiled pod: (PreemptResult, detail dict)."""

@@ -37,6 +37,8 @@ def load():
         lib.ksg_generation.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib.ksg_debug_compare_mirror.restype = C.c_int
         lib.ksg_debug_compare_mirror.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.ksg_debug_batching.restype = C.c_int
+        lib.ksg_debug_batching.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib.ksg_debug_loop_stats.restype = C.c_int
         lib.ksg_debug_loop_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         from .abi import Result
@@ -74,6 +76,12 @@ class Scheduler(Backend):
         lg, ev = C.c_uint64(), C.c_uint64()
         self._chk(self.lib.ksg_generation(self.ctx, C.byref(lg), C.byref(ev)), "generation")
         return lg.value, ev.value
+
+    def batching(self):
+        """(pods placed by an OpportunisticBatching hint, scheduling cycles counted) -- ksg_debug_batching."""
+        h, c = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.ksg_debug_batching(self.ctx, C.byref(h), C.byref(c)), "batching")
+        return h.value, c.value
 
     def loop_stats(self):
         """(batches whose persistent loop gave up, batches an in-process group re-ran over the all-reduce

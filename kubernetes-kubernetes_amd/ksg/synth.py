@@ -264,3 +264,29 @@ def default_topology_spreading(n_nodes, n_init, n_pods, seed=0x5EED):
                                                                             "targetPort": 8000}]}}
     pods = [pod_with_label(f"pod-{k}", "service-ns") for k in range(n_pods)]
     return nodes, init, pods, [service]
+
+
+PAUSE_310_1 = "registry.k8s.io/pause:3.10.1"  # the batching templates' image
+
+
+def batching(n_nodes, n_pods, kind="hostport"):
+    """scheduler_perf's OpportunisticBatching workloads (test/integration/scheduler_perf/batching/
+    performance-config.yaml): node-default nodes and one pod template that fits once per node --
+    HostPortConflict: templates/pod-hostport-80.yaml (100m / 100Mi, hostPort 80); ResourceSaturation:
+    templates/pod-saturation.yaml (3 cpu / 1Gi on 4-cpu nodes).  Run them with the no-topology profile
+    (batching/scheduler-config-no-topology.yaml: PodTopologySpread List defaulting, no default constraints).
+    -> (nodes, pods)."""
+    nodes = [node_default(f"node-{i:06d}") for i in range(n_nodes)]
+    pods = []
+    for k in range(n_pods):
+        if kind == "hostport":
+            p = PodW(f"pod-hostport-80-{k}", "default").container(
+                image=PAUSE_310_1, requests={"cpu": "100m", "memory": "100Mi"},
+                ports=[{"containerPort": 80, "hostPort": 80}])
+        elif kind == "saturation":
+            p = PodW(f"pod-saturation-{k}", "default").container(image=PAUSE_310_1,
+                                                                 requests={"cpu": "3", "memory": "1Gi"})
+        else:
+            raise ValueError(kind)
+        pods.append(p.obj())
+    return nodes, pods

@@ -51,6 +51,10 @@ int ksgo_preempt(ksgo_ctx *ctx, int32_t handle, const char *args_json, size_t ar
 
 /* Go math.Log restatement (exposed so tests can compare it with libm). */
 double ksgo_go_log(double x);
+/* time.Now() of the following scheduling cycles (OpportunisticBatching's maxBatchAge); 0: the wall clock */
+int ksgo_set_clock(ksgo_ctx *ctx, int64_t now_ns);
+/* one TestBatchBasic case through the OpportunisticBatch restatement (oracle.cpp) */
+int ksgo_debug_batch_basic(const char *json, size_t len, char *out, size_t cap);
 int ksgo_debug_pod_resources(const char *json, size_t len, int64_t *out, int32_t cap);
 /* container/heap Init over (score) with nodeScoreHeap.Less, returns index of the root. */
 int32_t ksgo_heap_root(const int64_t *scores, int32_t n);

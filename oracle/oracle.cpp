@@ -138,6 +138,7 @@ struct Config {
   // systemDefaultConstraints (podtopologyspread/plugin.go:46-57,124-127); List -> DefaultConstraints
   bool ptsSystemDefaulted = true;
   std::vector<TopologySpreadConstraint> ptsDefaults;
+  bool obGate = true;  // featureGates.OpportunisticBatching (Beta, on: pkg/features/kube_features.go:1674-1676)
   Config() {
     // default_plugins.go:35-50
     const int64_t w[KSG_NUM_PLUGINS] = {0, 0, 3, 2, 0, 1, 2, 2, 1, 1};
@@ -170,7 +171,10 @@ static bool decode_config(const mj::Value& v, Config* c, std::string* err) {
   if (v.has("cpuThreads")) c->threads = std::max(1, (int)v.i64("cpuThreads"));
   if (v.has("cpuSpinUs")) c->spin_us = std::max(0, (int)v.i64("cpuSpinUs"));
   if (v.has("cpuParallelWeights")) c->par_weights = v.boolean("cpuParallelWeights");
-  if (auto fg = v.has("featureGates")) c->taintCompareOps = fg->boolean("TaintTolerationComparisonOperators");
+  if (auto fg = v.has("featureGates")) {
+    c->taintCompareOps = fg->boolean("TaintTolerationComparisonOperators");
+    c->obGate = fg->boolean("OpportunisticBatching", true);
+  }
   if (auto w = v.has("scoreWeights"))
     for (auto& kv : w->obj) {
       int id = plugin_id(kv.first);
@@ -523,6 +527,79 @@ class Pool {
 };
 
 static inline double nowus() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+// framework.SortedScoredNodes (framework/interface.go:158-162): what schedulePod hands
+// StoreScheduleResults -- sortedNodeScores, the nodeScoreHeap after heap.Init and the winner's Pop
+// (schedule_one.go:1050-1098); or, for TestBatchBasic (runtime/batch_test.go:165-185), a plain list.
+struct SortedScoredNodes {
+  bool isList = false;
+  std::vector<HeapEnt> heap;       // heap order; HeapEnt::idx indexes names
+  std::vector<std::string> names;  // node names (list: in pop order)
+  size_t head = 0;
+  int Len() const { return isList ? (int)(names.size() - head) : (int)heap.size(); }
+  std::string Pop() {  // sortedNodeScores.Pop: heap.Pop (swap(0, n-1), down(0, n-1), drop the last)
+    if (isList) return names[head++];
+    const int n = (int)heap.size() - 1;
+    std::swap(heap[0], heap[n]);
+    heap_down(heap, 0, n);
+    const HeapEnt e = heap[n];
+    heap.pop_back();
+    return names[e.idx];
+  }
+};
+
+// OpportunisticBatching (framework/runtime/batch.go:31-242): the state a signed pod's cycle leaves for the
+// next pod of the same signature.
+struct OpportunisticBatch {
+  struct State { std::string signature; std::unique_ptr<SortedScoredNodes> sortedNodes; int64_t creationNs = 0; };
+  std::unique_ptr<State> state;
+  int64_t lastCycleCount = 0;  // lastCycle (batch.go:51-55)
+  std::string lastChosenNode;
+  bool lastSucceeded = false;
+  int64_t batchedPods = 0;
+  bool genericWorkloadEnabled = false;
+  static constexpr int64_t kMaxBatchAgeNs = 500LL * 1000 * 1000;  // maxBatchAge (:57)
+
+  bool stateEmpty() const {  // :230-232
+    return !state || !state->sortedNodes || state->sortedNodes->Len() == 0;
+  }
+  // batchStateCompatible (:167-226); lastChosenRejected(name) runs RunFilterPlugins on the node: -1 when
+  // the node is not in the snapshot (BatchFlushNodeMissing), 1 when the pod is rejected there
+  template <typename RejectFn>
+  bool compatible(const std::string* signature, const std::string& nominated, int64_t cycleCount, int64_t now,
+                  RejectFn lastChosenRejected) const {
+    if (stateEmpty()) return false;
+    if (cycleCount != lastCycleCount + 1)
+      if (!genericWorkloadEnabled || cycleCount != lastCycleCount) return false;  // BatchFlushPodSkipped
+    if (!lastSucceeded) return false;                                             // BatchFlushPodFailed
+    if (!nominated.empty()) return false;                                         // BatchFlushPodNominated
+    if (!signature || *signature != state->signature) return false;               // BatchFlushPodIncompatible
+    if (now > state->creationNs + kMaxBatchAgeNs) return false;                   // BatchFlushExpired
+    return lastChosenRejected(lastChosenNode) == 1;  // else BatchFlushNodeMissing / BatchFlushNodeNotFull
+  }
+  template <typename RejectFn>
+  std::string GetNodeHint(const std::string* signature, const std::string& nominated, int64_t cycleCount, int64_t now,
+                          RejectFn lastChosenRejected) {  // :65-95
+    if (!compatible(signature, nominated, cycleCount, now, lastChosenRejected)) return "";
+    return state->sortedNodes->Pop();
+  }
+  // StoreScheduleResults (:98-158); otherNodes may be null (schedulePod's one-feasible-node path)
+  void StoreScheduleResults(const std::string* signature, const std::string& hinted, const std::string& chosen,
+                            std::unique_ptr<SortedScoredNodes> otherNodes, int64_t cycleCount, int64_t now) {
+    lastCycleCount = cycleCount;
+    lastChosenNode = chosen;
+    lastSucceeded = true;
+    if (hinted == chosen) {
+      batchedPods++;
+      return;
+    }
+    if (signature && otherNodes && otherNodes->Len() > 0) {
+      state.reset(new State{*signature, std::move(otherNodes), now});
+    } else {
+      state.reset();
+    }
+  }
+};
+
 struct ksgo_ctx {
   Config cfg;
   double prof[10] = {};  // ksgo_debug_profile: microseconds per cycle section (CPU-baseline breakdown)
@@ -549,6 +626,13 @@ struct ksgo_ctx {
   std::map<int32_t, std::unique_ptr<Pod>> queue;  // compiled pods
   int32_t nextHandle = 1;
   std::map<int32_t, std::string> assumedUid;  // handle -> assumed pod uid
+  OpportunisticBatch batch;  // frameworkImpl.batch (framework/runtime/framework.go:1620-1626)
+  int64_t cycleCount = 0;    // SchedulingQueue.SchedulingCycle(): one per scheduling cycle of this context
+  int64_t clockNs = 0;       // ksgo_set_clock: time.Now() of the next cycles (0: the wall clock)
+  int64_t now() const {
+    if (clockNs) return clockNs;
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
 
   // UpdateSnapshot (backend/cache/cache.go:190-296), its list part.  A NodeInfo object stays alive
   // while its name is in snapMap (the snapshot owns copies upstream; here the list points at the
@@ -1458,12 +1542,71 @@ static void normalize_scores(Cycle& cy, int p, std::vector<int64_t>& sc, const s
 // ===========================================================================
 // schedulePod (schedule_one.go:564-618)
 // ===========================================================================
-static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out* ev) {
+// frameworkImpl.SignPod (framework/runtime/framework.go:884-924) over the profile's plugins, every one of
+// which implements SignPlugin (computeBatchablePlugins, :832-876): the fragments keyed by signer name, or
+// nil (false) as soon as one plugin refuses.  The volume plugins, DynamicResources and NodeDeclaredFeatures
+// are always in the profile here; a pod that needs a declared feature never reaches a cycle.
+static bool sign_pod(const ksgo_ctx* c, const Pod& p, std::string* sig) {
+  const Config& k = c->cfg;
+  const Pod::SignFragments& f = p.sign;
+  std::string o = "sched=" + f.schedulerName;  // SchedulerNameSignerName
+  if (k.enabled[KSG_PLUGIN_NODE_RESOURCES_FIT] || k.enabled[KSG_PLUGIN_BALANCED_ALLOCATION]) {
+    // Fit.SignPod / BalancedAllocation.SignPod (fit.go:174-195, balanced_allocation.go:121-142):
+    // computePodResourceRequest -- the preFilterState Resource as Fit's PreFilter builds it
+    Resource r;
+    int64_t pods = 0;
+    bool scalar = false;
+    for (auto& kv : pod_requests(p, nullptr, false)) {
+      if (kv.first == "memory") r.memory = std::max(r.memory, milli_to_value(kv.second));
+      else if (kv.first == "cpu") r.milliCPU = std::max(r.milliCPU, kv.second);
+      else if (kv.first == "ephemeral-storage") r.ephemeral = std::max(r.ephemeral, milli_to_value(kv.second));
+      else if (kv.first == "pods") pods = std::max(pods, milli_to_value(kv.second));
+      else if (is_scalar_resource_name(kv.first)) {
+        scalar = true;
+        r.scalar[kv.first] = std::max(r.scalar[kv.first], milli_to_value(kv.second));
+      }
+    }
+    o += "|res=" + std::to_string(r.milliCPU) + "," + std::to_string(r.memory) + "," + std::to_string(r.ephemeral) +
+         "," + std::to_string(pods) + (scalar ? ",{" : ",null");
+    if (scalar) {
+      for (auto& kv : r.scalar) o += kv.first + "=" + std::to_string(kv.second) + ";";
+      o += "}";
+    }
+  }
+  if (k.enabled[KSG_PLUGIN_TAINT_TOLERATION] || k.enabled[KSG_PLUGIN_NODE_UNSCHEDULABLE])
+    o += "|tol=" + f.tolerations;  // TolerationsSignerName (taint_toleration.go:61-65, node_unschedulable.go:118-122)
+  if (k.enabled[KSG_PLUGIN_INTER_POD_AFFINITY]) {  // interpodaffinity/plugin.go:62-78
+    if (p.hasPodAffinity || p.hasPodAntiAffinity) return false;
+    if (!k.ignorePreferredTermsOfExistingPods) o += "|lbl=" + f.labels;
+  }
+  if (k.enabled[KSG_PLUGIN_NODE_PORTS]) o += "|ports=" + f.hostPorts;  // node_ports.go:66-70
+  if (k.enabled[KSG_PLUGIN_POD_TOPOLOGY_SPREAD]) {                  // podtopologyspread/plugin.go:92-102
+    if (!p.tsc.empty()) return false;
+    if (k.ptsSystemDefaulted || !k.ptsDefaults.empty()) return false;  // pl.defaultConstraints non-empty
+  }
+  if (k.enabled[KSG_PLUGIN_NODE_AFFINITY]) o += "|na=" + f.nodeAffinity + "|nsel=" + f.nodeSelector;  // :78-88
+  if (k.enabled[KSG_PLUGIN_NODE_NAME]) o += "|nn=" + p.nodeName;          // node_name.go:60-64
+  if (k.enabled[KSG_PLUGIN_IMAGE_LOCALITY]) o += "|img=" + f.images;     // image_locality.go:55-67
+  o += "|vol=" + f.volumes;  // VolumeRestrictions / NodeVolumeLimits / VolumeBinding / VolumeZone
+  if (f.hasClaims) return false;  // DynamicResources (dynamicresources.go:236-241)
+  o += "|feat=";  // NodeDeclaredFeatures: no required feature
+  *sig = std::move(o);
+  return true;
+}
+
+static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out* ev, bool cycle) {
   const double R0 = nowus();
   c->rebuild_list();
   c->prof[9] += nowus() - R0;
   g_taint_compare_ops = c->cfg.taintCompareOps;
   const int N = (int)c->list.size();
+  // OpportunisticBatching's inputs: the cycle count, the pod's signature (SignPod, computed when the pod is
+  // queued upstream; the same value here), the clock
+  const int64_t cycleCount = cycle ? ++c->cycleCount : c->cycleCount;
+  std::string sigv;
+  const bool ob = cycle && c->cfg.obGate;
+  const std::string* sig = ob && sign_pod(c, pod, &sigv) ? &sigv : nullptr;
+  const int64_t now = ob ? c->now() : 0;
   res->status = KSG_CODE_SUCCESS;
   res->node_index = -1;
   res->evaluated_nodes = 0;
@@ -1588,6 +1731,30 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
       if (ev->node_reasons) ev->node_reasons[idx] = st.reasons;
     }
   };
+  // ---- GetNodeHint (schedule_one.go:650-668, batch.go:65-95) and evaluateNominatedNode (:718-752) with the hint:
+  // the hinted node alone through findNodesThatPassFilters; feasible -> it is the result
+  std::string hint;
+  int hintFailed = -1;  // a hinted node that failed its filters (its status is in NodeToStatus)
+  if (ob) {
+    hint = c->batch.GetNodeHint(sig, pod.nominatedNodeName, cycleCount, now, [&](const std::string& nm) {
+      NodeInfoO* ni = c->snapMap.count(nm) ? c->nodes[nm].get() : nullptr;  // nodeInfos.Get
+      if (!ni) return -1;
+      return filter_node(ni).ok() ? 0 : 1;  // RunFilterPlugins: IsRejected
+    });
+    if (!hint.empty() && c->snapMap.count(hint)) {  // GetNodeInPlacement: else an error, and the full pass
+      NodeInfoO* hn = c->nodes[hint].get();
+      Status st = filter_node(hn);
+      if (st.ok()) {  // schedulePod's one-feasible-node path (:588-598)
+        c->batch.StoreScheduleResults(sig, hint, hint, nullptr, cycleCount, now);
+        res->node_index = idx_of(hn);
+        res->feasible_nodes = 1;
+        res->evaluated_nodes = 1;
+        return KSG_OK;
+      }
+      record_failed(hn, st);
+      hintFailed = idx_of(hn);
+    }
+  }
   if (c->pool && numToFind >= numAll) {
     // CPU-baseline mode: Parallelizer.Until's chunks of the rotated order (schedule_one.go:840), then
     // the per-chunk feasible lists concatenated in chunk order -- the sequential loop's result
@@ -1631,6 +1798,11 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     }
   }
   double T2 = nowus(); c->prof[1] += T2 - T1;
+  if (hintFailed >= 0) {  // NodeToStatus is keyed by node: the hinted node counts once
+    bool again = false;
+    for (auto* ni : nodes) again = again || idx_of(ni) == hintFailed;
+    if (!again) ++failed;
+  }
   int processed = (int)feasible.size() + failed;
   int diagLen = failed;  // NodeToStatus.Len(): explicit per-node statuses only
   c->nextStartNodeIndex = (c->nextStartNodeIndex + processed) % N;  // :686-687
@@ -1644,6 +1816,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
   if (feasible.size() == 1) {  // :588-598
     res->node_index = idx_of(feasible[0]);
     res->evaluated_nodes = 1 + diagLen;
+    if (ob) c->batch.StoreScheduleResults(sig, hint, feasible[0]->node.name, nullptr, cycleCount, now);
     return KSG_OK;
   }
   res->evaluated_nodes = (int)feasible.size() + diagLen;
@@ -1733,6 +1906,15 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
   int win = heap_pop_index(h);
   res->node_index = idx_of(feasible[win]);
   res->total_score = totals[win];
+  if (ob) {  // newSortedNodeScores + Pop, then StoreScheduleResults with the rest (:605-611)
+    auto rest = std::make_unique<SortedScoredNodes>();
+    rest->heap = std::move(h);
+    for (auto* ni : feasible) rest->names.push_back(ni->node.name);
+    for (int i = F / 2 - 1; i >= 0; i--) heap_down(rest->heap, i, F);  // heap.Init
+    const std::string top = rest->Pop();
+    if (top != feasible[win]->node.name) { c->err = "oracle: heap root differs from the pop"; return KSG_EINVAL; }
+    c->batch.StoreScheduleResults(sig, hint, top, std::move(rest), cycleCount, now);
+  }
   c->prof[5] += nowus() - T2;
   return KSG_OK;
 }
@@ -1970,11 +2152,72 @@ int ksgo_pod_compile(ksgo_ctx* c, const char* json, size_t len, int32_t* handle)
       if (auto rc = sp->has("resourceClaims"))
         if (rc->is_arr() && !rc->arr.empty()) { c->err = "resourceClaims"; return KSG_ENOTSUP; }
     }
+    if (p->needsNodeFeatures) {  // NodeDeclaredFeatures' PreFilter would not Skip (nodedeclaredfeatures.go:86-104)
+      c->err = "the pod needs a declared node feature (NodeDeclaredFeatures)";
+      return KSG_ENOTSUP;
+    }
     int32_t h = c->nextHandle++;
     c->queue[h] = std::move(p);
     *handle = h;
     return KSG_OK;
   } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+
+int ksgo_set_clock(ksgo_ctx* c, int64_t now_ns) {
+  c->clockNs = now_ns;
+  return KSG_OK;
+}
+
+// TestBatchBasic (framework/runtime/batch_test.go:187-436), one case: the first pod's GetNodeHint and (if it
+// was scheduled) StoreScheduleResults at cycle 1, then the second pod's GetNodeHint at cycle 2 (3 when a pod of
+// another profile came between, 1 for the same PodGroup cycle) against the lister holding the first chosen
+// node, whose filter rejects the second pod iff both pod ids start with 'b' (BatchTestPlugin.Filter), and its
+// StoreScheduleResults.  in: {"firstPodID", "firstSig", "firstPodScheduledSuccessfully", "firstChosenNode",
+// "firstOtherNodes": [..] | null, "sameCycle", "skipPod", "secondPodID", "secondPodNominatedNodeName",
+// "secondSig", "secondChosenNode", "secondOtherNodes": [..] | null, "genericWorkloadEnabled"}; out: {"hint",
+// "empty", "signature", "sortedNodes": [..]}.
+int ksgo_debug_batch_basic(const char* json, size_t len, char* out, size_t cap) {
+  try {
+    mj::Value v = mj::parse(json, len);
+    OpportunisticBatch b;
+    b.genericWorkloadEnabled = v.boolean("genericWorkloadEnabled");
+    auto list = [&](const char* k) -> std::unique_ptr<SortedScoredNodes> {
+      const mj::Value* a = v.has(k);
+      if (!a) return nullptr;
+      auto s = std::make_unique<SortedScoredNodes>();
+      s->isList = true;
+      for (auto& x : a->arr) s->names.push_back(x.s);
+      return s;
+    };
+    const std::string fs = v.str("firstSig"), ss = v.str("secondSig");
+    auto never = [](const std::string&) { return -1; };
+    std::string hint = b.GetNodeHint(&fs, "", 1, 0, never);
+    if (!hint.empty()) { std::snprintf(out, cap, "{\"error\":\"first pod got a hint\"}"); return KSG_EINVAL; }
+    if (v.boolean("firstPodScheduledSuccessfully"))
+      b.StoreScheduleResults(&fs, hint, v.str("firstChosenNode"), list("firstOtherNodes"), 1, 0);
+    const int64_t cycle = v.boolean("skipPod") ? 3 : v.boolean("sameCycle") ? 1 : 2;
+    const std::string first = v.str("firstChosenNode");
+    const bool blocking = v.str("firstPodID").rfind("b", 0) == 0 && v.str("secondPodID").rfind("b", 0) == 0;
+    hint = b.GetNodeHint(&ss, v.str("secondPodNominatedNodeName"), cycle, 0, [&](const std::string& nm) {
+      if (nm != first) return -1;  // the lister holds only the first chosen node
+      return blocking ? 1 : 0;
+    });
+    b.StoreScheduleResults(&ss, hint, v.str("secondChosenNode"), list("secondOtherNodes"), cycle, 0);
+    std::string o = "{\"hint\":\"" + hint + "\",\"empty\":" + (b.stateEmpty() ? "true" : "false");
+    if (!b.stateEmpty()) {
+      o += ",\"signature\":\"" + b.state->signature + "\",\"sortedNodes\":[";
+      SortedScoredNodes& sn = *b.state->sortedNodes;
+      for (size_t i = sn.head; i < sn.names.size(); ++i) o += (i > sn.head ? ",\"" : "\"") + sn.names[i] + "\"";
+      o += "]";
+    }
+    o += "}";
+    if (o.size() + 1 > cap) return KSG_ENOMEM;
+    std::memcpy(out, o.c_str(), o.size() + 1);
+    return KSG_OK;
+  } catch (std::exception& e) {
+    std::snprintf(out, cap, "{\"error\":\"%s\"}", e.what());
+    return KSG_EINVAL;
+  }
 }
 
 int ksgo_pod_release(ksgo_ctx* c, int32_t handle) {
@@ -1985,7 +2228,7 @@ int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* r
   auto it = c->queue.find(handle);
   if (it == c->queue.end()) return KSG_ENOTFOUND;
   double A0 = nowus();
-  int rc = run_cycle(c, *it->second, result, ev);
+  int rc = run_cycle(c, *it->second, result, ev, true);
   double A1 = nowus(); c->prof[6] += A1 - A0; c->prof[8] += 1;
   if (rc != KSG_OK) return rc;
   if ((flags & KSG_FLAG_ASSUME) && result->status == KSG_CODE_SUCCESS && result->node_index >= 0) {
@@ -2317,7 +2560,7 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
   ksg_eval_out ev{};
   ev.node_code = code.data();
   ksg_result cr;
-  int rc = run_cycle(c, pod, &cr, &ev);
+  int rc = run_cycle(c, pod, &cr, &ev, false);  // the failed cycle's statuses again: not a new cycle
   if (rc) return rc;
   if (!pod.nominatedNodeName.empty()) {
     NodeInfoO* nn = nullptr;

@@ -2,6 +2,7 @@
 #include "oracle_model.hpp"
 
 #include <algorithm>
+#include <set>
 #include <cctype>
 #include <cstdio>
 #include <climits>
@@ -525,7 +526,161 @@ bool decode_pod(const mj::Value& v, Pod* out, std::string* err) {
   if (auto vols = sp->has("volumes"))
     for (auto& vol : vols->arr)
       if (auto im = vol.has("image")) out->imageVolumes.push_back(im->str("reference"));
+  sign_fragments(v, out);
   return true;
+}
+
+// ============================================================================
+// SignPod fragments (kube-scheduler/framework/signers.go; the plugins' SignPod methods)
+// ============================================================================
+// A canonical text of a JSON value: object keys sorted, null / "" / false / empty members dropped (the
+// omitempty fields json.Marshal leaves out of a typed object, so a field written as its zero value and an
+// absent one encode alike).
+static void canon(const mj::Value& v, std::string& o) {
+  switch (v.kind) {
+    case mj::Value::Null: o += "null"; return;
+    case mj::Value::Bool: o += v.b ? "true" : "false"; return;
+    case mj::Value::Number: o += v.s; return;
+    case mj::Value::String: o += '"'; o += v.s; o += '"'; return;
+    case mj::Value::Array:
+      o += '[';
+      for (size_t i = 0; i < v.arr.size(); ++i) {
+        if (i) o += ',';
+        canon(v.arr[i], o);
+      }
+      o += ']';
+      return;
+    case mj::Value::Object: {
+      std::vector<const std::pair<std::string, mj::Value>*> kv;
+      for (auto& m : v.obj) {
+        const mj::Value& x = m.second;
+        if (x.kind == mj::Value::Null || (x.kind == mj::Value::String && x.s.empty()) ||
+            (x.kind == mj::Value::Bool && !x.b) || (x.kind == mj::Value::Array && x.arr.empty()) ||
+            (x.kind == mj::Value::Object && x.obj.empty()))
+          continue;
+        kv.push_back(&m);
+      }
+      std::sort(kv.begin(), kv.end(), [](auto* a, auto* b) { return a->first < b->first; });
+      o += '{';
+      for (size_t i = 0; i < kv.size(); ++i) {
+        if (i) o += ',';
+        o += '"'; o += kv[i]->first; o += "\":";
+        canon(kv[i]->second, o);
+      }
+      o += '}';
+      return;
+    }
+  }
+}
+static std::string join_sorted(std::vector<std::string> v) {
+  std::sort(v.begin(), v.end());
+  std::string o = "[";
+  for (size_t i = 0; i < v.size(); ++i) o += (i ? "," : "") + v[i];
+  return o + "]";
+}
+static std::string str_map(const mj::Value* m) {  // a map[string]string: null when nil
+  if (!m) return "null";
+  std::vector<std::string> kv;
+  for (auto& e : m->obj) kv.push_back(e.first + "=" + (e.second.kind == mj::Value::String ? e.second.s : std::string()));
+  std::sort(kv.begin(), kv.end());
+  std::string o = "{";
+  for (auto& x : kv) o += x + ";";
+  return o + "}";
+}
+// NodeSelectorRequirementsSigner (signers.go:67-82): each requirement with its values sorted, then the list
+static std::string node_reqs_signer(const mj::Value* reqs) {
+  std::vector<std::string> out;
+  if (reqs)
+    for (auto& r : reqs->arr) {
+      std::vector<std::string> vals;
+      if (auto vs = r.has("values"))
+        for (auto& x : vs->arr) vals.push_back(x.s);
+      std::sort(vals.begin(), vals.end());
+      std::string t = "{key=" + r.str("key") + ";op=" + r.str("operator") + ";values=[";
+      for (auto& x : vals) t += x + ",";
+      out.push_back(t + "]}");
+    }
+  return join_sorted(out);
+}
+static std::string term_signer(const mj::Value* t) {  // NodeSelectorTermSigner (:87-101)
+  return "{exp=" + node_reqs_signer(t ? t->has("matchExpressions") : nullptr) +
+         ";fld=" + node_reqs_signer(t ? t->has("matchFields") : nullptr) + "}";
+}
+
+void sign_fragments(const mj::Value& v, Pod* out) {
+  Pod::SignFragments& f = out->sign;
+  const mj::Value* sp = v.has("spec");
+  const mj::Value* md = v.has("metadata");
+  f.labels = str_map(md ? md->has("labels") : nullptr);
+  f.schedulerName = sp ? sp->str("schedulerName") : "";
+  f.nodeSelector = str_map(sp ? sp->has("nodeSelector") : nullptr);
+  if (!sp) {
+    f.tolerations = f.hostPorts = f.images = f.volumes = "[]";
+    f.nodeAffinity = "null";
+    return;
+  }
+  {  // TolerationsSigner (:180-189): sort.Slice by (key, value) -- an insertion sort, stable, up to 12
+    std::vector<std::pair<std::pair<std::string, std::string>, std::string>> ts;
+    if (auto tl = sp->has("tolerations"))
+      for (auto& t : tl->arr) {
+        std::string c;
+        canon(t, c);
+        ts.push_back({{t.str("key"), t.str("value")}, c});
+      }
+    std::stable_sort(ts.begin(), ts.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    f.tolerations = "[";
+    for (auto& t : ts) f.tolerations += t.second + ",";
+    f.tolerations += "]";
+  }
+  std::set<int64_t> ports;  // HostPortsSigner (:50-65): containers then init containers
+  std::set<std::string> images;  // ImageLocality.SignPod (image_locality.go:55-67)
+  for (const char* key : {"containers", "initContainers"})
+    if (auto cs = sp->has(key))
+      for (auto& c : cs->arr) {
+        images.insert(normalized_image_name(c.str("image")));
+        if (auto ps = c.has("ports"))
+          for (auto& p : ps->arr)
+            if (p.i64("hostPort") != 0) ports.insert(p.i64("hostPort"));
+        if (auto rr = c.has("restartPolicyRules"))  // restartallcontainers.InferForScheduling
+          for (auto& r : rr->arr)
+            if (r.str("action") == "RestartAllContainers") out->needsNodeFeatures = true;
+      }
+  if (sp->boolean("hostNetwork") && sp->get("hostUsers") && sp->get("hostUsers")->kind == mj::Value::Bool &&
+      !sp->boolean("hostUsers", true))
+    out->needsNodeFeatures = true;  // usernamespaceshostnetwork.InferForScheduling
+  f.hostPorts = "[";
+  for (int64_t p : ports) f.hostPorts += std::to_string(p) + ",";
+  f.hostPorts += "]";
+  f.images = "[";
+  for (auto& x : images) f.images += x + ",";
+  f.images += "]";
+  {  // VolumesSigner (:192-208): every volume but ConfigMap / Secret ones, by its VolumeSource
+    std::vector<std::string> vs;
+    if (auto vols = sp->has("volumes"))
+      for (auto& vol : vols->arr) {
+        if (vol.has("configMap") || vol.has("secret")) continue;
+        mj::Value src = vol;
+        src.obj.erase(std::remove_if(src.obj.begin(), src.obj.end(), [](auto& m) { return m.first == "name"; }),
+                      src.obj.end());
+        std::string c;
+        canon(src, c);
+        vs.push_back(c);
+      }
+    f.volumes = join_sorted(vs);
+  }
+  f.nodeAffinity = "null";  // NodeAffinitySigner (:150-178): nil without spec.affinity.nodeAffinity
+  if (auto af = sp->has("affinity"))
+    if (auto na = af->has("nodeAffinity")) {
+      std::vector<std::string> pref, req;
+      if (auto pf = na->has("preferredDuringSchedulingIgnoredDuringExecution"))
+        for (auto& t : pf->arr)
+          pref.push_back("{w=" + std::to_string(t.i64("weight")) + ";p=" + term_signer(t.has("preference")) + "}");
+      if (auto rq = na->has("requiredDuringSchedulingIgnoredDuringExecution"))
+        if (auto terms = rq->has("nodeSelectorTerms"))
+          for (auto& t : terms->arr) req.push_back(term_signer(&t));
+      f.nodeAffinity = "{req=" + join_sorted(req) + ";pref=" + join_sorted(pref) + "}";
+    }
+  if (auto rc = sp->has("resourceClaims")) f.hasClaims = !rc->arr.empty();
 }
 
 // ============================================================================

@@ -138,6 +138,24 @@ struct Pod {
   // metav1.GetControllerOfNoCopy (apimachinery/pkg/apis/meta/v1/controller_ref.go:48-56)
   bool hasController = false;
   std::string ownerAPIVersion, ownerKind, ownerName;
+  // SignPod fragments (framework/runtime/framework.go:884-924 over the plugins' SignPod methods and the
+  // signers of staging/src/k8s.io/kube-scheduler/framework/signers.go), each a canonical text of the value
+  // json.Marshal would encode: two pods' fragments are equal iff the reference's encodings are.  The
+  // resources fragment depends on the profile's request options and is formed at signing time.
+  struct SignFragments {
+    std::string schedulerName;  // v1.Pod.Spec.SchedulerName
+    std::string tolerations;    // TolerationsSigner: sorted by (key, value), stable
+    std::string labels;         // v1.Pod.Labels (InterPodAffinity)
+    std::string hostPorts;      // HostPortsSigner: sorted distinct non-zero host ports
+    std::string nodeAffinity;   // NodeAffinitySigner
+    std::string nodeSelector;   // v1.Pod.Spec.NodeSelector
+    std::string images;         // ImageLocality: sorted distinct normalized image names
+    std::string volumes;        // VolumesSigner: sorted non-ConfigMap / non-Secret volume sources
+    bool hasClaims = false;     // spec.resourceClaims (DynamicResources refuses to sign)
+  } sign;
+  // NodeDeclaredFeatures: the pod needs a declared node feature (InferForPodScheduling non-empty:
+  // restartPolicyRules with RestartAllContainers, or hostNetwork with hostUsers false)
+  bool needsNodeFeatures = false;
 };
 
 struct Namespace { std::string name; Labels labels; };
@@ -155,6 +173,7 @@ TopologySpreadConstraint decode_tsc(const mj::Value& c);
 
 bool decode_node(const mj::Value& v, Node* out, std::string* err);
 bool decode_pod(const mj::Value& v, Pod* out, std::string* err);
+void sign_fragments(const mj::Value& v, Pod* out);  // Pod::sign, Pod::needsNodeFeatures
 bool decode_namespace(const mj::Value& v, Namespace* out, std::string* err);
 
 // ---- scheduler-side derived types ------------------------------------------------------
