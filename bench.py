@@ -92,7 +92,16 @@ WORKLOADS = {
            "preferred anti-affinity / zone spread)", 100000, 10000, 4),
     "dts": ("DefaultTopologySpreading (pods selected by a Service: PodTopologySpread system default "
             "constraints)", 5000, 5000, None),
+    # scheduler_perf batching/performance-config.yaml (OpportunisticBatching, no-topology profile)
+    "hostport": ("HostPortConflict (OpportunisticBatching; one hostPort-80 pod per node)", 20000, 0, None),
+    "saturation": ("ResourceSaturation (OpportunisticBatching; one 3-cpu pod per 4-cpu node)", 20000, 0, None),
 }
+
+# batching/scheduler-config-no-topology.yaml: PodTopologySpread List defaulting without default constraints,
+# the profile in which OpportunisticBatching acts
+BATCH_CLOCK_NS = 10 ** 15
+PROFILES = {"hostport": {"podTopologySpread": {"defaultingType": "List", "defaultConstraints": []}},
+            "saturation": {"podTopologySpread": {"defaultingType": "List", "defaultConstraints": []}}}
 
 
 def cpu_model():
@@ -138,19 +147,23 @@ def cpu_topology():
     return {"affinity_cpus": len(cpus), "physical_cores": len(cores), "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), extra=None):
+def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), extra=None, profile=None):
     """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
     Filter / Score loops over nodes on a pool of that many threads (the reference's
     Parallelizer.Until with parallelism 16), results identical to the sequential oracle
     (tests/test_oracle_parallel.py)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_binding import oracle
-    cfg = {"cpuThreads": threads} if threads > 1 else {}
+    cfg = dict(profile or {})
+    if threads > 1:
+        cfg["cpuThreads"] = threads
     if threads > 1 and extra:  # pool knobs (oracle.cpp: cpuSpinUs, cpuParallelWeights)
         cfg.update(extra)
     if pct != 100:  # the cut filter pass runs sequentially in the oracle (its Score loop stays parallel)
         cfg["percentageOfNodesToScore"] = pct
     o = oracle(cfg)
+    if profile:  # the batching workloads: one fixed clock, as the device's (no 500 ms expiry mid-run)
+        o.set_clock(BATCH_CLOCK_NS)
     for ob in objects:
         o.upsert_object(ob)
     for n in nodes:
@@ -241,6 +254,9 @@ def main():
         nodes, init, pods = synth.mixed_cluster(n_nodes, n_init, n_warm + n_meas)
     elif a.workload == "dts":
         nodes, init, pods, objects = synth.default_topology_spreading(n_nodes, n_init, n_warm + n_meas)
+    elif a.workload in PROFILES:
+        nodes, pods = synth.batching(n_nodes, n_warm + n_meas, a.workload)
+        init = []
     else:
         nodes, init, pods = synth.topology_spreading(n_nodes, n_init, n_warm + n_meas,
                                                      preferred_anti=a.workload == "c4-anti")
@@ -251,7 +267,8 @@ def main():
     def build(dev_exchange):
         """Scheduler with the cluster loaded, warm-up batches run (then forgotten, so the timed run
         starts from the config state); None if the warm-up failed on this rank."""
-        cfg = {"device": local, "kernelTimingStride": a.timing_stride, "percentageOfNodesToScore": a.pct}
+        cfg = dict(PROFILES.get(a.workload, {}), device=local, kernelTimingStride=a.timing_stride,
+                   percentageOfNodesToScore=a.pct)
         if a.extra_config:
             cfg.update(json.loads(a.extra_config))
         if sharded:  # one scheduler, nodes sharded over the ranks; the RCCL id comes from rank 0
@@ -261,6 +278,8 @@ def main():
             cfg["distributed"] = {"worldSize": world, "rank": rank, "ncclId": obj[0]}
             cfg["deviceExchange"] = dev_exchange
         s = Scheduler(cfg)
+        if a.workload in PROFILES:  # OpportunisticBatching's maxBatchAge clock: fixed, so oracle and device agree
+            s.set_clock(BATCH_CLOCK_NS)
         for ob in objects:
             s.upsert_object(ob)
         for n in nodes:
@@ -345,10 +364,10 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             # the reference's default parallelism (16 goroutines over nodes), then one thread
             v, done, cdt, ores = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads,
-                                              pct=a.pct, objects=objects)
+                                              pct=a.pct, objects=objects, profile=PROFILES.get(a.workload))
             bk = cpu_baseline.breakdown
             v1, done1, cdt1, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct,
-                                              objects=objects)
+                                              objects=objects, profile=PROFILES.get(a.workload))
             bk1 = cpu_baseline.breakdown
             # every CPU the process may use (affinity mask and cgroup quota)
             ncpu = usable_cpus()
@@ -356,7 +375,7 @@ def main():
                 va, donea, cdta = v, done, cdt
             else:
                 va, donea, cdta, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=ncpu,
-                                                  pct=a.pct, objects=objects)
+                                                  pct=a.pct, objects=objects, profile=PROFILES.get(a.workload))
             cpu = {"value": round(v, 2), "unit": "pods/s", "cores": a.cpu_threads, "kind": "port",
                    "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "

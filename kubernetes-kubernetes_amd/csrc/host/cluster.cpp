@@ -748,7 +748,10 @@ int Cluster::relayout_gather(bool* done) {
   if (nt > taint_cap_ || ni > img_cap_) return KSG_OK;
   if (fresh * 2 > n) return KSG_OK;  // mostly new columns: the full path is as cheap
   // device scratch: the index map, the new CSR offsets, one column block
-  const size_t blk = (size_t)cap * 8 * (size_t)std::max(view.scalar_cols, std::max(slots_used_, 1));
+  // (the widest block: the scalar columns, the label columns, or the host-port rows, which a batch of
+  // host-port pods widens by one slot per pod, Cluster::reserve_ports)
+  const size_t blk = (size_t)cap * std::max<size_t>(8 * (size_t)std::max(view.scalar_cols, std::max(slots_used_, 1)),
+                                                    4 * (size_t)std::max(view.port_slots, 1));
   const size_t o_src = 0, o_toff = ((size_t)n * 4 + 255) & ~size_t(255),
                o_ioff = o_toff + (((size_t)(cap + 1) * 4 + 255) & ~size_t(255)),
                o_blk = o_ioff + (((size_t)(cap + 1) * 4 + 255) & ~size_t(255));

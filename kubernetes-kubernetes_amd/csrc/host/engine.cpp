@@ -12,6 +12,7 @@
 // run_batch() then launches k_filter_score + k_select per pod on one stream with no host
 // round trip inside the batch (device-side AssumePod), and reads the results back once.
 #include <algorithm>
+#include <unordered_set>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -1637,16 +1638,21 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (int i = compiled; i < n && !pods_needed; ++i)
       pods_needed = existing_terms || !pods[i]->spreads.empty() || pods[i]->has_pod_affinity || pods[i]->has_pod_anti;
   }
-  {  // host ports the batch's assumes can add to one node (the device row must hold them)
-    int32_t extra = 0;
+  {  // host ports the batch's assumes can add to one node (the device row must hold them): the distinct
+     // (ip, protocol, port) entries -- HostPortInfo.Add is a set insert, so a port many pods share takes one
+     // slot (a batch of HostPortConflict pods needs one, not one per pod)
+    std::unordered_set<std::string> distinct;
+    auto add = [&](const HostPort& hp) {
+      if (hp.port > 0) distinct.insert(hp.ip + '\x1f' + hp.proto + '\x1f' + std::to_string(hp.port));
+    };
     for (int i = 0; i < n; ++i) {
       for (auto& k : pods[i]->containers)
-        for (auto& hp : k.ports) extra += hp.port > 0;
+        for (auto& hp : k.ports) add(hp);
       for (auto& k : pods[i]->init_containers)
         if (k.sidecar)
-          for (auto& hp : k.ports) extra += hp.port > 0;
+          for (auto& hp : k.ports) add(hp);
     }
-    c->reserve_ports(extra);
+    c->reserve_ports((int32_t)distinct.size());
   }
   const auto Tm = clk::now();
   if ((rc = c->ensure_mirror(pods_needed))) return rc;
