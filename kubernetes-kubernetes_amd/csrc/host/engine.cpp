@@ -1914,7 +1914,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         if (!cp[i].error) c->next_start = d.rot_next;  // the last launched pod's wins
       }
       r.total_score = d.feasible > 1 ? d.total : 0;
-      if (d.hinted) {  // OpportunisticBatching: the hinted node alone was evaluated (k_ob_hint)
+      const bool hinted = d.hinted && (reinterpret_cast<const PodDesc*>(cp[i].blob.data())->flags & DF_OB);
+      if (hinted) {  // OpportunisticBatching: the hinted node alone was evaluated (k_ob_hint; other paths
+                     // leave the word unset)
         r.evaluated_nodes = 1;
         ++ob_hinted_;
       }
@@ -2529,7 +2531,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       tot[i] = (int64_t)gath[(1 + kNumPlugins) * n + i];
     }
   }
-  if (eval && hr[0].hinted) {  // placed by the OpportunisticBatching hint: no status, no score (k_ob_hint)
+  const bool hinted0 = eval && hr[0].hinted && (reinterpret_cast<const PodDesc*>(cp[0].blob.data())->flags & DF_OB);
+  if (hinted0) {  // placed by the OpportunisticBatching hint: no status, no score (k_ob_hint)
     std::fill(st.begin(), st.end(), 0u);
     std::fill(outs.begin(), outs.end(), 0);
     std::fill(tot.begin(), tot.end(), 0);
@@ -2540,7 +2543,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     eval->prefilter_plugin = cp[0].prefilter_reject ? cp[0].prefilter_plugin : 255;
     uint32_t smask = cp[0].score_mask;
     if (!(hr[0].ipa_any & 8u)) smask &= ~(1u << P_IPA);  // InterPodAffinity PreScore Skip (scoring.go:207-209)
-    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject && !hr[0].hinted) ? smask : 0;
+    eval->score_plugin_mask = (hr[0].feasible > 1 && !cp[0].prefilter_reject && !hinted0) ? smask : 0;
     for (int32_t i = 0; i < N; ++i) {
       const uint32_t w = st[i];
       if (eval->node_code) eval->node_code[i] = (uint8_t)status_code(w);

@@ -907,7 +907,10 @@ def test_sched_loop_sampling_matches_oracle(native, unit, k):
     for seed, (n_nodes, topo) in enumerate([(700, False), (1900, True), (5000, False)]):
         rng, cfg, nodes, existing, names = rand_cluster(9400 + 10 * k + seed, n_nodes=n_nodes, n_existing=120,
                                                         topology=topo)
-        g, o = _pair(native, dict(cfg, **extra, percentageOfNodesToScore=pct, loopUnit=unit), nodes, existing)
+        # (the no-score profile disables PodTopologySpread, so OpportunisticBatching would act and its signed
+        # pods take the launch path: the gate is off here, this test is about the loop)
+        g, o = _pair(native, dict(cfg, **extra, percentageOfNodesToScore=pct, loopUnit=unit,
+                                  featureGates={"OpportunisticBatching": False}), nodes, existing)
         for rnd in range(2):
             pods = [rand_pod(rng, 500 * rnd + q, names, topology=topo and q % 5 == 2) for q in range(150)]
             rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)

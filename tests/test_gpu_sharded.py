@@ -23,6 +23,10 @@ pytestmark = pytest.mark.gpu
 def _group(world, cfg, nodes, existing):
     from ksg.native import Scheduler
     name = f"t-{uuid.uuid4().hex[:8]}"
+    # a node-sharded scheduler does not run OpportunisticBatching (ksg_create refuses a profile where it acts,
+    # e.g. PodTopologySpread disabled): the gate is off for every rank and the oracle alike
+    cfg = dict(cfg)
+    cfg.setdefault("featureGates", {"OpportunisticBatching": False})
     ranks = []
     for r in range(world):
         s = Scheduler(dict(cfg, device=0, distributed={"worldSize": world, "rank": r, "localGroup": name}))
