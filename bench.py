@@ -147,7 +147,7 @@ def cpu_topology():
     return {"affinity_cpus": len(cpus), "physical_cores": len(cores), "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), extra=None, profile=None):
+def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), extra=None, profile=None, warm=()):
     """Oracle (C++ restatement of the reference), same pods from the same state.  threads > 1: its
     Filter / Score loops over nodes on a pool of that many threads (the reference's
     Parallelizer.Until with parallelism 16), results identical to the sequential oracle
@@ -170,6 +170,16 @@ def cpu_baseline(nodes, init, pods, budget_s, threads=1, pct=100, objects=(), ex
         o.add_node(n)
     for p in init:
         o.add_pod(p)
+    # the device's warm-up, replayed (scheduled, then forgotten) where it leaves state behind: the
+    # rotation (percentageOfNodesToScore < 100) and OpportunisticBatching's cycle and stored list
+    wh = [o.compile(p) for p in warm]
+    if wh:
+        o.schedule_batch(wh, assume=True)
+        for h in wh:
+            try:
+                o.forget(h)
+            except Exception:
+                pass
     hs = [o.compile(p) for p in pods]
     done = 0
     results = []
@@ -361,13 +371,14 @@ def main():
 
     if rank == 0:
         cpu = None
+        warm = pods[:n_warm] if (a.pct != 100 or a.workload in PROFILES) else ()
         if not a.no_cpu_baseline and world == 1:
             # the reference's default parallelism (16 goroutines over nodes), then one thread
             v, done, cdt, ores = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds, threads=a.cpu_threads,
-                                              pct=a.pct, objects=objects, profile=PROFILES.get(a.workload))
+                                              pct=a.pct, objects=objects, profile=PROFILES.get(a.workload), warm=warm)
             bk = cpu_baseline.breakdown
             v1, done1, cdt1, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=1, pct=a.pct,
-                                              objects=objects, profile=PROFILES.get(a.workload))
+                                              objects=objects, profile=PROFILES.get(a.workload), warm=warm)
             bk1 = cpu_baseline.breakdown
             # every CPU the process may use (affinity mask and cgroup quota)
             ncpu = usable_cpus()
@@ -375,7 +386,7 @@ def main():
                 va, donea, cdta = v, done, cdt
             else:
                 va, donea, cdta, _ = cpu_baseline(nodes, init, pods[n_warm:], a.cpu_seconds / 2, threads=ncpu,
-                                                  pct=a.pct, objects=objects, profile=PROFILES.get(a.workload))
+                                                  pct=a.pct, objects=objects, profile=PROFILES.get(a.workload), warm=warm)
             cpu = {"value": round(v, 2), "unit": "pods/s", "cores": a.cpu_threads, "kind": "port",
                    "node_evals_per_s": round(v * n_nodes, 1),
                    "sample": f"first {done} of the {n_meas} measured pods from the same initial state, "
