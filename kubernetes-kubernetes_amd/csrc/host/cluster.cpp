@@ -40,7 +40,10 @@ int hw_queues() {
   return q;
 }
 static std::atomic<int> g_streams{0};
-bool stream_created() { return g_streams.fetch_add(1) + 1 + 1 <= hw_queues(); }  // + the null stream
+// + the null stream, + one spare: a rocprofv3 kernel trace of a W = 3 in-process group (profiles/
+// r05c_w3_queue_trace.txt) shows its three streams and the null stream on all four of HIP's default queues;
+// a stream this count cannot see (a library's internal one) then shares a rank's queue
+bool stream_created() { return g_streams.fetch_add(1) + 1 + 1 + 1 <= hw_queues(); }
 void stream_destroyed() { g_streams.fetch_sub(1); }
 
 Cluster::Cluster(const Config& c) : cfg(c) {

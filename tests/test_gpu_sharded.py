@@ -117,8 +117,9 @@ def test_random_streams_match_oracle_device_exchange(world, seed):
 def test_device_exchange_loop_c2(world):
     """The persistent loop across W ranks (granules stored into every rank's array), SchedulingBasic
     pods only, heterogeneous nodes (untied scores), batches long enough for the chunked pipeline.
-    In-process groups of GPU_MAX_HW_QUEUES (4) ranks or more cannot keep every rank's loop resident,
-    so W = 4 checks that they fall back to the all-reduce path."""
+    In-process groups need a hardware queue per rank plus the null stream's and a spare (the test process
+    asks HIP for 8, conftest.py), so W = 4 runs the loop as well; test_device_exchange_needs_own_queues
+    checks the fallback at the limit."""
     from ksg.synth import scheduling_basic
     nodes, init, pods = scheduling_basic(600 * world + 77, 300, 600, hetero=True)
     ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
@@ -425,23 +426,27 @@ def test_loop_give_up_retried_over_allreduce(world):
         assert s.compare_mirror(sync=True)[0] == 0
 
 
-@pytest.mark.skipif(os.environ.get("GPU_MAX_HW_QUEUES", "4") != "4", reason="counts HIP's default 4 hardware queues")
 def test_device_exchange_needs_own_queues():
     """In-process ranks take the device exchange only when every rank's stream has a hardware queue of its
-    own: with another context's stream alive, a W = 3 group's three streams plus the null
-    stream exceed GPU_MAX_HW_QUEUES = 4, so HIP would put two of them on one queue, where a rank's loop
-    waits behind a peer's loop that spins on it.  That group must keep the all-reduce path (and still
-    match the oracle); once the other context is gone, a new W = 3 group runs the loop."""
+    own, with the null stream's and one spare beside them: with Q = GPU_MAX_HW_QUEUES, a group
+    of Q - 2 ranks runs the loop, but not while another context's stream is alive -- HIP would then put two
+    streams on one queue, where a rank's loop waits behind a peer's loop that spins on it.  That group keeps
+    the all-reduce path (and still matches the oracle); once the other context is gone, a new group runs the
+    loop."""
     from ksg.native import Scheduler
     from ksg.synth import scheduling_basic
-    nodes, init, pods = scheduling_basic(1877, 300, 600, hetero=True)
+    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    world = q - 2
+    if world < 2 or world > 8:
+        pytest.skip(f"GPU_MAX_HW_QUEUES={q}: no in-process group size at the queue limit")
+    nodes, init, pods = scheduling_basic(1877 + 256 * world, 300, 600, hetero=True)
     other = Scheduler({"device": 0})
-    ranks, o = _group(3, {"deviceExchange": True}, nodes, init)
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
     _check(ranks, o, pods, chunk=300)
     assert _dominant(ranks) == {"k_filter_score"}
     for s in ranks:
         s.close()
     other.close()
-    ranks, o = _group(3, {"deviceExchange": True}, nodes, init)
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
     _check(ranks, o, pods, chunk=300)
     assert _dominant(ranks) == {"k_sched_loop"}
