@@ -978,18 +978,6 @@ Engine::Engine(Cluster* cl) : c(cl) {
 // A pod the persistent loop evaluates: node-local plugins only (no pod-table aggregation, no
 // PodTopologySpread / InterPodAffinity scores, no per-node evaluation output).
 // No extended-resource requests anywhere in the pod (the batch pipeline's compile-cannot-fail test).
-bool pod_scalar_free(const PodSpec& p) {
-  auto ok = [](const ResVec& v) {
-    for (auto& r : v)
-      if (r.name != "cpu" && r.name != "memory" && r.name != "ephemeral-storage") return false;
-    return true;
-  };
-  for (auto& k : p.containers)
-    if (!ok(k.req) || !ok(k.st_req) || !ok(k.st_alloc)) return false;
-  for (auto& k : p.init_containers)
-    if (!ok(k.req) || !ok(k.st_req) || !ok(k.st_alloc)) return false;
-  return ok(p.pod_requests) && ok(p.overhead) && ok(p.pod_st_req) && ok(p.pod_st_alloc);
-}
 static bool calc_scalar_free(const PodSpec& p) {  // decided once per pod at decode (ksg_pod_compile)
   return p.scalar_free >= 0 ? p.scalar_free != 0 : pod_scalar_free(p);
 }

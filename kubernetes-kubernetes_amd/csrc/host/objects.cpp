@@ -75,7 +75,7 @@ bool parse_quantity(const std::string& s, int64_t* milli) {
   return true;
 }
 
-int64_t milli_ceil(int64_t m) { return m >= 0 ? m / 1000 + (m % 1000 ? 1 : 0) : -((-m) / 1000); }
+int64_t milli_ceil(int64_t m) { return m >= 0 ? m / 1000 + (m % 1000 ? 1 : 0) : m / 1000; }
 
 bool parse_go_int(const std::string& s, int64_t* v) {
   if (s.empty()) return false;
@@ -246,6 +246,19 @@ bool parse_rfc3339(const std::string& s, int64_t* unix_ns) {
   return true;
 }
 
+// every request / overhead names cpu, memory or ephemeral-storage only (PodSpec::scalar_free)
+bool pod_scalar_free(const PodSpec& p) {
+  auto ok = [](const ResVec& v) {
+    for (auto& r : v)
+      if (r.name != "cpu" && r.name != "memory" && r.name != "ephemeral-storage") return false;
+    return true;
+  };
+  for (auto& k : p.containers)
+    if (!ok(k.req) || !ok(k.st_req) || !ok(k.st_alloc)) return false;
+  for (auto& k : p.init_containers)
+    if (!ok(k.req) || !ok(k.st_req) || !ok(k.st_alloc)) return false;
+  return ok(p.pod_requests) && ok(p.overhead) && ok(p.pod_st_req) && ok(p.pod_st_alloc);
+}
 static void pod_sign_fragments(const JDoc& d, const JVal& root, PodSpec* out);  // below
 
 bool decode_pod(const char* p, size_t n, PodSpec* out, std::string* err) {

@@ -25,7 +25,8 @@ using ResList = std::map<std::string, int64_t>;
 // staging/src/k8s.io/apimachinery/pkg/api/resource/quantity.go (ParseQuantity,
 // MilliValue/Value round up = ceil for the non-negative values requests carry).
 bool parse_quantity_milli(const std::string& s, int64_t* milli);
-inline int64_t milli_to_value(int64_t m) { return m >= 0 ? (m + 999) / 1000 : -((-m) / 1000); }
+// (ceil for m >= 0 without the m + 999 overflow at the int64 edge; truncation toward zero below 0)
+inline int64_t milli_to_value(int64_t m) { return m >= 0 ? m / 1000 + (m % 1000 ? 1 : 0) : m / 1000; }
 
 // ---- labels.Selector -----------------------------------------------------------------
 enum class Op { In, NotIn, Exists, DoesNotExist, Gt, Lt, Equals };
