@@ -244,8 +244,8 @@ int ksg_run_score_plugin(ksg_ctx *ctx, int32_t handle, int32_t plugin, const uin
  * AddPod extensions, filtering.go:157-212 / interpodaffinity/filtering.go:75-85), on both device paths
  * (the resident pod segments, and host-staged records for nodes of more than 128 pods, more than two
  * host ports per pod, more than 8 budgets, or a "now" earlier than a bound pod's start time).
- * KSG_ENOTSUP (nothing selected; ctx->err says which): a victim that moves the pod's counts under more
- * than 8 spread constraints, required affinity terms or existing-anti-affinity topology keys.
+ * Any number of spread constraints, affinity terms and existing-anti-affinity keys the pod compiler
+ * accepts is tracked (up to 8 of each kind in registers, more in a per-node device workspace).
  * detail (may be NULL) receives NUL-terminated JSON: {"offset", "numCandidates",
  * "potential", "message", "candidates": [{"node", "numPDBViolations", "victims": [uid...]}] (listCandidates),
  * "selected": <node|null>, "victims": [uid...]}; *detail_len gets its length (KSG_ENOMEM if cap is

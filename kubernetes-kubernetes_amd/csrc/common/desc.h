@@ -312,20 +312,26 @@ struct PickOut {
   int32_t offset, unsupported, pad[2];          // unsupported: some node's PSegOut flag bit 0
   PSegOut best_out;                             // the chosen node's result (victim masks)
 };
-constexpr int kPreemptCons = 8;  // DoNotSchedule constraints / affinity terms / keys whose counts the victims may move (more: unsupported)
+// DoNotSchedule constraints / affinity terms / existing-anti keys the register-resident dry run tracks per
+// kind; a preemptor with more takes the workspace-resident one (PreemptIn::wide), up to the compile's caps
+constexpr int kPreemptCons = 8;
 // What both dry-run kernels (k_preempt_seg, k_preempt) read about the victims' effects beyond Requested:
 // their scalar resources and the PodTopologySpread / InterPodAffinity counts they move.
 struct PreemptIn {
   int32_t pts_check, ipa_check;
-  const long long* pts_mm;   // [kPreemptCons][3]: per DoNotSchedule constraint the domain minimum, its
+  const long long* pts_mm;   // [n_ptsf][3]: per DoNotSchedule constraint the domain minimum, its
                              // multiplicity and the next larger count (k_pts_minima)
-  const int32_t* ex_contrib; // [slot][kPreemptCons]: the pod's required anti-affinity terms that match the
+  const int32_t* ex_contrib; // [slot][ex_stride]: the pod's required anti-affinity terms that match the
                              // preemptor, per existing-anti key (k_preempt_terms); nullptr: none
-  const long long* aff_tot;  // [kPreemptCons]: per required affinity term of a self-matching preemptor the
+  const long long* aff_tot;  // [n_raff]: per required affinity term of a self-matching preemptor the
                              // cycle's total count over its histogram (k_aff_totals); nullptr: not needed
   // the preemptor's extended resources (PodDesc scalar order, n_scalar of them, any number):
   const int64_t* vsc;        // [slot][n_scalar]: each pod's request of them (CalculateResource), 0 rows elsewhere
   int64_t* sreq;             // [n][n_scalar]: per node, the dry run's Requested of them (the kernel's scratch)
+  // the workspace-resident dry run (PreemptWide): per node 5 wide_c + 10 wide_g words, field-major and
+  // node-minor ([field][n]); wide_c = n_ptsf, wide_g = max(n_raff, n_ranti, n_exkeys); nullptr: registers
+  long long* wide;
+  int32_t wide_c, wide_g, ex_stride, pad;
 };
 struct PreemptView {
   const PRec* seg;           // [n][kSegCap]

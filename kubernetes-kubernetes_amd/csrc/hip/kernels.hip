@@ -4468,42 +4468,98 @@ hipError_t set_diag(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL
 // clone with the victims' RemovePod / AddPod applied (podtopologyspread/filtering.go:157-212).  Every
 // victim is on node i, so only the count of node i's own domain moves; the domain minimum becomes the
 // smaller of that count and the minimum over the other domains -- what criticalPaths.update tracks
-// exactly for a sequence of updates to one domain.  InterPodAffinity counts pass through unchanged.
+// exactly for a sequence of updates to one domain.  InterPodAffinity's counts move the same way
+// (filtering.go:75-85 updateWithPod): group 0 the preemptor's required affinity terms, group 1 its required
+// anti-affinity terms, group 2 the existing-anti keys, each entry the count of node i's own domain.
+//
+// The tracked state lives in one of two stores.  PreemptRegs: up to kPreemptCons entries of each kind in
+// registers (every loop over them is unrolled, so every index is static).  PreemptWide: any count the pod
+// compiler accepts, in a per-node workspace laid out field-major and node-minor ([field][n]), so a wave's
+// lanes touch consecutive words.
+struct PreemptRegs {
+  static constexpr bool kWide = false;
+  static constexpr int kCap = kPreemptCons;
+  mutable int64_t hb_[kCap], vi_[kCap], cnt0_[kCap], dlt_[kCap], excl_[kCap], atot_[kCap];
+  mutable int32_t ihb_[3 * kCap], ivi_[3 * kCap], idl_[3 * kCap];
+  __device__ __forceinline__ void bind(const PreemptIn&, int, int) {}
+  __device__ __forceinline__ int64_t& hb(int c) const { return hb_[c]; }
+  __device__ __forceinline__ int64_t& vi(int c) const { return vi_[c]; }
+  __device__ __forceinline__ int64_t& cnt0(int c) const { return cnt0_[c]; }
+  __device__ __forceinline__ int64_t& dlt(int c) const { return dlt_[c]; }
+  __device__ __forceinline__ int64_t& excl(int c) const { return excl_[c]; }
+  __device__ __forceinline__ int64_t& atot(int k) const { return atot_[k]; }
+  __device__ __forceinline__ int32_t& ihb(int g, int k) const { return ihb_[g * kCap + k]; }
+  __device__ __forceinline__ int32_t& ivi(int g, int k) const { return ivi_[g * kCap + k]; }
+  __device__ __forceinline__ int32_t& idl(int g, int k) const { return idl_[g * kCap + k]; }
+};
+struct PreemptWide {
+  static constexpr bool kWide = true;
+  long long* w;  // this node's word of field 0
+  size_t st;     // words between fields (the node count)
+  int C, G;
+  __device__ __forceinline__ void bind(const PreemptIn& in, int i, int n) {
+    w = in.wide + i;
+    st = (size_t)n;
+    C = in.wide_c;
+    G = in.wide_g;
+  }
+  __device__ __forceinline__ int64_t& f(int k) const { return *reinterpret_cast<int64_t*>(w + (size_t)k * st); }
+  __device__ __forceinline__ int64_t& hb(int c) const { return f(c); }
+  __device__ __forceinline__ int64_t& vi(int c) const { return f(C + c); }
+  __device__ __forceinline__ int64_t& cnt0(int c) const { return f(2 * C + c); }
+  __device__ __forceinline__ int64_t& dlt(int c) const { return f(3 * C + c); }
+  __device__ __forceinline__ int64_t& excl(int c) const { return f(4 * C + c); }
+  __device__ __forceinline__ int64_t& atot(int k) const { return f(5 * C + k); }
+  __device__ __forceinline__ int64_t& ihb(int g, int k) const { return f(5 * C + G + g * G + k); }
+  __device__ __forceinline__ int64_t& ivi(int g, int k) const { return f(5 * C + 4 * G + g * G + k); }
+  __device__ __forceinline__ int64_t& idl(int g, int k) const { return f(5 * C + 7 * G + g * G + k); }
+};
+// f(k) for k < n: a plain loop over the workspace, an unrolled guarded one over the registers
+template <class S, class F>
+__device__ __forceinline__ void each_k(int n, F&& f) {
+  if constexpr (S::kWide) {
+    for (int k = 0; k < n; ++k) f(k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < S::kCap; ++k)
+      if (k < n) f(k);
+  }
+}
+template <class S>
 struct PreemptTopo {
   ArenaTopo a;
-  int64_t hb[kPreemptCons];    // constraint c's histogram base, -1 unused
-  int64_t vi[kPreemptCons];    // node i's domain value under constraint c
-  int64_t cnt0[kPreemptCons];  // its cycle count
-  int64_t dlt[kPreemptCons];   // + reprieved - removed victims that constraint c counts
-  int64_t excl[kPreemptCons];  // minimum over the other domains
-  // InterPodAffinity (filtering.go:75-85 updateWithPod): [0, 4) the preemptor's required affinity terms,
-  // [4, 8) its required anti-affinity terms, [8, 12) the existing-anti keys; each moves the count of node
-  // i's own domain (its value of the term's key)
-  int32_t ihb[3 * kPreemptCons], ivi[3 * kPreemptCons];
-  int32_t idl[3 * kPreemptCons];
+  S s;
+  int32_t nc;     // DoNotSchedule constraints (an entry with hb < 0: node i is not eligible for it)
+  int32_t ng[3];  // entries per InterPodAffinity group
   // a preemptor matching its own required affinity terms (filtering.go:404-415): whether affinityCounts is
   // empty depends on every count, not only node i's -- the cycle's total per term (atot) with the victims'
   // deltas at node i's domains; nra < 0: not tracked (the cycle's bit)
-  int64_t atot[kPreemptCons];
   int32_t nra;
   __device__ __forceinline__ int64_t cnt(int32_t hist_base, int32_t lref, int32_t v, int ls) const {
     int64_t x = a.cnt(hist_base, lref, v, ls);
+    each_k<S>(nc, [&](int c) {
+      if (s.hb(c) == hist_base && s.vi(c) == v) x += s.dlt(c);
+    });
 #pragma unroll
-    for (int c = 0; c < kPreemptCons; ++c)
-      if (hb[c] == hist_base && vi[c] == v) x += dlt[c];
-#pragma unroll
-    for (int k = 0; k < 3 * kPreemptCons; ++k)
-      if (ihb[k] == hist_base && ivi[k] == v) x += idl[k];
+    for (int g = 0; g < 3; ++g)
+      each_k<S>(ng[g], [&](int k) {
+        if (s.ihb(g, k) == hist_base && s.ivi(g, k) == v) x += s.idl(g, k);
+      });
     return x;
   }
   __device__ __forceinline__ int64_t pmin(int c) const {
     int64_t r = a.pmin(c);
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k)
-      if (k == c && hb[k] >= 0) {
-        const int64_t own = cnt0[k] + dlt[k];
-        r = own < excl[k] ? own : excl[k];
-      }
+    auto own = [&](int k) {
+      const int64_t o = s.cnt0(k) + s.dlt(k);
+      r = o < s.excl(k) ? o : s.excl(k);
+    };
+    if constexpr (S::kWide) {
+      if (c < nc && s.hb(c) >= 0) own(c);
+    } else {
+      each_k<S>(nc, [&](int k) {
+        if (k == c && s.hb(k) >= 0) own(k);
+      });
+    }
     return r;
   }
   __device__ __forceinline__ uint32_t pndom(int c) const { return a.pndom(c); }
@@ -4511,20 +4567,18 @@ struct PreemptTopo {
     const uint32_t a0 = a.any();
     if (nra < 0) return a0;
     bool nonempty = false;  // affinityCounts after the removals / reprieves: some term's total is not 0
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k) {
-      if (k >= nra) continue;
-      int64_t x = atot[k];
-#pragma unroll
-      for (int j = 0; j < kPreemptCons; ++j)
-        if (j < nra && ihb[j] == ihb[k] && ivi[j] >= 0) x += idl[j];
+    each_k<S>(nra, [&](int k) {
+      int64_t x = s.atot(k);
+      each_k<S>(nra, [&](int j) {
+        if (s.ihb(0, j) == s.ihb(0, k) && s.ivi(0, j) >= 0) x += s.idl(0, j);
+      });
       nonempty |= x != 0;
-    }
+    });
     return (a0 & ~1u) | (nonempty ? 1u : 0u);
   }
 };
 
-// Per required affinity term of the preemptor (at most kPreemptCons): the cycle's total count over the term's
+// Per required affinity term of the preemptor: the cycle's total count over the term's
 // histogram (k_aggregate's arena) -- whether affinityCounts is empty once victims are removed (PreemptTopo::any).
 __global__ __launch_bounds__(kBlock) void k_aff_totals(BatchView b, int pod, long long* out) {
   const uint8_t* base = b.descs + b.desc_off[pod];
@@ -4609,8 +4663,7 @@ hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* 
 // The existing pods' required anti-affinity terms that match the preemptor (the term role of k_aggregate,
 // AffinityTerm.Matches, types.go:391-396), counted per owning pod-table slot and existing-anti key: what a
 // victim's RemovePod takes out of existingAntiAffinityCounts at its node (filtering.go:75-85).
-__global__ __launch_bounds__(kBlock) void k_preempt_terms(MirrorView m, BatchView b, int pod, int32_t* contrib,
-                                                          uint32_t* unsup) {
+__global__ __launch_bounds__(kBlock) void k_preempt_terms(MirrorView m, BatchView b, int pod, int32_t* contrib) {
   const int j = (int)blockIdx.x * kBlock + (int)threadIdx.x;
   if (j >= m.n_terms) return;
   const uint8_t* base = b.descs + b.desc_off[pod];
@@ -4629,16 +4682,13 @@ __global__ __launch_bounds__(kBlock) void k_preempt_terms(MirrorView m, BatchVie
   const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
   for (int e = 0; e < d.n_exkeys; ++e)
     if (ek[e].base == hb) {
-      if (e < kPreemptCons) atomicAdd(&contrib[(size_t)t.owner * kPreemptCons + e], 1);
-      else atomicOr(unsup, 1u);
+      atomicAdd(&contrib[(size_t)t.owner * (size_t)d.n_exkeys + e], 1);
       return;
     }
 }
-hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, uint32_t* unsup,
-                                hipStream_t s) {
+hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, hipStream_t s) {
   if (m.n_terms <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_preempt_terms, dim3((m.n_terms + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, b, pod,
-                     contrib, unsup);
+  hipLaunchKernelGGL(k_preempt_terms, dim3((m.n_terms + kBlock - 1) / kBlock), dim3(kBlock), 0, s, m, b, pod, contrib);
   return hipGetLastError();
 }
 
@@ -4684,127 +4734,122 @@ __device__ __forceinline__ uint32_t preempt_node_filters(const MirrorView& m, co
 }
 
 // The victims' topology effects at node i, as both dry-run kernels track them
+template <class S>
 struct TopoTrack {
-  PreemptTopo tp;
-  uint32_t elig;        // DoNotSchedule constraints node i is eligible for (pts_eligible)
-  int nra, nrn, nex;    // the preemptor's required affinity / anti-affinity terms, existing-anti keys tracked
-  bool pts_over;        // more DoNotSchedule constraints than PreemptTopo tracks
+  PreemptTopo<S> tp;
+  uint32_t elig;  // DoNotSchedule constraints node i is eligible for (pts_eligible)
 };
+template <class S>
 __device__ __forceinline__ void topo_track_init(const MirrorView& m, const BatchView& b, int pod, const uint8_t* base,
-                                                const PodDesc& d, int i, const PreemptIn& in, TopoTrack& T,
+                                                const PodDesc& d, int i, const PreemptIn& in, TopoTrack<S>& T,
                                                 uint32_t* flags) {
-  PreemptTopo& tp = T.tp;
+  PreemptTopo<S>& tp = T.tp;
+  const S& st = tp.s;
   tp.a = ArenaTopo{b.stats + pod, b.arena};
-#pragma unroll
-  for (int c = 0; c < kPreemptCons; ++c) tp.hb[c] = tp.vi[c] = -1, tp.cnt0[c] = tp.dlt[c] = tp.excl[c] = 0;
+  tp.s.bind(in, i, m.n);
   const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
-  T.elig = 0;
-  T.pts_over = in.pts_check && d.n_ptsf > kPreemptCons;
-  if (in.pts_check && !T.pts_over) {
-    T.elig = pts_eligible(m, base, d, cs, d.n_ptsf, i);
-#pragma unroll
-    for (int c = 0; c < kPreemptCons; ++c)
-      if (c < d.n_ptsf && ((T.elig >> c) & 1u)) {
-        const int32_t v = node_label(m, cs[c].slot, i);
-        tp.hb[c] = cs[c].hist_base;
-        tp.vi[c] = v;
-        tp.cnt0[c] = (int64_t)b.arena[cs[c].hist_base + v];
-        const long long* mm = in.pts_mm + 3 * c;
-        tp.excl[c] = (tp.cnt0[c] == mm[0] && mm[1] == 1) ? mm[2] : mm[0];
-      }
+  tp.nc = in.pts_check ? d.n_ptsf : 0;
+  tp.ng[0] = in.ipa_check ? d.n_raff : 0;
+  tp.ng[1] = in.ipa_check ? d.n_ranti : 0;
+  tp.ng[2] = (in.ipa_check && in.ex_contrib) ? d.n_exkeys : 0;
+  if constexpr (!S::kWide) {
+    // the host sends a preemptor beyond the registers to the workspace-resident dry run; a mismatch is an
+    // internal error the pick reports (PSegOut flag bit 0), never a wrong result
+    if (tp.nc > S::kCap || tp.ng[0] > S::kCap || tp.ng[1] > S::kCap || tp.ng[2] > S::kCap) {
+      *flags |= 1u;
+      tp.nc = tp.ng[0] = tp.ng[1] = tp.ng[2] = 0;
+    }
   }
-#pragma unroll
-  for (int k = 0; k < 3 * kPreemptCons; ++k) tp.ihb[k] = tp.ivi[k] = -1, tp.idl[k] = 0;
+  T.elig = tp.nc ? pts_eligible(m, base, d, cs, d.n_ptsf, i) : 0u;
+  each_k<S>(tp.nc, [&](int c) {
+    st.hb(c) = st.vi(c) = -1;
+    st.cnt0(c) = st.dlt(c) = st.excl(c) = 0;
+    if ((T.elig >> c) & 1u) {
+      const int32_t v = node_label(m, cs[c].slot, i);
+      st.hb(c) = cs[c].hist_base;
+      st.vi(c) = v;
+      st.cnt0(c) = (int64_t)b.arena[cs[c].hist_base + v];
+      const long long* mm = in.pts_mm + 3 * c;
+      st.excl(c) = (st.cnt0(c) == mm[0] && mm[1] == 1) ? mm[2] : mm[0];
+    }
+  });
   const IpaTerm* raff = at<IpaTerm>(base, d.raff_off);
   const IpaTerm* ranti = at<IpaTerm>(base, d.ranti_off);
   const KeyHist* ek = at<KeyHist>(base, d.exkeys_off);
-  T.nra = in.ipa_check ? d.n_raff : 0;
-  T.nrn = in.ipa_check ? d.n_ranti : 0;
-  T.nex = (in.ipa_check && in.ex_contrib) ? d.n_exkeys : 0;
+  each_k<S>(tp.ng[0], [&](int k) {
+    st.ihb(0, k) = raff[k].hist_base;
+    st.ivi(0, k) = node_label(m, raff[k].slot, i);
+    st.idl(0, k) = 0;
+  });
+  each_k<S>(tp.ng[1], [&](int k) {
+    st.ihb(1, k) = ranti[k].hist_base;
+    st.ivi(1, k) = node_label(m, ranti[k].slot, i);
+    st.idl(1, k) = 0;
+  });
+  each_k<S>(tp.ng[2], [&](int k) {
+    st.ihb(2, k) = ek[k].base;
+    st.ivi(2, k) = node_label(m, ek[k].slot, i);
+    st.idl(2, k) = 0;
+  });
   tp.nra = -1;
-  if (in.ipa_check && in.aff_tot && (d.ipa_flags & IPA_SELF_ALL) && T.nra <= kPreemptCons) {
-    tp.nra = T.nra;
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k) tp.atot[k] = k < T.nra ? (int64_t)in.aff_tot[k] : 0;
-  }
-  if (in.ipa_check) {
-    if (T.nra > kPreemptCons || T.nrn > kPreemptCons || T.nex > kPreemptCons) *flags |= 1u;  // beyond PreemptTopo
-#pragma unroll
-    for (int k = 0; k < kPreemptCons; ++k) {
-      if (k < T.nra) {
-        tp.ihb[k] = raff[k].hist_base;
-        tp.ivi[k] = node_label(m, raff[k].slot, i);
-      }
-      if (k < T.nrn) {
-        tp.ihb[kPreemptCons + k] = ranti[k].hist_base;
-        tp.ivi[kPreemptCons + k] = node_label(m, ranti[k].slot, i);
-      }
-      if (k < T.nex) {
-        tp.ihb[2 * kPreemptCons + k] = ek[k].base;
-        tp.ivi[2 * kPreemptCons + k] = node_label(m, ek[k].slot, i);
-      }
-    }
+  if (in.ipa_check && in.aff_tot && (d.ipa_flags & IPA_SELF_ALL)) {
+    tp.nra = tp.ng[0];
+    each_k<S>(tp.nra, [&](int k) { st.atot(k) = (int64_t)in.aff_tot[k]; });
   }
 }
-// The DoNotSchedule constraints whose count the victim in pod-table slot `slot` is part of (updateWithPod,
-// podtopologyspread/filtering.go:181-212): a victim in the preemptor's namespace that matches the constraint's
-// selector, at a node eligible for it.  Beyond kPreemptCons constraints a counted victim is unsupported.
-__device__ __forceinline__ uint32_t topo_counts(const MirrorView& m, const uint8_t* base, const PodDesc& d,
-                                                const TopoTrack& T, int32_t slot, uint32_t* flags) {
-  if (!T.elig && !T.pts_over) return 0u;
-  if (m.pod_ns[slot] != d.ns_id) return 0u;
-  const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
-  const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
-  const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
-  const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
-  if (T.pts_over) {
-    for (int32_t c = 0; c < d.n_ptsf; ++c)
-      if (lsel_match(sp + cs[c].sel, lb, ln)) *flags |= 1u;
-    return 0u;
-  }
-  uint32_t bits = 0;
-#pragma unroll
-  for (int c = 0; c < kPreemptCons; ++c)
-    if (((T.elig >> c) & 1u) && lsel_match(sp + cs[c].sel, lb, ln)) bits |= 1u << c;
-  return bits;
-}
-// The victim's InterPodAffinity effect (filtering.go:75-85), applied to x with sign sg: the preemptor's
-// affinity terms count it when it matches all of them, its anti-affinity terms each when it matches, and
-// its own required anti-affinity terms that match the preemptor count at their keys; false: no count moves
-__device__ __forceinline__ bool topo_ipa(const MirrorView& m, const uint8_t* base, const PodDesc& d, const TopoTrack& T,
-                                         const PreemptIn& in, int32_t slot, PreemptTopo& x, int sg) {
-  if (!in.ipa_check || (T.nra == 0 && T.nrn == 0 && T.nex == 0)) return false;
+// The victim in pod-table slot `slot` removed (sg = -1) or added back (+1) at node i; false: no count moves.
+// PodTopologySpread (updateWithPod, podtopologyspread/filtering.go:181-212): a victim in the preemptor's
+// namespace that matches a DoNotSchedule constraint's selector, at a node eligible for it.
+// InterPodAffinity (filtering.go:75-85): the preemptor's affinity terms count it when it matches all of
+// them, its anti-affinity terms each when it matches, and its own required anti-affinity terms that match
+// the preemptor count at their keys.  (A preemptor matching its own terms: affinityCounts emptied by the
+// removal flips the "no pod matches anywhere" rule, filtering.go:404-415 -- PreemptTopo::any.)
+template <class S>
+__device__ __forceinline__ bool topo_victim(const MirrorView& m, const uint8_t* base, const PodDesc& d,
+                                            const PreemptIn& in, TopoTrack<S>& T, int32_t slot, int sg) {
+  const S& st = T.tp.s;
   const int32_t ns = m.pod_ns[slot];
   const unsigned long long* lb = m.lbl_pool + m.pod_lbl_off[slot];
   const int32_t ln = (int32_t)m.pod_lbl_cnt[slot];
   const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
+  bool moved = false;
+  if (T.elig && ns == d.ns_id) {
+    const PtsCons* cs = at<PtsCons>(base, d.ptsf_off);
+    each_k<S>(T.tp.nc, [&](int c) {
+      if (((T.elig >> c) & 1u) && lsel_match(sp + cs[c].sel, lb, ln)) {
+        st.dlt(c) += sg;
+        moved = true;
+      }
+    });
+  }
+  const int nra = T.tp.ng[0], nrn = T.tp.ng[1], nex = T.tp.ng[2];
+  if (nra == 0 && nrn == 0 && nex == 0) return moved;
   const IpaTerm* raff = at<IpaTerm>(base, d.raff_off);
   const IpaTerm* ranti = at<IpaTerm>(base, d.ranti_off);
-  bool moved = false;
-  bool all = T.nra > 0;
-#pragma unroll
-  for (int k = 0; k < kPreemptCons; ++k)
-    if (k < T.nra) all = all && term_matches_pod(sp, raff[k], ns, lb, ln);
-#pragma unroll
-  for (int k = 0; k < kPreemptCons; ++k) {
-    if (all && k < T.nra && T.tp.ivi[k] >= 0) {
-      x.idl[k] += sg;
+  bool all = nra > 0;
+  each_k<S>(nra, [&](int k) { all = all && term_matches_pod(sp, raff[k], ns, lb, ln); });
+  if (all)
+    each_k<S>(nra, [&](int k) {
+      if (st.ivi(0, k) >= 0) {
+        st.idl(0, k) += sg;
+        moved = true;
+      }
+    });
+  each_k<S>(nrn, [&](int k) {
+    if (st.ivi(1, k) >= 0 && term_matches_pod(sp, ranti[k], ns, lb, ln)) {
+      st.idl(1, k) += sg;
       moved = true;
     }
-    if (k < T.nrn && T.tp.ivi[kPreemptCons + k] >= 0 && term_matches_pod(sp, ranti[k], ns, lb, ln)) {
-      x.idl[kPreemptCons + k] += sg;
-      moved = true;
-    }
-    if (k < T.nex && T.tp.ivi[2 * kPreemptCons + k] >= 0) {
-      const int32_t cn = in.ex_contrib[(size_t)slot * kPreemptCons + k];
+  });
+  each_k<S>(nex, [&](int k) {
+    if (st.ivi(2, k) >= 0) {
+      const int32_t cn = in.ex_contrib[(size_t)slot * in.ex_stride + k];
       if (cn) {
-        x.idl[2 * kPreemptCons + k] += sg * cn;
+        st.idl(2, k) += sg * cn;
         moved = true;
       }
     }
-  }
-  // (a preemptor matching its own terms: affinityCounts emptied by the removal flips the "no pod matches
-  // anywhere" rule, filtering.go:404-415 -- PreemptTopo::any from the totals and these deltas)
+  });
   return moved;
 }
 // the node's Requested of the preemptor's extended resources, in its scratch row (nullptr: none)
@@ -4818,6 +4863,7 @@ __device__ __forceinline__ int64_t* preempt_sreq(const MirrorView& m, const uint
 }
 
 // Host-staged victims (PNode / PVictim: the host sorted them and grouped them by PDB violation)
+template <class S>
 __global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, int pod, const PNode* pn,
                                                     const PVictim* pv, uint8_t* vout, POut* out, int all_nodes,
                                                     PreemptIn in) {
@@ -4847,7 +4893,7 @@ __global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, i
   NodeCore nc = load_core(m, i);
   int64_t* sreq = preempt_sreq(m, base, d, in, i);
   const int ns = d.n_scalar;
-  TopoTrack T;
+  TopoTrack<S> T;
   topo_track_init(m, b, pod, base, d, i, in, T, &o.flags);
   const PVictim* v = pv + nd.voff;
   bool moves = false;  // some victim moves a topology count: the topology filters re-run on every reprieve
@@ -4857,11 +4903,7 @@ __global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, i
     nc.reph -= v[q].eph;
     if (sreq)
       for (int k = 0; k < ns; ++k) sreq[k] -= in.vsc[(size_t)v[q].slot * ns + k];
-    const uint32_t kb = topo_counts(m, base, d, T, v[q].slot, &o.flags);
-#pragma unroll
-    for (int c = 0; c < kPreemptCons; ++c) T.tp.dlt[c] -= (kb >> c) & 1u;
-    moves |= kb != 0;
-    moves |= topo_ipa(m, base, d, T, in, v[q].slot, T.tp, -1);
+    moves |= topo_victim(m, base, d, in, T, v[q].slot, -1);
   }
   nc.npods -= nd.vcnt;
   bool port = (nd.flags & PN_BASE_PORT) != 0;
@@ -4878,21 +4920,18 @@ __global__ __launch_bounds__(kBlock) void k_preempt(MirrorView m, BatchView b, i
       t.npods += 1;
       const int64_t* add = sreq ? in.vsc + (size_t)x.slot * ns : nullptr;
       const bool tpo = port || (x.flags & PV_PORT) != 0;
-      const uint32_t kb = moves ? topo_counts(m, base, d, T, x.slot, &o.flags) : 0u;
-      PreemptTopo tt = T.tp;
-#pragma unroll
-      for (int c = 0; c < kPreemptCons; ++c) tt.dlt[c] += (kb >> c) & 1u;
-      const bool im = moves && topo_ipa(m, base, d, T, in, x.slot, tt, +1);
+      // tried back: the counts move now and move back if the preemptor no longer fits
+      const bool mv = moves && topo_victim(m, base, d, in, T, x.slot, +1);
       bool fits = preempt_node_filters(m, t, sreq, add, base, d, i, tpo) == 0;
-      if (fits && (kb || im)) fits = topo_filters(m, base, d, i, tt, 0) == 0;
+      if (fits && mv) fits = topo_filters(m, base, d, i, T.tp, 0) == 0;
       if (fits) {
         nc = t;
         if (sreq)
           for (int k = 0; k < ns; ++k) sreq[k] += add[k];
         port = tpo;
-        T.tp = tt;
         vout[nd.voff + q] = 0;
       } else {
+        if (mv) topo_victim(m, base, d, in, T, x.slot, -1);
         vout[nd.voff + q] = 1;
         o.nvictims += 1;
         o.nviolating += (x.flags & PV_VIOL) ? 1 : 0;
@@ -4906,7 +4945,10 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
                           uint8_t* vout, POut* out, int all_nodes, const PreemptIn& in, hipStream_t s) {
   const int nb = (m.n + kBlock - 1) / kBlock;
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_preempt, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pn, pv, vout, out, all_nodes, in);
+  if (in.wide)
+    hipLaunchKernelGGL(k_preempt<PreemptWide>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pn, pv, vout, out, all_nodes, in);
+  else
+    hipLaunchKernelGGL(k_preempt<PreemptRegs>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pn, pv, vout, out, all_nodes, in);
   return hipGetLastError();
 }
 
@@ -4915,6 +4957,7 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
 // victims (the segment suffix below the preemptor's priority), filterPodsWithPDBViolation
 // (default_preemption.go:406-452: selector programs against the pod table's labels, budgets in
 // registers), the victims' host-port conflicts and the node's remaining conflicting ports.
+template <class S>
 __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView b, int pod, PreemptView pv) {
   const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
   if (i >= m.n) return;
@@ -4947,7 +4990,7 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
     return;
   }
   const PreemptIn& in = pv.in;
-  TopoTrack T;
+  TopoTrack<S> T;
   topo_track_init(m, b, pod, base, d, i, in, T, &o.flags);
   const int ns = d.n_scalar;
   // filterPodsWithPDBViolation over the importance-ordered potential victims
@@ -4999,11 +5042,7 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
     nc.reph -= r[q].eph;
     if (const int64_t* a = vsc(r[q]))
       for (int k = 0; k < ns; ++k) sreq[k] -= a[k];
-    const uint32_t k = topo_counts(m, base, d, T, r[q].slot, &o.flags);
-#pragma unroll
-    for (int c = 0; c < kPreemptCons; ++c) T.tp.dlt[c] -= (k >> c) & 1u;
-    moves |= k != 0;
-    moves |= topo_ipa(m, base, d, T, in, r[q].slot, T.tp, -1);
+    moves |= topo_victim(m, base, d, in, T, r[q].slot, -1);
   }
   nc.npods -= cnt - first;
   uint32_t st = preempt_node_filters(m, nc, sreq, nullptr, base, d, i, port);
@@ -5023,20 +5062,16 @@ __global__ __launch_bounds__(kBlock) void k_preempt_seg(MirrorView m, BatchView 
         t.npods += 1;
         const int64_t* add = vsc(x);
         const bool tpo = port || conf(x.port[0]) || conf(x.port[1]);
-        const uint32_t k = moves ? topo_counts(m, base, d, T, x.slot, &o.flags) : 0u;
-        PreemptTopo tt = T.tp;
-#pragma unroll
-        for (int c = 0; c < kPreemptCons; ++c) tt.dlt[c] += (k >> c) & 1u;
-        const bool im = moves && topo_ipa(m, base, d, T, in, x.slot, tt, +1);
+        const bool mv = moves && topo_victim(m, base, d, in, T, x.slot, +1);
         bool fits = preempt_node_filters(m, t, sreq, add, base, d, i, tpo) == 0;
-        if (fits && (k || im)) fits = topo_filters(m, base, d, i, tt, 0) == 0;
+        if (fits && mv) fits = topo_filters(m, base, d, i, T.tp, 0) == 0;
         if (fits) {
           nc = t;
           if (add)
             for (int kk = 0; kk < ns; ++kk) sreq[kk] += add[kk];
           port = tpo;
-          T.tp = tt;
         } else {
+          if (mv) topo_victim(m, base, d, in, T, x.slot, -1);
           (q < 64 ? vm0 : vm1) |= 1ull << (q & 63);
           o.nvictims += 1;
           if (isv) {
@@ -5233,7 +5268,10 @@ hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_
 hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s) {
   const int nb = (m.n + kBlock - 1) / kBlock;
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_preempt_seg, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pv);
+  if (pv.in.wide)
+    hipLaunchKernelGGL(k_preempt_seg<PreemptWide>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pv);
+  else
+    hipLaunchKernelGGL(k_preempt_seg<PreemptRegs>, dim3(nb), dim3(kBlock), 0, s, m, b, pod, pv);
   return hipGetLastError();
 }
 

@@ -637,7 +637,7 @@ class Engine {
   DevBuf d_aspill;           // k_agg_loop: workgroup pod / term lists past the LDS ones (AggView::spill)
   DevBuf d_pre;              // k_preempt: per-node records, victims, per-node results, victim flags
   // k_preempt_seg: every node's pods as an importance-ordered segment (host copy + identities)
-  DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick, d_contrib_buf;
+  DevBuf d_seg, d_segcnt, d_psout, d_pdb, d_pick, d_contrib_buf, d_wide;
   DevBuf d_vsc;  // preemption: the pods' requests of the preemptor's extended resources + the per-node scratch
   std::vector<PRec> h_seg;
   std::vector<int32_t> h_segcnt;

@@ -33,8 +33,7 @@ hipError_t launch_preempt(const MirrorView& m, const BatchView& b, int pod, cons
 hipError_t launch_preempt_seg(const MirrorView& m, const BatchView& b, int pod, const PreemptView& pv, hipStream_t s);
 hipError_t launch_pts_minima(const BatchView& b, int pod, int ncons, long long* mm, hipStream_t s);
 hipError_t launch_aff_totals(const BatchView& b, int pod, int nterms, long long* out, hipStream_t s);
-hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, uint32_t* unsup,
-                                hipStream_t s);
+hipError_t launch_preempt_terms(const MirrorView& m, const BatchView& b, int pod, int32_t* contrib, hipStream_t s);
 hipError_t launch_preempt_pick(const PSegOut* out, int n, int64_t offset, int64_t pct, int64_t absn, int32_t* pot,
                                PickOut* res, hipStream_t s);
 
@@ -252,7 +251,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   // ---- DefaultPreemptionArgs + the call's inputs (validation_pluginargs.go:113-125)
   int64_t offset_in = 0, now = 0;
   int32_t pct = 10, absn = 100;
-  bool all_nodes = false, staged = false, list = false;
+  bool all_nodes = false, staged = false, list = false, force_wide = false;
   std::vector<Pdb> pdbs;
   try {
     JDoc d(args_json && args_len ? args_json : "{}", args_json && args_len ? args_len : 2);
@@ -267,6 +266,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
     absn = (int32_t)d.num(r, "minCandidateNodesAbsolute", 100);
     all_nodes = d.boolean(r, "allNodes");
     staged = d.boolean(r, "debugHostStaged");  // diagnostic: force the host-staged victim records
+    force_wide = d.boolean(r, "debugWideDryRun");  // diagnostic: the workspace-resident dry run at any size
     list = d.boolean(r, "listCandidates");      // detail lists every DryRunPreemption candidate
     d.each(d.get(r, "pdbs"), [&](const JVal& v) {
       Pdb b;
@@ -356,29 +356,39 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
   // the self-matching affinity totals, the existing anti-affinity terms per victim slot, and the victims'
   // requests of the preemptor's extended resources; d_pdb's head holds the minima and totals
   PreemptIn pin{};
+  const size_t mm_words = 3 * (size_t)D.n_ptsf + (size_t)D.n_raff;
   auto topo_prelude = [&]() -> int {
-    const size_t mm_b = 8 * 4 * kPreemptCons;  // k_pts_minima's [3 kPreemptCons], then k_aff_totals' [kPreemptCons]
-    if ((rc = ensure(d_pdb, mm_b + 64))) return rc;
+    // d_pdb's head: k_pts_minima's [3 n_ptsf], then k_aff_totals' [n_raff] (mm_words)
+    if ((rc = ensure(d_pdb, 8 * mm_words + 64))) return rc;
     long long* d_mm = (long long*)d_pdb.p;
-    const bool pts_minima = pts_on && D.n_ptsf <= kPreemptCons;
-    if (pts_minima) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
+    if (pts_on) PCHK(launch_pts_minima(bv, 0, D.n_ptsf, d_mm, s));
     // a preemptor matching its own required affinity terms: the cycle's per-term totals (PreemptTopo::any)
-    const bool aff_tot = ipa_on && (D.ipa_flags & IPA_SELF_ALL) && D.n_raff > 0 && D.n_raff <= kPreemptCons;
-    if (aff_tot) PCHK(launch_aff_totals(bv, 0, D.n_raff, d_mm + 3 * kPreemptCons, s));
+    const bool aff_tot = ipa_on && (D.ipa_flags & IPA_SELF_ALL) && D.n_raff > 0;
+    if (aff_tot) PCHK(launch_aff_totals(bv, 0, D.n_raff, d_mm + 3 * D.n_ptsf, s));
     // existing pods' required anti-affinity terms matching the preemptor, per slot and key
     const bool terms = ipa_on && D.n_exkeys > 0 && m.n_terms > 0;
     if (terms) {
-      const size_t cb = sizeof(int32_t) * kPreemptCons * (size_t)std::max(m.pods_hw, 1);
+      const size_t cb = sizeof(int32_t) * (size_t)D.n_exkeys * (size_t)std::max(m.pods_hw, 1);
       if ((rc = ensure(d_contrib_buf, cb + 64))) return rc;
-      PCHK(hipMemsetAsync(d_contrib_buf.p, 0, cb + 4, s));
-      // (a term beyond kPreemptCons keys also has n_exkeys > kPreemptCons, so the dry run flags every node:
-      // it counts only where the dry run reaches, at or before its cut)
-      PCHK(launch_preempt_terms(m, bv, 0, (int32_t*)d_contrib_buf.p, (uint32_t*)((uint8_t*)d_contrib_buf.p + cb), s));
+      PCHK(hipMemsetAsync(d_contrib_buf.p, 0, cb, s));
+      PCHK(launch_preempt_terms(m, bv, 0, (int32_t*)d_contrib_buf.p, s));
     }
+    // more DoNotSchedule constraints, affinity terms or existing-anti keys than the registers hold: the
+    // dry run keeps its per-node counts in a workspace (PreemptWide)
+    const int32_t wc = pts_on ? D.n_ptsf : 0;
+    const int32_t wg = ipa_on ? std::max(D.n_raff, std::max(D.n_ranti, D.n_exkeys)) : 0;
+    if (force_wide || wc > kPreemptCons || wg > kPreemptCons) {
+      const size_t wb = 8 * (size_t)std::max(5 * wc + 10 * wg, 1) * (size_t)std::max(std::max(N, m.n), 1);
+      if ((rc = ensure(d_wide, wb + 64))) return rc;
+      pin.wide = (long long*)d_wide.p;
+      pin.wide_c = wc;
+      pin.wide_g = wg;
+    }
+    pin.ex_stride = D.n_exkeys;
     pin.pts_check = pts_on ? 1 : 0;
     pin.ipa_check = ipa_on ? 1 : 0;
     pin.pts_mm = d_mm;
-    pin.aff_tot = aff_tot ? d_mm + 3 * kPreemptCons : nullptr;
+    pin.aff_tot = aff_tot ? d_mm + 3 * D.n_ptsf : nullptr;
     pin.ex_contrib = terms ? (const int32_t*)d_contrib_buf.p : nullptr;
     if (D.n_scalar > 0 && N > 0) {
       // each pod's request of the preemptor's extended resources, by pod-table slot (only pods that request
@@ -428,7 +438,7 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
           if (pdbs[k].disrupted.count(kv.second.name)) dis[kv.second.slot] |= (uint8_t)(1u << k);
     }
     if ((rc = stage_pod())) return rc;
-    const size_t mm_b = 8 * 4 * kPreemptCons;  // the prelude's minima and totals, then the budgets
+    const size_t mm_b = (8 * mm_words + 63) & ~(size_t)63;  // the prelude's minima and totals, then the budgets
     const size_t pd_b = sizeof(PdbDev) * pd.size(), pool_b = 4 * pool.size(), dis_b = dis.size();
     if ((rc = ensure(d_pdb, mm_b + pd_b + pool_b + dis_b + 64))) return rc;
     if ((rc = topo_prelude())) return rc;
@@ -459,10 +469,9 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       PCHK(hipMemcpyAsync(so.data(), d_psout.p, sizeof(PSegOut) * (size_t)N, hipMemcpyDeviceToHost, s));
     }
     if ((rc = finish_device())) return rc;
-    if (pick.unsupported) {
-      c->err = "preemption: a victim's effect on the pod's PodTopologySpread / InterPodAffinity counts is outside "
-               "what the device tracks (more than 8 constraints, terms or keys)";
-      return KSG_ENOTSUP;
+    if (pick.unsupported) {  // the register dry run met more entries than it holds: a host sizing bug
+      c->err = "preemption: internal error (dry-run store smaller than the preemptor's constraints)";
+      return KSG_EDEVICE;
     }
     for (int32_t i = 0; list && i < N; ++i) po[i] = NodeOut{so[i].st, so[i].nvictims, so[i].nviolating, so[i].flags};
   } else {
@@ -583,9 +592,8 @@ int Engine::preempt(const PodSpec& p, const char* args_json, size_t args_len, ks
       if (!nv.empty() && (int32_t)(nv.size() + vl.size()) >= ncand) break;
     }
     if (unsup && !seg) {
-      c->err = "preemption: a victim's effect on the pod's PodTopologySpread / InterPodAffinity counts is outside "
-               "what the device tracks (more than 8 constraints, terms or keys)";
-      return KSG_ENOTSUP;
+      c->err = "preemption: internal error (dry-run store smaller than the preemptor's constraints)";
+      return KSG_EDEVICE;
     }
   }
   std::vector<Cand> cands = nv;

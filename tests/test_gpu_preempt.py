@@ -97,10 +97,12 @@ def cluster(seed, n_nodes, per_node):
 
 def compare(dev, orc, pod, args):
     """Both device paths (the device-resident pod segments, and host-staged records via the
-    debugHostStaged diagnostic) against the oracle."""
+    debugHostStaged diagnostic), each with both dry-run stores (registers, and the per-node workspace
+    via debugWideDryRun), against the oracle."""
     args = dict(args, listCandidates=True)
     r2, d2 = orc.preempt(orc.compile(pod), args)
-    for extra in ({}, {"debugHostStaged": True}):
+    for extra in ({}, {"debugHostStaged": True}, {"debugWideDryRun": True},
+                  {"debugHostStaged": True, "debugWideDryRun": True}):
         r1, d1 = dev.preempt(dev.compile(pod), dict(args, **extra))
         assert r1.as_tuple() == r2.as_tuple(), (extra, r1.as_tuple(), r2.as_tuple(), d1, d2)
         assert d1 == d2, extra
@@ -351,6 +353,74 @@ def test_preempt_many_extended_resources(native, seed):
                 {"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "DoNotSchedule",
                  "labelSelector": {"matchLabels": {"app": rng.choice(["a", "b"])}}}]
         args = {"offset": rng.randrange(1000), "now": 1704153600 * 10 ** 9, "allNodes": rng.random() < 0.3,
+                "minCandidateNodesPercentage": 100, "minCandidateNodesAbsolute": 100}
+        r, _ = compare(dev, orc, pod, args)
+        found += r.status == 0
+    assert found > 0
+
+
+def many_keys_cluster(seed, n_nodes):
+    """Nodes labelled with 14 topology keys: 7 coarse ones (2-3 values, many nodes per domain) and 7 fine
+    ones (a value per pair of nodes); existing pods carry required anti-affinity terms over many distinct
+    keys, so the preemptor's existing-anti keys exceed the register store."""
+    rng = random.Random(seed)
+    coarse = [f"topo.example/c{k}" for k in range(7)]
+    fine = [f"topo.example/f{k}" for k in range(7)]
+    nodes = []
+    for i in range(n_nodes):
+        n = mk_node(i, rng)
+        for k, key in enumerate(coarse):
+            n["metadata"]["labels"][key] = f"v{rng.randrange(2 + k % 2)}"
+        for k, key in enumerate(fine):
+            n["metadata"]["labels"][key] = f"p{(i + k) // 2}"
+        nodes.append(n)
+    existing = []
+    for i, n in enumerate(nodes):
+        for k in range(rng.randrange(6)):
+            p = mk_pod(f"e{i}-{k}", rng, node=n["metadata"]["name"])
+            p["metadata"]["namespace"] = "default"
+            p["metadata"]["labels"] = {"app": rng.choice(["a", "b", "c"]), "tier": rng.choice(["x", "y"])}
+            p["spec"]["containers"][0]["resources"]["requests"].pop("example.com/gpu", None)
+            if rng.random() < 0.25:
+                p["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                    {"labelSelector": {"matchLabels": {"app": "d"}}, "topologyKey": rng.choice(fine)}]}}
+            existing.append(p)
+    return rng, nodes, existing, coarse, fine
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_preempt_beyond_register_store(native, seed):
+    """Preemptors with more than kPreemptCons (8) DoNotSchedule constraints, required affinity terms,
+    required anti-affinity terms or existing-anti keys: the workspace-resident dry run (PreemptWide) on both
+    device paths against the oracle's literal RemovePod / AddPod -- no limit below the pod compiler's own
+    (kMaxCons spread constraints, kMaxPodTerms terms per kind)."""
+    rng, nodes, existing, coarse, fine = many_keys_cluster(500 + seed, 40 + 20 * seed)
+    keys = coarse + fine
+    dev, orc = build(native, nodes, existing), build(oracle, nodes, existing)
+    found = 0
+    for q in range(12):
+        pod = mk_pod(f"w{q}", rng, prio=rng.choice([500, 1000]), big=True)
+        pod["metadata"]["namespace"] = "default"
+        # app=d: the existing pods' anti-affinity terms match it (existing-anti keys, up to 7 fine ones)
+        pod["metadata"]["labels"] = {"app": rng.choice(["a", "b", "d"]), "tier": rng.choice(["x", "y"])}
+        pod["spec"]["containers"][0]["resources"]["requests"].pop("example.com/gpu", None)
+        kind = q % 3
+        if kind == 0:  # 9-14 DoNotSchedule constraints, one per key
+            pod["spec"]["topologySpreadConstraints"] = [
+                {"maxSkew": rng.choice([1, 2, 4, 8]), "topologyKey": k, "whenUnsatisfiable": "DoNotSchedule",
+                 "labelSelector": {"matchLabels": {rng.choice(["app", "tier"]): rng.choice(["a", "b", "x"])}}}
+                for k in rng.sample(keys, rng.randrange(9, 15))]
+        elif kind == 1:  # 9-12 required anti-affinity terms (fine keys mostly: victims can clear a domain)
+            pod["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"app": rng.choice(["a", "b", "c"])}}, "topologyKey": k}
+                for k in fine + rng.sample(coarse, rng.randrange(2, 6))]}}
+        else:  # 9-11 required affinity terms the preemptor itself matches, plus anti terms on fine keys
+            pod["spec"]["affinity"] = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"tier": pod["metadata"]["labels"]["tier"]}}, "topologyKey": k}
+                for k in coarse + rng.sample(fine, rng.randrange(2, 5))]},
+                "podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                    {"labelSelector": {"matchLabels": {"app": "c"}}, "topologyKey": k} for k in rng.sample(fine, 3)]}}
+        args = {"offset": rng.randrange(1000), "allNodes": rng.random() < 0.5, "now": 1704153600 * 10 ** 9,
                 "minCandidateNodesPercentage": 100, "minCandidateNodesAbsolute": 100}
         r, _ = compare(dev, orc, pod, args)
         found += r.status == 0
