@@ -626,11 +626,12 @@ constexpr int kAggRingPods = 2048;   // the resident instance keeps kBlobLds pro
 constexpr int kAggRingTerms = 2048;  // room for the longer LDS offsets) and the shorter lists
 static_assert(kRingEntryBytes <= kBlobLds, "a ring entry is staged into a k_agg_loop program slot");
 constexpr int kAggSpillMax = 1 << 20;  // pod / term list entries past those per workgroup (HBM spill rows)
-constexpr int kAGran = 13;         // granules per participant per pod
+constexpr int kAGran = 14;         // granules per participant per pod
 constexpr int kAggStartRow = 1024; // k_agg_loop (node-sharded): the start barrier's granule row (= kLoopMaxPods)
 enum AggGran : int {
   AG_Z0 = 0,   // {InterPodAffinity "any" bits}: every count of the pod is in the shared region
-  AG_Z1 = 1,   // node-local DoNotSchedule constraint 0: {min count over my eligible nodes (24) | eligible nodes (20)}
+  AG_Z1 = 1,   // node-local DoNotSchedule constraint 0: {min count over my eligible nodes (24) | eligible nodes (12) |
+               //  of them at that minimum (12)}
   AG_Z2 = 2,   // ... constraint 1
   AG_A0 = 3,   // {feasible | feasible before nextStartNodeIndex}
   AG_A1 = 4,   // {max raw TaintToleration + 1 | max raw NodeAffinity + 1}
@@ -643,7 +644,9 @@ enum AggGran : int {
   AG_B = 10,   // packed (TotalScore, pre-order) key
   AG_BN = 11,  // the snapshot index + 1 of the workgroup's best node (every workgroup folds the
                // chosen pod into the next pod's counts)
-  AG_PX = 12,  // PodTopologySpread raw-score {max + 1 (24) | 2^24 - 1 - min (24)} over my scored nodes
+  AG_BC = 12,  // the template cache: my best node's counts under the next pod's node-local DoNotSchedule
+               // constraints {constraint 0 (24) | constraint 1 (24)} (the fold moves their minima without exchange Z)
+  AG_PX = 13,  // PodTopologySpread raw-score {max + 1 (24) | 2^24 - 1 - min (24)} over my scored nodes
 };
 constexpr int kAggScoreCons = 2;   // k_agg_loop: ScheduleAnyway constraints of a looped pod (per-node counts in LDS)
 constexpr int kAggPresBits = 76;   // k_agg_loop: presence bits of its non-hostname score constraints' domains
@@ -685,7 +688,26 @@ struct AggView {
   // staged program and entry -- through device memory (kRelayWords: the doorbell's four tagged words, then the
   // program, then the entry); the others poll that (nullptr: every workgroup polls the host)
   unsigned long long* relay;
+  // the template cache (batch instance): per workgroup kAggTc slots of kTcWords words, each a
+  // template's counts as this workgroup holds them; tcw[batch pod] the host's plan (TcWord; nullptr: off)
+  unsigned long long* tcache;
+  const uint32_t* tcw;
 };
+// k_agg_loop's template cache: a pod's counts are a function of its template (the program but for the fields
+// agg_same masks) and of the pods placed before it.  Each workgroup keeps the counts of up to kAggTc templates
+// in HBM, current through the last placement, so a pod of a cached template loads them instead of gathering.
+constexpr int kAggTc = 6;
+constexpr int kAggSlotsC = kLoopMaxBlk * kBlock;             // node slots per k_agg_loop workgroup
+constexpr int kTcLh = kAggGWords;                             // slot layout (words): shared-region totals,
+constexpr int kTcElig = kTcLh + kAggLocal * kAggSlotsC / 2;   // node-local histograms (int32),
+constexpr int kTcAny = kTcElig + kAggSlotsC / 4;              // eligibility (uint16), the IPA any bits
+constexpr int kTcWords = (kTcAny + 1 + 7) & ~7;
+// TcWord (per pod of a run): bits 0-3 slot + 1 (0: the pod's counts are not cached), bit 4 hit (the slot holds
+// its template's counts: loaded, not gathered), bits 8-13 the slots the loop folds the previous pod's
+// placement into while it decides this pod
+KSG_HD inline int tc_slot(uint32_t w) { return (int)(w & 15u) - 1; }
+KSG_HD inline bool tc_hit(uint32_t w) { return (w & 16u) != 0; }
+KSG_HD inline uint32_t tc_fold(uint32_t w) { return (w >> 8) & 63u; }
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)
 KSG_HD inline uint32_t pack_status(uint32_t code, uint32_t plugin, uint32_t reasons) {

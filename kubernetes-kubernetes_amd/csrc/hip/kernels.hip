@@ -2721,7 +2721,7 @@ struct AggTopo {
   __device__ __forceinline__ uint32_t pndom(int c) const { return nd[c]; }
   __device__ __forceinline__ uint32_t any() const { return ipa_any; }
 };
-constexpr int kAggSlots = kLoopMaxBlk * kBlock;  // node slots per workgroup
+constexpr int kAggSlots = kAggSlotsC;  // node slots per workgroup
 __device__ __forceinline__ int64_t AggTopo::cnt(int32_t, int32_t lref, int32_t v, int ls) const {
   return lref >= 0 ? (int64_t)gh[lref + v] : (int64_t)lh[(size_t)(-1 - lref) * kAggSlots + ls];
 }
@@ -2800,49 +2800,63 @@ __device__ __forceinline__ void agran_put(const AggView& av, int q, int gid, int
       if (r < av.world) __hip_atomic_store(av.grans[r] + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
-// One wave: poll granules [slot0, slot0 + NS) of every participant for pod q until all tags match.
-template <bool SHARD, int NS, int MS>
-__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, unsigned long long (&x)[NS][MS],
-                                           int nact = NS) {  // only granules [slot0, slot0 + nact) are polled
+// One wave: poll granules [slot0, slot0 + nact) of every participant for pod q until all tags match, and hand
+// each round of 64 participants' payloads to visit(r, x).  Round by round (ALL false): a round is visited as soon
+// as it is all there, so no round's payloads stay live (MS rounds of NS 64-bit granules held together were the
+// batch loop's register peak; the later rounds have usually arrived by then).  ALL: every round polled together,
+// then visited (the resident instance, whose register allocation fits that form).
+template <bool SHARD, int NS, int MS, bool ALL, class V>
+__device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0, V&& visit, int nact = NS) {
   const int lane = threadIdx.x & 63;
   const int P = (SHARD ? av.world : 1) * av.nwg;
   const unsigned long long* g = av.gran + (size_t)q * P * kAGran + slot0;
   const unsigned long long want = (unsigned long long)av.tag;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  for (uint32_t spins = 0;; ++spins) {
-    bool ok = true;
+  constexpr int kR = ALL ? MS : 1;  // rounds polled together
+  uint32_t spins = 0;
+#pragma unroll 1
+  for (int r0 = 0; r0 < MS; r0 += kR) {
+    if (64 * r0 >= P) break;
+    unsigned long long x[kR][NS];
+    for (;; ++spins) {
+      bool ok = true;
 #pragma unroll
-    for (int r = 0; r < MS; ++r) {
-      const int v = lane + 64 * r;
+      for (int r = 0; r < kR; ++r) {
+        const int v = lane + 64 * (r0 + r);
 #pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        unsigned long long y = want << 48;
-        if (v < P && k < nact)
-          y = SHARD ? __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                    : __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok &= (y >> 48) == want;
-        x[k][r] = y & kPayload;
+        for (int k = 0; k < NS; ++k) {
+          unsigned long long y = want << 48;
+          if (v < P && k < nact)
+            y = SHARD ? __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                      : __hip_atomic_load(g + (size_t)v * kAGran + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (y >> 48) == want;
+          x[r][k] = y & kPayload;
+        }
       }
-    }
-    if (__all(ok)) return true;
-    if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
-      const unsigned long long miss = __ballot(!ok);
-      uint32_t first = 0u;  // the first failure's record is kept (a later give-up is its consequence)
-      if (lane == 0 && __hip_atomic_compare_exchange_strong(av.fail, &first, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT)) {
-        __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail + 4, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_agg_loop
-        __hip_atomic_store(av.fail + 5, (uint32_t)av.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail + 6, (uint32_t)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(av.fail + 7, (uint32_t)(miss >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(ok)) break;
+      if ((spins & 255u) == 255u && __builtin_amdgcn_s_memrealtime() - t_start > 1000000000ull) {
+        const unsigned long long miss = __ballot(!ok);
+        uint32_t first = 0u;  // the first failure's record is kept (a later give-up is its consequence)
+        if (lane == 0 && __hip_atomic_compare_exchange_strong(av.fail, &first, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(av.fail + 1, (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(av.fail + 2, (uint32_t)slot0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(av.fail + 3, (uint32_t)__builtin_ctzll(miss), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(av.fail + 4, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_agg_loop
+          __hip_atomic_store(av.fail + 5, (uint32_t)av.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(av.fail + 6, (uint32_t)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(av.fail + 7, (uint32_t)(miss >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return false;
       }
-      return false;
+      if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+      __builtin_amdgcn_s_sleep(1);
     }
-    if ((spins & 63u) == 63u && __hip_atomic_load(av.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+      if (64 * (r0 + r) < P) visit(r0 + r, x[r]);
   }
+  return true;
 }
 
 // k_agg_loop's resident mode: the committed pod's pod-table entry (RingEntry, staged in LDS) into the
@@ -2891,7 +2905,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ unsigned long long s_ball[kAggThreads / 64];  // [wave] feasibility ballots
   __shared__ int32_t s_lh[kAggLocal * kAggSlots];          // node-local histograms
   __shared__ unsigned long long s_gh[kAggGWords];          // shared-region partials, then totals
-  __shared__ uint16_t s_elig[kAggSlots];                   // eligibility per node: DoNotSchedule c (bit c),
+  __shared__ __align__(16) uint16_t s_elig[kAggSlots];     // eligibility per node: DoNotSchedule c (bit c),
                                                            // ScheduleAnyway c (bit 8 + c)
   __shared__ uint32_t s_pc[kAggScoreCons][kAggSlots];      // PodTopologySpread score: count at my node's
                                                            // domain per constraint (~0u: the node lacks the key)
@@ -2903,6 +2917,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ uint32_t s_any, s_gany, s_ok, s_F, s_psb, s_acc, s_gbar;
   __shared__ long long s_lmin[kAggLocalCons];
   __shared__ uint32_t s_lcnt[kAggLocalCons];
+  __shared__ uint32_t s_latm[kAggLocalCons];   // my eligible nodes at my minimum (exchange Z)
+  __shared__ uint32_t s_lmult[kAggLocalCons];  // eligible nodes at the global minimum (exchange Z, then the folds)
+  __shared__ uint32_t s_bc[kAggLocalCons];     // the chosen node's counts under them before the fold (exchange B)
+  __shared__ uint32_t s_lstale;                // a fold took the last node off a minimum: exchange Z again
   __shared__ unsigned long long s_wx[kAggThreads / 64][4];
   __shared__ uint32_t s_wu[kAggThreads / 64][3];           // feasible, before the start, PTS non-ignored
   __shared__ unsigned long long s_wp[kAggThreads / 64][2]; // PTS domain presence bits [0, 64), [64, 128)
@@ -2937,6 +2955,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ int s_ring_end;                  // resident mode: -1: the launch ends
   __shared__ int s_pb, s_eb;                  // resident mode: the last staged program's / entry's bytes
   __shared__ int s_spec_q;                    // resident mode: the counts hold pod s_spec_q's plus its placement
+  __shared__ int32_t s_tc_off[kAggTc];        // template cache: each written slot's template (a pod's program offset)
+  __shared__ int s_gprev, s_lprev;            // template cache: pod q-1's node (-1: not placed), my slot of it (-1)
+  __shared__ uint32_t s_tcq;                  // template cache: pod q's decisions (kTq*, slots, fold mask)
+  // (the batch instance's template cache borrows a resident-mode doorbell word: pod q-1's node's eligibility under
+  // q+1's template)
+  uint32_t& s_elp = s_ll[0];
   const int w = blockIdx.x, G = av.nwg;
   const int P = SHARD ? av.world * G : G, gid = SHARD ? av.rank * G + w : w;  // participants (rank-major), mine
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
@@ -2963,6 +2987,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
 #endif
     if (av.stamps && w == 0 && t == 0) av.stamps[(size_t)q * kAggStamps + k] = __builtin_amdgcn_s_memrealtime();
   };
+  auto gstamp = [&](int q, int k) {  // the gathering waves (wave 2's lane 0) of workgroup 0
+#ifndef KSG_DIAG
+    if constexpr (kPxa) return;
+#endif
+    if (av.stamps && w == 0 && t == 128) av.stamps[(size_t)q * kAggStamps + k] = __builtin_amdgcn_s_memrealtime();
+  };
   auto wstamp = [&](int q, int k) {  // thread 0 of every workgroup
 #ifndef KSG_DIAG
     if constexpr (kPxa) return;
@@ -2973,8 +3003,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     uint32_t first = 0u;
     if (__hip_atomic_compare_exchange_strong(av.fail, &first, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT)) {
+      uint32_t wv = (uint32_t)w;  // (formed here: a copy hoisted out of the pod loop would hold a register)
+      asm volatile("" : "+v"(wv));
       __hip_atomic_store(av.fail + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(av.fail + 2, (uint32_t)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(av.fail + 2, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
   auto stage_prog = [&](int q, int tid, int nthr) __attribute__((always_inline)) {
@@ -2990,25 +3022,28 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   // ---- aggregation of pod q by threads [0, nthr) of a group (tid = my index in it), meeting at
   // gbar(): the pod's selectors against my pods, my pods' terms against the pod, my nodes'
   // DoNotSchedule eligibility; partials of shared keys into the pod's region; Z published by tid 0.
-  auto aggregate = [&](int q, int tid, int nthr, auto&& gbar) __attribute__((always_inline)) {
+  // (gather false: the counts are in LDS already -- the template cache -- and only the node-local DoNotSchedule
+  // minima and exchange Z remain, with the any bits as they stand)
+  auto aggregate = [&](int q, int tid, int nthr, auto&& gbar, bool gather = true) __attribute__((always_inline)) {
     const uint8_t* base = s_blob[q % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
     unsigned long long* region = av.region + (size_t)q * av.gwords;
-    const int gw = d.agg_gwords, nl = d.agg_nlocal;
+    const int gw = gather ? d.agg_gwords : 0, nl = gather ? d.agg_nlocal : 0;
     const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
     const int32_t* sp = at<int32_t>(base, d.sel_pool_off);
     for (int x = tid; x < nl * kAggSlots; x += nthr) s_lh[x] = 0;
     for (int x = tid; x < gw; x += nthr) s_gh[x] = 0ull;
     if (tid == 0) {
-      s_gany = 0;
+      s_gany = gather ? 0u : s_any;
       s_lmin[0] = s_lmin[1] = 0x7fffffffffffffffll;
       s_lcnt[0] = s_lcnt[1] = 0;
+      s_latm[0] = s_latm[1] = 0;
     }
     gbar();
     // node role: DoNotSchedule eligibility (nodeLabelsMatchSpreadConstraints + inclusion policies,
     // podtopologyspread/common.go:43-80) and the shared domains it makes present (filtering.go:255-311)
     const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-    for (int ls = tid; ls < kAggSlots; ls += nthr) {
+    for (int ls = tid; ls < (gather ? kAggSlots : 0); ls += nthr) {
       const int i = nlo + ls;
       uint32_t el = 0;
       if (ls < nk * kBlock && i < m.n && d.n_ptsf) {
@@ -3028,7 +3063,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       if (lref >= 0) atomicAdd(&s_gh[lref + v], (unsigned long long)wt);
       else atomicAdd(&s_lh[(-1 - lref) * kAggSlots + ls], (int32_t)wt);
     };
-    const uint32_t np = s_np, nitems = s_np + ((d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE)) ? s_nt : 0u);
+    const uint32_t np = s_np, nitems = !gather ? 0u : s_np + ((d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE)) ? s_nt : 0u);
     // a pod with no selector of its own (only existing pods' terms to test, e.g. a plain pod beside
     // anti-affinity pods) has nothing to do in the pod role: its scan starts at the term role
     const bool pod_role = d.n_ptsf || (PTSS && d.n_ptss) || d.n_raff || d.n_ranti || (d.ipa_flags & IPA_PREF);
@@ -3164,12 +3199,26 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my region atomics performed before Z
     if constexpr (SHARD) __threadfence_system();       // ... at the peers too
     gbar();
+    if (d.agg_local_cons) {  // my eligible nodes at my minimum (exchange Z sums those of the global one)
+      int li = 0;
+      for (int32_t c = 0; c < d.n_ptsf && li < kAggLocalCons; ++c) {
+        if (!((d.agg_local_cons >> c) & 1)) continue;
+        const long long mn = s_lmin[li];
+        uint32_t k = 0;
+        for (int ls = tid; ls < kAggSlots; ls += nthr)
+          if (((s_elig[ls] >> c) & 1u) && (long long)s_lh[(size_t)(-1 - cf[c].lref) * kAggSlots + ls] == mn) ++k;
+        if (k) atomicAdd(&s_latm[li], k);
+        ++li;
+      }
+      gbar();
+    }
     if (tid == 0) {  // every Z granule is published (zero for an absent constraint)
       unsigned long long z[2] = {0, 0};
       for (int li = 0; li < kAggLocalCons; ++li) {
         const long long mn = s_lmin[li];
         const unsigned long long m24 = mn > 0xffffffll ? 0xffffffull : (unsigned long long)mn;
-        z[li] = ((unsigned long long)s_lcnt[li] << 24) | m24;  // no eligible node: min 2^24-1
+        // no eligible node: min 2^24-1
+        z[li] = ((unsigned long long)(s_latm[li] & 0xfffu) << 36) | ((unsigned long long)(s_lcnt[li] & 0xfffu) << 24) | m24;
       }
       agran_put<SHARD>(av, q, gid, AG_Z0, s_gany);
       agran_put<SHARD>(av, q, gid, AG_Z1, z[0]);
@@ -3178,35 +3227,42 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   };
   // exchange Z of pod q (wave 0): OR of the any bits, node-local minima and domain counts
   auto sweep_z = [&](int q) __attribute__((always_inline)) {
-    unsigned long long z[3][MS];
-    const bool ok = agran_sweep<SHARD, 3>(av, q, AG_Z0, z);
-    uint32_t a = 0, c1 = 0, c2 = 0;
+    uint32_t a = 0, c1 = 0, c2 = 0, k1 = 0, k2 = 0;
     unsigned long long m1 = 0xffffffull, m2 = 0xffffffull;
-#pragma unroll
-    for (int r = 0; r < MS; ++r)
+    const bool ok = agran_sweep<SHARD, 3, MS, RING>(av, q, AG_Z0, [&](int r, const unsigned long long (&z)[3]) {
       if (lane + 64 * r < P) {
-        a |= (uint32_t)z[0][r];
-        const unsigned long long x1 = z[1][r] & 0xffffffull, x2 = z[2][r] & 0xffffffull;
-        c1 += (uint32_t)(z[1][r] >> 24);
-        c2 += (uint32_t)(z[2][r] >> 24);
+        a |= (uint32_t)z[0];
+        const unsigned long long x1 = z[1] & 0xffffffull, x2 = z[2] & 0xffffffull;
+        const uint32_t a1 = (uint32_t)(z[1] >> 36) & 0xfffu, a2 = (uint32_t)(z[2] >> 36) & 0xfffu;
+        c1 += (uint32_t)(z[1] >> 24) & 0xfffu;
+        c2 += (uint32_t)(z[2] >> 24) & 0xfffu;
+        k1 = x1 < m1 ? a1 : x1 == m1 ? k1 + a1 : k1;  // nodes at my lane's minimum so far
+        k2 = x2 < m2 ? a2 : x2 == m2 ? k2 + a2 : k2;
         m1 = x1 < m1 ? x1 : m1;
         m2 = x2 < m2 ? x2 : m2;
       }
+    });
+    unsigned long long g1 = m1, g2 = m2;
     for (int o = 32; o > 0; o >>= 1) {
       a |= (uint32_t)__shfl_xor((int)a, o, 64);
-      const unsigned long long y1 = __shfl_xor(m1, o, 64), y2 = __shfl_xor(m2, o, 64);
-      m1 = y1 < m1 ? y1 : m1;
-      m2 = y2 < m2 ? y2 : m2;
+      const unsigned long long y1 = __shfl_xor(g1, o, 64), y2 = __shfl_xor(g2, o, 64);
+      g1 = y1 < g1 ? y1 : g1;
+      g2 = y2 < g2 ? y2 : g2;
     }
     c1 = wave_sum_u32(c1);
     c2 = wave_sum_u32(c2);
+    k1 = wave_sum_u32(m1 == g1 ? k1 : 0u);  // the global minimum's multiplicity
+    k2 = wave_sum_u32(m2 == g2 ? k2 : 0u);
     if (lane == 0) {
       if (!ok) s_ok = 0u;
       s_any = a;
-      s_lmin[0] = (long long)m1;
-      s_lmin[1] = (long long)m2;
+      s_lmin[0] = (long long)g1;
+      s_lmin[1] = (long long)g2;
       s_lcnt[0] = c1;
       s_lcnt[1] = c2;
+      s_lmult[0] = k1;
+      s_lmult[1] = k2;
+      s_lstale = 0u;
     }
   };
   // the region's totals into LDS (all threads; then a barrier)
@@ -3252,11 +3308,20 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   };
   // minima() for a folded pod, by the gathering group's waves (wave index gw of gnw): per shared
   // DoNotSchedule constraint its minimum, present domains and how many of them sit at the minimum
-  auto minima_grp = [&](int q, int gwv, int gnw) __attribute__((always_inline)) {
+  // (node-local constraints: the minimum, domains and multiplicity exchange Z gave)
+  auto minima_grp = [&](int q, int gwv, int gnw, bool local = true) __attribute__((always_inline)) {
     const uint8_t* base = s_blob[q % 3];
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
     const PtsCons* cf = at<PtsCons>(base, d.ptsf_off);
     for (int32_t c = gwv; c < d.n_ptsf; c += gnw) {
+      if ((d.agg_local_cons >> c) & 1) {
+        const int li = __popc((uint32_t)d.agg_local_cons & ((1u << c) - 1u));
+        if (lane == 0 && local) {
+          s_pmin[c] = li < kAggLocalCons ? s_lmin[li] : 0;
+          s_pndom[c] = li < kAggLocalCons ? s_lcnt[li] : 0;
+        }
+        continue;
+      }
       long long mn = 0x7fffffffffffffffll;
       uint32_t cnt = 0;
       for (int v = lane; v < cf[c].nvals; v += 64)
@@ -3282,7 +3347,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   // its labels against q+1's selectors, its own terms against q+1 -- exactly what q+1's aggregation
   // would count for it, less the chosen node's label values (looked up once the node is known).
   // (plan_fold_b: the placed pod's program bp, the next pod's base)
-  auto plan_fold_b = [&](const uint8_t* bp, const uint8_t* base, int gl) __attribute__((always_inline)) {
+  // (emit(lref, label slot, constraint, weight, any bit, absent value) takes each item)
+  auto plan_fold_e = [&](const uint8_t* bp, const uint8_t* base, int gl, auto&& emit) __attribute__((always_inline)) {
     asm volatile("" : "+v"(gl));  // lane-dependent item selection stays in the loop (register pressure)
     const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
@@ -3290,10 +3356,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     const unsigned long long* pl = at<unsigned long long>(bp, dp.lbl_off);
     const int32_t pn = dp.n_lbl, pns = dp.ns_id;
     const bool term = (dp.flags & DF_TERMINATING) != 0;
-    // (s_nfi was reset after the previous fold: a reset here by one lane would race the others' pushes)
     auto push = [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb) __attribute__((always_inline)) {
-      const uint32_t k = atomicAdd(&s_nfi, 1u);
-      if (k < (uint32_t)kFoldMax) s_fi[k] = FoldItem{lref, slot, cons, wt, anyb, -1};
+      emit(lref, slot, cons, wt, anyb, -1);
     };
     // lane 0: PodTopologySpread + required affinity; 1..8 ranti; 9..16 paff; 17..24 panti; 32.. own terms
     if (gl == 0) {
@@ -3322,11 +3386,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     } else if (PTSS && gl >= 25 && gl < 25 + kAggScoreCons) {  // ScheduleAnyway constraint gl - 25 of pod q+1
       const int c = gl - 25;
       const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-      if (c < d.n_ptss && !term && pns == d.ns_id && !lsel_empty(sp + cs[c].sel) && lsel_match(sp + cs[c].sel, pl, pn)) {
-        const uint32_t k = atomicAdd(&s_nfi, 1u);
-        if (k < (uint32_t)kFoldMax)  // hostname: every node counts (no eligibility); else node test bit 8 + c
-          s_fi[k] = FoldItem{cs[c].lref, cs[c].slot, cs[c].hostname ? -1 : 8 + c, 1, 0u, cs[c].hostname ? 0 : cs[c].absent};
-      }
+      if (c < d.n_ptss && !term && pns == d.ns_id && !lsel_empty(sp + cs[c].sel) && lsel_match(sp + cs[c].sel, pl, pn))
+        // hostname: every node counts (no eligibility); else node test bit 8 + c
+        emit(cs[c].lref, cs[c].slot, cs[c].hostname ? -1 : 8 + c, 1, 0u, cs[c].hostname ? 0 : cs[c].absent);
     } else if (gl >= 32 && (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE))) {
       const int32_t* own = at<int32_t>(bp, dp.own_terms_off);
       for (int k2 = gl - 32; k2 < dp.n_own_terms; k2 += 32) {
@@ -3351,6 +3413,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       }
     }
   };
+  // the plan into LDS (s_fi / s_nfi; s_nfi was reset after the previous fold: a reset here by one lane would race
+  // the others' pushes)
+  auto plan_fold_b = [&](const uint8_t* bp, const uint8_t* base, int gl) __attribute__((always_inline)) {
+    plan_fold_e(bp, base, gl,
+                [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb, int32_t absent)
+                    __attribute__((always_inline)) {
+                      const uint32_t k = atomicAdd(&s_nfi, 1u);
+                      if (k < (uint32_t)kFoldMax) s_fi[k] = FoldItem{lref, slot, cons, wt, anyb, absent};
+                    });
+  };
   auto plan_fold = [&](int q, int gl) __attribute__((always_inline)) { plan_fold_b(s_blob[q % 3], s_blob[(q + 1) % 3], gl); };
   // the owner of pod q's node adds it (and its own terms) to my lists: one thread
   auto append = [&](int q, int lq) __attribute__((always_inline)) {
@@ -3367,18 +3439,33 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   };
   // fold the placed pod (the plan in s_fi, the chosen node's label values in s_fv, its eligibility s_el) into
   // the next pod's counts: shared ones everywhere, node-local ones at the owner (local slot lq); one wave
-  auto fold_pod = [&](int lq) __attribute__((always_inline)) {
-    if (s_gnode < 0) return;
+  // (fold_at: the placed pod at node nq with eligibility el under the counts' template; adj: the DoNotSchedule
+  // minima in s_pmin / s_pmult are current and move with the counts)
+  auto fold_at = [&](int lq, int nq, uint32_t el, bool adj, int q1) __attribute__((always_inline)) {
+    if (nq < 0) return;
     const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
-    const uint32_t el = s_el;
     uint32_t any = 0;
     for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) {
       const FoldItem it = s_fi[k];
       const int32_t v = s_fv[k] >= 0 ? s_fv[k] : it.absent;  // absent: the "" domain (DF_PTS_ANYTOPO)
       if (v < 0 || (it.cons >= 0 && !((el >> it.cons) & 1u))) continue;
+      if (adj && it.lref < 0 && it.cons >= 0 && it.cons < 8) {
+        // a node-local DoNotSchedule count went up by one at the chosen node (its count before: exchange B):
+        // the minimum moves only if that node was the last one holding it
+        const PodDesc& dn = *reinterpret_cast<const PodDesc*>(s_blob[q1 % 3]);
+        const int li = __popc((uint32_t)dn.agg_local_cons & ((1u << it.cons) - 1u));
+        if (li < kAggLocalCons && (long long)s_bc[li] == s_lmin[li]) {
+          if (s_lmult[li] > 1u) s_lmult[li] -= 1u;
+          else {
+            s_lmin[li] += 1;
+            s_pmin[it.cons] = s_lmin[li];
+            s_lstale = 1u;  // its multiplicity is unknown until exchange Z
+          }
+        }
+      }
       if (it.lref >= 0) {
         const unsigned long long old = atomicAdd(&s_gh[it.lref + v], (unsigned long long)(long long)it.wt);
-        if (it.cons >= 0 && it.cons < 8) {  // a DoNotSchedule domain count went up by one: its minimum moves
+        if (adj && it.cons >= 0 && it.cons < 8) {  // a DoNotSchedule domain count went up by one: its minimum moves
           const int c = it.cons;  // only if this was the minimum's one domain (one item per constraint)
           if ((long long)old == s_pmin[c]) {
             if (s_pmult[c] == 1u) s_pmin[c] = (long long)old + 1;
@@ -3392,6 +3479,113 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     }
     for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
     if (lane == 0) s_any |= any;
+  };
+  auto fold_pod = [&](int lq, int q1) __attribute__((always_inline)) { fold_at(lq, s_gnode, s_el, true, q1); };
+
+  // ---- the template cache (the batch instance; av.tcw nullptr: off).  A pod's counts are its template's
+  // counts after every placement before it.  While pod q is decided, the gathering waves write the counts of
+  // q's template back to its slot when q+1 is of another template, load q+1's from its slot when they are
+  // cached (a hit: no gather) and fold pod q-1's placement into the other cached templates' slots.
+  // (not the PodTopologySpread-scoring instances: their registers have no room for it, and the workloads that
+  // score spreading -- system default constraints -- stamp their pods from one template)
+  constexpr bool kTc = !SHARD && !RING && !PTSS;
+  constexpr uint32_t kTqWb = 1u, kTqHit = 2u, kTqLite = 4u;
+  // (the cache's addresses are formed where used -- opaque, so none of them is hoisted out of the pod loop and
+  // kept live across it: the loop has no registers to spare)
+  auto tc_word = [&](int q) -> uint32_t {
+    const uint32_t* p = av.tcw;
+    asm volatile("" : "+s"(p));
+    return p ? p[av.first_pod + q] : 0u;
+  };
+  auto tc_at = [&](int sl) {
+    unsigned long long* p = av.tcache;
+    asm volatile("" : "+s"(p));
+    return p + ((size_t)w * kAggTc + (size_t)sl) * kTcWords;
+  };
+  // pod q's counts in LDS (through pod q-1) into slot sl: threads [0, nthr) of a group
+  auto tc_store = [&](int q, int sl, int tid, int nthr) __attribute__((always_inline)) {
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(s_blob[q % 3]);
+    unsigned long long* cb = tc_at(sl);
+    for (int x = tid; x < d.agg_gwords; x += nthr) cb[x] = s_gh[x];
+    uint32_t* lh = reinterpret_cast<uint32_t*>(cb + kTcLh);
+    for (int x = tid; x < d.agg_nlocal * kAggSlots; x += nthr) lh[x] = (uint32_t)s_lh[x];
+    uint32_t* el = reinterpret_cast<uint32_t*>(cb + kTcElig);
+    const uint32_t* se = reinterpret_cast<const uint32_t*>(s_elig);
+    for (int x = tid; x < kAggSlots / 2; x += nthr) el[x] = se[x];
+    if (tid == 0) {
+      cb[kTcAny] = s_any;
+      s_tc_off[sl] = (int32_t)s_off[q];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // slot sl into LDS as pod q1's counts (agent-scope loads: this CU's L1 may hold the lines from an earlier pod)
+  auto tc_load = [&](int q1, int sl, int tid, int nthr) __attribute__((always_inline)) {
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(s_blob[q1 % 3]);
+    const unsigned long long* cb = tc_at(sl);
+    for (int x = tid; x < d.agg_gwords; x += nthr)
+      s_gh[x] = __hip_atomic_load(cb + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* lh = reinterpret_cast<const uint32_t*>(cb + kTcLh);
+    for (int x = tid; x < d.agg_nlocal * kAggSlots; x += nthr)
+      s_lh[x] = (int32_t)__hip_atomic_load(lh + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* el = reinterpret_cast<const uint32_t*>(cb + kTcElig);
+    uint32_t* se = reinterpret_cast<uint32_t*>(s_elig);
+    for (int x = tid; x < kAggSlots / 2; x += nthr) se[x] = __hip_atomic_load(el + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) s_any = (uint32_t)__hip_atomic_load(cb + kTcAny, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // node nq's eligibility under the template of program base (aggregate's node role)
+  auto elig_of = [&](const uint8_t* base, int nq) __attribute__((always_inline)) -> uint32_t {
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+    uint32_t el = d.n_ptsf ? pts_eligible(m, base, d, at<PtsCons>(base, d.ptsf_off), d.n_ptsf, nq) : 0u;
+    if (PTSS && d.n_ptss)
+      el |= pts_eligible(m, base, d, at<PtsCons>(base, d.ptss_off), d.n_ptss, nq, (d.flags & DF_PTS_ANYTOPO) == 0) << 8;
+    return el;
+  };
+  // pod q-1's placement into the counts just loaded for pod q+1 (one wave; the minima come after)
+  // (prep: the plan, the node's label values and eligibility -- before the load; apply: after it)
+  // (wave 2 plans and reads the label values, wave 3 the eligibility)
+  auto fold_prev_prep = [&](int q, int gl) __attribute__((always_inline)) {
+    const int nq = s_gprev;
+    if (nq < 0) return;
+    const uint8_t* base = s_blob[(q + 1) % 3];
+    if (wave == 3) {
+      const uint32_t el = elig_of(base, nq);
+      if (gl == 0) s_elp = el;
+      return;
+    }
+    plan_fold_b(s_blob[(q + 2) % 3], base, gl);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+    for (uint32_t k = (uint32_t)gl; k < nfi; k += 64) s_fv[k] = node_label(m, s_fi[k].slot, nq);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  };
+  auto fold_prev_apply = [&](int q, int gl) __attribute__((always_inline)) {
+    const int nq = s_gprev;
+    if (nq < 0) return;
+    fold_at(s_lprev, nq, s_elp, false, q + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (gl == 0) s_nfi = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // pod q-1's placement into cached slot sl (one wave; base: the slot's template program, in HBM)
+  auto fold_prev_tc = [&](int q, int sl, int gl, const uint8_t* base) __attribute__((always_inline)) {
+    const int nq = s_gprev, lq = s_lprev;
+    unsigned long long* cb = tc_at(sl);
+    int32_t* lh = reinterpret_cast<int32_t*>(cb + kTcLh);
+    const uint32_t el = elig_of(base, nq);
+    uint32_t any = 0;
+    plan_fold_e(s_blob[(q + 2) % 3], base, gl,
+                [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb, int32_t absent)
+                    __attribute__((always_inline)) {
+                      int32_t v = node_label(m, slot, nq);
+                      if (v < 0) v = absent;  // absent: the "" domain (DF_PTS_ANYTOPO)
+                      if (v < 0 || (cons >= 0 && !((el >> cons) & 1u))) return;
+                      if (lref >= 0) atomicAdd(cb + lref + v, (unsigned long long)(long long)wt);
+                      else if (lq >= 0) atomicAdd(lh + (size_t)(-1 - lref) * kAggSlots + lq, wt);
+                      any |= anyb;
+                    });
+    for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o, 64);
+    if (gl == 0 && any) atomicOr(reinterpret_cast<uint32_t*>(cb + kTcAny), any);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   auto wg_bar = [&]() __attribute__((always_inline)) { __syncthreads(); };
 
@@ -3425,6 +3619,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_pxd_q = -1;
     s_elig_q = -1;
     s_spec_q = -1;
+    s_gprev = -1;
+    s_lprev = -1;
+    s_tcq = 0;
+    s_lstale = 0u;
+    s_bc[0] = s_bc[1] = 0u;
+    s_lmult[0] = s_lmult[1] = 0u;
     s_pb = 0;
     s_eb = 0;
     for (int c = 0; c < kAggScoreCons; ++c) s_psz_used[c] = ~0u;
@@ -3457,8 +3657,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     // region before every participant has started (one granule row past the pods, kAggStartRow)
     if (t == 0) agran_put<SHARD>(av, kAggStartRow, gid, 0, 1ull);
     if (wave == 0) {
-      unsigned long long x0[1][MS];
-      if (!agran_sweep<SHARD, 1>(av, kAggStartRow, 0, x0) && lane == 0) s_ok = 0u;
+      if (!agran_sweep<SHARD, 1, MS, RING>(av, kAggStartRow, 0, [](int, const unsigned long long (&)[1]) {}) && lane == 0)
+        s_ok = 0u;
     }
     __syncthreads();
     if (!s_ok) return;
@@ -3470,7 +3670,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     if (!s_ok) return;
     load_totals(0, t, kAggThreads);
     __syncthreads();
-    minima(0);
+    if constexpr (kTc) minima_grp(0, wave, kAggThreads / 64);  // (with multiplicities: a fold may follow)
+    else minima(0);
     __syncthreads();
   }
   uint32_t gtarget = 0;  // waves 1..7: arrivals their group barrier waits for (s_gbar is monotonic)
@@ -3589,6 +3790,19 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     // nothing is gathered for it -- the fold below runs on the counts in LDS, then its minima are recomputed
     const bool same1 = sp1 && (reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3])->flags & DF_AGG_SAME) &&
                        !(av.debug & 4);
+    // the template cache: write pod q's counts back (q+1 is of another template), load q+1's (a hit), or keep
+    // them (same template) -- for a next pod with node-local DoNotSchedule minima too (lite1: no gather, only
+    // exchange Z after the placement)
+    // (decided by thread 0 into s_tcq, read where used: kept live across the pod they spill registers)
+    if (kTc && t == 0) {
+      const uint32_t tc0 = tc_word(q), tc1 = more ? tc_word(q + 1) : 0u, tcm = q > 0 ? tc_word(q - 1) : 0u;
+      const int ts0 = tc_slot(tc0), ts1 = tc_slot(tc1);
+      const bool wb = more && ts0 >= 0 && ts1 != ts0;
+      const bool hit1 = more && ts1 >= 0 && ts1 != ts0 && tc_hit(tc1);
+      const bool lite = more && !sp1 && !(av.debug & 1) && ts1 >= 0 && (ts1 == ts0 || hit1);
+      s_tcq = (wb ? kTqWb : 0u) | (hit1 ? kTqHit : 0u) | (lite ? kTqLite : 0u) | ((uint32_t)(ts0 & 15) << 8) |
+              ((uint32_t)(ts1 & 15) << 12) | (tc_fold(tc0) << 16) | ((tcm & 15u) << 24);
+    }
     stamp(q, 0);
     wstamp(q, 0);
 
@@ -3755,25 +3969,27 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           wstamp(q, 1);
         }
         const bool pts_q = PTSS && ((d.score_mask >> P_PTS) & 1u) != 0;
-        unsigned long long xa[6][MS];
-        const bool ok = agran_sweep<SHARD, 6>(av, q, AG_A0, xa, pts_q ? 6 : 4);
-        uint32_t F = 0, wp = 0, bf = 0;
-        unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0;
-#pragma unroll
-        for (int r = 0; r < MS; ++r) {
+        uint32_t F = 0, wp = 0, bf = 0, ni = 0;
+        unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0, p0 = 0, p1 = 0;
+        const bool ok = agran_sweep<SHARD, 6, MS, RING>(av, q, AG_A0, [&](int r, const unsigned long long (&xa)[6]) {
           const int v = lane + 64 * r;
           if (v < P) {
-            const uint32_t c = gran_a_count(xa[0][r]);
+            const uint32_t c = gran_a_count(xa[0]);
             F += c;
             if (v < gid) wp += c;
-            bf += gran_a_below(xa[0][r]);
-            const unsigned long long tv = gran_a_tp1(xa[1][r]), nv = gran_a_np1(xa[1][r]);
+            bf += gran_a_below(xa[0]);
+            const unsigned long long tv = gran_a_tp1(xa[1]), nv = gran_a_np1(xa[1]);
             tmax = tv > tmax ? tv : tmax;
             nmax = nv > nmax ? nv : nmax;
-            imax = xa[2][r] > imax ? xa[2][r] : imax;
-            inmax = xa[3][r] > inmax ? xa[3][r] : inmax;
+            imax = xa[2] > imax ? xa[2] : imax;
+            inmax = xa[3] > inmax ? xa[3] : inmax;
+            if (PTSS) {  // PodTopologySpread: non-ignored nodes, domain presence
+              ni += (uint32_t)(xa[5] & 0xfffffull);
+              p0 |= xa[4];
+              p1 |= xa[5] >> 20;
+            }
           }
-        }
+        }, pts_q ? 6 : 4);
         F = wave_sum_u32(F);
         bf = wave_sum_u32(bf);
         wp = wave_sum_u32(wp);
@@ -3782,15 +3998,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         imax = wave_max_u64(imax);
         inmax = wave_max_u64(inmax);
         if (pts_q) {  // the topology sizes (initPreScoreState, scoring.go:82-115)
-          uint32_t ni = 0;
-          unsigned long long p0 = 0, p1 = 0;
-#pragma unroll
-          for (int r = 0; r < MS; ++r)
-            if (lane + 64 * r < P) {
-              ni += (uint32_t)(xa[5][r] & 0xfffffull);
-              p0 |= xa[4][r];
-              p1 |= xa[5][r] >> 20;
-            }
           ni = wave_sum_u32(ni);
           for (int o = 32; o > 0; o >>= 1) {
             p0 |= __shfl_xor(p0, o, 64);
@@ -3884,16 +4091,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             hmn = s_pxm[1] > hmn ? s_pxm[1] : hmn;
             if (lane == 0) agran_put<SHARD>(av, q, gid, AG_PX, (hmx << 24) | hmn);
           }
-          unsigned long long xp[1][MS];
-          const bool okp = agran_sweep<SHARD, 1>(av, q, spec ? AG_PXA : AG_PX, xp);
           unsigned long long gx = 0, gn = 0;
-#pragma unroll
-          for (int r = 0; r < MS; ++r)
+          const bool okp = agran_sweep<SHARD, 1, MS, RING>(av, q, spec ? AG_PXA : AG_PX, [&](int r, const unsigned long long (&xp)[1]) {
             if (lane + 64 * r < P) {
-              const unsigned long long a = xp[0][r] >> 24, bb = xp[0][r] & 0xffffffull;
+              const unsigned long long a = xp[0] >> 24, bb = xp[0] & 0xffffffull;
               gx = a > gx ? a : gx;
               gn = bb > gn ? bb : gn;
             }
+          });
           gx = wave_max_u64(gx);
           gn = wave_max_u64(gn);
           // the next pod's guess (wave 1 decided spec before this: on a mismatch it published PX first, and on a
@@ -3979,7 +4184,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           // my candidate and its DoNotSchedule eligibility for pod q+1 (the gathering group's node
           // role computed it for all my nodes): if it wins, every workgroup folds pod q in there
           uint32_t el = 0;
-          if (sp1 && wn >= 0) {
+          if ((sp1 || (kTc && (s_tcq & kTqLite))) && wn >= 0) {
             const PodDesc& dn = *reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3]);
             if (dn.n_ptsf || dn.n_ptss) {
               while (__hip_atomic_load(&s_elig_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q + 1)
@@ -3990,27 +4195,54 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             el = s_elig[wn - nlo];  // resident: a fold into the next pod is of this pod's template
           }
           agran_put<SHARD>(av, q, gid, AG_BN, (unsigned long long)(uint32_t)(wn + 1) | ((unsigned long long)el << 32));
-        }
-        stamp(q, 3);
-        unsigned long long xb[2][MS];
-        const bool okb = ok && agran_sweep<SHARD, 2>(av, q, AG_B, xb);
-        unsigned long long bmx = 0, bnx = 0;
-        int bpart = -1;
-#pragma unroll
-        for (int r = 0; r < MS; ++r) {
-          const unsigned long long v = (lane + 64 * r) < P ? xb[0][r] : 0ull;
-          if (v > bmx) {
-            bmx = v;
-            bnx = xb[1][r];
-            bpart = lane + 64 * r;
+          if (kTc && (s_tcq & kTqLite)) {
+            // my candidate's counts under pod q+1's node-local DoNotSchedule constraints (its counts are in LDS:
+            // s_elig_q said so), for the fold's minima
+            unsigned long long bc = 0;
+            if (wn >= 0) {
+              const uint8_t* bn = s_blob[(q + 1) % 3];
+              const PodDesc& dn = *reinterpret_cast<const PodDesc*>(bn);
+              const PtsCons* cf = at<PtsCons>(bn, dn.ptsf_off);
+              int li = 0;
+              for (int32_t c = 0; c < dn.n_ptsf && li < kAggLocalCons; ++c) {
+                if (!((dn.agg_local_cons >> c) & 1)) continue;
+                const int32_t x = s_lh[(size_t)(-1 - cf[c].lref) * kAggSlots + (wn - nlo)];
+                bc |= (unsigned long long)(x > 0xffffff ? 0xffffff : x) << (24 * li);
+                ++li;
+              }
+            }
+            agran_put<SHARD>(av, q, gid, AG_BC, bc);
           }
         }
+        stamp(q, 3);
+        unsigned long long bmx = 0, bnx = 0, bcx = 0;
+        int bpart = -1;
+        // B, BN (, the template cache's BC: the next pod's node-local counts at the chosen node)
+        constexpr int kBs = kTc ? 3 : 2;
+        const uint32_t tqb = kTc ? s_tcq : 0u;
+        const bool okb = ok && agran_sweep<SHARD, kBs, MS, RING>(av, q, AG_B, [&](int r, const unsigned long long (&xb)[kBs]) {
+          const unsigned long long v = (lane + 64 * r) < P ? xb[0] : 0ull;
+          if (v > bmx) {
+            bmx = v;
+            bnx = xb[1];
+            if constexpr (kBs > 2) bcx = xb[2];
+            bpart = lane + 64 * r;
+          }
+        }, (tqb & kTqLite) ? 3 : 2);
         const unsigned long long gbest = wave_max_u64(bmx);
         const unsigned long long bh = __ballot(bmx == gbest && gbest != 0ull);
         const int hl = bh ? (int)__builtin_ctzll(bh) : 0;
         const int pw = (F > 0 && bh) ? __builtin_amdgcn_readlane(bpart, hl) : -1;
         const uint32_t bnlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bnx, hl);
         const uint32_t bnhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bnx >> 32), hl);
+        if (kTc && (tqb & kTqLite)) {
+          const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bcx & 0xffffffull), hl);
+          const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((bcx >> 24) & 0xffffffull), hl);
+          if (lane == 0) {
+            s_bc[0] = b0;
+            s_bc[1] = b1;
+          }
+        }
         const int gnode = (F > 0 && pw == gid) ? wn : -1;  // the chosen node, if it is mine
         // ======== commit (lane 0): the owner of the chosen node applies AssumePod to its LDS core and
         // the mirror; the pod joins my lists before the next pod that counts it ========
@@ -4042,7 +4274,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             }
           }
           // the chosen node and its eligibility for the fold, to the gathering group
-          if (sp1 || RING) {
+          if (sp1 || RING || kTc) {
             const bool placed = okb && F > 0 && pw >= 0 && (d.flags & DF_ASSUME) && d.slot >= 0;
             s_gnode = placed ? (int)bnlo - 1 : -1;
             s_el = placed ? bnhi : 0u;
@@ -4056,6 +4288,37 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       // ======== waves 2..7: pod q+1's counts before pod q is placed (folded in below), its
       // DoNotSchedule minima, then the program of pod q+2 ========
       const int gt = t - 128, gn = kAggThreads - 128;
+      const uint32_t tq = kTc ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tcq) : 0u;
+      const bool tc_hit1 = (tq & kTqHit) != 0, lite1 = (tq & kTqLite) != 0;
+      const int ts1 = (int)((tq >> 12) & 15u);
+      // the template cache, first: pod q's counts (through pod q-1) written back to its slot, q+1's loaded
+      // (through pod q-2's placement) and pod q-1's placement folded in (wave 2, both programs in LDS)
+      const bool prep = tc_hit1 && s_gprev >= 0;
+      if ((tq & kTqWb) || prep) {
+        if (prep && wave <= 3) fold_prev_prep(q, lane);
+        if ((tq & kTqWb) && (!prep || wave > 2)) tc_store(q, (int)((tq >> 8) & 15u), prep ? gt - 64 : gt, prep ? gn - 64 : gn);
+        grp_bar();
+      }
+      gstamp(q, 13);
+      if (tc_hit1) {
+        tc_load(q + 1, ts1, gt, gn);
+        grp_bar();
+        if (wave == 2) fold_prev_apply(q, lane);
+      }
+      gstamp(q, 14);
+      // (then pod q-1 into the other cached templates' slots, on waves 3..7 beside wave 2's work below)
+      const uint32_t fo = (tq >> 16) & 63u & ~(tc_hit1 ? 1u << ts1 : 0u);
+      auto fold_others = [&]() __attribute__((always_inline)) {
+        if (!fo || s_gprev < 0 || wave < 3) return;
+        uint32_t f = fo;
+        for (int k = 0; f; ++k) {
+          const int sl = __builtin_ctz(f);
+          f &= f - 1u;
+          // (the slot of pod q-1's own template: its program is pod q-1's, still in LDS)
+          if (k % (kAggThreads / 64 - 3) == wave - 3)
+            fold_prev_tc(q, sl, lane, (int)((tq >> 24) & 15u) == sl + 1 ? s_blob[(q + 2) % 3] : b.descs + s_tc_off[sl]);
+        }
+      };
       if (same1) {
         if (wave == 2) {
           if (lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4067,7 +4330,24 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
           for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
         }
+        fold_others();
+      } else if (sp1 && tc_hit1) {
+        // cached: q+1's counts are loaded (through pod q-1's placement); its minima by every gathering wave
+        if (wave == 2 && lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        grp_bar();  // (pod q-1 folded in)
+        minima_grp(q + 1, wave - 2, kAggThreads / 64 - 2);
+        if (wave == 2) {
+          plan_fold(q, lane);
+          while (__hip_atomic_load(&s_bn_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+            __builtin_amdgcn_s_sleep(1);
+          const int nq = s_gnode;
+          const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+          for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
+        }
+        fold_others();
       } else if (sp1) {
+        fold_others();
+        if (fo && s_gprev >= 0) grp_bar();  // (the gather below uses every gathering wave)
         aggregate(q + 1, gt, gn, grp_bar);
         if (wave == 2) {
           plan_fold(q, lane);
@@ -4085,7 +4365,29 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
           for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
         }
+      } else if (lite1) {
+        // node-local DoNotSchedule minima: the counts in LDS now -- kept (same template: the minima and their
+        // multiplicities too), or loaded: then exchange Z gives those (through pod q-1), here or (aggLoopDebug 64)
+        // after the placement; pod q's fold moves them
+        // (loaded: exchange Z after the placement gives them)
+        if (tc_hit1) grp_bar();  // (pod q-1 folded in)
+        if (wave == 2) {
+          if (lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          plan_fold(q, lane);
+        }
+        fold_others();
+        if (wave == 2) {
+          while (__hip_atomic_load(&s_bn_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
+            __builtin_amdgcn_s_sleep(1);
+          const int nq = s_gnode;
+          const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
+          for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
+        }
+      } else {
+        fold_others();
       }
+      if (fo && s_gprev >= 0 && !(sp1 && !tc_hit1 && !same1)) grp_bar();  // before pod q-1's program slot takes q+2's
+      gstamp(q, 15);
       if (!RING && q + 2 < av.npods) stage_prog(q + 2, gt, gn);  // s_blob[(q+2)%3] held pod q-1
     }
     __syncthreads();
@@ -4114,7 +4416,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         stamp(q, 6);
         stamp(q, 7);
         if (wave == 0) {
-          fold_pod(lq);
+          fold_pod(lq, q + 1);
           if (same1) {  // the minima over the folded counts (no gathered ones to adjust)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             minima_grp(q + 1, 0, 1);
@@ -4125,6 +4427,30 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           }
         }
         __syncthreads();
+      } else if (kTc && (s_tcq & kTqLite)) {
+        // pod q into q+1's counts: a node-local minimum moves by the chosen node's count (exchange B) and its
+        // multiplicity; exchange Z again only when the fold took the last node off it
+        const bool zend = (s_tcq & kTqHit) != 0;  // (loaded: exchange Z not run yet)
+        if (wave == 0) {
+          fold_at(lq, s_gnode, s_el, !zend, q + 1);
+          if (!zend) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            minima_grp(q + 1, 0, 1);
+          }
+          if (lane == 0) {
+            if (lq >= 0) append(q, lq);
+            s_nfi = 0;
+          }
+        }
+        __syncthreads();
+        if (zend || s_lstale) {
+          aggregate(q + 1, t, kAggThreads, wg_bar, false);
+          if (wave == 0) sweep_z(q + 1);
+          __syncthreads();
+          if (!s_ok) return;
+          minima_grp(q + 1, wave, kAggThreads / 64);
+          __syncthreads();
+        }
       } else {
         if (t == 0 && lq >= 0) append(q, lq);
         __syncthreads();
@@ -4134,7 +4460,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         if (!s_ok) return;
         load_totals(q + 1, t, kAggThreads);
         __syncthreads();
-        minima(q + 1);
+        if constexpr (kTc) minima_grp(q + 1, wave, kAggThreads / 64);  // (with multiplicities: a fold may follow)
+        else minima(q + 1);
         __syncthreads();
       }
     } else if (RING) {
@@ -4152,7 +4479,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
           for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          fold_pod(s_pend_ls);
+          fold_pod(s_pend_ls, q);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           minima_grp(q, 0, 1);
         }
@@ -4166,6 +4493,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       // lists -- within this launch; an agent-scope release / acquire here wrote back and invalidated the L2 of
       // every workgroup's XCD each pod: 11 µs per call at 100 000 nodes)
       __syncthreads();
+    }
+    if (kTc && t == 0) {  // pod q's placement, for the next pod's folds into the cached templates
+      s_gprev = s_gnode;
+      s_lprev = s_pend_ls;
     }
     stamp(q, 8);
   }

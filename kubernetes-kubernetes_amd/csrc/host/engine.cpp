@@ -1204,9 +1204,10 @@ Engine::~Engine() {
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
                     &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill, &d_relay,
                     &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf, &d_wide, &d_vsc,
-                    &d_ob, &d_ob_heap, &d_ob_map})
+                    &d_ob, &d_ob_heap, &d_ob_map, &d_tcache, &d_tcw})
     if (b->p) (void)hipFree(b->p);
   if (h_pinned) (void)hipHostFree(h_pinned);
+  if (h_tcw) (void)hipHostFree(h_tcw);
   if (ev0) (void)hipEventDestroy(ev0);
   if (ev1) (void)hipEventDestroy(ev1);
 }
@@ -1441,6 +1442,57 @@ static bool agg_same(const std::vector<uint8_t>& a, const std::vector<uint8_t>& 
 }
 
 static bool agg_same(const CompiledPod& a, const CompiledPod& b) { return !a.error && !b.error && agg_same(a.blob, b.blob); }
+
+// k_agg_loop's template cache plan for the run [i, j) (TcWord per pod, desc.h): each pod's template takes a slot
+// (a template already cached: a hit, its counts are loaded instead of gathered; else the least recently used
+// slot but the active one), and per pod q the slots the loop folds pod q-1's placement into while deciding q:
+// every slot written back before (a template's counts are written back when the pod after its last pod is of
+// another template), but q's own (its counts are in LDS) and q+1's when q+1 loads them (folded after the load).
+static void tc_plan(const std::vector<CompiledPod>& cp, int i, int j, uint32_t* out) {
+  const int R = j - i;
+  std::vector<int> ts((size_t)R, -1);
+  std::vector<uint8_t> hit((size_t)R, 0);
+  int rep[kAggTc];
+  int64_t used[kAggTc];
+  for (int s = 0; s < kAggTc; ++s) rep[s] = -1, used[s] = -1;
+  for (int k = 0; k < R; ++k) {
+    const CompiledPod& p = cp[(size_t)(i + k)];
+    const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
+    if (p.error || !(d.flags & DF_AGGREGATE)) continue;  // gathered as before, no slot
+    if (k > 0 && ts[(size_t)k - 1] >= 0 && agg_same(cp[(size_t)(i + k - 1)], p)) {
+      ts[(size_t)k] = ts[(size_t)k - 1];
+      used[ts[(size_t)k]] = k;
+      continue;
+    }
+    int s = -1;
+    for (int x = 0; x < kAggTc && s < 0; ++x)
+      if (rep[x] >= 0 && agg_same(cp[(size_t)rep[x]], p)) s = x;
+    if (s >= 0) {
+      hit[(size_t)k] = 1;
+    } else {
+      const int act = k > 0 ? ts[(size_t)k - 1] : -1;
+      int64_t best = INT64_MAX;
+      for (int x = 0; x < kAggTc; ++x)
+        if (x != act && used[x] < best) best = used[x], s = x;
+      rep[s] = i + k;
+    }
+    ts[(size_t)k] = s;
+    used[s] = k;
+  }
+  bool valid[kAggTc] = {};
+  for (int k = 0; k < R; ++k) {
+    const bool more = k + 1 < R;
+    const int t0 = ts[(size_t)k], t1 = more ? ts[(size_t)k + 1] : -1;
+    const bool h1 = more && t1 >= 0 && hit[(size_t)k + 1] && t1 != t0;
+    if (more && t1 >= 0 && !hit[(size_t)k + 1] && t1 != t0) valid[t1] = false;  // evicted: q+1 gathers into it
+    uint32_t f = 0;
+    if (k > 0)
+      for (int s = 0; s < kAggTc; ++s)
+        if (valid[s] && s != t0 && !(h1 && s == t1)) f |= 1u << s;
+    if (more && t0 >= 0 && t1 != t0) valid[t0] = true;  // written back while pod k is decided
+    out[k] = (t0 >= 0 ? (uint32_t)(t0 + 1) : 0u) | (hit[(size_t)k] ? 16u : 0u) | (f << 8);
+  }
+}
 
 int Engine::run_batch_api(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                           ksg_result* results, ksg_eval_out* eval) {
@@ -2120,6 +2172,22 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       av.region = (unsigned long long*)d_region.p;
       av.fail = (uint32_t*)d_fail.p;
       av.desc_bytes = (const uint32_t*)d_off.p + n;
+      // the template cache (aggLoopDebug bits 0 / 2: no folds / no same-template shortcut; bit 5: no cache)
+      if (!comm && !ptss && !(c->cfg.agg_debug & (1 | 4 | 32))) {
+        if (h_tcw_n < (size_t)n) {
+          if (h_tcw) (void)hipHostFree(h_tcw);
+          h_tcw = nullptr;
+          h_tcw_n = 0;
+          HIPCHK(hipHostMalloc((void**)&h_tcw, (size_t)n * 2 * 4, hipHostMallocDefault));
+          h_tcw_n = (size_t)n * 2;
+        }
+        if ((rc = ensure(d_tcw, (size_t)n * 4 + 64))) return rc;
+        if ((rc = ensure(d_tcache, (size_t)G * kAggTc * kTcWords * 8))) return rc;
+        tc_plan(cp, i, j, h_tcw + i);
+        HIPCHK(hipMemcpyAsync((uint32_t*)d_tcw.p + i, h_tcw + i, (size_t)(j - i) * 4, hipMemcpyHostToDevice, s));
+        av.tcw = (const uint32_t*)d_tcw.p;
+        av.tcache = (unsigned long long*)d_tcache.p;
+      }
       if (c->cfg.loop_stamps) {
         const size_t sb = ((size_t)n * kAggStamps + (size_t)n * G * 4) * 8;
         if ((rc = ensure(d_astamps, sb))) return rc;
@@ -2350,6 +2418,23 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
             std::fprintf(stderr, "[k_agg_loop phase 2, us] my half %.3f (without a gathering beside it: %.3f, %d pods)  "
                          "wait wave 1 %.3f  B publish %.3f  eligibility + BN publish %.3f\n", p2[0] / c2,
                          cns2 ? ns_half / cns2 : 0.0, cns2, p2[1] / c2, p2[2] / c2, p2[3] / c2);
+        }
+        {  // the gathering waves' template-cache work (workgroup 0, wave 2): from phase 1's end to the write-back
+           // / fold done (13), the load done (14), the window's end (15)
+          double wa[3] = {0};
+          int wc = 0;
+          for (auto& r : aruns)
+            for (int q = r.first; q < r.first + r.count; ++q) {
+              const unsigned long long* t = &st[(size_t)q * kAggStamps];
+              if (!t[1] || !t[13] || !t[14] || !t[15]) continue;
+              wa[0] += (double)(t[13] - t[1]) / 100.0;
+              wa[1] += (double)(t[14] - t[13]) / 100.0;
+              wa[2] += (double)(t[15] - t[14]) / 100.0;
+              wc++;
+            }
+          if (wc)
+            std::fprintf(stderr, "[k_agg_loop template cache, %d pods, us] write-back + fold %.3f  load %.3f  rest %.3f\n",
+                         wc, wa[0] / wc, wa[1] / wc, wa[2] / wc);
         }
         if (cnt)
           std::fprintf(stderr, "[k_agg_loop stamps, %d pods, us] phase1 %.3f  A %.3f  phase2+B publish %.3f  "

@@ -656,6 +656,10 @@ class Engine {
                   double* bytes, int* timed);
   void* h_pinned = nullptr;
   size_t h_pinned_bytes = 0;
+  // k_agg_loop's template cache: the slots (kAggTc per workgroup) and the per-pod plan (TcWord), pinned + device
+  DevBuf d_tcache, d_tcw;
+  uint32_t* h_tcw = nullptr;
+  size_t h_tcw_n = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;  // sampled k_filter_score timing events (pairs)
   int ensure(DevBuf& b, size_t bytes);

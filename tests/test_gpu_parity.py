@@ -999,6 +999,51 @@ def test_agg_loop_same_template_runs(native, wg):
     assert g.compare_mirror(sync=False) == (0, -1)
 
 
+@pytest.mark.parametrize("wg,seed", [(0, 0), (7, 1), (1, 2), (0, 3)])
+def test_agg_loop_template_cache(native, wg, seed):
+    """k_agg_loop's template cache: pods of up to nine templates in random order (more than the six slots, so
+    templates are evicted and gathered again), C3's rotation among them -- pod affinity, node affinity beside
+    existing affinity terms, hostname spread honouring node affinity and taints (node-local DoNotSchedule minima:
+    the counts are kept or loaded, exchange Z after the placement) -- zone spread, required / preferred
+    anti-affinity, unplaceable pods.  A pod of a cached template loads its counts and folds the previous pod's
+    placement in; every placement is folded into the other cached templates.  Against the oracle and the loop
+    with the cache off (aggLoopDebug 32)."""
+    from ksg import synth
+    rng = random.Random(8800 + seed)
+    nodes, init, _ = synth.scheduling_c3(700, 500, 0)
+    for k, n in enumerate(nodes):  # two zones, so zone spread and zone affinity have more than one domain
+        n["metadata"]["labels"]["topology.kubernetes.io/zone"] = f"zone{1 + k % 2}"
+    kinds = [lambda n: synth.pod_with_pod_affinity(n, "sched-1"),
+             lambda n: synth.pod_with_node_affinity(n, "sched-1", ["zone1", "zone2"]),
+             lambda n: synth.pod_with_node_inclusion_policy(n, "sched-1"),
+             lambda n: synth.pod_with_topology_spreading(n, "sched-1"),
+             lambda n: synth.pod_with_required_anti_affinity(n, "sched-1"),
+             lambda n: synth.pod_with_preferred_pod_anti_affinity(n, "sched-1"),
+             lambda n: synth.pod_with_node_affinity(n, "sched-1", ["zone2"]),
+             lambda n: synth.pod_with_pod_affinity(n, "sched-0"),
+             lambda n: synth.pod_with_topology_spreading(n, "sched-0")]
+    pods = []
+    for k in range(360):
+        if k < 90:
+            kind = k % 3  # C3's rotation first
+        else:
+            kind = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 2, 2, 0])
+        pods.append(kinds[kind](f"c{k}"))
+    big = synth.pod_with_node_inclusion_policy("huge", "sched-1")
+    big["spec"]["containers"][0]["resources"] = {"requests": {"cpu": "1000"}}
+    pods[120:120] = [big]
+    base = {"loopWorkgroups": wg} if wg else {}
+    g, o = _pair(native, base, nodes, init)
+    g2, _ = _pair(native, dict(base, aggLoopDebug=32), nodes, init)
+    rs = g.schedule_batch([g.compile(p) for p in pods], assume=True)
+    rs2 = g2.schedule_batch([g2.compile(p) for p in pods], assume=True)
+    assert g.kernel_stats()[3] == "k_agg_loop"
+    for q, p in enumerate(pods):
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rs[q].as_tuple() == ro.as_tuple() == rs2[q].as_tuple(), f"pod {q} ({p['metadata']['name']})"
+    assert g.compare_mirror(sync=False) == (0, -1)
+
+
 @pytest.mark.parametrize("debug", [0, 8, 28, -1])
 def test_resident_agg_same_template_calls(native, debug):
     """ksg_schedule_one of runs of identical pods through the resident k_agg_loop: a pod posted right after
