@@ -3489,7 +3489,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   // (not the PodTopologySpread-scoring instances: their registers have no room for it, and the workloads that
   // score spreading -- system default constraints -- stamp their pods from one template)
   constexpr bool kTc = !SHARD && !RING && !PTSS;
-  constexpr uint32_t kTqWb = 1u, kTqHit = 2u, kTqLite = 4u;
+  // kTqOne: q+1's counts are loaded and its template has one node-local DoNotSchedule constraint -- its minimum
+  // rides exchange B (each workgroup's part in AG_BC beside the chosen node's count), no exchange Z
+  constexpr uint32_t kTqWb = 1u, kTqHit = 2u, kTqLite = 4u, kTqOne = 8u;
   // (the cache's addresses are formed where used -- opaque, so none of them is hoisted out of the pod loop and
   // kept live across it: the loop has no registers to spare)
   auto tc_word = [&](int q) -> uint32_t {
@@ -3800,7 +3802,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       const bool wb = more && ts0 >= 0 && ts1 != ts0;
       const bool hit1 = more && ts1 >= 0 && ts1 != ts0 && tc_hit(tc1);
       const bool lite = more && !sp1 && !(av.debug & 1) && ts1 >= 0 && (ts1 == ts0 || hit1);
-      s_tcq = (wb ? kTqWb : 0u) | (hit1 ? kTqHit : 0u) | (lite ? kTqLite : 0u) | ((uint32_t)(ts0 & 15) << 8) |
+      const bool one = lite && hit1 && !(av.debug & 64) &&
+                       __popc((uint32_t)reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3])->agg_local_cons) == 1;
+      s_tcq = (wb ? kTqWb : 0u) | (hit1 ? kTqHit : 0u) | (lite ? kTqLite : 0u) | (one ? kTqOne : 0u) | ((uint32_t)(ts0 & 15) << 8) |
               ((uint32_t)(ts1 & 15) << 12) | (tc_fold(tc0) << 16) | ((tcm & 15u) << 24);
     }
     stamp(q, 0);
@@ -4211,6 +4215,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
                 ++li;
               }
             }
+            if (s_tcq & kTqOne)  // {my candidate's count (14) | my minimum (14) | nodes at it (10) | nodes (10)}
+              bc = (bc & 0x3fffull) | ((unsigned long long)(s_lmin[0] > 0x3fff ? 0x3fff : s_lmin[0]) << 14) |
+                   ((unsigned long long)(s_latm[0] & 0x3ffu) << 28) | ((unsigned long long)(s_lcnt[0] & 0x3ffu) << 38);
             agran_put<SHARD>(av, q, gid, AG_BC, bc);
           }
         }
@@ -4220,6 +4227,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         // B, BN (, the template cache's BC: the next pod's node-local counts at the chosen node)
         constexpr int kBs = kTc ? 3 : 2;
         const uint32_t tqb = kTc ? s_tcq : 0u;
+        unsigned long long zm = 0x3fffull;  // (kTqOne: the merged minimum of AG_BC's parts, nodes at it, nodes)
+        uint32_t zk = 0, zc = 0;
         const bool okb = ok && agran_sweep<SHARD, kBs, MS, RING>(av, q, AG_B, [&](int r, const unsigned long long (&xb)[kBs]) {
           const unsigned long long v = (lane + 64 * r) < P ? xb[0] : 0ull;
           if (v > bmx) {
@@ -4227,6 +4236,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             bnx = xb[1];
             if constexpr (kBs > 2) bcx = xb[2];
             bpart = lane + 64 * r;
+          }
+          if constexpr (kBs > 2) {
+            if ((tqb & kTqOne) && lane + 64 * r < P) {
+              const unsigned long long x = (xb[2] >> 14) & 0x3fffull;
+              const uint32_t a = (uint32_t)(xb[2] >> 28) & 0x3ffu;
+              zc += (uint32_t)(xb[2] >> 38) & 0x3ffu;
+              zk = x < zm ? a : x == zm ? zk + a : zk;
+              zm = x < zm ? x : zm;
+            }
           }
         }, (tqb & kTqLite) ? 3 : 2);
         const unsigned long long gbest = wave_max_u64(bmx);
@@ -4236,11 +4254,31 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         const uint32_t bnlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bnx, hl);
         const uint32_t bnhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bnx >> 32), hl);
         if (kTc && (tqb & kTqLite)) {
-          const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bcx & 0xffffffull), hl);
+          const bool one = (tqb & kTqOne) != 0;
+          const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bcx & (one ? 0x3fffull : 0xffffffull)), hl);
           const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((bcx >> 24) & 0xffffffull), hl);
+          if (one) {  // pod q+1's node-local minimum, its multiplicity and domains (through pod q-1)
+            unsigned long long g = zm;
+            for (int o = 32; o > 0; o >>= 1) {
+              const unsigned long long y = __shfl_xor(g, o, 64);
+              g = y < g ? y : g;
+            }
+            zc = wave_sum_u32(zc);
+            zk = wave_sum_u32(zm == g ? zk : 0u);
+            if (lane == 0) {
+              const uint8_t* bn = s_blob[(q + 1) % 3];
+              const int c = __builtin_ctz((uint32_t)reinterpret_cast<const PodDesc*>(bn)->agg_local_cons);
+              s_lmin[0] = (long long)g;
+              s_lcnt[0] = zc;
+              s_lmult[0] = zk;
+              s_lstale = 0u;
+              s_pmin[c] = (long long)g;
+              s_pndom[c] = zc;
+            }
+          }
           if (lane == 0) {
             s_bc[0] = b0;
-            s_bc[1] = b1;
+            s_bc[1] = one ? 0u : b1;
           }
         }
         const int gnode = (F > 0 && pw == gid) ? wn : -1;  // the chosen node, if it is mine
@@ -4369,9 +4407,34 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         // node-local DoNotSchedule minima: the counts in LDS now -- kept (same template: the minima and their
         // multiplicities too), or loaded: then exchange Z gives those (through pod q-1), here or (aggLoopDebug 64)
         // after the placement; pod q's fold moves them
-        // (loaded: exchange Z after the placement gives them)
+        // (loaded: exchange Z after the placement gives them -- or, one such constraint (kTqOne), exchange B
+        // carries each workgroup's minimum, its nodes and those at it, from wave 2 here)
         if (tc_hit1) grp_bar();  // (pod q-1 folded in)
         if (wave == 2) {
+          if (tq & kTqOne) {
+            const uint8_t* bn = s_blob[(q + 1) % 3];
+            const PodDesc& dn = *reinterpret_cast<const PodDesc*>(bn);
+            const int c = __builtin_ctz((uint32_t)dn.agg_local_cons);
+            const int32_t* lh = s_lh + (size_t)(-1 - at<PtsCons>(bn, dn.ptsf_off)[c].lref) * kAggSlots;
+            long long mn = 0x7fffffffffffffffll;
+            uint32_t cnt = 0;
+            for (int ls = lane; ls < kAggSlots; ls += 64)
+              if ((s_elig[ls] >> c) & 1u) {
+                mn = lh[ls] < mn ? lh[ls] : mn;
+                ++cnt;
+              }
+            mn = (long long)dec_i64(~wave_max_u64(~enc_i64(mn)));
+            cnt = wave_sum_u32(cnt);
+            uint32_t atm = 0;
+            for (int ls = lane; ls < kAggSlots; ls += 64)
+              if (((s_elig[ls] >> c) & 1u) && (long long)lh[ls] == mn) ++atm;
+            atm = wave_sum_u32(atm);
+            if (lane == 0) {
+              s_lmin[0] = mn;
+              s_lcnt[0] = cnt;
+              s_latm[0] = atm;
+            }
+          }
           if (lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           plan_fold(q, lane);
         }
@@ -4430,7 +4493,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       } else if (kTc && (s_tcq & kTqLite)) {
         // pod q into q+1's counts: a node-local minimum moves by the chosen node's count (exchange B) and its
         // multiplicity; exchange Z again only when the fold took the last node off it
-        const bool zend = (s_tcq & kTqHit) != 0;  // (loaded: exchange Z not run yet)
+        const bool zend = (s_tcq & kTqHit) && !(s_tcq & kTqOne);  // (loaded, exchange Z not run yet)
         if (wave == 0) {
           fold_at(lq, s_gnode, s_el, !zend, q + 1);
           if (!zend) {
