@@ -703,10 +703,12 @@ constexpr int kTcElig = kTcLh + kAggLocal * kAggSlotsC / 2;   // node-local hist
 constexpr int kTcAny = kTcElig + kAggSlotsC / 4;              // eligibility (uint16), the IPA any bits
 constexpr int kTcWords = (kTcAny + 1 + 7) & ~7;
 // TcWord (per pod of a run): bits 0-3 slot + 1 (0: the pod's counts are not cached), bit 4 hit (the slot holds
-// its template's counts: loaded, not gathered), bits 8-13 the slots the loop folds the previous pod's
-// placement into while it decides this pod
+// its template's counts: loaded, not gathered), bit 5 the write-back while this pod is decided stores the
+// template's node eligibility too (static: once per slot assignment), bits 8-13 the slots the loop folds the
+// previous pod's placement into while it decides this pod
 KSG_HD inline int tc_slot(uint32_t w) { return (int)(w & 15u) - 1; }
 KSG_HD inline bool tc_hit(uint32_t w) { return (w & 16u) != 0; }
+KSG_HD inline bool tc_elig(uint32_t w) { return (w & 32u) != 0; }
 KSG_HD inline uint32_t tc_fold(uint32_t w) { return (w >> 8) & 63u; }
 
 // packed per-node status word: code(4) | plugin(4, 15 = none) | reasons(24)

@@ -2958,6 +2958,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   __shared__ int32_t s_tc_off[kAggTc];        // template cache: each written slot's template (a pod's program offset)
   __shared__ int s_gprev, s_lprev;            // template cache: pod q-1's node (-1: not placed), my slot of it (-1)
   __shared__ uint32_t s_tcq;                  // template cache: pod q's decisions (kTq*, slots, fold mask)
+  __shared__ uint32_t s_gbar5;                // template cache: waves 3..7's barrier (monotonic)
+  __shared__ uint32_t s_tcr[4];               // template cache: TcWord of pod p in s_tcr[p % 4] (pods q-1 .. q+2)
   // (the batch instance's template cache borrows a resident-mode doorbell word: pod q-1's node's eligibility under
   // q+1's template)
   uint32_t& s_elp = s_ll[0];
@@ -3491,7 +3493,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   constexpr bool kTc = !SHARD && !RING && !PTSS;
   // kTqOne: q+1's counts are loaded and its template has one node-local DoNotSchedule constraint -- its minimum
   // rides exchange B (each workgroup's part in AG_BC beside the chosen node's count), no exchange Z
-  constexpr uint32_t kTqWb = 1u, kTqHit = 2u, kTqLite = 4u, kTqOne = 8u;
+  constexpr uint32_t kTqWb = 1u, kTqHit = 2u, kTqLite = 4u, kTqOne = 8u, kTqEw = 16u;
   // (the cache's addresses are formed where used -- opaque, so none of them is hoisted out of the pod loop and
   // kept live across it: the loop has no registers to spare)
   auto tc_word = [&](int q) -> uint32_t {
@@ -3505,7 +3507,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     return p + ((size_t)w * kAggTc + (size_t)sl) * kTcWords;
   };
   // pod q's counts in LDS (through pod q-1) into slot sl: threads [0, nthr) of a group
-  auto tc_store = [&](int q, int sl, int tid, int nthr) __attribute__((always_inline)) {
+  // (ew: the eligibility too -- static per template, stored once per slot assignment)
+  auto tc_store = [&](int q, int sl, int tid, int nthr, bool ew) __attribute__((always_inline)) {
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(s_blob[q % 3]);
     unsigned long long* cb = tc_at(sl);
     for (int x = tid; x < d.agg_gwords; x += nthr) cb[x] = s_gh[x];
@@ -3513,7 +3516,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     for (int x = tid; x < d.agg_nlocal * kAggSlots; x += nthr) lh[x] = (uint32_t)s_lh[x];
     uint32_t* el = reinterpret_cast<uint32_t*>(cb + kTcElig);
     const uint32_t* se = reinterpret_cast<const uint32_t*>(s_elig);
-    for (int x = tid; x < kAggSlots / 2; x += nthr) el[x] = se[x];
+    for (int x = tid; x < (ew ? kAggSlots / 2 : 0); x += nthr) el[x] = se[x];
     if (tid == 0) {
       cb[kTcAny] = s_any;
       s_tc_off[sl] = (int32_t)s_off[q];
@@ -3624,6 +3627,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     s_gprev = -1;
     s_lprev = -1;
     s_tcq = 0;
+    s_gbar5 = 0;
     s_lstale = 0u;
     s_bc[0] = s_bc[1] = 0u;
     s_lmult[0] = s_lmult[1] = 0u;
@@ -3649,6 +3653,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   }
   if (!RING && av.npods > 0) stage_prog(0, t, kAggThreads);
   if (!RING && av.npods > 1) stage_prog(1, t, kAggThreads);
+  if (kTc && t < 2) s_tcr[t] = t < av.npods ? tc_word(t) : 0u;  // (then pod q+2's while pod q is decided)
   __syncthreads();
   if (s_np > pcap || s_nt > tcap) {  // host-checked; never taken
     if (t == 0) fail(0xfffffffeu);
@@ -3677,6 +3682,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     __syncthreads();
   }
   uint32_t gtarget = 0;  // waves 1..7: arrivals their group barrier waits for (s_gbar is monotonic)
+  uint32_t gtarget5 = 0;  // waves 3..7: likewise for s_gbar5
   auto grp_bar = [&]() __attribute__((always_inline)) {
     gtarget += kAggThreads / 64 - 2;  // waves 2..7
     if (lane == 0) __hip_atomic_fetch_add(&s_gbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3797,14 +3803,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     // exchange Z after the placement)
     // (decided by thread 0 into s_tcq, read where used: kept live across the pod they spill registers)
     if (kTc && t == 0) {
-      const uint32_t tc0 = tc_word(q), tc1 = more ? tc_word(q + 1) : 0u, tcm = q > 0 ? tc_word(q - 1) : 0u;
+      const uint32_t tc0 = s_tcr[q & 3], tc1 = more ? s_tcr[(q + 1) & 3] : 0u, tcm = q > 0 ? s_tcr[(q - 1) & 3] : 0u;
       const int ts0 = tc_slot(tc0), ts1 = tc_slot(tc1);
       const bool wb = more && ts0 >= 0 && ts1 != ts0;
       const bool hit1 = more && ts1 >= 0 && ts1 != ts0 && tc_hit(tc1);
       const bool lite = more && !sp1 && !(av.debug & 1) && ts1 >= 0 && (ts1 == ts0 || hit1);
       const bool one = lite && hit1 && !(av.debug & 64) &&
                        __popc((uint32_t)reinterpret_cast<const PodDesc*>(s_blob[(q + 1) % 3])->agg_local_cons) == 1;
-      s_tcq = (wb ? kTqWb : 0u) | (hit1 ? kTqHit : 0u) | (lite ? kTqLite : 0u) | (one ? kTqOne : 0u) | ((uint32_t)(ts0 & 15) << 8) |
+      s_tcq = (wb ? kTqWb : 0u) | (hit1 ? kTqHit : 0u) | (lite ? kTqLite : 0u) | (one ? kTqOne : 0u) |
+              (wb && tc_elig(tc0) ? kTqEw : 0u) | ((uint32_t)(ts0 & 15) << 8) |
               ((uint32_t)(ts1 & 15) << 12) | (tc_fold(tc0) << 16) | ((tcm & 15u) << 24);
     }
     stamp(q, 0);
@@ -4327,6 +4334,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       // DoNotSchedule minima, then the program of pod q+2 ========
       const int gt = t - 128, gn = kAggThreads - 128;
       const uint32_t tq = kTc ? (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tcq) : 0u;
+      if (kTc && t == 128) s_tcr[(q + 2) & 3] = q + 2 < av.npods ? tc_word(q + 2) : 0u;  // (read at pod q+1's top)
       const bool tc_hit1 = (tq & kTqHit) != 0, lite1 = (tq & kTqLite) != 0;
       const int ts1 = (int)((tq >> 12) & 15u);
       // the template cache, first: pod q's counts (through pod q-1) written back to its slot, q+1's loaded
@@ -4334,7 +4342,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
       const bool prep = tc_hit1 && s_gprev >= 0;
       if ((tq & kTqWb) || prep) {
         if (prep && wave <= 3) fold_prev_prep(q, lane);
-        if ((tq & kTqWb) && (!prep || wave > 2)) tc_store(q, (int)((tq >> 8) & 15u), prep ? gt - 64 : gt, prep ? gn - 64 : gn);
+        if ((tq & kTqWb) && (!prep || wave > 2)) tc_store(q, (int)((tq >> 8) & 15u), prep ? gt - 64 : gt, prep ? gn - 64 : gn, (tq & kTqEw) != 0);
         grp_bar();
       }
       gstamp(q, 13);
@@ -4357,6 +4365,24 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             fold_prev_tc(q, sl, lane, (int)((tq >> 24) & 15u) == sl + 1 ? s_blob[(q + 2) % 3] : b.descs + s_tc_off[sl]);
         }
       };
+      // waves 3..7, while wave 2 finishes pod q's fold plan: the other slots' folds, then pod q+2's program into
+      // pod q-1's slot (nothing reads pod q-1's program after them)
+      bool staged = false;
+      auto fold_stage = [&]() __attribute__((always_inline)) {
+        fold_others();
+        if (kTc && !RING && q + 2 < av.npods) {
+          if (wave >= 3) {
+            if (fo && s_gprev >= 0) {
+              gtarget5 += kAggThreads / 64 - 3;
+              if (lane == 0) __hip_atomic_fetch_add(&s_gbar5, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+              while (__hip_atomic_load(&s_gbar5, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gtarget5)
+                __builtin_amdgcn_s_sleep(1);
+            }
+            stage_prog(q + 2, t - 192, kAggThreads - 192);
+          }
+          staged = true;
+        }
+      };
       if (same1) {
         if (wave == 2) {
           if (lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4368,7 +4394,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
           for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
         }
-        fold_others();
+        fold_stage();
       } else if (sp1 && tc_hit1) {
         // cached: q+1's counts are loaded (through pod q-1's placement); its minima by every gathering wave
         if (wave == 2 && lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4382,7 +4408,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
           for (uint32_t k = (uint32_t)lane; k < nfi; k += 64) s_fv[k] = nq >= 0 ? node_label(m, s_fi[k].slot, nq) : -1;
         }
-        fold_others();
+        fold_stage();
       } else if (sp1) {
         fold_others();
         if (fo && s_gprev >= 0) grp_bar();  // (the gather below uses every gathering wave)
@@ -4438,7 +4464,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
           if (lane == 0) __hip_atomic_store(&s_elig_q, q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           plan_fold(q, lane);
         }
-        fold_others();
+        fold_stage();
         if (wave == 2) {
           while (__hip_atomic_load(&s_bn_q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q)
             __builtin_amdgcn_s_sleep(1);
@@ -4448,10 +4474,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         }
       } else {
         fold_others();
+        if (fo && s_gprev >= 0) grp_bar();  // before pod q-1's program slot takes q+2's
       }
-      if (fo && s_gprev >= 0 && !(sp1 && !tc_hit1 && !same1)) grp_bar();  // before pod q-1's program slot takes q+2's
       gstamp(q, 15);
-      if (!RING && q + 2 < av.npods) stage_prog(q + 2, gt, gn);  // s_blob[(q+2)%3] held pod q-1
+      if (!RING && q + 2 < av.npods && !staged) stage_prog(q + 2, gt, gn);  // s_blob[(q+2)%3] held pod q-1
     }
     __syncthreads();
     if (!s_ok) return;

@@ -1479,18 +1479,22 @@ static void tc_plan(const std::vector<CompiledPod>& cp, int i, int j, uint32_t* 
     ts[(size_t)k] = s;
     used[s] = k;
   }
-  bool valid[kAggTc] = {};
+  bool valid[kAggTc] = {}, elig[kAggTc] = {};  // elig: the slot holds its template's eligibility (static) already
   for (int k = 0; k < R; ++k) {
     const bool more = k + 1 < R;
     const int t0 = ts[(size_t)k], t1 = more ? ts[(size_t)k + 1] : -1;
     const bool h1 = more && t1 >= 0 && hit[(size_t)k + 1] && t1 != t0;
-    if (more && t1 >= 0 && !hit[(size_t)k + 1] && t1 != t0) valid[t1] = false;  // evicted: q+1 gathers into it
+    if (more && t1 >= 0 && !hit[(size_t)k + 1] && t1 != t0) valid[t1] = elig[t1] = false;  // evicted: q+1 gathers into it
     uint32_t f = 0;
     if (k > 0)
       for (int s = 0; s < kAggTc; ++s)
         if (valid[s] && s != t0 && !(h1 && s == t1)) f |= 1u << s;
-    if (more && t0 >= 0 && t1 != t0) valid[t0] = true;  // written back while pod k is decided
-    out[k] = (t0 >= 0 ? (uint32_t)(t0 + 1) : 0u) | (hit[(size_t)k] ? 16u : 0u) | (f << 8);
+    bool ew = false;  // this write-back stores the eligibility too
+    if (more && t0 >= 0 && t1 != t0) {  // written back while pod k is decided
+      ew = !elig[t0];
+      valid[t0] = elig[t0] = true;
+    }
+    out[k] = (t0 >= 0 ? (uint32_t)(t0 + 1) : 0u) | (hit[(size_t)k] ? 16u : 0u) | (ew ? 32u : 0u) | (f << 8);
   }
 }
 
