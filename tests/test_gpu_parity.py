@@ -1085,6 +1085,28 @@ def test_resident_agg_same_template_calls(native, debug):
     assert g.compare_mirror(sync=True)[0] == 0
 
 
+def test_resident_ring_same_flag_only_difference(native):
+    """ksg_schedule_one of consecutive pods whose programs differ in one flag bit only (DF_TERMINATING: every
+    third pod carries a deletionTimestamp, so as an assumed pod it counts for nobody's spreading): the resident
+    k_agg_loop's RING_SAME shortcut reuses the previous program with the slot, rotation and DF_AGG_SAME patched,
+    so it must not take such a pod for the same one.  Against the oracle pod by pod, and the
+    mirror against the cache."""
+    from ksg import synth
+    nodes, init, _ = synth.topology_spreading(900, 600, 0)
+    g, o = _pair(native, {}, nodes, init)
+    agg = 0
+    for k in range(45):
+        p = synth.pod_with_topology_spreading(f"f{k}", "sched-1")
+        if k % 3 == 1:
+            p["metadata"]["deletionTimestamp"] = "2024-01-01T00:00:00Z"
+        rg, _ = g.schedule_one(g.compile(p), assume=True)
+        ro, _ = o.schedule_one(o.compile(p), assume=True)
+        assert rg.as_tuple() == ro.as_tuple(), f"pod {k}"
+        agg += g.kernel_stats()[3] == "k_agg_loop"
+    assert agg > 30, f"only {agg} of 45 calls ran in the resident k_agg_loop"
+    assert g.compare_mirror(sync=True)[0] == 0
+
+
 @pytest.mark.parametrize("wg", [1, 0])
 def test_agg_loop_spilled_lists(native, wg):
     """k_agg_loop workgroups whose nodes hold more pods / affinity terms than their LDS lists (5120 each in
