@@ -3982,7 +3982,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         const bool pts_q = PTSS && ((d.score_mask >> P_PTS) & 1u) != 0;
         uint32_t F = 0, wp = 0, bf = 0, ni = 0;
         unsigned long long tmax = 0, nmax = 0, imax = 0, inmax = 0, p0 = 0, p1 = 0;
-        const bool ok = agran_sweep<SHARD, 6, MS, RING>(av, q, AG_A0, [&](int r, const unsigned long long (&xa)[6]) {
+        const bool ok = agran_sweep<SHARD, PTSS ? 6 : 4, MS, RING || !PTSS>(av, q, AG_A0, [&](int r, const auto& xa) {
           const int v = lane + 64 * r;
           if (v < P) {
             const uint32_t c = gran_a_count(xa[0]);
@@ -3994,7 +3994,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
             nmax = nv > nmax ? nv : nmax;
             imax = xa[2] > imax ? xa[2] : imax;
             inmax = xa[3] > inmax ? xa[3] : inmax;
-            if (PTSS) {  // PodTopologySpread: non-ignored nodes, domain presence
+            if constexpr (PTSS) {  // PodTopologySpread: non-ignored nodes, domain presence
               ni += (uint32_t)(xa[5] & 0xfffffull);
               p0 |= xa[4];
               p1 |= xa[5] >> 20;
@@ -4236,7 +4236,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
         const uint32_t tqb = kTc ? s_tcq : 0u;
         unsigned long long zm = 0x3fffull;  // (kTqOne: the merged minimum of AG_BC's parts, nodes at it, nodes)
         uint32_t zk = 0, zc = 0;
-        const bool okb = ok && agran_sweep<SHARD, kBs, MS, RING>(av, q, AG_B, [&](int r, const unsigned long long (&xb)[kBs]) {
+        const bool okb = ok && agran_sweep<SHARD, kBs, MS, RING || !PTSS>(av, q, AG_B, [&](int r, const unsigned long long (&xb)[kBs]) {
           const unsigned long long v = (lane + 64 * r) < P ? xb[0] : 0ull;
           if (v > bmx) {
             bmx = v;
@@ -4824,7 +4824,8 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
   } else {
     if (av.ptss && av.nwg <= 64) go(k_agg_loop<false, true, false, 1>);
     else if (av.ptss) go(k_agg_loop<false, true>);
-    else go(k_agg_loop<false, false>);
+    else if (av.nwg <= 64) go(k_agg_loop<false, false, false, 1>);  // one sweep round (C3, C4)
+    else go(k_agg_loop<false, false>);  // up to four rounds, polled together (C5)
   }
   return hipGetLastError();
 }
@@ -4861,6 +4862,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_agg_loop<true, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<false, true, true>),
                       reinterpret_cast<const void*>(&k_agg_loop<false, true, false, 1>),
+                      reinterpret_cast<const void*>(&k_agg_loop<false, false, false, 1>),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr),
                       reinterpret_cast<const void*>(&k_ob_hint),            reinterpret_cast<const void*>(&k_ob_store),
                       reinterpret_cast<const void*>(&k_ob_remap)};
