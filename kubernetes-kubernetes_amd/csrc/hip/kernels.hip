@@ -1724,8 +1724,8 @@ __device__ __forceinline__ void gran_put(const LoopView& lv, int q, int gid, int
 // until every tag matches (relaxed loads, s_sleep between passes).  x[s][r] = payload of
 // participant lane + 64 r; false on give-up.
 constexpr int kMaxSweep = 4;  // P <= 256 participants
-template <int NS>
-__device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0, unsigned long long (&x)[NS][kMaxSweep]) {
+template <int NS, int MS>
+__device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0, unsigned long long (&x)[NS][MS]) {
   const int lane = threadIdx.x & 63;
   const int P = lv.world * lv.nwg;
   const unsigned long long* g = lv.gran[lv.world == 1 ? 0 : lv.rank] + (size_t)q * P * kGran + slot0;
@@ -1736,7 +1736,7 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
   for (uint32_t spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
-    for (int r = 0; r < kMaxSweep; ++r) {
+    for (int r = 0; r < MS; ++r) {
       const int v = lane + 64 * r;
 #pragma unroll
       for (int k = 0; k < NS; ++k) {
@@ -1920,7 +1920,8 @@ constexpr int kLoopThreads = kBlock + 128;  // NW = 4: four evaluation waves, on
 __constant__ int8_t kWaveMap[3][kLoopThreads / 64] = {{0, 1, 2, 3, 4, 5}, {4, 0, 1, 2, 5, 3}, {0, 1, 4, 3, 5, 2}};
 // RING: the resident instance (pods through lv.ring, one run per pod); the batch instance has no run
 // loop at all (its one run is the whole launch), so its code is what it was before the ring existed.
-template <int NW, bool RING>
+// MS: sweep rounds of 64 participants (the one-round instance for grids of at most 64: no masked-off rounds)
+template <int NW, bool RING, int MS = kMaxSweep>
 __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
   constexpr int U = NW * 64;                  // nodes per unit: one per evaluation-wave lane
   constexpr int kLoopThreads = U + 128;       // NW evaluation waves, one selection wave, one helper wave
@@ -2288,12 +2289,12 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
       // ======== selection wave: exchange A, phase 2, exchange B, pre-evaluation, staging ========
       stamp_s(q, 0);  // exchange A of this pod was published at the end of the previous one
       if (kSt && lv.wstamps && lane == 0) lv.wstamps[((size_t)q * G + w) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-      unsigned long long xa[2][kMaxSweep];
-      bool ok = gran_sweep<2>(lv, q, 0, xa);
+      unsigned long long xa[2][MS];
+      bool ok = gran_sweep<2, MS>(lv, q, 0, xa);
       uint32_t F = 0, wp = 0, bf = 0;
       unsigned long long tmax = 0, nmax = 0;
 #pragma unroll
-      for (int r = 0; r < kMaxSweep; ++r) {
+      for (int r = 0; r < MS; ++r) {
         const int v = lane + 64 * r;
         if (v < P) {
           const uint32_t c = gran_a_count(xa[0][r]);
@@ -2327,11 +2328,11 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         mn = wave_max_u64(mn);
         a_granules(mt != 0ull ? 1u : 0u, 0u, mt, mn, &g0, &g1);
         if (lane == 0) gran_put(lv, q + kLoopMaxPods, gid, 1, g1);
-        unsigned long long xm[1][kMaxSweep];
-        ok = gran_sweep<1>(lv, q + kLoopMaxPods, 1, xm);
+        unsigned long long xm[1][MS];
+        ok = gran_sweep<1, MS>(lv, q + kLoopMaxPods, 1, xm);
         tmax = nmax = 0;
 #pragma unroll
-        for (int r = 0; r < kMaxSweep; ++r) {
+        for (int r = 0; r < MS; ++r) {
           if (lane + 64 * r < P) {
             const unsigned long long tv = xm[0][r] & 0xffffffull, nv = (xm[0][r] >> 24) & 0xffffffull;
             tmax = tv > tmax ? tv : tmax;
@@ -2369,24 +2370,24 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
         __hip_atomic_store(&s_cand_q, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       stamp_s(q, 3);
-      unsigned long long xb[2][kMaxSweep];
+      unsigned long long xb[2][MS];
       if (lv.world == 1 && rotd) {  // the keys and the (K+1)-th node's processedNodes
-        ok = ok && gran_sweep<2>(lv, q, 2, xb);
+        ok = ok && gran_sweep<2, MS>(lv, q, 2, xb);
       } else if (lv.world == 1) {  // unsharded: the owner is found locally, only the keys cross workgroups
-        unsigned long long k1[1][kMaxSweep];
-        ok = ok && gran_sweep<1>(lv, q, 2, k1);
+        unsigned long long k1[1][MS];
+        ok = ok && gran_sweep<1, MS>(lv, q, 2, k1);
 #pragma unroll
-        for (int r = 0; r < kMaxSweep; ++r) {
+        for (int r = 0; r < MS; ++r) {
           xb[0][r] = k1[0][r];
           xb[1][r] = 0;
         }
       } else {
-        ok = ok && gran_sweep<2>(lv, q, 2, xb);
+        ok = ok && gran_sweep<2, MS>(lv, q, 2, xb);
       }
       unsigned long long bm = 0, pm = 0;
       int bnode = -1;
 #pragma unroll
-      for (int r = 0; r < kMaxSweep; ++r) {
+      for (int r = 0; r < MS; ++r) {
         const unsigned long long v = (lane + 64 * r) < P ? xb[0][r] : 0ull;
         if (v > bm) {
           bm = v;
@@ -4792,10 +4793,17 @@ hipError_t launch_max_reduce(unsigned long long* dst, const RankPtrs& src, int n
 hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const LoopView& lv, hipStream_t s,
                              hipEvent_t t0, hipEvent_t t1, int unit) {
   if (lv.ring) {  // resident (no timing events: the launch spans many calls)
-    if (unit == 128)
+    if (unit == 128 && lv.world * lv.nwg <= 64)
+      hipLaunchKernelGGL((k_sched_loop<2, true, 1>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
+    else if (unit == 128)
       hipLaunchKernelGGL((k_sched_loop<2, true>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
     else
       hipLaunchKernelGGL((k_sched_loop<4, true>), dim3(lv.nwg), dim3(kLoopThreads), 0, s, m, b, lv);
+  } else if (unit == 128 && lv.world * lv.nwg <= 64) {  // one sweep round (C2's 40 workgroups)
+    if (t0)
+      hipExtLaunchKernelGGL((k_sched_loop<2, false, 1>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, t0, t1, 0, m, b, lv);
+    else
+      hipLaunchKernelGGL((k_sched_loop<2, false, 1>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, m, b, lv);
   } else if (unit == 128) {
     if (t0)
       hipExtLaunchKernelGGL((k_sched_loop<2, false>), dim3(lv.nwg), dim3(2 * 64 + 128), 0, s, t0, t1, 0, m, b, lv);
@@ -4854,7 +4862,8 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_xpack_p),            reinterpret_cast<const void*>(&k_select_shard),
                       reinterpret_cast<const void*>(&k_commit),             reinterpret_cast<const void*>(&k_max_reduce),
                       reinterpret_cast<const void*>(&k_sched_loop<4, false>), reinterpret_cast<const void*>(&k_sched_loop<2, false>),
-                      reinterpret_cast<const void*>(&k_sched_loop<4, true>), reinterpret_cast<const void*>(&k_sched_loop<2, true>),         reinterpret_cast<const void*>(&k_sample_find),
+                      reinterpret_cast<const void*>(&k_sched_loop<4, true>), reinterpret_cast<const void*>(&k_sched_loop<2, true>),
+                      reinterpret_cast<const void*>(&k_sched_loop<2, false, 1>), reinterpret_cast<const void*>(&k_sched_loop<2, true, 1>),         reinterpret_cast<const void*>(&k_sample_find),
                       reinterpret_cast<const void*>(&k_sample_apply),        reinterpret_cast<const void*>(&k_sample_shard_a),
                       reinterpret_cast<const void*>(&k_sample_shard_b),        reinterpret_cast<const void*>(&k_node_update),
                       reinterpret_cast<const void*>(&k_node_dyn),           reinterpret_cast<const void*>(&k_agg_loop<false, false>),
