@@ -8,8 +8,9 @@ loop-eligible pods exchange through the persistent loop's granules stored into e
 oracle's ScheduleResult for every pod of the stream (sequential assume semantics), including
 empty shards (clusters smaller than W * 256 nodes) and PodTopologySpread/InterPodAffinity pods.
 """
-import gc
 import os
+import subprocess
+import sys
 import threading
 import uuid
 
@@ -429,19 +430,12 @@ def test_loop_give_up_retried_over_allreduce(world):
         assert s.compare_mirror(sync=True)[0] == 0
 
 
-def test_device_exchange_needs_own_queues():
-    """In-process ranks take the device exchange only when every rank's stream has a hardware queue of its
-    own, with the null stream's and one spare beside them (DESIGN.md §6): with Q = GPU_MAX_HW_QUEUES, a group
-    of Q - 2 ranks runs the loop, but not while another context's stream is alive -- HIP would then put two
-    streams on one queue, where a rank's loop waits behind a peer's loop that spins on it.  That group keeps
-    the all-reduce path (and still matches the oracle); once the other context is gone, a new group runs the
-    loop."""
+def _queue_policy_scenario():
+    """test_device_exchange_needs_own_queues' body; run in a fresh process (see the test)."""
     from ksg.native import Scheduler
     from ksg.synth import scheduling_basic
     q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     world = q - 2
-    if world < 2 or world > 8:
-        pytest.skip(f"GPU_MAX_HW_QUEUES={q}: no in-process group size at the queue limit")
     nodes, init, pods = scheduling_basic(1877 + 256 * world, 300, 600, hetero=True)
     other = Scheduler({"device": 0})
     ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
@@ -450,17 +444,27 @@ def test_device_exchange_needs_own_queues():
     for s in ranks:
         s.close()
     other.close()
-    # HIP hands the new group's streams their hardware queues; one suite run in about five (round 5) saw a
-    # group formed right after the closes give up once on every rank (results still the oracle's, re-run
-    # over the all-reduce path): a queue of the closed streams not yet released when the new ones were
-    # assigned.  The group is formed again once in that case, and the second one must run clean.
-    for attempt in range(2):
-        ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
-        stats = _check(ranks, o, pods, chunk=300, stats_only=True)
-        if all(st == (0, 0) for st in stats) or attempt == 1:
-            break
-        for s in ranks:
-            s.close()
-        gc.collect()
-    assert all(st == (0, 0) for st in stats), f"persistent-loop give-ups / re-runs per rank: {stats}"
+    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
+    _check(ranks, o, pods, chunk=300)
     assert _dominant(ranks) == {"k_sched_loop"}
+
+
+def test_device_exchange_needs_own_queues():
+    """In-process ranks take the device exchange only when every rank's stream has a hardware queue of its
+    own, with the null stream's and one spare beside them (DESIGN.md §6): with Q = GPU_MAX_HW_QUEUES, a group
+    of Q - 2 ranks runs the loop, but not while another context's stream is alive -- HIP would then put two
+    streams on one queue, where a rank's loop waits behind a peer's loop that spins on it.  That group keeps
+    the all-reduce path (and still matches the oracle); once the other context is gone, a new group runs the
+    loop.  The library counts the streams it creates; the suite's own process has by then run hundreds of
+    contexts, torch and RCCL, whose queues it cannot see (two suite runs in round 5 saw the loop group give up
+    on every rank, results still the oracle's), so the scenario runs in a process of its own, as a
+    deployment's scheduler process would."""
+    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if q - 2 < 2 or q - 2 > 8:
+        pytest.skip(f"GPU_MAX_HW_QUEUES={q}: no in-process group size at the queue limit")
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_gpu_sharded as t; t._queue_policy_scenario(); "
+            "print('queue policy scenario ok')" % (here, os.path.join(os.path.dirname(here), "kubernetes-kubernetes_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, GPU_MAX_HW_QUEUES=str(q)),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "queue policy scenario ok" in r.stdout, (r.stdout[-3000:] + r.stderr[-3000:])
