@@ -335,6 +335,15 @@ int ksg_debug_schedule_calls(ksg_ctx *ctx, const int32_t *handles, int32_t n, ui
  * (noderesources/fit.go:317-325, spec only).  Returns 8, or KSG_EINVAL. */
 int ksg_debug_pod_resources(const char *pod_json, size_t len, int64_t *out, int32_t cap);
 
+/* OpportunisticBatching's SignPod (framework/runtime/framework.go:884-924) of one v1.Pod under one profile
+ * (config_json as for ksg_create; no context, no device): the signature text -- one signer key per fragment
+ * the profile's plugins contribute, equal texts for equal json.Marshal bytes of the reference's fragment
+ * map -- into out (NUL-terminated, *out_len its length).  Returns 1 (signed), 0 (nil: a plugin refused, e.g.
+ * InterPodAffinity for a pod with affinity terms, PodTopologySpread with constraints or defaults), or
+ * KSG_EINVAL (bad JSON, or cap too small). */
+int ksg_debug_pod_signature(const char *config_json, size_t config_len, const char *pod_json, size_t pod_len, char *out,
+                            size_t cap, size_t *out_len);
+
 /* Parity diagnostics of the node-sharded exchange (no device needed), so host-side protocol tests drive the
  * layout the kernels use rather than a copy of it.  ksg_debug_exchange_layout fills out[0..20] with
  * kMaxShards, the all-reduce word indices XA_CNT, XA_BELOW, XA_NONIGN, XA_MAX_TAINT, XA_MAX_NA, XA_MAX_IPA,

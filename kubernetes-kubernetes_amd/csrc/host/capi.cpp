@@ -450,6 +450,32 @@ int ksg_debug_pod_resources(const char* pod_json, size_t len, int64_t* out, int3
   return 8;
 }
 
+int ksg_debug_pod_signature(const char* config_json, size_t config_len, const char* pod_json, size_t pod_len, char* out,
+                            size_t cap, size_t* out_len) {
+  using namespace ksg;
+  if (!pod_json || !out || !out_len) return KSG_EINVAL;
+  try {
+    Config cfg;
+    PodSpec p;
+    std::string err, sig;
+    if (config_json && config_len && !decode_config(config_json, config_len, &cfg, &err)) return KSG_EINVAL;
+    if (!decode_pod(pod_json, pod_len, &p, &err)) return KSG_EINVAL;
+    // the request Fit signs: the spec's (fit.go:317-325), as the cycle compile takes it
+    const PodResources fit = p.has_status_res ? calc_fit_request(p) : calc_resources(p);
+    if (!sign_text(cfg, p, fit, &sig)) {
+      *out_len = 0;
+      if (cap) out[0] = 0;
+      return 0;
+    }
+    if (sig.size() + 1 > cap) return KSG_EINVAL;
+    std::memcpy(out, sig.c_str(), sig.size() + 1);
+    *out_len = sig.size();
+    return 1;
+  } catch (const std::exception&) {
+    return KSG_EINVAL;
+  }
+}
+
 int ksg_debug_exchange_layout(int32_t* out, int32_t cap) {
   using namespace ksg;
   const int32_t v[] = {kMaxShards, XA_CNT,   XA_BELOW, XA_NONIGN,  XA_MAX_TAINT, XA_MAX_NA,   XA_MAX_IPA,

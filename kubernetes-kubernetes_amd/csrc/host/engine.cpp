@@ -25,6 +25,27 @@
 
 namespace ksg {
 
+// KSG_HOST_TRACE=1: each rank thread's host steps inside run_batch (microseconds since the process's first
+// mark), printed to stderr when the call returns -- where a thread waited while its peers' loops spun.
+static bool htrace_on() {
+  static const bool on = [] { const char* e = std::getenv("KSG_HOST_TRACE"); return e && *e == '1'; }();
+  return on;
+}
+static thread_local std::string g_htrace;
+static void htrace(const char* what, long a = -1) {
+  if (!htrace_on()) return;
+  static const auto t0 = std::chrono::steady_clock::now();
+  char b[96];
+  std::snprintf(b, sizeof b, " %.0f:%s%s%ld", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(),
+                what, a >= 0 ? "=" : "", a >= 0 ? a : 0L);
+  g_htrace += b;
+}
+static void htrace_flush(int rank) {
+  if (!htrace_on() || g_htrace.empty()) return;
+  std::fprintf(stderr, "[htrace rank %d]%s\n", rank, g_htrace.c_str());
+  g_htrace.clear();
+}
+
 hipError_t launch_filter_score(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, hipEvent_t t0,
                                hipEvent_t t1, int blk0, int nblk, bool lds);
 hipError_t launch_select(const MirrorView& m, const BatchView& b, int pod, hipStream_t s, bool lds);
@@ -1001,7 +1022,18 @@ bool Engine::ob_acting() const {
 // frameworkImpl.SignPod (framework.go:884-924): the fragments of the profile's plugins keyed by signer
 // name, nil (-1) when a plugin refuses; equal texts <=> equal json.Marshal bytes.  Interned per context.
 int32_t Engine::sign(const PodSpec& p, const PodResources& fit) {
-  const Config& k = c->cfg;
+  std::string o;
+  if (!sign_text(c->cfg, p, fit, &o)) return -1;
+  auto it = ob_sigs_.find(o);
+  if (it != ob_sigs_.end()) return it->second;
+  const int32_t id = (int32_t)ob_sigs_.size();
+  ob_sigs_.emplace(std::move(o), id);
+  return id;
+}
+
+// The signature text itself: one "|key=value" per signer key the profile's plugins contribute (each key once,
+// as the reference's fragment map holds it), false for a nil signature (a plugin refused: SignPod returns nil).
+bool sign_text(const Config& k, const PodSpec& p, const PodResources& fit, std::string* out) {
   const PodSpec::Sign& f = p.sign;
   std::string o = "sched=" + f.sched;
   if (k.enabled[P_FIT] || k.enabled[P_BAL]) {  // Fit / BalancedAllocation: computePodResourceRequest
@@ -1018,22 +1050,19 @@ int32_t Engine::sign(const PodSpec& p, const PodResources& fit) {
   }
   if (k.enabled[P_TAINT] || k.enabled[P_UNSCHED]) o += "|tol=" + f.tols;
   if (k.enabled[P_IPA]) {  // interpodaffinity/plugin.go:62-78
-    if (p.has_pod_affinity || p.has_pod_anti) return -1;
+    if (p.has_pod_affinity || p.has_pod_anti) return false;
     if (!k.ignore_pref_existing) o += "|lbl=" + f.labels;
   }
   if (k.enabled[P_PORTS]) o += "|ports=" + f.ports;
-  if (k.enabled[P_PTS] && (!p.spreads.empty() || k.pts_system_defaulted || !k.pts_defaults.empty())) return -1;
+  if (k.enabled[P_PTS] && (!p.spreads.empty() || k.pts_system_defaulted || !k.pts_defaults.empty())) return false;
   if (k.enabled[P_NA]) o += "|na=" + f.na + "|nsel=" + f.nsel;
   if (k.enabled[P_NODENAME]) o += "|nn=" + p.node_name;
   if (k.enabled[P_IMG]) o += "|img=" + f.images;
   o += "|vol=" + f.vols;  // the four volume plugins
-  if (f.claims) return -1;  // DynamicResources
-  o += "|feat=";            // NodeDeclaredFeatures: nothing required (else the pod is refused at compile)
-  auto it = ob_sigs_.find(o);
-  if (it != ob_sigs_.end()) return it->second;
-  const int32_t id = (int32_t)ob_sigs_.size();
-  ob_sigs_.emplace(std::move(o), id);
-  return id;
+  if (f.claims) return false;  // DynamicResources
+  o += "|feat=";               // NodeDeclaredFeatures: nothing required (else the pod is refused at compile)
+  *out = std::move(o);
+  return true;
 }
 
 int64_t Engine::ob_now() const {
@@ -1501,7 +1530,10 @@ static void tc_plan(const std::vector<CompiledPod>& cp, int i, int j, uint32_t* 
 int Engine::run_batch_api(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                           ksg_result* results, ksg_eval_out* eval) {
   fault_first_ = -1;
+  htrace("batch", (long)pods.size());
   const int rc = run_batch(pods, handles, assume, results, eval);
+  htrace("ret", rc < 0 ? -rc : rc);
+  htrace_flush(comm ? c->cfg.rank : 0);
   if (fault_first_ >= 0) ++loop_give_ups_;
   if (!comm || !c->cfg.nccl_id.empty() || eval) return rc;
   // In-process groups (one device): every rank learns every rank's outcome before anyone retries.  A loop
@@ -1699,6 +1731,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     c->reserve_ports((int32_t)distinct.size());
   }
   const auto Tm = clk::now();
+  htrace("mirror");
   if ((rc = c->ensure_mirror(pods_needed))) return rc;
   if (ob_acting() && (rc = ob_sync(c->stream))) return rc;
   mirror_us_ = std::chrono::duration<double, std::micro>(clk::now() - Tm).count();
@@ -1712,7 +1745,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   }
   if (compiled < n)  // room for the chunks still to be compiled (re-sized after a sync if they outgrow it)
     desc_bytes = std::max(desc_bytes * 2 * (size_t)n / (size_t)compiled, (size_t)n * 1024);
+  htrace("scratch");
   if ((rc = ensure_scratch(desc_bytes, n, eval != nullptr, arena_words))) return rc;
+  htrace("scratched");
   const size_t meta = ((size_t)n * 8 + 15) & ~size_t(15);
   const size_t meta_all = meta + (((size_t)n * (sizeof(PodStats) + sizeof(DevResult) + 4) + 15) & ~size_t(15));
   uint8_t* hp = nullptr;
@@ -1776,16 +1811,21 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       }
       o += cp[i].blob.size();
     }
+    htrace("h2d", (long)(o - o0));
     if (b > a) {
       HIPCHK(hipMemcpyAsync((uint8_t*)d_descs.p + o0, hdesc + o0, o - o0, hipMemcpyHostToDevice, st_));
+      htrace("c1");
       if (a == 0 && b == n) {  // the whole batch: offsets, sizes and stats are one contiguous range
         HIPCHK(hipMemcpyAsync(d_meta.p, hp, meta + (size_t)n * sizeof(PodStats), hipMemcpyHostToDevice, st_));
       } else {
         HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + a, h_offs + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice, st_));
+        htrace("c2");
         HIPCHK(hipMemcpyAsync((uint32_t*)d_off.p + n + a, h_offs + n + a, (size_t)(b - a) * 4, hipMemcpyHostToDevice,
                               st_));
+        htrace("c3");
         HIPCHK(hipMemcpyAsync((PodStats*)d_stats.p + a, hs + a, (size_t)(b - a) * sizeof(PodStats),
                               hipMemcpyHostToDevice, st_));
+        htrace("c4");
       }
     }
     if (async) {
@@ -1926,6 +1966,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       HIPCHK(hipStreamWaitEvent(cstream, pev[2 * chunks.size() + 1], 0));
       ds = cstream;
     }
+    htrace("close", upto);
     HIPCHK(hipMemcpyAsync(hr + a, (DevResult*)d_results.p + a, (size_t)(upto - a) * sizeof(DevResult),
                           hipMemcpyDeviceToHost, ds));
     if (use_loop || use_agg) HIPCHK(hipMemcpyAsync(hfail + chunks.size(), d_fail.p, 4, hipMemcpyDeviceToHost, ds));
@@ -2032,9 +2073,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // compile + stage the chunk starting at pod i while the device runs the chunks before it
   auto next_chunk = [&](int i) -> int {
     const int b = chunk_end(i);
+    htrace("compile", i);
     c->defer_relayout = true;  // the earlier chunks' assumes are not in the shadow yet
     int r2 = compile_upto(b);
     c->defer_relayout = false;
+    htrace("compiled", b);
     auto drain = [&]() -> int {  // close chunk k, wait for both streams
       if ((chunks.empty() || chunks.back().b < i) && close_chunk(i)) return KSG_EDEVICE;
       HIPCHK(hipStreamSynchronize(s));
@@ -2062,6 +2105,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (c->layout_dirty || (c->pods_dirty && pods_needed) || o + need > desc_cap || aw > arena_words) {
       // the mirror must be re-laid out or the buffers grown: drain the device and mirror what it
       // assumed first (the same state a batch boundary here would give)
+      htrace("drain", i);
       if ((r2 = drain())) return r2;
       if (c->cfg.loop_stamps)
         std::fprintf(stderr, "[host] pipeline drained before pod %d (%s)\n", i,
@@ -2079,7 +2123,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       map_pinned();
       bv = bview(n);
     }
-    return stage(i, b);
+    htrace("stage", i);
+    r2 = stage(i, b);
+    htrace("staged", i);
+    return r2;
   };
   for (int i = 0; i < n && (!comm || dx);) {
     if (i > 0 && std::binary_search(bnd.begin(), bnd.end(), i) && (chunks.empty() || chunks.back().b < i)) {
@@ -2119,12 +2166,14 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       lv.wave_map = c->cfg.loop_wave_map;
       lv.wstamps = c->cfg.loop_stamps ? (unsigned long long*)d_stamps.p + (size_t)n * 8 + 64 + (size_t)i * GS * 8 : nullptr;
       // in-process ranks: every rank is past its allocations before any rank's first loop starts
+      if ((runs.empty() || regate) && comm) htrace("gate", i);
       if ((runs.empty() || regate) && comm && comm->launch_gate()) {
         c->err = comm->err;
         return KSG_EDEVICE;
       }
       regate = false;
       const bool tl = loop_timed(runs.size());
+      htrace("loop", i);
       HIPCHK(launch_sched_loop(m, bv, lv, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr,
                                unit));
       runs.push_back({i, j - i, rb, false, tl});
@@ -2276,7 +2325,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     for (size_t k = (size_t)settled; k < chunks.size(); ++k) {
       const auto Tw = clk::now();
       const double s0 = settle_us;
+      htrace("wait", (long)k);
       HIPCHK(hipEventSynchronize(cev[k]));
+      htrace("waited", (long)k);
       const double wt = std::chrono::duration<double, std::micro>(clk::now() - Tw).count();
       if ((use_loop || use_agg) && hfail[k]) return loop_fault(chunks[k].a, fault_detail());
       if ((rc = settle(chunks[k].a, chunks[k].b))) return rc;

@@ -253,6 +253,8 @@ struct Config {
   Config();
 };
 bool decode_config(const char* p, size_t n, Config* c, std::string* err);
+// SignPod's text for profile k (Engine::sign interns it); false: a nil signature (framework.go:884-924)
+bool sign_text(const Config& k, const PodSpec& p, const PodResources& fit, std::string* out);
 bool valid_ns_term(const NSTerm& t);
 
 // ===================================================================================

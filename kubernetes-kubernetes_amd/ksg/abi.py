@@ -165,6 +165,10 @@ class Backend:
         except Exception:
             pass
 
+    def last_error(self):
+        """The context's last error text (ksg_last_error); after a recovered loop give-up, its detail."""
+        return self.f["last_error"](self.ctx).decode(errors="replace")
+
     def _chk(self, rc, what):
         if rc < 0:
             raise KsgError(f"{what}: rc={rc}: {self.f['last_error'](self.ctx).decode(errors='replace')}")

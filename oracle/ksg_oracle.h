@@ -56,6 +56,9 @@ int ksgo_set_clock(ksgo_ctx *ctx, int64_t now_ns);
 /* one TestBatchBasic case through the OpportunisticBatch restatement (oracle.cpp) */
 int ksgo_debug_batch_basic(const char *json, size_t len, char *out, size_t cap);
 int ksgo_debug_pod_resources(const char *json, size_t len, int64_t *out, int32_t cap);
+/* SignPod of one pod under one profile, as ksg_debug_pod_signature (1 signed, 0 nil) */
+int ksgo_debug_pod_signature(const char *cfg, size_t cfg_len, const char *json, size_t len, char *out, size_t cap,
+                             size_t *out_len);
 /* container/heap Init over (score) with nodeScoreHeap.Less, returns index of the root. */
 int32_t ksgo_heap_root(const int64_t *scores, int32_t n);
 

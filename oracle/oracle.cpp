@@ -21,6 +21,7 @@
 #include <climits>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <cmath>
@@ -2708,6 +2709,31 @@ int ksgo_debug_pod_resources(const char* json, size_t len, int64_t* out, int32_t
   const int64_t o[8] = {r.res.milliCPU, r.res.memory, r.res.ephemeral, r.non0CPU, r.non0Mem, fit[0], fit[1], fit[2]};
   for (int k = 0; k < 8; ++k) out[k] = o[k];
   return 8;
+}
+
+// SignPod of one pod under one profile (sign_pod above), as ksg_debug_pod_signature: 1 signed (text in out),
+// 0 nil, KSG_EINVAL on bad input.
+int ksgo_debug_pod_signature(const char* cfg, size_t cfg_len, const char* json, size_t len, char* out, size_t cap,
+                             size_t* out_len) {
+  if (!json || !out || !out_len) return KSG_EINVAL;
+  std::unique_ptr<ksgo_ctx, void (*)(ksgo_ctx*)> c(ksgo_create(cfg, cfg_len), ksgo_destroy);
+  if (!c) return KSG_EINVAL;
+  std::string err, sig;
+  Pod p;
+  try {
+    if (!decode_pod(mj::parse(json, len), &p, &err)) return KSG_EINVAL;
+  } catch (const std::exception&) {
+    return KSG_EINVAL;
+  }
+  if (!sign_pod(c.get(), p, &sig)) {
+    *out_len = 0;
+    if (cap) out[0] = 0;
+    return 0;
+  }
+  if (sig.size() + 1 > cap) return KSG_EINVAL;
+  std::memcpy(out, sig.c_str(), sig.size() + 1);
+  *out_len = sig.size();
+  return 1;
 }
 
 int32_t ksgo_heap_root(const int64_t* scores, int32_t n) {

@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 # fixtures that are not ksg.h cycles: the OpportunisticBatch state machine (tests/test_batching_oracle.py)
-NOT_CYCLES = {"batch_basic"}
+NOT_CYCLES = {"batch_basic", "signatures"}
 
 
 def load_cases():
