@@ -197,10 +197,13 @@ int ksg_forget(ksg_ctx *ctx, int32_t handle);
  * (GetNodeHint, evaluateNominatedNode: schedule_one.go:650-668,718-752) -- ksg_result.evaluated_nodes 1,
  * feasible_nodes 1, no scores; else it runs the full cycle and stores its own list (StoreScheduleResults).
  * Every pod of a ksg_schedule_one / ksg_schedule_batch call is one scheduling cycle (SchedulingCycle()),
- * and the call reads the clock once: ksg_set_clock(ctx, now_ns) makes it now_ns (a caller's time.Now(),
- * nanoseconds), 0 the wall clock (CLOCK_MONOTONIC).  A node-sharded context refuses such a profile at
- * ksg_create.  ksg_debug_batching: pods placed by a hint so far, and the cycles counted. */
+ * and each cycle reads the clock when it starts (batch.go:202): ksg_set_clock(ctx, now_ns) makes it now_ns (a
+ * caller's time.Now(), nanoseconds), 0 the wall clock (CLOCK_MONOTONIC); ksg_debug_clock_step(ctx, step_ns)
+ * advances that fixed clock by step_ns per cycle (a test's clock that moves inside one call).  A node-sharded
+ * context refuses such a profile at ksg_create.  ksg_debug_batching: pods placed by a hint so far, and the
+ * cycles counted. */
 int ksg_set_clock(ksg_ctx *ctx, int64_t now_ns);
+int ksg_debug_clock_step(ksg_ctx *ctx, int64_t step_ns);
 int ksg_debug_batching(const ksg_ctx *ctx, uint64_t *hinted, uint64_t *cycles);
 
 /* ---- plugin-granular entry points ---------------------------------------------------

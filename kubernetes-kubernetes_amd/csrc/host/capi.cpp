@@ -400,6 +400,12 @@ int ksg_set_clock(ksg_ctx* ctx, int64_t now_ns) {
   return KSG_OK;
 }
 
+int ksg_debug_clock_step(ksg_ctx* ctx, int64_t step_ns) {
+  if (!ctx || step_ns < 0) return KSG_EINVAL;
+  ctx->engine->ob_clock_step_ = step_ns;
+  return KSG_OK;
+}
+
 int ksg_debug_batching(const ksg_ctx* ctx, uint64_t* hinted, uint64_t* cycles) {
   if (!ctx || !hinted || !cycles) return KSG_EINVAL;
   *hinted = ctx->engine->ob_hinted_;

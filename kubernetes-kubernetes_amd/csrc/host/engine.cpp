@@ -1065,8 +1065,12 @@ bool sign_text(const Config& k, const PodSpec& p, const PodResources& fit, std::
   return true;
 }
 
-int64_t Engine::ob_now() const {
-  if (ob_clock_) return ob_clock_;
+int64_t Engine::ob_now() {
+  if (ob_clock_) {  // ksg_set_clock's value; ksg_debug_clock_step advances it by a step per read (cycle)
+    const int64_t v = ob_clock_;
+    ob_clock_ += ob_clock_step_;
+    return v;
+  }
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
@@ -1654,9 +1658,10 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const auto Tv0 = clk::now();
   std::vector<CompiledPod> cp(n);
   int compiled = 0;
-  // OpportunisticBatching: every pod of the call is one scheduling cycle; the call reads the clock once
+  // OpportunisticBatching: every pod of the call is one scheduling cycle, which reads the clock when it starts
+  // (batch.go:202 time.Now(); here at the pod's compile, which precedes its device cycle by at most a chunk)
   const bool ob_on = ob_acting();
-  const int64_t ob_clock = ob_on ? ob_now() : 0;
+  const int64_t ob_clock0 = ob_clock_;
   const int64_t ob_cycle0 = ob_cycle_;
   const int32_t ob_prev0 = ob_prev_sig_;
   // compile pods [compiled, b) against the cache (PreFilter / PreScore on the host)
@@ -1669,7 +1674,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       next_slot_ = -1;
       if (rc) return rc;
       if (cp[i].prefilter_error) cp[i].error = true;  // PreFilter Error: status Error, no launch
-      if (ob_on) ob_sequence(cp[i], *pods[i], ob_clock);
+      if (ob_on) ob_sequence(cp[i], *pods[i], ob_now());
       if (!cp[i].prefilter_reject && !cp[i].prefilter_error && !rotdev()) {
         // nextStartNodeIndex = (old + processed) % len(allNodes) (schedule_one.go:686-687)
         const int64_t N = (int64_t)c->order().size();
@@ -1686,6 +1691,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if ((rc = compile_upto(pipe ? bnd[0] : n))) {  // nothing launched: the batch fails as a whole
       c->next_start = start;
       ob_cycle_ = ob_cycle0;
+      ob_clock_ = ob_clock0;
       ob_prev_sig_ = ob_prev0;
       if (!pre_slot.empty())
         for (int32_t sl : pre_slot) c->pod_table_drop(sl);
@@ -2979,11 +2985,15 @@ int Engine::schedule_resident(const PodSpec& p, int32_t handle, ksg_result* res,
     return KSG_OK;
   }
   *handled = true;
-  if (ob_acting()) {  // a scheduling cycle of an unsigned pod (signed ones take run_batch's path)
+  // a scheduling cycle of an unsigned pod (signed ones take run_batch's path), counted once the pod can no
+  // longer fall back to the launch path (whose run_batch counts it itself)
+  auto ob_count = [&]() {
+    if (!ob_acting()) return;
     ++ob_cycle_;
     ob_prev_sig_ = -1;
-  }
+  };
   if (cp.error || cp.prefilter_reject) {  // decided on the host (run_batch's settle gives the same)
+    ob_count();
     c->pod_table_drop(cp.slot);
     *res = ksg_result{};
     res->status = cp.error ? KSG_CODE_ERROR : KSG_CODE_UNSCHEDULABLE;
@@ -3156,6 +3166,7 @@ relaunch:
     res_q_ = 0;
   }
   // post the pod (and its pod-table entry), wait for its result
+  if (!reposted) ob_count();
   const auto T1 = clk::now();
   const int q = res_q_;
   const uint32_t bytes = (uint32_t)cp.blob.size();

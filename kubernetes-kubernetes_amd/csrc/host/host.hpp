@@ -608,8 +608,9 @@ class Engine {
   int ob_sequence(CompiledPod& cp, const PodSpec& p, int64_t now);  // the cycle's count, clock, hint permission
   int ob_sync(hipStream_t s);      // device state allocated; node indices remapped after a list rebuild
   void ob_invalidate();            // after a device fault: no hint from a state the fault may have torn
-  int64_t ob_now() const;          // time.Now() for a scheduling call (ksg_set_clock, else the wall clock)
+  int64_t ob_now();                // time.Now() of one scheduling cycle (ksg_set_clock, else the wall clock)
   int64_t ob_clock_ = 0;
+  int64_t ob_clock_step_ = 0;      // ksg_debug_clock_step: the fixed clock advances by this per cycle
   int64_t ob_cycle_ = 0;           // SchedulingCycle(): one per scheduling cycle of this context
   int32_t ob_prev_sig_ = -1;       // the previous cycle's signature (-1: nil, or no previous cycle)
   uint64_t ob_list_gen_ = 0;       // the node-list generation the device state's indices refer to

@@ -126,6 +126,7 @@ def _sig(lib, prefix):
       C.POINTER(C.c_int64))
     d("preempt", C.c_int, vp, i32, cp, sz, C.POINTER(PreemptResult), C.c_char_p, sz, C.POINTER(sz))
     d("set_clock", C.c_int, vp, C.c_int64)
+    d("debug_clock_step", C.c_int, vp, C.c_int64)
     return f
 
 
@@ -315,6 +316,10 @@ class Backend:
     def set_clock(self, now_ns):
         """time.Now() of the next scheduling calls, ns (OpportunisticBatching's maxBatchAge); 0: the wall clock."""
         self._chk(self.f["set_clock"](self.ctx, int(now_ns)), "set_clock")
+
+    def clock_step(self, step_ns):
+        """The fixed clock advances by step_ns per scheduling cycle (ksg_debug_clock_step)."""
+        self._chk(self.f["debug_clock_step"](self.ctx, int(step_ns)), "debug_clock_step")
 
     def preempt(self, handle, args=None, detail_cap=1 << 20):
         """DefaultPreemption PostFilter for a compiled pod: (PreemptResult, detail dict)."""

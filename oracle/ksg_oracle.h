@@ -53,6 +53,7 @@ int ksgo_preempt(ksgo_ctx *ctx, int32_t handle, const char *args_json, size_t ar
 double ksgo_go_log(double x);
 /* time.Now() of the following scheduling cycles (OpportunisticBatching's maxBatchAge); 0: the wall clock */
 int ksgo_set_clock(ksgo_ctx *ctx, int64_t now_ns);
+int ksgo_debug_clock_step(ksgo_ctx *ctx, int64_t step_ns);
 /* one TestBatchBasic case through the OpportunisticBatch restatement (oracle.cpp) */
 int ksgo_debug_batch_basic(const char *json, size_t len, char *out, size_t cap);
 int ksgo_debug_pod_resources(const char *json, size_t len, int64_t *out, int32_t cap);

@@ -630,8 +630,13 @@ struct ksgo_ctx {
   OpportunisticBatch batch;  // frameworkImpl.batch (framework/runtime/framework.go:1620-1626)
   int64_t cycleCount = 0;    // SchedulingQueue.SchedulingCycle(): one per scheduling cycle of this context
   int64_t clockNs = 0;       // ksgo_set_clock: time.Now() of the next cycles (0: the wall clock)
-  int64_t now() const {
-    if (clockNs) return clockNs;
+  int64_t clockStep = 0;     // ksgo_debug_clock_step: the fixed clock advances by this per cycle (per read)
+  int64_t now() {
+    if (clockNs) {
+      const int64_t v = clockNs;
+      clockNs += clockStep;
+      return v;
+    }
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
 
@@ -2166,6 +2171,11 @@ int ksgo_pod_compile(ksgo_ctx* c, const char* json, size_t len, int32_t* handle)
 
 int ksgo_set_clock(ksgo_ctx* c, int64_t now_ns) {
   c->clockNs = now_ns;
+  return KSG_OK;
+}
+int ksgo_debug_clock_step(ksgo_ctx* c, int64_t step_ns) {
+  if (!c || step_ns < 0) return KSG_EINVAL;
+  c->clockStep = step_ns;
   return KSG_OK;
 }
 

@@ -82,3 +82,23 @@ def test_expiry_and_clock():
         lib.ksgo_set_clock(C.c_void_p(o.ctx), t)
         out.append(_hinted(o.schedule_one(o.compile(p), assume=True)[0]))
     assert out == [False, True, True, False, True, True]
+
+
+def test_clock_step_expires_state_inside_a_batch():
+    """ksgo_debug_clock_step: each cycle reads the clock (batch.go:202) and the fixed clock advances per read, so
+    one schedule_batch call expires the stored state (maxBatchAge 500 ms) the way separate cycles would: with
+    a 300 ms step the state a pod stores is 300 ms old at the next pod (hint), then 600 ms at the one after --
+    but each hinted pod keeps the state (its creation time is that of the pod that stored it), so hints come
+    only every second pod."""
+    from ksg.synth import batching
+    nodes, pods = batching(30, 30, "hostport")
+    seq = {}
+    for step in (0, 300):
+        o = oracle(NO_TOPOLOGY)
+        for n in nodes:
+            o.add_node(n)
+        o.set_clock(10 ** 12)
+        o.clock_step(step * 10 ** 6)
+        seq[step] = [_hinted(r) for r in o.schedule_batch([o.compile(p) for p in pods[:8]], assume=True)]
+    assert seq[0] == [False] + [True] * 7
+    assert seq[300] == [False, True, False, True, False, True, False, True]

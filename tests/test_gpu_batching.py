@@ -173,3 +173,25 @@ def test_sharded_context_refuses_an_acting_profile():
     from ksg.native import Scheduler
     with pytest.raises(KsgError, match="OpportunisticBatching"):
         Scheduler(dict(NO_TOPOLOGY, device=0, distributed={"worldSize": 2, "rank": 0, "localGroup": "ob-refuse"}))
+
+
+@pytest.mark.parametrize("step_ms", [0, 120, 300, 700])
+def test_clock_advancing_inside_a_batch(step_ms):
+    """Each scheduling cycle reads the clock (batch.go:202), not each call: with a fixed clock that advances by
+    step_ms per cycle (ksg_debug_clock_step) inside one schedule_batch call, the device's hint decisions
+    (maxBatchAge expiry included) equal the oracle's pod by pod."""
+    from ksg.synth import batching
+    nodes, pods = batching(200, 240, "hostport")
+    g, o = _pair(NO_TOPOLOGY, nodes)
+    for b in (g, o):
+        b.set_clock(10 ** 15)
+        b.clock_step(step_ms * 10 ** 6)
+    rg = [r.as_tuple() for r in g.schedule_batch([g.compile(p) for p in pods], assume=True)]
+    ro = [r.as_tuple() for r in o.schedule_batch([o.compile(p) for p in pods], assume=True)]
+    assert rg == ro
+    hinted = sum(r[2] == 1 and r[3] == 1 and r[0] == 0 for r in ro)
+    assert g.batching() == (hinted, len(pods))
+    if step_ms >= 500:
+        assert hinted == 0
+    elif step_ms == 300:
+        assert 0 < hinted < len(pods) * 2 // 3
