@@ -177,7 +177,12 @@ enum DescFlags : uint32_t {
   DF_OB = 1u << 23,                // OpportunisticBatching: a signed pod (SignPod non-nil, framework.go:884-924) --
                                    // k_ob_hint may place it on the stored heap's next node, k_ob_store keeps its
                                    // cycle's sorted nodes for the next pod (framework/runtime/batch.go:65-229)
+  DF_NOMINATED = 1u << 24,         // status.nominatedNodeName names a snapshot node (nominated_node): k_nominated
+                                   // runs that node's filters alone first (evaluateNominatedNode, schedule_one.go:
+                                   // 657-669,714-745); feasible: the pod goes there, else the full pass follows
 };
+// a pod the per-pod path may place before its full evaluation (PodStats::ob_done: 1 hint, 2 nominated node)
+constexpr uint32_t DF_EARLY = DF_OB | DF_NOMINATED;
 
 struct PodDesc {
   uint32_t blob_bytes;   // header + blob, 16-byte multiple
@@ -245,6 +250,9 @@ struct PodDesc {
                                        // without a nominated node -- GetNodeHint may find the state usable
   int64_t ob_cycle;                    // SchedulingQueue.SchedulingCycle() of this pod's cycle
   int64_t ob_now;                      // time.Now() of this cycle, ns (maxBatchAge, batch.go:57,208)
+  // ---- evaluateNominatedNode (DF_NOMINATED)
+  int32_t nominated_node;              // snapshot index of status.nominatedNodeName
+  int32_t nom_pad;
 };
 
 // ---- DefaultPreemption: SelectVictimsOnNode per node, one thread each ----------
@@ -355,7 +363,7 @@ struct DevResult {
   uint64_t key;       // winning packed key (debug)
   uint32_t ipa_any;   // PodStats::ipa_any (PreFilter / PreScore Skip decisions taken on the device)
   uint32_t rot_next;  // DF_ROTDEV: nextStartNodeIndex after this pod
-  uint32_t hinted;    // DF_OB: 1 when the pod took the OpportunisticBatching hint (no full evaluation)
+  uint32_t hinted;    // 1: the pod took the OpportunisticBatching hint, 2: its nominated node (no full evaluation)
   uint32_t pad;
 };
 
@@ -381,8 +389,11 @@ struct PodStats {
                                       // (node-sharded: -2 on the ranks that do not hold it)
   int32_t keep[4];                    // node-sharded cut: this rank's kept nodes are the feasible ones in
                                       // [keep[0], keep[1]) or [keep[2], keep[3]) (k_sample_shard_b)
-  uint32_t ob_done;                   // DF_OB: k_ob_hint placed the pod; the full-evaluation kernels return at once
-  uint32_t pad[2];
+  uint32_t ob_done;                   // DF_EARLY: k_ob_hint (1) or k_nominated (2) placed the pod; the full-evaluation
+                                      // kernels return at once
+  uint32_t nom_failed;                // 1 + the snapshot index of a nominated / hinted node whose filters failed alone
+                                      // (its status is in NodeToStatus: processedNodes counts it once), 0: none
+  uint32_t pad;
 };
 
 // OpportunisticBatching's state on the device (framework/runtime/batch.go:31-58): the sorted nodes a signed

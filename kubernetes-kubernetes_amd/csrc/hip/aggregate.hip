@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(MirrorView m, BatchView b,
 __global__ __launch_bounds__(kBlock) void k_pts_score(MirrorView m, BatchView b, int pod, int blk0) {
   {  // OpportunisticBatching: placed by k_ob_hint, no scores (kernels.hip ob_skip)
     const PodDesc* pd = reinterpret_cast<const PodDesc*>(b.descs + b.desc_off[pod]);
-    if ((pd->flags & DF_OB) && b.stats[pod].ob_done) return;
+    if ((pd->flags & DF_EARLY) && b.stats[pod].ob_done) return;
   }
   const uint8_t* base = b.descs + b.desc_off[pod];
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);

@@ -427,6 +427,10 @@ __device__ __forceinline__ NodeEval eval_node(const MirrorView& m, const BatchVi
       const int32_t* sub = at<int32_t>(base, d.subset_off);
       bool in = false;
       for (int k = 0; k < d.subset_cnt; ++k) in |= sub[k] == i;
+      // (a nominated node outside the list that failed alone keeps that status: NodeToStatus holds it, the
+      // absent-node status is only the default, schedule_one.go:657-682; it fails again here, never feasible)
+      if constexpr (kStore)  // (the launch path: nominated pods never run in the persistent loops)
+        in |= (d.flags & DF_NOMINATED) && b.stats[pod].nom_failed == (uint32_t)i + 1u;
       st = in ? 0u : pack_status(C_UU, 15u, KSG_R_PREFILTER);
     }
     if (st == 0) {
@@ -693,11 +697,12 @@ __device__ NodeEval eval_node_fast(const MirrorView& m, const PodFast& pf, const
   return eval_core_fast(m, nc, bal2(nc.rcpu, nc.acpu, nc.rmem, nc.amem), pf, base, d, i);
 }
 
-// OpportunisticBatching: a pod k_ob_hint placed on the stored heap's next node skips the full evaluation
-// (every launch of its per-pod path returns at once; k_select still clears its histograms)
+// A pod k_ob_hint placed on the stored heap's next node (OpportunisticBatching), or k_nominated on its nominated
+// node, skips the full evaluation (every launch of its per-pod path returns at once; k_select still clears its
+// histograms)
 __device__ __forceinline__ bool ob_skip(const BatchView& b, int pod) {
   const PodDesc* d = reinterpret_cast<const PodDesc*>(b.descs + b.desc_off[pod]);
-  return (d->flags & DF_OB) && b.stats[pod].ob_done;
+  return (d->flags & DF_EARLY) && b.stats[pod].ob_done;
 }
 
 // =====================================================================================================
@@ -1051,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) void k_select(MirrorView m, BatchView b, in
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
   PodStats* ps = b.stats + pod;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if ((d.flags & DF_OB) && ps->ob_done) {  // placed by k_ob_hint: only the histograms to clear
+  if ((d.flags & DF_EARLY) && ps->ob_done) {  // placed by k_ob_hint / k_nominated: only the histograms to clear
     for (int w = blockIdx.x * kBlock + threadIdx.x; w < d.arena_words; w += nblocks * kBlock) b.arena[w] = 0ull;
     return;
   }
@@ -1156,7 +1161,10 @@ __global__ void k_ob_hint(MirrorView m, BatchView b, int pod) {
   st.len = n;
   const int hint = top.node;
   if (hint < 0 || hint >= m.n) return;  // no longer in the snapshot: an error, then the full pass
-  if (run_filters(m, load_core(m, hint), base, d, hint, &rt, at, 0) != 0) return;  // the full pass decides
+  if (run_filters(m, load_core(m, hint), base, d, hint, &rt, at, 0) != 0) {  // the full pass decides
+    ps->nom_failed = (uint32_t)hint + 1u;  // its status is in NodeToStatus (k_sample_find counts it once)
+    return;
+  }
   if (d.flags & DF_ROTDEV) {  // the hint path leaves nextStartNodeIndex alone
     ps->rot_out = d.prev_pod < 0 ? ps->rot_in : b.stats[d.prev_pod].rot_out;
     ps->processed = 1;
@@ -1169,6 +1177,36 @@ __global__ void k_ob_hint(MirrorView m, BatchView b, int pod) {
   st.last_node = hint;
 }
 
+// k_nominated (one thread, after PreFilter and the pod's histograms): evaluateNominatedNode (schedule_one.go:657-669,
+// 714-745) for status.nominatedNodeName -- that node's filters alone (RunFilterPluginsWithNominatedPods: this
+// context tracks no other pod's nomination).  Feasible: the pod is placed there (schedulePod's one-feasible-node
+// path, :586-598; nextStartNodeIndex stays).  Else the node's status joins NodeToStatus (kept for evaluation
+// output, counted once by k_sample_find) and the full pass follows.
+__global__ void k_nominated(MirrorView m, BatchView b, int pod) {
+  if (threadIdx.x != 0) return;
+  const uint8_t* base = b.descs + b.desc_off[pod];
+  const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
+  PodStats* ps = b.stats + pod;
+  if (!(d.flags & DF_NOMINATED) || (d.flags & DF_PREFILTER_REJECT)) return;
+  const int nn = d.nominated_node;
+  if (nn < 0 || nn >= m.n) return;
+  int64_t rt = 0;
+  const uint32_t st = run_filters(m, load_core(m, nn), base, d, nn, &rt, ArenaTopo{ps, b.arena}, 0);
+  if (st != 0) {
+    ps->nom_failed = (uint32_t)nn + 1u;
+    if (d.flags & DF_EVAL_OUT) b.status[nn] = st;
+    return;
+  }
+  if (d.flags & DF_ROTDEV) {
+    ps->rot_out = d.prev_pod < 0 ? ps->rot_in : b.stats[d.prev_pod].rot_out;
+    ps->processed = 1;
+  }
+  commit_result(m, b, base, d, ps, pod, 1u, nn, 0ull);
+  b.results[pod].hinted = 2u;
+  b.results[pod].evaluated = 1;  // EvaluatedNodes = 1 + diagnosis.NodeToStatus.Len() (no failure yet)
+  ps->ob_done = 2u;
+}
+
 // k_ob_store (one workgroup, after k_select): StoreScheduleResults (batch.go:98-158) for a signed pod whose
 // full evaluation placed it.  One feasible node: the state is dropped (nil list).  Otherwise the feasible
 // list's (TotalScore, node) entries k_select wrote in feasible order become newSortedNodeScores' heap
@@ -1177,7 +1215,7 @@ __global__ void k_ob_hint(MirrorView m, BatchView b, int pod) {
 __global__ __launch_bounds__(1024) void k_ob_store(BatchView b, int pod) {
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(b.descs + b.desc_off[pod]);
   PodStats* ps = b.stats + pod;
-  if (!(d.flags & DF_OB) || ps->ob_done) return;
+  if (!(d.flags & DF_OB) || ps->ob_done == 1u) return;  // (placed on its nominated node: the one-node path below)
   const DevResult r = b.results[pod];
   if (r.status != (int32_t)C_OK || r.node < 0) return;  // FitError / Error: nothing stored (schedulePod returns first)
   ObState& st = *b.ob;
@@ -1281,6 +1319,23 @@ __global__ __launch_bounds__(kBlock) void k_sample_find(MirrorView m, BatchView 
       processed = (uint32_t)((end - s + N) % N);
     }
   }
+  if (ps->nom_failed) {  // a nominated / hinted node that failed alone is in NodeToStatus: once more unless the
+                         // full pass reached it (rotated position < processed; outside a PreFilterResult list: never)
+    const int nf = (int)ps->nom_failed - 1;
+    int pos = -1;
+    if (!sub) {
+      pos = (nf - s + N) % N;
+    } else {
+      __shared__ int s_nf;
+      if (threadIdx.x == 0) s_nf = -1;
+      __syncthreads();
+      for (int q = threadIdx.x; q < cnt; q += kBlock)
+        if (subset[q] == nf) s_nf = q;
+      __syncthreads();
+      if (s_nf >= 0) pos = (s_nf - (int)(rot_in % (uint32_t)cnt) + cnt) % cnt;
+    }
+    if (pos < 0 || pos >= (int)processed) ++processed;
+  }
   if (threadIdx.x == 0) {
     ps->rot = (uint32_t)s;
     ps->samp_end = end;
@@ -1314,7 +1369,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_apply(MirrorView m, BatchView
     inproc = i < m.n && (end < 0 || in_cyclic(i, s, end));
   const unsigned long long word = b.fmask[(size_t)blk * (kBlock / 64) + wave];
   const bool kept = inproc && ((word >> lane) & 1ull);
-  if (!shard && (d.flags & DF_EVAL_OUT) && i < m.n && !inproc) b.status[i] = 0u;
+  if (!shard && (d.flags & DF_EVAL_OUT) && i < m.n && !inproc && ps->nom_failed != (uint32_t)i + 1u) b.status[i] = 0u;
   const unsigned long long ballot = __ballot(kept);
   if (lane == 0) b.fmask[(size_t)blk * (kBlock / 64) + wave] = ballot;
   const uint32_t sm = d.score_mask;
@@ -4628,6 +4683,10 @@ hipError_t launch_ob_hint(const MirrorView& m, const BatchView& b, int pod, hipS
   hipLaunchKernelGGL(k_ob_hint, dim3(1), dim3(64), 0, s, m, b, pod);
   return hipGetLastError();
 }
+hipError_t launch_nominated(const MirrorView& m, const BatchView& b, int pod, hipStream_t s) {
+  hipLaunchKernelGGL(k_nominated, dim3(1), dim3(64), 0, s, m, b, pod);
+  return hipGetLastError();
+}
 hipError_t launch_ob_store(const BatchView& b, int pod, hipStream_t s) {
   hipLaunchKernelGGL(k_ob_store, dim3(1), dim3(1024), 0, s, b, pod);
   return hipGetLastError();
@@ -4874,6 +4933,7 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_agg_loop<false, false, false, 1>),
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr),
                       reinterpret_cast<const void*>(&k_ob_hint),            reinterpret_cast<const void*>(&k_ob_store),
+                      reinterpret_cast<const void*>(&k_nominated),
                       reinterpret_cast<const void*>(&k_ob_remap)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);

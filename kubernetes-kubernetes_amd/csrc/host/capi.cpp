@@ -228,6 +228,11 @@ int ksg_pod_compile(ksg_ctx* ctx, const char* pod_json, size_t len, int32_t* han
                  "outside the device path";
       return KSG_ENOTSUP;
     }
+    if (!p.nominated_node.empty() && ctx->engine->comm) {  // evaluateNominatedNode runs on one device's mirror
+      ctx->err = "pod " + p.ns + "/" + p.name + ": status.nominatedNodeName on a node-sharded context (the nominated "
+                 "node's single-node pass is not sharded)";
+      return KSG_ENOTSUP;
+    }
     // the pod's pod-table entry (labels, affinity terms) compiled once, as NewPodInfo does at enqueue
     ctx->cluster->pod_table_precompile(p);
     const int32_t h = ctx->engine->next_handle++;

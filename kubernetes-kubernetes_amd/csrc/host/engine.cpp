@@ -72,6 +72,7 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
 hipError_t warm_kernels();
 hipError_t warm_aggregate();
 hipError_t launch_ob_hint(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
+hipError_t launch_nominated(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
 hipError_t launch_ob_store(const BatchView& b, int pod, hipStream_t s);
 hipError_t launch_ob_remap(ObState* st, ObEnt* h, const int32_t* map, int nold, int maxlen, hipStream_t s);
 hipError_t loop_occupancy(int (&occ)[4]);
@@ -322,6 +323,15 @@ int Engine::compile(const PodSpec& p, Mode mode, int plugin, bool assume, bool e
   if (!p.node_name.empty()) {
     int32_t ix = c->index_of(p.node_name);
     D.node_name = ix >= 0 ? ix : -2;
+  }
+  // evaluateNominatedNode (schedule_one.go:657-669,714-745): a status.nominatedNodeName in the snapshot is tried
+  // alone first (k_nominated); one that is not is an error the reference logs before the full pass
+  if (mode == CYCLE && !p.nominated_node.empty()) {
+    const int32_t ix = c->index_of(p.nominated_node);
+    if (ix >= 0) {
+      D.flags |= DF_NOMINATED;
+      D.nominated_node = ix;
+    }
   }
 
   // TaintToleration: per distinct taint, "not tolerated" bits (taint_toleration.go:102-196)
@@ -1006,8 +1016,9 @@ static bool calc_scalar_free(const PodSpec& p) {  // decided once per pod at dec
 bool Engine::rotdev() const {
   bool any_score = false;
   for (int q : {P_TAINT, P_NA, P_FIT, P_PTS, P_IPA, P_BAL, P_IMG}) any_score |= c->cfg.enabled[q];
-  // (OpportunisticBatching: a hinted pod leaves nextStartNodeIndex alone, which only the device knows)
-  return c->cfg.pct != 100 || !any_score || ob_acting();
+  // (OpportunisticBatching: a hinted pod leaves nextStartNodeIndex alone, which only the device knows; so does
+  // a pod placed on its nominated node, and one whose nominated node failed may count that node once more)
+  return c->cfg.pct != 100 || !any_score || ob_acting() || nom_batch_;
 }
 
 // ---- OpportunisticBatching (framework/runtime/batch.go:31-242) --------------------------
@@ -1138,7 +1149,7 @@ int Engine::ob_sync(hipStream_t s) {
 bool Engine::loop_ok(const CompiledPod& p) const {
   if (p.error) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
-  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_OB)) return false;
+  if (d.flags & (DF_AGGREGATE | DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_EARLY)) return false;
   if (d.score_mask & ((1u << P_PTS) | (1u << P_IPA))) return false;
   // percentageOfNodesToScore / no-score profiles: the loop cuts the list and carries nextStartNodeIndex
   // itself (k_sched_loop), unsharded, over the whole snapshot (no PreFilterResult)
@@ -1150,7 +1161,7 @@ bool Engine::loop_ok(const CompiledPod& p) const {
 bool Engine::agg_loop_ok(const CompiledPod& p) const {
   if (p.error || !p.agg_ok || p.blob.size() > (size_t)kAggBlobLds) return false;
   const PodDesc& d = *reinterpret_cast<const PodDesc*>(p.blob.data());
-  if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET | DF_OB))
+  if (d.flags & (DF_EVAL_OUT | DF_SCORE_ERROR | DF_ALL_FEASIBLE | DF_ROTDEV | DF_PREFILTER_REJECT | DF_SUBSET | DF_EARLY))
     return false;
   // the fold plan holds <= 8 items per kind of the next pod's constraints / terms plus one per own
   // term of the pod just placed (kFoldMax = 80 in k_agg_loop)
@@ -1583,6 +1594,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const int n = (int)pods.size();
   if (n == 0) return KSG_OK;
   if (eval && n != 1) return KSG_EINVAL;
+  struct NomReset {
+    bool* f;
+    ~NomReset() { *f = false; }
+  } nom_reset{&nom_batch_};
+  for (int i = 0; i < n && !nom_batch_; ++i) nom_batch_ = !pods[i]->nominated_node.empty();
   c->order();
   if (c->order().empty()) {  // ErrNoNodesAvailable (schedule_one.go:569-571)
     for (int i = 0; i < n; ++i) results[i] = ksg_result{KSG_CODE_ERROR, -1, 0, 0, 0};
@@ -2005,11 +2021,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         if (!cp[i].error) c->next_start = d.rot_next;  // the last launched pod's wins
       }
       r.total_score = d.feasible > 1 ? d.total : 0;
-      const bool hinted = d.hinted && (reinterpret_cast<const PodDesc*>(cp[i].blob.data())->flags & DF_OB);
-      if (hinted) {  // OpportunisticBatching: the hinted node alone was evaluated (k_ob_hint; other paths
-                     // leave the word unset)
+      const uint32_t early = reinterpret_cast<const PodDesc*>(cp[i].blob.data())->flags & DF_EARLY;
+      if (d.hinted && early) {  // the hinted (k_ob_hint) or nominated (k_nominated) node alone was evaluated
+                                // (other paths leave the word unset)
         r.evaluated_nodes = 1;
-        ++ob_hinted_;
+        if (d.hinted == 1u) ++ob_hinted_;
       }
       if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
       if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
@@ -2277,6 +2293,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     const PodDesc& hd = *reinterpret_cast<const PodDesc*>(cp[i].blob.data());
     const bool lds = cp[i].blob.size() <= (size_t)kBlobLds;
     if (hd.flags & DF_AGGREGATE) HIPCHK(launch_aggregate(m, bv, i, hd, s));
+    if (hd.flags & DF_NOMINATED) HIPCHK(launch_nominated(m, bv, i, s));  // evaluateNominatedNode (counts ready)
     if (hd.flags & DF_OB) HIPCHK(launch_ob_hint(m, bv, i, s));  // GetNodeHint (its counts are ready)
     const bool t = stride > 0 && i % stride == 0;
     if (t) {

@@ -611,6 +611,8 @@ class Engine {
   int64_t ob_now();                // time.Now() of one scheduling cycle (ksg_set_clock, else the wall clock)
   int64_t ob_clock_ = 0;
   int64_t ob_clock_step_ = 0;      // ksg_debug_clock_step: the fixed clock advances by this per cycle
+  bool nom_batch_ = false;         // this batch holds a pod with status.nominatedNodeName (rotdev: its outcome
+                                   // moves nextStartNodeIndex on the device)
   int64_t ob_cycle_ = 0;           // SchedulingCycle(): one per scheduling cycle of this context
   int32_t ob_prev_sig_ = -1;       // the previous cycle's signature (-1: nil, or no previous cycle)
   uint64_t ob_list_gen_ = 0;       // the node-list generation the device state's indices refer to

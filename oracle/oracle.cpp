@@ -1720,6 +1720,7 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
   }
   std::vector<NodeInfoO*> feasible;
   int failed = 0;
+  int visited = numAll;  // rotated positions [0, visited) went through the filters (the rest: cut off)
   auto filter_node = [&](NodeInfoO* ni) {
     Status st;
     for (int p : kFilterOrder) {
@@ -1737,29 +1738,32 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
       if (ev->node_reasons) ev->node_reasons[idx] = st.reasons;
     }
   };
-  // ---- GetNodeHint (schedule_one.go:650-668, batch.go:65-95) and evaluateNominatedNode (:718-752) with the hint:
-  // the hinted node alone through findNodesThatPassFilters; feasible -> it is the result
+  // ---- GetNodeHint (schedule_one.go:650-655, batch.go:65-95), then evaluateNominatedNode (:657-669,714-745) with
+  // the pod's status.nominatedNodeName, else the hint: that node alone through findNodesThatPassFilters;
+  // feasible -> it is the result (nextStartNodeIndex stays), else its status joins NodeToStatus and the full
+  // pass follows.  A name not in the snapshot: GetNodeInPlacement and Get fail, the error is logged
+  // (HandleErrorWithContext) and the full pass follows.
   std::string hint;
-  int hintFailed = -1;  // a hinted node that failed its filters (its status is in NodeToStatus)
-  if (ob) {
+  int hintFailed = -1;  // a nominated / hinted node that failed its filters (its status is in NodeToStatus)
+  if (ob)
     hint = c->batch.GetNodeHint(sig, pod.nominatedNodeName, cycleCount, now, [&](const std::string& nm) {
       NodeInfoO* ni = c->snapMap.count(nm) ? c->nodes[nm].get() : nullptr;  // nodeInfos.Get
       if (!ni) return -1;
       return filter_node(ni).ok() ? 0 : 1;  // RunFilterPlugins: IsRejected
     });
-    if (!hint.empty() && c->snapMap.count(hint)) {  // GetNodeInPlacement: else an error, and the full pass
-      NodeInfoO* hn = c->nodes[hint].get();
-      Status st = filter_node(hn);
-      if (st.ok()) {  // schedulePod's one-feasible-node path (:588-598)
-        c->batch.StoreScheduleResults(sig, hint, hint, nullptr, cycleCount, now);
-        res->node_index = idx_of(hn);
-        res->feasible_nodes = 1;
-        res->evaluated_nodes = 1;
-        return KSG_OK;
-      }
-      record_failed(hn, st);
-      hintFailed = idx_of(hn);
+  const std::string& nnn = !pod.nominatedNodeName.empty() ? pod.nominatedNodeName : hint;
+  if (!nnn.empty() && c->snapMap.count(nnn)) {
+    NodeInfoO* hn = c->nodes[nnn].get();
+    Status st = filter_node(hn);
+    if (st.ok()) {  // schedulePod's one-feasible-node path (:586-598)
+      if (ob) c->batch.StoreScheduleResults(sig, hint, nnn, nullptr, cycleCount, now);
+      res->node_index = idx_of(hn);
+      res->feasible_nodes = 1;
+      res->evaluated_nodes = 1;
+      return KSG_OK;
     }
+    record_failed(hn, st);
+    hintFailed = idx_of(hn);
   }
   if (c->pool && numToFind >= numAll) {
     // CPU-baseline mode: Parallelizer.Until's chunks of the rotated order (schedule_one.go:840), then
@@ -1795,7 +1799,10 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
       NodeInfoO* ni = nodes[(c->nextStartNodeIndex + i) % numAll];
       Status st = filter_node(ni);
       if (st.ok()) {
-        if ((int64_t)feasible.size() + 1 > numToFind) break;  // cancel: enough feasible nodes
+        if ((int64_t)feasible.size() + 1 > numToFind) {  // cancel: enough feasible nodes
+          visited = i;
+          break;
+        }
         feasible.push_back(ni);
       } else {
         ++failed;
@@ -1804,9 +1811,10 @@ static int run_cycle(ksgo_ctx* c, const Pod& pod, ksg_result* res, ksg_eval_out*
     }
   }
   double T2 = nowus(); c->prof[1] += T2 - T1;
-  if (hintFailed >= 0) {  // NodeToStatus is keyed by node: the hinted node counts once
+  if (hintFailed >= 0) {  // NodeToStatus is keyed by node: the nominated / hinted node counts once -- again only if
+                          // the full pass reached it (it fails there too: same state, same filters)
     bool again = false;
-    for (auto* ni : nodes) again = again || idx_of(ni) == hintFailed;
+    for (int i = 0; i < visited && !again; ++i) again = idx_of(nodes[(c->nextStartNodeIndex + i) % numAll]) == hintFailed;
     if (!again) ++failed;
   }
   int processed = (int)feasible.size() + failed;

@@ -850,6 +850,10 @@ class PodB(Builder):
         self.o["spec"]["priority"] = p
         return self
 
+    def m_NominatedNodeName(self, n):  # wrappers.go: Status.NominatedNodeName
+        self.o.setdefault("status", {})["nominatedNodeName"] = n
+        return self
+
     def m_OwnerReference(self, name, gvk):  # wrappers.go:353-363: a controller reference
         self.o["metadata"]["ownerReferences"] = [{"apiVersion": gvk["apiVersion"], "kind": gvk["kind"],
                                                    "name": name, "controller": True}]
