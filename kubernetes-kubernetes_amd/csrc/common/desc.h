@@ -9,6 +9,7 @@
 //    (the work upstream does in PreFilter/PreScore) and consumed by every node thread.
 // Plain C++ PODs only -- this header is included by .cpp (g++/hipcc host) and .hip files.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #if defined(__HIP__) || defined(__HIPCC__)
@@ -616,8 +617,11 @@ constexpr int kGran = 4;
 // A persistent loop's give-up record (LoopView::fail / AggView::fail): [0] flag, [1] pod of the run
 // (the granule row; or a k_agg_loop check code), [2] granule (or workgroup), [3] first missing sweep
 // lane, [4] loop (1 k_sched_loop, 2 k_agg_loop), [5] its granule tag, [6, 7] the sweep's missing-lane
-// ballot at the give-up (lane l: some participant l + 64 k had not published)
-constexpr int kFailWords = 8;
+// ballot at the give-up (lane l: some participant l + 64 k had not published); the launch's entry, written by
+// workgroup 0 while no give-up is recorded: [8] its HW_ID register (ME / pipe / HQD it was dispatched from),
+// [9] its XCC, [10, 11] s_memrealtime at entry; [12, 13] s_memrealtime at the give-up, [14] the giving-up
+// wave's HW_ID, [15] its XCC (a rank whose loop entered after a peer gave up was not resident with it)
+constexpr int kFailWords = 16;
 constexpr int kFailBytes = kFailWords * 4;
 
 // ---- persistent loop for pods with pod-table aggregation (k_agg_loop) ---------------
@@ -704,6 +708,24 @@ struct AggView {
   unsigned long long* tcache;
   const uint32_t* tcw;
 };
+// In-process rank groups (localGroup, one device) run every rank's persistent loop in one dispatch
+// (k_sched_loop_group / k_agg_loop_group): rank r's launch arguments, [world] of them in device
+// memory, staged by the group's leader.
+struct LoopGroupArg {
+  MirrorView m;
+  BatchView b;
+  LoopView lv;
+};
+struct AggGroupArg {
+  MirrorView m;
+  BatchView b;
+  AggView av;
+};
+// (the single-device loop kernels read their three by-value arguments through these layouts: the kernarg segment
+// places each argument at the next multiple of its alignment, as a struct places its members)
+static_assert(offsetof(LoopGroupArg, b) == sizeof(MirrorView) && offsetof(LoopGroupArg, lv) == sizeof(MirrorView) + sizeof(BatchView) &&
+              offsetof(AggGroupArg, av) == sizeof(MirrorView) + sizeof(BatchView) && alignof(MirrorView) == 8 &&
+              alignof(BatchView) == 8 && alignof(LoopView) == 8 && alignof(AggView) == 8, "kernel argument layout");
 // k_agg_loop's template cache: a pod's counts are a function of its template (the program but for the fields
 // agg_same masks) and of the pods placed before it.  Each workgroup keeps the counts of up to kAggTc templates
 // in HBM, current through the last placement, so a pod of a cached template loads them instead of gathering.

@@ -1775,6 +1775,29 @@ __device__ __forceinline__ void gran_put(const LoopView& lv, int q, int gid, int
   for (int r = 0; r < lv.world; ++r) __hip_atomic_store(lv.gran[r] + at, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The hardware registers a give-up record names (desc.h kFailWords): HW_ID (gfx9 layout: pipe [7:6], HQD
+// [26:24], ME [31:30]) and XCC_ID, read with s_getreg (no memory access)
+__device__ __forceinline__ uint32_t hw_id_reg() { return (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4); }
+__device__ __forceinline__ uint32_t xcc_id_reg() { return (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); }
+// fail words 8..11: the launch's entry, by (the rank's) workgroup 0's first lane, unless a give-up is already recorded
+__device__ __forceinline__ void loop_entry_record(uint32_t* fail, int w) {
+  if (!fail || w != 0 || threadIdx.x != 0 || __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return;
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __hip_atomic_store(fail + 8, hw_id_reg(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fail + 9, xcc_id_reg(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fail + 10, (uint32_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fail + 11, (uint32_t)(t >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// fail words 12..15: the give-up's time and the giving-up wave's hardware ids
+__device__ __forceinline__ void give_up_record(uint32_t* fail) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  __hip_atomic_store(fail + 12, (uint32_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fail + 13, (uint32_t)(t >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fail + 14, hw_id_reg(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(fail + 15, xcc_id_reg(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One wave: poll granules [slot0, slot0 + NS) of all P participants of pod q in the local array
 // until every tag matches (relaxed loads, s_sleep between passes).  x[s][r] = payload of
 // participant lane + 64 r; false on give-up.
@@ -1815,6 +1838,7 @@ __device__ __forceinline__ bool gran_sweep(const LoopView& lv, int q, int slot0,
         __hip_atomic_store(lv.fail + 5, (uint32_t)lv.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(lv.fail + 6, (uint32_t)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(lv.fail + 7, (uint32_t)(miss >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        give_up_record(lv.fail);
         __hip_atomic_store(lv.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
@@ -1976,8 +2000,11 @@ __constant__ int8_t kWaveMap[3][kLoopThreads / 64] = {{0, 1, 2, 3, 4, 5}, {4, 0,
 // RING: the resident instance (pods through lv.ring, one run per pod); the batch instance has no run
 // loop at all (its one run is the whole launch), so its code is what it was before the ring existed.
 // MS: sweep rounds of 64 participants (the one-round instance for grids of at most 64: no masked-off rounds)
-template <int NW, bool RING, int MS = kMaxSweep>
-__global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
+// (the body of k_sched_loop and k_sched_loop_group: w = the workgroup this block plays in its rank)
+// (GRP: the group instance takes w from its block index; the others read blockIdx.x itself, as before the group
+// instance existed -- their register allocation is that sensitive)
+template <int NW, bool RING, int MS, bool GRP>
+__device__ __forceinline__ void sched_loop_body(const MirrorView& m, const BatchView& b, const LoopView& lv, const int w_grp) {
   constexpr int U = NW * 64;                  // nodes per unit: one per evaluation-wave lane
   constexpr int kLoopThreads = U + 128;       // NW evaluation waves, one selection wave, one helper wave
   __shared__ __align__(16) uint8_t s_blob[3][kBlobLds];  // pod p's program in s_blob[p % 3]
@@ -2010,7 +2037,8 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   // percentageOfNodesToScore (DF_ROTDEV): s_rot[p & 1] = pod p's rotation start (nextStartNodeIndex),
   // s_proc = the decided pod's processedNodes (schedule_one.go:686-687, 809-824)
   __shared__ uint32_t s_rot[2], s_proc;
-  const int w = blockIdx.x, G = lv.nwg;
+  const int w = GRP ? w_grp : (int)blockIdx.x, G = lv.nwg;
+  if constexpr (!RING) loop_entry_record(lv.fail, w);  // (the resident instance is never sharded)
   const int gid = lv.rank * G + w, P = lv.world * G;  // my participant index, participants (rank-major)
   // my node units [k0, k1) of the rank's range (lv.blk0 / lv.nblk count 256-node blocks)
   const int ub0 = lv.blk0 * (kBlock / U), unb = lv.nblk * (kBlock / U);
@@ -2276,7 +2304,7 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
     // (relay: workgroup 0 polls the host and relays the word through device memory, where the other workgroups
     // poll: one PCIe poller instead of G; a staged program is still read from the host's ring by all)
     if (threadIdx.x == 0) {
-      const bool hostp = lv.relay == nullptr || blockIdx.x == 0;
+      const bool hostp = lv.relay == nullptr || blockIdx.x == 0;  // (RING: never GRP)
       const unsigned long long v = ring_wait_ctl(hostp ? &lv.ring->ctl : lv.relay, hostp ? &lv.ring->exited : nullptr,
                                                  run0, lv.npods, lv.ring_idle);
       if (lv.relay && hostp) __hip_atomic_store(lv.relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // stops too
@@ -2742,6 +2770,23 @@ __global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, Batc
   run0 = run_end;
   }
 }
+// The views are read where the kernel arguments lie (the kernarg segment, laid out as LoopGroupArg): binding the
+// by-value parameters to the body's references made the compiler copy them into registers up front (scratch spills)
+template <int NW, bool RING, int MS = kMaxSweep>
+__global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop(MirrorView m, BatchView b, LoopView lv) {
+  const LoopGroupArg& a = *(const LoopGroupArg*)__builtin_amdgcn_kernarg_segment_ptr();
+  sched_loop_body<NW, RING, MS, false>(a.m, a.b, a.lv, 0);
+}
+// In-process rank groups (localGroup: W contexts on one device): every rank's loop in ONE dispatch, block
+// r * G + w playing rank r's workgroup w with rank r's views.  Loops of separate dispatches on separate
+// hardware queues are not co-scheduled by the command processor (one rank's loop entered only
+// when its peers gave up); the workgroups of one dispatch that fits the device are.
+template <int NW, int MS>
+__global__ __launch_bounds__(NW * 64 + 128) void k_sched_loop_group(const LoopGroupArg* __restrict__ ga, int G) {
+  const int r = (int)blockIdx.x / G;
+  const LoopGroupArg& a = ga[r];
+  sched_loop_body<NW, false, MS, true>(a.m, a.b, a.lv, (int)blockIdx.x - r * G);
+}
 
 
 // =====================================================================================================
@@ -2902,6 +2947,7 @@ __device__ __forceinline__ bool agran_sweep(const AggView& av, int q, int slot0,
           __hip_atomic_store(av.fail + 5, (uint32_t)av.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(av.fail + 6, (uint32_t)miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(av.fail + 7, (uint32_t)(miss >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          give_up_record(av.fail);
         }
         return false;
       }
@@ -2945,8 +2991,9 @@ __device__ __forceinline__ void apply_entry(const MirrorView& m, const uint8_t* 
 // end of the pod before it), no staging ahead.
 // MS: sweep rounds of 64 participants (kMaxSweep = 4: up to 256; the 1-round instance for grids of at most 64
 // workgroups holds a quarter of the exchange registers, which pays for the PodTopologySpread PX skip, as in RING)
-template <bool SHARD, bool PTSS, bool RING = false, int MS = kMaxSweep>
-__global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
+// (the body of k_agg_loop and k_agg_loop_group: w = the workgroup this block plays in its rank)
+template <bool SHARD, bool PTSS, bool RING, int MS, bool GRP>
+__device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchView& b, const AggView& av, const int w_grp) {
   constexpr bool kPxa = RING || MS < kMaxSweep;  // phase 1 guesses the PTS raw scores (AG_PXA)
   constexpr int kBlob = RING ? kBlobLds : kAggBlobLds;       // program slot bytes (desc.h)
   constexpr uint32_t kLp = RING ? kAggRingPods : kAggPods;     // LDS list entries (the rest spill to HBM)
@@ -3019,7 +3066,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
   // (the batch instance's template cache borrows a resident-mode doorbell word: pod q-1's node's eligibility under
   // q+1's template)
   uint32_t& s_elp = s_ll[0];
-  const int w = blockIdx.x, G = av.nwg;
+  const int w = GRP ? w_grp : (int)blockIdx.x, G = av.nwg;
+  loop_entry_record(av.fail, w);
   const int P = SHARD ? av.world * G : G, gid = SHARD ? av.rank * G + w : w;  // participants (rank-major), mine
   const int k0 = av.blk0 + (int)((int64_t)av.nblk * w / G), k1 = av.blk0 + (int)((int64_t)av.nblk * (w + 1) / G);
   const int nk = k1 - k0;  // <= kLoopMaxBlk (host-checked)
@@ -4646,6 +4694,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchVie
     stamp(q, 8);
   }
 }
+template <bool SHARD, bool PTSS, bool RING = false, int MS = kMaxSweep>
+__global__ __launch_bounds__(kAggThreads) void k_agg_loop(MirrorView m, BatchView b, AggView av) {
+  const AggGroupArg& a = *(const AggGroupArg*)__builtin_amdgcn_kernarg_segment_ptr();  // (k_sched_loop)
+  agg_loop_body<SHARD, PTSS, RING, MS, false>(a.m, a.b, a.av, 0);
+}
+// In-process rank groups: every rank's node-sharded k_agg_loop in one dispatch (k_sched_loop_group)
+__global__ __launch_bounds__(kAggThreads) void k_agg_loop_group(const AggGroupArg* __restrict__ ga, int G) {
+  const int r = (int)blockIdx.x / G;
+  const AggGroupArg& a = ga[r];
+  agg_loop_body<true, true, false, kMaxSweep, true>(a.m, a.b, a.av, (int)blockIdx.x - r * G);
+}
 
 }  // namespace ksg
 
@@ -4896,6 +4955,37 @@ hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggVie
   }
   return hipGetLastError();
 }
+// A rank's group launch arguments into the leader's device array, stream-ordered (the kernel arguments are
+// copied at enqueue time, and the loop before it on the stream has ended before this overwrites its slot)
+template <class A>
+__global__ void k_put_group_arg(A a, A* dst) {
+  if (threadIdx.x == 0) *dst = a;
+}
+hipError_t launch_put_group_arg(const LoopGroupArg& a, LoopGroupArg* dst, hipStream_t s) {
+  hipLaunchKernelGGL(k_put_group_arg<LoopGroupArg>, dim3(1), dim3(64), 0, s, a, dst);
+  return hipGetLastError();
+}
+hipError_t launch_put_group_arg(const AggGroupArg& a, AggGroupArg* dst, hipStream_t s) {
+  hipLaunchKernelGGL(k_put_group_arg<AggGroupArg>, dim3(1), dim3(64), 0, s, a, dst);
+  return hipGetLastError();
+}
+// In-process rank groups: every rank's loop in one dispatch of world * nwg workgroups (ga: [world] in device
+// memory; the same instance choice as launch_sched_loop / launch_agg_loop's node-sharded batch instances)
+hipError_t launch_sched_loop_group(const LoopGroupArg* ga, int world, int nwg, hipStream_t s, hipEvent_t t0,
+                                   hipEvent_t t1, int unit) {
+  const dim3 grid(world * nwg);
+  if (unit == 128 && world * nwg <= 64)
+    hipExtLaunchKernelGGL((k_sched_loop_group<2, 1>), grid, dim3(2 * 64 + 128), 0, s, t0, t1, 0, ga, nwg);
+  else if (unit == 128)
+    hipExtLaunchKernelGGL((k_sched_loop_group<2, kMaxSweep>), grid, dim3(2 * 64 + 128), 0, s, t0, t1, 0, ga, nwg);
+  else
+    hipExtLaunchKernelGGL((k_sched_loop_group<4, kMaxSweep>), grid, dim3(kLoopThreads), 0, s, t0, t1, 0, ga, nwg);
+  return hipGetLastError();
+}
+hipError_t launch_agg_loop_group(const AggGroupArg* ga, int world, int nwg, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
+  hipExtLaunchKernelGGL(k_agg_loop_group, dim3(world * nwg), dim3(kAggThreads), 0, s, t0, t1, 0, ga, nwg);
+  return hipGetLastError();
+}
 // Workgroups of each persistent loop one CU holds at once (the loops' grids must be resident as a whole:
 // every workgroup spins on the others' granules): [0] k_sched_loop 128-node unit, [1] 256-node unit,
 // [2] k_agg_loop, [3] its node-sharded instance.  0 means the kernel cannot be resident at all.
@@ -4934,6 +5024,12 @@ hipError_t warm_kernels() {
                       reinterpret_cast<const void*>(&k_gather_rows),        reinterpret_cast<const void*>(&k_gather_csr),
                       reinterpret_cast<const void*>(&k_ob_hint),            reinterpret_cast<const void*>(&k_ob_store),
                       reinterpret_cast<const void*>(&k_nominated),
+                      reinterpret_cast<const void*>(&k_sched_loop_group<2, 1>),
+                      reinterpret_cast<const void*>(&k_sched_loop_group<2, kMaxSweep>),
+                      reinterpret_cast<const void*>(&k_sched_loop_group<4, kMaxSweep>),
+                      reinterpret_cast<const void*>(&k_agg_loop_group),
+                      reinterpret_cast<const void*>(&k_put_group_arg<LoopGroupArg>),
+                      reinterpret_cast<const void*>(&k_put_group_arg<AggGroupArg>),
                       reinterpret_cast<const void*>(&k_ob_remap)};
   for (const void* f : fs) {
     const hipError_t e = hipFuncGetAttributes(&a, f);

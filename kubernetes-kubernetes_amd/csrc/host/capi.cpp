@@ -37,8 +37,10 @@ static thread_local std::string g_create_error;
 static int with_err(ksg_ctx* ctx, int rc);
 static int quiesce(ksg_ctx* ctx) { return with_err(ctx, ctx->engine->resident_stop()); }
 
+// A call that succeeded may still leave a message: a loop give-up recovered over the all-reduce path
+// ("recovered: ..." with give_up_detail's missing participants, Engine::run_batch_api) is kept too.
 static int with_err(ksg_ctx* ctx, int rc) {
-  if (rc != KSG_OK) {
+  if (rc != KSG_OK || !ctx->cluster->err.empty()) {
     if (!ctx->cluster->err.empty()) ctx->err = ctx->cluster->err;
     ctx->cluster->err.clear();
   }
@@ -85,7 +87,7 @@ ksg_ctx* ksg_create(const char* config_json, size_t len) {
         return nullptr;
       }
       std::string err;
-      ctx->engine->comm = make_comm(cfg, ctx->cluster->own_queue, &err);
+      ctx->engine->comm = make_comm(cfg, &err);
       if (!ctx->engine->comm) {
         g_create_error = err;
         delete ctx;

@@ -32,26 +32,10 @@ static const char* zone_key(const NodeSpec& n, std::string* out) {  // node/topo
   return out->c_str();
 }
 
-int hw_queues() {
-  static const int q = [] {
-    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
-    return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
-  }();
-  return q;
-}
-static std::atomic<int> g_streams{0};
-// + the null stream, + one spare: a rocprofv3 kernel trace of a W = 3 in-process group (profiles/
-// r05c_w3_queue_trace.txt) shows its three streams and the null stream on all four of HIP's default queues;
-// a stream this count cannot see (a library's internal one) then shares a rank's queue
-bool stream_created() { return g_streams.fetch_add(1) + 1 + 1 + 1 <= hw_queues(); }
-void stream_destroyed() { g_streams.fetch_sub(1); }
-
 Cluster::Cluster(const Config& c) : cfg(c) {
   std::memset(&view, 0, sizeof(view));
   if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
     err = "cannot open HIP device " + std::to_string(cfg.device);
-  else
-    own_queue = stream_created();
 }
 
 Cluster::~Cluster() {
@@ -60,10 +44,7 @@ Cluster::~Cluster() {
     if (b.p) (void)hipFree(b.p);
   if (upd_dev_.p) (void)hipFree(upd_dev_.p);
   if (dyn_dev_.p) (void)hipFree(dyn_dev_.p);
-  if (stream) {
-    (void)hipStreamDestroy(stream);
-    stream_destroyed();
-  }
+  if (stream) (void)hipStreamDestroy(stream);
 }
 
 void* Cluster::dalloc(size_t bytes) {

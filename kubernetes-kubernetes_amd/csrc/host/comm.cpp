@@ -52,7 +52,6 @@ class RcclComm : public Comm {
       err = "share_buffers: allocation failed";
       return KSG_EDEVICE;
     }
-    (void)stream_created();
     int rc = KSG_OK;
     if (hipMemcpy(d + (size_t)rank * hb, &h, hb, hipMemcpyHostToDevice) != hipSuccess ||
         ncclAllGather(d + (size_t)rank * hb, d, hb, ncclChar, comm, s) != ncclSuccess ||
@@ -63,7 +62,6 @@ class RcclComm : public Comm {
     }
     (void)hipFree(d);
     (void)hipStreamDestroy(s);
-    stream_destroyed();
     if (rc) return rc;
     all->assign(world, nullptr);
     for (int r = 0; r < world; ++r) {
@@ -125,8 +123,9 @@ struct LocalGroup {
   std::mutex mu;
   std::condition_variable cv;
   int world = 0, arrived = 0, members = 0;
-  bool own_queues = true;  // every member's stream has a hardware queue of its own
   uint64_t gen = 0;
+  hipEvent_t launched = nullptr;  // group_launch: the leader's event after the group's dispatch
+  int launch_rc = 0;              // ... and the leader's status
   std::vector<unsigned long long*> bufs;
   std::vector<hipEvent_t> evs;
   std::vector<size_t> counts;
@@ -150,6 +149,7 @@ class LocalComm : public Comm {
   ~LocalComm() override {
     for (hipEvent_t e : ring)
       if (e) (void)hipEventDestroy(e);
+    if (launched) (void)hipEventDestroy(launched);
     std::lock_guard<std::mutex> lk(g_groups_mu);
     if (g && --g->members == 0) g_groups.erase(name);
   }
@@ -216,9 +216,56 @@ class LocalComm : public Comm {
     return KSG_OK;
   }
 
-  bool own_queues() const override {
-    std::lock_guard<std::mutex> lk(g->mu);
-    return g->members == g->world && g->own_queues;
+  bool in_process() const override { return true; }
+
+  hipEvent_t launched = nullptr;  // the leader's (rank 0's) group_launch event
+  int group_launch(void* req, hipStream_t s, const GroupLaunchFn& leader) override {
+    hipEvent_t ev = ring[next_ev];
+    next_ev = (next_ev + 1) % kRing;
+    if (hipEventRecord(ev, s) != hipSuccess) {  // everything this rank enqueued before its loop
+      err = "group launch: hipEventRecord failed";
+      return KSG_EDEVICE;
+    }
+    int sl = 0;
+    if (!rendezvous(reinterpret_cast<unsigned long long*>(req), ev, 0, &sl)) {
+      err = "group launch: ranks did not issue the same launch sequence (timeout)";
+      return KSG_EDEVICE;
+    }
+    if (rank == 0) {  // every rank is blocked in the second rendezvous until this is enqueued
+      std::vector<void*> reqs(world);
+      int rc = KSG_OK;
+      for (int r = 0; r < world; ++r) {
+        reqs[r] = g->snap_bufs[sl][r];
+        if (r && hipStreamWaitEvent(s, g->snap_evs[sl][r], 0) != hipSuccess) rc = KSG_EDEVICE;
+      }
+      if (!launched && hipEventCreateWithFlags(&launched, hipEventDisableTiming) != hipSuccess) rc = KSG_EDEVICE;
+      if (rc == KSG_OK) rc = leader(s, reqs);
+      if (rc == KSG_OK && hipEventRecord(launched, s) != hipSuccess) rc = KSG_EDEVICE;
+      std::lock_guard<std::mutex> lk(g->mu);
+      g->launched = launched;
+      g->launch_rc = rc;
+    }
+    if (!rendezvous(nullptr, nullptr, 0, &sl)) {
+      err = "group launch: launch rendezvous timed out";
+      return KSG_EDEVICE;
+    }
+    int rc;
+    hipEvent_t done;
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      rc = g->launch_rc;
+      done = g->launched;
+    }
+    if (rc != KSG_OK) {
+      err = "group launch: the leader could not enqueue the group's dispatch";
+      return KSG_EDEVICE;
+    }
+    // (the leader records `launched` again only after every rank has passed the next first rendezvous)
+    if (rank != 0 && hipStreamWaitEvent(s, done, 0) != hipSuccess) {
+      err = "group launch: hipStreamWaitEvent failed";
+      return KSG_EDEVICE;
+    }
+    return KSG_OK;
   }
 
   int agree(int64_t mine, std::vector<int64_t>* all) override {
@@ -256,7 +303,7 @@ class LocalComm : public Comm {
   }
 };
 
-std::unique_ptr<Comm> make_comm(const Config& cfg, bool own_queue, std::string* err) {
+std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err) {
   if (!cfg.sharded()) return nullptr;
   if (!cfg.nccl_id.empty()) {
     ncclUniqueId id;
@@ -299,7 +346,6 @@ std::unique_ptr<Comm> make_comm(const Config& cfg, bool own_queue, std::string* 
       return nullptr;
     }
     ++g->members;
-    g->own_queues = g->own_queues && own_queue;
     c->g = g;
   }
   return c;

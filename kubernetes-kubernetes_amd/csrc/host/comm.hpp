@@ -15,6 +15,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -41,9 +42,17 @@ class Comm {
   // collective: every rank passes its device buffer; all[r] becomes rank r's buffer as mapped in
   // this process (in-process: the pointer itself; RCCL ranks: an IPC mapping of the peer's memory)
   virtual int share_buffers(void* mine, std::vector<void*>* all) = 0;
-  // every rank's stream has a hardware queue of its own (in-process groups: all ranks joined and
-  // each Cluster::own_queue; RCCL ranks each own a device)
-  virtual bool own_queues() const { return true; }
+  // In-process groups (one device): every rank's persistent loop goes into ONE dispatch (DESIGN.md §6:
+  // loops dispatched separately on separate hardware queues are not co-scheduled).  Each rank passes its
+  // launch request (`req`, valid until the call returns); the leader (rank 0) makes its stream wait for every
+  // rank's stream, calls leader(its stream, every rank's req) to enqueue the group's dispatch, and every other
+  // rank's stream then waits for that.  RCCL ranks (a device each) launch their own loops and never call this.
+  using GroupLaunchFn = std::function<int(hipStream_t, const std::vector<void*>&)>;
+  virtual int group_launch(void* req, hipStream_t s, const GroupLaunchFn& leader) {
+    err = "group_launch: only in-process groups launch their loops together";
+    return -1;
+  }
+  virtual bool in_process() const { return false; }
   // host-side: all[r] = rank r's `mine` (in-process groups; the RCCL transport has no host channel and
   // returns only its own value)
   virtual int agree(int64_t mine, std::vector<int64_t>* all) {
@@ -54,8 +63,7 @@ class Comm {
 };
 
 // nullptr + *err on failure; cfg.world == 1 never creates one
-// own_queue: this rank's stream has a hardware queue of its own (Cluster::own_queue)
-std::unique_ptr<Comm> make_comm(const Config& cfg, bool own_queue, std::string* err);
+std::unique_ptr<Comm> make_comm(const Config& cfg, std::string* err);
 // ncclGetUniqueId as 256 hex characters (rank 0 creates it and hands it to every rank)
 int comm_unique_id(std::string* hex, std::string* err);
 

@@ -69,6 +69,11 @@ hipError_t launch_sched_loop(const MirrorView& m, const BatchView& b, const Loop
                              hipEvent_t t0, hipEvent_t t1, int unit);
 hipError_t launch_agg_loop(const MirrorView& m, const BatchView& b, const AggView& av, hipStream_t s, hipEvent_t t0,
                            hipEvent_t t1);
+hipError_t launch_put_group_arg(const LoopGroupArg& a, LoopGroupArg* dst, hipStream_t s);
+hipError_t launch_put_group_arg(const AggGroupArg& a, AggGroupArg* dst, hipStream_t s);
+hipError_t launch_sched_loop_group(const LoopGroupArg* ga, int world, int nwg, hipStream_t s, hipEvent_t t0,
+                                   hipEvent_t t1, int unit);
+hipError_t launch_agg_loop_group(const AggGroupArg* ga, int world, int nwg, hipStream_t s, hipEvent_t t0, hipEvent_t t1);
 hipError_t warm_kernels();
 hipError_t warm_aggregate();
 hipError_t launch_ob_hint(const MirrorView& m, const BatchView& b, int pod, hipStream_t s);
@@ -1241,12 +1246,9 @@ Engine::~Engine() {
   for (hipEvent_t e : lev) (void)hipEventDestroy(e);
   for (hipEvent_t e : cev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pev) (void)hipEventDestroy(e);
-  if (cstream) {
-    (void)hipStreamDestroy(cstream);
-    stream_destroyed();
-  }
+  if (cstream) (void)hipStreamDestroy(cstream);
   for (DevBuf* b : {&d_descs, &d_meta, &d_status, &d_fmask, &d_blk, &d_fixed, &d_raw, &d_out,
-                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_agran, &d_region, &d_astamps, &d_aspill, &d_relay,
+                    &d_total, &d_arena, &d_xa, &d_xp, &d_xb, &d_xs, &d_gran, &d_fail, &d_grp, &d_agran, &d_region, &d_astamps, &d_aspill, &d_relay,
                     &d_evg, &d_aggpeers, &d_pre, &d_seg, &d_segcnt, &d_psout, &d_pdb, &d_pick, &d_contrib_buf, &d_wide, &d_vsc,
                     &d_ob, &d_ob_heap, &d_ob_map, &d_tcache, &d_tcw})
     if (b->p) (void)hipFree(b->p);
@@ -1455,10 +1457,19 @@ static std::string give_up_detail(const uint32_t* f, const std::vector<unsigned 
     now[(size_t)p] = row.size() >= (size_t)P * ng && (row[(size_t)p * ng + f[2]] >> 48) != (unsigned long long)f[5];
     at[(size_t)p] = ((ball >> (p & 63)) & 1ull) && (P <= 64 || now[(size_t)p]);
   }
+  // fail words 8..15: where and when the launch entered and gave up (HW_ID: pipe [7:6], HQD [26:24], ME [31:30];
+  // s_memrealtime at 100 MHz, shown in us, one clock for every rank on the device)
+  auto hw = [](uint32_t id, uint32_t xcc) {
+    return "ME " + std::to_string(id >> 30) + " pipe " + std::to_string((id >> 6) & 3u) + " HQD " +
+           std::to_string((id >> 24) & 7u) + " XCC " + std::to_string(xcc & 15u);
+  };
+  const unsigned long long te = (unsigned long long)f[10] | ((unsigned long long)f[11] << 32);
+  const unsigned long long tg = (unsigned long long)f[12] | ((unsigned long long)f[13] << 32);
   return std::string(f[4] == 2 ? "k_agg_loop" : "k_sched_loop") + " granule row " + std::to_string(f[1]) + " slot " +
          std::to_string(f[2]) + ": missing at the give-up " + participants_by_rank(at, world, g) +
          (P > 64 ? " (sweep lanes fold 64 participants: intersected with the drain)" : "") + "; still missing after the drain " +
-         participants_by_rank(now, world, g);
+         participants_by_rank(now, world, g) + "; this launch entered at t=" + std::to_string(te / 100) + " us (" +
+         hw(f[8], f[9]) + "), gave up at t=" + std::to_string(tg / 100) + " us (" + hw(f[14], f[15]) + ")";
 }
 
 // k_agg_loop: pod b's counts are defined exactly as pod a's (DF_AGG_SAME) -- the same program but for the fields
@@ -1542,6 +1553,36 @@ static void tc_plan(const std::vector<CompiledPod>& cp, int i, int j, uint32_t* 
   }
 }
 
+// In-process groups (localGroup, one device): this rank's persistent loop joins the group's single dispatch
+// (Comm::group_launch).  The leader stages every rank's launch arguments into its own d_grp, in
+// stream order, and launches world * nwg workgroups; block r * nwg + w runs rank r's workgroup w.  Rank r's
+// timing events bracket the group's dispatch on the leader's stream (rank 0's ride its dispatch packet).
+int Engine::group_launch(GroupReq* req, bool agg, int nwg, int unit) {
+  const int W = c->cfg.world;
+  void* grp = d_grp.p;  // (the leader's: only rank 0's callback runs)
+  auto leader = [&](hipStream_t ls, const std::vector<void*>& reqs) -> int {
+    if (!grp || (int)reqs.size() != W) return KSG_EDEVICE;
+    auto rq = [&](int r) -> const GroupReq& { return *static_cast<const GroupReq*>(reqs[(size_t)r]); };
+    for (int r = 0; r < W; ++r)
+      if ((agg ? launch_put_group_arg(rq(r).aa, (AggGroupArg*)grp + r, ls)
+               : launch_put_group_arg(rq(r).la, (LoopGroupArg*)grp + r, ls)) != hipSuccess)
+        return KSG_EDEVICE;
+    for (int r = 1; r < W; ++r)
+      if (rq(r).t0 && hipEventRecord(rq(r).t0, ls) != hipSuccess) return KSG_EDEVICE;
+    const hipError_t e = agg ? launch_agg_loop_group((const AggGroupArg*)grp, W, nwg, ls, rq(0).t0, rq(0).t1)
+                             : launch_sched_loop_group((const LoopGroupArg*)grp, W, nwg, ls, rq(0).t0, rq(0).t1, unit);
+    if (e != hipSuccess) return KSG_EDEVICE;
+    for (int r = 1; r < W; ++r)
+      if (rq(r).t1 && hipEventRecord(rq(r).t1, ls) != hipSuccess) return KSG_EDEVICE;
+    return KSG_OK;
+  };
+  if (comm->group_launch(req, c->stream, leader) != KSG_OK) {
+    c->err = comm->err;
+    return KSG_EDEVICE;
+  }
+  return KSG_OK;
+}
+
 int Engine::run_batch_api(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                           ksg_result* results, ksg_eval_out* eval) {
   fault_first_ = -1;
@@ -1608,13 +1649,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   const auto T0 = clk::now();
   // ---- the chunk plan (needs the exchange mode of a sharded context)
   const int W = comm ? c->cfg.world : 1;
-  // In-process ranks (localGroup, one device) need every rank's loop resident at once, so every
-  // rank's stream must have a hardware queue of its own: on a shared queue a rank's loop waits behind
-  // a peer's loop that spins on it (Cluster::own_queue).  The group decides as one (Comm::own_queues):
-  // otherwise it keeps the all-reduce path.
+  // (in-process ranks -- localGroup, one device -- launch every rank's loop in one dispatch: group_launch below)
   const bool rccl = !c->cfg.nccl_id.empty();
-  const bool dx = comm && !force_allreduce_ && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl)) &&
-                  (rccl || comm->own_queues());
+  const bool dx = comm && !force_allreduce_ && (c->cfg.dev_exchange == 1 || (c->cfg.dev_exchange < 0 && rccl));
   // Host/device pipeline: the batch runs as chunks.  While the device schedules chunk k the host
   // compiles and stages chunk k+1, then mirrors the finished chunks' assumes into the cache.  Only
   // chunk 0's compile and the last chunk's bookkeeping are exposed, so chunk 0 is short (32 pods,
@@ -1798,12 +1835,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
   // programs, offsets, stats of pods [a, b) into pinned memory, then their H2D copies
   // chunks after the first go up on the copy stream while the device runs the chunk before them;
   // the compute stream waits for them before the chunk's first launch
-  // (not for in-process rank groups: their streams already outnumber the hardware queues, and a
-  // copy stream's event wait sharing a queue with a peer's loop launch would hold that loop back)
+  // (not for in-process rank groups: the group's leader waits for each rank's compute stream before the
+  // group's loop dispatch, so the staging stays on it)
   const bool copy_stream = pipe && (!comm || rccl);
   if (copy_stream && !cstream) {
     HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-    (void)stream_created();
   }
   while (pev.size() < 2 * bnd.size()) {
     hipEvent_t e;
@@ -1964,6 +2000,9 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
     if (use_loop && (rc = gran_setup())) return rc;
     if ((rc = ensure(d_fail, kFailBytes))) return rc;
     HIPCHK(hipMemsetAsync(d_fail.p, 0, kFailBytes, s));
+    // in-process groups: the leader's array of every rank's launch arguments (group_launch)
+    if (comm && comm->in_process() && (rc = ensure(d_grp, (size_t)W * std::max(sizeof(LoopGroupArg), sizeof(AggGroupArg)))))
+      return rc;
     if (c->cfg.loop_stamps) {
       const size_t sb = (size_t)n * 8 * 8 + 64 * 8 + (size_t)n * std::max(G, GS) * 8 * 8;
       if ((rc = ensure(d_stamps, sb))) return rc;
@@ -2029,8 +2068,8 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       }
       if (cp[i].prefilter_reject) { r.status = KSG_CODE_UNSCHEDULABLE; r.node_index = -1; r.feasible_nodes = 0; }
       if (assume && r.status == KSG_CODE_SUCCESS && r.node_index >= 0) {
-        static uint64_t seq = 0;
-        std::string uid = pods[i]->uid + "#a" + std::to_string(++seq);
+        // (a per-context count, as the oracle's assumeSeq: victims name assumed pods by this uid)
+        std::string uid = pods[i]->uid + "#a" + std::to_string(++assume_seq_);
         // a node-sharded k_agg_loop applies the AssumePod to the mirror on the node's own rank only (the
         // other ranks record the result and the pod table entry): theirs go up with the next node updates
         const bool foreign = agg_pod[(size_t)i] && comm &&
@@ -2196,8 +2235,16 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       regate = false;
       const bool tl = loop_timed(runs.size());
       htrace("loop", i);
-      HIPCHK(launch_sched_loop(m, bv, lv, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr,
-                               unit));
+      hipEvent_t t0 = tl ? lev[2 * runs.size()] : nullptr, t1 = tl ? lev[2 * runs.size() + 1] : nullptr;
+      if (comm && comm->in_process()) {
+        GroupReq req{};
+        req.la = LoopGroupArg{m, bv, lv};
+        req.t0 = t0;
+        req.t1 = t1;
+        if ((rc = group_launch(&req, false, GS, unit))) return rc;
+      } else {
+        HIPCHK(launch_sched_loop(m, bv, lv, s, t0, t1, unit));
+      }
       runs.push_back({i, j - i, rb, false, tl});
       launches += j - i;
       i = j;
@@ -2278,7 +2325,16 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       }
       regate = false;
       const bool tl = loop_timed(runs.size());
-      HIPCHK(launch_agg_loop(m, bv, av, s, tl ? lev[2 * runs.size()] : nullptr, tl ? lev[2 * runs.size() + 1] : nullptr));
+      hipEvent_t t0 = tl ? lev[2 * runs.size()] : nullptr, t1 = tl ? lev[2 * runs.size() + 1] : nullptr;
+      if (comm && comm->in_process()) {
+        GroupReq req{};
+        req.aa = AggGroupArg{m, bv, av};
+        req.t0 = t0;
+        req.t1 = t1;
+        if ((rc = group_launch(&req, true, G, 0))) return rc;
+      } else {
+        HIPCHK(launch_agg_loop(m, bv, av, s, t0, t1));
+      }
       runs.push_back({i, j - i, rb, true, tl});
       std::fill(agg_pod.begin() + i, agg_pod.begin() + j, (uint8_t)1);
       launches += j - i;
@@ -3330,7 +3386,7 @@ relaunch:
   }
   res->total_score = d.feasible > 1 ? d.total : 0;
   if (res->status == KSG_CODE_SUCCESS && res->node_index >= 0) {
-    std::string uid = p.uid + "#r" + std::to_string(++res_seq_);
+    std::string uid = p.uid + "#a" + std::to_string(++assume_seq_);  // (as run_batch: the oracle's naming)
     if ((rc = c->add_pod(p, uid, /*device_done=*/true, cp.slot, &c->order()[(size_t)res->node_index], &cp.res)))
       return rc;
     assumed[handle] = uid;

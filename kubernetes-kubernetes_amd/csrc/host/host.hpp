@@ -27,14 +27,6 @@
 
 namespace ksg {
 
-// HIP streams this library holds in the process (every context's stream, copy streams, transient
-// ones).  The HIP runtime gives a new stream its own hardware queue while the process holds fewer
-// than GPU_MAX_HW_QUEUES (default 4) and shares the least-used one after that; the null stream takes
-// one too.  stream_created() returns whether the new stream's queue is its own.
-int hw_queues();
-bool stream_created();
-void stream_destroyed();
-
 // ===================================================================================
 // objects
 // ===================================================================================
@@ -435,11 +427,6 @@ class Cluster {
   // ---- HBM mirror
   MirrorView view;
   hipStream_t stream = nullptr;
-  // the stream got a hardware queue of its own: when it was created, every stream of this library in
-  // the process plus the null stream fitted in GPU_MAX_HW_QUEUES (stream_created below).  In-process
-  // rank groups need it for the device exchange (a rank's loop queued behind a peer's spinning loop
-  // on a shared queue never starts).
-  bool own_queue = true;
   bool layout_dirty = true;
   bool defer_relayout = false;  // ensure_label_slot only marks layout_dirty (pods in flight)
   bool mirror_suspect = false;  // device columns may hold assumes the cache lacks: rebuild all of them
@@ -632,6 +619,15 @@ class Engine {
   DevBuf d_xa, d_xp, d_xb, d_xs;  // node-sharded exchange vectors, one set per pod of the batch
   DevBuf d_evg;             // node-sharded evaluation output, gathered over the ranks
   DevBuf d_gran, d_fail, d_stamps;  // k_sched_loop: exchange granules (local), give-up flag, stamps
+  uint64_t assume_seq_ = 0;  // assumed pods' cache uids: "<uid>#a<n>", n counted per context
+  DevBuf d_grp;  // in-process groups, the leader's: every rank's loop launch arguments (group_launch)
+  // one rank's part of an in-process group's loop dispatch (Comm::group_launch): its arguments, its timing events
+  struct GroupReq {
+    LoopGroupArg la;
+    AggGroupArg aa;
+    hipEvent_t t0, t1;
+  };
+  int group_launch(GroupReq* req, bool agg, int nwg, int unit);
   std::vector<unsigned long long*> gran_all;  // every rank's granule array as mapped here ([rank] = d_gran)
   uint32_t gran_tag = 0;
   DevBuf d_agran, d_region;  // k_agg_loop: exchange granules, per-pod shared regions (fixed size once set up)
@@ -678,7 +674,6 @@ class Engine {
   int res_kind_ = 0;              // the running launch: 1 k_sched_loop, 2 k_agg_loop (pod-table pods)
   int64_t res_terms_ = 0;         // k_agg_loop: own affinity terms of the pods posted (its spill rows' budget)
   std::chrono::steady_clock::time_point res_last_{};  // the last result the host took
-  uint64_t res_seq_ = 0;          // assumed-pod uid suffix
   double res_prof_[5] = {};       // loopStamps: compile / post / device / settle us, calls
 };
 

@@ -10,7 +10,7 @@ process, each reporting per rank its loop give-ups / re-runs, the dominant kerne
       <W>k   the same group, kept open (closed by the next 'c')
       <W>r   the same group on the all-reduce path (deviceExchange off)
       c      close kept groups
-The sequence of test_device_exchange_needs_own_queues is  o,6,x,6  (DESIGN.md §6)."""
+The round-5 give-up sequence is  o,6,x,6  (test_group_loops_start_together_after_contexts_closed)."""
 import os
 import sys
 import threading

@@ -113,17 +113,17 @@ def test_random_streams_match_oracle_device_exchange(world, seed):
     _check(ranks, o, [rand_pod(rng, k, names) for k in range(80)], chunk=32)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 6, 8])
 def test_device_exchange_loop_c2(world):
     """The persistent loop across W ranks (granules stored into every rank's array), SchedulingBasic
     pods only, heterogeneous nodes (untied scores), batches long enough for the chunked pipeline.
-    In-process groups need a hardware queue per rank plus the null stream's and a spare (the test process
-    asks HIP for 8, conftest.py), so W = 4 runs the loop as well; test_device_exchange_needs_own_queues
-    checks the fallback at the limit."""
+    In-process groups launch every rank's loop in one dispatch, so any W up to
+    kMaxShards runs the loop, with zero give-ups (_check)."""
     from ksg.synth import scheduling_basic
     nodes, init, pods = scheduling_basic(600 * world + 77, 300, 600, hetero=True)
     ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
     _check(ranks, o, pods, chunk=300)
+    assert _dominant(ranks) == {"k_sched_loop"}
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -426,37 +426,19 @@ def test_loop_give_up_retried_over_allreduce(world):
         assert s.compare_mirror(sync=True)[0] == 0
 
 
-def test_device_exchange_needs_own_queues():
-    """In-process ranks take the device exchange only when every rank's stream has a hardware queue of its
-    own, with the null stream's and one spare beside them: with Q = GPU_MAX_HW_QUEUES, a group
-    of Q - 2 ranks runs the loop, but not while another context's stream is alive -- HIP would then put two
-    streams on one queue, where a rank's loop waits behind a peer's loop that spins on it.  That group keeps
-    the all-reduce path (and still matches the oracle); once the other context is gone, a new group runs the
-    loop."""
+def test_group_loops_start_together_after_contexts_closed():
+    """The sequence that gave up in round 5: a W = 6 group beside another live context, then
+    -- both closed -- a second W = 6 group, then a W = 8 group beside three live contexts.  The loops of
+    separate dispatches on separate hardware queues were not co-scheduled (the give-up records showed one
+    rank's loop entering only when its peers gave up, 10 s later); every group now runs its ranks' loops in
+    ONE dispatch, so every group runs the loop with zero give-ups and the oracle's results."""
     from ksg.native import Scheduler
     from ksg.synth import scheduling_basic
-    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-    world = q - 2
-    if world < 2 or world > 8:
-        pytest.skip(f"GPU_MAX_HW_QUEUES={q}: no in-process group size at the queue limit")
-    nodes, init, pods = scheduling_basic(1877 + 256 * world, 300, 600, hetero=True)
-    other = Scheduler({"device": 0})
-    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
-    _check(ranks, o, pods, chunk=300)
-    assert _dominant(ranks) == {"k_filter_score"}
-    for s in ranks:
-        s.close()
-    other.close()
-    ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
-    got = _run_ranks(ranks, pods, 300)
-    for k, p in enumerate(pods):
-        want = o.schedule_one(o.compile(p), assume=True)[0].as_tuple()
-        for r in range(world):
-            assert got[r][k] == want, f"rank {r} pod {k}: {got[r][k]} != oracle {want}"
-    assert _dominant(ranks) == {"k_sched_loop"}
-    stats = [s.loop_stats() for s in ranks]
-    if any(st != (0, 0) for st in stats):
-        # open (DESIGN.md §6): a group formed after the earlier contexts closed gave up on its first loop on
-        # every rank in most late-round-5 suite runs (W = Q - 2 and Q - 3, in a fresh process too); the re-run
-        # over the all-reduce path returned the oracle's results (asserted above)
-        pytest.xfail(f"loop group formed after closed contexts gave up and re-ran: {stats}")
+    for world, others in ((6, 1), (6, 0), (8, 3)):
+        nodes, init, pods = scheduling_basic(1877 + 256 * world, 300, 600, hetero=True)
+        live = [Scheduler({"device": 0}) for _ in range(others)]
+        ranks, o = _group(world, {"deviceExchange": True}, nodes, init)
+        _check(ranks, o, pods, chunk=300)
+        assert _dominant(ranks) == {"k_sched_loop"}
+        for s in ranks + live:
+            s.close()
