@@ -2738,8 +2738,11 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       tot[i] = (int64_t)gath[(1 + kNumPlugins) * n + i];
     }
   }
-  const bool hinted0 = eval && hr[0].hinted && (reinterpret_cast<const PodDesc*>(cp[0].blob.data())->flags & DF_OB);
-  if (hinted0) {  // placed by the OpportunisticBatching hint: no status, no score (k_ob_hint)
+  const bool hinted0 =
+      eval && hr[0].hinted && (reinterpret_cast<const PodDesc*>(cp[0].blob.data())->flags & (DF_OB | DF_EARLY));
+  // placed on the OpportunisticBatching hint (k_ob_hint) or on its nominated node (k_nominated), which alone went
+  // through the filters (schedule_one.go:586-598, 657-669): no other node has a status, no node a score
+  if (hinted0) {
     std::fill(st.begin(), st.end(), 0u);
     std::fill(outs.begin(), outs.end(), 0);
     std::fill(tot.begin(), tot.end(), 0);
