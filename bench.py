@@ -79,6 +79,21 @@ def parse():
 
 
 # workload -> (name, default nodes, default init pods, BASELINE configs index)
+# kernel_stats() of every batch this process ran (warm-up and timed): KSG_LOOP_PODS_OUT=<file> writes the pods
+# each persistent-loop kernel ran, so a PMC pass's bytes over all of a kernel's dispatches divide by the pods they
+# covered (scripts/prof_summary.py)
+LOOP_PODS = []
+
+
+def write_loop_pods():
+    path = os.environ.get("KSG_LOOP_PODS_OUT")
+    if path:
+        tot = {}
+        for _, _, n, k in LOOP_PODS:
+            tot[k] = tot.get(k, 0) + n
+        json.dump(tot, open(path, "w"))
+
+
 WORKLOADS = {
     "c1": ("SchedulingBasic", 500, 500, 0),
     "c2": ("SchedulingBasic", 5000, 1000, 1),
@@ -302,6 +317,7 @@ def main():
         try:
             for w in range(max(a.warmup, 1 if sharded else 0)):
                 s.schedule_batch(handles[w * a.batch:(w + 1) * a.batch], assume=True)
+                LOOP_PODS.append(s.kernel_stats())
             for h in handles[:max(a.warmup, 1 if sharded else 0) * a.batch]:
                 try:
                     s.forget(h)
@@ -338,6 +354,8 @@ def main():
         kstats.append(s.kernel_stats())
     barrier()
     dt = time.perf_counter() - t0
+    LOOP_PODS.extend(kstats)
+    write_loop_pods()
     for _, rs in arrays:  # ksg_result: int32 status first, 24-byte records
         placed += int((np.frombuffer(rs, dtype=np.int32).reshape(len(rs), -1)[:, 0] == 0).sum())
     if dist is not None:

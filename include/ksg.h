@@ -287,7 +287,8 @@ int ksg_shard_range(const ksg_ctx *ctx, int32_t *first_node, int32_t *num_nodes)
 /* Measurement of the last batch (bench.py): *kernel 0 -> the average k_filter_score duration
  * (HIP events on the dispatch packets) and its algorithmic bytes per launch; *kernel 1 -> most
  * pods ran in the persistent k_sched_loop: its duration per pod and algorithmic bytes per pod;
- * *kernel 2 -> the same for k_agg_loop (pods with PodTopologySpread / InterPodAffinity counts). */
+ * *kernel 2 -> the same for k_agg_loop (pods with PodTopologySpread / InterPodAffinity counts).
+ * *launches: the k_filter_score launches, or the pods the dominant loop kernel ran. */
 int ksg_last_batch_kernel_stats(const ksg_ctx *ctx, double *avg_kernel_ms,
                                 double *bytes_per_launch, int32_t *launches, int32_t *kernel);
 

@@ -2463,6 +2463,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
       last_kernel = 1 + k;
       last_kernel_ms = tp[k] ? lms[k] / tp[k] : 0.0;  // per pod over the timed launches
       last_bytes = lb[k] / lp[k];
+      last_launches = lp[k];  // the pods that loop kernel ran
     }
     if (c->cfg.loop_stamps) {  // mean per-phase time (us) of the looped pods, workgroup 0's view
       std::vector<LoopRun> sruns, aruns;

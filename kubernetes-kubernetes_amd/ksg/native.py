@@ -56,8 +56,9 @@ class Scheduler(Backend):
         super().__init__(load(), "ksg_", config)
 
     def kernel_stats(self):
-        """(avg ms, algorithmic bytes, pods, kernel name) of the last batch: per k_filter_score
-        launch, or per pod inside a persistent loop (k_sched_loop, k_agg_loop) when most pods ran there."""
+        """(avg ms, algorithmic bytes, launches, kernel name) of the last batch: per k_filter_score
+        launch, or per pod inside a persistent loop (k_sched_loop, k_agg_loop) when most pods ran there
+        (launches: the pods that loop ran)."""
         ms, by, n, k = C.c_double(), C.c_double(), C.c_int32(), C.c_int32()
         self._chk(self.lib.ksg_last_batch_kernel_stats(self.ctx, C.byref(ms), C.byref(by), C.byref(n), C.byref(k)),
                   "kernel_stats")

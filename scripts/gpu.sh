@@ -43,14 +43,20 @@ for s in "$@"; do
       step "bench_$wl" 400 python -u bench.py $(bench_args "$wl") --steps "$n" --warmup 1 --cpu-seconds 5 ;;
     prof=*)
       wl=${s#prof=}
+      export KSG_LOOP_PODS_OUT="gpurun_out/prof/loop_pods_trace_$wl.json"
       step "prof_$wl" 400 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof/trace_$wl" -o run -- \
-        python3 bench.py $(bench_args "$wl") --steps 3 --warmup 1 --no-cpu-baseline ;;
+        python3 bench.py $(bench_args "$wl") --steps 3 --warmup 1 --no-cpu-baseline --no-sub
+      unset KSG_LOOP_PODS_OUT ;;
     pmc=*)
       wl=${s#pmc=}
+      # (each pass also writes the pods every loop kernel ran: bench.py KSG_LOOP_PODS_OUT)
+      export KSG_LOOP_PODS_OUT="gpurun_out/prof/loop_pods_fetch_$wl.json"
       step "pmcf_$wl" 300 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/prof/pmc_fetch_$wl" -o run -- \
-        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline
+        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline --no-sub
+      export KSG_LOOP_PODS_OUT="gpurun_out/prof/loop_pods_write_$wl.json"
       step "pmcw_$wl" 300 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/prof/pmc_write_$wl" -o run -- \
-        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline ;;
+        python3 bench.py $(bench_args "$wl") --steps 1 --warmup 1 --no-cpu-baseline --no-sub
+      unset KSG_LOOP_PODS_OUT ;;
     sq=*)
       wl=${s#sq=}
       step "sq_$wl" 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \

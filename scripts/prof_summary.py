@@ -23,14 +23,20 @@ def main():
     tag = sys.argv[1]
     nodes = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
     workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
-    # pods per k_sched_loop dispatch, on average: a 1000-pod batch runs as 7 chunks (engine.cpp
-    # run_batch: 32, 160, 485, 194, 78, 31, 20), each one loop dispatch
+    # pods per loop dispatch, on average: from the pods bench.py counted per loop kernel over the profiled run
+    # (KSG_LOOP_PODS_OUT, gpurun_out/prof/loop_pods_<pass>.json) when present, else this argument (a 1000-pod
+    # batch of one loop kernel runs as 7 chunks: engine.cpp run_batch 32, 160, 485, 194, 78, 31, 20)
     loop_pods = float(sys.argv[4]) if len(sys.argv) > 4 else 1000.0 / 7.0
+
+    def pods_file(sub):
+        p = os.path.join(PROF, "loop_pods_" + sub.split("pmc_", 1)[-1] + ".json")
+        return json.load(open(p)) if os.path.exists(p) else {}
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     # KSG_PROF_TRACE: the kernel-trace directory under gpurun_out/prof (default "trace")
     c = sqlite3.connect(os.path.join(PROF, os.environ.get("KSG_PROF_TRACE", "trace"), "run_results.db"))
     rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    tpods = pods_file(os.environ.get("KSG_PROF_TRACE", "trace"))
     lines = [f"# rocprofv3 --kernel-trace --stats -- python3 bench.py (tag {tag})",
              f"{'kernel':60s} {'calls':>8s} {'total_us':>12s} {'avg_us':>9s} {'pct':>6s}"]
     for n, calls, tot, avg, pct in rows:  # top_kernels is in us; kernels.duration is ns
@@ -43,17 +49,21 @@ def main():
             lines.append(f"{kn} dispatch duration us: median {d[len(d) // 2] / 1e3:.3f} "
                          f"p10 {d[len(d) // 10] / 1e3:.3f} p90 {d[9 * len(d) // 10] / 1e3:.3f}")
             if kn in ("k_sched_loop", "k_agg_loop"):
-                lines.append(f"{kn} per pod us (mean dispatch / {loop_pods:.2f} pods per dispatch): "
-                             f"{sum(d) / len(d) / 1e3 / loop_pods:.3f}")
+                lp = tpods[kn] / len(d) if tpods.get(kn) else loop_pods
+                lines.append(f"{kn} per pod us (mean dispatch / {lp:.2f} pods per dispatch"
+                             + (", the pods bench.py counted" if tpods.get(kn) else "") + f"): "
+                             f"{sum(d) / len(d) / 1e3 / lp:.3f}")
     open(os.path.join(out, f"{tag}_kernel_stats.txt"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
     per = {}
+    ppods = {}  # counter -> {kernel: pods its dispatches ran in that pass}
     sfx = os.environ.get("KSG_PROF_PMC_SUFFIX", "")  # e.g. "_c4": gpurun_out/prof/pmc_fetch_c4
     for counter, sub in (("FETCH_SIZE", "pmc_fetch" + sfx), ("WRITE_SIZE", "pmc_write" + sfx)):
         p = os.path.join(PROF, sub, "run_results.db")
         if not os.path.exists(p):
             continue
+        ppods[counter] = pods_file(sub)
         cc = sqlite3.connect(p)
         for name, val in cc.execute("select kernel_name, value from counters_collection where counter_name=?",
                                     (counter,)):
@@ -70,12 +80,19 @@ def main():
         pl.append(f"{k:60s} dispatches {len(f):6d} FETCH_KiB {fa:10.2f} (x2 {2 * fa:10.2f}) WRITE_KiB {wa:10.2f}")
         for kn, per_unit in (("k_filter_score", 1), ("k_sched_loop", loop_pods), ("k_agg_loop", loop_pods)):
             if k.split("<")[0].endswith(kn):  # (templated kernels: k_sched_loop<2, false>)
-                traffic[kn] = {"kernel": kn, "nodes": nodes, "workload": workload, "fetch_kib_raw": fa / per_unit,
-                               "write_kib": wa / per_unit,
-                               "bytes_per_launch": round((fa + wa) * 1024.0 / per_unit, 1),
-                               "bytes_per_launch_fetch_x2": round((2 * fa + wa) * 1024.0 / per_unit, 1),
+                # the pass's bytes over every dispatch of the kernel / the pods those dispatches ran
+                pf = ppods.get("FETCH_SIZE", {}).get(kn)
+                pw = ppods.get("WRITE_SIZE", {}).get(kn)
+                uf = pf / len(f) if pf and f else per_unit
+                uw = pw / len(w) if pw and w else per_unit
+                traffic[kn] = {"kernel": kn, "nodes": nodes, "workload": workload, "fetch_kib_raw": fa / uf,
+                               "write_kib": wa / uw,
+                               "bytes_per_launch": round((fa / uf + wa / uw) * 1024.0, 1),
+                               "bytes_per_launch_fetch_x2": round((2 * fa / uf + wa / uw) * 1024.0, 1),
                                "note": f"FETCH_SIZE+WRITE_SIZE per {kn} dispatch"
-                                       + (f" / {per_unit} pods" if per_unit > 1 else "")
+                                       + (f" / {uf:.2f} (fetch pass) and {uw:.2f} (write pass) pods per dispatch"
+                                          + (", the pods bench.py counted" if pf and pw else "")
+                                          if kn != "k_filter_score" else "")
                                        + ", separate PMC passes (tag " + tag + ")"}
     open(os.path.join(out, f"{tag}_pmc.txt"), "w").write("\n".join(pl) + "\n")
     print("\n".join(pl))
