@@ -188,6 +188,19 @@ int ksg_schedule_batch(ksg_ctx *ctx, const int32_t *handles, int32_t n, uint32_t
 /* Cache.ForgetPod (cache.go:412) of an assumed pod -- unreserveAndForget (schedule_one.go:358) */
 int ksg_forget(ksg_ctx *ctx, int32_t handle);
 
+/* ---- the scheduling queue's nominator (backend/queue/nominator.go) -------------------
+ * Pods nominated to a node and waiting for it (PostFilter's NominatingInfo, status.nominatedNodeName).
+ * ksg_add_nominated_pod: PodNominator.AddNominatedPod / UpdateNominatedPod of pod_json -- its uid is nominated
+ * to its status.nominatedNodeName with its spec.priority, replacing an earlier nomination of the uid (none: the
+ * uid is forgotten).  ksg_delete_nominated_pod: DeleteNominatedPodIfExists (also done by every assume of the uid
+ * through this context, schedule_one.go:1131-1134).  A pod's own nomination is evaluateNominatedNode (the pod
+ * tries that node alone first).  OTHER pods' nominations change a pod's Filter: RunFilterPluginsWithNominatedPods
+ * (framework.go:1211-1294) adds every pod of equal or higher priority nominated to a node before filtering it,
+ * which this library does not run -- ksg_schedule_one / ksg_schedule_batch / ksg_preempt return KSG_ENOTSUP,
+ * scheduling nothing, when a pod of the call has such a nomination on a snapshot node besides its own. */
+int ksg_add_nominated_pod(ksg_ctx *ctx, const char *pod_json, size_t len);
+int ksg_delete_nominated_pod(ksg_ctx *ctx, const char *uid);
+
 /* ---- OpportunisticBatching (framework/runtime/batch.go:31-242) ----------------------
  * With featureGates.OpportunisticBatching on (the default) and a profile whose PodTopologySpread has no
  * default constraints (disabled, or {"defaultingType": "List", "defaultConstraints": []}), pods get a

@@ -254,6 +254,7 @@ int ksg_schedule_one(ksg_ctx* ctx, int32_t handle, uint32_t flags, ksg_result* r
   GUARD({
     auto it = ctx->engine->queue.find(handle);
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
+    if (const int rn = ctx->engine->check_nominations({&it->second})) return with_err(ctx, rn);
     if (!eval && (flags & KSG_FLAG_ASSUME)) {  // a resident loop (k_sched_loop / k_agg_loop), else the launch path
       bool handled = false;
       const int rc = ctx->engine->schedule_resident(it->second, handle, result, &handled);
@@ -279,6 +280,7 @@ int ksg_schedule_batch(ksg_ctx* ctx, const int32_t* handles, int32_t n, uint32_t
       if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
       pods.push_back(&it->second);
     }
+    if (const int rn = ctx->engine->check_nominations(pods)) return with_err(ctx, rn);
     return with_err(ctx, ctx->engine->run_batch_api(pods, hs, (flags & KSG_FLAG_ASSUME) != 0, results, nullptr));
   })
 }
@@ -293,6 +295,27 @@ int ksg_forget(ksg_ctx* ctx, int32_t handle) {  // Cache.ForgetPod (backend/cach
     ctx->engine->assumed.erase(it);
     return with_err(ctx, ctx->cluster->remove_pod(uid));
   })
+}
+
+int ksg_add_nominated_pod(ksg_ctx* ctx, const char* pod_json, size_t len) {  // nominator.go:60-103
+  if (!ctx || !pod_json) return KSG_EINVAL;
+  GUARD({
+    PodSpec p;
+    if (!decode_pod(pod_json, len, &p, &ctx->err)) return KSG_EINVAL;
+    if (p.uid.empty()) {
+      ctx->err = "ksg_add_nominated_pod: metadata.uid is empty";
+      return KSG_EINVAL;
+    }
+    ctx->engine->nominated.erase(p.uid);  // deleteUnlocked: at most one nomination per uid
+    if (!p.nominated_node.empty()) ctx->engine->nominated[p.uid] = std::make_pair(p.nominated_node, p.priority);
+    return KSG_OK;
+  })
+}
+
+int ksg_delete_nominated_pod(ksg_ctx* ctx, const char* uid) {  // nominator.go:138-...
+  if (!ctx || !uid) return KSG_EINVAL;
+  ctx->engine->nominated.erase(uid);
+  return KSG_OK;
 }
 
 int ksg_run_filter_plugin(ksg_ctx* ctx, int32_t handle, int32_t plugin, int32_t* prefilter_code, uint8_t* codes,
@@ -315,6 +338,8 @@ int ksg_preempt(ksg_ctx* ctx, int32_t handle, const char* args_json, size_t args
     if (it == ctx->engine->queue.end()) return KSG_ENOTFOUND;
     // node-sharded contexts: every rank holds the whole mirror and pod table, so each rank runs the
     // PostFilter over every node by itself (no exchange) and returns the identical choice
+    // (SelectVictimsOnNode filters with the nominated pods too: refused likewise)
+    if (const int rn = ctx->engine->check_nominations({&it->second})) return with_err(ctx, rn);
     if (const int rs = quiesce(ctx)) return rs;
     std::string d;
     const int rc = ctx->engine->preempt(it->second, args_json, args_len, result, detail ? &d : nullptr);

@@ -1583,6 +1583,23 @@ int Engine::group_launch(GroupReq* req, bool agg, int nwg, int unit) {
   return KSG_OK;
 }
 
+// RunFilterPluginsWithNominatedPods (framework.go:1211-1294) filters a node with the pods nominated to it of equal or
+// higher priority added (addGENominatedPods: corev1.PodPriority >= the pod's, another uid), which this library does
+// not run: a call in which some pod would see such a nomination on a snapshot node is refused before anything runs.
+int Engine::check_nominations(const std::vector<const PodSpec*>& pods) {
+  if (nominated.empty()) return KSG_OK;
+  c->order();  // (the snapshot's index, current)
+  for (const PodSpec* p : pods)
+    for (const auto& kv : nominated)
+      if (kv.first != p->uid && kv.second.second >= p->priority && c->index_of(kv.second.first) >= 0) {
+        c->err = "pod " + p->ns + "/" + p->name + ": pod uid " + kv.first + " (priority " + std::to_string(kv.second.second) +
+                 ") is nominated to node " + kv.second.first +
+                 "; filtering with nominated pods (RunFilterPluginsWithNominatedPods) runs outside the device path";
+        return KSG_ENOTSUP;
+      }
+  return KSG_OK;
+}
+
 int Engine::run_batch_api(const std::vector<const PodSpec*>& pods, const std::vector<int32_t>& handles, bool assume,
                           ksg_result* results, ksg_eval_out* eval) {
   fault_first_ = -1;
@@ -2077,6 +2094,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         int rc2 = c->add_pod(*pods[i], uid, /*device_done=*/!foreign, cp[i].slot, &c->order()[r.node_index], &cp[i].res);
         if (rc2) return rc2;
         assumed[handles.empty() ? -1 : handles[i]] = uid;
+        nominated.erase(pods[i]->uid);  // an assumed pod's nomination ends (schedule_one.go:1131-1134)
       } else {
         c->pod_table_drop(cp[i].slot);  // not placed: the reserved pod-table slot never went live
       }
@@ -3394,6 +3412,7 @@ relaunch:
     if ((rc = c->add_pod(p, uid, /*device_done=*/true, cp.slot, &c->order()[(size_t)res->node_index], &cp.res)))
       return rc;
     assumed[handle] = uid;
+    nominated.erase(p.uid);  // (schedule_one.go:1131-1134)
   } else {
     c->pod_table_drop(cp.slot);
   }

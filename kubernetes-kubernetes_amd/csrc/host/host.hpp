@@ -531,6 +531,11 @@ class Engine {
   Cluster* c;
   std::unordered_map<int32_t, PodSpec> queue;  // handle -> compiled-for-API pod (find / insert / erase only)
   std::unordered_map<int32_t, std::string> assumed;  // handle -> uid
+  // the nominator (ksg_add_nominated_pod): pod uid -> (nominated node name, spec.priority)
+  std::unordered_map<std::string, std::pair<std::string, int32_t>> nominated;
+  // KSG_ENOTSUP (+ err) when a pod of the call would see another pod's nomination of equal or higher priority on a
+  // snapshot node (RunFilterPluginsWithNominatedPods, not run here)
+  int check_nominations(const std::vector<const PodSpec*>& pods);
   int32_t next_handle = 1;
 
   enum Mode { CYCLE, FILTER_ONE, SCORE_ONE };

@@ -121,6 +121,8 @@ def _sig(lib, prefix):
     d("schedule_one", C.c_int, vp, i32, u32, C.POINTER(Result), C.POINTER(EvalOut))
     d("schedule_batch", C.c_int, vp, C.POINTER(i32), i32, u32, C.POINTER(Result))
     d("forget", C.c_int, vp, i32)
+    d("add_nominated_pod", C.c_int, vp, cp, sz)
+    d("delete_nominated_pod", C.c_int, vp, cp)
     d("run_filter_plugin", C.c_int, vp, i32, i32, C.POINTER(i32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint32))
     d("run_score_plugin", C.c_int, vp, i32, i32, C.POINTER(C.c_uint8), C.POINTER(i32), C.POINTER(C.c_int64),
       C.POINTER(C.c_int64))
@@ -286,6 +288,15 @@ class Backend:
 
     def forget(self, handle):
         self._chk(self.f["forget"](self.ctx, handle), "forget")
+
+    def add_nominated_pod(self, pod):
+        """The nominator's AddNominatedPod / UpdateNominatedPod: pod's uid is nominated to its
+        status.nominatedNodeName (none: forgotten)."""
+        b = _js(pod)
+        self._chk(self.f["add_nominated_pod"](self.ctx, b, len(b)), "add_nominated_pod")
+
+    def delete_nominated_pod(self, uid):
+        self._chk(self.f["delete_nominated_pod"](self.ctx, uid.encode()), "delete_nominated_pod")
 
     def run_filter_plugin(self, handle, plugin):
         """PreFilter + Filter of one plugin on every node -> (prefilter_code, codes, reasons)."""

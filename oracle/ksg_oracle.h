@@ -38,6 +38,9 @@ int ksgo_schedule_one(ksgo_ctx *ctx, int32_t handle, uint32_t flags, ksg_result 
 int ksgo_schedule_batch(ksgo_ctx *ctx, const int32_t *handles, int32_t n, uint32_t flags,
                         ksg_result *results);
 int ksgo_forget(ksgo_ctx *ctx, int32_t handle);
+/* the nominator, same contract as ksg_add_nominated_pod / ksg_delete_nominated_pod (include/ksg.h) */
+int ksgo_add_nominated_pod(ksgo_ctx *ctx, const char *json, size_t len);
+int ksgo_delete_nominated_pod(ksgo_ctx *ctx, const char *uid);
 /* CPU-baseline breakdown: microseconds per cycle section since the last call (see oracle.cpp) */
 int ksgo_debug_profile(ksgo_ctx *ctx, double *out, int n);
 int ksgo_run_filter_plugin(ksgo_ctx *ctx, int32_t handle, int32_t plugin, int32_t *prefilter_code,

@@ -630,6 +630,10 @@ struct ksgo_ctx {
   OpportunisticBatch batch;  // frameworkImpl.batch (framework/runtime/framework.go:1620-1626)
   int64_t cycleCount = 0;    // SchedulingQueue.SchedulingCycle(): one per scheduling cycle of this context
   int64_t clockNs = 0;       // ksgo_set_clock: time.Now() of the next cycles (0: the wall clock)
+  // the scheduling queue's nominator (backend/queue/nominator.go:60-150; ksgo_add_nominated_pod): uid -> (node,
+  // priority).  Boundary, as the product (include/ksg.h): RunFilterPluginsWithNominatedPods is not restated; a
+  // call in which a pod would see another pod's nomination of equal or higher priority is refused
+  std::map<std::string, std::pair<std::string, int32_t>> nominated;
   int64_t clockStep = 0;     // ksgo_debug_clock_step: the fixed clock advances by this per cycle (per read)
   int64_t now() {
     if (clockNs) {
@@ -2243,9 +2247,38 @@ int ksgo_pod_release(ksgo_ctx* c, int32_t handle) {
   return c->queue.erase(handle) ? KSG_OK : KSG_ENOTFOUND;
 }
 
+// addGENominatedPods' condition (framework.go:1265-1294): another uid nominated to a snapshot node with priority >= the
+// pod's -- refused (the boundary above)
+static int check_nominations(ksgo_ctx* c, const Pod& p) {
+  if (c->nominated.empty()) return KSG_OK;
+  c->rebuild_list();
+  for (const auto& kv : c->nominated)
+    if (kv.first != p.uid && kv.second.second >= p.priority && c->snapMap.count(kv.second.first)) {
+      c->err = "another pod of equal or higher priority is nominated to node " + kv.second.first;
+      return KSG_ENOTSUP;
+    }
+  return KSG_OK;
+}
+
+int ksgo_add_nominated_pod(ksgo_ctx* c, const char* json, size_t len) {  // nominator.go:60-103 (ModeNoop)
+  try {
+    Pod p;
+    if (!decode_pod(mj::parse(json, len), &p, &c->err)) return KSG_EINVAL;
+    if (p.uid.empty()) { c->err = "metadata.uid is empty"; return KSG_EINVAL; }
+    c->nominated.erase(p.uid);
+    if (!p.nominatedNodeName.empty()) c->nominated[p.uid] = {p.nominatedNodeName, p.priority};
+    return KSG_OK;
+  } catch (std::exception& e) { c->err = e.what(); return KSG_EINVAL; }
+}
+int ksgo_delete_nominated_pod(ksgo_ctx* c, const char* uid) {  // nominator.go:138-150
+  c->nominated.erase(uid);
+  return KSG_OK;
+}
+
 int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* result, ksg_eval_out* ev) {
   auto it = c->queue.find(handle);
   if (it == c->queue.end()) return KSG_ENOTFOUND;
+  if (const int rn = check_nominations(c, *it->second)) return rn;
   double A0 = nowus();
   int rc = run_cycle(c, *it->second, result, ev, true);
   double A1 = nowus(); c->prof[6] += A1 - A0; c->prof[8] += 1;
@@ -2260,6 +2293,7 @@ int ksgo_schedule_one(ksgo_ctx* c, int32_t handle, uint32_t flags, ksg_result* r
     node_add_pod(*c->nodes[p.nodeName], pi.get());
     c->assumedUid[handle] = p.uid;
     c->pods[p.uid] = std::move(pi);
+    c->nominated.erase(it->second->uid);  // DeleteNominatedPodIfExists (schedule_one.go:1131-1134)
   }
   c->prof[7] += nowus() - A1;
   return KSG_OK;
@@ -2274,6 +2308,11 @@ int ksgo_debug_profile(ksgo_ctx* c, double* out, int n) {
 }
 
 int ksgo_schedule_batch(ksgo_ctx* c, const int32_t* handles, int32_t n, uint32_t flags, ksg_result* results) {
+  for (int32_t i = 0; i < n; ++i) {  // (refused as a whole, before any pod: the product's contract)
+    auto it = c->queue.find(handles[i]);
+    if (it == c->queue.end()) return KSG_ENOTFOUND;
+    if (const int rn = check_nominations(c, *it->second)) return rn;
+  }
   for (int32_t i = 0; i < n; ++i) {
     int rc = ksgo_schedule_one(c, handles[i], flags, &results[i], nullptr);
     if (rc != KSG_OK) return rc;
@@ -2520,6 +2559,7 @@ int ksgo_preempt(ksgo_ctx* c, int32_t handle, const char* args_json, size_t args
   auto it = c->queue.find(handle);
   if (it == c->queue.end()) return KSG_ENOTFOUND;
   const Pod& pod = *it->second;
+  if (const int rn = check_nominations(c, pod)) return rn;  // (SelectVictimsOnNode filters with them too)
   *res = ksg_preempt_result{};
   res->status = KSG_CODE_UNSCHEDULABLE;
   res->node_index = -1;

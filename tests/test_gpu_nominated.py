@@ -146,3 +146,11 @@ def test_sharded_context_declines_nominated_pods():
     pod = _nominate({"metadata": {"name": "p", "uid": "p"}, "spec": {"containers": []}}, "n1")
     with pytest.raises(KsgError, match="rc=-5"):
         ranks[0].compile(pod)
+
+
+def test_nominator_boundary_matches_oracle():
+    """Other pods' nominations (ksg_add_nominated_pod): the device refuses exactly the calls the oracle refuses
+    and schedules the rest identically (tests/nominator_scenario.py)."""
+    from ksg.native import Scheduler
+    from nominator_scenario import run
+    assert run(Scheduler({})) == run(oracle({}))
