@@ -44,6 +44,7 @@ Cluster::~Cluster() {
     if (b.p) (void)hipFree(b.p);
   if (upd_dev_.p) (void)hipFree(upd_dev_.p);
   if (dyn_dev_.p) (void)hipFree(dyn_dev_.p);
+  if (gather_dev_.p) (void)hipFree(gather_dev_.p);  // (LeakSanitizer over the host-stub build, tests/asan)
   if (stream) (void)hipStreamDestroy(stream);
 }
 
