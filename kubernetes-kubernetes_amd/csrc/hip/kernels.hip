@@ -2309,6 +2309,8 @@ __device__ __forceinline__ void sched_loop_body(const MirrorView& m, const Batch
                                                  run0, lv.npods, lv.ring_idle);
       if (lv.relay && hostp) __hip_atomic_store(lv.relay, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // stops too
       s_ring_ctl = v;
+      // (diagnostic build: stamp 7 of a resident pod = workgroup 0 saw its doorbell; the batch loop's phase-1 end)
+      if (kSt && lv.stamps && w == 0 && (v & kCtlStop) != kCtlStop) lv.stamps[(size_t)run0 * 8 + 7] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const unsigned long long ctl = s_ring_ctl;

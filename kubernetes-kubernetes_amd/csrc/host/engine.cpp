@@ -2990,6 +2990,30 @@ int Engine::resident_stop() {
   __atomic_store_n(&ring_->ll[0], (unsigned long long)kRingStop, __ATOMIC_RELEASE);
   res_running_ = false;
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->cfg.loop_stamps && res_kind_ == 1 && res_q_ > 1 && d_stamps.p) {
+    // k_sched_loop ring pods, workgroup 0 (diagnostic build): doorbell seen (7) -> exchange A start (0: relay,
+    // staging, phase 1, A publish) -> A swept (1) -> phase 2 (2) -> B published (3) -> B swept (4) -> barrier (5)
+    // -> commit + result posted + barrier (6) -> the next pod's doorbell seen (host settle, compile, post, poll)
+    std::vector<unsigned long long> st((size_t)res_q_ * 8);
+    HIPCHK(hipMemcpy(st.data(), d_stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+    static const int ks[] = {7, 0, 1, 2, 3, 4, 5, 6};
+    double a[8] = {0};
+    int cnt = 0;
+    for (int q = 0; q + 1 < res_q_; ++q) {
+      const unsigned long long* t = &st[(size_t)q * 8];
+      const unsigned long long nx = st[(size_t)(q + 1) * 8 + 7];
+      bool ok = nx != 0;
+      for (int k : ks) ok = ok && t[k] != 0;
+      if (!ok) continue;
+      for (int k = 0; k < 7; ++k) a[k] += (double)(t[ks[k + 1]] - t[ks[k]]) / 100.0;
+      a[7] += (double)(nx - t[6]) / 100.0;
+      cnt++;
+    }
+    if (cnt)
+      std::fprintf(stderr, "[k_sched_loop ring stamps, %d pods, us] doorbell -> A start %.2f  A %.2f  phase2 %.2f  "
+                   "publishB %.2f  B %.2f  barrier %.2f  commit+post %.2f | next doorbell %.2f\n", cnt, a[0] / cnt,
+                   a[1] / cnt, a[2] / cnt, a[3] / cnt, a[4] / cnt, a[5] / cnt, a[6] / cnt, a[7] / cnt);
+  }
   if (c->cfg.loop_stamps && res_kind_ == 2 && res_q_ > 0 && d_astamps.p) {
     // k_agg_loop ring pods, workgroup 0's view (us): ring wait -> staged -> counts gathered (+ Z) -> totals ->
     // minima | phase 1 | A | phase 2 | B publish | B sweep + commit | end of pod
@@ -3183,6 +3207,11 @@ relaunch:
       lv.wave_map = c->cfg.loop_wave_map;
       lv.ring = ring_dev_;
       lv.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;  // s_memrealtime: 100 MHz
+      if (c->cfg.loop_stamps) {  // per-pod phase stamps (the resident instance writes them in the diagnostic build)
+        if ((rc = ensure(d_stamps, (size_t)kLoopMaxPods * 8 * 8))) return fail(rc);
+        HIPCHK(hipMemsetAsync(d_stamps.p, 0, (size_t)kLoopMaxPods * 8 * 8, s));
+        lv.stamps = (unsigned long long*)d_stamps.p;
+      }
       if (c->cfg.ring_relay_min > 0 && GS >= c->cfg.ring_relay_min) {  // as k_agg_loop's below (one buffer)
         if ((rc = ensure(d_relay, (size_t)kRelayWords * 8))) return fail(rc);
         HIPCHK(hipMemsetAsync(d_relay.p, 0, (size_t)kRelayWords * 8, s));

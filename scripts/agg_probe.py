@@ -1,5 +1,5 @@
 """Diagnostic: k_agg_loop per-phase stamps (workgroup 0's view) and pods/s on the aggregation
-workloads: python scripts/agg_probe.py c3|c4|c4-anti|c5 [loopWorkgroups]."""
+workloads: python scripts/agg_probe.py c3|c4|c4-anti|c5|dts [loopWorkgroups]."""
 import os
 import sys
 import time
@@ -16,11 +16,15 @@ if wl == "c3":
     nodes, init, pods = synth.scheduling_c3(5000, 5000, 2000)
 elif wl in ("c4", "c4-anti"):
     nodes, init, pods = synth.topology_spreading(15000, 15000, 2000, preferred_anti=wl == "c4-anti")
+elif wl == "dts":
+    nodes, init, pods, objects = synth.default_topology_spreading(5000, 5000, 2000)
 else:
     nodes, init, pods = synth.mixed_cluster(100000, 10000, 2000)
 s = Scheduler({"device": 0, "loopWorkgroups": wg, "loopStamps": True, "aggLoopDebug": dbg})
 for ns in synth.namespaces() if hasattr(synth, "namespaces") else []:
     s.upsert_namespace(ns)
+for ob in (objects if wl == "dts" else []):
+    s.upsert_object(ob)
 for n in nodes:
     s.add_node(n)
 for p in init:
