@@ -607,6 +607,8 @@ struct LoopView {
   int32_t wave_map;          // which hardware wave plays which role (k_sched_loop kWaveMap; 0: identity)
   PodRing* ring;             // resident mode (nullptr: a batch run): pods arrive one by one through the ring
   unsigned long long ring_idle;  // resident mode: s_memrealtime ticks (100 MHz) without a pod before leaving
+  int32_t ring_ahead;        // resident mode: evaluate the next pod's phase 1 ahead of its doorbell (config residentAhead)
+  int32_t pad_ring;
   // resident mode with many workgroups: workgroup 0 alone polls the host's ctl and relays the word through
   // device memory (relay[0]), where the others poll (nullptr: every workgroup polls the host)
   unsigned long long* relay;

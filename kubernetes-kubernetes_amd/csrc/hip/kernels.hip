@@ -2271,10 +2271,12 @@ __device__ __forceinline__ void sched_loop_body(const MirrorView& m, const Batch
       a = s_x[par][0][v] > a ? s_x[par][0][v] : a;
       bb = s_x[par][1][v] > bb ? s_x[par][1][v] : bb;
     }
-    if (reinterpret_cast<const PodDesc*>(s_blob[pq % 3])->flags & DF_ROTDEV) {  // counted from the ballots
+    const PodDesc& dp = *reinterpret_cast<const PodDesc*>(s_blob[pq % 3]);
+    if (RING || (dp.flags & DF_ROTDEV)) {  // counted from the ballots (resident: phase 1 may have run ahead)
+      const int srot = (dp.flags & DF_ROTDEV) ? (int)s_rot[pq & 1] : dp.rot_start;
       bl = 0;
       for (int kk = 0; kk < nk; ++kk)
-        for (int v = 0; v < NW; ++v) bl += (uint32_t)__popcll(s_ball[par][kk][v] & below_mask_v(kk, v, (int)s_rot[pq & 1]));
+        for (int v = 0; v < NW; ++v) bl += (uint32_t)__popcll(s_ball[par][kk][v] & below_mask_v(kk, v, srot));
     }
     unsigned long long g0, g1;
     a_granules(c, bl, a, bb, &g0, &g1);
@@ -2296,6 +2298,8 @@ __device__ __forceinline__ void sched_loop_body(const MirrorView& m, const Batch
   __syncthreads();
   // A batch launch is one run of pods [0, npods).  Resident mode (lv.ring): every pod is a run of its
   // own, started when the host posts it; the pod index q (granules, stamps, results) keeps counting.
+  // resident mode: the pod whose phase 1 was evaluated ahead of its doorbell (-1: none; see the run's end)
+  int spec_for = -1;
   for (int run0 = 0;;) {
   int run_end = lv.npods;
   if constexpr (RING) {
@@ -2346,7 +2350,11 @@ __device__ __forceinline__ void sched_loop_body(const MirrorView& m, const Batch
     }
   }
   __syncthreads();
-  if (t < U) phase1(lv.first_pod + run0, run0 % 3, run0 & 1, nullptr);
+  // (resident: a RING_SAME pod -- the previous call's program but for its slot and rotation, which phase 1 does not
+  // read -- whose phase 1 ran ahead, against these same cores, skips it; publish_a recounts its nodes before the
+  // rotation start from the ballots)
+  const bool ahead = RING && spec_for == run0 && ((s_ring_ctl >> 11) & 1ull);
+  if (t < U && !ahead) phase1(lv.first_pod + run0, run0 % 3, run0 & 1, nullptr);
   __syncthreads();
   if (vt == U) {
     const PodDesc& d0 = *reinterpret_cast<const PodDesc*>(s_blob[run0 % 3]);
@@ -2769,6 +2777,15 @@ __device__ __forceinline__ void sched_loop_body(const MirrorView& m, const Batch
     stamp_s(q, 6);
   }
   if constexpr (!RING) return;
+  // Resident: the next call's pod is most often of this one's template (kube-scheduler pops a ReplicaSet's pods
+  // one after another).  Its phase 1 against the cores as this commit left them runs now, before its doorbell,
+  // and is used if the doorbell says RING_SAME.  Default-plugin pods only (the fast path reads no HBM column).
+  if (lv.ring_ahead && (reinterpret_cast<const PodDesc*>(s_blob[run0 % 3])->flags & DF_FAST) && run_end < lv.npods) {
+    if (t < U) phase1(lv.first_pod + run_end, run0 % 3, run_end & 1, nullptr);
+    spec_for = run_end;
+  } else {
+    spec_for = -1;
+  }
   run0 = run_end;
   }
 }

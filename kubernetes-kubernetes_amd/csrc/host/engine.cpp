@@ -3207,6 +3207,7 @@ relaunch:
       lv.wave_map = c->cfg.loop_wave_map;
       lv.ring = ring_dev_;
       lv.ring_idle = (unsigned long long)kResidentIdleMs * 100000ull;  // s_memrealtime: 100 MHz
+      lv.ring_ahead = c->cfg.resident_ahead ? 1 : 0;
       if (c->cfg.loop_stamps) {  // per-pod phase stamps (the resident instance writes them in the diagnostic build)
         if ((rc = ensure(d_stamps, (size_t)kLoopMaxPods * 8 * 8))) return fail(rc);
         HIPCHK(hipMemsetAsync(d_stamps.p, 0, (size_t)kLoopMaxPods * 8 * 8, s));

@@ -224,10 +224,12 @@ struct Config {
                                 // between calls, fed through a host-pinned pod ring ("residentLoop")
   bool agg_loop = true;         // runs of PTS/IPA pods go through k_agg_loop (with persistent_loop)
   int agg_debug = 0;            // AggView::debug (diagnostic)
-  int ring_relay_min = 48;      // resident k_agg_loop: relay the doorbell through device memory from this many
-                                // workgroups on (one PCIe poller instead of G)
+  // resident loops: relay the doorbell through device memory from this many workgroups on (one PCIe poller instead
+  // of G; round 6, profiles/r06d_resident_ab.txt: C2's 40 workgroups 19.8 -> 14.8 us per call, DTS's 20 27.0 -> 25.3)
+  int ring_relay_min = 2;
   int first_chunk = 32;         // pods in a pipelined batch's first chunk (the host work before the first launch)
   int loop_wave_map = 0;        // k_sched_loop role-to-wave placement (kWaveMap in kernels.hip)
+  bool resident_ahead = true;   // resident k_sched_loop: the next pod's phase 1 ahead of its doorbell (LoopView)
   int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node units, CUs, 128))
   int loop_unit = 128;          // k_sched_loop nodes per workgroup unit: 128 (when it fits) or 256 ("loopUnit")

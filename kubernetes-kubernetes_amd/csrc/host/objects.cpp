@@ -894,9 +894,10 @@ bool decode_config(const char* p, size_t n, Config* c, std::string* err) {
     c->loop_unit = (int)d.num(r, "loopUnit", 128) == 256 ? 256 : 128;
     if (const JVal* al = d.get(r, "aggLoop")) c->agg_loop = al->type == JVal::BOOL && al->b;
     c->agg_debug = (int)d.num(r, "aggLoopDebug", 0);
-    c->ring_relay_min = (int)d.num(r, "ringRelayMinWorkgroups", 48);
+    c->ring_relay_min = (int)d.num(r, "ringRelayMinWorkgroups", 2);
     c->debug_give_up_at = (int)d.num(r, "debugLoopGiveUpAt", -1);
     c->loop_wave_map = (int)d.num(r, "loopWaveMap", 0);
+    if (const JVal* ra = d.get(r, "residentAhead")) c->resident_ahead = !(ra->type == JVal::BOOL && !ra->b);
     c->first_chunk = std::max(8, std::min(256, (int)d.num(r, "pipelineFirstChunk", 32)));
     if (c->loop_wave_map < 0 || c->loop_wave_map > 2) c->loop_wave_map = 0;
     if (const JVal* dx = d.get(r, "deviceExchange")) c->dev_exchange = dx->type == JVal::BOOL && dx->b ? 1 : 0;

@@ -7,6 +7,7 @@ ksg_schedule_batch of the same pods.  Prints one JSON line per workload.
                                                         dts (DefaultTopologySpreading), c4 (TopologySpreading
                                                         15000 nodes), c3, c4-anti, c5 (100 000 nodes), c2big (SchedulingBasic at 100 000 nodes)
   python scripts/single_pod_probe.py stamps [workload]  the resident call's host / device split
+  python scripts/single_pod_probe.py ab [workload]      resident variants (residentAhead, the doorbell relay)
 single_resident_us times the calls from Python (ctypes), single_resident_native_us from native code
 (ksg_debug_schedule_calls), as a binding's goroutine issues them.
 Every resident call's result is checked against the oracle (after timing), so a fast wrong answer
@@ -85,6 +86,16 @@ def run(wl, cfg, n_pods=2000, batch=False, check=False, native=False):
 
 def main():
     args = sys.argv[1:]
+    if args[:1] == ["ab"]:  # resident-loop variants, native calls, oracle-checked, interleaved twice on one box
+        wl = args[1] if len(args) > 1 else "c2"
+        variants = [("ahead+relay", {"ringRelayMinWorkgroups": 1}), ("ahead", {}),
+                    ("relay", {"residentAhead": False, "ringRelayMinWorkgroups": 1}), ("neither", {"residentAhead": False})]
+        for rep in range(2):
+            for name, cfg in variants:
+                nus, _, nmism = run(wl, cfg, check=rep == 0, native=True)
+                print(json.dumps({"workload": wl, "variant": name, "rep": rep, "single_resident_native_us": round(nus, 2),
+                                  "native_oracle_mismatches": nmism}), flush=True)
+        return
     if args[:1] == ["stamps"]:  # printed at the loop's stop
         wl = args[1] if len(args) > 1 else "c2"
         print(json.dumps({"workload": wl, "single_resident_us": round(run(wl, {"loopStamps": True})[0], 1),
