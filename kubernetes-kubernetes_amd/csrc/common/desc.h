@@ -573,8 +573,13 @@ constexpr int kRingEntryBytes = 8192;  // (staged into one of the resident k_agg
 //               below: nothing is staged, the loop copies q-1's in LDS and patches them) | RING_AGG_SAME
 //               (k_agg_loop: the program's DF_AGG_SAME);
 //   ll[1..3]:   RING_SAME: {slot, rot_start, entry lbl_off}; else {program bytes, entry bytes, 0}.
+//   RING_TERMS (with RING_SAME): the pod's own affinity terms are pod q-1's but for their term-table indices and
+//               the term-pool offset of their words (a pod stamped from the same template): PodRing::patch[q %
+//               kRingSlots] holds {new tpool_off | n << 32} and the n indices (int32 pairs); the loop rewrites the
+//               program's own-term list and the entry's terms (index, owner, word offsets) in LDS.
 // A stop is ll[0]'s tag kRingStop.
-enum : uint32_t { RING_SAME = 1u, RING_AGG_SAME = 2u };
+enum : uint32_t { RING_SAME = 1u, RING_AGG_SAME = 2u, RING_TERMS = 4u };
+constexpr int kPatchWords = 1 + 4 * kAggMaxTerms / 2;  // RING_TERMS: the header and up to 4 * kAggMaxTerms indices
 constexpr int kRingLL = 4;
 constexpr int kRelayWords = kRingLL + kBlobLds / 8 + kRingEntryBytes / 8;  // AggView::relay
 // k_sched_loop polls one word instead (its registers leave no room for four): ctl = {q + 1 (bits 0-10) |
@@ -590,6 +595,7 @@ struct alignas(128) PodRing {
   RingResult res[kRingSlots];
   alignas(128) uint8_t blob[kRingSlots][kBlobLds];
   alignas(128) uint8_t entry[kRingSlots][kRingEntryBytes];
+  alignas(128) unsigned long long patch[kRingSlots][kPatchWords];  // [host] RING_TERMS
 };
 
 struct LoopView {
@@ -679,7 +685,8 @@ struct AggView {
   int32_t debug;              // diagnostic (config "aggLoopDebug"): bit 0 never fold (gather every pod after
                               // the previous one is placed), bit 1 never DF_LFAST, bit 2 no same-template
                               // shortcut (DF_AGG_SAME), bit 3 (host) no RING_SAME -- the resident loops stage
-                              // every pod over PCIe, bit 4 the resident loop always runs exchange PX
+                              // every pod over PCIe, bit 4 the resident loop always runs exchange PX,
+                              // bit 7 (host: residentAhead false) no phase 1 ahead of the doorbell
   unsigned long long* gran;   // [npods][world * nwg][kAGran] (this rank's)
   unsigned long long* region; // [npods][gwords]: shared-region sums (zeroed by the host; this rank's)
   // node shards: participants are world * nwg workgroups, rank-major.  Every granule and

@@ -3077,6 +3077,8 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
   __shared__ int s_ring_end;                  // resident mode: -1: the launch ends
   __shared__ int s_pb, s_eb;                  // resident mode: the last staged program's / entry's bytes
   __shared__ int s_spec_q;                    // resident mode: the counts hold pod s_spec_q's plus its placement
+  __shared__ int s_ahead_q;                   // resident mode: phase 1 of pod s_ahead_q's program again is in LDS
+  __shared__ unsigned long long s_patch[kPatchWords];  // resident mode: a RING_TERMS doorbell's patch
   __shared__ int32_t s_tc_off[kAggTc];        // template cache: each written slot's template (a pod's program offset)
   __shared__ int s_gprev, s_lprev;            // template cache: pod q-1's node (-1: not placed), my slot of it (-1)
   __shared__ uint32_t s_tcq;                  // template cache: pod q's decisions (kTq*, slots, fold mask)
@@ -3473,7 +3475,10 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
   // would count for it, less the chosen node's label values (looked up once the node is known).
   // (plan_fold_b: the placed pod's program bp, the next pod's base)
   // (emit(lref, label slot, constraint, weight, any bit, absent value) takes each item)
-  auto plan_fold_e = [&](const uint8_t* bp, const uint8_t* base, int gl, auto&& emit) __attribute__((always_inline)) {
+  // (ent: the placed pod's RingEntry in LDS -- its own terms and their term-pool words as the owner's commit writes
+  // them to the device tables, which only the owner may read back (resident mode); nullptr: read the tables)
+  auto plan_fold_e = [&](const uint8_t* bp, const uint8_t* base, int gl, const uint8_t* ent, auto&& emit)
+                         __attribute__((always_inline)) {
     asm volatile("" : "+v"(gl));  // lane-dependent item selection stays in the loop (register pressure)
     const PodDesc& dp = *reinterpret_cast<const PodDesc*>(bp);
     const PodDesc& d = *reinterpret_cast<const PodDesc*>(base);
@@ -3516,8 +3521,12 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
         emit(cs[c].lref, cs[c].slot, cs[c].hostname ? -1 : 8 + c, 1, 0u, cs[c].hostname ? 0 : cs[c].absent);
     } else if (gl >= 32 && (d.ipa_flags & (IPA_EXIST_FILTER | IPA_EXIST_SCORE))) {
       const int32_t* own = at<int32_t>(bp, dp.own_terms_off);
+      // (the entry lists the terms in the program's order: both are the slot's pt_terms, engine.cpp / podtable.cpp)
+      const RingEntry* he = reinterpret_cast<const RingEntry*>(ent);
+      const int32_t* etw = ent ? reinterpret_cast<const int32_t*>(ent + sizeof(RingEntry) + (size_t)he->lbl_cnt * 8) : nullptr;
+      const RingTerm* ert = ent ? reinterpret_cast<const RingTerm*>(etw + ((he->tpool_cnt + 1) & ~1)) : nullptr;
       for (int k2 = gl - 32; k2 < dp.n_own_terms; k2 += 32) {
-        const DTerm tm = m.terms[own[k2]];
+        const DTerm tm = ent ? ert[k2].d : m.terms[own[k2]];
         if (tm.key >= d.n_keytab) continue;
         const int32_t* kt = at<int32_t>(base, d.keytab_off) + (size_t)tm.key * kKeytabStride;
         const bool anti = tm.kind == T_REQ_ANTI;
@@ -3529,19 +3538,23 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
         else if (tm.kind == T_PREF_ANTI) wt = -tm.weight;
         else wt = 1;
         if (hb < 0 || wt == 0) continue;
-        const int32_t* tp = m.term_pool;
+        // (the entry holds the term-pool words [tpool_off, tpool_off + tpool_cnt): the offsets are rebased, never the
+        // pointer -- an LDS pointer moved below its start is outside the LDS aperture once it is a flat address)
+        const int32_t* tp = ent ? etw : m.term_pool;
+        const int32_t tb = ent ? he->tpool_off : 0;
         const unsigned long long* il = at<unsigned long long>(base, d.lbl_off);
         const unsigned long long* nsl = at<unsigned long long>(base, d.nslbl_off);
-        if ((id_in(tp + tm.ns_off, tm.ns_cnt, d.ns_id) || lsel_match(tp + tm.nssel, nsl, d.n_nslbl)) &&
-            lsel_match(tp + tm.sel, il, d.n_lbl))
+        if ((id_in(tp + (tm.ns_off - tb), tm.ns_cnt, d.ns_id) || lsel_match(tp + (tm.nssel - tb), nsl, d.n_nslbl)) &&
+            lsel_match(tp + (tm.sel - tb), il, d.n_lbl))
           push(anti ? kt[3] : kt[4], kt[0], -1, wt, anti ? 4u : 8u);
       }
     }
   };
   // the plan into LDS (s_fi / s_nfi; s_nfi was reset after the previous fold: a reset here by one lane would race
   // the others' pushes)
-  auto plan_fold_b = [&](const uint8_t* bp, const uint8_t* base, int gl) __attribute__((always_inline)) {
-    plan_fold_e(bp, base, gl,
+  auto plan_fold_b = [&](const uint8_t* bp, const uint8_t* base, int gl, const uint8_t* ent = nullptr)
+                         __attribute__((always_inline)) {
+    plan_fold_e(bp, base, gl, ent,
                 [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb, int32_t absent)
                     __attribute__((always_inline)) {
                       const uint32_t k = atomicAdd(&s_nfi, 1u);
@@ -3701,7 +3714,7 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
     int32_t* lh = reinterpret_cast<int32_t*>(cb + kTcLh);
     const uint32_t el = elig_of(base, nq);
     uint32_t any = 0;
-    plan_fold_e(s_blob[(q + 2) % 3], base, gl,
+    plan_fold_e(s_blob[(q + 2) % 3], base, gl, nullptr,
                 [&](int32_t lref, int32_t slot, int32_t cons, int32_t wt, uint32_t anyb, int32_t absent)
                     __attribute__((always_inline)) {
                       int32_t v = node_label(m, slot, nq);
@@ -3747,6 +3760,7 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
     s_pxd_q = -1;
     s_elig_q = -1;
     s_spec_q = -1;
+    s_ahead_q = -1;
     s_gprev = -1;
     s_lprev = -1;
     s_tcq = 0;
@@ -3814,6 +3828,7 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
   };
 
   for (int q = 0; q < av.npods; ++q) {
+    bool ahead = false;  // resident: this pod's phase 1 ran at the end of the pod before (below)
     if constexpr (RING) {
       // ======== resident mode: pod q from the ring (host memory, bypassing the device caches): its program
       // into s_blob[q % 3], its pod-table entry into s_blob[(q + 1) % 3]; then its counts ========
@@ -3841,6 +3856,18 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
       if (rmode & RING_SAME) {
+        if (rmode & RING_TERMS) {  // the patch words, one per lane of wave 0 (workgroup 0 of a relay passes them on)
+          if (wave == 0) {
+            const unsigned long long* src = hostp ? av.ring->patch[q % kRingSlots] : av.relay + kRingLL;
+            unsigned long long x = 0;
+            if (lane < kPatchWords) x = __hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane < kPatchWords) s_patch[lane] = x;
+            if (relay && hostp) {
+              if (lane < kPatchWords) __hip_atomic_store(av.relay + kRingLL + lane, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the relayed words landed before the doorbell
+            }
+          }
+        }
         relay_doorbell();
         // pod q-1's program and entry but for the slot, the rotation and the label-pool offset (the host
         // compared the rest byte for byte): copied in LDS -- the entry first, its buffer takes the program
@@ -3861,6 +3888,23 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
           RingEntry& en = *reinterpret_cast<RingEntry*>(ed);
           en.slot = ew8 ? (int32_t)s_ll[1] : -1;
           en.lbl_off = s_ll[3];
+          if (rmode & RING_TERMS) {  // (the host replayed this patch on pod q-1's bytes and compared the result)
+            const int32_t toff = (int32_t)(uint32_t)s_patch[0], n = (int32_t)(s_patch[0] >> 32);
+            const int32_t* js = reinterpret_cast<const int32_t*>(&s_patch[1]);
+            int32_t* own = reinterpret_cast<int32_t*>(s_blob[q % 3] + dn.own_terms_off);
+            const int32_t dt = toff - en.tpool_off;
+            RingTerm* rt = reinterpret_cast<RingTerm*>(reinterpret_cast<uint8_t*>(ed) + sizeof(RingEntry) +
+                                                       (size_t)en.lbl_cnt * 8 + (size_t)((en.tpool_cnt + 1) & ~1) * 4);
+            en.tpool_off = toff;
+            for (int32_t k = 0; k < n && k < 2 * (kPatchWords - 1); ++k) {
+              own[k] = js[k];
+              rt[k].j = js[k];
+              rt[k].d.owner = en.slot;
+              rt[k].d.sel += dt;
+              rt[k].d.nssel += dt;
+              rt[k].d.ns_off += dt;
+            }
+          }
         }
       } else {
         const int pw8 = (int)s_ll[1] / 8, ew8 = (int)s_ll[2] / 8;
@@ -3872,11 +3916,23 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
         const unsigned long long* sp_ = hostp ? ps_ : av.relay + kRingLL;
         const unsigned long long* se_ = hostp ? es_ - pw8 : av.relay + kRingLL;
         const bool put = relay && hostp;
-        for (int k = t; k < pw8 + ew8; k += kAggThreads) {
-          const unsigned long long x = __hip_atomic_load((k < pw8 ? sp_ : se_) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (k < pw8) pd[k] = x;
-          else ed[k - pw8] = x;
-          if (put) __hip_atomic_store(av.relay + kRingLL + k, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every word of a thread's share in flight at once (one round trip each), then stored
+        constexpr int kStageW = (kBlobLds + kRingEntryBytes) / 8 / kAggThreads;
+        static_assert(kStageW * 8 * kAggThreads == kBlobLds + kRingEntryBytes, "staging share");
+        unsigned long long xs[kStageW];
+#pragma unroll
+        for (int i = 0; i < kStageW; ++i) {
+          const int k = t + i * kAggThreads;
+          xs[i] = 0;
+          if (k < pw8 + ew8) xs[i] = __hip_atomic_load((k < pw8 ? sp_ : se_) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+#pragma unroll
+        for (int i = 0; i < kStageW; ++i) {
+          const int k = t + i * kAggThreads;
+          if (k >= pw8 + ew8) break;
+          if (k < pw8) pd[k] = xs[i];
+          else ed[k - pw8] = xs[i];
+          if (put) __hip_atomic_store(av.relay + kRingLL + k, xs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (put) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the relayed bytes landed before the doorbell
@@ -3894,6 +3950,7 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
       // the same template as pod q-1 (host: DF_AGG_SAME): pod q's counts are q-1's plus q-1's placement,
       // folded into the counts in LDS at the end of pod q-1 already (s_spec_q)
       const PodDesc& dq = *reinterpret_cast<const PodDesc*>(s_blob[q % 3]);
+      ahead = (rmode & RING_SAME) && (dq.flags & DF_AGG_SAME) && s_spec_q == q - 1 && s_ahead_q == q - 1 && q > 0;
       if (!((dq.flags & DF_AGG_SAME) && s_spec_q == q - 1 && q > 0)) {
         aggregate(q, t, kAggThreads, wg_bar);
         if (wave == 0) sweep_z(q);
@@ -3941,118 +3998,135 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
     wstamp(q, 0);
 
     // ======== phase 1: my node (LDS core, LDS counts) ========
-    {
-      const AggTopo tp{s_gh, s_lh, s_pmin, s_pndom, s_any};
-      NodeEval ne{1u, false, 0, 0, 0, 0};
-      PodFast pf;
-      if ((d.flags & DF_LFAST) && !(av.debug & 2)) pf = load_fast(base, d);
-      else pf.flags = d.flags & ~DF_LFAST;
-      // opaque per pod: keeps the compiler from hoisting my node's column addresses out of the pod
-      // loop, where they would stay live (and spill) across the exchanges
-      int my_iq = my_i;
-      asm volatile("" : "+v"(my_iq));
-      if (my_node) ne = eval_agg(m, lds_core(s_core, kk, tt), s_core.bwo[kk][tt], pf, base, d, my_iq, tp, t);
-      const bool feas = ne.st == 0;
-      const unsigned long long ballot = __ballot(feas);
-      // PodTopologySpread score inputs (scoring.go:61-115, 199-226): the count at my node's domain per
-      // constraint (the weights need exchange A's topology sizes), and the domains of my feasible,
-      // non-ignored nodes as presence bits
-      unsigned long long pb0 = 0, pb1 = 0;
-      bool pts_on = false;
-      if (PTSS && ((d.score_mask >> P_PTS) & 1u)) {
+    // (a lambda: the resident instance also runs it at the end of the pod before, for a next pod of the same
+    // program -- `ahead`)
+    auto phase1 = [&]() __attribute__((always_inline)) {
+      {
+        const AggTopo tp{s_gh, s_lh, s_pmin, s_pndom, s_any};
+        NodeEval ne{1u, false, 0, 0, 0, 0};
+        PodFast pf;
+        if ((d.flags & DF_LFAST) && !(av.debug & 2)) pf = load_fast(base, d);
+        else pf.flags = d.flags & ~DF_LFAST;
+        // opaque per pod: keeps the compiler from hoisting my node's column addresses out of the pod
+        // loop, where they would stay live (and spill) across the exchanges
+        int my_iq = my_i;
+        asm volatile("" : "+v"(my_iq));
+        if (my_node) ne = eval_agg(m, lds_core(s_core, kk, tt), s_core.bwo[kk][tt], pf, base, d, my_iq, tp, t);
+        const bool feas = ne.st == 0;
+        const unsigned long long ballot = __ballot(feas);
+        // PodTopologySpread score inputs (scoring.go:61-115, 199-226): the count at my node's domain per
+        // constraint (the weights need exchange A's topology sizes), and the domains of my feasible,
+        // non-ignored nodes as presence bits
+        unsigned long long pb0 = 0, pb1 = 0;
+        bool pts_on = false;
+        if (PTSS && ((d.score_mask >> P_PTS) & 1u)) {
+          const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
+          const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
+          bool ign = false;
+          uint32_t cnt[kAggScoreCons];
+  #pragma unroll
+          for (int c = 0; c < kAggScoreCons; ++c) {
+            cnt[c] = ~0u;
+            if (c < d.n_ptss && my_node) {
+              const int32_t v = node_label(m, cs[c].slot, my_iq);
+              if (v >= 0) cnt[c] = (uint32_t)tp.cnt(cs[c].hist_base, cs[c].lref, cs[c].hostname ? 0 : v, t);
+              else ign |= !anytopo;
+            }
+            s_pc[c][t] = cnt[c];
+          }
+          pts_on = feas && !ign;
+          if (pts_on)
+  #pragma unroll
+            for (int c = 0; c < kAggScoreCons; ++c)
+              if (c < d.n_ptss && !cs[c].hostname) {
+                const int b = cs[c].pbit + pts_domain(m, cs[c], my_iq);
+                if (b < 64) pb0 |= 1ull << b;
+                else pb1 |= 1ull << (b - 64);
+              }
+  #pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            pb0 |= __shfl_xor(pb0, o, 64);
+            pb1 |= __shfl_xor(pb1, o, 64);
+          }
+        }
+        const unsigned long long pball = __ballot(pts_on);
+        const int lim = d.rot_start - (nlo + wave * 64);
+        const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+        s_sv[t] = SlotVal{ne.fixed, (uint32_t)ne.rt, (uint32_t)ne.rna};
+        s_ri[t] = ne.ripa;
+        unsigned long long et = 0, en = 0, ei = 0, ni = ~0ull;
+        if (feas) {
+          et = enc_i64(ne.rt);
+          en = enc_i64(ne.rna);
+          ei = enc_i64(ne.ripa);
+          ni = ei;
+        }
+        et = wave_max_u64(et);
+        en = wave_max_u64(en);
+        ei = wave_max_u64(ei);
+        ni = ~wave_max_u64(~ni);
+        if (lane == 0) {
+          s_ball[wave] = ballot;
+          s_wu[wave][0] = (uint32_t)__popcll(ballot);
+          s_wu[wave][1] = (uint32_t)__popcll(ballot & bm);
+          s_wu[wave][2] = (uint32_t)__popcll(pball);
+          s_wp[wave][0] = pb0;
+          s_wp[wave][1] = pb1;
+          s_wx[wave][0] = et;
+          s_wx[wave][1] = en;
+          s_wx[wave][2] = ei;
+          s_wx[wave][3] = ni;
+        }
+      }
+      __syncthreads();
+      if (PTSS && kPxa && ((d.score_mask >> P_PTS) & 1u) && s_psz_used[0] != ~0u) {
+        // each slot's raw PodTopologySpread score with the previous scored pod's topology sizes (the
+        // arithmetic of the score pass after exchange A, below); exchange A checks the sizes and carries
+        // the max / min (AG_PXA)
         const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
         const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
-        bool ign = false;
-        uint32_t cnt[kAggScoreCons];
-#pragma unroll
+        int tq = t;  // opaque per pod: the slot addresses are not hoisted out of the pod loop (registers)
+        asm volatile("" : "+v"(tq));
+        bool ign = false, have = true;
+        double score = 0.0;
+  #pragma unroll
         for (int c = 0; c < kAggScoreCons; ++c) {
-          cnt[c] = ~0u;
-          if (c < d.n_ptss && my_node) {
-            const int32_t v = node_label(m, cs[c].slot, my_iq);
-            if (v >= 0) cnt[c] = (uint32_t)tp.cnt(cs[c].hist_base, cs[c].lref, cs[c].hostname ? 0 : v, t);
-            else ign |= !anytopo;
+          if (c >= d.n_ptss) continue;
+          have = have && s_psz_used[c] != ~0u;
+          const uint32_t cnt = s_pc[c][tq];
+          if (cnt == ~0u) {
+            ign |= !anytopo;
+            continue;
           }
-          s_pc[c][t] = cnt[c];
+          if (!have) continue;
+          const double prod = (double)cnt * s_pwt[c];
+          const double term = prod + (double)(cs[c].max_skew - 1);
+          score = score + term;
         }
-        pts_on = feas && !ign;
-        if (pts_on)
-#pragma unroll
-          for (int c = 0; c < kAggScoreCons; ++c)
-            if (c < d.n_ptss && !cs[c].hostname) {
-              const int b = cs[c].pbit + pts_domain(m, cs[c], my_iq);
-              if (b < 64) pb0 |= 1ull << b;
-              else pb1 |= 1ull << (b - 64);
-            }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          pb0 |= __shfl_xor(pb0, o, 64);
-          pb1 |= __shfl_xor(pb1, o, 64);
+        const bool scored = have && ((s_ball[tq >> 6] >> (tq & 63)) & 1ull) && !ign;
+        const uint32_t raw = scored ? (uint32_t)(int64_t)round(score) : 0u;
+        s_praw[tq] = scored ? raw : ~0u;
+        unsigned long long hx = scored ? (unsigned long long)raw + 1ull : 0ull;
+        unsigned long long hn = scored ? (1ull << 24) - 1ull - raw : 0ull;
+        hx = wave_max_u64(hx);
+        hn = wave_max_u64(hn);
+        if (lane == 0) {
+          s_wq[wave][0] = hx;
+          s_wq[wave][1] = hn;
         }
+        __syncthreads();
       }
-      const unsigned long long pball = __ballot(pts_on);
-      const int lim = d.rot_start - (nlo + wave * 64);
-      const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
-      s_sv[t] = SlotVal{ne.fixed, (uint32_t)ne.rt, (uint32_t)ne.rna};
-      s_ri[t] = ne.ripa;
-      unsigned long long et = 0, en = 0, ei = 0, ni = ~0ull;
-      if (feas) {
-        et = enc_i64(ne.rt);
-        en = enc_i64(ne.rna);
-        ei = enc_i64(ne.ripa);
-        ni = ei;
-      }
-      et = wave_max_u64(et);
-      en = wave_max_u64(en);
-      ei = wave_max_u64(ei);
-      ni = ~wave_max_u64(~ni);
+    };
+    if (!ahead) {
+      phase1();
+    } else {
+      // the same program's phase 1 against the cores and the folded counts this pod sees ran at the end of pod
+      // q-1 (the host compared the program bytes: only the slot, the rotation and the label-pool offset differ,
+      // and phase 1 reads the rotation alone): the count before the new rotation start, from the ballots
       if (lane == 0) {
-        s_ball[wave] = ballot;
-        s_wu[wave][0] = (uint32_t)__popcll(ballot);
-        s_wu[wave][1] = (uint32_t)__popcll(ballot & bm);
-        s_wu[wave][2] = (uint32_t)__popcll(pball);
-        s_wp[wave][0] = pb0;
-        s_wp[wave][1] = pb1;
-        s_wx[wave][0] = et;
-        s_wx[wave][1] = en;
-        s_wx[wave][2] = ei;
-        s_wx[wave][3] = ni;
-      }
-    }
-    __syncthreads();
-    if (PTSS && kPxa && ((d.score_mask >> P_PTS) & 1u) && s_psz_used[0] != ~0u) {
-      // each slot's raw PodTopologySpread score with the previous scored pod's topology sizes (the
-      // arithmetic of the score pass after exchange A, below); exchange A checks the sizes and carries
-      // the max / min (AG_PXA)
-      const PtsCons* cs = at<PtsCons>(base, d.ptss_off);
-      const bool anytopo = (d.flags & DF_PTS_ANYTOPO) != 0;
-      int tq = t;  // opaque per pod: the slot addresses are not hoisted out of the pod loop (registers)
-      asm volatile("" : "+v"(tq));
-      bool ign = false, have = true;
-      double score = 0.0;
-#pragma unroll
-      for (int c = 0; c < kAggScoreCons; ++c) {
-        if (c >= d.n_ptss) continue;
-        have = have && s_psz_used[c] != ~0u;
-        const uint32_t cnt = s_pc[c][tq];
-        if (cnt == ~0u) {
-          ign |= !anytopo;
-          continue;
-        }
-        if (!have) continue;
-        const double prod = (double)cnt * s_pwt[c];
-        const double term = prod + (double)(cs[c].max_skew - 1);
-        score = score + term;
-      }
-      const bool scored = have && ((s_ball[tq >> 6] >> (tq & 63)) & 1ull) && !ign;
-      const uint32_t raw = scored ? (uint32_t)(int64_t)round(score) : 0u;
-      s_praw[tq] = scored ? raw : ~0u;
-      unsigned long long hx = scored ? (unsigned long long)raw + 1ull : 0ull;
-      unsigned long long hn = scored ? (1ull << 24) - 1ull - raw : 0ull;
-      hx = wave_max_u64(hx);
-      hn = wave_max_u64(hn);
-      if (lane == 0) {
-        s_wq[wave][0] = hx;
-        s_wq[wave][1] = hn;
+        const int lim = d.rot_start - (nlo + wave * 64);
+        const unsigned long long bm = lim <= 0 ? 0ull : lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+        s_wu[wave][1] = (uint32_t)__popcll(s_ball[wave] & bm);
       }
       __syncthreads();
     }
@@ -4681,11 +4755,14 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
       // (written by the owner's committing thread) is read by the owner's gathers of the pods after it.  While the host
       // turns around, pod q is folded into the counts in LDS as a next pod of its own template would count
       // it (the plan against q's own program): a next pod marked DF_AGG_SAME starts from them, any other
-      // gathers afresh.  (q's own terms would be read from the table the owner wrote: not for pods with them.)
+      // gathers afresh.  (q's own terms come from its entry in LDS, not the tables the owner wrote.)
       if (wave == 0) {
-        const bool sp = (d.flags & DF_AGGREGATE) && spec(d) && d.n_own_terms == 0 && !(av.debug & 4);
+        // (q's own terms from its entry in LDS: the device term table is the owner's to read back)
+        const RingEntry& he = *reinterpret_cast<const RingEntry*>(s_blob[(q + 1) % 3]);
+        const bool sp = (d.flags & DF_AGGREGATE) && spec(d) && !(av.debug & 4) &&
+                        (d.n_own_terms == 0 || (he.slot >= 0 && he.nterms == d.n_own_terms));
         if (sp) {
-          plan_fold_b(s_blob[q % 3], s_blob[q % 3], lane);
+          plan_fold_b(s_blob[q % 3], s_blob[q % 3], lane, s_blob[(q + 1) % 3]);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           const int nq = s_gnode;
           const uint32_t nfi = s_nfi < (uint32_t)kFoldMax ? s_nfi : (uint32_t)kFoldMax;
@@ -4705,6 +4782,12 @@ __device__ __forceinline__ void agg_loop_body(const MirrorView& m, const BatchVi
       // lists -- within this launch; an agent-scope release / acquire here wrote back and invalidated the L2 of
       // every workgroup's XCD each pod: 11 µs per call at 100 000 nodes)
       __syncthreads();
+      // and phase 1 of pod q's program again, against the cores this commit left and the folded counts: a next
+      // pod of the same program (RING_SAME + DF_AGG_SAME, as a binding pops a ReplicaSet's pods) skips it
+      if (!(av.debug & 128) && s_spec_q == q) {
+        phase1();
+        if (t == 0) s_ahead_q = q;
+      }
     }
     if (kTc && t == 0) {  // pod q's placement, for the next pod's folds into the cached templates
       s_gprev = s_gnode;

@@ -1498,6 +1498,64 @@ static bool agg_same(const std::vector<uint8_t>& a, const std::vector<uint8_t>& 
 
 static bool agg_same(const CompiledPod& a, const CompiledPod& b) { return !a.error && !b.error && agg_same(a.blob, b.blob); }
 
+// The resident k_agg_loop's RING_TERMS doorbell (desc.h): pod b (program nb, entry ne) is pod a's but for its slot,
+// rotation, DF_AGG_SAME, label-pool offset -- as RING_SAME -- and its own affinity terms' table indices and the
+// term-pool offset of their words.  The loop's patch is replayed on a's bytes; true (and the patch words) only when
+// the result equals b's program and entry byte for byte.
+// (why: the first check that failed, for the loopStamps report -- 1 sizes, 2 the terms, 3 the program, 4 the entry's
+// terms, 5 the entry)
+static bool ring_terms_patch(const std::vector<uint8_t>& pa, const std::vector<uint8_t>& pb, const std::vector<uint8_t>& ea,
+                             const uint8_t* eb, size_t eb_bytes, unsigned long long* patch, int* why) {
+  *why = 1;
+  if (pa.size() != pb.size() || pa.size() < sizeof(PodDesc) || ea.size() != eb_bytes || eb_bytes < sizeof(RingEntry))
+    return false;
+  *why = 2;
+  const PodDesc& hb = *reinterpret_cast<const PodDesc*>(pb.data());
+  const PodDesc& ha = *reinterpret_cast<const PodDesc*>(pa.data());
+  const int32_t n = hb.n_own_terms;
+  if (n <= 0 || n > 2 * (kPatchWords - 1) || ha.n_own_terms != n || ha.own_terms_off != hb.own_terms_off ||
+      hb.own_terms_off < (int32_t)sizeof(PodDesc) || (size_t)hb.own_terms_off + (size_t)n * 4 > pb.size())
+    return false;
+  std::vector<uint8_t> p = pa;
+  PodDesc& pd = *reinterpret_cast<PodDesc*>(p.data());
+  pd.slot = hb.slot;
+  pd.rot_start = hb.rot_start;
+  pd.flags = (pd.flags & ~DF_AGG_SAME) | (hb.flags & DF_AGG_SAME);
+  int32_t js[2 * (kPatchWords - 1)] = {};
+  std::memcpy(js, pb.data() + hb.own_terms_off, (size_t)n * 4);
+  std::memcpy(p.data() + hb.own_terms_off, js, (size_t)n * 4);
+  *why = 3;
+  if (std::memcmp(p.data(), pb.data(), p.size()) != 0) return false;
+  *why = 4;
+  std::vector<uint8_t> e = ea;
+  RingEntry& en = *reinterpret_cast<RingEntry*>(e.data());
+  const RingEntry& nb = *reinterpret_cast<const RingEntry*>(eb);
+  if (en.nterms != n) return false;
+  const size_t rt_at = sizeof(RingEntry) + (size_t)en.lbl_cnt * 8 + (size_t)((en.tpool_cnt + 1) & ~1) * 4;
+  if (en.slot < 0 || rt_at + (size_t)n * sizeof(RingTerm) > e.size()) return false;
+  const int32_t dt = nb.tpool_off - en.tpool_off;
+  en.slot = nb.slot;
+  en.lbl_off = nb.lbl_off;
+  en.tpool_off = nb.tpool_off;
+  for (int32_t k = 0; k < n; ++k) {
+    RingTerm r;
+    std::memcpy(&r, e.data() + rt_at + (size_t)k * sizeof(RingTerm), sizeof r);
+    r.j = js[k];
+    r.d.owner = en.slot;
+    r.d.sel += dt;
+    r.d.nssel += dt;
+    r.d.ns_off += dt;
+    std::memcpy(e.data() + rt_at + (size_t)k * sizeof(RingTerm), &r, sizeof r);
+  }
+  *why = 5;
+  if (std::memcmp(e.data(), eb, eb_bytes) != 0) return false;
+  *why = 0;
+  patch[0] = (unsigned long long)(uint32_t)nb.tpool_off | ((unsigned long long)(uint32_t)n << 32);
+  std::memset(patch + 1, 0, (kPatchWords - 1) * 8);
+  std::memcpy(patch + 1, js, (size_t)n * 4);
+  return true;
+}
+
 // k_agg_loop's template cache plan for the run [i, j) (TcWord per pod, desc.h): each pod's template takes a slot
 // (a template already cached: a hit, its counts are loaded instead of gathered; else the least recently used
 // slot but the active one), and per pod q the slots the loop folds pod q-1's placement into while deciding q:
@@ -2984,6 +3042,11 @@ int Engine::resident_stop() {
     std::fprintf(stderr, "[resident loop, %d calls, us per call] compile %.2f  post %.2f  device (post -> result seen) %.2f  "
                  "settle %.2f\n", (int)n, res_prof_[0] / n, res_prof_[1] / n, res_prof_[2] / n, res_prof_[3] / n);
     for (double& v : res_prof_) v = 0;
+    std::fprintf(stderr, "[k_agg_loop ring posts] same %ld  own terms patched %ld  staged: sizes %ld, terms %ld, program %ld, "
+                 "entry terms %ld, entry %ld, first %ld, no entry %ld, program size %ld, entry size %ld\n", res_posts_[0],
+                 res_posts_[1], res_posts_[3], res_posts_[4], res_posts_[5], res_posts_[6], res_posts_[7], res_posts_[8],
+                 res_posts_[9], res_posts_[10], res_posts_[11]);
+    for (long& v : res_posts_) v = 0;
   }
   if (!res_running_) return KSG_OK;
   __atomic_store_n(&ring_->ctl, kCtlStop, __ATOMIC_RELEASE);
@@ -3264,7 +3327,7 @@ relaunch:
       av.spill = (uint32_t*)d_aspill.p;
       av.spill_pods = (int32_t)spill_p;
       av.spill_terms = (int32_t)spill_t;
-      av.debug = c->cfg.agg_debug;
+      av.debug = c->cfg.agg_debug | (c->cfg.resident_ahead ? 0 : 128);  // 128: no phase 1 ahead of the doorbell
       av.give_up_at = -1;
       av.gran = (unsigned long long*)d_agran.p;
       av.region = (unsigned long long*)d_region.p;
@@ -3348,10 +3411,24 @@ relaunch:
       same = std::memcmp(res_prev_entry_.data(), entry, entry_bytes) == 0;
       pe = keep;
     }
-    if (c->cfg.agg_debug & 8) same = false;  // diagnostic: every pod staged over PCIe
+    // else, a pod of the same template with own affinity terms: the same but for the terms' table indices and the
+    // term-pool offset of their words (RING_TERMS) -- the patch is replayed here on the previous bytes, and taken
+    // only when that reproduces this pod's program and entry exactly
+    bool terms = false;
+    unsigned long long patch[kPatchWords] = {};
+    int why = q == 0 ? 6 : !entry_bytes ? 7 : res_prev_blob_.size() != cp.blob.size() ? 8 : 9;
+    if (!same && q > 0 && entry_bytes && res_prev_blob_.size() == cp.blob.size() && res_prev_entry_.size() == entry_bytes)
+      terms = ring_terms_patch(res_prev_blob_, cp.blob, res_prev_entry_, entry, entry_bytes, patch, &why);
+    res_posts_[same ? 0 : terms ? 1 : 2 + why]++;
+    if (terms) {
+      same = true;
+      lbl_off = reinterpret_cast<const RingEntry*>(entry)->lbl_off;
+    }
+    if (c->cfg.agg_debug & 8) same = terms = false;  // diagnostic: every pod staged over PCIe
     uint32_t dw[kRingLL];
     if (same) {
-      dw[0] = RING_SAME | (aggsame ? RING_AGG_SAME : 0u);
+      if (terms) std::memcpy(ring_->patch[q % kRingSlots], patch, sizeof patch);
+      dw[0] = RING_SAME | (terms ? RING_TERMS : 0u) | (aggsame ? RING_AGG_SAME : 0u);
       dw[1] = (uint32_t)hd.slot;
       dw[2] = (uint32_t)hd.rot_start;
       dw[3] = lbl_off;

@@ -229,7 +229,7 @@ struct Config {
   int ring_relay_min = 2;
   int first_chunk = 32;         // pods in a pipelined batch's first chunk (the host work before the first launch)
   int loop_wave_map = 0;        // k_sched_loop role-to-wave placement (kWaveMap in kernels.hip)
-  bool resident_ahead = true;   // resident k_sched_loop: the next pod's phase 1 ahead of its doorbell (LoopView)
+  bool resident_ahead = true;   // resident loops: the next pod's phase 1 ahead of its doorbell (LoopView, AggView bit 7)
   int debug_give_up_at = -1;    // diagnostic: the persistent loops give up at this pod of a run
   int loop_wg = 0;              // k_sched_loop workgroups (0: min(node units, CUs, 128))
   int loop_unit = 128;          // k_sched_loop nodes per workgroup unit: 128 (when it fits) or 256 ("loopUnit")
@@ -678,6 +678,7 @@ class Engine {
   bool res_running_ = false;
   int res_q_ = 0, res_gs_ = 0, res_unit_ = 0;  // pods posted to the running launch; its geometry
   std::vector<uint8_t> res_prev_blob_, res_prev_entry_;  // k_agg_loop ring: the program / entry posted last
+  long res_posts_[12] = {};  // k_agg_loop ring posts: same, RING_TERMS, staged (+ ring_terms_patch's why) (loopStamps)
   int res_kind_ = 0;              // the running launch: 1 k_sched_loop, 2 k_agg_loop (pod-table pods)
   int64_t res_terms_ = 0;         // k_agg_loop: own affinity terms of the pods posted (its spill rows' budget)
   std::chrono::steady_clock::time_point res_last_{};  // the last result the host took

@@ -181,6 +181,14 @@ size_t Cluster::ring_entry(int32_t s, uint8_t* out, size_t cap) const {
   // the device arrays must already hold every index the entry writes (as upload_pod_table sized them)
   int32_t jmax = -1;
   for (int32_t j : js) jmax = std::max(jmax, j);
+  // the entry carries the words of the last pod put, which must be this slot's: every word its terms name lies in
+  // them (the resident k_agg_loop writes them to the device pool, and folds the pod from them in LDS)
+  const int64_t wlo = last_tpool_off, whi = (int64_t)last_tpool_off + last_tpool_cnt;
+  for (int32_t j : js) {
+    const DTerm& d = tt[(size_t)j];
+    if (d.sel < wlo || d.sel >= whi || d.nssel < wlo || d.nssel >= whi || d.ns_off < wlo || d.ns_off + d.ns_cnt > whi)
+      return 0;
+  }
   const size_t ps = ((size_t)s + 1) * 4;
   if (!pt_dev_[0].p || pt_dev_[0].bytes < ps || pt_dev_[1].bytes < ps || pt_dev_[2].bytes < ps || pt_dev_[3].bytes < ps ||
       pt_dev_[4].bytes < ps || pt_dev_[5].bytes < ((size_t)lo + lc) * 8 ||

@@ -67,10 +67,10 @@ for s in "$@"; do
       for k in $(seq 1 "$n"); do step "repeat_${sc%.py}_$k" 200 python3 -u "scripts/$sc" ${args//,/ }; done ;;
     pydiag=*)
       a=${s#pydiag=}; sc=${a%%:*}; args=""; [ "$a" != "$sc" ] && args=${a#*:}
-      step "pydiag_${sc%.py}" 400 env KSG_LIB="$PWD/kubernetes-kubernetes_amd/lib/libksg_diag.so" python3 -u "scripts/$sc" ${args//,/ } ;;
+      n=${args//[^A-Za-z0-9]/_}; step "pydiag_${sc%.py}${n:+_${n:0:40}}" 400 env KSG_LIB="$PWD/kubernetes-kubernetes_amd/lib/libksg_diag.so" python3 -u "scripts/$sc" ${args//,/ } ;;
     py=*)
       a=${s#py=}; sc=${a%%:*}; args=""; [ "$a" != "$sc" ] && args=${a#*:}
-      step "py_${sc%.py}" 400 python3 -u "scripts/$sc" ${args//,/ } ;;
+      n=${args//[^A-Za-z0-9]/_}; step "py_${sc%.py}${n:+_${n:0:40}}" 400 python3 -u "scripts/$sc" ${args//,/ } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -5,9 +5,10 @@ ksg_schedule_batch of the same pods.  Prints one JSON line per workload.
 
   python scripts/single_pod_probe.py [workload ...]     c2 (SchedulingBasic 5000 nodes, default), c2pct0,
                                                         dts (DefaultTopologySpreading), c4 (TopologySpreading
-                                                        15000 nodes), c3, c4-anti, c5 (100 000 nodes), c2big (SchedulingBasic at 100 000 nodes)
+                                                        15000 nodes), c3, c3aff (C3's pod-affinity pods alone), c4-anti, c5 (100 000 nodes), c2big (SchedulingBasic at 100 000 nodes)
   python scripts/single_pod_probe.py stamps [workload]  the resident call's host / device split
-  python scripts/single_pod_probe.py ab [workload]      resident variants (residentAhead, the doorbell relay)
+  python scripts/single_pod_probe.py ab [workload]      resident variants (residentAhead, the doorbell relay, and
+                                                        k_agg_loop's same-template shortcuts off: aggLoopDebug 8 / 12)
 single_resident_us times the calls from Python (ctypes), single_resident_native_us from native code
 (ksg_debug_schedule_calls), as a binding's goroutine issues them.
 Every resident call's result is checked against the oracle (after timing), so a fast wrong answer
@@ -35,6 +36,9 @@ def cluster(wl, n_pods):
         nodes, init, pods, objects = synth.default_topology_spreading(5000, 5000, n_pods)
     elif wl == "c3":
         nodes, init, pods = synth.scheduling_c3(5000, 5000, n_pods)
+    elif wl == "c3aff":  # C3's cluster, the measured stream one template: pod-with-pod-affinity (own terms)
+        nodes, init, _ = synth.scheduling_c3(5000, 5000, 0)
+        pods = [synth.pod_with_pod_affinity(f"pod-{k}", "sched-1") for k in range(n_pods)]
     elif wl == "c5":
         nodes, init, pods = synth.mixed_cluster(100000, 10000, n_pods)
     else:
@@ -89,7 +93,9 @@ def main():
     if args[:1] == ["ab"]:  # resident-loop variants, native calls, oracle-checked, interleaved twice on one box
         wl = args[1] if len(args) > 1 else "c2"
         variants = [("ahead+relay", {"ringRelayMinWorkgroups": 1}), ("ahead", {}),
-                    ("relay", {"residentAhead": False, "ringRelayMinWorkgroups": 1}), ("neither", {"residentAhead": False})]
+                    ("relay", {"residentAhead": False, "ringRelayMinWorkgroups": 1}), ("neither", {"residentAhead": False}),
+                    # k_agg_loop: every pod staged over PCIe (no RING_SAME / RING_TERMS), and no fold either
+                    ("staged", {"aggLoopDebug": 8}), ("staged+gathered", {"aggLoopDebug": 12})]
         for rep in range(2):
             for name, cfg in variants:
                 nus, _, nmism = run(wl, cfg, check=rep == 0, native=True)
