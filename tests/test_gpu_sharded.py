@@ -74,10 +74,11 @@ def _run_ranks(ranks, pods, chunk):
 
 def _check(ranks, o, pods, chunk=64, forced_give_up=False):
     got = _run_ranks(ranks, pods, chunk)
+    bad = []  # every rank's mismatches (the first 12), so an intermittent one is characterised when it shows
     for k, p in enumerate(pods):
         want = o.schedule_one(o.compile(p), assume=True)[0].as_tuple()
-        for r in range(len(ranks)):
-            assert got[r][k] == want, f"rank {r} pod {k}: {got[r][k]} != oracle {want}"
+        bad += [f"rank {r} pod {k}: {got[r][k]} != oracle {want}" for r in range(len(ranks)) if got[r][k] != want]
+    assert not bad, f"{len(bad)} mismatches (status, node, evaluated, feasible, score): " + "; ".join(bad[:12])
     # (give-ups, all-reduce re-runs) per rank: a recovered give-up must not pass as a clean run
     stats = [s.loop_stats() for s in ranks]
     if forced_give_up:
