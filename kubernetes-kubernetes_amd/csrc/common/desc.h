@@ -620,8 +620,11 @@ struct LoopView {
   unsigned long long* relay;
 };
 // exchange granules per participant per pod: A0 {count, count before nextStartNodeIndex},
-// A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only)
-constexpr int kGran = 4;
+// A1 {max raw TT + 1, max raw NA + 1}, B {packed key < 2^48}, B_node (sharded only) -- four words used, the row
+// padded to 16 (one 128-byte line per participant, no line written by two workgroups): k_sched_loop 5.33 -> 5.28 us
+// per pod at C2, 5.28 -> 5.25 at C1 (interleaved A/B, profiles/r06g_granule_stride_ab.txt).  The same padding of
+// k_agg_loop's 14-word rows measured slower (DTS 16.13 -> 16.43 us per pod) and was not kept.
+constexpr int kGran = 16;
 // A persistent loop's give-up record (LoopView::fail / AggView::fail): [0] flag, [1] pod of the run
 // (the granule row; or a k_agg_loop check code), [2] granule (or workgroup), [3] first missing sweep
 // lane, [4] loop (1 k_sched_loop, 2 k_agg_loop), [5] its granule tag, [6, 7] the sweep's missing-lane
