@@ -2344,6 +2344,7 @@ int Engine::run_batch(const std::vector<const PodSpec*>& pods, const std::vector
         HIPCHK(hipEventCreate(&e));
         lev.push_back(e);
       }
+      gw = (gw + 15) & ~15;  // whole 128-byte lines per pod's row: no line holds two pods' sums
       const size_t rbytes = (size_t)(j - i) * (size_t)gw * 8;  // <= kLoopMaxPods * kAggGWords words
       HIPCHK(hipMemsetAsync(d_region.p, 0, rbytes, s));  // (sharded: the loop's start barrier orders the peers' adds)
       AggView av{};
